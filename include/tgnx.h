@@ -1,0 +1,191 @@
+/* libtgnx — MI355X-native (gfx950) TGN temporal link-prediction hot path, C ABI.
+ *
+ * Every entry point takes plain device pointers, int64 sizes and a HIP stream
+ * passed as `void*` (a hipStream_t; NULL = the default stream).  Nothing here
+ * allocates: scratch comes from a caller-provided workspace whose size the
+ * matching *_ws_bytes() query returns, so a sequence of calls can be captured
+ * into a HIP graph.  All launches are asynchronous on `stream`.
+ *
+ * Return value: TGNX_OK (0) or a negative code; tgnx_last_error() then holds a
+ * message (thread-local).  Indices are int64 (the reference's torch.long),
+ * times are fp32 (the reference casts t to float32, temporal_dataset.py:42,53).
+ *
+ * The reference has no native layer: its "FFI" is the Python import seam at
+ * pyg-mem-tgn.py:16-25.  Each function below cites the reference code it
+ * replaces; INTEGRATION.md shows the ctypes binding a maintainer would add.
+ */
+#ifndef TGNX_H
+#define TGNX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TGNX_OK 0
+#define TGNX_EINVAL (-1)   /* bad argument / shape / capacity */
+#define TGNX_EHIP (-2)     /* HIP launch or runtime error */
+#define TGNX_ETOOBIG (-3)  /* size beyond what this build supports */
+
+int tgnx_version(void);
+const char* tgnx_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * Temporal neighbour ring — LastNeighborLoader (neighbor_loader.py:15-109).
+ * State: nbr int64[N*K], eid int64[N*K], t fp32[N*K] (row-major [N,K]), newest
+ * first in every row; eid < 0 marks an empty slot; assoc int64[N].
+ * ------------------------------------------------------------------------ */
+
+/* reset_state (neighbor_loader.py:106-109): eid = -1, t = -1. */
+int tgnx_ring_reset(int64_t* eid, float* t, int64_t num_nodes, int32_t size, void* stream);
+
+/* __call__ (neighbor_loader.py:26-50).  Query n_id[q] (any int64 ids < N).
+ * Outputs (capacity cap_nodes >= q*(1+K), cap_edges >= q*K):
+ *   out_nid[M]          sorted unique of n_id ∪ valid neighbours
+ *   out_ei[2*cap_edges] row 0 (local neighbour) at [0,E), row 1 (local centre) at [cap_edges, cap_edges+E)
+ *   out_eid[E], out_t[E] in query-row-major, slot order (centre order, then newest first)
+ *   assoc[out_nid[i]] = i
+ *   counts[0] = M, counts[1] = E   (device int64[2])
+ * Workspace: tgnx_ring_sample_ws_bytes(N, q) bytes, zero-filled before the FIRST call
+ * (the kernels leave it zeroed again). */
+size_t tgnx_ring_sample_ws_bytes(int64_t num_nodes, int64_t q);
+int tgnx_ring_sample(const int64_t* nbr, const int64_t* eid, const float* t, int64_t num_nodes,
+                     int32_t size, const int64_t* n_id, int64_t q, int64_t* assoc, int64_t* out_nid,
+                     int64_t* out_ei, int64_t* out_eid, float* out_t, int64_t cap_nodes,
+                     int64_t cap_edges, int64_t* counts, void* ws, size_t ws_bytes, void* stream);
+
+/* insert (neighbor_loader.py:52-104) of events (src[i], dst[i], t[i]) with
+ * e_id = cur_e_id + i, both directions; keeps the K largest e_id per node
+ * (and, as the reference does at :100, the K largest t values separately);
+ * assoc[unique touched nodes, sorted] = rank.  B <= tgnx_ring_insert_max_batch().
+ * Canonical rule for a node with > K entries in one call: the K newest survive. */
+int tgnx_ring_insert_max_batch(void);
+int tgnx_ring_insert(int64_t* nbr, int64_t* eid, float* t, int64_t num_nodes, int32_t size,
+                     const int64_t* src, const int64_t* dst, const float* ev_t, int64_t B,
+                     int64_t cur_e_id, int64_t* assoc, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Negative destinations — NegLinkSamplerDest.sample (neg_sampler.py:8-23):
+ * uniform over dst_nodes[n_dst], redrawn where equal to pos[i].  Counter-based
+ * RNG keyed by (seed, offset + i, attempt): replayable, graph-safe.
+ * ------------------------------------------------------------------------ */
+int tgnx_neg_sample(const int64_t* dst_nodes, int64_t n_dst, const int64_t* pos, int64_t B,
+                    uint64_t seed, uint64_t offset, int64_t* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Dependency blocks — get_block / dependecyAwareBatch (dependencyGraph.py:8-49),
+ * host (CPU, single pass, O(E)) and device versions: per batch of `batch`
+ * consecutive events, block = 1 + max(last[src], last[dst]).
+ * ------------------------------------------------------------------------ */
+int tgnx_block_ids_host(const int64_t* src, const int64_t* dst, int64_t num_events, int64_t batch,
+                        int64_t* out);
+
+
+/* ------------------------------------------------------------------------
+ * TGNN step — the running reference model (model_utils.py:14-237, 422-697) and
+ * its epoch loop (epoch_utils.py:15-318), fused.
+ *
+ * The per-dependency-block loop of model_utils.py:68-157 is evaluated for all
+ * blocks of a batch in one parallel pass: every (row, block) embedding is a
+ * segment whose in-edges are the root's ring row (sampled at batch start),
+ * its self-loop (ones features, t = 0; epoch_utils.py:246-250) and the
+ * intra-batch edges of earlier blocks (model_utils.py:151-157); time_assoc as
+ * of block i is reconstructed per source node from the batch's sorted touch
+ * list.  EdgeGATConv runs in its exact collapsed form: only
+ * U_e = attn_e·W_e, U_{l,r} = attn_{l,r}·W_n reach the output (ft is [N,H,1],
+ * :560-563), so the embedding is drop(mem) + (1/H)·Σ_h ft_h.
+ *
+ * ctl is a device int64[16] control block (see TGNX_CTL_*); every kernel of a
+ * step reads the batch geometry from it, so a step can be replayed from a
+ * HIP graph.  The model's parameters live in one flat fp32 buffer laid out by
+ * tgnx_tgnn_param_layout (names = the reference's state_dict keys).
+ * ------------------------------------------------------------------------ */
+#define TGNX_CTL_BATCH_START 0  /* offset of the batch's first event in the ev_* arrays */
+#define TGNX_CTL_CUR_EID 1      /* e_id of that event (neighbor_loader.py:59) */
+#define TGNX_CTL_B 2            /* events in the batch (global batch under DP) */
+#define TGNX_CTL_GEN 3          /* node-map generation stamp */
+#define TGNX_CTL_ADAM_T 4       /* optimizer step count */
+#define TGNX_CTL_S 5            /* segments (rows) assembled */
+#define TGNX_CTL_E 6            /* edges assembled (train) */
+#define TGNX_CTL_LO 7           /* this rank's event slice [lo, hi) */
+#define TGNX_CTL_HI 8
+#define TGNX_CTL_SEED 9         /* per-batch RNG seed (dropout) */
+#define TGNX_CTL_NB 10          /* batches advanced since the last reset */
+#define TGNX_CTL_ERR 11         /* device-side error flags (0 = ok) */
+#define TGNX_CTL_LOSS 12        /* (double) running sum of loss * B (epoch_utils.py:310) */
+#define TGNX_CTL_WORDS 16
+
+#define TGNX_TGNN_NPARAM 15     /* te_w te_b attn_l attn_r attn_e Wn bn We be Ws bs Wd bd Wo bo */
+
+typedef struct {
+  int64_t num_nodes;  /* N */
+  int32_t ring;       /* K = sampling.neighbor[0] */
+  int32_t mem_dim;    /* D = gnn.dim_out (time_dim == D, model_utils.py:18); <= 128 */
+  int32_t msg_dim;    /* d (edge-feature width); d + D <= 320 */
+  int32_t heads;      /* H = gnn.att_head; 8 */
+  int32_t max_batch;  /* capacity of B (global batch); <= 2730 */
+  int32_t max_neg;    /* capacity of negatives per event (1 train, K' eval) */
+  float feat_drop;    /* 0.6 in the reference (model_utils.py:664) */
+  float attn_drop;    /* 0.6 (model_utils.py:665) */
+  float lr, beta1, beta2, eps;  /* Adam (model_utils.py:709-710) */
+} tgnx_tgnn_config;
+
+typedef struct {
+  /* events, indexed like the split arrays; the batch starts at ctl[BATCH_START] */
+  const int64_t* ev_src;
+  const int64_t* ev_dst;
+  const float* ev_t;
+  const int64_t* ev_blk;   /* dependency block id of each event */
+  const float* ev_msg;     /* [*, d] raw message of each event (intra-batch edge features) */
+  int64_t* neg;            /* [*, Kn] negatives, same indexing (train: written by the step) */
+  const int64_t* dst_nodes;/* unique destinations for train negatives */
+  int64_t n_dst;
+  const float* feat;       /* feature table indexed by ring e_id [*, d] (epoch_utils.py:224) */
+  int64_t* nbr;            /* ring state (neighbor_loader.py:19-22) */
+  int64_t* eid;
+  float* rt;
+  int64_t* assoc;
+  float* time_assoc;       /* [N] model_utils.py:22 */
+  const float* memory;     /* [N, D] model_utils.py:270 */
+  float* params;           /* flat, tgnx_tgnn_param_layout */
+  float* grads;            /* same layout + 1 trailing slot (batch loss) */
+  float* adam_m;
+  float* adam_v;
+  int64_t* ctl;            /* int64[TGNX_CTL_WORDS] */
+  float* out_pos;          /* [B] logits (event order in train, block order in eval) */
+  float* out_neg;          /* [B*Kn] */
+  double* mrr;             /* eval: per-batch MRR, indexed by ctl[NB]-1 */
+  void* ws;                /* tgnx_tgnn_ws_bytes(cfg) bytes, zero-filled once */
+  void* node_map;          /* int32[4*N], zero-filled once (persistent across steps) */
+} tgnx_tgnn_buffers;
+
+int tgnx_tgnn_param_layout(const tgnx_tgnn_config* cfg, int64_t* offsets /* [TGNX_TGNN_NPARAM+1] */);
+size_t tgnx_tgnn_ws_bytes(const tgnx_tgnn_config* cfg);
+
+/* Set up the next batch.  mode 0: explicit (batch_start, B, cur_e_id as given);
+ * mode 1: resident (next consecutive batch of `batch` events in [split_lo, split_hi),
+ * cur_e_id = the event's global index).  Increments GEN and NB; for train also ADAM_T.
+ * rank/world slice the batch's rows for data parallelism. */
+int tgnx_tgnn_advance(int64_t* ctl, int32_t mode, int64_t batch_start, int64_t B, int64_t cur_e_id,
+                      int64_t split_lo, int64_t split_hi, int64_t batch, int32_t rank, int32_t world,
+                      uint64_t base_seed, int32_t train, void* stream);
+
+/* Train step, part 1 (epoch_utils.py:196-303 up to loss.backward): negatives (if gen_neg),
+ * assembly, collapsed forward, predictor + BCE, backward; writes grads (+ loss slot). */
+int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t gen_neg,
+                            int32_t dropout, void* stream);
+/* Train step, part 2 (optimizer.step + neighbor_loader.insert + time_assoc): Adam on the
+ * (possibly all-reduced) grads, ring insert of the whole batch, time_assoc update, loss sum. */
+int tgnx_tgnn_train_update(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, void* stream);
+/* Eval step (epoch_utils.py:28-157): Kn negatives per event, logits in block order,
+ * per-batch MRR (TGB rank rule), insert, time_assoc as model_utils.py:77-83 leaves it.
+ * tile_quirk = 1 pairs negative row r with source r mod B (model_utils.py:192). */
+int tgnx_tgnn_eval_step(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t Kn,
+                        int32_t tile_quirk, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TGNX_H */

@@ -60,7 +60,17 @@ class RefTimeEncode(nn.Module):
         self.w.bias = nn.Parameter(torch.zeros(dimension).float())
 
     def forward(self, t):
-        return torch.cos(self.w(t))
+        # cos(Linear(1,D)(t)).  torch-CPU's addmm rounds w*t+b with an FMA on its vectorised rows but
+        # not on tail rows (probe in DESIGN.md §Oracle), so the reference's argument is only defined
+        # to +-1 ulp; at dt ~ 1e6 that is up to 0.25 rad on the highest-frequency dims.  The oracle
+        # fixes the argument to the exactly-rounded FMA (double product is exact for fp32 inputs),
+        # i.e. torch's vectorised path — the rounding the HIP kernel's fmaf reproduces.
+        w = self.w.weight.view(1, -1)
+        arg = (t.double() * w.double() + self.w.bias.double()).float()
+        if torch.is_grad_enabled() and (self.w.weight.requires_grad or t.requires_grad):
+            # same value, autograd through the fp32 graph
+            arg = arg.detach() + (t * w + self.w.bias - (t * w + self.w.bias).detach())
+        return torch.cos(arg)
 
 
 class RefEdgePredictor(nn.Module):

@@ -1,0 +1,1456 @@
+// Fused TGNN train / eval step on gfx950 — the running reference path:
+//   epoch_utils.py:15-318 (batch assembly, loss, insert), model_utils.py:61-159 (block loop),
+//   :201-237 (TimeEncode), :422-455 (TemporalEdgePreprocess), :565-612 (EdgeGATConv),
+//   :688-697 (TemporalTransformerConv), :165-195 (EdgePredictor), :709-710 (Adam).
+//
+// Design:
+//  * No DGL graph, no unique/relabel: a "segment" is one predictor row (s / p / n of an
+//    event).  Its in-edges in the reference's block-i subgraph are exactly: the root's ring
+//    row (sampled before the batch), its self-loop (ones features, t = 0) and one edge per
+//    earlier-block event the root took part in as src or dst (model_utils.py:151-157).
+//  * time_assoc as of block i (model_utils.py:77-83) is rebuilt per source node from the
+//    batch's touch list, sorted by (node, block, kind, event) in one workgroup.
+//  * EdgeGATConv collapsed exactly: el/er/ee only enter through head dots, so
+//    x_eh = U_e[h]·efeat_e + U_l[h]·nfeat_src + c, U = attn·W (a 372-wide dot per edge
+//    per head instead of an 800-wide GEMM row); backward re-expands dU into dW / dattn.
+//  * One wave (64 lanes) per segment, lanes over feature dims; online softmax per head.
+#include "tgnx_ring_dev.h"
+
+namespace tgnx {
+
+constexpr int H = 8;          // gnn.att_head
+constexpr int DMAX = 128;     // gnn.dim_out (memory/time/embedding dim) capacity
+constexpr int FMAX = 320;     // d + D capacity
+constexpr int TOUCH_MAX = 8192;
+constexpr int GBWD = 64;      // workgroups of the backward kernel (= partial slabs)
+constexpr int MRR_SLOTS = 65536;  // per-batch MRR ring in buffers.mrr
+
+// ------------------------------------------------------------------ layouts
+struct Lay {
+  int64_t te_w, te_b, attn_l, attn_r, attn_e, Wn, bn, We, be, Ws, bs, Wd, bd, Wo, bo, total;
+};
+__host__ __device__ inline int64_t al4(int64_t x) { return (x + 3) & ~int64_t(3); }
+static Lay make_lay(int D, int d) {
+  const int64_t F = d + D;
+  Lay L;
+  int64_t o = 0;
+  L.te_w = o; o += al4(D);
+  L.te_b = o; o += al4(D);
+  L.attn_l = o; o += al4(H * D);
+  L.attn_r = o; o += al4(H * D);
+  L.attn_e = o; o += al4(H * D);
+  L.Wn = o; o += al4((int64_t)H * D * D);
+  L.bn = o; o += al4(H * D);
+  L.We = o; o += al4((int64_t)H * D * F);
+  L.be = o; o += al4(H * D);
+  L.Ws = o; o += al4((int64_t)D * D);
+  L.bs = o; o += al4(D);
+  L.Wd = o; o += al4((int64_t)D * D);
+  L.bd = o; o += al4(D);
+  L.Wo = o; o += al4(D);
+  L.bo = o; o += al4(1);
+  L.total = o;
+  return L;
+}
+// derived per step from the params (collapse kernel)
+struct ULay {
+  int64_t Ue, Ul, Ur, ce, cl, cr, WsT, WdT, Ws1, Wd1, total;
+};
+static ULay make_ulay(int D, int d) {
+  const int64_t F = d + D;
+  ULay U;
+  int64_t o = 0;
+  U.Ue = o; o += al4(H * F);
+  U.Ul = o; o += al4(H * D);
+  U.Ur = o; o += al4(H * D);
+  U.ce = o; o += al4(H);
+  U.cl = o; o += al4(H);
+  U.cr = o; o += al4(H);
+  U.WsT = o; o += al4((int64_t)D * D);
+  U.WdT = o; o += al4((int64_t)D * D);
+  U.Ws1 = o; o += al4(D);
+  U.Wd1 = o; o += al4(D);
+  U.total = o;
+  return U;
+}
+// backward partial slab: dUe[H*F] dUl[H*D] dUr[H*D] dce[H] dcl[H] dcr[H] dw[D] db[D]
+struct PLay {
+  int Ue, Ul, Ur, ce, cl, cr, w, b, total;
+};
+__host__ __device__ inline PLay make_play(int D, int d) {
+  const int F = d + D;
+  PLay P;
+  P.Ue = 0;
+  P.Ul = H * F;
+  P.Ur = P.Ul + H * D;
+  P.ce = P.Ur + H * D;
+  P.cl = P.ce + H;
+  P.cr = P.cl + H;
+  P.w = P.cr + H;
+  P.b = P.w + D;
+  P.total = P.b + D;
+  return P;
+}
+
+// ------------------------------------------------------------------ context
+struct Ctx {
+  int64_t N;
+  int K, D, d, F, Kn, drop, quirk;
+  float pf, pa, inv_kf, inv_ka;
+  float lr, b1, b2, eps;
+  const int64_t *ev_src, *ev_dst;
+  const float* ev_t;
+  const int64_t* ev_blk;
+  const float* ev_msg;
+  int64_t* neg;
+  const int64_t* dst_nodes;
+  int64_t n_dst;
+  const float* feat;
+  int64_t *nbr, *eid;
+  float* rt;
+  int64_t* assoc;
+  float* ta;
+  const float* mem;
+  float *params, *grads, *am, *av;
+  int64_t* ctl;
+  float *out_pos, *out_neg;
+  double* mrr;
+  int4* nodemap;
+  // workspace
+  uint64_t* touches;
+  int* seg_eoff;
+  int* seg_nintra;
+  float* seg_out;
+  float* seg_stats;
+  float* seg_g;
+  float* X;
+  float* U;
+  float* evs;
+  float* slabs;
+  float* red;
+  float* blkmax;
+  int* blk_rank;
+  int* blk_order;
+  float* HS;
+  int64_t Ecap;
+  int Bmax;
+  Lay L;
+  ULay UL;
+  PLay PL;
+};
+
+// touch key: node << 26 | block << 14 | kind << 12 | event ; kind 0 = neg, 1 = pos dst, 2 = src
+__device__ __forceinline__ int64_t knode(uint64_t k) { return (int64_t)(k >> 26); }
+__device__ __forceinline__ int kblk(uint64_t k) { return (int)((k >> 14) & 4095u); }
+__device__ __forceinline__ int kkind(uint64_t k) { return (int)((k >> 12) & 3u); }
+__device__ __forceinline__ int kev(uint64_t k) { return (int)(k & 4095u); }
+__device__ __forceinline__ uint64_t mkkey(int64_t node, int blk, int kind, int ev) {
+  return ((uint64_t)node << 26) | ((uint64_t)blk << 14) | ((uint64_t)kind << 12) | (uint64_t)ev;
+}
+
+__device__ __forceinline__ float keepf(uint64_t h, float p, float inv) { return u01(h) >= p ? inv : 0.0f; }
+__device__ __forceinline__ float node_keep(const Ctx& c, uint64_t seed, int blk, int64_t u, int dd) {
+  return keepf(hash4(seed, 1, ((uint64_t)blk << 32) ^ (uint64_t)u, (uint64_t)dd), c.pf, c.inv_kf);
+}
+__device__ __forceinline__ uint64_t seg_key(int blk, int64_t root) { return ((uint64_t)blk << 32) ^ (uint64_t)root; }
+
+// time_assoc[u] as of block `blk` of the current batch (model_utils.py:77-83)
+template <bool TRAIN>
+__device__ __forceinline__ float ta_at(const Ctx& c, int64_t u, int blk, int gen, const float* evt) {
+  const int4 inf = c.nodemap[u];
+  if (inf.x == gen) {
+    int lo = inf.y, hi = inf.y + inf.z;
+    if (TRAIN) {  // last assignment in blocks <= blk: order n, p, s within a block
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (kblk(c.touches[mid]) <= blk) lo = mid + 1; else hi = mid;
+      }
+      if (lo > inf.y) return evt[kev(c.touches[lo - 1])];
+    } else {      // eval: time_assoc[:] = max(t_blk), then s/p of the block
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (kblk(c.touches[mid]) < blk) lo = mid + 1; else hi = mid;
+      }
+      if (lo < inf.y + inf.z && kblk(c.touches[lo]) == blk) return evt[kev(c.touches[lo])];
+      return c.blkmax[blk];
+    }
+  }
+  return TRAIN ? c.ta[u] : c.blkmax[blk];
+}
+
+// ------------------------------------------------------------------ small kernels
+__global__ void tgnn_advance(int64_t* ctl, int mode, int64_t batch_start, int64_t B, int64_t cur, int64_t split_lo,
+                             int64_t split_hi, int64_t batch, int rank, int world, uint64_t base_seed, int train) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t bs = batch_start, Bv = B, ce = cur;
+  if (mode == 1) {
+    int64_t nb = ctl[TGNX_CTL_NB];
+    bs = split_lo + nb * batch;
+    Bv = bs >= split_hi ? 0 : (split_hi - bs < batch ? split_hi - bs : batch);
+    ce = bs;
+  }
+  ctl[TGNX_CTL_BATCH_START] = bs;
+  ctl[TGNX_CTL_B] = Bv;
+  ctl[TGNX_CTL_CUR_EID] = ce;
+  ctl[TGNX_CTL_GEN] += 1;
+  ctl[TGNX_CTL_NB] += 1;
+  if (train && Bv > 0) ctl[TGNX_CTL_ADAM_T] += 1;
+  ctl[TGNX_CTL_LO] = Bv * rank / world;
+  ctl[TGNX_CTL_HI] = Bv * (rank + 1) / world;
+  ctl[TGNX_CTL_SEED] = (int64_t)(mix64(base_seed ^ mix64((uint64_t)ctl[TGNX_CTL_NB])) >> 1);
+}
+
+__global__ void tgnn_negs(Ctx c) {
+  const int64_t B = c.ctl[TGNX_CTL_B];
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int64_t p = c.ev_dst[start + i];
+  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+  const uint64_t off = (uint64_t)c.ctl[TGNX_CTL_CUR_EID] + (uint64_t)i;
+  int64_t v = c.dst_nodes[0];
+  for (uint64_t attempt = 0; attempt < 64; ++attempt) {
+    uint64_t h = hash4(seed, 0x6E656773ull, off, attempt);
+    uint64_t r = (uint64_t)(((__uint128_t)(h >> 11) * (uint64_t)c.n_dst) >> 53);
+    v = c.dst_nodes[r];
+    if (v != p) break;
+  }
+  c.neg[start + i] = v;
+}
+
+// U = attn·W per head (exact collapse of EdgeGATConv's el/er/ee), predictor transposes/row sums
+__global__ void tgnn_collapse(Ctx c) {
+  const int D = c.D, F = c.F;
+  const float* P = c.params;
+  const int64_t nUe = (int64_t)H * F, nUl = H * D, nP = (int64_t)D * D;
+  const int64_t total = nUe + 2 * nUl + 3 * H + 2 * nP + 2 * D;
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total; x += (int64_t)gridDim.x * blockDim.x) {
+    int64_t y = x;
+    if (y < nUe) {
+      int h = (int)(y / F), f = (int)(y % F);
+      float s = 0.f;
+      for (int dd = 0; dd < D; ++dd) s += P[c.L.attn_e + h * D + dd] * P[c.L.We + (int64_t)(h * D + dd) * F + f];
+      c.U[c.UL.Ue + y] = s;
+      continue;
+    }
+    y -= nUe;
+    if (y < 2 * nUl) {
+      int which = (int)(y / nUl);
+      int64_t z = y % nUl;
+      int h = (int)(z / D), k = (int)(z % D);
+      const float* a = P + (which == 0 ? c.L.attn_l : c.L.attn_r) + h * D;
+      float s = 0.f;
+      for (int dd = 0; dd < D; ++dd) s += a[dd] * P[c.L.Wn + (int64_t)(h * D + dd) * D + k];
+      c.U[(which == 0 ? c.UL.Ul : c.UL.Ur) + z] = s;
+      continue;
+    }
+    y -= 2 * nUl;
+    if (y < 3 * H) {
+      int which = (int)(y / H), h = (int)(y % H);
+      const float* a = P + (which == 0 ? c.L.attn_e : which == 1 ? c.L.attn_l : c.L.attn_r) + h * D;
+      const float* b = P + (which == 0 ? c.L.be : c.L.bn) + h * D;
+      float s = 0.f;
+      for (int dd = 0; dd < D; ++dd) s += a[dd] * b[dd];
+      c.U[(which == 0 ? c.UL.ce : which == 1 ? c.UL.cl : c.UL.cr) + h] = s;
+      continue;
+    }
+    y -= 3 * H;
+    if (y < 2 * nP) {
+      int which = (int)(y / nP);
+      int64_t z = y % nP;
+      int dd = (int)(z / D), o = (int)(z % D);
+      c.U[(which == 0 ? c.UL.WsT : c.UL.WdT) + z] = P[(which == 0 ? c.L.Ws : c.L.Wd) + (int64_t)o * D + dd];
+      continue;
+    }
+    y -= 2 * nP;
+    {
+      int which = (int)(y / D), o = (int)(y % D);
+      const float* w = P + (which == 0 ? c.L.Ws : c.L.Wd) + (int64_t)o * D;
+      float s = 0.f;
+      for (int dd = 0; dd < D; ++dd) s += w[dd];
+      c.U[(which == 0 ? c.UL.Ws1 : c.UL.Wd1) + o] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ assembly (one workgroup)
+template <bool TRAIN>
+__global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int sh[20];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int tid = threadIdx.x, T = blockDim.x;
+  if (B == 0) {
+    if (tid == 0) c.ctl[TGNX_CTL_S] = c.ctl[TGNX_CTL_E] = 0;
+    return;
+  }
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int gen = (int)c.ctl[TGNX_CTL_GEN];
+  const int64_t* src = c.ev_src + start;
+  const int64_t* dst = c.ev_dst + start;
+  const float* evt = c.ev_t + start;
+  const int64_t* blk = c.ev_blk + start;
+  const int64_t* neg = c.neg + start * c.Kn;
+  const int NT = TRAIN ? 3 * B : 2 * B;
+  if (NT > TOUCH_MAX || B > c.Bmax || B > 4095) {
+    if (tid == 0) c.ctl[TGNX_CTL_ERR] |= 1;
+    return;
+  }
+  const int n = next_pow2(NT);
+  uint64_t* key = reinterpret_cast<uint64_t*>(smem);
+  int* run_start = reinterpret_cast<int*>(smem + (size_t)TOUCH_MAX * 8);
+  for (int p = tid; p < n; p += T) {
+    uint64_t k = ~0ull;
+    if (p < NT) {
+      int e = p % B, which = p / B;  // 0 = s, 1 = p, 2 = n
+      int64_t node = which == 0 ? src[e] : which == 1 ? dst[e] : neg[e];
+      k = mkkey(node, (int)blk[e], 2 - which, e);
+    }
+    key[p] = k;
+  }
+  __syncthreads();
+  bitonic_sort_u64(key, n);
+  for (int p = tid; p < NT; p += T) c.touches[p] = key[p];
+  // runs
+  int pc = (NT + T - 1) / T;
+  int p0 = tid * pc, p1 = min(NT, p0 + pc);
+  int cnt = 0;
+  for (int p = p0; p < p1; ++p) cnt += (p == 0 || knode(key[p]) != knode(key[p - 1]));
+  int U;
+  int rid = block_excl_scan(cnt, sh, &U);
+  for (int p = p0; p < p1; ++p)
+    if (p == 0 || knode(key[p]) != knode(key[p - 1])) run_start[rid++] = p;
+  __syncthreads();
+  for (int r = tid; r < U; r += T) {
+    const int a = run_start[r];
+    const int e = r + 1 < U ? run_start[r + 1] : NT;
+    const int64_t node = knode(key[a]);
+    c.nodemap[node] = make_int4(gen, a, e - a, 0);
+    if (TRAIN) {
+      int sp = 0, cur = -1, sp_at = 0;
+      for (int j = a; j < e; ++j) {
+        const uint64_t k = key[j];
+        const int b = kblk(k);
+        if (b != cur) {
+          cur = b;
+          sp_at = sp;
+        }
+        const int kind = kkind(k), ev = kev(k);
+        const int row = kind == 2 ? ev : kind == 1 ? B + ev : 2 * B + ev;
+        c.seg_nintra[row] = sp_at;
+        if (kind != 0) ++sp;
+      }
+    }
+  }
+  __syncthreads();
+  // block bookkeeping
+  {
+    float* bmax = c.blkmax;
+    for (int b = tid; b < B; b += T) bmax[b] = -INFINITY;
+    __syncthreads();
+    for (int e = tid; e < B; e += T) {
+      const int b = (int)blk[e];
+      atomicMax(&bmax[b], evt[e]);
+    }
+    __syncthreads();
+    // stable order by block: rank = #events in smaller blocks + #earlier events in same block
+    int* bc = run_start;
+    for (int b = tid; b < B; b += T) bc[b] = 0;
+    __syncthreads();
+    for (int e = tid; e < B; e += T) atomicAdd(&bc[(int)blk[e]], 1);
+    __syncthreads();
+    int chunk = (B + T - 1) / T;
+    int b0 = tid * chunk, b1 = min(B, b0 + chunk);
+    int s = 0;
+    for (int b = b0; b < b1; ++b) s += bc[b];
+    int tot;
+    int base = block_excl_scan(s, sh, &tot);
+    for (int b = b0; b < b1; ++b) {
+      int v = bc[b];
+      bc[b] = base;
+      base += v;
+    }
+    __syncthreads();
+    for (int e = tid; e < B; e += T) {
+      const int b = (int)blk[e];
+      int before = 0;
+      for (int j = 0; j < e; ++j) before += ((int)blk[j] == b);
+      const int rk = bc[b] + before;
+      c.blk_rank[e] = rk;
+      c.blk_order[rk] = e;
+    }
+  }
+  __syncthreads();
+  if (TRAIN) {
+    // edge offsets for the saved per-edge logits: ring valid + self loop + intra
+    const int S = 3 * B;
+    int chunk = (S + T - 1) / T;
+    int r0 = tid * chunk, r1 = min(S, r0 + chunk);
+    int s = 0;
+    for (int r = r0; r < r1; ++r) {
+      const int e = r % B, which = r / B;
+      const int64_t node = which == 0 ? src[e] : which == 1 ? dst[e] : neg[e];
+      int nr = 0;
+      for (int j = 0; j < c.K; ++j) nr += (c.eid[node * c.K + j] >= 0);
+      const int v = nr + 1 + c.seg_nintra[r];
+      c.seg_eoff[r] = v;
+      s += v;
+    }
+    int tot;
+    int base = block_excl_scan(s, sh, &tot);
+    for (int r = r0; r < r1; ++r) {
+      const int v = c.seg_eoff[r];
+      c.seg_eoff[r] = base;
+      base += v;
+    }
+    if (tid == 0) {
+      c.seg_eoff[S] = tot;
+      c.ctl[TGNX_CTL_S] = S;
+      c.ctl[TGNX_CTL_E] = tot;
+      if (tot > c.Ecap) c.ctl[TGNX_CTL_ERR] |= 2;
+    }
+  } else if (tid == 0) {
+    c.ctl[TGNX_CTL_S] = (int64_t)B * (2 + c.Kn);
+    c.ctl[TGNX_CTL_E] = 0;
+  }
+}
+
+// ------------------------------------------------------------------ segment geometry
+struct Seg {
+  int kind, i, cc, row, blk;
+  int64_t root;
+};
+__device__ __forceinline__ bool seg_of(const Ctx& c, int w, int B, int lo, int hi, Seg& s) {
+  const int nloc = hi - lo;
+  const int Kn = c.Kn;
+  if (w >= nloc * (2 + Kn)) return false;
+  if (w < nloc) {
+    s.kind = 2; s.i = lo + w; s.cc = 0;
+  } else if (w < 2 * nloc) {
+    s.kind = 1; s.i = lo + w - nloc; s.cc = 0;
+  } else {
+    const int q = w - 2 * nloc;
+    s.kind = 0; s.i = lo + q / Kn; s.cc = q % Kn;
+  }
+  s.row = s.kind == 2 ? s.i : s.kind == 1 ? B + s.i : 2 * B + s.i * Kn + s.cc;
+  return true;
+}
+
+// Per-lane model registers shared by forward and backward.
+template <int NJ>
+struct LaneW {
+  float ue[NJ][H];
+  float tw[NJ], tb[NJ];
+  float ul[2][H];
+  __device__ __forceinline__ void load(const Ctx& c, int lane) {
+#pragma unroll
+    for (int jj = 0; jj < NJ; ++jj) {
+      const int f = lane + 64 * jj;
+      const bool ok = f < c.F;
+#pragma unroll
+      for (int h = 0; h < H; ++h) ue[jj][h] = ok ? c.U[c.UL.Ue + h * c.F + f] : 0.f;
+      const bool enc = ok && f >= c.d;
+      tw[jj] = enc ? c.params[c.L.te_w + (f - c.d)] : 0.f;
+      tb[jj] = enc ? c.params[c.L.te_b + (f - c.d)] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int dd = lane + 64 * q;
+#pragma unroll
+      for (int h = 0; h < H; ++h) ul[q][h] = dd < c.D ? c.U[c.UL.Ul + h * c.D + dd] : 0.f;
+    }
+  }
+};
+
+// Edge walker: ring row (newest first) → self loop → intra-batch edges of earlier blocks
+struct EdgeWalk {
+  int64_t my_nbr, my_eid;
+  float my_rt;
+  int nring, nintra, rp, re;
+  __device__ __forceinline__ void init(const Ctx& c, const Seg& s, int gen, int lane) {
+    my_nbr = -1; my_eid = -1; my_rt = 0.f;
+    if (lane < c.K) {
+      my_eid = c.eid[s.root * c.K + lane];
+      my_nbr = c.nbr[s.root * c.K + lane];
+      my_rt = c.rt[s.root * c.K + lane];
+    }
+    nring = __popcll(__ballot(lane < c.K && my_eid >= 0));
+    const int4 inf = c.nodemap[s.root];
+    rp = 0; re = 0; nintra = 0;
+    if (inf.x == gen) {
+      rp = inf.y; re = inf.y + inf.z;
+      for (int j = rp; j < re; ++j) {
+        const uint64_t k = c.touches[j];
+        if (kblk(k) >= s.blk) break;
+        nintra += (kkind(k) != 0);
+      }
+    }
+  }
+  __device__ __forceinline__ int count() const { return nring + 1 + nintra; }
+  // returns source node u, feature row (nullptr = self-loop ones), edge time
+  __device__ __forceinline__ void edge(const Ctx& c, const Seg& s, int o, const int64_t* src, const int64_t* dst,
+                                       const float* evt, const float* msg, int64_t& u, const float*& fp, float& bt) {
+    if (o < nring) {
+      u = __shfl(my_nbr, o);
+      const int64_t e = __shfl(my_eid, o);
+      bt = __shfl(my_rt, o);
+      fp = c.feat + e * c.d;
+    } else if (o == nring) {
+      u = s.root; bt = 0.f; fp = nullptr;
+    } else {
+      uint64_t k;
+      do { k = c.touches[rp++]; } while (kkind(k) == 0);
+      const int ev = kev(k);
+      u = kkind(k) == 2 ? dst[ev] : src[ev];
+      fp = msg + (int64_t)ev * c.d;
+      bt = evt[ev];
+    }
+  }
+};
+
+// ------------------------------------------------------------------ forward: one wave per segment
+template <int NJ, bool TRAIN>
+__global__ void __launch_bounds__(256) tgnn_attn_fwd(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int lane = threadIdx.x & 63;
+  Seg s;
+  if (!seg_of(c, blockIdx.x * 4 + (threadIdx.x >> 6), B, (int)c.ctl[TGNX_CTL_LO], (int)c.ctl[TGNX_CTL_HI], s)) return;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int64_t* src = c.ev_src + start;
+  const int64_t* dst = c.ev_dst + start;
+  const float* evt = c.ev_t + start;
+  const float* msg = c.ev_msg + start * c.d;
+  const int64_t* neg = c.neg + start * c.Kn;
+  s.root = s.kind == 2 ? src[s.i] : s.kind == 1 ? dst[s.i] : neg[s.i * c.Kn + s.cc];
+  s.blk = (int)c.ev_blk[start + s.i];
+  const int gen = (int)c.ctl[TGNX_CTL_GEN];
+  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+  const bool drop = TRAIN && c.drop;
+
+  LaneW<NJ> W;
+  W.load(c, lane);
+  float cel[H], er[H];
+  float nfr[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int dd = lane + 64 * q;
+    float v = dd < c.D ? c.mem[s.root * c.D + dd] : 0.f;
+    if (drop && dd < c.D) v *= node_keep(c, seed, s.blk, s.root, dd);
+    nfr[q] = v;
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    float p = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int dd = lane + 64 * q;
+      if (dd < c.D) p += c.U[c.UL.Ur + h * c.D + dd] * nfr[q];
+    }
+    er[h] = wave_sum(p) + c.U[c.UL.cr + h];
+    cel[h] = c.U[c.UL.ce + h] + c.U[c.UL.cl + h];
+  }
+  EdgeWalk ew;
+  ew.init(c, s, gen, lane);
+  const int E = ew.count();
+  int eoff = 0;
+  if (TRAIN) {
+    eoff = c.seg_eoff[s.row];
+    if (eoff + E > c.Ecap) return;
+  }
+  const uint64_t sk = seg_key(s.blk, s.root);
+  float m[H], l[H], acc[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    m[h] = -INFINITY; l[h] = 0.f; acc[h] = 0.f;
+  }
+  for (int o = 0; o < E; ++o) {
+    int64_t u;
+    const float* fp;
+    float bt;
+    ew.edge(c, s, o, src, dst, evt, msg, u, fp, bt);
+    const float dt = bt - ta_at<TRAIN>(c, u, s.blk, gen, evt);
+    float part[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) part[h] = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < NJ; ++jj) {
+      const int f = lane + 64 * jj;
+      if (f < c.F) {
+        float v;
+        if (f < c.d) v = fp ? fp[f] : 1.0f;
+        else v = cosf(fmaf(W.tw[jj], dt, W.tb[jj]));
+        if (drop) v *= keepf(hash4(seed, 2, sk, ((uint64_t)o << 16) | (uint64_t)f), c.pf, c.inv_kf);
+#pragma unroll
+        for (int h = 0; h < H; ++h) part[h] += W.ue[jj][h] * v;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int dd = lane + 64 * q;
+      if (dd < c.D) {
+        float v = c.mem[u * c.D + dd];
+        if (drop) v *= node_keep(c, seed, s.blk, u, dd);
+#pragma unroll
+        for (int h = 0; h < H; ++h) part[h] += W.ul[q][h] * v;
+      }
+    }
+    float xs = 0.f;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float x = wave_sum(part[h]) + cel[h];
+      float sc = x + er[h];
+      sc = sc > 0.f ? sc : 0.2f * sc;
+      const float mn = fmaxf(m[h], sc);
+      const float r = expf(m[h] - mn);
+      const float e = expf(sc - mn);
+      float wgt = e;
+      if (drop) wgt *= keepf(hash4(seed, 3, sk, ((uint64_t)o << 16) | (uint64_t)h), c.pa, c.inv_ka);
+      l[h] = l[h] * r + e;
+      acc[h] = acc[h] * r + wgt * x;
+      m[h] = mn;
+      if (lane == h) xs = x;
+    }
+    if (TRAIN && lane < H) c.X[(int64_t)(eoff + o) * H + lane] = xs;
+  }
+  float out = 0.f;
+  float st[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const float ft = acc[h] / l[h];
+    out += ft;
+    if (lane == h) {
+      st[0] = m[h]; st[1] = l[h]; st[2] = ft; st[3] = er[h];
+    }
+  }
+  out *= (1.0f / H);
+  if (lane == 0) c.seg_out[s.row] = out;
+  if (TRAIN && lane < H) {
+    float* sp = c.seg_stats + (int64_t)s.row * 4 * H;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sp[k * H + lane] = st[k];
+  }
+}
+
+// ------------------------------------------------------------------ predictor (train): one wave per event
+__device__ __forceinline__ float softplus(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
+
+__global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
+  __shared__ float se[4][3][DMAX];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
+  const int i = lo + blockIdx.x * 4 + wv;
+  const bool active = B > 0 && i < hi && c.ctl[TGNX_CTL_ERR] == 0;
+  const int D = c.D;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+  int blk = 0;
+  if (active) {
+    blk = (int)c.ev_blk[start + i];
+    const int64_t roots[3] = {c.ev_src[start + i], c.ev_dst[start + i], c.neg[start + i]};
+    const int segs[3] = {i, B + i, 2 * B + i};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const float sv = c.seg_out[segs[r]];
+      for (int dd = lane; dd < D; dd += 64) {
+        float v = c.mem[roots[r] * D + dd];
+        if (c.drop) v *= node_keep(c, seed, blk, roots[r], dd);
+        se[wv][r][dd] = v + sv;
+      }
+    }
+  }
+  __syncthreads();
+  if (!active) return;
+  const float* P = c.params;
+  float hs[2], hp[2], hn[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int o = lane + 64 * q;
+    float a = 0.f, b = 0.f, d2 = 0.f;
+    if (o < D) {
+      a = P[c.L.bs + o]; b = P[c.L.bd + o]; d2 = b;
+      const float* WsT = c.U + c.UL.WsT;
+      const float* WdT = c.U + c.UL.WdT;
+      for (int dd = 0; dd < D; ++dd) {
+        a += WsT[dd * D + o] * se[wv][0][dd];
+        b += WdT[dd * D + o] * se[wv][1][dd];
+        d2 += WdT[dd * D + o] * se[wv][2][dd];
+      }
+    }
+    hs[q] = a; hp[q] = b; hn[q] = d2;
+  }
+  float hpos[2], hneg[2], zp = 0.f, zn = 0.f;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int o = lane + 64 * q;
+    hpos[q] = fmaxf(hs[q] + hp[q], 0.f);
+    hneg[q] = fmaxf(hs[q] + hn[q], 0.f);
+    if (o < D) {
+      zp += P[c.L.Wo + o] * hpos[q];
+      zn += P[c.L.Wo + o] * hneg[q];
+    }
+  }
+  zp = wave_sum(zp) + P[c.L.bo];
+  zn = wave_sum(zn) + P[c.L.bo];
+  const float invB = 1.0f / (float)B;
+  const float dzp = (1.0f / (1.0f + expf(-zp)) - 1.0f) * invB;
+  const float dzn = (1.0f / (1.0f + expf(-zn))) * invB;
+  const float li = (softplus(-zp) + softplus(zn)) * invB;
+  float* ev = c.evs + (int64_t)i * (8 * D + 4);
+  float gs = 0.f, gp = 0.f, gn = 0.f;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int o = lane + 64 * q;
+    if (o < D) {
+      const float wo = P[c.L.Wo + o];
+      const float dhp = hpos[q] > 0.f ? dzp * wo : 0.f;
+      const float dhn = hneg[q] > 0.f ? dzn * wo : 0.f;
+      const float A = dhp + dhn;
+      gs += A * c.U[c.UL.Ws1 + o];
+      gp += dhp * c.U[c.UL.Wd1 + o];
+      gn += dhn * c.U[c.UL.Wd1 + o];
+      ev[0 * D + o] = A;
+      ev[1 * D + o] = se[wv][0][o];
+      ev[2 * D + o] = dhp;
+      ev[3 * D + o] = se[wv][1][o];
+      ev[4 * D + o] = dhn;
+      ev[5 * D + o] = se[wv][2][o];
+      ev[6 * D + o] = hpos[q];
+      ev[7 * D + o] = hneg[q];
+    }
+  }
+  gs = wave_sum(gs);
+  gp = wave_sum(gp);
+  gn = wave_sum(gn);
+  if (lane == 0) {
+    c.seg_g[i] = gs;
+    c.seg_g[B + i] = gp;
+    c.seg_g[2 * B + i] = gn;
+    c.out_pos[i] = zp;
+    c.out_neg[i] = zn;
+    ev[8 * D + 0] = dzp;
+    ev[8 * D + 1] = dzn;
+    ev[8 * D + 2] = li;
+  }
+}
+
+// predictor parameter gradients: sums over the rank's events of outer products
+__global__ void tgnn_pred_reduce(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int D = c.D;
+  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
+  const int64_t DD = (int64_t)D * D;
+  const int64_t total = 2 * DD + 3 * D + 2;
+  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (x >= total) return;
+  const bool ok = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
+  const int S = 8 * D + 4;
+  float acc = 0.f;
+  if (x < DD) {  // dWs[o][dd] = Σ A[o] es[dd]
+    const int o = (int)(x / D), dd = (int)(x % D);
+    if (ok)
+      for (int i = lo; i < hi; ++i) acc += c.evs[(int64_t)i * S + o] * c.evs[(int64_t)i * S + D + dd];
+    c.grads[c.L.Ws + x] = acc;
+  } else if (x < 2 * DD) {  // dWd[o][dd] = Σ dhp[o] ep[dd] + dhn[o] en[dd]
+    const int64_t y = x - DD;
+    const int o = (int)(y / D), dd = (int)(y % D);
+    if (ok)
+      for (int i = lo; i < hi; ++i) {
+        const float* e = c.evs + (int64_t)i * S;
+        acc += e[2 * D + o] * e[3 * D + dd] + e[4 * D + o] * e[5 * D + dd];
+      }
+    c.grads[c.L.Wd + y] = acc;
+  } else {
+    const int y = (int)(x - 2 * DD);
+    if (y < D) {  // dbs = Σ A
+      if (ok) for (int i = lo; i < hi; ++i) acc += c.evs[(int64_t)i * S + y];
+      c.grads[c.L.bs + y] = acc;
+    } else if (y < 2 * D) {  // dbd = Σ dhp + dhn
+      const int o = y - D;
+      if (ok) for (int i = lo; i < hi; ++i) acc += c.evs[(int64_t)i * S + 2 * D + o] + c.evs[(int64_t)i * S + 4 * D + o];
+      c.grads[c.L.bd + o] = acc;
+    } else if (y < 3 * D) {  // dWo = Σ dzp hpos + dzn hneg
+      const int o = y - 2 * D;
+      if (ok)
+        for (int i = lo; i < hi; ++i) {
+          const float* e = c.evs + (int64_t)i * S;
+          acc += e[8 * D] * e[6 * D + o] + e[8 * D + 1] * e[7 * D + o];
+        }
+      c.grads[c.L.Wo + o] = acc;
+    } else if (y == 3 * D) {  // dbo
+      if (ok) for (int i = lo; i < hi; ++i) acc += c.evs[(int64_t)i * S + 8 * D] + c.evs[(int64_t)i * S + 8 * D + 1];
+      c.grads[c.L.bo] = acc;
+    } else {  // batch loss slot
+      if (ok) for (int i = lo; i < hi; ++i) acc += c.evs[(int64_t)i * S + 8 * D + 2];
+      c.grads[c.L.total] = acc;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward: persistent waves
+template <int NJ>
+__global__ void __launch_bounds__(256) tgnn_attn_bwd(Ctx c) {
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const PLay PL = c.PL;
+  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) red[p] = 0.f;
+  __syncthreads();
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int64_t* src = c.ev_src + start;
+  const int64_t* dst = c.ev_dst + start;
+  const float* evt = c.ev_t + start;
+  const float* msg = c.ev_msg + start * c.d;
+  const int64_t* neg = c.neg + start * c.Kn;
+  const int gen = (int)c.ctl[TGNX_CTL_GEN];
+  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+  const bool drop = c.drop;
+  const bool ok = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
+
+  LaneW<NJ> W;
+  W.load(c, lane);
+  float aUe[NJ][H], aUl[2][H], aUr[2][H], aw[NJ], ab[NJ];
+  float ace[H], acl[H], acr[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+#pragma unroll
+    for (int jj = 0; jj < NJ; ++jj) aUe[jj][h] = 0.f;
+    aUl[0][h] = aUl[1][h] = aUr[0][h] = aUr[1][h] = 0.f;
+    ace[h] = acl[h] = acr[h] = 0.f;
+  }
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) aw[jj] = ab[jj] = 0.f;
+
+  const int nrows = ok ? (hi - lo) * (2 + c.Kn) : 0;
+  for (int w = blockIdx.x * 4 + wv; w < nrows; w += gridDim.x * 4) {
+    Seg s;
+    seg_of(c, w, B, lo, hi, s);
+    const float g = c.seg_g[s.row];
+    if (g == 0.f) continue;
+    s.root = s.kind == 2 ? src[s.i] : s.kind == 1 ? dst[s.i] : neg[s.i * c.Kn + s.cc];
+    s.blk = (int)c.ev_blk[start + s.i];
+    const float gh = g * (1.0f / H);
+    const float* sp = c.seg_stats + (int64_t)s.row * 4 * H;
+    float m[H], l[H], ft[H], er[H], der[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      m[h] = sp[h]; l[h] = sp[H + h]; ft[h] = sp[2 * H + h]; er[h] = sp[3 * H + h]; der[h] = 0.f;
+    }
+    float nfr[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int dd = lane + 64 * q;
+      float v = dd < c.D ? c.mem[s.root * c.D + dd] : 0.f;
+      if (drop && dd < c.D) v *= node_keep(c, seed, s.blk, s.root, dd);
+      nfr[q] = v;
+    }
+    EdgeWalk ew;
+    ew.init(c, s, gen, lane);
+    const int E = ew.count();
+    const int eoff = c.seg_eoff[s.row];
+    if (eoff + E > c.Ecap) continue;
+    const uint64_t sk = seg_key(s.blk, s.root);
+    for (int o = 0; o < E; ++o) {
+      int64_t u;
+      const float* fp;
+      float bt;
+      ew.edge(c, s, o, src, dst, evt, msg, u, fp, bt);
+      const float dt = bt - ta_at<true>(c, u, s.blk, gen, evt);
+      float v[NJ], km[NJ], sn[NJ];
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj) {
+        const int f = lane + 64 * jj;
+        v[jj] = 0.f; km[jj] = 1.f; sn[jj] = 0.f;
+        if (f < c.F) {
+          if (f < c.d) {
+            v[jj] = fp ? fp[f] : 1.0f;
+          } else {
+            float sa, ca;
+            sincosf(fmaf(W.tw[jj], dt, W.tb[jj]), &sa, &ca);
+            v[jj] = ca;
+            sn[jj] = sa;
+          }
+          if (drop) km[jj] = keepf(hash4(seed, 2, sk, ((uint64_t)o << 16) | (uint64_t)f), c.pf, c.inv_kf);
+          v[jj] *= km[jj];
+        }
+      }
+      float nfu[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int dd = lane + 64 * q;
+        float x = dd < c.D ? c.mem[u * c.D + dd] : 0.f;
+        if (drop && dd < c.D) x *= node_keep(c, seed, s.blk, u, dd);
+        nfu[q] = x;
+      }
+      const float* xp = c.X + (int64_t)(eoff + o) * H;
+      float dx[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const float xh = xp[h];
+        float sc = xh + er[h];
+        const float lk = sc > 0.f ? 1.f : 0.2f;
+        sc = sc > 0.f ? sc : 0.2f * sc;
+        const float a = expf(sc - m[h]) / l[h];
+        const float mk = drop ? keepf(hash4(seed, 3, sk, ((uint64_t)o << 16) | (uint64_t)h), c.pa, c.inv_ka) : 1.f;
+        const float ds = a * gh * (xh * mk - ft[h]) * lk;
+        dx[h] = gh * a * mk + ds;
+        der[h] += ds;
+        ace[h] += dx[h];
+        acl[h] += dx[h];
+      }
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj) {
+        float denc = 0.f;
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          aUe[jj][h] += dx[h] * v[jj];
+          denc += dx[h] * W.ue[jj][h];
+        }
+        const int f = lane + 64 * jj;
+        if (f >= c.d && f < c.F) {
+          const float gz = -denc * km[jj] * sn[jj];
+          aw[jj] += gz * dt;
+          ab[jj] += gz;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int h = 0; h < H; ++h) aUl[q][h] += dx[h] * nfu[q];
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      acr[h] += der[h];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) aUr[q][h] += der[h] * nfr[q];
+    }
+  }
+  // deterministic workgroup reduction: waves add in order
+  for (int k = 0; k < 4; ++k) {
+    if (wv == k) {
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj) {
+        const int f = lane + 64 * jj;
+        if (f < c.F) {
+#pragma unroll
+          for (int h = 0; h < H; ++h) red[PL.Ue + h * c.F + f] += aUe[jj][h];
+          if (f >= c.d) {
+            red[PL.w + f - c.d] += aw[jj];
+            red[PL.b + f - c.d] += ab[jj];
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int dd = lane + 64 * q;
+        if (dd < c.D) {
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            red[PL.Ul + h * c.D + dd] += aUl[q][h];
+            red[PL.Ur + h * c.D + dd] += aUr[q][h];
+          }
+        }
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          red[PL.ce + h] += ace[h];
+          red[PL.cl + h] += acl[h];
+          red[PL.cr + h] += acr[h];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* slab = c.slabs + (int64_t)blockIdx.x * PL.total;
+  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) slab[p] = red[p];
+}
+
+__global__ void tgnn_grad_reduce(Ctx c, int G) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= c.PL.total) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += c.slabs[(int64_t)g * c.PL.total + p];
+  c.red[p] = s;
+}
+
+// re-expand the collapsed gradients into the reference's parameters
+__global__ void tgnn_grad_expand(Ctx c) {
+  const Lay L = c.L;
+  const PLay PL = c.PL;
+  const int D = c.D, F = c.F;
+  const float* P = c.params;
+  const float* r = c.red;
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < L.Ws; x += (int64_t)gridDim.x * blockDim.x) {
+    float g = 0.f;
+    if (x >= L.te_w && x < L.te_w + D) {
+      g = r[PL.w + (x - L.te_w)];
+    } else if (x >= L.te_b && x < L.te_b + D) {
+      g = r[PL.b + (x - L.te_b)];
+    } else if ((x >= L.attn_l && x < L.attn_l + H * D) || (x >= L.attn_r && x < L.attn_r + H * D)) {
+      const bool isl = x < L.attn_r;
+      const int j = (int)(x - (isl ? L.attn_l : L.attn_r));
+      const int h = j / D;
+      const float* dU = r + (isl ? PL.Ul : PL.Ur) + h * D;
+      const float* w = P + L.Wn + (int64_t)j * D;
+      for (int k = 0; k < D; ++k) g += w[k] * dU[k];
+      g += P[L.bn + j] * r[(isl ? PL.cl : PL.cr) + h];
+    } else if (x >= L.attn_e && x < L.attn_e + H * D) {
+      const int j = (int)(x - L.attn_e);
+      const int h = j / D;
+      const float* dU = r + PL.Ue + h * F;
+      const float* w = P + L.We + (int64_t)j * F;
+      for (int f = 0; f < F; ++f) g += w[f] * dU[f];
+      g += P[L.be + j] * r[PL.ce + h];
+    } else if (x >= L.Wn && x < L.Wn + (int64_t)H * D * D) {
+      const int64_t y = x - L.Wn;
+      const int j = (int)(y / D), k = (int)(y % D), h = j / D;
+      g = P[L.attn_l + j] * r[PL.Ul + h * D + k] + P[L.attn_r + j] * r[PL.Ur + h * D + k];
+    } else if (x >= L.bn && x < L.bn + H * D) {
+      const int j = (int)(x - L.bn), h = j / D;
+      g = P[L.attn_l + j] * r[PL.cl + h] + P[L.attn_r + j] * r[PL.cr + h];
+    } else if (x >= L.We && x < L.We + (int64_t)H * D * F) {
+      const int64_t y = x - L.We;
+      const int j = (int)(y / F), f = (int)(y % F), h = j / D;
+      g = P[L.attn_e + j] * r[PL.Ue + h * F + f];
+    } else if (x >= L.be && x < L.be + H * D) {
+      const int j = (int)(x - L.be), h = j / D;
+      g = P[L.attn_e + j] * r[PL.ce + h];
+    }
+    c.grads[x] = g;
+  }
+}
+
+// torch.optim.Adam (single-tensor form), bias corrections from the device step count
+__global__ void tgnn_adam(Ctx c) {
+  const int64_t B = c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
+  const double bc1 = 1.0 - pow((double)c.b1, (double)t);
+  const double bc2 = 1.0 - pow((double)c.b2, (double)t);
+  const float step = (float)(c.lr / bc1);
+  const float bc2s = (float)sqrt(bc2);
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < c.L.total; x += (int64_t)gridDim.x * blockDim.x) {
+    const float g = c.grads[x];
+    float m = c.am[x], v = c.av[x];
+    m = m + (1.0f - c.b1) * (g - m);
+    v = v * c.b2 + (1.0f - c.b2) * g * g;
+    c.am[x] = m;
+    c.av[x] = v;
+    const float den = sqrtf(v) / bc2s + c.eps;
+    c.params[x] -= step * (m / den);
+  }
+}
+
+// ------------------------------------------------------------------ finish: time_assoc + ring insert (1 WG)
+template <bool TRAIN>
+__global__ void __launch_bounds__(1024) tgnn_finish(Ctx c) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int sh[20];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const float* evt = c.ev_t + start;
+  const int NT = TRAIN ? 3 * B : 2 * B;
+  if (TRAIN) {  // final time_assoc = last assignment of each touched node (model_utils.py:81-83)
+    for (int j = threadIdx.x; j < NT; j += blockDim.x) {
+      const uint64_t k = c.touches[j];
+      if (j == NT - 1 || knode(c.touches[j + 1]) != knode(k)) c.ta[knode(k)] = evt[kev(k)];
+    }
+  } else {      // after tgnn_ta_fill: s/p of the last block keep their own t (model_utils.py:79-83)
+    int kmax = 0;
+    for (int e = 0; e < B; ++e) kmax = max(kmax, (int)c.ev_blk[start + e]);
+    for (int j = threadIdx.x; j < NT; j += blockDim.x) {
+      const uint64_t k = c.touches[j];
+      if (kblk(k) == kmax) c.ta[knode(k)] = evt[kev(k)];
+    }
+  }
+  ring_insert_block(c.nbr, c.eid, c.rt, c.K, c.ev_src + start, c.ev_dst + start, evt, B,
+                    c.ctl[TGNX_CTL_CUR_EID], c.assoc, smem, sh);
+  if (threadIdx.x == 0) {
+    if (TRAIN) {
+      double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
+      *loss += (double)c.grads[c.L.total] * (double)B;
+    }
+  }
+}
+
+__global__ void tgnn_ta_fill(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  int kmax = 0;
+  for (int e = 0; e < B; ++e) kmax = max(kmax, (int)c.ev_blk[start + e]);
+  const float v = c.blkmax[kmax];
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < c.N; x += (int64_t)gridDim.x * blockDim.x)
+    c.ta[x] = v;
+}
+
+// ------------------------------------------------------------------ eval predictor + MRR
+// phase 1: one wave per event: source projection (kept in block order) and the positive logit
+__global__ void __launch_bounds__(256) tgnn_pred_eval_src(Ctx c) {
+  __shared__ float se[4][2][DMAX];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * 4 + wv;
+  const bool active = B > 0 && i < B && c.ctl[TGNX_CTL_ERR] == 0;
+  const int D = c.D;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  if (active) {
+    const int64_t roots[2] = {c.ev_src[start + i], c.ev_dst[start + i]};
+    const int segs[2] = {i, B + i};
+    for (int r = 0; r < 2; ++r) {
+      const float sv = c.seg_out[segs[r]];
+      for (int dd = lane; dd < D; dd += 64) se[wv][r][dd] = c.mem[roots[r] * D + dd] + sv;
+    }
+  }
+  __syncthreads();
+  if (!active) return;
+  const float* P = c.params;
+  const int rho = c.blk_rank[i];
+  float z = 0.f;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int o = lane + 64 * q;
+    if (o < D) {
+      float a = P[c.L.bs + o], b = P[c.L.bd + o];
+      for (int dd = 0; dd < D; ++dd) {
+        a += c.U[c.UL.WsT + dd * D + o] * se[wv][0][dd];
+        b += c.U[c.UL.WdT + dd * D + o] * se[wv][1][dd];
+      }
+      c.HS[(int64_t)rho * D + o] = a;
+      z += P[c.L.Wo + o] * fmaxf(a + b, 0.f);
+    }
+  }
+  z = wave_sum(z) + P[c.L.bo];
+  if (lane == 0) c.out_pos[rho] = z;
+}
+
+// phase 2: one wave per negative row, rows in block order (model_utils.py:135-137, 159)
+__global__ void __launch_bounds__(256) tgnn_pred_eval_neg(Ctx c) {
+  __shared__ float se[4][DMAX];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int Kn = c.Kn;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wv;
+  const bool active = B > 0 && r < (int64_t)B * Kn && c.ctl[TGNX_CTL_ERR] == 0;
+  const int D = c.D;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  int rho = 0;
+  if (active) {
+    rho = (int)(r / Kn);
+    const int cc = (int)(r % Kn);
+    const int i = c.blk_order[rho];
+    const int64_t root = c.neg[(start + i) * Kn + cc];
+    const float sv = c.seg_out[2 * B + i * Kn + cc];
+    for (int dd = lane; dd < D; dd += 64) se[wv][dd] = c.mem[root * D + dd] + sv;
+  }
+  __syncthreads();
+  if (!active) return;
+  const float* P = c.params;
+  const int srow = c.quirk ? (int)(r % B) : rho;   // h_src.tile(neg_samples, 1) (model_utils.py:192)
+  float z = 0.f;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int o = lane + 64 * q;
+    if (o < D) {
+      float b = P[c.L.bd + o];
+      for (int dd = 0; dd < D; ++dd) b += c.U[c.UL.WdT + dd * D + o] * se[wv][dd];
+      z += P[c.L.Wo + o] * fmaxf(c.HS[(int64_t)srow * D + o] + b, 0.f);
+    }
+  }
+  z = wave_sum(z) + P[c.L.bo];
+  if (lane == 0) c.out_neg[r] = z;
+}
+
+// TGB rank rule: rank = 0.5 (#neg > pos + #neg >= pos) + 1; batch MRR = mean 1/rank
+__global__ void __launch_bounds__(1024) tgnn_mrr(Ctx c) {
+  __shared__ double red[1024];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int Kn = c.Kn;
+  double s = 0.0;
+  for (int rho = threadIdx.x; rho < B; rho += blockDim.x) {
+    const float p = c.out_pos[rho];
+    int gt = 0, ge = 0;
+    const float* ng = c.out_neg + (int64_t)rho * Kn;
+    for (int k = 0; k < Kn; ++k) {
+      gt += ng[k] > p;
+      ge += ng[k] >= p;
+    }
+    s += 1.0 / (0.5 * (gt + ge) + 1.0);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) c.mrr[(c.ctl[TGNX_CTL_NB] - 1) & (MRR_SLOTS - 1)] = red[0] / (double)B;
+}
+
+// ------------------------------------------------------------------ host glue
+static size_t carve(size_t& off, size_t bytes) {
+  size_t o = off;
+  off += (bytes + 255) & ~size_t(255);
+  return o;
+}
+
+struct WsLay {
+  size_t touches, seg_eoff, seg_nintra, seg_out, seg_stats, seg_g, X, U, evs, slabs, red, blkmax, blk_rank,
+      blk_order, HS, total;
+  int64_t Ecap;
+};
+static WsLay make_ws(const tgnx_tgnn_config* cfg) {
+  WsLay W;
+  const int64_t B = cfg->max_batch, Kn = cfg->max_neg < 1 ? 1 : cfg->max_neg;
+  const int D = cfg->mem_dim, d = cfg->msg_dim;
+  W.Ecap = 3 * B * (cfg->ring + 1) + 2 * B * B + 64;
+  size_t off = 0;
+  W.touches = carve(off, (size_t)TOUCH_MAX * 8);
+  W.seg_eoff = carve(off, (size_t)(3 * B + 1) * 4);
+  W.seg_nintra = carve(off, (size_t)3 * B * 4);
+  W.seg_out = carve(off, (size_t)B * (2 + (Kn > 1 ? Kn : 1)) * 4);
+  W.seg_stats = carve(off, (size_t)3 * B * 4 * H * 4);
+  W.seg_g = carve(off, (size_t)3 * B * 4);
+  W.X = carve(off, (size_t)W.Ecap * H * 4);
+  W.U = carve(off, (size_t)make_ulay(D, d).total * 4);
+  W.evs = carve(off, (size_t)B * (8 * D + 4) * 4);
+  W.slabs = carve(off, (size_t)GBWD * make_play(D, d).total * 4);
+  W.red = carve(off, (size_t)make_play(D, d).total * 4);
+  W.blkmax = carve(off, (size_t)B * 4);
+  W.blk_rank = carve(off, (size_t)B * 4);
+  W.blk_order = carve(off, (size_t)B * 4);
+  W.HS = carve(off, (size_t)B * D * 4);
+  W.total = off;
+  return W;
+}
+
+static int check_cfg(const tgnx_tgnn_config* cfg) {
+  TGNX_CHECK_ARG(cfg, "tgnn: null config");
+  TGNX_CHECK_ARG(cfg->heads == H, "tgnn: heads must be %d (gnn.att_head), got %d", H, cfg->heads);
+  TGNX_CHECK_ARG(cfg->mem_dim > 0 && cfg->mem_dim <= DMAX, "tgnn: mem_dim must be in [1, %d]", DMAX);
+  TGNX_CHECK_ARG(cfg->msg_dim >= 0 && cfg->msg_dim + cfg->mem_dim <= FMAX, "tgnn: msg_dim + mem_dim must be <= %d",
+                 FMAX);
+  TGNX_CHECK_ARG(cfg->ring > 0 && cfg->ring <= KMAX && cfg->ring <= 64, "tgnn: ring size must be in [1, %d]", KMAX);
+  TGNX_CHECK_ARG(cfg->max_batch > 0 && 3 * cfg->max_batch <= TOUCH_MAX, "tgnn: max_batch must be in [1, %d]",
+                 TOUCH_MAX / 3);
+  TGNX_CHECK_ARG(cfg->num_nodes > 0 && cfg->num_nodes < (1ll << 37), "tgnn: bad num_nodes");
+  return TGNX_OK;
+}
+
+static int make_ctx(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* b, int Kn, Ctx& c) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(b && b->ctl && b->ws && b->node_map && b->params && b->ev_src && b->ev_dst && b->ev_t && b->ev_blk,
+                 "tgnn: null buffer");
+  memset(&c, 0, sizeof(c));
+  c.N = cfg->num_nodes;
+  c.K = cfg->ring;
+  c.D = cfg->mem_dim;
+  c.d = cfg->msg_dim;
+  c.F = c.d + c.D;
+  c.Kn = Kn;
+  c.pf = cfg->feat_drop;
+  c.pa = cfg->attn_drop;
+  c.inv_kf = cfg->feat_drop < 1.f ? 1.0f / (1.0f - cfg->feat_drop) : 0.f;
+  c.inv_ka = cfg->attn_drop < 1.f ? 1.0f / (1.0f - cfg->attn_drop) : 0.f;
+  c.lr = cfg->lr;
+  c.b1 = cfg->beta1;
+  c.b2 = cfg->beta2;
+  c.eps = cfg->eps;
+  c.ev_src = b->ev_src;
+  c.ev_dst = b->ev_dst;
+  c.ev_t = b->ev_t;
+  c.ev_blk = b->ev_blk;
+  c.ev_msg = b->ev_msg;
+  c.neg = b->neg;
+  c.dst_nodes = b->dst_nodes;
+  c.n_dst = b->n_dst;
+  c.feat = b->feat;
+  c.nbr = b->nbr;
+  c.eid = b->eid;
+  c.rt = b->rt;
+  c.assoc = b->assoc;
+  c.ta = b->time_assoc;
+  c.mem = b->memory;
+  c.params = b->params;
+  c.grads = b->grads;
+  c.am = b->adam_m;
+  c.av = b->adam_v;
+  c.ctl = b->ctl;
+  c.out_pos = b->out_pos;
+  c.out_neg = b->out_neg;
+  c.mrr = b->mrr;
+  c.nodemap = reinterpret_cast<int4*>(b->node_map);
+  WsLay W = make_ws(cfg);
+  char* ws = reinterpret_cast<char*>(b->ws);
+  c.touches = reinterpret_cast<uint64_t*>(ws + W.touches);
+  c.seg_eoff = reinterpret_cast<int*>(ws + W.seg_eoff);
+  c.seg_nintra = reinterpret_cast<int*>(ws + W.seg_nintra);
+  c.seg_out = reinterpret_cast<float*>(ws + W.seg_out);
+  c.seg_stats = reinterpret_cast<float*>(ws + W.seg_stats);
+  c.seg_g = reinterpret_cast<float*>(ws + W.seg_g);
+  c.X = reinterpret_cast<float*>(ws + W.X);
+  c.U = reinterpret_cast<float*>(ws + W.U);
+  c.evs = reinterpret_cast<float*>(ws + W.evs);
+  c.slabs = reinterpret_cast<float*>(ws + W.slabs);
+  c.red = reinterpret_cast<float*>(ws + W.red);
+  c.blkmax = reinterpret_cast<float*>(ws + W.blkmax);
+  c.blk_rank = reinterpret_cast<int*>(ws + W.blk_rank);
+  c.blk_order = reinterpret_cast<int*>(ws + W.blk_order);
+  c.HS = reinterpret_cast<float*>(ws + W.HS);
+  c.Ecap = W.Ecap;
+  c.Bmax = cfg->max_batch;
+  c.L = make_lay(c.D, c.d);
+  c.UL = make_ulay(c.D, c.d);
+  c.PL = make_play(c.D, c.d);
+  return TGNX_OK;
+}
+
+static inline int grid_for(int64_t n, int per) { return (int)((n + per - 1) / per); }
+
+template <bool TRAIN>
+static int launch_attn_fwd(const Ctx& c, int rows_cap, hipStream_t s) {
+  const int F = c.F;
+  const int g = grid_for(rows_cap, 4);
+  if (g == 0) return TGNX_OK;
+  if (F <= 64) tgnn_attn_fwd<1, TRAIN><<<g, 256, 0, s>>>(c);
+  else if (F <= 128) tgnn_attn_fwd<2, TRAIN><<<g, 256, 0, s>>>(c);
+  else if (F <= 192) tgnn_attn_fwd<3, TRAIN><<<g, 256, 0, s>>>(c);
+  else if (F <= 256) tgnn_attn_fwd<4, TRAIN><<<g, 256, 0, s>>>(c);
+  else tgnn_attn_fwd<5, TRAIN><<<g, 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_attn_fwd");
+  return TGNX_OK;
+}
+
+static int launch_attn_bwd(const Ctx& c, hipStream_t s) {
+  const int F = c.F;
+  const size_t shm = (size_t)c.PL.total * 4;
+  if (F <= 64) tgnn_attn_bwd<1><<<GBWD, 256, shm, s>>>(c);
+  else if (F <= 128) tgnn_attn_bwd<2><<<GBWD, 256, shm, s>>>(c);
+  else if (F <= 192) tgnn_attn_bwd<3><<<GBWD, 256, shm, s>>>(c);
+  else if (F <= 256) tgnn_attn_bwd<4><<<GBWD, 256, shm, s>>>(c);
+  else tgnn_attn_bwd<5><<<GBWD, 256, shm, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_attn_bwd");
+  return TGNX_OK;
+}
+
+static size_t assemble_smem() { return (size_t)TOUCH_MAX * 8 + (size_t)TOUCH_MAX * 4; }
+
+}  // namespace tgnx
+
+using namespace tgnx;
+
+extern "C" {
+
+int tgnx_tgnn_param_layout(const tgnx_tgnn_config* cfg, int64_t* off) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(off, "tgnx_tgnn_param_layout: null output");
+  Lay L = make_lay(cfg->mem_dim, cfg->msg_dim);
+  const int64_t v[TGNX_TGNN_NPARAM + 1] = {L.te_w, L.te_b, L.attn_l, L.attn_r, L.attn_e, L.Wn, L.bn, L.We,
+                                           L.be,   L.Ws,   L.bs,     L.Wd,     L.bd,     L.Wo, L.bo, L.total};
+  for (int k = 0; k <= TGNX_TGNN_NPARAM; ++k) off[k] = v[k];
+  return TGNX_OK;
+}
+
+size_t tgnx_tgnn_ws_bytes(const tgnx_tgnn_config* cfg) {
+  if (check_cfg(cfg)) return 0;
+  return make_ws(cfg).total;
+}
+
+int tgnx_tgnn_advance(int64_t* ctl, int32_t mode, int64_t batch_start, int64_t B, int64_t cur_e_id, int64_t split_lo,
+                      int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed, int32_t train,
+                      void* stream) {
+  TGNX_CHECK_ARG(ctl && (mode == 0 || mode == 1) && world >= 1 && rank >= 0 && rank < world,
+                 "tgnx_tgnn_advance: bad arguments");
+  TGNX_CHECK_ARG(mode == 0 ? (B >= 0 && B < 4096) : (batch > 0 && batch < 4096), "tgnx_tgnn_advance: batch too large");
+  tgnn_advance<<<1, 64, 0, as_stream(stream)>>>(ctl, mode, batch_start, B, cur_e_id, split_lo, split_hi, batch, rank,
+                                                world, base_seed, train);
+  TGNX_LAUNCH_CHECK("tgnn_advance");
+  return TGNX_OK;
+}
+
+int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t gen_neg,
+                            int32_t dropout, void* stream) {
+  Ctx c;
+  int rc = make_ctx(cfg, buf, 1, c);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(buf->neg && buf->grads && buf->out_pos && buf->out_neg && buf->feat && buf->ev_msg && buf->memory &&
+                     buf->time_assoc && buf->nbr && buf->eid && buf->rt,
+                 "tgnx_tgnn_train_fwd_bwd: null buffer");
+  TGNX_CHECK_ARG(!gen_neg || (buf->dst_nodes && buf->n_dst > 0), "tgnx_tgnn_train_fwd_bwd: no destination set");
+  c.drop = dropout && (c.pf > 0.f || c.pa > 0.f);
+  hipStream_t s = as_stream(stream);
+  const int Bmax = cfg->max_batch;
+  if (gen_neg) {
+    tgnn_negs<<<grid_for(Bmax, 256), 256, 0, s>>>(c);
+    TGNX_LAUNCH_CHECK("tgnn_negs");
+  }
+  tgnn_assemble<true><<<1, 1024, assemble_smem(), s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_assemble");
+  tgnn_collapse<<<256, 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_collapse");
+  rc = launch_attn_fwd<true>(c, 3 * Bmax, s);
+  if (rc) return rc;
+  tgnn_pred_train<<<grid_for(Bmax, 4), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_pred_train");
+  tgnn_pred_reduce<<<grid_for(2 * (int64_t)c.D * c.D + 3 * c.D + 2, 256), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_pred_reduce");
+  rc = launch_attn_bwd(c, s);
+  if (rc) return rc;
+  tgnn_grad_reduce<<<grid_for(c.PL.total, 256), 256, 0, s>>>(c, GBWD);
+  TGNX_LAUNCH_CHECK("tgnn_grad_reduce");
+  tgnn_grad_expand<<<grid_for(c.L.Ws, 256), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_grad_expand");
+  return TGNX_OK;
+}
+
+int tgnx_tgnn_train_update(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, void* stream) {
+  Ctx c;
+  int rc = make_ctx(cfg, buf, 1, c);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(buf->grads && buf->adam_m && buf->adam_v, "tgnx_tgnn_train_update: null optimizer buffer");
+  hipStream_t s = as_stream(stream);
+  tgnn_adam<<<grid_for(c.L.total, 256), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_adam");
+  tgnn_finish<true><<<1, 1024, ring_insert_smem_bytes(cfg->max_batch), s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_finish");
+  return TGNX_OK;
+}
+
+int tgnx_tgnn_eval_step(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t Kn, int32_t tile_quirk,
+                        void* stream) {
+  Ctx c;
+  TGNX_CHECK_ARG(Kn >= 1 && Kn <= cfg->max_neg, "tgnx_tgnn_eval_step: Kn must be in [1, max_neg]");
+  int rc = make_ctx(cfg, buf, Kn, c);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(buf->neg && buf->out_pos && buf->out_neg && buf->mrr && buf->feat && buf->ev_msg && buf->memory,
+                 "tgnx_tgnn_eval_step: null buffer");
+  c.quirk = tile_quirk ? 1 : 0;
+  c.drop = 0;
+  hipStream_t s = as_stream(stream);
+  const int Bmax = cfg->max_batch;
+  tgnn_assemble<false><<<1, 1024, assemble_smem(), s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_assemble");
+  tgnn_collapse<<<256, 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_collapse");
+  rc = launch_attn_fwd<false>(c, (int64_t)Bmax * (2 + Kn), s);
+  if (rc) return rc;
+  tgnn_pred_eval_src<<<grid_for(Bmax, 4), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_pred_eval_src");
+  tgnn_pred_eval_neg<<<grid_for((int64_t)Bmax * Kn, 4), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_pred_eval_neg");
+  tgnn_mrr<<<1, 1024, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_mrr");
+  tgnn_ta_fill<<<grid_for(cfg->num_nodes, 256) < 4096 ? grid_for(cfg->num_nodes, 256) : 4096, 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_ta_fill");
+  tgnn_finish<false><<<1, 1024, ring_insert_smem_bytes(cfg->max_batch), s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_finish");
+  return TGNX_OK;
+}
+
+}  // extern "C"

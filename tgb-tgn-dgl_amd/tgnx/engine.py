@@ -1,0 +1,157 @@
+"""Host orchestration of the fused TGNN step (one process per GPU).
+
+A train step (epoch_utils.py:186-315) is two C-ABI calls on the current HIP stream:
+  tgnx_tgnn_train_fwd_bwd  negatives, assembly, forward, predictor + BCE, backward -> flat grads
+  [torch.distributed.all_reduce(grads) when world_size > 1 — RCCL over xGMI]
+  tgnx_tgnn_train_update   Adam, ring insert of the whole (global) batch, time_assoc
+An eval step (epoch_utils.py:28-157) is one call (tgnx_tgnn_eval_step).  Batch
+geometry lives in a device control block, so steps never synchronise the host
+and a sequence of them can be captured in a HIP graph (tgnx.graph).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .model import TGNN, FusedAdam, TgnnConfig
+
+CTL = dict(BATCH_START=0, CUR_EID=1, B=2, GEN=3, ADAM_T=4, S=5, E=6, LO=7, HI=8, SEED=9, NB=10, ERR=11, LOSS=12)
+
+P = ctypes.c_void_p
+
+
+class TgnnBuffers(ctypes.Structure):
+    _fields_ = [("ev_src", P), ("ev_dst", P), ("ev_t", P), ("ev_blk", P), ("ev_msg", P), ("neg", P),
+                ("dst_nodes", P), ("n_dst", ctypes.c_int64), ("feat", P), ("nbr", P), ("eid", P), ("rt", P),
+                ("assoc", P), ("time_assoc", P), ("memory", P), ("params", P), ("grads", P), ("adam_m", P),
+                ("adam_v", P), ("ctl", P), ("out_pos", P), ("out_neg", P), ("mrr", P), ("ws", P), ("node_map", P)]
+
+
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+class TgnnEngine:
+    """Owns the device workspace of one model + one neighbour ring."""
+
+    def __init__(self, model: TGNN, loader, feat: torch.Tensor, optimizer: FusedAdam | None,
+                 dst_nodes: torch.Tensor | None = None, max_neg: int | None = None, seed: int = 0,
+                 rank: int = 0, world: int = 1):
+        self.model, self.loader, self.opt = model, loader, optimizer
+        self.dev = model.device
+        cfg = model.cfg
+        if max_neg is not None and max_neg > cfg.max_neg:
+            cfg.max_neg = int(max_neg)
+        if cfg.ring != loader.size:
+            cfg.ring = loader.size
+        self.cfg = cfg
+        self.feat = feat.to(self.dev, torch.float32).contiguous()
+        nb = _lib.lib().tgnx_tgnn_ws_bytes(ctypes.byref(cfg))
+        if nb == 0:
+            raise RuntimeError(f"tgnx_tgnn_ws_bytes: invalid config: {_lib.lib().tgnx_last_error().decode()}")
+        self.ws = torch.zeros(nb, dtype=torch.uint8, device=self.dev)
+        self.node_map = torch.zeros(4 * cfg.num_nodes, dtype=torch.int32, device=self.dev)
+        self.ctl = torch.zeros(16, dtype=torch.int64, device=self.dev)
+        cap = cfg.max_batch * max(cfg.max_neg, 1)
+        self.out_pos = torch.zeros(cfg.max_batch, dtype=torch.float32, device=self.dev)
+        self.out_neg = torch.zeros(cap, dtype=torch.float32, device=self.dev)
+        self.mrr = torch.zeros(1 << 16, dtype=torch.float64, device=self.dev)
+        self.dst_nodes = None if dst_nodes is None else dst_nodes.to(self.dev, torch.long).contiguous()
+        self.seed, self.rank, self.world = int(seed), int(rank), int(world)
+        if optimizer is None:
+            self.adam_m = torch.zeros_like(model.flat)
+            self.adam_v = torch.zeros_like(model.flat)
+        else:
+            self.adam_m, self.adam_v = optimizer.exp_avg, optimizer.exp_avg_sq
+        self._neg_scratch = None
+
+    # ------------------------------------------------------------------ plumbing
+    def _buffers(self, src, dst, t, blk, msg, neg) -> TgnnBuffers:
+        m, ld = self.model, self.loader
+        b = TgnnBuffers()
+        b.ev_src, b.ev_dst, b.ev_t, b.ev_blk, b.ev_msg = _p(src), _p(dst), _p(t), _p(blk), _p(msg)
+        b.neg = neg if isinstance(neg, int) else _p(neg)
+        b.dst_nodes = _p(self.dst_nodes)
+        b.n_dst = 0 if self.dst_nodes is None else self.dst_nodes.numel()
+        b.feat = _p(self.feat)
+        b.nbr, b.eid, b.rt, b.assoc = _p(ld.neighbors), _p(ld.e_id), _p(ld.t), _p(ld._assoc)
+        b.time_assoc, b.memory = _p(m.time_assoc), _p(m.memory.memory)
+        b.params, b.grads, b.adam_m, b.adam_v = _p(m.flat), _p(m.grad_flat), _p(self.adam_m), _p(self.adam_v)
+        b.ctl, b.out_pos, b.out_neg, b.mrr = _p(self.ctl), _p(self.out_pos), _p(self.out_neg), _p(self.mrr)
+        b.ws, b.node_map = _p(self.ws), _p(self.node_map)
+        return b
+
+    def _stream(self):
+        return _lib.stream(self.dev)
+
+    def advance(self, mode, batch_start=0, B=0, cur_e_id=0, split_lo=0, split_hi=0, batch=1, train=True):
+        _lib.call("tgnx_tgnn_advance", _p(self.ctl), mode, batch_start, B, cur_e_id, split_lo, split_hi, batch,
+                  self.rank, self.world, self.seed, 1 if train else 0, self._stream())
+
+    def _allreduce_grads(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.model.grad_flat)
+
+    # ------------------------------------------------------------------ explicit (per-batch tensors)
+    @staticmethod
+    def _dev_batch(dev, src, dst, t, msg, blk):
+        f = lambda x, dt: torch.as_tensor(x).to(dev, dt, non_blocking=True).contiguous()  # noqa: E731
+        return f(src, torch.long), f(dst, torch.long), f(t, torch.float32), f(msg, torch.float32), f(blk, torch.long)
+
+    def train_batch(self, src, dst, t, msg, blk, neg=None, dropout=True):
+        """One train iteration on an explicit batch (epoch_utils.py:194-304)."""
+        dev = self.dev
+        src, dst, t, msg, blk = self._dev_batch(dev, src, dst, t, msg, blk)
+        B = int(src.numel())
+        gen_neg = neg is None
+        if gen_neg:
+            neg = torch.empty(B, dtype=torch.long, device=dev)
+        else:
+            neg = torch.as_tensor(neg).to(dev, torch.long).reshape(-1).contiguous()
+        self.advance(0, 0, B, self.loader.cur_e_id, train=True)
+        buf = self._buffers(src, dst, t, blk, msg, neg)
+        _lib.call("tgnx_tgnn_train_fwd_bwd", ctypes.byref(self.cfg), ctypes.byref(buf), 1 if gen_neg else 0,
+                  1 if (dropout and self.model.training) else 0, self._stream())
+        self._allreduce_grads()
+        _lib.call("tgnx_tgnn_train_update", ctypes.byref(self.cfg), ctypes.byref(buf), self._stream())
+        self.loader.cur_e_id += B
+        self._keep = (src, dst, t, msg, blk, neg)   # keep alive until the stream consumes them
+        return self.out_pos[:B], self.out_neg[:B], neg
+
+    def eval_batch(self, src, dst, t, msg, blk, neg2d, tile_quirk=True):
+        """One eval iteration (epoch_utils.py:28-157); returns (pos[B], neg[B,K'], mrr) in block order."""
+        dev = self.dev
+        src, dst, t, msg, blk = self._dev_batch(dev, src, dst, t, msg, blk)
+        neg2d = torch.as_tensor(neg2d).to(dev, torch.long).contiguous()
+        B, Kn = neg2d.shape
+        if Kn > self.cfg.max_neg:
+            raise RuntimeError(f"eval_batch: {Kn} negatives per event > max_neg={self.cfg.max_neg}")
+        self.advance(0, 0, B, self.loader.cur_e_id, train=False)
+        buf = self._buffers(src, dst, t, blk, msg, neg2d)
+        _lib.call("tgnx_tgnn_eval_step", ctypes.byref(self.cfg), ctypes.byref(buf), Kn, 1 if tile_quirk else 0,
+                  self._stream())
+        self.loader.cur_e_id += B
+        self._keep = (src, dst, t, msg, blk, neg2d)
+        nb = int(self.ctl[CTL["NB"]])
+        return self.out_pos[:B], self.out_neg[:B * Kn].view(B, Kn), self.mrr[(nb - 1) & 0xFFFF]
+
+    # ------------------------------------------------------------------ status
+    def check(self):
+        err = int(self.ctl[CTL["ERR"]])
+        if err:
+            raise RuntimeError(f"tgnx TGNN step reported device error flags {err:#x} "
+                               "(1: batch above capacity, 2: edge capacity exceeded)")
+
+    def loss_sum(self) -> float:
+        return float(self.ctl.view(torch.float64)[CTL["LOSS"]])
+
+    def reset_loss(self):
+        self.ctl.view(torch.float64)[CTL["LOSS"]] = 0.0
+
+    def reset_counters(self):
+        self.ctl[CTL["NB"]] = 0
