@@ -1,0 +1,234 @@
+"""Benchmark: temporal edges/s of the fused TGN(N) train step on tgbl-wiki-shaped batches.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step is one train batch of the running reference path (epoch_utils.py:186-315):
+negatives, sampler read, all dependency blocks of the batch (model_utils.py:68-157),
+predictor + BCE, backward, Adam, neighbour-ring insert.  Synthetic wiki-shaped stream
+(TGB data is not downloadable here), events resident in HBM.
+Data-parallel: the global batch is B·N events, every rank replays the ring/time state of the
+whole batch and computes its 1/N of the rows; gradients are all-reduced over RCCL (weak scaling).
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tgb-tgn-dgl_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_EDGE = None   # set from the config: SURVEY.md §8(d) per sampled edge 20 + 4d + 4D + 4
+BYTES_PER_ROOT = None   # per root 4D + 4
+
+
+def block_ids(src, dst, batch):
+    from tgnx import _lib
+    out = np.empty_like(src)
+    _lib.call("tgnx_block_ids_host", src.ctypes.data, dst.ctypes.data, src.shape[0], batch, out.ctypes.data)
+    return out
+
+
+def cpu_baseline(stream, B, budget_s=15.0, max_batches=40):
+    """Oracle (faithful per-block CPU restatement, the 'port') on the same stream, bounded sample."""
+    sys.path.insert(0, ROOT)
+    from oracle import blocks_ref
+    from oracle.epoch_ref import train_batch
+    from oracle.sampler_ref import RefLastNeighborLoader
+    from oracle.tgnn_ref import RefTGNN
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+    torch.set_num_threads(cores)
+    N, d = stream.shape.num_nodes, stream.shape.msg_dim
+    torch.manual_seed(0)
+    model = RefTGNN(d, 100, N)            # dropout as the reference's first epoch (0.6 / 0.6)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    loader = RefLastNeighborLoader(N, 10)
+    feats = torch.from_numpy(stream.msg)
+    rng = np.random.default_rng(0)
+    n = 0
+    t_total = 0.0
+    while n < max_batches and t_total < budget_s:
+        sl = slice(n * B, (n + 1) * B)
+        src, dst = stream.src[sl], stream.dst[sl]
+        blk = blocks_ref.block_ids(src, dst, B)
+        neg = rng.choice(stream.dst_nodes, size=src.shape[0])
+        args = [torch.from_numpy(x) for x in (src, dst, neg, stream.t[sl].astype(np.float32), stream.msg[sl], blk)]
+        t0 = time.perf_counter()
+        train_batch(model, opt, loader, feats, args[0], args[1], args[2], args[3], args[4], args[5])
+        dt = time.perf_counter() - t0
+        if n > 0:                         # first batch (empty ring, allocator warm-up) excluded
+            t_total += dt
+        n += 1
+    timed = max(n - 1, 1)
+    return {"value": round(timed * B / max(t_total, 1e-9), 2), "unit": "events/s", "cores": cores, "kind": "port",
+            "sample": f"oracle per-block restatement (oracle/epoch_ref.py), train batches 2..{n} of the same "
+                      f"wiki-shaped stream, B={B}, K=10, dropout 0.6 (reference epoch 1), torch CPU threads={cores}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--batch", type=int, default=200, help="events per GPU per step")
+    ap.add_argument("--dataset", default="tgbl-wiki")
+    ap.add_argument("--no-dropout", action="store_true", help="train mode without dropout (reference epochs >= 2)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe-steps", type=int, default=100)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from tgnx import _lib
+    from tgnx.engine import TgnnEngine
+    from tgnx.model import TGNN, getOptimizer
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.synth import SHAPES, make_stream
+
+    shape = SHAPES[args.dataset]
+    stream = make_stream(shape, seed=0)
+    N, d, D, K = shape.num_nodes, shape.msg_dim, 100, 10
+    Bg = args.batch * world
+    blk = block_ids(stream.src, stream.dst, Bg)
+    ev = dict(src=torch.from_numpy(stream.src).to(dev), dst=torch.from_numpy(stream.dst).to(dev),
+              t=torch.from_numpy(stream.t.astype(np.float32)).to(dev), blk=torch.from_numpy(blk).to(dev),
+              msg=torch.from_numpy(stream.msg).to(dev))
+    g = torch.Generator().manual_seed(0)
+    model = TGNN(d, D, N, dev, ring=K, max_batch=Bg, max_neg=1, generator=g)
+    opt = getOptimizer({"gnn": model}, 1e-4)
+    loader = LastNeighborLoader(N, K, device=dev)
+    dst_nodes = torch.from_numpy(np.unique(stream.dst))
+    eng = TgnnEngine(model, loader, ev["msg"], opt, dst_nodes=dst_nodes, seed=1234, rank=rank, world=world)
+    neg_buf = torch.zeros(stream.num_events, dtype=torch.long, device=dev)
+    eng.bind_resident(ev["src"], ev["dst"], ev["t"], ev["blk"], ev["msg"], neg_buf, 0, stream.train_end, Bg,
+                      dropout=not args.no_dropout)
+    nb_epoch = math.ceil(stream.train_end / Bg)
+    counter = {"i": 0}
+
+    def step():
+        if counter["i"] % nb_epoch == 0:
+            eng.begin_epoch()
+        eng.resident_train_step()
+        counter["i"] += 1
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    e0, s0 = eng.units()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    e1, s1 = eng.units()
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    eng.check()
+    loss = eng.loss_sum()
+    assert math.isfinite(loss), "non-finite loss"
+
+    # live kernel timing (HIP events on the launch stream) for the roofline, same workload
+    bytes_edge = 20 + 4 * d + 4 * D + 4
+    bytes_root = 4 * D + 4
+    probes = {}
+    for name, kid in (("tgnn_attn_fwd", 1), ("tgnn_attn_bwd", 2)):
+        _lib.call("tgnx_probe_enable", kid)
+        pe0, ps0 = eng.units()
+        for _ in range(args.probe_steps):
+            step()
+        barrier()
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        _lib.call("tgnx_probe_read", ctypes.byref(ms), ctypes.byref(n))
+        _lib.call("tgnx_probe_enable", 0)
+        pe1, ps1 = eng.units()
+        launches = max(int(n.value), 1)
+        avg_ms = ms.value / launches
+        # units per launch: edges/segments this rank's launch processed (rows are sliced per rank)
+        edges = (pe1 - pe0) / launches / world
+        roots = (ps1 - ps0) / launches
+        algo = edges * bytes_edge + roots * bytes_root
+        probes[name] = dict(avg_us=avg_ms * 1e3, launches=launches, edges=edges, roots=roots, bytes=algo,
+                            gbs=algo / (avg_ms * 1e-3) / 1e9)
+    dom = max(probes, key=lambda k: probes[k]["avg_us"])
+    pd = probes[dom]
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(dom, {}).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(stream, args.batch)
+
+    if rank == 0:
+        out = {
+            "metric": "temporal edges/sec on tgbl-wiki TGN (train step)",
+            "value": round(args.steps * Bg / elapsed, 1),
+            "unit": "events/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic tgbl-wiki-shaped stream (SURVEY.md §8d), events resident in HBM",
+            "config": {"workload": f"{args.dataset} TGNN (running reference path: DGL EdgeGATConv block loop), "
+                                   f"batch {args.batch}/GPU, {K} temporal neighbours, H=8, D=100, d={d}, "
+                                   f"dropout {'off' if args.no_dropout else '0.6 (epoch-1)'}",
+                       "global_batch": Bg, "parallelism": f"dp{world}",
+                       "edges_per_step": round((e1 - e0) / args.steps / world, 1),
+                       "blocks_per_batch_mean": float(np.mean([blk[i:i + Bg].max() + 1
+                                                               for i in range(0, stream.train_end, Bg)]))},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(pd["gbs"], 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(pd["gbs"] / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "avg_launch_us": round(pd["avg_us"], 3),
+                         "algo_bytes_per_launch": round(pd["bytes"]),
+                         "bytes_model": f"SURVEY §8(d): {bytes_edge} B/edge (ring entry 20 + feature 4d + "
+                                        f"neighbour memory 4D + time 4) x edges + {bytes_root} B/root x roots"},
+            "kernels_us": {k: round(v["avg_us"], 3) for k, v in probes.items()},
+            "cpu_baseline": cpu,
+            "loss_sum": round(loss, 4),
+        }
+        print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -82,6 +82,22 @@ int tgnx_neg_sample(const int64_t* dst_nodes, int64_t n_dst, const int64_t* pos,
 int tgnx_block_ids_host(const int64_t* src, const int64_t* dst, int64_t num_events, int64_t batch,
                         int64_t* out);
 
+/* ------------------------------------------------------------------------
+ * Kernel probe (measurement only): while enabled, every launch of kernel
+ * `kernel_id` (TGNX_K_*) is bracketed by a pair of hipEvents recorded on the
+ * launch stream; tgnx_probe_read waits for them and returns the summed
+ * duration (ms) and the launch count, then clears.  Off by default.
+ * ------------------------------------------------------------------------ */
+#define TGNX_K_ATTN_FWD 1
+#define TGNX_K_ATTN_BWD 2
+#define TGNX_K_ASSEMBLE 3
+#define TGNX_K_PRED 4
+#define TGNX_K_FINISH 5
+#define TGNX_K_ATTN_FWD_EVAL 6
+#define TGNX_K_ADAM 7
+int tgnx_probe_enable(int32_t kernel_id);
+int tgnx_probe_read(double* total_ms, int64_t* launches);
+
 
 /* ------------------------------------------------------------------------
  * TGNN step — the running reference model (model_utils.py:14-237, 422-697) and
@@ -115,6 +131,8 @@ int tgnx_block_ids_host(const int64_t* src, const int64_t* dst, int64_t num_even
 #define TGNX_CTL_NB 10          /* batches advanced since the last reset */
 #define TGNX_CTL_ERR 11         /* device-side error flags (0 = ok) */
 #define TGNX_CTL_LOSS 12        /* (double) running sum of loss * B (epoch_utils.py:310) */
+#define TGNX_CTL_SUM_E 13       /* running sum of assembled edges (roofline units) */
+#define TGNX_CTL_SUM_S 14       /* running sum of assembled segments */
 #define TGNX_CTL_WORDS 16
 
 #define TGNX_TGNN_NPARAM 15     /* te_w te_b attn_l attn_r attn_e Wn bn We be Ws bs Wd bd Wo bo */

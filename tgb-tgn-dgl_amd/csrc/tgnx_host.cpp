@@ -8,6 +8,8 @@
 #include <algorithm>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/tgnx.h"
 
 namespace tgnx {
@@ -21,7 +23,58 @@ void set_error(const char* fmt, ...) {
 }
 }  // namespace tgnx
 
+namespace tgnx {
+// ------------------------------------------------------------------ kernel probe
+struct Probe {
+  int id = 0;
+  std::vector<hipEvent_t> ev;  // start/stop pairs
+  size_t used = 0;
+};
+static Probe g_probe;
+
+void probe_begin(int id, hipStream_t s) {
+  if (g_probe.id != id) return;
+  if (g_probe.used + 2 > g_probe.ev.size()) {
+    size_t n = g_probe.ev.size() ? g_probe.ev.size() * 2 : 512;
+    while (g_probe.ev.size() < n) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return;
+      g_probe.ev.push_back(e);
+    }
+  }
+  (void)hipEventRecord(g_probe.ev[g_probe.used], s);
+}
+void probe_end(int id, hipStream_t s) {
+  if (g_probe.id != id || g_probe.used + 2 > g_probe.ev.size()) return;
+  (void)hipEventRecord(g_probe.ev[g_probe.used + 1], s);
+  g_probe.used += 2;
+}
+}  // namespace tgnx
+
 extern "C" {
+
+int tgnx_probe_enable(int32_t kernel_id) {
+  tgnx::g_probe.id = kernel_id;
+  tgnx::g_probe.used = 0;
+  return TGNX_OK;
+}
+
+int tgnx_probe_read(double* total_ms, int64_t* launches) {
+  double ms = 0.0;
+  for (size_t i = 0; i + 1 < tgnx::g_probe.used; i += 2) {
+    if (hipEventSynchronize(tgnx::g_probe.ev[i + 1]) != hipSuccess) {
+      tgnx::set_error("tgnx_probe_read: event sync failed");
+      return TGNX_EHIP;
+    }
+    float f = 0.f;
+    (void)hipEventElapsedTime(&f, tgnx::g_probe.ev[i], tgnx::g_probe.ev[i + 1]);
+    ms += f;
+  }
+  if (total_ms) *total_ms = ms;
+  if (launches) *launches = (int64_t)(tgnx::g_probe.used / 2);
+  tgnx::g_probe.used = 0;
+  return TGNX_OK;
+}
 
 int tgnx_version(void) { return 1; }
 

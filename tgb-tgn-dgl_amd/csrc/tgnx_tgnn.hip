@@ -18,11 +18,15 @@
 
 namespace tgnx {
 
+void probe_begin(int id, hipStream_t s);
+void probe_end(int id, hipStream_t s);
+
 constexpr int H = 8;          // gnn.att_head
 constexpr int DMAX = 128;     // gnn.dim_out (memory/time/embedding dim) capacity
 constexpr int FMAX = 320;     // d + D capacity
 constexpr int TOUCH_MAX = 8192;
-constexpr int GBWD = 64;      // workgroups of the backward kernel (= partial slabs)
+constexpr int GBWD = 128;     // workgroups of the edge backward kernel (= partial slabs)
+constexpr int GSEG = 64;      // workgroups of the segment backward kernel
 constexpr int MRR_SLOTS = 65536;  // per-batch MRR ring in buffers.mrr
 
 // ------------------------------------------------------------------ layouts
@@ -92,6 +96,15 @@ __host__ __device__ inline PLay make_play(int D, int d) {
   return P;
 }
 
+// per-edge descriptor written by tgnn_edge_meta (32 B)
+struct __attribute__((aligned(16))) EdgeMeta {
+  int64_t u;     // source node
+  int64_t frow;  // >= 0: feature-table row (ring e_id); -1: self loop (ones); <= -2: -(event row) - 2
+  float dt;      // edge time - time_assoc[u] as of the segment's block
+  int seg, o, blk;
+  int64_t root;
+};
+
 // ------------------------------------------------------------------ context
 struct Ctx {
   int64_t N;
@@ -118,22 +131,27 @@ struct Ctx {
   int4* nodemap;
   // workspace
   uint64_t* touches;
+  int* sp_pref;
+  uint64_t* sp_keys;
+  int* seg_cnt;
   int* seg_eoff;
-  int* seg_nintra;
   float* seg_out;
   float* seg_stats;
   float* seg_g;
   float* X;
+  float* DX;
+  struct EdgeMeta* meta;
   float* U;
   float* evs;
   float* slabs;
+  float* slabs_s;
   float* red;
   float* blkmax;
   int* blk_rank;
   int* blk_order;
   float* HS;
   int64_t Ecap;
-  int Bmax;
+  int Bmax, Ge, Gs;
   Lay L;
   ULay UL;
   PLay PL;
@@ -274,6 +292,9 @@ __global__ void tgnn_collapse(Ctx c) {
 }
 
 // ------------------------------------------------------------------ assembly (one workgroup)
+// Sorts the batch's node touches (src / dst / neg rows) by (node, block, kind, event), builds the
+// node map {gen, run start, run length, first s/p index}, the compacted s/p touch list (the
+// intra-batch edges of model_utils.py:151-152 in block order), per-block max t and block order.
 template <bool TRAIN>
 __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -310,120 +331,67 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   }
   __syncthreads();
   bitonic_sort_u64(key, n);
-  for (int p = tid; p < NT; p += T) c.touches[p] = key[p];
-  // runs
-  int pc = (NT + T - 1) / T;
-  int p0 = tid * pc, p1 = min(NT, p0 + pc);
-  int cnt = 0;
-  for (int p = p0; p < p1; ++p) cnt += (p == 0 || knode(key[p]) != knode(key[p - 1]));
-  int U;
-  int rid = block_excl_scan(cnt, sh, &U);
-  for (int p = p0; p < p1; ++p)
-    if (p == 0 || knode(key[p]) != knode(key[p - 1])) run_start[rid++] = p;
-  __syncthreads();
-  for (int r = tid; r < U; r += T) {
-    const int a = run_start[r];
-    const int e = r + 1 < U ? run_start[r + 1] : NT;
-    const int64_t node = knode(key[a]);
-    c.nodemap[node] = make_int4(gen, a, e - a, 0);
-    if (TRAIN) {
-      int sp = 0, cur = -1, sp_at = 0;
-      for (int j = a; j < e; ++j) {
-        const uint64_t k = key[j];
-        const int b = kblk(k);
-        if (b != cur) {
-          cur = b;
-          sp_at = sp;
-        }
-        const int kind = kkind(k), ev = kev(k);
-        const int row = kind == 2 ? ev : kind == 1 ? B + ev : 2 * B + ev;
-        c.seg_nintra[row] = sp_at;
-        if (kind != 0) ++sp;
-      }
-    }
-  }
-  __syncthreads();
-  // block bookkeeping
+  const int pc = (NT + T - 1) / T;
+  const int p0 = tid * pc, p1 = min(NT, p0 + pc);
+  // compacted s/p list (kind != 0), exclusive prefix over the sorted touches
   {
-    float* bmax = c.blkmax;
-    for (int b = tid; b < B; b += T) bmax[b] = -INFINITY;
-    __syncthreads();
-    for (int e = tid; e < B; e += T) {
-      const int b = (int)blk[e];
-      atomicMax(&bmax[b], evt[e]);
-    }
-    __syncthreads();
-    // stable order by block: rank = #events in smaller blocks + #earlier events in same block
-    int* bc = run_start;
-    for (int b = tid; b < B; b += T) bc[b] = 0;
-    __syncthreads();
-    for (int e = tid; e < B; e += T) atomicAdd(&bc[(int)blk[e]], 1);
-    __syncthreads();
-    int chunk = (B + T - 1) / T;
-    int b0 = tid * chunk, b1 = min(B, b0 + chunk);
-    int s = 0;
-    for (int b = b0; b < b1; ++b) s += bc[b];
+    int cnt = 0;
+    for (int p = p0; p < p1; ++p) cnt += kkind(key[p]) != 0;
     int tot;
-    int base = block_excl_scan(s, sh, &tot);
-    for (int b = b0; b < b1; ++b) {
-      int v = bc[b];
-      bc[b] = base;
-      base += v;
+    int base = block_excl_scan(cnt, sh, &tot);
+    for (int p = p0; p < p1; ++p) {
+      c.touches[p] = key[p];
+      c.sp_pref[p] = base;
+      if (kkind(key[p]) != 0) c.sp_keys[base++] = key[p];
     }
+    if (tid == 0) c.sp_pref[NT] = tot;
+  }
+  // node runs -> node map
+  {
+    int cnt = 0;
+    for (int p = p0; p < p1; ++p) cnt += (p == 0 || knode(key[p]) != knode(key[p - 1]));
+    int U;
+    int rid = block_excl_scan(cnt, sh, &U);
+    for (int p = p0; p < p1; ++p)
+      if (p == 0 || knode(key[p]) != knode(key[p - 1])) run_start[rid++] = p;
     __syncthreads();
-    for (int e = tid; e < B; e += T) {
-      const int b = (int)blk[e];
-      int before = 0;
-      for (int j = 0; j < e; ++j) before += ((int)blk[j] == b);
-      const int rk = bc[b] + before;
-      c.blk_rank[e] = rk;
-      c.blk_order[rk] = e;
+    for (int r = tid; r < U; r += T) {
+      const int a = run_start[r];
+      const int e = r + 1 < U ? run_start[r + 1] : NT;
+      c.nodemap[knode(key[a])] = make_int4(gen, a, e - a, c.sp_pref[a]);
     }
   }
   __syncthreads();
-  if (TRAIN) {
-    // edge offsets for the saved per-edge logits: ring valid + self loop + intra
-    const int S = 3 * B;
-    int chunk = (S + T - 1) / T;
-    int r0 = tid * chunk, r1 = min(S, r0 + chunk);
-    int s = 0;
-    for (int r = r0; r < r1; ++r) {
-      const int e = r % B, which = r / B;
-      const int64_t node = which == 0 ? src[e] : which == 1 ? dst[e] : neg[e];
-      int nr = 0;
-      for (int j = 0; j < c.K; ++j) nr += (c.eid[node * c.K + j] >= 0);
-      const int v = nr + 1 + c.seg_nintra[r];
-      c.seg_eoff[r] = v;
-      s += v;
-    }
-    int tot;
-    int base = block_excl_scan(s, sh, &tot);
-    for (int r = r0; r < r1; ++r) {
-      const int v = c.seg_eoff[r];
-      c.seg_eoff[r] = base;
-      base += v;
-    }
-    if (tid == 0) {
-      c.seg_eoff[S] = tot;
-      c.ctl[TGNX_CTL_S] = S;
-      c.ctl[TGNX_CTL_E] = tot;
-      if (tot > c.Ecap) c.ctl[TGNX_CTL_ERR] |= 2;
-    }
-  } else if (tid == 0) {
-    c.ctl[TGNX_CTL_S] = (int64_t)B * (2 + c.Kn);
-    c.ctl[TGNX_CTL_E] = 0;
+  // per-block max t (eval's time_assoc[:] = max, model_utils.py:78) and stable block order
+  float* bmax = c.blkmax;
+  for (int b = tid; b < B; b += T) bmax[b] = -INFINITY;
+  __syncthreads();
+  for (int e = tid; e < B; e += T) atomicMax(&bmax[(int)blk[e]], evt[e]);
+  const int nb = next_pow2(B);
+  for (int p = tid; p < nb; p += T) key[p] = p < B ? (((uint64_t)blk[p] << 12) | (uint64_t)p) : ~0ull;
+  __syncthreads();
+  bitonic_sort_u64(key, nb);
+  for (int r = tid; r < B; r += T) {
+    const int e = (int)(key[r] & 4095u);
+    c.blk_rank[e] = r;
+    c.blk_order[r] = e;
+  }
+  if (tid == 0) {
+    const int nloc = (int)(c.ctl[TGNX_CTL_HI] - c.ctl[TGNX_CTL_LO]);
+    c.ctl[TGNX_CTL_S] = (int64_t)nloc * (2 + c.Kn);
   }
 }
 
 // ------------------------------------------------------------------ segment geometry
+// Segment w (this rank's rows): [0, nloc) src rows, [nloc, 2 nloc) dst rows, then neg rows.
 struct Seg {
-  int kind, i, cc, row, blk;
+  int kind, i, cc, blk;
   int64_t root;
 };
-__device__ __forceinline__ bool seg_of(const Ctx& c, int w, int B, int lo, int hi, Seg& s) {
+__device__ __forceinline__ bool seg_of(const Ctx& c, int w, int lo, int hi, int64_t start, Seg& s) {
   const int nloc = hi - lo;
   const int Kn = c.Kn;
-  if (w >= nloc * (2 + Kn)) return false;
+  if (w < 0 || w >= nloc * (2 + Kn)) return false;
   if (w < nloc) {
     s.kind = 2; s.i = lo + w; s.cc = 0;
   } else if (w < 2 * nloc) {
@@ -432,106 +400,192 @@ __device__ __forceinline__ bool seg_of(const Ctx& c, int w, int B, int lo, int h
     const int q = w - 2 * nloc;
     s.kind = 0; s.i = lo + q / Kn; s.cc = q % Kn;
   }
-  s.row = s.kind == 2 ? s.i : s.kind == 1 ? B + s.i : 2 * B + s.i * Kn + s.cc;
+  s.root = s.kind == 2 ? c.ev_src[start + s.i] : s.kind == 1 ? c.ev_dst[start + s.i]
+                                                             : c.neg[(start + s.i) * Kn + s.cc];
+  s.blk = (int)c.ev_blk[start + s.i];
   return true;
 }
 
-// Per-lane model registers shared by forward and backward.
-template <int NJ>
-struct LaneW {
-  float ue[NJ][H];
-  float tw[NJ], tb[NJ];
-  float ul[2][H];
-  __device__ __forceinline__ void load(const Ctx& c, int lane) {
-#pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) {
-      const int f = lane + 64 * jj;
-      const bool ok = f < c.F;
-#pragma unroll
-      for (int h = 0; h < H; ++h) ue[jj][h] = ok ? c.U[c.UL.Ue + h * c.F + f] : 0.f;
-      const bool enc = ok && f >= c.d;
-      tw[jj] = enc ? c.params[c.L.te_w + (f - c.d)] : 0.f;
-      tb[jj] = enc ? c.params[c.L.te_b + (f - c.d)] : 0.f;
+// in-edge count of every segment: ring row + self loop + intra-batch edges of earlier blocks
+__global__ void tgnn_seg_count(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int S = (int)c.ctl[TGNX_CTL_S];
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (B == 0 || w >= S || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int gen = (int)c.ctl[TGNX_CTL_GEN];
+  Seg s;
+  seg_of(c, w, (int)c.ctl[TGNX_CTL_LO], (int)c.ctl[TGNX_CTL_HI], start, s);
+  int nring = 0;
+  for (int j = 0; j < c.K; ++j) nring += c.eid[s.root * c.K + j] >= 0;
+  int nintra = 0;
+  const int4 inf = c.nodemap[s.root];
+  if (inf.x == gen) {
+    int lo = inf.w, hi = c.sp_pref[inf.y + inf.z];
+    const int base = lo;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (kblk(c.sp_keys[mid]) < s.blk) lo = mid + 1; else hi = mid;
     }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int dd = lane + 64 * q;
-#pragma unroll
-      for (int h = 0; h < H; ++h) ul[q][h] = dd < c.D ? c.U[c.UL.Ul + h * c.D + dd] : 0.f;
-    }
+    nintra = lo - base;
   }
-};
+  c.seg_cnt[w] = nring | (nintra << 8);
+}
 
-// Edge walker: ring row (newest first) → self loop → intra-batch edges of earlier blocks
-struct EdgeWalk {
-  int64_t my_nbr, my_eid;
-  float my_rt;
-  int nring, nintra, rp, re;
-  __device__ __forceinline__ void init(const Ctx& c, const Seg& s, int gen, int lane) {
-    my_nbr = -1; my_eid = -1; my_rt = 0.f;
-    if (lane < c.K) {
-      my_eid = c.eid[s.root * c.K + lane];
-      my_nbr = c.nbr[s.root * c.K + lane];
-      my_rt = c.rt[s.root * c.K + lane];
-    }
-    nring = __popcll(__ballot(lane < c.K && my_eid >= 0));
-    const int4 inf = c.nodemap[s.root];
-    rp = 0; re = 0; nintra = 0;
-    if (inf.x == gen) {
-      rp = inf.y; re = inf.y + inf.z;
-      for (int j = rp; j < re; ++j) {
-        const uint64_t k = c.touches[j];
-        if (kblk(k) >= s.blk) break;
-        nintra += (kkind(k) != 0);
-      }
-    }
-  }
-  __device__ __forceinline__ int count() const { return nring + 1 + nintra; }
-  // returns source node u, feature row (nullptr = self-loop ones), edge time
-  __device__ __forceinline__ void edge(const Ctx& c, const Seg& s, int o, const int64_t* src, const int64_t* dst,
-                                       const float* evt, const float* msg, int64_t& u, const float*& fp, float& bt) {
-    if (o < nring) {
-      u = __shfl(my_nbr, o);
-      const int64_t e = __shfl(my_eid, o);
-      bt = __shfl(my_rt, o);
-      fp = c.feat + e * c.d;
-    } else if (o == nring) {
-      u = s.root; bt = 0.f; fp = nullptr;
-    } else {
-      uint64_t k;
-      do { k = c.touches[rp++]; } while (kkind(k) == 0);
-      const int ev = kev(k);
-      u = kkind(k) == 2 ? dst[ev] : src[ev];
-      fp = msg + (int64_t)ev * c.d;
-      bt = evt[ev];
-    }
-  }
-};
-
-// ------------------------------------------------------------------ forward: one wave per segment
-template <int NJ, bool TRAIN>
-__global__ void __launch_bounds__(256) tgnn_attn_fwd(Ctx c) {
+// exclusive scan of the edge counts (one workgroup) -> edge offsets
+__global__ void __launch_bounds__(1024) tgnn_seg_scan(Ctx c) {
+  __shared__ int sh[20];
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int lane = threadIdx.x & 63;
-  Seg s;
-  if (!seg_of(c, blockIdx.x * 4 + (threadIdx.x >> 6), B, (int)c.ctl[TGNX_CTL_LO], (int)c.ctl[TGNX_CTL_HI], s)) return;
-  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
-  const int64_t* src = c.ev_src + start;
-  const int64_t* dst = c.ev_dst + start;
-  const float* evt = c.ev_t + start;
-  const float* msg = c.ev_msg + start * c.d;
-  const int64_t* neg = c.neg + start * c.Kn;
-  s.root = s.kind == 2 ? src[s.i] : s.kind == 1 ? dst[s.i] : neg[s.i * c.Kn + s.cc];
-  s.blk = (int)c.ev_blk[start + s.i];
-  const int gen = (int)c.ctl[TGNX_CTL_GEN];
-  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-  const bool drop = TRAIN && c.drop;
+  const int S = (int)c.ctl[TGNX_CTL_S];
+  const int T = blockDim.x;
+  const int chunk = (S + T - 1) / T;
+  const int r0 = threadIdx.x * chunk, r1 = min(S, r0 + chunk);
+  int s = 0;
+  for (int r = r0; r < r1; ++r) {
+    const int v = c.seg_cnt[r];
+    s += (v & 255) + 1 + (v >> 8);
+  }
+  int tot;
+  int base = block_excl_scan(s, sh, &tot);
+  for (int r = r0; r < r1; ++r) {
+    c.seg_eoff[r] = base;
+    const int v = c.seg_cnt[r];
+    base += (v & 255) + 1 + (v >> 8);
+  }
+  if (threadIdx.x == 0) {
+    c.seg_eoff[S] = tot;
+    c.ctl[TGNX_CTL_E] = tot;
+    c.ctl[TGNX_CTL_SUM_E] += tot;
+    c.ctl[TGNX_CTL_SUM_S] += S;
+    if (tot > c.Ecap) c.ctl[TGNX_CTL_ERR] |= 2;
+  }
+}
 
-  LaneW<NJ> W;
-  W.load(c, lane);
-  float cel[H], er[H];
-  float nfr[2];
+// one thread per edge: source node, feature row, dt = t_edge - time_assoc[src] as of the block
+template <bool TRAIN>
+__global__ void tgnn_edge_meta(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int S = (int)c.ctl[TGNX_CTL_S];
+  const int E = (int)c.ctl[TGNX_CTL_E];
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int lo_ev = (int)c.ctl[TGNX_CTL_LO], hi_ev = (int)c.ctl[TGNX_CTL_HI];
+  const int gen = (int)c.ctl[TGNX_CTL_GEN];
+  const float* evt = c.ev_t + start;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) {
+    int lo = 0, hi = S;  // last w with eoff[w] <= e
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (c.seg_eoff[mid] <= e) lo = mid; else hi = mid;
+    }
+    const int w = lo;
+    const int o = e - c.seg_eoff[w];
+    Seg s;
+    seg_of(c, w, lo_ev, hi_ev, start, s);
+    const int nring = c.seg_cnt[w] & 255;
+    EdgeMeta m;
+    float bt;
+    if (o < nring) {
+      const int64_t idx = s.root * c.K + o;
+      m.u = c.nbr[idx];
+      m.frow = c.eid[idx];
+      bt = c.rt[idx];
+    } else if (o == nring) {
+      m.u = s.root;
+      m.frow = -1;
+      bt = 0.f;
+    } else {
+      const uint64_t k = c.sp_keys[c.nodemap[s.root].w + (o - nring - 1)];
+      const int ev = kev(k);
+      m.u = kkind(k) == 2 ? c.ev_dst[start + ev] : c.ev_src[start + ev];
+      m.frow = -(start + ev) - 2;
+      bt = evt[ev];
+    }
+    m.dt = bt - ta_at<TRAIN>(c, m.u, s.blk, gen, evt);
+    m.seg = w;
+    m.o = o;
+    m.blk = s.blk;
+    m.root = s.root;
+    c.meta[e] = m;
+  }
+}
+
+__device__ __forceinline__ const float* feat_row(const Ctx& c, int64_t frow) {
+  return frow >= 0 ? c.feat + frow * c.d : frow == -1 ? nullptr : c.ev_msg + (-(frow + 2)) * c.d;
+}
+
+// x_eh = U_e[h]·efeat_e + U_l[h]·drop(mem[src]) + c : 16 lanes per edge, U staged in LDS [dim][head]
+__global__ void __launch_bounds__(256) tgnn_edge_fwd(Ctx c) {
+  __shared__ __attribute__((aligned(16))) float Us[(FMAX + DMAX) * H];
+  __shared__ float Tw[DMAX], Tb[DMAX];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int F = c.F, D = c.D, d = c.d, FD = c.F + c.D;
+  for (int x = threadIdx.x; x < FD * H; x += blockDim.x) {
+    const int f = x / H, h = x % H;
+    Us[x] = f < F ? c.U[c.UL.Ue + h * F + f] : c.U[c.UL.Ul + h * D + (f - F)];
+  }
+  for (int x = threadIdx.x; x < D; x += blockDim.x) {
+    Tw[x] = c.params[c.L.te_w + x];
+    Tb[x] = c.params[c.L.te_b + x];
+  }
+  __syncthreads();
+  float cst[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) cst[h] = c.U[c.UL.ce + h] + c.U[c.UL.cl + h];
+  const int E = (int)c.ctl[TGNX_CTL_E];
+  const bool drop = c.drop;
+  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+  const int sub = threadIdx.x & 15;
+  for (int e = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; e < E; e += (gridDim.x * blockDim.x) >> 4) {
+    const EdgeMeta m = c.meta[e];
+    const float* fp = feat_row(c, m.frow);
+    const float* mu = c.mem + m.u * D;
+    const uint64_t sk = seg_key(m.blk, m.root);
+    float acc[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) acc[h] = 0.f;
+    for (int f = sub; f < FD; f += 16) {
+      float v;
+      if (f < d) v = fp ? fp[f] : 1.0f;
+      else if (f < F) v = cosf(fmaf(Tw[f - d], m.dt, Tb[f - d]));
+      else v = mu[f - F];
+      if (drop) {
+        v *= f < F ? keepf(hash4(seed, 2, sk, ((uint64_t)m.o << 16) | (uint64_t)f), c.pf, c.inv_kf)
+                   : node_keep(c, seed, m.blk, m.u, f - F);
+      }
+      const float4 u0 = *reinterpret_cast<const float4*>(&Us[f * H]);
+      const float4 u1 = *reinterpret_cast<const float4*>(&Us[f * H + 4]);
+      acc[0] += u0.x * v; acc[1] += u0.y * v; acc[2] += u0.z * v; acc[3] += u0.w * v;
+      acc[4] += u1.x * v; acc[5] += u1.y * v; acc[6] += u1.z * v; acc[7] += u1.w * v;
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      float v = acc[h];
+      v += __shfl_xor(v, 8, 16);
+      v += __shfl_xor(v, 4, 16);
+      v += __shfl_xor(v, 2, 16);
+      v += __shfl_xor(v, 1, 16);
+      acc[h] = v + cst[h];
+    }
+    if (sub == 0) {
+      float4* xp = reinterpret_cast<float4*>(c.X + (int64_t)e * H);
+      xp[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      xp[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+  }
+}
+
+__device__ __forceinline__ void load_x8(const float* p, float (&x)[H]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0];
+  const float4 b = reinterpret_cast<const float4*>(p)[1];
+  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+}
+
+// er_h of a segment's root (model_utils.py:588): lanes over the memory dims
+__device__ __forceinline__ void root_er(const Ctx& c, const Seg& s, uint64_t seed, bool drop, int lane,
+                                       float (&er)[H], float (&nfr)[2]) {
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int dd = lane + 64 * q;
@@ -548,70 +602,53 @@ __global__ void __launch_bounds__(256) tgnn_attn_fwd(Ctx c) {
       if (dd < c.D) p += c.U[c.UL.Ur + h * c.D + dd] * nfr[q];
     }
     er[h] = wave_sum(p) + c.U[c.UL.cr + h];
-    cel[h] = c.U[c.UL.ce + h] + c.U[c.UL.cl + h];
   }
-  EdgeWalk ew;
-  ew.init(c, s, gen, lane);
-  const int E = ew.count();
-  int eoff = 0;
-  if (TRAIN) {
-    eoff = c.seg_eoff[s.row];
-    if (eoff + E > c.Ecap) return;
-  }
+}
+
+// per segment: LeakyReLU, edge softmax per head (model_utils.py:595-597), ft = Σ a·x, head mean
+template <bool TRAIN>
+__global__ void __launch_bounds__(256) tgnn_seg_fwd(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int S = (int)c.ctl[TGNX_CTL_S];
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= S) return;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  Seg s;
+  seg_of(c, w, (int)c.ctl[TGNX_CTL_LO], (int)c.ctl[TGNX_CTL_HI], start, s);
+  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+  const bool drop = TRAIN && c.drop;
+  float er[H], nfr[2];
+  root_er(c, s, seed, drop, lane, er, nfr);
+  const int e0 = c.seg_eoff[w], ne = c.seg_eoff[w + 1] - e0;
   const uint64_t sk = seg_key(s.blk, s.root);
   float m[H], l[H], acc[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) {
     m[h] = -INFINITY; l[h] = 0.f; acc[h] = 0.f;
   }
-  for (int o = 0; o < E; ++o) {
-    int64_t u;
-    const float* fp;
-    float bt;
-    ew.edge(c, s, o, src, dst, evt, msg, u, fp, bt);
-    const float dt = bt - ta_at<TRAIN>(c, u, s.blk, gen, evt);
-    float part[H];
-#pragma unroll
-    for (int h = 0; h < H; ++h) part[h] = 0.f;
-#pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) {
-      const int f = lane + 64 * jj;
-      if (f < c.F) {
-        float v;
-        if (f < c.d) v = fp ? fp[f] : 1.0f;
-        else v = cosf(fmaf(W.tw[jj], dt, W.tb[jj]));
-        if (drop) v *= keepf(hash4(seed, 2, sk, ((uint64_t)o << 16) | (uint64_t)f), c.pf, c.inv_kf);
-#pragma unroll
-        for (int h = 0; h < H; ++h) part[h] += W.ue[jj][h] * v;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int dd = lane + 64 * q;
-      if (dd < c.D) {
-        float v = c.mem[u * c.D + dd];
-        if (drop) v *= node_keep(c, seed, s.blk, u, dd);
-#pragma unroll
-        for (int h = 0; h < H; ++h) part[h] += W.ul[q][h] * v;
-      }
-    }
-    float xs = 0.f;
+  for (int base = 0; base < ne; base += 64) {
+    const int o = base + lane;
+    const bool ok = o < ne;
+    float x[H];
+    if (ok) load_x8(c.X + (int64_t)(e0 + o) * H, x);
 #pragma unroll
     for (int h = 0; h < H; ++h) {
-      const float x = wave_sum(part[h]) + cel[h];
-      float sc = x + er[h];
-      sc = sc > 0.f ? sc : 0.2f * sc;
-      const float mn = fmaxf(m[h], sc);
+      float sc = -INFINITY;
+      if (ok) {
+        sc = x[h] + er[h];
+        sc = sc > 0.f ? sc : 0.2f * sc;
+      }
+      const float mn = fmaxf(m[h], wave_max(sc));
+      const float ex = ok ? expf(sc - mn) : 0.f;
+      float wgt = ex;
+      if (drop && ok) wgt *= keepf(hash4(seed, 3, sk, ((uint64_t)o << 16) | (uint64_t)h), c.pa, c.inv_ka);
       const float r = expf(m[h] - mn);
-      const float e = expf(sc - mn);
-      float wgt = e;
-      if (drop) wgt *= keepf(hash4(seed, 3, sk, ((uint64_t)o << 16) | (uint64_t)h), c.pa, c.inv_ka);
-      l[h] = l[h] * r + e;
-      acc[h] = acc[h] * r + wgt * x;
+      l[h] = l[h] * r + wave_sum(ex);
+      acc[h] = acc[h] * r + wave_sum(ok ? wgt * x[h] : 0.f);
       m[h] = mn;
-      if (lane == h) xs = x;
     }
-    if (TRAIN && lane < H) c.X[(int64_t)(eoff + o) * H + lane] = xs;
   }
   float out = 0.f;
   float st[4] = {0.f, 0.f, 0.f, 0.f};
@@ -623,13 +660,215 @@ __global__ void __launch_bounds__(256) tgnn_attn_fwd(Ctx c) {
       st[0] = m[h]; st[1] = l[h]; st[2] = ft; st[3] = er[h];
     }
   }
-  out *= (1.0f / H);
-  if (lane == 0) c.seg_out[s.row] = out;
+  if (lane == 0) c.seg_out[w] = out * (1.0f / H);
   if (TRAIN && lane < H) {
-    float* sp = c.seg_stats + (int64_t)s.row * 4 * H;
+    float* sp = c.seg_stats + (int64_t)w * 4 * H;
 #pragma unroll
     for (int k = 0; k < 4; ++k) sp[k * H + lane] = st[k];
   }
+}
+
+// ------------------------------------------------------------------ backward
+// per segment: dx_eh from the saved logits (softmax + LeakyReLU + attn dropout backward),
+// d er -> dU_r partials (persistent waves, deterministic workgroup reduction)
+__global__ void __launch_bounds__(256) tgnn_seg_bwd(Ctx c) {
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const PLay PL = c.PL;
+  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) red[p] = 0.f;
+  __syncthreads();
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const bool okb = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
+  const int S = okb ? (int)c.ctl[TGNX_CTL_S] : 0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
+  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+  const bool drop = c.drop;
+  float aUr[2][H], acr[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    aUr[0][h] = aUr[1][h] = 0.f;
+    acr[h] = 0.f;
+  }
+  for (int w = blockIdx.x * 4 + wv; w < S; w += gridDim.x * 4) {
+    const float g = c.seg_g[w];
+    if (g == 0.f) continue;
+    Seg s;
+    seg_of(c, w, lo, hi, start, s);
+    const float gh = g * (1.0f / H);
+    const float* sp = c.seg_stats + (int64_t)w * 4 * H;
+    float m[H], l[H], ft[H], er[H], der[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      m[h] = sp[h]; l[h] = sp[H + h]; ft[h] = sp[2 * H + h]; er[h] = sp[3 * H + h]; der[h] = 0.f;
+    }
+    const int e0 = c.seg_eoff[w], ne = c.seg_eoff[w + 1] - e0;
+    const uint64_t sk = seg_key(s.blk, s.root);
+    for (int base = 0; base < ne; base += 64) {
+      const int o = base + lane;
+      const bool ok = o < ne;
+      float x[H], dx[H];
+      if (ok) load_x8(c.X + (int64_t)(e0 + o) * H, x);
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        float ds = 0.f;
+        dx[h] = 0.f;
+        if (ok) {
+          float sc = x[h] + er[h];
+          const float lk = sc > 0.f ? 1.f : 0.2f;
+          sc = sc > 0.f ? sc : 0.2f * sc;
+          const float a = expf(sc - m[h]) / l[h];
+          const float mk = drop ? keepf(hash4(seed, 3, sk, ((uint64_t)o << 16) | (uint64_t)h), c.pa, c.inv_ka) : 1.f;
+          ds = a * gh * (x[h] * mk - ft[h]) * lk;
+          dx[h] = gh * a * mk + ds;
+        }
+        der[h] += wave_sum(ds);
+      }
+      if (ok) {
+        float4* dp = reinterpret_cast<float4*>(c.DX + (int64_t)(e0 + o) * H);
+        dp[0] = make_float4(dx[0], dx[1], dx[2], dx[3]);
+        dp[1] = make_float4(dx[4], dx[5], dx[6], dx[7]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int dd = lane + 64 * q;
+      float v = dd < c.D ? c.mem[s.root * c.D + dd] : 0.f;
+      if (drop && dd < c.D) v *= node_keep(c, seed, s.blk, s.root, dd);
+#pragma unroll
+      for (int h = 0; h < H; ++h) aUr[q][h] += der[h] * v;
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) acr[h] += der[h];
+  }
+  for (int k = 0; k < 4; ++k) {
+    if (wv == k) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int dd = lane + 64 * q;
+        if (dd < c.D)
+#pragma unroll
+          for (int h = 0; h < H; ++h) red[PL.Ur + h * c.D + dd] += aUr[q][h];
+      }
+      if (lane == 0)
+#pragma unroll
+        for (int h = 0; h < H; ++h) red[PL.cr + h] += acr[h];
+    }
+    __syncthreads();
+  }
+  float* slab = c.slabs_s + (int64_t)blockIdx.x * PL.total;
+  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) slab[p] = red[p];
+}
+
+// per edge: dU_e += dx ⊗ efeat, dU_l += dx ⊗ drop(mem[src]), TimeEncode dw/db (lanes over dims)
+template <int NJ>
+__global__ void __launch_bounds__(256) tgnn_edge_bwd(Ctx c) {
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const PLay PL = c.PL;
+  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) red[p] = 0.f;
+  __syncthreads();
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const bool okb = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
+  const int E = okb ? (int)c.ctl[TGNX_CTL_E] : 0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int F = c.F, D = c.D, d = c.d, FD = F + D;
+  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+  const bool drop = c.drop;
+  float ue[NJ][H], tw[NJ], tb[NJ];
+  float aU[NJ][H], aw[NJ], ab[NJ], ac[H];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int f = lane + 64 * j;
+    const bool enc = f >= d && f < F;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      ue[j][h] = enc ? c.U[c.UL.Ue + h * F + f] : 0.f;
+      aU[j][h] = 0.f;
+    }
+    tw[j] = enc ? c.params[c.L.te_w + f - d] : 0.f;
+    tb[j] = enc ? c.params[c.L.te_b + f - d] : 0.f;
+    aw[j] = ab[j] = 0.f;
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) ac[h] = 0.f;
+  for (int e = blockIdx.x * 4 + wv; e < E; e += gridDim.x * 4) {
+    const EdgeMeta m = c.meta[e];
+    float dx[H];
+    load_x8(c.DX + (int64_t)e * H, dx);
+    const float* fp = feat_row(c, m.frow);
+    const float* mu = c.mem + m.u * D;
+    const uint64_t sk = seg_key(m.blk, m.root);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int f = lane + 64 * j;
+      if (f < FD) {
+        float v, km = 1.f, sn = 0.f;
+        if (f < d) {
+          v = fp ? fp[f] : 1.0f;
+        } else if (f < F) {
+          float sa, ca;
+          sincosf(fmaf(tw[j], m.dt, tb[j]), &sa, &ca);
+          v = ca;
+          sn = sa;
+        } else {
+          v = mu[f - F];
+        }
+        if (drop) km = f < F ? keepf(hash4(seed, 2, sk, ((uint64_t)m.o << 16) | (uint64_t)f), c.pf, c.inv_kf)
+                             : node_keep(c, seed, m.blk, m.u, f - F);
+        v *= km;
+        float denc = 0.f;
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          aU[j][h] += dx[h] * v;
+          denc += dx[h] * ue[j][h];
+        }
+        if (f >= d && f < F) {
+          const float gz = -denc * km * sn;
+          aw[j] += gz * m.dt;
+          ab[j] += gz;
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) ac[h] += dx[h];
+  }
+  for (int k = 0; k < 4; ++k) {
+    if (wv == k) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int f = lane + 64 * j;
+        if (f < FD) {
+#pragma unroll
+          for (int h = 0; h < H; ++h) {
+            if (f < F) red[PL.Ue + h * F + f] += aU[j][h];
+            else red[PL.Ul + h * D + (f - F)] += aU[j][h];
+          }
+          if (f >= d && f < F) {
+            red[PL.w + f - d] += aw[j];
+            red[PL.b + f - d] += ab[j];
+          }
+        }
+      }
+      if (lane == 0)
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          red[PL.ce + h] += ac[h];
+          red[PL.cl + h] += ac[h];
+        }
+    }
+    __syncthreads();
+  }
+  float* slab = c.slabs + (int64_t)blockIdx.x * PL.total;
+  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) slab[p] = red[p];
+}
+
+__global__ void tgnn_grad_reduce(Ctx c, int Ge, int Gs) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= c.PL.total) return;
+  float s = 0.f;
+  for (int g = 0; g < Ge; ++g) s += c.slabs[(int64_t)g * c.PL.total + p];
+  for (int g = 0; g < Gs; ++g) s += c.slabs_s[(int64_t)g * c.PL.total + p];
+  c.red[p] = s;
 }
 
 // ------------------------------------------------------------------ predictor (train): one wave per event
@@ -641,6 +880,7 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
   const int i = lo + blockIdx.x * 4 + wv;
+  const int nloc = hi - lo;
   const bool active = B > 0 && i < hi && c.ctl[TGNX_CTL_ERR] == 0;
   const int D = c.D;
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
@@ -649,7 +889,7 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
   if (active) {
     blk = (int)c.ev_blk[start + i];
     const int64_t roots[3] = {c.ev_src[start + i], c.ev_dst[start + i], c.neg[start + i]};
-    const int segs[3] = {i, B + i, 2 * B + i};
+    const int segs[3] = {i - lo, nloc + i - lo, 2 * nloc + i - lo};
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
       const float sv = c.seg_out[segs[r]];
@@ -724,9 +964,9 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
   gp = wave_sum(gp);
   gn = wave_sum(gn);
   if (lane == 0) {
-    c.seg_g[i] = gs;
-    c.seg_g[B + i] = gp;
-    c.seg_g[2 * B + i] = gn;
+    c.seg_g[i - lo] = gs;
+    c.seg_g[nloc + i - lo] = gp;
+    c.seg_g[2 * nloc + i - lo] = gn;
     c.out_pos[i] = zp;
     c.out_neg[i] = zn;
     ev[8 * D + 0] = dzp;
@@ -735,245 +975,71 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
   }
 }
 
-// predictor parameter gradients: sums over the rank's events of outer products
-__global__ void tgnn_pred_reduce(Ctx c) {
+// predictor weight gradients dWs = Σ_i A_i ⊗ e_s,i and dWd = Σ_i dhp_i ⊗ e_p,i + dhn_i ⊗ e_n,i:
+// AᵀB products over the events, one 16x16 output tile per wave on v_mfma_f32_16x16x4_f32
+// (exact fp32, k-ordered fmaf chain).  Grid: 2 * ceil(D/16)^2 waves.
+__global__ void __launch_bounds__(64) tgnn_pred_reduce_mfma(Ctx c) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
   const int B = (int)c.ctl[TGNX_CTL_B];
   const int D = c.D;
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
-  const int64_t DD = (int64_t)D * D;
-  const int64_t total = 2 * DD + 3 * D + 2;
-  const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (x >= total) return;
   const bool ok = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
+  const int nt = (D + 15) / 16;
+  const int which = blockIdx.x / (nt * nt);
+  const int t = blockIdx.x % (nt * nt), tm = t / nt, tn = t % nt;
+  const int lane = threadIdx.x;
+  const int S = 8 * D + 4;
+  const int m = tm * 16 + (lane & 15), n = tn * 16 + (lane & 15), kk = lane >> 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int npass = which == 0 ? 1 : 2;
+  for (int pass = 0; pass < npass && ok; ++pass) {
+    // which 0: A = cols [0,D) (dhp+dhn), B = cols [D,2D) (e_s)
+    // which 1: pass 0: A = [2D,3D) dhp, B = [3D,4D) e_p ; pass 1: A = [4D,5D) dhn, B = [5D,6D) e_n
+    const int ca = which == 0 ? 0 : (pass == 0 ? 2 * D : 4 * D);
+    const int cb = which == 0 ? D : (pass == 0 ? 3 * D : 5 * D);
+    for (int i0 = lo; i0 < hi; i0 += 4) {
+      const int i = i0 + kk;
+      const bool in = i < hi;
+      const float a = (in && m < D) ? c.evs[(int64_t)i * S + ca + m] : 0.f;
+      const float b = (in && n < D) ? c.evs[(int64_t)i * S + cb + n] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    }
+  }
+  float* out = c.grads + (which == 0 ? c.L.Ws : c.L.Wd);
+  const int col = tn * 16 + (lane & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = tm * 16 + (lane >> 4) * 4 + r;
+    if (row < D && col < D) out[(int64_t)row * D + col] = acc[r];
+  }
+}
+
+// predictor bias / output-layer gradients and the batch loss: one wave per output, lanes over events
+__global__ void __launch_bounds__(256) tgnn_pred_reduce_vec(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int D = c.D;
+  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
+  const bool ok = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
+  const int lane = threadIdx.x & 63;
+  const int y = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (y >= 3 * D + 2) return;
   const int S = 8 * D + 4;
   float acc = 0.f;
-  if (x < DD) {  // dWs[o][dd] = Σ A[o] es[dd]
-    const int o = (int)(x / D), dd = (int)(x % D);
-    if (ok)
-      for (int i = lo; i < hi; ++i) acc += c.evs[(int64_t)i * S + o] * c.evs[(int64_t)i * S + D + dd];
-    c.grads[c.L.Ws + x] = acc;
-  } else if (x < 2 * DD) {  // dWd[o][dd] = Σ dhp[o] ep[dd] + dhn[o] en[dd]
-    const int64_t y = x - DD;
-    const int o = (int)(y / D), dd = (int)(y % D);
-    if (ok)
-      for (int i = lo; i < hi; ++i) {
-        const float* e = c.evs + (int64_t)i * S;
-        acc += e[2 * D + o] * e[3 * D + dd] + e[4 * D + o] * e[5 * D + dd];
-      }
-    c.grads[c.L.Wd + y] = acc;
-  } else {
-    const int y = (int)(x - 2 * DD);
-    if (y < D) {  // dbs = Σ A
-      if (ok) for (int i = lo; i < hi; ++i) acc += c.evs[(int64_t)i * S + y];
-      c.grads[c.L.bs + y] = acc;
-    } else if (y < 2 * D) {  // dbd = Σ dhp + dhn
-      const int o = y - D;
-      if (ok) for (int i = lo; i < hi; ++i) acc += c.evs[(int64_t)i * S + 2 * D + o] + c.evs[(int64_t)i * S + 4 * D + o];
-      c.grads[c.L.bd + o] = acc;
-    } else if (y < 3 * D) {  // dWo = Σ dzp hpos + dzn hneg
-      const int o = y - 2 * D;
-      if (ok)
-        for (int i = lo; i < hi; ++i) {
-          const float* e = c.evs + (int64_t)i * S;
-          acc += e[8 * D] * e[6 * D + o] + e[8 * D + 1] * e[7 * D + o];
-        }
-      c.grads[c.L.Wo + o] = acc;
-    } else if (y == 3 * D) {  // dbo
-      if (ok) for (int i = lo; i < hi; ++i) acc += c.evs[(int64_t)i * S + 8 * D] + c.evs[(int64_t)i * S + 8 * D + 1];
-      c.grads[c.L.bo] = acc;
-    } else {  // batch loss slot
-      if (ok) for (int i = lo; i < hi; ++i) acc += c.evs[(int64_t)i * S + 8 * D + 2];
-      c.grads[c.L.total] = acc;
-    }
+  for (int i = lo + lane; ok && i < hi; i += 64) {
+    const float* e = c.evs + (int64_t)i * S;
+    if (y < D) acc += e[y];                                                  // dbs = Σ (dhp + dhn)
+    else if (y < 2 * D) acc += e[2 * D + y - D] + e[4 * D + y - D];          // dbd
+    else if (y < 3 * D) acc += e[8 * D] * e[6 * D + y - 2 * D] + e[8 * D + 1] * e[7 * D + y - 2 * D];  // dWo
+    else if (y == 3 * D) acc += e[8 * D] + e[8 * D + 1];                     // dbo
+    else acc += e[8 * D + 2];                                                // batch loss
   }
-}
-
-// ------------------------------------------------------------------ backward: persistent waves
-template <int NJ>
-__global__ void __launch_bounds__(256) tgnn_attn_bwd(Ctx c) {
-  extern __shared__ __attribute__((aligned(16))) float red[];
-  const PLay PL = c.PL;
-  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) red[p] = 0.f;
-  __syncthreads();
-  const int B = (int)c.ctl[TGNX_CTL_B];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
-  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
-  const int64_t* src = c.ev_src + start;
-  const int64_t* dst = c.ev_dst + start;
-  const float* evt = c.ev_t + start;
-  const float* msg = c.ev_msg + start * c.d;
-  const int64_t* neg = c.neg + start * c.Kn;
-  const int gen = (int)c.ctl[TGNX_CTL_GEN];
-  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-  const bool drop = c.drop;
-  const bool ok = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
-
-  LaneW<NJ> W;
-  W.load(c, lane);
-  float aUe[NJ][H], aUl[2][H], aUr[2][H], aw[NJ], ab[NJ];
-  float ace[H], acl[H], acr[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-#pragma unroll
-    for (int jj = 0; jj < NJ; ++jj) aUe[jj][h] = 0.f;
-    aUl[0][h] = aUl[1][h] = aUr[0][h] = aUr[1][h] = 0.f;
-    ace[h] = acl[h] = acr[h] = 0.f;
-  }
-#pragma unroll
-  for (int jj = 0; jj < NJ; ++jj) aw[jj] = ab[jj] = 0.f;
-
-  const int nrows = ok ? (hi - lo) * (2 + c.Kn) : 0;
-  for (int w = blockIdx.x * 4 + wv; w < nrows; w += gridDim.x * 4) {
-    Seg s;
-    seg_of(c, w, B, lo, hi, s);
-    const float g = c.seg_g[s.row];
-    if (g == 0.f) continue;
-    s.root = s.kind == 2 ? src[s.i] : s.kind == 1 ? dst[s.i] : neg[s.i * c.Kn + s.cc];
-    s.blk = (int)c.ev_blk[start + s.i];
-    const float gh = g * (1.0f / H);
-    const float* sp = c.seg_stats + (int64_t)s.row * 4 * H;
-    float m[H], l[H], ft[H], er[H], der[H];
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      m[h] = sp[h]; l[h] = sp[H + h]; ft[h] = sp[2 * H + h]; er[h] = sp[3 * H + h]; der[h] = 0.f;
-    }
-    float nfr[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int dd = lane + 64 * q;
-      float v = dd < c.D ? c.mem[s.root * c.D + dd] : 0.f;
-      if (drop && dd < c.D) v *= node_keep(c, seed, s.blk, s.root, dd);
-      nfr[q] = v;
-    }
-    EdgeWalk ew;
-    ew.init(c, s, gen, lane);
-    const int E = ew.count();
-    const int eoff = c.seg_eoff[s.row];
-    if (eoff + E > c.Ecap) continue;
-    const uint64_t sk = seg_key(s.blk, s.root);
-    for (int o = 0; o < E; ++o) {
-      int64_t u;
-      const float* fp;
-      float bt;
-      ew.edge(c, s, o, src, dst, evt, msg, u, fp, bt);
-      const float dt = bt - ta_at<true>(c, u, s.blk, gen, evt);
-      float v[NJ], km[NJ], sn[NJ];
-#pragma unroll
-      for (int jj = 0; jj < NJ; ++jj) {
-        const int f = lane + 64 * jj;
-        v[jj] = 0.f; km[jj] = 1.f; sn[jj] = 0.f;
-        if (f < c.F) {
-          if (f < c.d) {
-            v[jj] = fp ? fp[f] : 1.0f;
-          } else {
-            float sa, ca;
-            sincosf(fmaf(W.tw[jj], dt, W.tb[jj]), &sa, &ca);
-            v[jj] = ca;
-            sn[jj] = sa;
-          }
-          if (drop) km[jj] = keepf(hash4(seed, 2, sk, ((uint64_t)o << 16) | (uint64_t)f), c.pf, c.inv_kf);
-          v[jj] *= km[jj];
-        }
-      }
-      float nfu[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int dd = lane + 64 * q;
-        float x = dd < c.D ? c.mem[u * c.D + dd] : 0.f;
-        if (drop && dd < c.D) x *= node_keep(c, seed, s.blk, u, dd);
-        nfu[q] = x;
-      }
-      const float* xp = c.X + (int64_t)(eoff + o) * H;
-      float dx[H];
-#pragma unroll
-      for (int h = 0; h < H; ++h) {
-        const float xh = xp[h];
-        float sc = xh + er[h];
-        const float lk = sc > 0.f ? 1.f : 0.2f;
-        sc = sc > 0.f ? sc : 0.2f * sc;
-        const float a = expf(sc - m[h]) / l[h];
-        const float mk = drop ? keepf(hash4(seed, 3, sk, ((uint64_t)o << 16) | (uint64_t)h), c.pa, c.inv_ka) : 1.f;
-        const float ds = a * gh * (xh * mk - ft[h]) * lk;
-        dx[h] = gh * a * mk + ds;
-        der[h] += ds;
-        ace[h] += dx[h];
-        acl[h] += dx[h];
-      }
-#pragma unroll
-      for (int jj = 0; jj < NJ; ++jj) {
-        float denc = 0.f;
-#pragma unroll
-        for (int h = 0; h < H; ++h) {
-          aUe[jj][h] += dx[h] * v[jj];
-          denc += dx[h] * W.ue[jj][h];
-        }
-        const int f = lane + 64 * jj;
-        if (f >= c.d && f < c.F) {
-          const float gz = -denc * km[jj] * sn[jj];
-          aw[jj] += gz * dt;
-          ab[jj] += gz;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int h = 0; h < H; ++h) aUl[q][h] += dx[h] * nfu[q];
-    }
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      acr[h] += der[h];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) aUr[q][h] += der[h] * nfr[q];
-    }
-  }
-  // deterministic workgroup reduction: waves add in order
-  for (int k = 0; k < 4; ++k) {
-    if (wv == k) {
-#pragma unroll
-      for (int jj = 0; jj < NJ; ++jj) {
-        const int f = lane + 64 * jj;
-        if (f < c.F) {
-#pragma unroll
-          for (int h = 0; h < H; ++h) red[PL.Ue + h * c.F + f] += aUe[jj][h];
-          if (f >= c.d) {
-            red[PL.w + f - c.d] += aw[jj];
-            red[PL.b + f - c.d] += ab[jj];
-          }
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int dd = lane + 64 * q;
-        if (dd < c.D) {
-#pragma unroll
-          for (int h = 0; h < H; ++h) {
-            red[PL.Ul + h * c.D + dd] += aUl[q][h];
-            red[PL.Ur + h * c.D + dd] += aUr[q][h];
-          }
-        }
-      }
-      if (lane == 0) {
-#pragma unroll
-        for (int h = 0; h < H; ++h) {
-          red[PL.ce + h] += ace[h];
-          red[PL.cl + h] += acl[h];
-          red[PL.cr + h] += acr[h];
-        }
-      }
-    }
-    __syncthreads();
-  }
-  float* slab = c.slabs + (int64_t)blockIdx.x * PL.total;
-  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) slab[p] = red[p];
-}
-
-__global__ void tgnn_grad_reduce(Ctx c, int G) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= c.PL.total) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += c.slabs[(int64_t)g * c.PL.total + p];
-  c.red[p] = s;
+  acc = wave_sum(acc);
+  if (lane != 0) return;
+  if (y < D) c.grads[c.L.bs + y] = acc;
+  else if (y < 2 * D) c.grads[c.L.bd + y - D] = acc;
+  else if (y < 3 * D) c.grads[c.L.Wo + y - 2 * D] = acc;
+  else if (y == 3 * D) c.grads[c.L.bo] = acc;
+  else c.grads[c.L.total] = acc;
 }
 
 // re-expand the collapsed gradients into the reference's parameters
@@ -1199,27 +1265,35 @@ static size_t carve(size_t& off, size_t bytes) {
 }
 
 struct WsLay {
-  size_t touches, seg_eoff, seg_nintra, seg_out, seg_stats, seg_g, X, U, evs, slabs, red, blkmax, blk_rank,
-      blk_order, HS, total;
-  int64_t Ecap;
+  size_t touches, sp_pref, sp_keys, seg_cnt, seg_eoff, seg_out, seg_stats, seg_g, X, DX, meta, U, evs, slabs,
+      slabs_s, red, blkmax, blk_rank, blk_order, HS, total;
+  int64_t Ecap, Scap;
 };
 static WsLay make_ws(const tgnx_tgnn_config* cfg) {
   WsLay W;
   const int64_t B = cfg->max_batch, Kn = cfg->max_neg < 1 ? 1 : cfg->max_neg;
   const int D = cfg->mem_dim, d = cfg->msg_dim;
-  W.Ecap = 3 * B * (cfg->ring + 1) + 2 * B * B + 64;
+  W.Scap = B * (2 + (Kn > 1 ? Kn : 1));
+  if (W.Scap < 3 * B) W.Scap = 3 * B;
+  W.Ecap = W.Scap * (cfg->ring + 1) + 2 * B * B + 64;
+  const int P = make_play(D, d).total;
   size_t off = 0;
   W.touches = carve(off, (size_t)TOUCH_MAX * 8);
-  W.seg_eoff = carve(off, (size_t)(3 * B + 1) * 4);
-  W.seg_nintra = carve(off, (size_t)3 * B * 4);
-  W.seg_out = carve(off, (size_t)B * (2 + (Kn > 1 ? Kn : 1)) * 4);
+  W.sp_pref = carve(off, (size_t)(TOUCH_MAX + 1) * 4);
+  W.sp_keys = carve(off, (size_t)TOUCH_MAX * 8);
+  W.seg_cnt = carve(off, (size_t)W.Scap * 4);
+  W.seg_eoff = carve(off, (size_t)(W.Scap + 1) * 4);
+  W.seg_out = carve(off, (size_t)W.Scap * 4);
   W.seg_stats = carve(off, (size_t)3 * B * 4 * H * 4);
   W.seg_g = carve(off, (size_t)3 * B * 4);
   W.X = carve(off, (size_t)W.Ecap * H * 4);
+  W.DX = carve(off, (size_t)(3 * B * (cfg->ring + 1) + 2 * B * B + 64) * H * 4);
+  W.meta = carve(off, (size_t)W.Ecap * sizeof(EdgeMeta));
   W.U = carve(off, (size_t)make_ulay(D, d).total * 4);
   W.evs = carve(off, (size_t)B * (8 * D + 4) * 4);
-  W.slabs = carve(off, (size_t)GBWD * make_play(D, d).total * 4);
-  W.red = carve(off, (size_t)make_play(D, d).total * 4);
+  W.slabs = carve(off, (size_t)GBWD * P * 4);
+  W.slabs_s = carve(off, (size_t)GSEG * P * 4);
+  W.red = carve(off, (size_t)P * 4);
   W.blkmax = carve(off, (size_t)B * 4);
   W.blk_rank = carve(off, (size_t)B * 4);
   W.blk_order = carve(off, (size_t)B * 4);
@@ -1288,15 +1362,20 @@ static int make_ctx(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* b, int
   WsLay W = make_ws(cfg);
   char* ws = reinterpret_cast<char*>(b->ws);
   c.touches = reinterpret_cast<uint64_t*>(ws + W.touches);
+  c.sp_pref = reinterpret_cast<int*>(ws + W.sp_pref);
+  c.sp_keys = reinterpret_cast<uint64_t*>(ws + W.sp_keys);
+  c.seg_cnt = reinterpret_cast<int*>(ws + W.seg_cnt);
   c.seg_eoff = reinterpret_cast<int*>(ws + W.seg_eoff);
-  c.seg_nintra = reinterpret_cast<int*>(ws + W.seg_nintra);
   c.seg_out = reinterpret_cast<float*>(ws + W.seg_out);
   c.seg_stats = reinterpret_cast<float*>(ws + W.seg_stats);
   c.seg_g = reinterpret_cast<float*>(ws + W.seg_g);
   c.X = reinterpret_cast<float*>(ws + W.X);
+  c.DX = reinterpret_cast<float*>(ws + W.DX);
+  c.meta = reinterpret_cast<EdgeMeta*>(ws + W.meta);
   c.U = reinterpret_cast<float*>(ws + W.U);
   c.evs = reinterpret_cast<float*>(ws + W.evs);
   c.slabs = reinterpret_cast<float*>(ws + W.slabs);
+  c.slabs_s = reinterpret_cast<float*>(ws + W.slabs_s);
   c.red = reinterpret_cast<float*>(ws + W.red);
   c.blkmax = reinterpret_cast<float*>(ws + W.blkmax);
   c.blk_rank = reinterpret_cast<int*>(ws + W.blk_rank);
@@ -1304,6 +1383,8 @@ static int make_ctx(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* b, int
   c.HS = reinterpret_cast<float*>(ws + W.HS);
   c.Ecap = W.Ecap;
   c.Bmax = cfg->max_batch;
+  c.Ge = GBWD;
+  c.Gs = GSEG;
   c.L = make_lay(c.D, c.d);
   c.UL = make_ulay(c.D, c.d);
   c.PL = make_play(c.D, c.d);
@@ -1312,33 +1393,58 @@ static int make_ctx(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* b, int
 
 static inline int grid_for(int64_t n, int per) { return (int)((n + per - 1) / per); }
 
-template <bool TRAIN>
-static int launch_attn_fwd(const Ctx& c, int rows_cap, hipStream_t s) {
-  const int F = c.F;
-  const int g = grid_for(rows_cap, 4);
-  if (g == 0) return TGNX_OK;
-  if (F <= 64) tgnn_attn_fwd<1, TRAIN><<<g, 256, 0, s>>>(c);
-  else if (F <= 128) tgnn_attn_fwd<2, TRAIN><<<g, 256, 0, s>>>(c);
-  else if (F <= 192) tgnn_attn_fwd<3, TRAIN><<<g, 256, 0, s>>>(c);
-  else if (F <= 256) tgnn_attn_fwd<4, TRAIN><<<g, 256, 0, s>>>(c);
-  else tgnn_attn_fwd<5, TRAIN><<<g, 256, 0, s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_attn_fwd");
-  return TGNX_OK;
-}
-
-static int launch_attn_bwd(const Ctx& c, hipStream_t s) {
-  const int F = c.F;
-  const size_t shm = (size_t)c.PL.total * 4;
-  if (F <= 64) tgnn_attn_bwd<1><<<GBWD, 256, shm, s>>>(c);
-  else if (F <= 128) tgnn_attn_bwd<2><<<GBWD, 256, shm, s>>>(c);
-  else if (F <= 192) tgnn_attn_bwd<3><<<GBWD, 256, shm, s>>>(c);
-  else if (F <= 256) tgnn_attn_bwd<4><<<GBWD, 256, shm, s>>>(c);
-  else tgnn_attn_bwd<5><<<GBWD, 256, shm, s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_attn_bwd");
-  return TGNX_OK;
-}
-
 static size_t assemble_smem() { return (size_t)TOUCH_MAX * 8 + (size_t)TOUCH_MAX * 4; }
+
+static int edge_grid(int64_t Ecap) {
+  const int64_t g = (Ecap * 16 + 255) / 256;
+  return (int)(g < 2048 ? (g < 1 ? 1 : g) : 2048);
+}
+
+// assembly -> counts -> offsets -> edge metadata -> collapsed weights -> edge logits -> segment softmax
+template <bool TRAIN>
+static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
+  probe_begin(TGNX_K_ASSEMBLE, s);
+  tgnn_assemble<TRAIN><<<1, 1024, assemble_smem(), s>>>(c);
+  probe_end(TGNX_K_ASSEMBLE, s);
+  TGNX_LAUNCH_CHECK("tgnn_assemble");
+  tgnn_seg_count<<<grid_for(Scap, 256), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_seg_count");
+  tgnn_seg_scan<<<1, 1024, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_seg_scan");
+  tgnn_edge_meta<TRAIN><<<edge_grid(c.Ecap) / 4 + 1, 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_edge_meta");
+  tgnn_collapse<<<256, 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_collapse");
+  const int pid = TRAIN ? TGNX_K_ATTN_FWD : TGNX_K_ATTN_FWD_EVAL;
+  probe_begin(pid, s);
+  tgnn_edge_fwd<<<edge_grid(c.Ecap), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_edge_fwd");
+  tgnn_seg_fwd<TRAIN><<<grid_for(Scap, 4), 256, 0, s>>>(c);
+  probe_end(pid, s);
+  TGNX_LAUNCH_CHECK("tgnn_seg_fwd");
+  return TGNX_OK;
+}
+
+static int launch_backward(const Ctx& c, hipStream_t s) {
+  const size_t shm = (size_t)c.PL.total * 4;
+  probe_begin(TGNX_K_ATTN_BWD, s);
+  tgnn_seg_bwd<<<GSEG, 256, shm, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_seg_bwd");
+  const int FD = c.F + c.D;
+  if (FD <= 64) tgnn_edge_bwd<1><<<GBWD, 256, shm, s>>>(c);
+  else if (FD <= 128) tgnn_edge_bwd<2><<<GBWD, 256, shm, s>>>(c);
+  else if (FD <= 192) tgnn_edge_bwd<3><<<GBWD, 256, shm, s>>>(c);
+  else if (FD <= 256) tgnn_edge_bwd<4><<<GBWD, 256, shm, s>>>(c);
+  else if (FD <= 320) tgnn_edge_bwd<5><<<GBWD, 256, shm, s>>>(c);
+  else if (FD <= 384) tgnn_edge_bwd<6><<<GBWD, 256, shm, s>>>(c);
+  else tgnn_edge_bwd<7><<<GBWD, 256, shm, s>>>(c);
+  probe_end(TGNX_K_ATTN_BWD, s);
+  TGNX_LAUNCH_CHECK("tgnn_edge_bwd");
+  tgnn_grad_reduce<<<grid_for(c.PL.total, 256), 256, 0, s>>>(c, GBWD, GSEG);
+  TGNX_LAUNCH_CHECK("tgnn_grad_reduce");
+  return TGNX_OK;
+}
+
 
 }  // namespace tgnx
 
@@ -1390,20 +1496,21 @@ int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers
     tgnn_negs<<<grid_for(Bmax, 256), 256, 0, s>>>(c);
     TGNX_LAUNCH_CHECK("tgnn_negs");
   }
-  tgnn_assemble<true><<<1, 1024, assemble_smem(), s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_assemble");
-  tgnn_collapse<<<256, 256, 0, s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_collapse");
-  rc = launch_attn_fwd<true>(c, 3 * Bmax, s);
+  rc = launch_forward<true>(c, 3 * (int64_t)Bmax, s);
   if (rc) return rc;
+  probe_begin(TGNX_K_PRED, s);
   tgnn_pred_train<<<grid_for(Bmax, 4), 256, 0, s>>>(c);
+  probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgnn_pred_train");
-  tgnn_pred_reduce<<<grid_for(2 * (int64_t)c.D * c.D + 3 * c.D + 2, 256), 256, 0, s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_pred_reduce");
-  rc = launch_attn_bwd(c, s);
+  {
+    const int nt = (c.D + 15) / 16;
+    tgnn_pred_reduce_mfma<<<2 * nt * nt, 64, 0, s>>>(c);
+    TGNX_LAUNCH_CHECK("tgnn_pred_reduce_mfma");
+    tgnn_pred_reduce_vec<<<grid_for(3 * c.D + 2, 4), 256, 0, s>>>(c);
+    TGNX_LAUNCH_CHECK("tgnn_pred_reduce_vec");
+  }
+  rc = launch_backward(c, s);
   if (rc) return rc;
-  tgnn_grad_reduce<<<grid_for(c.PL.total, 256), 256, 0, s>>>(c, GBWD);
-  TGNX_LAUNCH_CHECK("tgnn_grad_reduce");
   tgnn_grad_expand<<<grid_for(c.L.Ws, 256), 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgnn_grad_expand");
   return TGNX_OK;
@@ -1415,9 +1522,13 @@ int tgnx_tgnn_train_update(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers*
   if (rc) return rc;
   TGNX_CHECK_ARG(buf->grads && buf->adam_m && buf->adam_v, "tgnx_tgnn_train_update: null optimizer buffer");
   hipStream_t s = as_stream(stream);
+  probe_begin(TGNX_K_ADAM, s);
   tgnn_adam<<<grid_for(c.L.total, 256), 256, 0, s>>>(c);
+  probe_end(TGNX_K_ADAM, s);
   TGNX_LAUNCH_CHECK("tgnn_adam");
+  probe_begin(TGNX_K_FINISH, s);
   tgnn_finish<true><<<1, 1024, ring_insert_smem_bytes(cfg->max_batch), s>>>(c);
+  probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgnn_finish");
   return TGNX_OK;
 }
@@ -1434,11 +1545,7 @@ int tgnx_tgnn_eval_step(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* bu
   c.drop = 0;
   hipStream_t s = as_stream(stream);
   const int Bmax = cfg->max_batch;
-  tgnn_assemble<false><<<1, 1024, assemble_smem(), s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_assemble");
-  tgnn_collapse<<<256, 256, 0, s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_collapse");
-  rc = launch_attn_fwd<false>(c, (int64_t)Bmax * (2 + Kn), s);
+  rc = launch_forward<false>(c, (int64_t)Bmax * (2 + Kn), s);
   if (rc) return rc;
   tgnn_pred_eval_src<<<grid_for(Bmax, 4), 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgnn_pred_eval_src");

@@ -28,6 +28,8 @@ SIGNATURES = {
     "tgnx_ring_insert": (ctypes.c_int, [P, P, P, c_i64, c_i32, P, P, P, c_i64, c_i64, P, c_vp]),
     "tgnx_neg_sample": (ctypes.c_int, [P, c_i64, P, c_i64, c_u64, c_u64, P, c_vp]),
     "tgnx_block_ids_host": (ctypes.c_int, [P, P, c_i64, c_i64, P]),
+    "tgnx_probe_enable": (ctypes.c_int, [c_i32]),
+    "tgnx_probe_read": (ctypes.c_int, [P, P]),
     "tgnx_tgnn_param_layout": (ctypes.c_int, [P, P]),
     "tgnx_tgnn_ws_bytes": (c_sz, [P]),
     "tgnx_tgnn_advance": (ctypes.c_int, [P, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64,

@@ -140,6 +140,41 @@ class TgnnEngine:
         nb = int(self.ctl[CTL["NB"]])
         return self.out_pos[:B], self.out_neg[:B * Kn].view(B, Kn), self.mrr[(nb - 1) & 0xFFFF]
 
+    # ------------------------------------------------------------------ resident (events in HBM)
+    def bind_resident(self, src, dst, t, blk, msg, neg_buf, split_lo, split_hi, batch, dropout=True):
+        """Point the step at device-resident event arrays (global event index = row): the batch
+        cursor lives in the control block, so a step is three launches of C calls and no host sync."""
+        self._res_keep = (src, dst, t, blk, msg, neg_buf)
+        self._res_buf = self._buffers(src, dst, t, blk, msg, neg_buf)
+        self._res = (int(split_lo), int(split_hi), int(batch))
+        self._res_drop = 1 if (dropout and self.model.training) else 0
+        L = _lib.lib()
+        self._f = (L.tgnx_tgnn_advance, L.tgnx_tgnn_train_fwd_bwd, L.tgnx_tgnn_train_update)
+        self._cfg_ref = ctypes.byref(self.cfg)
+        self._buf_ref = ctypes.byref(self._res_buf)
+        self._ctl_p = ctypes.c_void_p(self.ctl.data_ptr())
+
+    def begin_epoch(self):
+        """epoch_utils.py:175 — neighbor_loader.reset_state() at every train epoch; batch cursor to 0."""
+        self.loader.reset_state()
+        self.ctl[CTL["NB"]] = 0
+
+    def resident_train_step(self):
+        adv, fb, up = self._f
+        st = self._stream()
+        lo, hi, batch = self._res
+        rc = adv(self._ctl_p, 1, 0, 0, 0, lo, hi, batch, self.rank, self.world, self.seed, 1, st)
+        rc |= fb(self._cfg_ref, self._buf_ref, 1, self._res_drop, st)
+        if rc:
+            raise RuntimeError(f"tgnx resident step failed: {_lib.lib().tgnx_last_error().decode()}")
+        self._allreduce_grads()
+        if up(self._cfg_ref, self._buf_ref, st):
+            raise RuntimeError(f"tgnx resident update failed: {_lib.lib().tgnx_last_error().decode()}")
+
+    def units(self):
+        """(sum of assembled edges, sum of segments) since the last reset — roofline units."""
+        return int(self.ctl[13]), int(self.ctl[14])
+
     # ------------------------------------------------------------------ status
     def check(self):
         err = int(self.ctl[CTL["ERR"]])
