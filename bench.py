@@ -161,7 +161,7 @@ def main():
     bytes_edge = 20 + 4 * d + 4 * D + 4
     bytes_root = 4 * D + 4
     probes = {}
-    for name, kid in (("tgnn_attn_fwd", 1), ("tgnn_attn_bwd", 2)):
+    for name, kid in (("tgnn_edge_fwd", 1), ("tgnn_edge_bwd", 2), ("tgnn_seg_fwd", 6), ("tgnn_seg_bwd", 8)):
         _lib.call("tgnx_probe_enable", kid)
         pe0, ps0 = eng.units()
         for _ in range(args.probe_steps):
@@ -173,10 +173,12 @@ def main():
         pe1, ps1 = eng.units()
         launches = max(int(n.value), 1)
         avg_ms = ms.value / launches
-        # units per launch: edges/segments this rank's launch processed (rows are sliced per rank)
-        edges = (pe1 - pe0) / launches / world
+        # units per launch: edges / segments this rank's launch processed (rows are sliced per rank).
+        # Edge kernels gather per edge the ring entry / edge record, feature row and neighbour memory
+        # row (SURVEY §8(d) per sampled edge); segment kernels read per root its memory row + time.
+        edges = (pe1 - pe0) / launches
         roots = (ps1 - ps0) / launches
-        algo = edges * bytes_edge + roots * bytes_root
+        algo = edges * bytes_edge if name.startswith("tgnn_edge") else roots * bytes_root
         probes[name] = dict(avg_us=avg_ms * 1e3, launches=launches, edges=edges, roots=roots, bytes=algo,
                             gbs=algo / (avg_ms * 1e-3) / 1e9)
     dom = max(probes, key=lambda k: probes[k]["avg_us"])
@@ -219,8 +221,8 @@ def main():
                          "unit": "GB/s", "frac": round(pd["gbs"] / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "avg_launch_us": round(pd["avg_us"], 3),
                          "algo_bytes_per_launch": round(pd["bytes"]),
-                         "bytes_model": f"SURVEY §8(d): {bytes_edge} B/edge (ring entry 20 + feature 4d + "
-                                        f"neighbour memory 4D + time 4) x edges + {bytes_root} B/root x roots"},
+                         "bytes_model": f"SURVEY §8(d): edge kernels {bytes_edge} B/edge (ring entry 20 + feature 4d + "
+                                        f"neighbour memory 4D + time 4) x edges; segment kernels {bytes_root} B/root"},
             "kernels_us": {k: round(v["avg_us"], 3) for k, v in probes.items()},
             "cpu_baseline": cpu,
             "loss_sum": round(loss, 4),

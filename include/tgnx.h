@@ -88,13 +88,15 @@ int tgnx_block_ids_host(const int64_t* src, const int64_t* dst, int64_t num_even
  * launch stream; tgnx_probe_read waits for them and returns the summed
  * duration (ms) and the launch count, then clears.  Off by default.
  * ------------------------------------------------------------------------ */
-#define TGNX_K_ATTN_FWD 1
-#define TGNX_K_ATTN_BWD 2
+#define TGNX_K_EDGE_FWD 1       /* tgnn_edge_fwd  */
+#define TGNX_K_EDGE_BWD 2       /* tgnn_edge_bwd  */
 #define TGNX_K_ASSEMBLE 3
 #define TGNX_K_PRED 4
 #define TGNX_K_FINISH 5
-#define TGNX_K_ATTN_FWD_EVAL 6
+#define TGNX_K_SEG_FWD 6        /* tgnn_seg_fwd (train and eval) */
 #define TGNX_K_ADAM 7
+#define TGNX_K_SEG_BWD 8        /* tgnn_seg_bwd */
+#define TGNX_K_EDGE_META 9      /* tgnn_edge_meta */
 int tgnx_probe_enable(int32_t kernel_id);
 int tgnx_probe_read(double* total_ms, int64_t* launches);
 

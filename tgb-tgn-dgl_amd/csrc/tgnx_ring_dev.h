@@ -46,72 +46,45 @@ __device__ __forceinline__ void ring_insert_block(int64_t* __restrict__ nbr, int
   for (int p = p0; p < p1; ++p)
     if (p == 0 || (key[p] >> 32) != (key[p - 1] >> 32)) run_start[rid++] = p;
   __syncthreads();
-  for (int r = threadIdx.x; r < U; r += T) {
-    int a = run_start[r];
-    int c = (r + 1 < U ? run_start[r + 1] : n2) - a;
-    int64_t v = (int64_t)(key[a] >> 32);
-    assoc[v] = r;
-    int m = c < K ? c : K;
-    // new entries (newest first), canonical K newest when c > K
-    int64_t ne[KMAX], nn[KMAX];
-    float nt[KMAX];
-    for (int j = 0; j < m; ++j) {
-      uint64_t kk = key[a + j];
-      int i = B - 1 - (int)((kk & 0xFFFFFFFFull) >> 1);
-      int dir = (int)(kk & 1ull);
-      ne[j] = cur + i;
-      nn[j] = dir == 0 ? src[i] : dst[i];
-      nt[j] = ev_t[i];
-    }
-    // old row
-    int64_t oe[KMAX], on[KMAX];
-    float ot[KMAX];
+  // one wave per node run: lanes [0,K) hold the old slots, lanes [K, K+m) the m newest new entries;
+  // each candidate's output slot is its rank by e_id (desc) and, separately, by t (desc) —
+  // top-K of [old | dense] exactly as neighbor_loader.py:91-104, with no per-thread arrays.
+  const int lane = threadIdx.x & 63, nwv = T >> 6;
+  for (int r = threadIdx.x >> 6; r < U; r += nwv) {
+    const int a = run_start[r];
+    const int c = (r + 1 < U ? run_start[r + 1] : n2) - a;
+    const int64_t v = (int64_t)(key[a] >> 32);
+    if (lane == 0) assoc[v] = r;
+    const int m = c < K ? c : K;
     int64_t* er = eid + v * K;
     int64_t* nr = nbr + v * K;
     float* tr = rt + v * K;
-    for (int j = 0; j < K; ++j) {
-      oe[j] = er[j];
-      on[j] = nr[j];
-      ot[j] = tr[j];
+    int64_t ce = INT64_MIN, cn = -1;
+    float ct = -INFINITY;
+    const bool cand = lane < K + m;
+    if (lane < K) {
+      ce = er[lane];
+      cn = nr[lane];
+      ct = tr[lane];
+    } else if (cand) {
+      const uint64_t kk = key[a + lane - K];
+      const int i = B - 1 - (int)((kk & 0xFFFFFFFFull) >> 1);
+      ce = cur + i;
+      cn = (kk & 1ull) == 0 ? src[i] : dst[i];
+      ct = ev_t[i];
     }
-    // e_id top-K of [old | dense] (dense = m new + (K-m) empty), neighbours follow e_id
-    int io = 0, in = 0;
-    for (int s = 0; s < K; ++s) {
-      int64_t eo = io < K ? oe[io] : -1;
-      int64_t en = in < m ? ne[in] : -1;
-      if (en > eo) {
-        er[s] = en;
-        nr[s] = nn[in];
-        ++in;
-      } else {
-        er[s] = eo;
-        nr[s] = eo >= 0 ? on[io] : -1;
-        ++io;
-      }
+    int re = 0, rtk = 0;
+    for (int j = 0; j < K + m; ++j) {
+      const int64_t oe = __shfl(ce, j);
+      const float ot = __shfl(ct, j);
+      re += (oe > ce) || (oe == ce && j < lane);
+      rtk += (ot > ct) || (ot == ct && j < lane);
     }
-    // t top-K of [old t | new t + (-1) padding] (neighbor_loader.py:100: independent of e_id)
-    for (int x = 1; x < m; ++x) {  // sort new t descending (m <= K)
-      float y = nt[x];
-      int z = x - 1;
-      while (z >= 0 && nt[z] < y) {
-        nt[z + 1] = nt[z];
-        --z;
-      }
-      nt[z + 1] = y;
+    if (cand && re < K) {
+      er[re] = ce;
+      nr[re] = ce >= 0 ? cn : -1;
     }
-    io = 0;
-    in = 0;
-    for (int s = 0; s < K; ++s) {
-      float to = io < K ? ot[io] : -1.0f;
-      float tn = in < m ? nt[in] : -1.0f;
-      if (tn > to) {
-        tr[s] = tn;
-        ++in;
-      } else {
-        tr[s] = to;
-        ++io;
-      }
-    }
+    if (cand && rtk < K) tr[rtk] = ct;
   }
   __syncthreads();
 }

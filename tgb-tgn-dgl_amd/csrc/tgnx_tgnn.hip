@@ -25,7 +25,7 @@ constexpr int H = 8;          // gnn.att_head
 constexpr int DMAX = 128;     // gnn.dim_out (memory/time/embedding dim) capacity
 constexpr int FMAX = 320;     // d + D capacity
 constexpr int TOUCH_MAX = 8192;
-constexpr int GBWD = 128;     // workgroups of the edge backward kernel (= partial slabs)
+constexpr int GBWD = 256;     // workgroups of the edge backward kernel (= partial slabs)
 constexpr int GSEG = 64;      // workgroups of the segment backward kernel
 constexpr int MRR_SLOTS = 65536;  // per-batch MRR ring in buffers.mrr
 
@@ -236,58 +236,72 @@ __global__ void tgnn_negs(Ctx c) {
   c.neg[start + i] = v;
 }
 
-// U = attn·W per head (exact collapse of EdgeGATConv's el/er/ee), predictor transposes/row sums
-__global__ void tgnn_collapse(Ctx c) {
+// U = attn·W per head (exact collapse of EdgeGATConv's el/er/ee), predictor transposes/row sums.
+// Blocks [0, nb_dot): 64 outputs of U_e / U_l / U_r x 4 split-d waves (coalesced over outputs);
+// then 4 row sums per block (wave each, lanes over the row); then the two predictor transposes.
+__device__ __forceinline__ int collapse_dot_blocks(const Ctx& c) {
+  return (H * c.F + 63) / 64 + 2 * ((H * c.D + 63) / 64);
+}
+__global__ void __launch_bounds__(256) tgnn_collapse(Ctx c) {
+  __shared__ float part[4][64];
   const int D = c.D, F = c.F;
   const float* P = c.params;
-  const int64_t nUe = (int64_t)H * F, nUl = H * D, nP = (int64_t)D * D;
-  const int64_t total = nUe + 2 * nUl + 3 * H + 2 * nP + 2 * D;
-  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total; x += (int64_t)gridDim.x * blockDim.x) {
-    int64_t y = x;
-    if (y < nUe) {
-      int h = (int)(y / F), f = (int)(y % F);
-      float s = 0.f;
-      for (int dd = 0; dd < D; ++dd) s += P[c.L.attn_e + h * D + dd] * P[c.L.We + (int64_t)(h * D + dd) * F + f];
-      c.U[c.UL.Ue + y] = s;
-      continue;
-    }
-    y -= nUe;
-    if (y < 2 * nUl) {
-      int which = (int)(y / nUl);
-      int64_t z = y % nUl;
-      int h = (int)(z / D), k = (int)(z % D);
-      const float* a = P + (which == 0 ? c.L.attn_l : c.L.attn_r) + h * D;
-      float s = 0.f;
-      for (int dd = 0; dd < D; ++dd) s += a[dd] * P[c.L.Wn + (int64_t)(h * D + dd) * D + k];
-      c.U[(which == 0 ? c.UL.Ul : c.UL.Ur) + z] = s;
-      continue;
-    }
-    y -= 2 * nUl;
-    if (y < 3 * H) {
-      int which = (int)(y / H), h = (int)(y % H);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nbe = (H * F + 63) / 64, nbl = (H * D + 63) / 64;
+  const int nb_dot = nbe + 2 * nbl;
+  const int nrow = 3 * H + 2 * D;
+  const int nb_row = (nrow + 3) / 4;
+  int b = blockIdx.x;
+  if (b < nb_dot) {
+    int which, o;
+    if (b < nbe) { which = 0; o = b * 64 + lane; }
+    else if (b < nbe + nbl) { which = 1; o = (b - nbe) * 64 + lane; }
+    else { which = 2; o = (b - nbe - nbl) * 64 + lane; }
+    const int n_out = which == 0 ? H * F : H * D;
+    const int W = which == 0 ? F : D;
+    float s = 0.f;
+    if (o < n_out) {
+      const int h = o / W, k = o % W;
       const float* a = P + (which == 0 ? c.L.attn_e : which == 1 ? c.L.attn_l : c.L.attn_r) + h * D;
-      const float* b = P + (which == 0 ? c.L.be : c.L.bn) + h * D;
-      float s = 0.f;
-      for (int dd = 0; dd < D; ++dd) s += a[dd] * b[dd];
-      c.U[(which == 0 ? c.UL.ce : which == 1 ? c.UL.cl : c.UL.cr) + h] = s;
-      continue;
+      const float* M = P + (which == 0 ? c.L.We : c.L.Wn);
+      for (int dd = wv; dd < D; dd += 4) s += a[dd] * M[(int64_t)(h * D + dd) * W + k];
     }
-    y -= 3 * H;
-    if (y < 2 * nP) {
-      int which = (int)(y / nP);
-      int64_t z = y % nP;
-      int dd = (int)(z / D), o = (int)(z % D);
-      c.U[(which == 0 ? c.UL.WsT : c.UL.WdT) + z] = P[(which == 0 ? c.L.Ws : c.L.Wd) + (int64_t)o * D + dd];
-      continue;
+    part[wv][lane] = s;
+    __syncthreads();
+    if (wv == 0 && o < n_out) {
+      const float v = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+      c.U[(which == 0 ? c.UL.Ue : which == 1 ? c.UL.Ul : c.UL.Ur) + o] = v;
     }
-    y -= 2 * nP;
-    {
-      int which = (int)(y / D), o = (int)(y % D);
+    return;
+  }
+  b -= nb_dot;
+  if (b < nb_row) {
+    const int y = b * 4 + wv;
+    if (y >= nrow) return;
+    float s = 0.f;
+    if (y < 3 * H) {
+      const int which = y / H, h = y % H;
+      const float* a = P + (which == 0 ? c.L.attn_e : which == 1 ? c.L.attn_l : c.L.attn_r) + h * D;
+      const float* bb = P + (which == 0 ? c.L.be : c.L.bn) + h * D;
+      for (int dd = lane; dd < D; dd += 64) s += a[dd] * bb[dd];
+      s = wave_sum(s);
+      if (lane == 0) c.U[(which == 0 ? c.UL.ce : which == 1 ? c.UL.cl : c.UL.cr) + h] = s;
+    } else {
+      const int z = y - 3 * H, which = z / D, o = z % D;
       const float* w = P + (which == 0 ? c.L.Ws : c.L.Wd) + (int64_t)o * D;
-      float s = 0.f;
-      for (int dd = 0; dd < D; ++dd) s += w[dd];
-      c.U[(which == 0 ? c.UL.Ws1 : c.UL.Wd1) + o] = s;
+      for (int dd = lane; dd < D; dd += 64) s += w[dd];
+      s = wave_sum(s);
+      if (lane == 0) c.U[(which == 0 ? c.UL.Ws1 : c.UL.Wd1) + o] = s;
     }
+    return;
+  }
+  b -= nb_row;
+  const int64_t nP = (int64_t)D * D;
+  for (int64_t x = (int64_t)b * blockDim.x + threadIdx.x; x < 2 * nP; x += (int64_t)(gridDim.x - nb_dot - nb_row) * blockDim.x) {
+    const int which = (int)(x / nP);
+    const int64_t z = x % nP;
+    const int dd = (int)(z / D), o = (int)(z % D);
+    c.U[(which == 0 ? c.UL.WsT : c.UL.WdT) + z] = P[(which == 0 ? c.L.Ws : c.L.Wd) + (int64_t)o * D + dd];
   }
 }
 
@@ -791,10 +805,23 @@ __global__ void __launch_bounds__(256) tgnn_edge_bwd(Ctx c) {
   }
 #pragma unroll
   for (int h = 0; h < H; ++h) ac[h] = 0.f;
-  for (int e = blockIdx.x * 4 + wv; e < E; e += gridDim.x * 4) {
-    const EdgeMeta m = c.meta[e];
+  const int stride = gridDim.x * 4;
+  int e = blockIdx.x * 4 + wv;
+  EdgeMeta mnext;
+  float dxn[H];
+  if (e < E) {
+    mnext = c.meta[e];
+    load_x8(c.DX + (int64_t)e * H, dxn);
+  }
+  for (; e < E; e += stride) {
+    const EdgeMeta m = mnext;
     float dx[H];
-    load_x8(c.DX + (int64_t)e * H, dx);
+#pragma unroll
+    for (int h = 0; h < H; ++h) dx[h] = dxn[h];
+    if (e + stride < E) {  // one edge ahead: its descriptor and dx load under this edge's math
+      mnext = c.meta[e + stride];
+      load_x8(c.DX + (int64_t)(e + stride) * H, dxn);
+    }
     const float* fp = feat_row(c, m.frow);
     const float* mu = c.mem + m.u * D;
     const uint64_t sk = seg_key(m.blk, m.root);
@@ -862,13 +889,20 @@ __global__ void __launch_bounds__(256) tgnn_edge_bwd(Ctx c) {
   for (int p = threadIdx.x; p < PL.total; p += blockDim.x) slab[p] = red[p];
 }
 
-__global__ void tgnn_grad_reduce(Ctx c, int Ge, int Gs) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= c.PL.total) return;
+// sum the partial slabs: 8 threads per output (lanes 8p..8p+7), fixed order -> deterministic
+__global__ void __launch_bounds__(256) tgnn_grad_reduce(Ctx c, int Ge, int Gs) {
+  const int P = c.PL.total;
+  const int p = (blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+  const int sl = threadIdx.x & 7;
   float s = 0.f;
-  for (int g = 0; g < Ge; ++g) s += c.slabs[(int64_t)g * c.PL.total + p];
-  for (int g = 0; g < Gs; ++g) s += c.slabs_s[(int64_t)g * c.PL.total + p];
-  c.red[p] = s;
+  if (p < P) {
+    for (int g = sl; g < Ge; g += 8) s += c.slabs[(int64_t)g * P + p];
+    for (int g = sl; g < Gs; g += 8) s += c.slabs_s[(int64_t)g * P + p];
+  }
+  s += __shfl_xor(s, 4, 8);
+  s += __shfl_xor(s, 2, 8);
+  s += __shfl_xor(s, 1, 8);
+  if (p < P && sl == 0) c.red[p] = s;
 }
 
 // ------------------------------------------------------------------ predictor (train): one wave per event
@@ -978,8 +1012,9 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
 // predictor weight gradients dWs = Σ_i A_i ⊗ e_s,i and dWd = Σ_i dhp_i ⊗ e_p,i + dhn_i ⊗ e_n,i:
 // AᵀB products over the events, one 16x16 output tile per wave on v_mfma_f32_16x16x4_f32
 // (exact fp32, k-ordered fmaf chain).  Grid: 2 * ceil(D/16)^2 waves.
-__global__ void __launch_bounds__(64) tgnn_pred_reduce_mfma(Ctx c) {
+__global__ void __launch_bounds__(256) tgnn_pred_reduce_mfma(Ctx c) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
+  __shared__ f32x4 part[4][64];
   const int B = (int)c.ctl[TGNX_CTL_B];
   const int D = c.D;
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
@@ -987,7 +1022,7 @@ __global__ void __launch_bounds__(64) tgnn_pred_reduce_mfma(Ctx c) {
   const int nt = (D + 15) / 16;
   const int which = blockIdx.x / (nt * nt);
   const int t = blockIdx.x % (nt * nt), tm = t / nt, tn = t % nt;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int S = 8 * D + 4;
   const int m = tm * 16 + (lane & 15), n = tn * 16 + (lane & 15), kk = lane >> 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -997,14 +1032,24 @@ __global__ void __launch_bounds__(64) tgnn_pred_reduce_mfma(Ctx c) {
     // which 1: pass 0: A = [2D,3D) dhp, B = [3D,4D) e_p ; pass 1: A = [4D,5D) dhn, B = [5D,6D) e_n
     const int ca = which == 0 ? 0 : (pass == 0 ? 2 * D : 4 * D);
     const int cb = which == 0 ? D : (pass == 0 ? 3 * D : 5 * D);
-    for (int i0 = lo; i0 < hi; i0 += 4) {
-      const int i = i0 + kk;
-      const bool in = i < hi;
-      const float a = (in && m < D) ? c.evs[(int64_t)i * S + ca + m] : 0.f;
-      const float b = (in && n < D) ? c.evs[(int64_t)i * S + cb + n] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    // k-steps of 4 events; wave wv takes steps wv, wv+4, ...; 8 steps' loads in flight
+    for (int s0 = lo + 4 * wv; s0 < hi; s0 += 4 * 4 * 8) {
+      float a[8], b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = s0 + 16 * u + kk;
+        const bool in = i < hi;
+        a[u] = (in && m < D) ? c.evs[(int64_t)i * S + ca + m] : 0.f;
+        b[u] = (in && n < D) ? c.evs[(int64_t)i * S + cb + n] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc, 0, 0, 0);
     }
   }
+  part[wv][lane] = acc;
+  __syncthreads();
+  if (wv != 0) return;
+  acc = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
   float* out = c.grads + (which == 0 ? c.L.Ws : c.L.Wd);
   const int col = tn * 16 + (lane & 15);
 #pragma unroll
@@ -1055,21 +1100,8 @@ __global__ void tgnn_grad_expand(Ctx c) {
       g = r[PL.w + (x - L.te_w)];
     } else if (x >= L.te_b && x < L.te_b + D) {
       g = r[PL.b + (x - L.te_b)];
-    } else if ((x >= L.attn_l && x < L.attn_l + H * D) || (x >= L.attn_r && x < L.attn_r + H * D)) {
-      const bool isl = x < L.attn_r;
-      const int j = (int)(x - (isl ? L.attn_l : L.attn_r));
-      const int h = j / D;
-      const float* dU = r + (isl ? PL.Ul : PL.Ur) + h * D;
-      const float* w = P + L.Wn + (int64_t)j * D;
-      for (int k = 0; k < D; ++k) g += w[k] * dU[k];
-      g += P[L.bn + j] * r[(isl ? PL.cl : PL.cr) + h];
-    } else if (x >= L.attn_e && x < L.attn_e + H * D) {
-      const int j = (int)(x - L.attn_e);
-      const int h = j / D;
-      const float* dU = r + PL.Ue + h * F;
-      const float* w = P + L.We + (int64_t)j * F;
-      for (int f = 0; f < F; ++f) g += w[f] * dU[f];
-      g += P[L.be + j] * r[PL.ce + h];
+    } else if (x >= L.attn_l && x < L.Wn) {
+      continue;  // tgnn_grad_attn
     } else if (x >= L.Wn && x < L.Wn + (int64_t)H * D * D) {
       const int64_t y = x - L.Wn;
       const int j = (int)(y / D), k = (int)(y % D), h = j / D;
@@ -1086,6 +1118,35 @@ __global__ void tgnn_grad_expand(Ctx c) {
       g = P[L.attn_e + j] * r[PL.ce + h];
     }
     c.grads[x] = g;
+  }
+}
+
+// d attn_{l,r}[h,d] = W_n[hD+d,:]·dU_{l,r}[h,:] + b_n[hD+d]·dc ; d attn_e likewise with W_e:
+// one wave per output, lanes over the contraction
+__global__ void __launch_bounds__(256) tgnn_grad_attn(Ctx c) {
+  const Lay L = c.L;
+  const PLay PL = c.PL;
+  const int D = c.D, F = c.F;
+  const int y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (y >= 3 * H * D) return;
+  const int which = y / (H * D), j = y % (H * D), h = j / D;
+  const float* P = c.params;
+  const float* r = c.red;
+  float g = 0.f;
+  if (which < 2) {
+    const float* dU = r + (which == 0 ? PL.Ul : PL.Ur) + h * D;
+    const float* w = P + L.Wn + (int64_t)j * D;
+    for (int k = lane; k < D; k += 64) g += w[k] * dU[k];
+  } else {
+    const float* dU = r + PL.Ue + h * F;
+    const float* w = P + L.We + (int64_t)j * F;
+    for (int f = lane; f < F; f += 64) g += w[f] * dU[f];
+  }
+  g = wave_sum(g);
+  if (lane == 0) {
+    if (which == 0) c.grads[L.attn_l + j] = g + P[L.bn + j] * r[PL.cl + h];
+    else if (which == 1) c.grads[L.attn_r + j] = g + P[L.bn + j] * r[PL.cr + h];
+    else c.grads[L.attn_e + j] = g + P[L.be + j] * r[PL.ce + h];
   }
 }
 
@@ -1411,25 +1472,33 @@ static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
   TGNX_LAUNCH_CHECK("tgnn_seg_count");
   tgnn_seg_scan<<<1, 1024, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgnn_seg_scan");
+  probe_begin(TGNX_K_EDGE_META, s);
   tgnn_edge_meta<TRAIN><<<edge_grid(c.Ecap) / 4 + 1, 256, 0, s>>>(c);
+  probe_end(TGNX_K_EDGE_META, s);
   TGNX_LAUNCH_CHECK("tgnn_edge_meta");
-  tgnn_collapse<<<256, 256, 0, s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_collapse");
-  const int pid = TRAIN ? TGNX_K_ATTN_FWD : TGNX_K_ATTN_FWD_EVAL;
-  probe_begin(pid, s);
+  {
+    const int nb = (H * c.F + 63) / 64 + 2 * ((H * c.D + 63) / 64) + (3 * H + 2 * c.D + 3) / 4 + 64;
+    tgnn_collapse<<<nb, 256, 0, s>>>(c);
+    TGNX_LAUNCH_CHECK("tgnn_collapse");
+  }
+  probe_begin(TGNX_K_EDGE_FWD, s);
   tgnn_edge_fwd<<<edge_grid(c.Ecap), 256, 0, s>>>(c);
+  probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgnn_edge_fwd");
+  probe_begin(TGNX_K_SEG_FWD, s);
   tgnn_seg_fwd<TRAIN><<<grid_for(Scap, 4), 256, 0, s>>>(c);
-  probe_end(pid, s);
+  probe_end(TGNX_K_SEG_FWD, s);
   TGNX_LAUNCH_CHECK("tgnn_seg_fwd");
   return TGNX_OK;
 }
 
 static int launch_backward(const Ctx& c, hipStream_t s) {
   const size_t shm = (size_t)c.PL.total * 4;
-  probe_begin(TGNX_K_ATTN_BWD, s);
+  probe_begin(TGNX_K_SEG_BWD, s);
   tgnn_seg_bwd<<<GSEG, 256, shm, s>>>(c);
+  probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgnn_seg_bwd");
+  probe_begin(TGNX_K_EDGE_BWD, s);
   const int FD = c.F + c.D;
   if (FD <= 64) tgnn_edge_bwd<1><<<GBWD, 256, shm, s>>>(c);
   else if (FD <= 128) tgnn_edge_bwd<2><<<GBWD, 256, shm, s>>>(c);
@@ -1438,9 +1507,9 @@ static int launch_backward(const Ctx& c, hipStream_t s) {
   else if (FD <= 320) tgnn_edge_bwd<5><<<GBWD, 256, shm, s>>>(c);
   else if (FD <= 384) tgnn_edge_bwd<6><<<GBWD, 256, shm, s>>>(c);
   else tgnn_edge_bwd<7><<<GBWD, 256, shm, s>>>(c);
-  probe_end(TGNX_K_ATTN_BWD, s);
+  probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgnn_edge_bwd");
-  tgnn_grad_reduce<<<grid_for(c.PL.total, 256), 256, 0, s>>>(c, GBWD, GSEG);
+  tgnn_grad_reduce<<<grid_for((int64_t)c.PL.total * 8, 256), 256, 0, s>>>(c, GBWD, GSEG);
   TGNX_LAUNCH_CHECK("tgnn_grad_reduce");
   return TGNX_OK;
 }
@@ -1504,15 +1573,17 @@ int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers
   TGNX_LAUNCH_CHECK("tgnn_pred_train");
   {
     const int nt = (c.D + 15) / 16;
-    tgnn_pred_reduce_mfma<<<2 * nt * nt, 64, 0, s>>>(c);
+    tgnn_pred_reduce_mfma<<<2 * nt * nt, 256, 0, s>>>(c);
     TGNX_LAUNCH_CHECK("tgnn_pred_reduce_mfma");
     tgnn_pred_reduce_vec<<<grid_for(3 * c.D + 2, 4), 256, 0, s>>>(c);
     TGNX_LAUNCH_CHECK("tgnn_pred_reduce_vec");
   }
   rc = launch_backward(c, s);
   if (rc) return rc;
-  tgnn_grad_expand<<<grid_for(c.L.Ws, 256), 256, 0, s>>>(c);
+  tgnn_grad_expand<<<grid_for(c.L.Ws, 256) < 2048 ? grid_for(c.L.Ws, 256) : 2048, 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgnn_grad_expand");
+  tgnn_grad_attn<<<grid_for(3 * H * c.D, 4), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgnn_grad_attn");
   return TGNX_OK;
 }
 
