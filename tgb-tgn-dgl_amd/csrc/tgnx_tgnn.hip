@@ -184,12 +184,12 @@ __device__ __forceinline__ float ta_at(const Ctx& c, int64_t u, int blk, int gen
         if (kblk(c.touches[mid]) <= blk) lo = mid + 1; else hi = mid;
       }
       if (lo > inf.y) return evt[kev(c.touches[lo - 1])];
-    } else {      // eval: time_assoc[:] = max(t_blk), then s/p of the block
-      while (lo < hi) {
+    } else {      // eval: time_assoc[:] = max(t_blk), then p then s of the block, in batch order
+      while (lo < hi) {  // last touch with block <= blk (blocks from the val/test swap may repeat a node)
         int mid = (lo + hi) >> 1;
-        if (kblk(c.touches[mid]) < blk) lo = mid + 1; else hi = mid;
+        if (kblk(c.touches[mid]) <= blk) lo = mid + 1; else hi = mid;
       }
-      if (lo < inf.y + inf.z && kblk(c.touches[lo]) == blk) return evt[kev(c.touches[lo])];
+      if (lo > inf.y && kblk(c.touches[lo - 1]) == blk) return evt[kev(c.touches[lo - 1])];
       return c.blkmax[blk];
     }
   }

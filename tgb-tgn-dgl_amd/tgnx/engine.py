@@ -103,8 +103,9 @@ class TgnnEngine:
         f = lambda x, dt: torch.as_tensor(x).to(dev, dt, non_blocking=True).contiguous()  # noqa: E731
         return f(src, torch.long), f(dst, torch.long), f(t, torch.float32), f(msg, torch.float32), f(blk, torch.long)
 
-    def train_batch(self, src, dst, t, msg, blk, neg=None, dropout=True):
-        """One train iteration on an explicit batch (epoch_utils.py:194-304)."""
+    def train_batch(self, src, dst, t, msg, blk, neg=None, dropout=True, update=True):
+        """One train iteration on an explicit batch (epoch_utils.py:194-304).  update=False stops
+        after the gradients (no all-reduce, no Adam, no ring insert): see apply_update()."""
         dev = self.dev
         src, dst, t, msg, blk = self._dev_batch(dev, src, dst, t, msg, blk)
         B = int(src.numel())
@@ -117,11 +118,19 @@ class TgnnEngine:
         buf = self._buffers(src, dst, t, blk, msg, neg)
         _lib.call("tgnx_tgnn_train_fwd_bwd", ctypes.byref(self.cfg), ctypes.byref(buf), 1 if gen_neg else 0,
                   1 if (dropout and self.model.training) else 0, self._stream())
-        self._allreduce_grads()
+        self._keep = (src, dst, t, msg, blk, neg)   # keep alive until the stream consumes them
+        self._pending = (buf, B)
+        if update:
+            self.apply_update()
+        return self.out_pos[:B], self.out_neg[:B], neg
+
+    def apply_update(self, allreduce=True):
+        """All-reduce (world > 1), Adam, ring insert + time_assoc for the last train_batch."""
+        buf, B = self._pending
+        if allreduce:
+            self._allreduce_grads()
         _lib.call("tgnx_tgnn_train_update", ctypes.byref(self.cfg), ctypes.byref(buf), self._stream())
         self.loader.cur_e_id += B
-        self._keep = (src, dst, t, msg, blk, neg)   # keep alive until the stream consumes them
-        return self.out_pos[:B], self.out_neg[:B], neg
 
     def eval_batch(self, src, dst, t, msg, blk, neg2d, tile_quirk=True):
         """One eval iteration (epoch_utils.py:28-157); returns (pos[B], neg[B,K'], mrr) in block order."""
