@@ -90,6 +90,7 @@ def main():
     ap.add_argument("--no-dropout", action="store_true", help="train mode without dropout (reference epochs >= 2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--probe-steps", type=int, default=100)
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,11 +127,17 @@ def main():
                       dropout=not args.no_dropout)
     nb_epoch = math.ceil(stream.train_end / Bg)
     counter = {"i": 0}
+    use_graph = not args.no_graph
+    if use_graph:
+        eng.capture_resident(1)
 
-    def step():
+    def step(eager=False):
         if counter["i"] % nb_epoch == 0:
             eng.begin_epoch()
-        eng.resident_train_step()
+        if use_graph and not eager:
+            eng.replay_resident()
+        else:
+            eng.resident_train_step()
         counter["i"] += 1
 
     def barrier():
@@ -165,7 +172,7 @@ def main():
         _lib.call("tgnx_probe_enable", kid)
         pe0, ps0 = eng.units()
         for _ in range(args.probe_steps):
-            step()
+            step(eager=True)          # probes record events around eager launches
         barrier()
         ms, n = ctypes.c_double(), ctypes.c_int64()
         _lib.call("tgnx_probe_read", ctypes.byref(ms), ctypes.byref(n))
@@ -214,6 +221,7 @@ def main():
                                    f"batch {args.batch}/GPU, {K} temporal neighbours, H=8, D=100, d={d}, "
                                    f"dropout {'off' if args.no_dropout else '0.6 (epoch-1)'}",
                        "global_batch": Bg, "parallelism": f"dp{world}",
+                       "launch": "hip-graph replay per step" if use_graph else "eager",
                        "edges_per_step": round((e1 - e0) / args.steps / world, 1),
                        "blocks_per_batch_mean": float(np.mean([blk[i:i + Bg].max() + 1
                                                                for i in range(0, stream.train_end, Bg)]))},

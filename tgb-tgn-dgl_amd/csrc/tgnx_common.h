@@ -112,6 +112,25 @@ __device__ __forceinline__ void bitonic_sort_u64(uint64_t* key, int n) {
   }
 }
 
+// Sort n distinct uint64 keys in LDS, ascending, by the whole block: barrier-free rank sort
+// (each key's slot = number of smaller keys) for n <= 1024, bitonic above.  `tmp` holds n keys.
+__device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, int n_pow2) {
+  if (n <= 1024) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) tmp[i] = key[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint64_t k = tmp[i];
+      int r = 0;
+      for (int j = 0; j < n; ++j) r += tmp[j] < k;
+      key[r] = k;
+    }
+    for (int i = n + threadIdx.x; i < n_pow2; i += blockDim.x) key[i] = ~0ull;
+    __syncthreads();
+  } else {
+    bitonic_sort_u64(key, n_pow2);
+  }
+}
+
 __host__ __device__ __forceinline__ int next_pow2(int v) {
   int p = 1;
   while (p < v) p <<= 1;

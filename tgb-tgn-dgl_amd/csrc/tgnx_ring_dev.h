@@ -34,7 +34,7 @@ __device__ __forceinline__ void ring_insert_block(int64_t* __restrict__ nbr, int
     key[p] = k;
   }
   __syncthreads();
-  bitonic_sort_u64(key, n);
+  sort_u64(key, reinterpret_cast<uint64_t*>(run_start + n2 + (n2 & 1)), n2, n);
   // run starts -> run ids
   const int T = blockDim.x;
   int pc = (n2 + T - 1) / T;
@@ -90,7 +90,8 @@ __device__ __forceinline__ void ring_insert_block(int64_t* __restrict__ nbr, int
 }
 
 __host__ __device__ __forceinline__ size_t ring_insert_smem_bytes(int B) {
-  return (size_t)next_pow2(2 * B) * 8 + (size_t)2 * B * 4;
+  // keys + run starts (+ rank-sort scratch for 2B <= 1024)
+  return (size_t)next_pow2(2 * B) * 8 + (size_t)(2 * B + 2) * 4 + (2 * B <= 1024 ? (size_t)2 * B * 8 : 0);
 }
 
 }  // namespace tgnx

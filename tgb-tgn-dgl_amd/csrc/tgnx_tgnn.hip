@@ -108,7 +108,7 @@ struct __attribute__((aligned(16))) EdgeMeta {
 // ------------------------------------------------------------------ context
 struct Ctx {
   int64_t N;
-  int K, D, d, F, Kn, drop, quirk;
+  int K, D, d, F, Kn, drop, quirk, gen_neg;
   float pf, pa, inv_kf, inv_ka;
   float lr, b1, b2, eps;
   const int64_t *ev_src, *ev_dst;
@@ -167,10 +167,30 @@ __device__ __forceinline__ uint64_t mkkey(int64_t node, int blk, int kind, int e
 }
 
 __device__ __forceinline__ float keepf(uint64_t h, float p, float inv) { return u01(h) >= p ? inv : 0.0f; }
-__device__ __forceinline__ float node_keep(const Ctx& c, uint64_t seed, int blk, int64_t u, int dd) {
-  return keepf(hash4(seed, 1, ((uint64_t)blk << 32) ^ (uint64_t)u, (uint64_t)dd), c.pf, c.inv_kf);
-}
 __device__ __forceinline__ uint64_t seg_key(int blk, int64_t root) { return ((uint64_t)blk << 32) ^ (uint64_t)root; }
+// Dropout masks: a 64-bit base per (batch seed, stream, key) computed once per edge / node, then
+// a 32-bit murmur finaliser per element.  Forward and backward call the same functions, and
+// duplicate (block, root) segments share keys, as the reference draws one mask per block.
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t drop_base(uint64_t seed, uint64_t stream, uint64_t key, uint64_t sub) {
+  return (uint32_t)hash4(seed, stream, key, sub);
+}
+__device__ __forceinline__ float keep32(uint32_t base, uint32_t idx, float p, float inv) {
+  const uint32_t h = fmix32(base ^ (idx * 0x9E3779B9u));
+  return (float)(h >> 8) * (1.0f / 16777216.0f) >= p ? inv : 0.0f;
+}
+__device__ __forceinline__ uint32_t node_base(uint64_t seed, int blk, int64_t u) {
+  return drop_base(seed, 1, ((uint64_t)blk << 32) ^ (uint64_t)u, 0);
+}
+__device__ __forceinline__ float node_keep(const Ctx& c, uint64_t seed, int blk, int64_t u, int dd) {
+  return keep32(node_base(seed, blk, u), (uint32_t)dd, c.pf, c.inv_kf);
+}
+// edge feature mask base (stream 2) and attention mask base (stream 3) of edge o of a segment
+__device__ __forceinline__ uint32_t efeat_base(uint64_t seed, uint64_t sk, int o) { return drop_base(seed, 2, sk, (uint64_t)o); }
+__device__ __forceinline__ uint32_t attn_base(uint64_t seed, uint64_t sk, int o) { return drop_base(seed, 3, sk, (uint64_t)o); }
 
 // time_assoc[u] as of block `blk` of the current batch (model_utils.py:77-83)
 template <bool TRAIN>
@@ -216,24 +236,6 @@ __global__ void tgnn_advance(int64_t* ctl, int mode, int64_t batch_start, int64_
   ctl[TGNX_CTL_LO] = Bv * rank / world;
   ctl[TGNX_CTL_HI] = Bv * (rank + 1) / world;
   ctl[TGNX_CTL_SEED] = (int64_t)(mix64(base_seed ^ mix64((uint64_t)ctl[TGNX_CTL_NB])) >> 1);
-}
-
-__global__ void tgnn_negs(Ctx c) {
-  const int64_t B = c.ctl[TGNX_CTL_B];
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= B) return;
-  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
-  const int64_t p = c.ev_dst[start + i];
-  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-  const uint64_t off = (uint64_t)c.ctl[TGNX_CTL_CUR_EID] + (uint64_t)i;
-  int64_t v = c.dst_nodes[0];
-  for (uint64_t attempt = 0; attempt < 64; ++attempt) {
-    uint64_t h = hash4(seed, 0x6E656773ull, off, attempt);
-    uint64_t r = (uint64_t)(((__uint128_t)(h >> 11) * (uint64_t)c.n_dst) >> 53);
-    v = c.dst_nodes[r];
-    if (v != p) break;
-  }
-  c.neg[start + i] = v;
 }
 
 // U = attn·W per head (exact collapse of EdgeGATConv's el/er/ee), predictor transposes/row sums.
@@ -305,6 +307,60 @@ __global__ void __launch_bounds__(256) tgnn_collapse(Ctx c) {
   }
 }
 
+// ------------------------------------------------------------------ segment geometry
+// Segment w (this rank's rows): [0, nloc) src rows, [nloc, 2 nloc) dst rows, then neg rows.
+struct Seg {
+  int kind, i, cc, blk;
+  int64_t root;
+};
+__device__ __forceinline__ bool seg_of(const Ctx& c, int w, int lo, int hi, int64_t start, Seg& s) {
+  const int nloc = hi - lo;
+  const int Kn = c.Kn;
+  if (w < 0 || w >= nloc * (2 + Kn)) return false;
+  if (w < nloc) {
+    s.kind = 2; s.i = lo + w; s.cc = 0;
+  } else if (w < 2 * nloc) {
+    s.kind = 1; s.i = lo + w - nloc; s.cc = 0;
+  } else {
+    const int q = w - 2 * nloc;
+    s.kind = 0; s.i = lo + q / Kn; s.cc = q % Kn;
+  }
+  s.root = s.kind == 2 ? c.ev_src[start + s.i] : s.kind == 1 ? c.ev_dst[start + s.i]
+                                                             : c.neg[(start + s.i) * Kn + s.cc];
+  s.blk = (int)c.ev_blk[start + s.i];
+  return true;
+}
+
+// in-edge count of a segment: ring row + self loop + intra-batch edges of earlier blocks
+// (returned packed: nring | nintra << 8)
+__device__ __forceinline__ int seg_count_one(const Ctx& c, int w, int lo, int hi, int64_t start, int gen) {
+  Seg s;
+  seg_of(c, w, lo, hi, start, s);
+  int nring = 0;
+  for (int j = 0; j < c.K; ++j) nring += c.eid[s.root * c.K + j] >= 0;
+  int nintra = 0;
+  const int4 inf = c.nodemap[s.root];
+  if (inf.x == gen) {
+    int a = inf.w, z = c.sp_pref[inf.y + inf.z];
+    const int base = a;
+    while (a < z) {
+      const int mid = (a + z) >> 1;
+      if (kblk(c.sp_keys[mid]) < s.blk) a = mid + 1; else z = mid;
+    }
+    nintra = a - base;
+  }
+  return nring | (nintra << 8);
+}
+
+__global__ void tgnn_seg_count(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int S = (int)c.ctl[TGNX_CTL_S];
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (B == 0 || w >= S || c.ctl[TGNX_CTL_ERR] != 0 || c.ctl[TGNX_CTL_E] >= 0) return;  // E >= 0: done in assemble
+  c.seg_cnt[w] = seg_count_one(c, w, (int)c.ctl[TGNX_CTL_LO], (int)c.ctl[TGNX_CTL_HI],
+                               c.ctl[TGNX_CTL_BATCH_START], (int)c.ctl[TGNX_CTL_GEN]);
+}
+
 // ------------------------------------------------------------------ assembly (one workgroup)
 // Sorts the batch's node touches (src / dst / neg rows) by (node, block, kind, event), builds the
 // node map {gen, run start, run length, first s/p index}, the compacted s/p touch list (the
@@ -334,6 +390,22 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   const int n = next_pow2(NT);
   uint64_t* key = reinterpret_cast<uint64_t*>(smem);
   int* run_start = reinterpret_cast<int*>(smem + (size_t)TOUCH_MAX * 8);
+  uint64_t* tmp = reinterpret_cast<uint64_t*>(smem + (size_t)TOUCH_MAX * 12);
+  if (TRAIN && c.gen_neg) {  // NegLinkSamplerDest.sample (neg_sampler.py:8-23), counter-based stream
+    const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+    const uint64_t off = (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
+    for (int i = tid; i < B; i += T) {
+      const int64_t pd = dst[i];
+      int64_t v = c.dst_nodes[0];
+      for (uint64_t attempt = 0; attempt < 64; ++attempt) {
+        const uint64_t h = hash4(seed, 0x6E656773ull, off + (uint64_t)i, attempt);
+        v = c.dst_nodes[(uint64_t)(((__uint128_t)(h >> 11) * (uint64_t)c.n_dst) >> 53)];
+        if (v != pd) break;
+      }
+      c.neg[start + i] = v;
+    }
+    __syncthreads();
+  }
   for (int p = tid; p < n; p += T) {
     uint64_t k = ~0ull;
     if (p < NT) {
@@ -344,7 +416,7 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     key[p] = k;
   }
   __syncthreads();
-  bitonic_sort_u64(key, n);
+  sort_u64(key, tmp, NT, n);
   const int pc = (NT + T - 1) / T;
   const int p0 = tid * pc, p1 = min(NT, p0 + pc);
   // compacted s/p list (kind != 0), exclusive prefix over the sorted touches
@@ -384,73 +456,50 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   const int nb = next_pow2(B);
   for (int p = tid; p < nb; p += T) key[p] = p < B ? (((uint64_t)blk[p] << 12) | (uint64_t)p) : ~0ull;
   __syncthreads();
-  bitonic_sort_u64(key, nb);
+  sort_u64(key, tmp, B, nb);
   for (int r = tid; r < B; r += T) {
     const int e = (int)(key[r] & 4095u);
     c.blk_rank[e] = r;
     c.blk_order[r] = e;
   }
-  if (tid == 0) {
-    const int nloc = (int)(c.ctl[TGNX_CTL_HI] - c.ctl[TGNX_CTL_LO]);
-    c.ctl[TGNX_CTL_S] = (int64_t)nloc * (2 + c.Kn);
-  }
-}
-
-// ------------------------------------------------------------------ segment geometry
-// Segment w (this rank's rows): [0, nloc) src rows, [nloc, 2 nloc) dst rows, then neg rows.
-struct Seg {
-  int kind, i, cc, blk;
-  int64_t root;
-};
-__device__ __forceinline__ bool seg_of(const Ctx& c, int w, int lo, int hi, int64_t start, Seg& s) {
-  const int nloc = hi - lo;
-  const int Kn = c.Kn;
-  if (w < 0 || w >= nloc * (2 + Kn)) return false;
-  if (w < nloc) {
-    s.kind = 2; s.i = lo + w; s.cc = 0;
-  } else if (w < 2 * nloc) {
-    s.kind = 1; s.i = lo + w - nloc; s.cc = 0;
-  } else {
-    const int q = w - 2 * nloc;
-    s.kind = 0; s.i = lo + q / Kn; s.cc = q % Kn;
-  }
-  s.root = s.kind == 2 ? c.ev_src[start + s.i] : s.kind == 1 ? c.ev_dst[start + s.i]
-                                                             : c.neg[(start + s.i) * Kn + s.cc];
-  s.blk = (int)c.ev_blk[start + s.i];
-  return true;
-}
-
-// in-edge count of every segment: ring row + self loop + intra-batch edges of earlier blocks
-__global__ void tgnn_seg_count(Ctx c) {
-  const int B = (int)c.ctl[TGNX_CTL_B];
-  const int S = (int)c.ctl[TGNX_CTL_S];
-  const int w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (B == 0 || w >= S || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
-  const int gen = (int)c.ctl[TGNX_CTL_GEN];
-  Seg s;
-  seg_of(c, w, (int)c.ctl[TGNX_CTL_LO], (int)c.ctl[TGNX_CTL_HI], start, s);
-  int nring = 0;
-  for (int j = 0; j < c.K; ++j) nring += c.eid[s.root * c.K + j] >= 0;
-  int nintra = 0;
-  const int4 inf = c.nodemap[s.root];
-  if (inf.x == gen) {
-    int lo = inf.w, hi = c.sp_pref[inf.y + inf.z];
-    const int base = lo;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (kblk(c.sp_keys[mid]) < s.blk) lo = mid + 1; else hi = mid;
+  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
+  const int S = (hi - lo) * (2 + c.Kn);
+  if (TRAIN) {  // segments are few (3 per event): counts + offsets here, no extra launches
+    __syncthreads();
+    const int chunk = (S + T - 1) / T;
+    const int r0 = tid * chunk, r1 = min(S, r0 + chunk);
+    int s = 0;
+    for (int r = r0; r < r1; ++r) {
+      const int v = seg_count_one(c, r, lo, hi, start, gen);
+      c.seg_cnt[r] = v;
+      s += (v & 255) + 1 + (v >> 8);
     }
-    nintra = lo - base;
+    int tot;
+    int base = block_excl_scan(s, sh, &tot);
+    for (int r = r0; r < r1; ++r) {
+      c.seg_eoff[r] = base;
+      const int v = c.seg_cnt[r];
+      base += (v & 255) + 1 + (v >> 8);
+    }
+    if (tid == 0) {
+      c.seg_eoff[S] = tot;
+      c.ctl[TGNX_CTL_S] = S;
+      c.ctl[TGNX_CTL_E] = tot;
+      c.ctl[TGNX_CTL_SUM_E] += tot;
+      c.ctl[TGNX_CTL_SUM_S] += S;
+      if (tot > c.Ecap) c.ctl[TGNX_CTL_ERR] |= 2;
+    }
+  } else if (tid == 0) {
+    c.ctl[TGNX_CTL_S] = S;
+    c.ctl[TGNX_CTL_E] = -1;   // counted by tgnn_seg_count / tgnn_seg_scan
   }
-  c.seg_cnt[w] = nring | (nintra << 8);
 }
 
 // exclusive scan of the edge counts (one workgroup) -> edge offsets
 __global__ void __launch_bounds__(1024) tgnn_seg_scan(Ctx c) {
   __shared__ int sh[20];
   const int B = (int)c.ctl[TGNX_CTL_B];
-  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0 || c.ctl[TGNX_CTL_E] >= 0) return;
   const int S = (int)c.ctl[TGNX_CTL_S];
   const int T = blockDim.x;
   const int chunk = (S + T - 1) / T;
@@ -529,7 +578,19 @@ __device__ __forceinline__ const float* feat_row(const Ctx& c, int64_t frow) {
   return frow >= 0 ? c.feat + frow * c.d : frow == -1 ? nullptr : c.ev_msg + (-(frow + 2)) * c.d;
 }
 
-// x_eh = U_e[h]·efeat_e + U_l[h]·drop(mem[src]) + c : 16 lanes per edge, U staged in LDS [dim][head]
+// x_eh = U_e[h]·efeat_e + U_l[h]·drop(mem[src]) + c : 16 lanes per edge, U staged in LDS [dim][head].
+// Gathers (feature row dims [0,d), memory row dims [F, F+D)) are issued before any math; the
+// time-encoding dims [d, F) need no gather and run in a rolled loop (cosf is long).
+constexpr int NFEAT16 = (FMAX - DMAX + 15) / 16 + 1;  // feature values per lane (d <= FMAX - D)
+constexpr int NMEM16 = DMAX / 16;                     // memory values per lane
+
+__device__ __forceinline__ void fma8(float (&acc)[H], const float* us, float x) {
+  const float4 u0 = *reinterpret_cast<const float4*>(us);
+  const float4 u1 = *reinterpret_cast<const float4*>(us + 4);
+  acc[0] += u0.x * x; acc[1] += u0.y * x; acc[2] += u0.z * x; acc[3] += u0.w * x;
+  acc[4] += u1.x * x; acc[5] += u1.y * x; acc[6] += u1.z * x; acc[7] += u1.w * x;
+}
+
 __global__ void __launch_bounds__(256) tgnn_edge_fwd(Ctx c) {
   __shared__ __attribute__((aligned(16))) float Us[(FMAX + DMAX) * H];
   __shared__ float Tw[DMAX], Tb[DMAX];
@@ -556,32 +617,53 @@ __global__ void __launch_bounds__(256) tgnn_edge_fwd(Ctx c) {
     const EdgeMeta m = c.meta[e];
     const float* fp = feat_row(c, m.frow);
     const float* mu = c.mem + m.u * D;
-    const uint64_t sk = seg_key(m.blk, m.root);
+    float vf[NFEAT16], vm[NMEM16];
+#pragma unroll
+    for (int j = 0; j < NFEAT16; ++j) {
+      const int f = sub + 16 * j;
+      vf[j] = f < d ? (fp ? fp[f] : 1.0f) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NMEM16; ++j) {
+      const int k = sub + 16 * j;
+      vm[j] = k < D ? mu[k] : 0.f;
+    }
+    const uint32_t eb = drop ? efeat_base(seed, seg_key(m.blk, m.root), m.o) : 0u;
+    const uint32_t nb = drop ? node_base(seed, m.blk, m.u) : 0u;
     float acc[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) acc[h] = 0.f;
-    for (int f = sub; f < FD; f += 16) {
-      float v;
-      if (f < d) v = fp ? fp[f] : 1.0f;
-      else if (f < F) v = cosf(fmaf(Tw[f - d], m.dt, Tb[f - d]));
-      else v = mu[f - F];
-      if (drop) {
-        v *= f < F ? keepf(hash4(seed, 2, sk, ((uint64_t)m.o << 16) | (uint64_t)f), c.pf, c.inv_kf)
-                   : node_keep(c, seed, m.blk, m.u, f - F);
+    for (int f = d + sub; f < F; f += 16) {  // time encoding (model_utils.py:235, :447)
+      float x = cosf(fmaf(Tw[f - d], m.dt, Tb[f - d]));
+      if (drop) x *= keep32(eb, (uint32_t)f, c.pf, c.inv_kf);
+      fma8(acc, &Us[f * H], x);
+    }
+#pragma unroll
+    for (int j = 0; j < NFEAT16; ++j) {
+      const int f = sub + 16 * j;
+      if (f < d) {
+        float x = vf[j];
+        if (drop) x *= keep32(eb, (uint32_t)f, c.pf, c.inv_kf);
+        fma8(acc, &Us[f * H], x);
       }
-      const float4 u0 = *reinterpret_cast<const float4*>(&Us[f * H]);
-      const float4 u1 = *reinterpret_cast<const float4*>(&Us[f * H + 4]);
-      acc[0] += u0.x * v; acc[1] += u0.y * v; acc[2] += u0.z * v; acc[3] += u0.w * v;
-      acc[4] += u1.x * v; acc[5] += u1.y * v; acc[6] += u1.z * v; acc[7] += u1.w * v;
+    }
+#pragma unroll
+    for (int j = 0; j < NMEM16; ++j) {
+      const int k = sub + 16 * j;
+      if (k < D) {
+        float x = vm[j];
+        if (drop) x *= keep32(nb, (uint32_t)k, c.pf, c.inv_kf);
+        fma8(acc, &Us[(F + k) * H], x);
+      }
     }
 #pragma unroll
     for (int h = 0; h < H; ++h) {
-      float v = acc[h];
-      v += __shfl_xor(v, 8, 16);
-      v += __shfl_xor(v, 4, 16);
-      v += __shfl_xor(v, 2, 16);
-      v += __shfl_xor(v, 1, 16);
-      acc[h] = v + cst[h];
+      float x = acc[h];
+      x += __shfl_xor(x, 8, 16);
+      x += __shfl_xor(x, 4, 16);
+      x += __shfl_xor(x, 2, 16);
+      x += __shfl_xor(x, 1, 16);
+      acc[h] = x + cst[h];
     }
     if (sub == 0) {
       float4* xp = reinterpret_cast<float4*>(c.X + (int64_t)e * H);
@@ -647,6 +729,7 @@ __global__ void __launch_bounds__(256) tgnn_seg_fwd(Ctx c) {
     const bool ok = o < ne;
     float x[H];
     if (ok) load_x8(c.X + (int64_t)(e0 + o) * H, x);
+    const uint32_t ab = drop ? attn_base(seed, sk, o) : 0u;
 #pragma unroll
     for (int h = 0; h < H; ++h) {
       float sc = -INFINITY;
@@ -657,7 +740,7 @@ __global__ void __launch_bounds__(256) tgnn_seg_fwd(Ctx c) {
       const float mn = fmaxf(m[h], wave_max(sc));
       const float ex = ok ? expf(sc - mn) : 0.f;
       float wgt = ex;
-      if (drop && ok) wgt *= keepf(hash4(seed, 3, sk, ((uint64_t)o << 16) | (uint64_t)h), c.pa, c.inv_ka);
+      if (drop && ok) wgt *= keep32(ab, (uint32_t)h, c.pa, c.inv_ka);
       const float r = expf(m[h] - mn);
       l[h] = l[h] * r + wave_sum(ex);
       acc[h] = acc[h] * r + wave_sum(ok ? wgt * x[h] : 0.f);
@@ -723,6 +806,7 @@ __global__ void __launch_bounds__(256) tgnn_seg_bwd(Ctx c) {
       const bool ok = o < ne;
       float x[H], dx[H];
       if (ok) load_x8(c.X + (int64_t)(e0 + o) * H, x);
+      const uint32_t ab = drop ? attn_base(seed, sk, o) : 0u;
 #pragma unroll
       for (int h = 0; h < H; ++h) {
         float ds = 0.f;
@@ -732,7 +816,7 @@ __global__ void __launch_bounds__(256) tgnn_seg_bwd(Ctx c) {
           const float lk = sc > 0.f ? 1.f : 0.2f;
           sc = sc > 0.f ? sc : 0.2f * sc;
           const float a = expf(sc - m[h]) / l[h];
-          const float mk = drop ? keepf(hash4(seed, 3, sk, ((uint64_t)o << 16) | (uint64_t)h), c.pa, c.inv_ka) : 1.f;
+          const float mk = drop ? keep32(ab, (uint32_t)h, c.pa, c.inv_ka) : 1.f;
           ds = a * gh * (x[h] * mk - ft[h]) * lk;
           dx[h] = gh * a * mk + ds;
         }
@@ -778,8 +862,13 @@ __global__ void __launch_bounds__(256) tgnn_seg_bwd(Ctx c) {
 template <int NJ>
 __global__ void __launch_bounds__(256) tgnn_edge_bwd(Ctx c) {
   extern __shared__ __attribute__((aligned(16))) float red[];
+  __shared__ __attribute__((aligned(16))) float Uenc[DMAX * H];   // U_e[h][d + k] as [k][h]
   const PLay PL = c.PL;
   for (int p = threadIdx.x; p < PL.total; p += blockDim.x) red[p] = 0.f;
+  for (int x = threadIdx.x; x < c.D * H; x += blockDim.x) {
+    const int k = x / H, h = x % H;
+    Uenc[x] = c.U[c.UL.Ue + h * c.F + c.d + k];
+  }
   __syncthreads();
   const int B = (int)c.ctl[TGNX_CTL_B];
   const bool okb = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
@@ -788,76 +877,85 @@ __global__ void __launch_bounds__(256) tgnn_edge_bwd(Ctx c) {
   const int F = c.F, D = c.D, d = c.d, FD = F + D;
   const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
   const bool drop = c.drop;
-  float ue[NJ][H], tw[NJ], tb[NJ];
+  float tw[NJ], tb[NJ];
   float aU[NJ][H], aw[NJ], ab[NJ], ac[H];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int f = lane + 64 * j;
     const bool enc = f >= d && f < F;
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-      ue[j][h] = enc ? c.U[c.UL.Ue + h * F + f] : 0.f;
-      aU[j][h] = 0.f;
-    }
+    for (int h = 0; h < H; ++h) aU[j][h] = 0.f;
     tw[j] = enc ? c.params[c.L.te_w + f - d] : 0.f;
     tb[j] = enc ? c.params[c.L.te_b + f - d] : 0.f;
     aw[j] = ab[j] = 0.f;
   }
 #pragma unroll
   for (int h = 0; h < H; ++h) ac[h] = 0.f;
+  constexpr int NE = 2;  // edges in flight per wave
   const int stride = gridDim.x * 4;
-  int e = blockIdx.x * 4 + wv;
-  EdgeMeta mnext;
-  float dxn[H];
-  if (e < E) {
-    mnext = c.meta[e];
-    load_x8(c.DX + (int64_t)e * H, dxn);
-  }
-  for (; e < E; e += stride) {
-    const EdgeMeta m = mnext;
-    float dx[H];
+  for (int e0 = blockIdx.x * 4 + wv; e0 < E; e0 += NE * stride) {
+    EdgeMeta m[NE];
+    float dx[NE][H];
+    float v[NE][NJ];
 #pragma unroll
-    for (int h = 0; h < H; ++h) dx[h] = dxn[h];
-    if (e + stride < E) {  // one edge ahead: its descriptor and dx load under this edge's math
-      mnext = c.meta[e + stride];
-      load_x8(c.DX + (int64_t)(e + stride) * H, dxn);
-    }
-    const float* fp = feat_row(c, m.frow);
-    const float* mu = c.mem + m.u * D;
-    const uint64_t sk = seg_key(m.blk, m.root);
+    for (int k = 0; k < NE; ++k) {
+      const int e = e0 + k * stride;
+      if (e < E) {
+        m[k] = c.meta[e];
+        load_x8(c.DX + (int64_t)e * H, dx[k]);
+      } else {
+        m[k].u = 0; m[k].frow = -1; m[k].dt = 0.f; m[k].blk = 0; m[k].o = 0; m[k].root = 0; m[k].seg = 0;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int f = lane + 64 * j;
-      if (f < FD) {
-        float v, km = 1.f, sn = 0.f;
-        if (f < d) {
-          v = fp ? fp[f] : 1.0f;
-        } else if (f < F) {
-          float sa, ca;
-          sincosf(fmaf(tw[j], m.dt, tb[j]), &sa, &ca);
-          v = ca;
-          sn = sa;
-        } else {
-          v = mu[f - F];
-        }
-        if (drop) km = f < F ? keepf(hash4(seed, 2, sk, ((uint64_t)m.o << 16) | (uint64_t)f), c.pf, c.inv_kf)
-                             : node_keep(c, seed, m.blk, m.u, f - F);
-        v *= km;
-        float denc = 0.f;
-#pragma unroll
-        for (int h = 0; h < H; ++h) {
-          aU[j][h] += dx[h] * v;
-          denc += dx[h] * ue[j][h];
-        }
-        if (f >= d && f < F) {
-          const float gz = -denc * km * sn;
-          aw[j] += gz * m.dt;
-          ab[j] += gz;
-        }
+        for (int h = 0; h < H; ++h) dx[k][h] = 0.f;
       }
     }
 #pragma unroll
-    for (int h = 0; h < H; ++h) ac[h] += dx[h];
+    for (int k = 0; k < NE; ++k) {  // all gathers of the NE edges before any math
+      const float* fp = feat_row(c, m[k].frow);
+      const float* mu = c.mem + m[k].u * D;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int f = lane + 64 * j;
+        float x = 0.f;
+        if (f < d) x = fp ? fp[f] : 1.0f;
+        else if (f >= F && f < FD) x = mu[f - F];
+        v[k][j] = x;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      const uint32_t eb = drop ? efeat_base(seed, seg_key(m[k].blk, m[k].root), m[k].o) : 0u;
+      const uint32_t nb = drop ? node_base(seed, m[k].blk, m[k].u) : 0u;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int f = lane + 64 * j;
+        if (f < FD) {
+          float x = v[k][j], km = 1.f, sn = 0.f;
+          const bool enc = f >= d && f < F;
+          if (enc) {
+            float sa, ca;
+            sincosf(fmaf(tw[j], m[k].dt, tb[j]), &sa, &ca);
+            x = ca;
+            sn = sa;
+          }
+          if (drop) km = f < F ? keep32(eb, (uint32_t)f, c.pf, c.inv_kf) : keep32(nb, (uint32_t)(f - F), c.pf, c.inv_kf);
+          x *= km;
+#pragma unroll
+          for (int h = 0; h < H; ++h) aU[j][h] += dx[k][h] * x;
+          if (enc) {
+            const float4 u0 = *reinterpret_cast<const float4*>(&Uenc[(f - d) * H]);
+            const float4 u1 = *reinterpret_cast<const float4*>(&Uenc[(f - d) * H + 4]);
+            const float denc = dx[k][0] * u0.x + dx[k][1] * u0.y + dx[k][2] * u0.z + dx[k][3] * u0.w +
+                               dx[k][4] * u1.x + dx[k][5] * u1.y + dx[k][6] * u1.z + dx[k][7] * u1.w;
+            const float gz = -denc * km * sn;
+            aw[j] += gz * m[k].dt;
+            ab[j] += gz;
+          }
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < H; ++h) ac[h] += dx[k][h];
+    }
   }
   for (int k = 0; k < 4; ++k) {
     if (wv == k) {
@@ -1012,6 +1110,8 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
 // predictor weight gradients dWs = Σ_i A_i ⊗ e_s,i and dWd = Σ_i dhp_i ⊗ e_p,i + dhn_i ⊗ e_n,i:
 // AᵀB products over the events, one 16x16 output tile per wave on v_mfma_f32_16x16x4_f32
 // (exact fp32, k-ordered fmaf chain).  Grid: 2 * ceil(D/16)^2 waves.
+__device__ void pred_reduce_vec_body(const Ctx& c, int y, int lane);
+
 __global__ void __launch_bounds__(256) tgnn_pred_reduce_mfma(Ctx c) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   __shared__ f32x4 part[4][64];
@@ -1020,6 +1120,10 @@ __global__ void __launch_bounds__(256) tgnn_pred_reduce_mfma(Ctx c) {
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
   const bool ok = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
   const int nt = (D + 15) / 16;
+  if ((int)blockIdx.x >= 2 * nt * nt) {  // trailing blocks: bias / output-layer / loss sums
+    pred_reduce_vec_body(c, ((int)blockIdx.x - 2 * nt * nt) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+    return;
+  }
   const int which = blockIdx.x / (nt * nt);
   const int t = blockIdx.x % (nt * nt), tm = t / nt, tn = t % nt;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1060,13 +1164,11 @@ __global__ void __launch_bounds__(256) tgnn_pred_reduce_mfma(Ctx c) {
 }
 
 // predictor bias / output-layer gradients and the batch loss: one wave per output, lanes over events
-__global__ void __launch_bounds__(256) tgnn_pred_reduce_vec(Ctx c) {
+__device__ void pred_reduce_vec_body(const Ctx& c, int y, int lane) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   const int D = c.D;
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
   const bool ok = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
-  const int lane = threadIdx.x & 63;
-  const int y = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (y >= 3 * D + 2) return;
   const int S = 8 * D + 4;
   float acc = 0.f;
@@ -1088,13 +1190,20 @@ __global__ void __launch_bounds__(256) tgnn_pred_reduce_vec(Ctx c) {
 }
 
 // re-expand the collapsed gradients into the reference's parameters
-__global__ void tgnn_grad_expand(Ctx c) {
+__device__ void grad_attn_body(const Ctx& c, int y, int lane);
+
+// blocks [0, nexp): elementwise dU -> dW / db re-expansion; trailing blocks: d attn (wave per output)
+__global__ void __launch_bounds__(256) tgnn_grad_expand(Ctx c, int nexp) {
+  if ((int)blockIdx.x >= nexp) {
+    grad_attn_body(c, ((int)blockIdx.x - nexp) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+    return;
+  }
   const Lay L = c.L;
   const PLay PL = c.PL;
   const int D = c.D, F = c.F;
   const float* P = c.params;
   const float* r = c.red;
-  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < L.Ws; x += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < L.Ws; x += (int64_t)nexp * blockDim.x) {
     float g = 0.f;
     if (x >= L.te_w && x < L.te_w + D) {
       g = r[PL.w + (x - L.te_w)];
@@ -1123,11 +1232,10 @@ __global__ void tgnn_grad_expand(Ctx c) {
 
 // d attn_{l,r}[h,d] = W_n[hD+d,:]·dU_{l,r}[h,:] + b_n[hD+d]·dc ; d attn_e likewise with W_e:
 // one wave per output, lanes over the contraction
-__global__ void __launch_bounds__(256) tgnn_grad_attn(Ctx c) {
+__device__ void grad_attn_body(const Ctx& c, int y, int lane) {
   const Lay L = c.L;
   const PLay PL = c.PL;
   const int D = c.D, F = c.F;
-  const int y = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (y >= 3 * H * D) return;
   const int which = y / (H * D), j = y % (H * D), h = j / D;
   const float* P = c.params;
@@ -1454,7 +1562,7 @@ static int make_ctx(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* b, int
 
 static inline int grid_for(int64_t n, int per) { return (int)((n + per - 1) / per); }
 
-static size_t assemble_smem() { return (size_t)TOUCH_MAX * 8 + (size_t)TOUCH_MAX * 4; }
+static size_t assemble_smem() { return (size_t)TOUCH_MAX * 12 + (size_t)1024 * 8; }
 
 static int edge_grid(int64_t Ecap) {
   const int64_t g = (Ecap * 16 + 255) / 256;
@@ -1468,10 +1576,12 @@ static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
   tgnn_assemble<TRAIN><<<1, 1024, assemble_smem(), s>>>(c);
   probe_end(TGNX_K_ASSEMBLE, s);
   TGNX_LAUNCH_CHECK("tgnn_assemble");
-  tgnn_seg_count<<<grid_for(Scap, 256), 256, 0, s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_seg_count");
-  tgnn_seg_scan<<<1, 1024, 0, s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_seg_scan");
+  if (!TRAIN) {
+    tgnn_seg_count<<<grid_for(Scap, 256), 256, 0, s>>>(c);
+    TGNX_LAUNCH_CHECK("tgnn_seg_count");
+    tgnn_seg_scan<<<1, 1024, 0, s>>>(c);
+    TGNX_LAUNCH_CHECK("tgnn_seg_scan");
+  }
   probe_begin(TGNX_K_EDGE_META, s);
   tgnn_edge_meta<TRAIN><<<edge_grid(c.Ecap) / 4 + 1, 256, 0, s>>>(c);
   probe_end(TGNX_K_EDGE_META, s);
@@ -1561,10 +1671,7 @@ int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers
   c.drop = dropout && (c.pf > 0.f || c.pa > 0.f);
   hipStream_t s = as_stream(stream);
   const int Bmax = cfg->max_batch;
-  if (gen_neg) {
-    tgnn_negs<<<grid_for(Bmax, 256), 256, 0, s>>>(c);
-    TGNX_LAUNCH_CHECK("tgnn_negs");
-  }
+  c.gen_neg = gen_neg ? 1 : 0;
   rc = launch_forward<true>(c, 3 * (int64_t)Bmax, s);
   if (rc) return rc;
   probe_begin(TGNX_K_PRED, s);
@@ -1573,17 +1680,16 @@ int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers
   TGNX_LAUNCH_CHECK("tgnn_pred_train");
   {
     const int nt = (c.D + 15) / 16;
-    tgnn_pred_reduce_mfma<<<2 * nt * nt, 256, 0, s>>>(c);
+    tgnn_pred_reduce_mfma<<<2 * nt * nt + grid_for(3 * c.D + 2, 4), 256, 0, s>>>(c);
     TGNX_LAUNCH_CHECK("tgnn_pred_reduce_mfma");
-    tgnn_pred_reduce_vec<<<grid_for(3 * c.D + 2, 4), 256, 0, s>>>(c);
-    TGNX_LAUNCH_CHECK("tgnn_pred_reduce_vec");
   }
   rc = launch_backward(c, s);
   if (rc) return rc;
-  tgnn_grad_expand<<<grid_for(c.L.Ws, 256) < 2048 ? grid_for(c.L.Ws, 256) : 2048, 256, 0, s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_grad_expand");
-  tgnn_grad_attn<<<grid_for(3 * H * c.D, 4), 256, 0, s>>>(c);
-  TGNX_LAUNCH_CHECK("tgnn_grad_attn");
+  {
+    const int nexp = grid_for(c.L.Ws, 256) < 1024 ? grid_for(c.L.Ws, 256) : 1024;
+    tgnn_grad_expand<<<nexp + grid_for(3 * H * c.D, 4), 256, 0, s>>>(c, nexp);
+    TGNX_LAUNCH_CHECK("tgnn_grad_expand");
+  }
   return TGNX_OK;
 }
 

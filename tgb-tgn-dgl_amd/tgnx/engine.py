@@ -180,6 +180,62 @@ class TgnnEngine:
         if up(self._cfg_ref, self._buf_ref, st):
             raise RuntimeError(f"tgnx resident update failed: {_lib.lib().tgnx_last_error().decode()}")
 
+    def capture_resident(self, steps_per_graph: int = 1):
+        """Capture `steps_per_graph` resident train steps into HIP graphs (torch.cuda.CUDAGraph).
+        Every kernel reads its batch from the device control block, so replaying a graph advances
+        through consecutive batches.  world > 1: the gradient all-reduce stays eager between a
+        captured forward/backward graph and a captured update graph."""
+        adv, fb, up = self._f
+        lo, hi, batch = self._res
+        cfg, buf, ctl = self._cfg_ref, self._buf_ref, self._ctl_p
+
+        def pre():
+            st = self._stream()
+            rc = adv(ctl, 1, 0, 0, 0, lo, hi, batch, self.rank, self.world, self.seed, 1, st)
+            rc |= fb(cfg, buf, 1, self._res_drop, st)
+            if rc:
+                raise RuntimeError(_lib.lib().tgnx_last_error().decode())
+
+        def post():
+            if up(cfg, buf, self._stream()):
+                raise RuntimeError(_lib.lib().tgnx_last_error().decode())
+
+        # capture runs the work once? no: capture only records; keep the cursor unchanged
+        torch.cuda.synchronize(self.dev)
+        saved = self.ctl.clone()
+        sstream = torch.cuda.Stream(self.dev)
+        sstream.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(sstream):   # warm the caching allocator on the side stream
+            pass
+        torch.cuda.current_stream(self.dev).wait_stream(sstream)
+        if self.world == 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(steps_per_graph):
+                    pre()
+                    post()
+            self._graphs = (g, None)
+        else:
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                pre()
+            with torch.cuda.graph(g2):
+                post()
+            self._graphs = (g1, g2)
+        self._steps_per_graph = steps_per_graph
+        torch.cuda.synchronize(self.dev)
+        self.ctl.copy_(saved)
+
+    def replay_resident(self):
+        """Run `steps_per_graph` resident steps from the captured graph(s)."""
+        g1, g2 = self._graphs
+        if g2 is None:
+            g1.replay()
+        else:
+            g1.replay()
+            self._allreduce_grads()
+            g2.replay()
+
     def units(self):
         """(sum of assembled edges, sum of segments) since the last reset — roofline units."""
         return int(self.ctl[13]), int(self.ctl[14])
