@@ -25,7 +25,17 @@ constexpr int H = 8;          // gnn.att_head
 constexpr int DMAX = 128;     // gnn.dim_out (memory/time/embedding dim) capacity
 constexpr int FMAX = 320;     // d + D capacity
 constexpr int TOUCH_MAX = 8192;
-constexpr int GBWD = 256;     // workgroups of the edge backward kernel (= partial slabs)
+#ifndef TGNX_GBWD
+#define TGNX_GBWD 256
+#endif
+#ifndef TGNX_BWD_WAVES
+#define TGNX_BWD_WAVES 8
+#endif
+#ifndef TGNX_BWD_NE
+#define TGNX_BWD_NE 2
+#endif
+constexpr int GBWD = TGNX_GBWD;            // workgroups of the edge backward kernel (= partial slabs)
+constexpr int BWD_WAVES = TGNX_BWD_WAVES;  // waves per edge backward workgroup
 constexpr int GSEG = 64;      // workgroups of the segment backward kernel
 constexpr int MRR_SLOTS = 65536;  // per-batch MRR ring in buffers.mrr
 
@@ -58,7 +68,7 @@ static Lay make_lay(int D, int d) {
 }
 // derived per step from the params (collapse kernel)
 struct ULay {
-  int64_t Ue, Ul, Ur, ce, cl, cr, WsT, WdT, Ws1, Wd1, total;
+  int64_t Ue, Ul, Ur, ce, cl, cr, WsT, WdT, Ws1, Wd1, ones, total;
 };
 static ULay make_ulay(int D, int d) {
   const int64_t F = d + D;
@@ -74,6 +84,7 @@ static ULay make_ulay(int D, int d) {
   U.WdT = o; o += al4((int64_t)D * D);
   U.Ws1 = o; o += al4(D);
   U.Wd1 = o; o += al4(D);
+  U.ones = o; o += al4(FMAX);  // feature row of self loops (all ones), so gathers need no branch
   U.total = o;
   return U;
 }
@@ -96,13 +107,14 @@ __host__ __device__ inline PLay make_play(int D, int d) {
   return P;
 }
 
-// per-edge descriptor written by tgnn_edge_meta (32 B)
+// per-edge descriptor written by tgnn_edge_meta (48 B)
 struct __attribute__((aligned(16))) EdgeMeta {
   int64_t u;     // source node
   int64_t frow;  // >= 0: feature-table row (ring e_id); -1: self loop (ones); <= -2: -(event row) - 2
   float dt;      // edge time - time_assoc[u] as of the segment's block
   int seg, o, blk;
   int64_t root;
+  uint32_t eb, nb;  // dropout mask bases: edge features / time encoding, source memory row
 };
 
 // ------------------------------------------------------------------ context
@@ -253,6 +265,8 @@ __global__ void __launch_bounds__(256) tgnn_collapse(Ctx c) {
   const int nb_dot = nbe + 2 * nbl;
   const int nrow = 3 * H + 2 * D;
   const int nb_row = (nrow + 3) / 4;
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < FMAX; i += blockDim.x) c.U[c.UL.ones + i] = 1.0f;
   int b = blockIdx.x;
   if (b < nb_dot) {
     int which, o;
@@ -570,6 +584,13 @@ __global__ void tgnn_edge_meta(Ctx c) {
     m.o = o;
     m.blk = s.blk;
     m.root = s.root;
+    if (c.drop) {
+      const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+      m.eb = efeat_base(seed, seg_key(s.blk, s.root), o);
+      m.nb = node_base(seed, s.blk, m.u);
+    } else {
+      m.eb = m.nb = 0u;
+    }
     c.meta[e] = m;
   }
 }
@@ -589,6 +610,41 @@ __device__ __forceinline__ void fma8(float (&acc)[H], const float* us, float x) 
   const float4 u1 = *reinterpret_cast<const float4*>(us + 4);
   acc[0] += u0.x * x; acc[1] += u0.y * x; acc[2] += u0.z * x; acc[3] += u0.w * x;
   acc[4] += u1.x * x; acc[5] += u1.y * x; acc[6] += u1.z * x; acc[7] += u1.w * x;
+}
+
+// sin/cos of a float argument with an exact reduction: Cody-Waite in double (pi/2 split in two
+// doubles, exact for |z| < 2^31) and double polynomials on |r| <= pi/4 (fdlibm kernel
+// coefficients), rounded once to float.  Time-encoding arguments w*dt + b reach 1e6..1e9, where
+// ocml's sincosf takes a long, divergent Payne-Hanek path; fp64 FMA runs at the fp32 rate on gfx950.
+__device__ __forceinline__ void te_reduce(float z, double& r, int& q) {
+  const double x = (double)z;
+  const double k = rint(x * 0.63661977236758134308);
+  r = fma(-k, 1.5707963267948965580e+00, x);
+  r = fma(-k, 6.1232339957367658e-17, r);
+  q = (int)(int64_t)k;
+}
+__device__ __forceinline__ double te_sin_poly(double r, double r2) {
+  return r + r * r2 * (-1.66666666666666324348e-01 + r2 * (8.33333333332248946124e-03 +
+         r2 * (-1.98412698298579493134e-04 + r2 * (2.75573137070700676789e-06 + r2 * -2.50507602534068634195e-08))));
+}
+__device__ __forceinline__ double te_cos_poly(double r2) {
+  return 1.0 - 0.5 * r2 + r2 * r2 * (4.16666666666666019037e-02 + r2 * (-1.38888888888741095749e-03 +
+         r2 * (2.48015872894767294178e-05 + r2 * (-2.75573143513906633035e-07 + r2 * 2.08757232129817482790e-09))));
+}
+__device__ __forceinline__ void te_sincos(float z, float& sn, float& cs) {
+  double r; int q;
+  te_reduce(z, r, q);
+  const double r2 = r * r, s = te_sin_poly(r, r2), co = te_cos_poly(r2);
+  const double s1 = (q & 1) ? co : s, c1 = (q & 1) ? s : co;
+  sn = (float)((q & 2) ? -s1 : s1);
+  cs = (float)(((q + 1) & 2) ? -c1 : c1);
+}
+__device__ __forceinline__ float te_cos(float z) {
+  double r; int q;
+  te_reduce(z, r, q);
+  const double r2 = r * r;
+  const double v = (q & 1) ? te_sin_poly(r, r2) : te_cos_poly(r2);
+  return (float)(((q + 1) & 2) ? -v : v);
 }
 
 __global__ void __launch_bounds__(256) tgnn_edge_fwd(Ctx c) {
@@ -628,13 +684,12 @@ __global__ void __launch_bounds__(256) tgnn_edge_fwd(Ctx c) {
       const int k = sub + 16 * j;
       vm[j] = k < D ? mu[k] : 0.f;
     }
-    const uint32_t eb = drop ? efeat_base(seed, seg_key(m.blk, m.root), m.o) : 0u;
-    const uint32_t nb = drop ? node_base(seed, m.blk, m.u) : 0u;
+    const uint32_t eb = m.eb, nb = m.nb;
     float acc[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) acc[h] = 0.f;
     for (int f = d + sub; f < F; f += 16) {  // time encoding (model_utils.py:235, :447)
-      float x = cosf(fmaf(Tw[f - d], m.dt, Tb[f - d]));
+      float x = te_cos(fmaf(Tw[f - d], m.dt, Tb[f - d]));
       if (drop) x *= keep32(eb, (uint32_t)f, c.pf, c.inv_kf);
       fma8(acc, &Us[f * H], x);
     }
@@ -858,149 +913,211 @@ __global__ void __launch_bounds__(256) tgnn_seg_bwd(Ctx c) {
   for (int p = threadIdx.x; p < PL.total; p += blockDim.x) slab[p] = red[p];
 }
 
-// per edge: dU_e += dx ⊗ efeat, dU_l += dx ⊗ drop(mem[src]), TimeEncode dw/db (lanes over dims)
-template <int NJ>
-__global__ void __launch_bounds__(256) tgnn_edge_bwd(Ctx c) {
-  extern __shared__ __attribute__((aligned(16))) float red[];
-  __shared__ __attribute__((aligned(16))) float Uenc[DMAX * H];   // U_e[h][d + k] as [k][h]
+// dU_e, dU_l, dw, db, dc_e, dc_l partials of the edge terms (backward of tgnn_edge_fwd).
+// Lanes own feature columns and waves stride over edges, so every reduction over edges stays in
+// registers.  Column classes are compile-time (CF feature columns, CT time-encoding columns, CT
+// memory columns); gathers use clamped indices (values of lanes past the end are never written
+// out), the self-loop row points at a row of ones: the loop body has no divergent control flow.
+// Two register sets ping-pong so one edge's gathers are in flight during the other's math.  Each
+// wave leaves its partial in LDS and the workgroup sums them in a fixed order into its slab.
+template <int CF, int CT, bool DROP>
+__global__ void __launch_bounds__(64 * BWD_WAVES) tgnn_edge_bwd(Ctx c) {
+  constexpr int NJ = CF + 2 * CT;
+  extern __shared__ __attribute__((aligned(16))) float part[];   // [BWD_WAVES][PL.total]
+  __shared__ __attribute__((aligned(16))) float Uenc[DMAX * H];   // U_e[h][d + i] as [i][h], zero for i >= D
   const PLay PL = c.PL;
-  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) red[p] = 0.f;
-  for (int x = threadIdx.x; x < c.D * H; x += blockDim.x) {
-    const int k = x / H, h = x % H;
-    Uenc[x] = c.U[c.UL.Ue + h * c.F + c.d + k];
+  const int F = c.F, D = c.D, d = c.d;
+  for (int x = threadIdx.x; x < DMAX * H; x += blockDim.x) {
+    const int i = x / H, h = x % H;
+    Uenc[x] = i < D ? c.U[c.UL.Ue + h * F + d + i] : 0.f;
   }
-  __syncthreads();
   const int B = (int)c.ctl[TGNX_CTL_B];
   const bool okb = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
   const int E = okb ? (int)c.ctl[TGNX_CTL_E] : 0;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int F = c.F, D = c.D, d = c.d, FD = F + D;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-  const bool drop = c.drop;
-  float tw[NJ], tb[NJ];
-  float aU[NJ][H], aw[NJ], ab[NJ], ac[H];
+  const float* ones = c.U + c.UL.ones;
+  int fidx[CF > 0 ? CF : 1], kidx[CT];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int f = lane + 64 * j;
-    const bool enc = f >= d && f < F;
+  for (int j = 0; j < CF; ++j) fidx[j] = min(lane + 64 * j, d - 1);
+#pragma unroll
+  for (int j = 0; j < CT; ++j) kidx[j] = min(lane + 64 * j, D - 1);
+  float aU[NJ][H], tw[CT], tb[CT], aw[CT], ab[CT], ac[H];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int h = 0; h < H; ++h) aU[j][h] = 0.f;
-    tw[j] = enc ? c.params[c.L.te_w + f - d] : 0.f;
-    tb[j] = enc ? c.params[c.L.te_b + f - d] : 0.f;
+#pragma unroll
+  for (int j = 0; j < CT; ++j) {
+    const int i = lane + 64 * j;
+    tw[j] = i < D ? c.params[c.L.te_w + i] : 0.f;
+    tb[j] = i < D ? c.params[c.L.te_b + i] : 0.f;
     aw[j] = ab[j] = 0.f;
   }
 #pragma unroll
   for (int h = 0; h < H; ++h) ac[h] = 0.f;
-  constexpr int NE = 2;  // edges in flight per wave
-  const int stride = gridDim.x * 4;
-  for (int e0 = blockIdx.x * 4 + wv; e0 < E; e0 += NE * stride) {
-    EdgeMeta m[NE];
-    float dx[NE][H];
-    float v[NE][NJ];
+  __syncthreads();
+
+  struct Slot {
+    float dt, dx[H], vf[CF > 0 ? CF : 1], vm[CT];
+    uint32_t eb, nb;
+  };
+  // issue the loads of edge e into slot S (meta via scalar loads: e is wave-uniform)
+  auto load = [&](int e, Slot& S) {
+    const EdgeMeta m = c.meta[e];
+    const float* fp = m.frow >= 0 ? c.feat + m.frow * d : m.frow == -1 ? ones : c.ev_msg + (-(m.frow + 2)) * d;
+    const float* mu = c.mem + m.u * D;
 #pragma unroll
-    for (int k = 0; k < NE; ++k) {
-      const int e = e0 + k * stride;
-      if (e < E) {
-        m[k] = c.meta[e];
-        load_x8(c.DX + (int64_t)e * H, dx[k]);
-      } else {
-        m[k].u = 0; m[k].frow = -1; m[k].dt = 0.f; m[k].blk = 0; m[k].o = 0; m[k].root = 0; m[k].seg = 0;
+    for (int j = 0; j < CF; ++j) S.vf[j] = fp[fidx[j]];
 #pragma unroll
-        for (int h = 0; h < H; ++h) dx[k][h] = 0.f;
-      }
+    for (int j = 0; j < CT; ++j) S.vm[j] = mu[kidx[j]];
+    load_x8(c.DX + (int64_t)e * H, S.dx);
+    S.dt = m.dt;
+    S.eb = m.eb;
+    S.nb = m.nb;
+  };
+  auto math = [&](const Slot& S) {
+#pragma unroll
+    for (int j = 0; j < CF; ++j) {
+      float x = S.vf[j];
+      if (DROP) x *= keep32(S.eb, (uint32_t)(lane + 64 * j), c.pf, c.inv_kf);
+#pragma unroll
+      for (int h = 0; h < H; ++h) aU[j][h] += S.dx[h] * x;
     }
 #pragma unroll
-    for (int k = 0; k < NE; ++k) {  // all gathers of the NE edges before any math
-      const float* fp = feat_row(c, m[k].frow);
-      const float* mu = c.mem + m[k].u * D;
+    for (int j = 0; j < CT; ++j) {  // time encoding dim i: x = cos(w_i dt + b_i)  (model_utils.py:235)
+      const int i = lane + 64 * j;
+      float sn, cs;
+      te_sincos(fmaf(tw[j], S.dt, tb[j]), sn, cs);
+      const float km = DROP ? keep32(S.eb, (uint32_t)(d + i), c.pf, c.inv_kf) : 1.f;
+      const float x = cs * km;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int f = lane + 64 * j;
-        float x = 0.f;
-        if (f < d) x = fp ? fp[f] : 1.0f;
-        else if (f >= F && f < FD) x = mu[f - F];
-        v[k][j] = x;
-      }
+      for (int h = 0; h < H; ++h) aU[CF + j][h] += S.dx[h] * x;
+      const float4 u0 = *reinterpret_cast<const float4*>(&Uenc[(i & (DMAX - 1)) * H]);
+      const float4 u1 = *reinterpret_cast<const float4*>(&Uenc[(i & (DMAX - 1)) * H + 4]);
+      const float denc = S.dx[0] * u0.x + S.dx[1] * u0.y + S.dx[2] * u0.z + S.dx[3] * u0.w +
+                         S.dx[4] * u1.x + S.dx[5] * u1.y + S.dx[6] * u1.z + S.dx[7] * u1.w;
+      const float gz = -denc * km * sn;
+      aw[j] += gz * S.dt;
+      ab[j] += gz;
     }
 #pragma unroll
-    for (int k = 0; k < NE; ++k) {
-      const uint32_t eb = drop ? efeat_base(seed, seg_key(m[k].blk, m[k].root), m[k].o) : 0u;
-      const uint32_t nb = drop ? node_base(seed, m[k].blk, m[k].u) : 0u;
+    for (int j = 0; j < CT; ++j) {
+      float x = S.vm[j];
+      if (DROP) x *= keep32(S.nb, (uint32_t)(lane + 64 * j), c.pf, c.inv_kf);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int f = lane + 64 * j;
-        if (f < FD) {
-          float x = v[k][j], km = 1.f, sn = 0.f;
-          const bool enc = f >= d && f < F;
-          if (enc) {
-            float sa, ca;
-            sincosf(fmaf(tw[j], m[k].dt, tb[j]), &sa, &ca);
-            x = ca;
-            sn = sa;
-          }
-          if (drop) km = f < F ? keep32(eb, (uint32_t)f, c.pf, c.inv_kf) : keep32(nb, (uint32_t)(f - F), c.pf, c.inv_kf);
-          x *= km;
+      for (int h = 0; h < H; ++h) aU[CF + CT + j][h] += S.dx[h] * x;
+    }
 #pragma unroll
-          for (int h = 0; h < H; ++h) aU[j][h] += dx[k][h] * x;
-          if (enc) {
-            const float4 u0 = *reinterpret_cast<const float4*>(&Uenc[(f - d) * H]);
-            const float4 u1 = *reinterpret_cast<const float4*>(&Uenc[(f - d) * H + 4]);
-            const float denc = dx[k][0] * u0.x + dx[k][1] * u0.y + dx[k][2] * u0.z + dx[k][3] * u0.w +
-                               dx[k][4] * u1.x + dx[k][5] * u1.y + dx[k][6] * u1.z + dx[k][7] * u1.w;
-            const float gz = -denc * km * sn;
-            aw[j] += gz * m[k].dt;
-            ab[j] += gz;
-          }
-        }
+    for (int h = 0; h < H; ++h) ac[h] += S.dx[h];
+  };
+
+  const int stride = gridDim.x * BWD_WAVES;
+  int e = blockIdx.x * BWD_WAVES + wv;
+  Slot A, Bs;
+  if (e < E) load(e, A);
+  while (e < E) {
+    const int e1 = e + stride;
+    if (e1 < E) load(e1, Bs);
+    math(A);
+    if (e1 >= E) break;
+    const int e2 = e1 + stride;
+    if (e2 < E) load(e2, A);
+    math(Bs);
+    e = e2;
+  }
+  // this wave's partial -> LDS row wv (entries owned by nobody are zeroed in the sum below)
+  float* pw = part + wv * PL.total;
+#pragma unroll
+  for (int j = 0; j < CF; ++j) {
+    const int f = lane + 64 * j;
+    if (f < d)
+#pragma unroll
+      for (int h = 0; h < H; ++h) pw[PL.Ue + h * F + f] = aU[j][h];
+  }
+#pragma unroll
+  for (int j = 0; j < CT; ++j) {
+    const int i = lane + 64 * j;
+    if (i < D) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        pw[PL.Ue + h * F + d + i] = aU[CF + j][h];
+        pw[PL.Ul + h * D + i] = aU[CF + CT + j][h];
       }
-#pragma unroll
-      for (int h = 0; h < H; ++h) ac[h] += dx[k][h];
+      pw[PL.w + i] = aw[j];
+      pw[PL.b + i] = ab[j];
     }
   }
-  for (int k = 0; k < 4; ++k) {
-    if (wv == k) {
+  if (lane == 0)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int f = lane + 64 * j;
-        if (f < FD) {
-#pragma unroll
-          for (int h = 0; h < H; ++h) {
-            if (f < F) red[PL.Ue + h * F + f] += aU[j][h];
-            else red[PL.Ul + h * D + (f - F)] += aU[j][h];
-          }
-          if (f >= d && f < F) {
-            red[PL.w + f - d] += aw[j];
-            red[PL.b + f - d] += ab[j];
-          }
-        }
-      }
-      if (lane == 0)
-#pragma unroll
-        for (int h = 0; h < H; ++h) {
-          red[PL.ce + h] += ac[h];
-          red[PL.cl + h] += ac[h];
-        }
+    for (int h = 0; h < H; ++h) {
+      pw[PL.ce + h] = ac[h];
+      pw[PL.cl + h] = ac[h];
     }
-    __syncthreads();
-  }
+  __syncthreads();
   float* slab = c.slabs + (int64_t)blockIdx.x * PL.total;
-  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) slab[p] = red[p];
+  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) {
+    float s = 0.f;
+    const bool owned = (p < PL.Ur) || (p >= PL.ce && p < PL.cr) || p >= PL.w;
+    if (owned)
+#pragma unroll
+      for (int w = 0; w < BWD_WAVES; ++w) s += part[w * PL.total + p];
+    slab[p] = s;
+  }
 }
 
-// sum the partial slabs: 8 threads per output (lanes 8p..8p+7), fixed order -> deterministic
-__global__ void __launch_bounds__(256) tgnn_grad_reduce(Ctx c, int Ge, int Gs) {
+template <int CF, int CT, bool DROP>
+static void launch_edge_bwd_t(const Ctx& c, size_t shp, hipStream_t s) {
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)tgnn_edge_bwd<CF, CT, DROP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              150 * 1024);
+    return true;
+  }();
+  (void)attr;
+  tgnn_edge_bwd<CF, CT, DROP><<<GBWD, 64 * BWD_WAVES, shp, s>>>(c);
+}
+template <int CF>
+static void launch_edge_bwd_cf(const Ctx& c, size_t shp, hipStream_t s) {
+  const bool two = c.D > 64;
+  if (c.drop) two ? launch_edge_bwd_t<CF, 2, true>(c, shp, s) : launch_edge_bwd_t<CF, 1, true>(c, shp, s);
+  else two ? launch_edge_bwd_t<CF, 2, false>(c, shp, s) : launch_edge_bwd_t<CF, 1, false>(c, shp, s);
+}
+static void launch_edge_bwd(const Ctx& c, hipStream_t s) {
+  const size_t shp = (size_t)BWD_WAVES * c.PL.total * 4;
+  switch ((c.d + 63) / 64) {
+    case 0: launch_edge_bwd_cf<0>(c, shp, s); break;
+    case 1: launch_edge_bwd_cf<1>(c, shp, s); break;
+    case 2: launch_edge_bwd_cf<2>(c, shp, s); break;
+    case 3: launch_edge_bwd_cf<3>(c, shp, s); break;
+    case 4: launch_edge_bwd_cf<4>(c, shp, s); break;
+    default: launch_edge_bwd_cf<5>(c, shp, s); break;
+  }
+}
+
+// Sum the partial slabs in a fixed order (deterministic): a workgroup owns 64 consecutive outputs
+// (one per lane, coalesced rows), its 16 waves take every 16th slab, LDS combines the waves.
+constexpr int RED_WAVES = 16;
+__global__ void __launch_bounds__(64 * RED_WAVES) tgnn_grad_reduce(Ctx c, int Ge, int Gs) {
+  __shared__ float acc[RED_WAVES][64];
   const int P = c.PL.total;
-  const int p = (blockIdx.x * blockDim.x + threadIdx.x) >> 3;
-  const int sl = threadIdx.x & 7;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int p = blockIdx.x * 64 + lane;
   float s = 0.f;
   if (p < P) {
-    for (int g = sl; g < Ge; g += 8) s += c.slabs[(int64_t)g * P + p];
-    for (int g = sl; g < Gs; g += 8) s += c.slabs_s[(int64_t)g * P + p];
+#pragma unroll 4
+    for (int g = wv; g < Ge; g += RED_WAVES) s += c.slabs[(int64_t)g * P + p];
+#pragma unroll 4
+    for (int g = wv; g < Gs; g += RED_WAVES) s += c.slabs_s[(int64_t)g * P + p];
   }
-  s += __shfl_xor(s, 4, 8);
-  s += __shfl_xor(s, 2, 8);
-  s += __shfl_xor(s, 1, 8);
-  if (p < P && sl == 0) c.red[p] = s;
+  acc[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && p < P) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < RED_WAVES; ++w) t += acc[w][lane];
+    c.red[p] = t;
+  }
 }
 
 // ------------------------------------------------------------------ predictor (train): one wave per event
@@ -1610,16 +1727,10 @@ static int launch_backward(const Ctx& c, hipStream_t s) {
   TGNX_LAUNCH_CHECK("tgnn_seg_bwd");
   probe_begin(TGNX_K_EDGE_BWD, s);
   const int FD = c.F + c.D;
-  if (FD <= 64) tgnn_edge_bwd<1><<<GBWD, 256, shm, s>>>(c);
-  else if (FD <= 128) tgnn_edge_bwd<2><<<GBWD, 256, shm, s>>>(c);
-  else if (FD <= 192) tgnn_edge_bwd<3><<<GBWD, 256, shm, s>>>(c);
-  else if (FD <= 256) tgnn_edge_bwd<4><<<GBWD, 256, shm, s>>>(c);
-  else if (FD <= 320) tgnn_edge_bwd<5><<<GBWD, 256, shm, s>>>(c);
-  else if (FD <= 384) tgnn_edge_bwd<6><<<GBWD, 256, shm, s>>>(c);
-  else tgnn_edge_bwd<7><<<GBWD, 256, shm, s>>>(c);
+  launch_edge_bwd(c, s);
   probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgnn_edge_bwd");
-  tgnn_grad_reduce<<<grid_for((int64_t)c.PL.total * 8, 256), 256, 0, s>>>(c, GBWD, GSEG);
+  tgnn_grad_reduce<<<(c.PL.total + 63) / 64, 64 * RED_WAVES, 0, s>>>(c, GBWD, GSEG);
   TGNX_LAUNCH_CHECK("tgnn_grad_reduce");
   return TGNX_OK;
 }

@@ -11,7 +11,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtgnx.so")
+LIB_PATH = os.environ.get("TGNX_LIB") or os.path.join(_HERE, "libtgnx.so")
 
 c_i32, c_i64, c_u64, c_sz, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p
 P = c_vp  # every device pointer crosses as void*
