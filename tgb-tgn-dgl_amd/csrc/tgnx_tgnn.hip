@@ -599,19 +599,6 @@ __device__ __forceinline__ const float* feat_row(const Ctx& c, int64_t frow) {
   return frow >= 0 ? c.feat + frow * c.d : frow == -1 ? nullptr : c.ev_msg + (-(frow + 2)) * c.d;
 }
 
-// x_eh = U_e[h]·efeat_e + U_l[h]·drop(mem[src]) + c : 16 lanes per edge, U staged in LDS [dim][head].
-// Gathers (feature row dims [0,d), memory row dims [F, F+D)) are issued before any math; the
-// time-encoding dims [d, F) need no gather and run in a rolled loop (cosf is long).
-constexpr int NFEAT16 = (FMAX - DMAX + 15) / 16 + 1;  // feature values per lane (d <= FMAX - D)
-constexpr int NMEM16 = DMAX / 16;                     // memory values per lane
-
-__device__ __forceinline__ void fma8(float (&acc)[H], const float* us, float x) {
-  const float4 u0 = *reinterpret_cast<const float4*>(us);
-  const float4 u1 = *reinterpret_cast<const float4*>(us + 4);
-  acc[0] += u0.x * x; acc[1] += u0.y * x; acc[2] += u0.z * x; acc[3] += u0.w * x;
-  acc[4] += u1.x * x; acc[5] += u1.y * x; acc[6] += u1.z * x; acc[7] += u1.w * x;
-}
-
 // sin/cos of a float argument with an exact reduction: Cody-Waite in double (pi/2 split in two
 // doubles, exact for |z| < 2^31) and double polynomials on |r| <= pi/4 (fdlibm kernel
 // coefficients), rounded once to float.  Time-encoding arguments w*dt + b reach 1e6..1e9, where
@@ -647,84 +634,156 @@ __device__ __forceinline__ float te_cos(float z) {
   return (float)(((q + 1) & 2) ? -v : v);
 }
 
+// Column map shared by the edge kernels (a wave per edge, lanes over columns): CF feature
+// columns (dims lane + 64j of the edge feature row, j < CF), CT time-encoding columns (dims
+// d + lane + 64j) and CT memory columns (dims lane + 64j of the source memory row).  Gathers use
+// clamped indices and the self-loop row points at a row of ones, so no load is predicated;
+// lanes past the end read finite values whose weights / outputs are zero / never written.
+template <int CF, int CT>
+struct EdgeCols {
+  int fidx[CF > 0 ? CF : 1], kidx[CT];
+  __device__ __forceinline__ EdgeCols(int lane, int d, int D) {
+#pragma unroll
+    for (int j = 0; j < CF; ++j) fidx[j] = min(lane + 64 * j, d - 1);
+#pragma unroll
+    for (int j = 0; j < CT; ++j) kidx[j] = min(lane + 64 * j, D - 1);
+  }
+};
+template <int CF, int CT>
+struct EdgeVals {
+  float dt, vf[CF > 0 ? CF : 1], vm[CT];
+  uint32_t eb, nb;
+};
+template <int CF, int CT>
+__device__ __forceinline__ void edge_gather(const Ctx& c, int e, const EdgeCols<CF, CT>& cols, EdgeVals<CF, CT>& S) {
+  const EdgeMeta m = c.meta[e];
+  const float* fp = m.frow >= 0 ? c.feat + m.frow * c.d
+                                : m.frow == -1 ? c.U + c.UL.ones : c.ev_msg + (-(m.frow + 2)) * c.d;
+  const float* mu = c.mem + m.u * c.D;
+#pragma unroll
+  for (int j = 0; j < CF; ++j) S.vf[j] = fp[cols.fidx[j]];
+#pragma unroll
+  for (int j = 0; j < CT; ++j) S.vm[j] = mu[cols.kidx[j]];
+  S.dt = m.dt;
+  S.eb = m.eb;
+  S.nb = m.nb;
+}
+
+// Sum of v[0..7] over the wave by recursive halving (10 shuffles): on return lane l holds the
+// total of head l / 8 (lanes with l % 8 == 0 write).
+__device__ __forceinline__ float wave_sum8(const float (&v)[H], int lane) {
+  const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+  float k4[4], k2[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float keep = b5 ? v[4 + i] : v[i], send = b5 ? v[i] : v[4 + i];
+    k4[i] = keep + __shfl_xor(send, 32, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float keep = b4 ? k4[2 + i] : k4[i], send = b4 ? k4[i] : k4[2 + i];
+    k2[i] = keep + __shfl_xor(send, 16, 64);
+  }
+  float s = (b3 ? k2[1] : k2[0]) + __shfl_xor(b3 ? k2[0] : k2[1], 8, 64);
+  s += __shfl_xor(s, 4, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 1, 64);
+  return s;
+}
+
+// x_eh = U_e[h]·[efeat_e, drop(cos(w dt + b))] + U_l[h]·drop(mem[src]) + c_h   (model_utils.py:447-452
+// collapsed): a wave per edge, each lane's U columns held in registers across
+// edges, two gather sets ping-pong so one edge's loads are in flight during the other's math.
+#ifndef TGNX_GFWD
+#define TGNX_GFWD 512
+#endif
+constexpr int GFWD = TGNX_GFWD;
+template <int CF, int CT, bool DROP>
 __global__ void __launch_bounds__(256) tgnn_edge_fwd(Ctx c) {
-  __shared__ __attribute__((aligned(16))) float Us[(FMAX + DMAX) * H];
-  __shared__ float Tw[DMAX], Tb[DMAX];
+  constexpr int NJ = CF + 2 * CT;
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int F = c.F, D = c.D, d = c.d, FD = c.F + c.D;
-  for (int x = threadIdx.x; x < FD * H; x += blockDim.x) {
-    const int f = x / H, h = x % H;
-    Us[x] = f < F ? c.U[c.UL.Ue + h * F + f] : c.U[c.UL.Ul + h * D + (f - F)];
-  }
-  for (int x = threadIdx.x; x < D; x += blockDim.x) {
-    Tw[x] = c.params[c.L.te_w + x];
-    Tb[x] = c.params[c.L.te_b + x];
-  }
-  __syncthreads();
-  float cst[H];
+  const int F = c.F, D = c.D, d = c.d;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float Ur[NJ][H], tw[CT], tb[CT];
 #pragma unroll
-  for (int h = 0; h < H; ++h) cst[h] = c.U[c.UL.ce + h] + c.U[c.UL.cl + h];
+  for (int j = 0; j < CF; ++j) {
+    const int f = lane + 64 * j;
+#pragma unroll
+    for (int h = 0; h < H; ++h) Ur[j][h] = f < d ? c.U[c.UL.Ue + h * F + f] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < CT; ++j) {
+    const int i = lane + 64 * j;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      Ur[CF + j][h] = i < D ? c.U[c.UL.Ue + h * F + d + i] : 0.f;
+      Ur[CF + CT + j][h] = i < D ? c.U[c.UL.Ul + h * D + i] : 0.f;
+    }
+    tw[j] = i < D ? c.params[c.L.te_w + i] : 0.f;
+    tb[j] = i < D ? c.params[c.L.te_b + i] : 0.f;
+  }
+  const float cst = c.U[c.UL.ce + (lane >> 3)] + c.U[c.UL.cl + (lane >> 3)];
+  const EdgeCols<CF, CT> cols(lane, d, D);
   const int E = (int)c.ctl[TGNX_CTL_E];
-  const bool drop = c.drop;
-  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-  const int sub = threadIdx.x & 15;
-  for (int e = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; e < E; e += (gridDim.x * blockDim.x) >> 4) {
-    const EdgeMeta m = c.meta[e];
-    const float* fp = feat_row(c, m.frow);
-    const float* mu = c.mem + m.u * D;
-    float vf[NFEAT16], vm[NMEM16];
-#pragma unroll
-    for (int j = 0; j < NFEAT16; ++j) {
-      const int f = sub + 16 * j;
-      vf[j] = f < d ? (fp ? fp[f] : 1.0f) : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < NMEM16; ++j) {
-      const int k = sub + 16 * j;
-      vm[j] = k < D ? mu[k] : 0.f;
-    }
-    const uint32_t eb = m.eb, nb = m.nb;
+  auto math = [&](int e, const EdgeVals<CF, CT>& S) {
     float acc[H];
 #pragma unroll
     for (int h = 0; h < H; ++h) acc[h] = 0.f;
-    for (int f = d + sub; f < F; f += 16) {  // time encoding (model_utils.py:235, :447)
-      float x = te_cos(fmaf(Tw[f - d], m.dt, Tb[f - d]));
-      if (drop) x *= keep32(eb, (uint32_t)f, c.pf, c.inv_kf);
-      fma8(acc, &Us[f * H], x);
+#pragma unroll
+    for (int j = 0; j < CF; ++j) {
+      float x = S.vf[j];
+      if (DROP) x *= keep32(S.eb, (uint32_t)(lane + 64 * j), c.pf, c.inv_kf);
+#pragma unroll
+      for (int h = 0; h < H; ++h) acc[h] += Ur[j][h] * x;
     }
 #pragma unroll
-    for (int j = 0; j < NFEAT16; ++j) {
-      const int f = sub + 16 * j;
-      if (f < d) {
-        float x = vf[j];
-        if (drop) x *= keep32(eb, (uint32_t)f, c.pf, c.inv_kf);
-        fma8(acc, &Us[f * H], x);
-      }
+    for (int j = 0; j < CT; ++j) {  // time encoding (model_utils.py:235)
+      float x = te_cos(fmaf(tw[j], S.dt, tb[j]));
+      if (DROP) x *= keep32(S.eb, (uint32_t)(d + lane + 64 * j), c.pf, c.inv_kf);
+#pragma unroll
+      for (int h = 0; h < H; ++h) acc[h] += Ur[CF + j][h] * x;
     }
 #pragma unroll
-    for (int j = 0; j < NMEM16; ++j) {
-      const int k = sub + 16 * j;
-      if (k < D) {
-        float x = vm[j];
-        if (drop) x *= keep32(nb, (uint32_t)k, c.pf, c.inv_kf);
-        fma8(acc, &Us[(F + k) * H], x);
-      }
-    }
+    for (int j = 0; j < CT; ++j) {
+      float x = S.vm[j];
+      if (DROP) x *= keep32(S.nb, (uint32_t)(lane + 64 * j), c.pf, c.inv_kf);
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-      float x = acc[h];
-      x += __shfl_xor(x, 8, 16);
-      x += __shfl_xor(x, 4, 16);
-      x += __shfl_xor(x, 2, 16);
-      x += __shfl_xor(x, 1, 16);
-      acc[h] = x + cst[h];
+      for (int h = 0; h < H; ++h) acc[h] += Ur[CF + CT + j][h] * x;
     }
-    if (sub == 0) {
-      float4* xp = reinterpret_cast<float4*>(c.X + (int64_t)e * H);
-      xp[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-      xp[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-    }
+    const float s = wave_sum8(acc, lane);
+    if ((lane & 7) == 0) c.X[(int64_t)e * H + (lane >> 3)] = s + cst;
+  };
+  const int stride = gridDim.x * 4;
+  int e = blockIdx.x * 4 + wv;
+  EdgeVals<CF, CT> A, Bv;
+  if (e < E) edge_gather(c, e, cols, A);
+  while (e < E) {
+    const int e1 = e + stride;
+    if (e1 < E) edge_gather(c, e1, cols, Bv);
+    math(e, A);
+    if (e1 >= E) break;
+    const int e2 = e1 + stride;
+    if (e2 < E) edge_gather(c, e2, cols, A);
+    math(e1, Bv);
+    e = e2;
+  }
+}
+template <int CF>
+static void launch_edge_fwd_cf(const Ctx& c, hipStream_t s) {
+  const bool two = c.D > 64;
+  if (c.drop) two ? tgnn_edge_fwd<CF, 2, true><<<GFWD, 256, 0, s>>>(c) : tgnn_edge_fwd<CF, 1, true><<<GFWD, 256, 0, s>>>(c);
+  else two ? tgnn_edge_fwd<CF, 2, false><<<GFWD, 256, 0, s>>>(c) : tgnn_edge_fwd<CF, 1, false><<<GFWD, 256, 0, s>>>(c);
+}
+static void launch_edge_fwd(const Ctx& c, hipStream_t s) {
+  switch ((c.d + 63) / 64) {
+    case 0: launch_edge_fwd_cf<0>(c, s); break;
+    case 1: launch_edge_fwd_cf<1>(c, s); break;
+    case 2: launch_edge_fwd_cf<2>(c, s); break;
+    case 3: launch_edge_fwd_cf<3>(c, s); break;
+    case 4: launch_edge_fwd_cf<4>(c, s); break;
+    default: launch_edge_fwd_cf<5>(c, s); break;
   }
 }
 
@@ -937,12 +996,7 @@ __global__ void __launch_bounds__(64 * BWD_WAVES) tgnn_edge_bwd(Ctx c) {
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-  const float* ones = c.U + c.UL.ones;
-  int fidx[CF > 0 ? CF : 1], kidx[CT];
-#pragma unroll
-  for (int j = 0; j < CF; ++j) fidx[j] = min(lane + 64 * j, d - 1);
-#pragma unroll
-  for (int j = 0; j < CT; ++j) kidx[j] = min(lane + 64 * j, D - 1);
+  const EdgeCols<CF, CT> cols(lane, d, D);
   float aU[NJ][H], tw[CT], tb[CT], aw[CT], ab[CT], ac[H];
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
@@ -960,28 +1014,18 @@ __global__ void __launch_bounds__(64 * BWD_WAVES) tgnn_edge_bwd(Ctx c) {
   __syncthreads();
 
   struct Slot {
-    float dt, dx[H], vf[CF > 0 ? CF : 1], vm[CT];
-    uint32_t eb, nb;
+    EdgeVals<CF, CT> g;
+    float dx[H];
   };
-  // issue the loads of edge e into slot S (meta via scalar loads: e is wave-uniform)
   auto load = [&](int e, Slot& S) {
-    const EdgeMeta m = c.meta[e];
-    const float* fp = m.frow >= 0 ? c.feat + m.frow * d : m.frow == -1 ? ones : c.ev_msg + (-(m.frow + 2)) * d;
-    const float* mu = c.mem + m.u * D;
-#pragma unroll
-    for (int j = 0; j < CF; ++j) S.vf[j] = fp[fidx[j]];
-#pragma unroll
-    for (int j = 0; j < CT; ++j) S.vm[j] = mu[kidx[j]];
+    edge_gather(c, e, cols, S.g);
     load_x8(c.DX + (int64_t)e * H, S.dx);
-    S.dt = m.dt;
-    S.eb = m.eb;
-    S.nb = m.nb;
   };
   auto math = [&](const Slot& S) {
 #pragma unroll
     for (int j = 0; j < CF; ++j) {
-      float x = S.vf[j];
-      if (DROP) x *= keep32(S.eb, (uint32_t)(lane + 64 * j), c.pf, c.inv_kf);
+      float x = S.g.vf[j];
+      if (DROP) x *= keep32(S.g.eb, (uint32_t)(lane + 64 * j), c.pf, c.inv_kf);
 #pragma unroll
       for (int h = 0; h < H; ++h) aU[j][h] += S.dx[h] * x;
     }
@@ -989,8 +1033,8 @@ __global__ void __launch_bounds__(64 * BWD_WAVES) tgnn_edge_bwd(Ctx c) {
     for (int j = 0; j < CT; ++j) {  // time encoding dim i: x = cos(w_i dt + b_i)  (model_utils.py:235)
       const int i = lane + 64 * j;
       float sn, cs;
-      te_sincos(fmaf(tw[j], S.dt, tb[j]), sn, cs);
-      const float km = DROP ? keep32(S.eb, (uint32_t)(d + i), c.pf, c.inv_kf) : 1.f;
+      te_sincos(fmaf(tw[j], S.g.dt, tb[j]), sn, cs);
+      const float km = DROP ? keep32(S.g.eb, (uint32_t)(d + i), c.pf, c.inv_kf) : 1.f;
       const float x = cs * km;
 #pragma unroll
       for (int h = 0; h < H; ++h) aU[CF + j][h] += S.dx[h] * x;
@@ -999,13 +1043,13 @@ __global__ void __launch_bounds__(64 * BWD_WAVES) tgnn_edge_bwd(Ctx c) {
       const float denc = S.dx[0] * u0.x + S.dx[1] * u0.y + S.dx[2] * u0.z + S.dx[3] * u0.w +
                          S.dx[4] * u1.x + S.dx[5] * u1.y + S.dx[6] * u1.z + S.dx[7] * u1.w;
       const float gz = -denc * km * sn;
-      aw[j] += gz * S.dt;
+      aw[j] += gz * S.g.dt;
       ab[j] += gz;
     }
 #pragma unroll
     for (int j = 0; j < CT; ++j) {
-      float x = S.vm[j];
-      if (DROP) x *= keep32(S.nb, (uint32_t)(lane + 64 * j), c.pf, c.inv_kf);
+      float x = S.g.vm[j];
+      if (DROP) x *= keep32(S.g.nb, (uint32_t)(lane + 64 * j), c.pf, c.inv_kf);
 #pragma unroll
       for (int h = 0; h < H; ++h) aU[CF + CT + j][h] += S.dx[h] * x;
     }
@@ -1709,7 +1753,7 @@ static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
     TGNX_LAUNCH_CHECK("tgnn_collapse");
   }
   probe_begin(TGNX_K_EDGE_FWD, s);
-  tgnn_edge_fwd<<<edge_grid(c.Ecap), 256, 0, s>>>(c);
+  launch_edge_fwd(c, s);
   probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgnn_edge_fwd");
   probe_begin(TGNX_K_SEG_FWD, s);
