@@ -13,12 +13,12 @@ constexpr int INSERT_MAX_B = 4096;
 // both with e_id = cur + i.  Key = node << 32 | (B-1-i) << 1 | dir sorts node-ascending,
 // newest-first; runs of one node are merged with that node's ring row.
 
-// `smem` must hold next_pow2(2B)*8 + 2B*4 bytes, `sh` >= 20 ints; called by a whole workgroup.
-__device__ __forceinline__ void ring_insert_block(int64_t* __restrict__ nbr, int64_t* __restrict__ eid,
-                                                  float* __restrict__ rt, int K, const int64_t* __restrict__ src,
-                                                  const int64_t* __restrict__ dst, const float* __restrict__ ev_t,
-                                                  int B, int64_t cur, int64_t* __restrict__ assoc,
-                                                  unsigned char* smem, int* sh) {
+// Insert plan of one batch (LastNeighborLoader.insert, neighbor_loader.py:52-104): the 2B entries
+// (node << 32 | (B-1-i) << 1 | dir; dir 0 = dst side holding src, 1 = src side holding dst) sorted
+// in LDS so each node's run lists its new entries newest first; run_start[r] = first entry of run r.
+// Returns the number of runs.  Needs the whole workgroup.
+__device__ __forceinline__ int ring_plan_block(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int B,
+                                               unsigned char* smem, int* sh, uint64_t** key_out, int** runs_out) {
   const int n2 = 2 * B;
   const int n = next_pow2(n2);
   uint64_t* key = reinterpret_cast<uint64_t*>(smem);
@@ -35,7 +35,6 @@ __device__ __forceinline__ void ring_insert_block(int64_t* __restrict__ nbr, int
   }
   __syncthreads();
   sort_u64(key, reinterpret_cast<uint64_t*>(run_start + n2 + (n2 & 1)), n2, n);
-  // run starts -> run ids
   const int T = blockDim.x;
   int pc = (n2 + T - 1) / T;
   int p0 = threadIdx.x * pc, p1 = min(n2, p0 + pc);
@@ -46,45 +45,69 @@ __device__ __forceinline__ void ring_insert_block(int64_t* __restrict__ nbr, int
   for (int p = p0; p < p1; ++p)
     if (p == 0 || (key[p] >> 32) != (key[p - 1] >> 32)) run_start[rid++] = p;
   __syncthreads();
-  // one wave per node run: lanes [0,K) hold the old slots, lanes [K, K+m) the m newest new entries;
-  // each candidate's output slot is its rank by e_id (desc) and, separately, by t (desc) —
-  // top-K of [old | dense] exactly as neighbor_loader.py:91-104, with no per-thread arrays.
-  const int lane = threadIdx.x & 63, nwv = T >> 6;
+  *key_out = key;
+  *runs_out = run_start;
+  return U;
+}
+
+// Merge of run r (entries key[a, a+cnt), one node) into the node's ring, by one wave: lanes [0,K)
+// hold the old slots, lanes [K, K+m) the m = min(cnt, K) newest new entries; each candidate's slot
+// is its rank by e_id (desc) and, separately, by t (desc) — top-K of [old | dense] exactly as
+// neighbor_loader.py:91-104.  `key` may live in LDS or global memory.
+__device__ __forceinline__ void ring_merge_run(int64_t* __restrict__ nbr, int64_t* __restrict__ eid,
+                                               float* __restrict__ rt, int K, const int64_t* __restrict__ src,
+                                               const int64_t* __restrict__ dst, const float* __restrict__ ev_t, int B,
+                                               int64_t cur, int64_t* __restrict__ assoc, const uint64_t* key, int a,
+                                               int cnt, int r, int lane) {
+  const int64_t v = (int64_t)(key[a] >> 32);
+  if (lane == 0) assoc[v] = r;
+  const int m = cnt < K ? cnt : K;
+  int64_t* er = eid + v * K;
+  int64_t* nr = nbr + v * K;
+  float* tr = rt + v * K;
+  int64_t ce = INT64_MIN, cn = -1;
+  float ct = -INFINITY;
+  const bool cand = lane < K + m;
+  if (lane < K) {
+    ce = er[lane];
+    cn = nr[lane];
+    ct = tr[lane];
+  } else if (cand) {
+    const uint64_t kk = key[a + lane - K];
+    const int i = B - 1 - (int)((kk & 0xFFFFFFFFull) >> 1);
+    ce = cur + i;
+    cn = (kk & 1ull) == 0 ? src[i] : dst[i];
+    ct = ev_t[i];
+  }
+  int re = 0, rtk = 0;
+  for (int j = 0; j < K + m; ++j) {
+    const int64_t oe = __shfl(ce, j);
+    const float ot = __shfl(ct, j);
+    re += (oe > ce) || (oe == ce && j < lane);
+    rtk += (ot > ct) || (ot == ct && j < lane);
+  }
+  if (cand && re < K) {
+    er[re] = ce;
+    nr[re] = ce >= 0 ? cn : -1;
+  }
+  if (cand && rtk < K) tr[rtk] = ct;
+}
+
+// Whole insert in one workgroup (the standalone tgnx_ring_insert): plan, then a wave per run.
+__device__ __forceinline__ void ring_insert_block(int64_t* __restrict__ nbr, int64_t* __restrict__ eid,
+                                                  float* __restrict__ rt, int K, const int64_t* __restrict__ src,
+                                                  const int64_t* __restrict__ dst, const float* __restrict__ ev_t,
+                                                  int B, int64_t cur, int64_t* __restrict__ assoc,
+                                                  unsigned char* smem, int* sh) {
+  uint64_t* key;
+  int* run_start;
+  const int U = ring_plan_block(src, dst, B, smem, sh, &key, &run_start);
+  const int n2 = 2 * B;
+  const int lane = threadIdx.x & 63, nwv = blockDim.x >> 6;
   for (int r = threadIdx.x >> 6; r < U; r += nwv) {
     const int a = run_start[r];
-    const int c = (r + 1 < U ? run_start[r + 1] : n2) - a;
-    const int64_t v = (int64_t)(key[a] >> 32);
-    if (lane == 0) assoc[v] = r;
-    const int m = c < K ? c : K;
-    int64_t* er = eid + v * K;
-    int64_t* nr = nbr + v * K;
-    float* tr = rt + v * K;
-    int64_t ce = INT64_MIN, cn = -1;
-    float ct = -INFINITY;
-    const bool cand = lane < K + m;
-    if (lane < K) {
-      ce = er[lane];
-      cn = nr[lane];
-      ct = tr[lane];
-    } else if (cand) {
-      const uint64_t kk = key[a + lane - K];
-      const int i = B - 1 - (int)((kk & 0xFFFFFFFFull) >> 1);
-      ce = cur + i;
-      cn = (kk & 1ull) == 0 ? src[i] : dst[i];
-      ct = ev_t[i];
-    }
-    int re = 0, rtk = 0;
-    for (int j = 0; j < K + m; ++j) {
-      const int64_t oe = __shfl(ce, j);
-      const float ot = __shfl(ct, j);
-      re += (oe > ce) || (oe == ce && j < lane);
-      rtk += (ot > ct) || (ot == ct && j < lane);
-    }
-    if (cand && re < K) {
-      er[re] = ce;
-      nr[re] = ce >= 0 ? cn : -1;
-    }
-    if (cand && rtk < K) tr[rtk] = ct;
+    const int cnt = (r + 1 < U ? run_start[r + 1] : n2) - a;
+    ring_merge_run(nbr, eid, rt, K, src, dst, ev_t, B, cur, assoc, key, a, cnt, r, lane);
   }
   __syncthreads();
 }

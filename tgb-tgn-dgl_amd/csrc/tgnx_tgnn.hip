@@ -38,6 +38,8 @@ constexpr int GBWD = TGNX_GBWD;            // workgroups of the edge backward ke
 constexpr int BWD_WAVES = TGNX_BWD_WAVES;  // waves per edge backward workgroup
 constexpr int GSEG = 64;      // workgroups of the segment backward kernel
 constexpr int MRR_SLOTS = 65536;  // per-batch MRR ring in buffers.mrr
+constexpr int BATCH_MAX = 2048;   // max events per batch (touch sort capacity 3 * BATCH_MAX in LDS)
+enum { MISC_RUNS = 0, MISC_KMAX = 1, MISC_WORDS = 16 };
 
 // ------------------------------------------------------------------ layouts
 struct Lay {
@@ -162,6 +164,9 @@ struct Ctx {
   int* blk_rank;
   int* blk_order;
   float* HS;
+  uint64_t* rkeys;  // ring insert plan: sorted entries (2B)
+  int* rruns;       // run starts (U + 1)
+  int* misc;        // MISC_* scalars
   int64_t Ecap;
   int Bmax, Ge, Gs;
   Lay L;
@@ -375,21 +380,43 @@ __global__ void tgnn_seg_count(Ctx c) {
                                c.ctl[TGNX_CTL_BATCH_START], (int)c.ctl[TGNX_CTL_GEN]);
 }
 
-// ------------------------------------------------------------------ assembly (one workgroup)
-// Sorts the batch's node touches (src / dst / neg rows) by (node, block, kind, event), builds the
-// node map {gen, run start, run length, first s/p index}, the compacted s/p touch list (the
-// intra-batch edges of model_utils.py:151-152 in block order), per-block max t and block order.
+// ------------------------------------------------------------------ assembly (two workgroups)
+// Workgroup 0 sorts the batch's node touches (src / dst / neg rows) by (node, block, kind, event),
+// builds the node map {gen, run start, run length, first s/p index}, the compacted s/p touch list
+// (the intra-batch edges of model_utils.py:151-152 in block order), per-block max t and block
+// order, and (train) each segment's in-edge count + the edge offsets, all from the sorted touches in
+// LDS.  Workgroup 1 meanwhile builds the ring insert plan (neighbor_loader.py:52-104) that
+// tgnn_finish applies with a wave per node.
+// LDS of workgroup 0: sorted keys [next_pow2(NT)] u64 | run starts [NT] | run id per touch [NT] |
+// rank-sort scratch [1024] u64.
+__host__ __device__ inline size_t assemble_smem_bytes(int Bmax) {
+  const int NT = 3 * Bmax;
+  return (size_t)next_pow2(NT) * 8 + (size_t)NT * 8 + 1024 * 8;
+}
 template <bool TRAIN>
 __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int sh[20];
   const int B = (int)c.ctl[TGNX_CTL_B];
   const int tid = threadIdx.x, T = blockDim.x;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  if (blockIdx.x == 1) {  // ring insert plan
+    if (B == 0 || B > c.Bmax) return;
+    uint64_t* key;
+    int* runs;
+    const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs);
+    for (int p = tid; p < 2 * B; p += T) c.rkeys[p] = key[p];
+    for (int r = tid; r < U; r += T) c.rruns[r] = runs[r];
+    if (tid == 0) {
+      c.rruns[U] = 2 * B;
+      c.misc[MISC_RUNS] = U;
+    }
+    return;
+  }
   if (B == 0) {
     if (tid == 0) c.ctl[TGNX_CTL_S] = c.ctl[TGNX_CTL_E] = 0;
     return;
   }
-  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   const int gen = (int)c.ctl[TGNX_CTL_GEN];
   const int64_t* src = c.ev_src + start;
   const int64_t* dst = c.ev_dst + start;
@@ -397,14 +424,16 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   const int64_t* blk = c.ev_blk + start;
   const int64_t* neg = c.neg + start * c.Kn;
   const int NT = TRAIN ? 3 * B : 2 * B;
-  if (NT > TOUCH_MAX || B > c.Bmax || B > 4095) {
+  if (B > c.Bmax || B > 4095) {
     if (tid == 0) c.ctl[TGNX_CTL_ERR] |= 1;
     return;
   }
   const int n = next_pow2(NT);
+  const int NTc = 3 * c.Bmax;
   uint64_t* key = reinterpret_cast<uint64_t*>(smem);
-  int* run_start = reinterpret_cast<int*>(smem + (size_t)TOUCH_MAX * 8);
-  uint64_t* tmp = reinterpret_cast<uint64_t*>(smem + (size_t)TOUCH_MAX * 12);
+  int* run_start = reinterpret_cast<int*>(smem + (size_t)next_pow2(NTc) * 8);
+  int* run_of = run_start + NTc;
+  uint64_t* tmp = reinterpret_cast<uint64_t*>(run_of + NTc);
   if (TRAIN && c.gen_neg) {  // NegLinkSamplerDest.sample (neg_sampler.py:8-23), counter-based stream
     const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
     const uint64_t off = (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
@@ -446,19 +475,42 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     }
     if (tid == 0) c.sp_pref[NT] = tot;
   }
-  // node runs -> node map
+  // node runs -> node map; run id of every touch
   {
     int cnt = 0;
     for (int p = p0; p < p1; ++p) cnt += (p == 0 || knode(key[p]) != knode(key[p - 1]));
     int U;
     int rid = block_excl_scan(cnt, sh, &U);
-    for (int p = p0; p < p1; ++p)
+    for (int p = p0; p < p1; ++p) {
       if (p == 0 || knode(key[p]) != knode(key[p - 1])) run_start[rid++] = p;
+      run_of[p] = rid - 1;
+    }
     __syncthreads();
     for (int r = tid; r < U; r += T) {
       const int a = run_start[r];
       const int e = r + 1 < U ? run_start[r + 1] : NT;
       c.nodemap[knode(key[a])] = make_int4(gen, a, e - a, c.sp_pref[a]);
+    }
+  }
+  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
+  const int nloc = hi - lo;
+  const int S = nloc * (2 + c.Kn);
+  if (TRAIN) {  // in-edge count of each segment (= touch p of this rank's rows, Kn == 1):
+    // ring fill + self loop + s/p touches of the node in earlier blocks = sp_pref[first touch of
+    // (node, block)] - sp_pref[run start]
+    for (int p = tid; p < NT; p += T) {
+      const uint64_t k = key[p];
+      const int ev = kev(k);
+      if (ev < lo || ev >= hi) continue;
+      const int kind = kkind(k);
+      const int w = kind == 2 ? ev - lo : kind == 1 ? nloc + ev - lo : 2 * nloc + (ev - lo);
+      int g = p;
+      while (g > 0 && (key[g - 1] >> 14) == (k >> 14)) --g;
+      const int64_t v = knode(k);
+      int nring = 0;
+      for (int j = 0; j < c.K; ++j) nring += c.eid[v * c.K + j] >= 0;
+      const int nintra = c.sp_pref[g] - c.sp_pref[run_start[run_of[p]]];
+      c.seg_cnt[w] = nring | (nintra << 8);
     }
   }
   __syncthreads();
@@ -476,16 +528,13 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     c.blk_rank[e] = r;
     c.blk_order[r] = e;
   }
-  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
-  const int S = (hi - lo) * (2 + c.Kn);
-  if (TRAIN) {  // segments are few (3 per event): counts + offsets here, no extra launches
-    __syncthreads();
+  if (tid == 0) c.misc[MISC_KMAX] = (int)(key[B - 1] >> 12);
+  if (TRAIN) {  // segment edge offsets
     const int chunk = (S + T - 1) / T;
     const int r0 = tid * chunk, r1 = min(S, r0 + chunk);
     int s = 0;
     for (int r = r0; r < r1; ++r) {
-      const int v = seg_count_one(c, r, lo, hi, start, gen);
-      c.seg_cnt[r] = v;
+      const int v = c.seg_cnt[r];
       s += (v & 255) + 1 + (v >> 8);
     }
     int tot;
@@ -1440,46 +1489,45 @@ __global__ void tgnn_adam(Ctx c) {
   }
 }
 
-// ------------------------------------------------------------------ finish: time_assoc + ring insert (1 WG)
+// End of a step (many workgroups): time_assoc of the touched nodes (model_utils.py:77-83), the ring
+// insert of the whole batch with a wave per node run of tgnn_assemble's plan, the loss sum.
 template <bool TRAIN>
-__global__ void __launch_bounds__(1024) tgnn_finish(Ctx c) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ int sh[20];
+__global__ void __launch_bounds__(256) tgnn_finish(Ctx c) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   const float* evt = c.ev_t + start;
   const int NT = TRAIN ? 3 * B : 2 * B;
-  if (TRAIN) {  // final time_assoc = last assignment of each touched node (model_utils.py:81-83)
-    for (int j = threadIdx.x; j < NT; j += blockDim.x) {
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
+  if (TRAIN) {  // final time_assoc = last assignment of each touched node
+    for (int j = gt; j < NT; j += gs) {
       const uint64_t k = c.touches[j];
       if (j == NT - 1 || knode(c.touches[j + 1]) != knode(k)) c.ta[knode(k)] = evt[kev(k)];
     }
-  } else {      // after tgnn_ta_fill: s/p of the last block keep their own t (model_utils.py:79-83)
-    int kmax = 0;
-    for (int e = 0; e < B; ++e) kmax = max(kmax, (int)c.ev_blk[start + e]);
-    for (int j = threadIdx.x; j < NT; j += blockDim.x) {
+  } else {      // after tgnn_ta_fill: s/p of the last block keep their own t, the later assignment
+    const int kmax = c.misc[MISC_KMAX];  // (s after p, batch order) wins = last of its (node, block) group
+    for (int j = gt; j < NT; j += gs) {
       const uint64_t k = c.touches[j];
-      if (kblk(k) == kmax) c.ta[knode(k)] = evt[kev(k)];
+      if (kblk(k) == kmax && (j == NT - 1 || (c.touches[j + 1] >> 14) != (k >> 14))) c.ta[knode(k)] = evt[kev(k)];
     }
   }
-  ring_insert_block(c.nbr, c.eid, c.rt, c.K, c.ev_src + start, c.ev_dst + start, evt, B,
-                    c.ctl[TGNX_CTL_CUR_EID], c.assoc, smem, sh);
-  if (threadIdx.x == 0) {
-    if (TRAIN) {
-      double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
-      *loss += (double)c.grads[c.L.total] * (double)B;
-    }
+  const int U = c.misc[MISC_RUNS];
+  const int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r < U) {
+    const int a = c.rruns[r];
+    ring_merge_run(c.nbr, c.eid, c.rt, c.K, c.ev_src + start, c.ev_dst + start, evt, B, c.ctl[TGNX_CTL_CUR_EID],
+                   c.assoc, c.rkeys, a, c.rruns[r + 1] - a, r, threadIdx.x & 63);
+  }
+  if (TRAIN && gt == 0) {
+    double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
+    *loss += (double)c.grads[c.L.total] * (double)B;
   }
 }
 
 __global__ void tgnn_ta_fill(Ctx c) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
-  int kmax = 0;
-  for (int e = 0; e < B; ++e) kmax = max(kmax, (int)c.ev_blk[start + e]);
-  const float v = c.blkmax[kmax];
+  const float v = c.blkmax[c.misc[MISC_KMAX]];
   for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < c.N; x += (int64_t)gridDim.x * blockDim.x)
     c.ta[x] = v;
 }
@@ -1596,7 +1644,7 @@ static size_t carve(size_t& off, size_t bytes) {
 
 struct WsLay {
   size_t touches, sp_pref, sp_keys, seg_cnt, seg_eoff, seg_out, seg_stats, seg_g, X, DX, meta, U, evs, slabs,
-      slabs_s, red, blkmax, blk_rank, blk_order, HS, total;
+      slabs_s, red, blkmax, blk_rank, blk_order, HS, rkeys, rruns, misc, total;
   int64_t Ecap, Scap;
 };
 static WsLay make_ws(const tgnx_tgnn_config* cfg) {
@@ -1628,6 +1676,9 @@ static WsLay make_ws(const tgnx_tgnn_config* cfg) {
   W.blk_rank = carve(off, (size_t)B * 4);
   W.blk_order = carve(off, (size_t)B * 4);
   W.HS = carve(off, (size_t)B * D * 4);
+  W.rkeys = carve(off, (size_t)2 * B * 8);
+  W.rruns = carve(off, (size_t)(2 * B + 2) * 4);
+  W.misc = carve(off, (size_t)MISC_WORDS * 4);
   W.total = off;
   return W;
 }
@@ -1639,8 +1690,8 @@ static int check_cfg(const tgnx_tgnn_config* cfg) {
   TGNX_CHECK_ARG(cfg->msg_dim >= 0 && cfg->msg_dim + cfg->mem_dim <= FMAX, "tgnn: msg_dim + mem_dim must be <= %d",
                  FMAX);
   TGNX_CHECK_ARG(cfg->ring > 0 && cfg->ring <= KMAX && cfg->ring <= 64, "tgnn: ring size must be in [1, %d]", KMAX);
-  TGNX_CHECK_ARG(cfg->max_batch > 0 && 3 * cfg->max_batch <= TOUCH_MAX, "tgnn: max_batch must be in [1, %d]",
-                 TOUCH_MAX / 3);
+  TGNX_CHECK_ARG(cfg->max_batch > 0 && cfg->max_batch <= BATCH_MAX, "tgnn: max_batch must be in [1, %d]",
+                 BATCH_MAX);
   TGNX_CHECK_ARG(cfg->num_nodes > 0 && cfg->num_nodes < (1ll << 37), "tgnn: bad num_nodes");
   return TGNX_OK;
 }
@@ -1711,6 +1762,9 @@ static int make_ctx(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* b, int
   c.blk_rank = reinterpret_cast<int*>(ws + W.blk_rank);
   c.blk_order = reinterpret_cast<int*>(ws + W.blk_order);
   c.HS = reinterpret_cast<float*>(ws + W.HS);
+  c.rkeys = reinterpret_cast<uint64_t*>(ws + W.rkeys);
+  c.rruns = reinterpret_cast<int*>(ws + W.rruns);
+  c.misc = reinterpret_cast<int*>(ws + W.misc);
   c.Ecap = W.Ecap;
   c.Bmax = cfg->max_batch;
   c.Ge = GBWD;
@@ -1723,7 +1777,6 @@ static int make_ctx(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* b, int
 
 static inline int grid_for(int64_t n, int per) { return (int)((n + per - 1) / per); }
 
-static size_t assemble_smem() { return (size_t)TOUCH_MAX * 12 + (size_t)1024 * 8; }
 
 static int edge_grid(int64_t Ecap) {
   const int64_t g = (Ecap * 16 + 255) / 256;
@@ -1734,7 +1787,7 @@ static int edge_grid(int64_t Ecap) {
 template <bool TRAIN>
 static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
   probe_begin(TGNX_K_ASSEMBLE, s);
-  tgnn_assemble<TRAIN><<<1, 1024, assemble_smem(), s>>>(c);
+  tgnn_assemble<TRAIN><<<2, 1024, assemble_smem_bytes(c.Bmax), s>>>(c);
   probe_end(TGNX_K_ASSEMBLE, s);
   TGNX_LAUNCH_CHECK("tgnn_assemble");
   if (!TRAIN) {
@@ -1859,7 +1912,7 @@ int tgnx_tgnn_train_update(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers*
   probe_end(TGNX_K_ADAM, s);
   TGNX_LAUNCH_CHECK("tgnn_adam");
   probe_begin(TGNX_K_FINISH, s);
-  tgnn_finish<true><<<1, 1024, ring_insert_smem_bytes(cfg->max_batch), s>>>(c);
+  tgnn_finish<true><<<(2 * cfg->max_batch + 3) / 4, 256, 0, s>>>(c);
   probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgnn_finish");
   return TGNX_OK;
@@ -1887,7 +1940,7 @@ int tgnx_tgnn_eval_step(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* bu
   TGNX_LAUNCH_CHECK("tgnn_mrr");
   tgnn_ta_fill<<<grid_for(cfg->num_nodes, 256) < 4096 ? grid_for(cfg->num_nodes, 256) : 4096, 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgnn_ta_fill");
-  tgnn_finish<false><<<1, 1024, ring_insert_smem_bytes(cfg->max_batch), s>>>(c);
+  tgnn_finish<false><<<(2 * cfg->max_batch + 3) / 4, 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgnn_finish");
   return TGNX_OK;
 }
