@@ -183,6 +183,11 @@ typedef struct {
 
 int tgnx_tgnn_param_layout(const tgnx_tgnn_config* cfg, int64_t* offsets /* [TGNX_TGNN_NPARAM+1] */);
 size_t tgnx_tgnn_ws_bytes(const tgnx_tgnn_config* cfg);
+/* Byte offset in ws of the int32[TGNX_MISC_WORDS] per-step diagnostics block: [0] node runs of the
+ * ring insert plan, [1] last block id; int64 phase timestamps (wall clock) from [16] in builds with
+ * -DTGNX_TIMING.  Measurement only. */
+#define TGNX_MISC_WORDS 64
+size_t tgnx_tgnn_ws_misc_offset(const tgnx_tgnn_config* cfg);
 
 /* Set up the next batch.  mode 0: explicit (batch_start, B, cur_e_id as given);
  * mode 1: resident (next consecutive batch of `batch` events in [split_lo, split_hi),
@@ -193,11 +198,12 @@ int tgnx_tgnn_advance(int64_t* ctl, int32_t mode, int64_t batch_start, int64_t B
                       uint64_t base_seed, int32_t train, void* stream);
 
 /* Train step, part 1 (epoch_utils.py:196-303 up to loss.backward): negatives (if gen_neg),
- * assembly, collapsed forward, predictor + BCE, backward; writes grads (+ loss slot). */
+ * assembly, collapsed forward, predictor + BCE, backward; writes grads (+ loss slot).  Also applies
+ * the batch's neighbor_loader.insert + time_assoc update (epoch_utils.py:304, model_utils.py:81-83)
+ * once the forward has read them (nothing later in the step does). */
 int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t gen_neg,
                             int32_t dropout, void* stream);
-/* Train step, part 2 (optimizer.step + neighbor_loader.insert + time_assoc): Adam on the
- * (possibly all-reduced) grads, ring insert of the whole batch, time_assoc update, loss sum. */
+/* Train step, part 2 (optimizer.step): Adam on the (possibly all-reduced) grads, loss sum. */
 int tgnx_tgnn_train_update(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, void* stream);
 /* Eval step (epoch_utils.py:28-157): Kn negatives per event, logits in block order,
  * per-batch MRR (TGB rank rule), insert, time_assoc as model_utils.py:77-83 leaves it.

@@ -112,23 +112,68 @@ __device__ __forceinline__ void bitonic_sort_u64(uint64_t* key, int n) {
   }
 }
 
-// Sort n distinct uint64 keys in LDS, ascending, by the whole block: barrier-free rank sort
-// (each key's slot = number of smaller keys) for n <= 1024, bitonic above.  `tmp` holds n keys.
-__device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, int n_pow2) {
-  if (n <= 1024) {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) tmp[i] = key[i];
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-      const uint64_t k = tmp[i];
-      int r = 0;
-      for (int j = 0; j < n; ++j) r += tmp[j] < k;
-      key[r] = k;
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const unsigned lo = __shfl_xor((unsigned)v, m, WAVE), hi = __shfl_xor((unsigned)(v >> 32), m, WAVE);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// lane i <- lane i ^ J, picking the cheapest cross-lane path for each distance: DPP quad_perm
+// (1, 2), DPP row_ror:8 (8), ds_swizzle xor mode within 32 lanes (4, 16), bpermute (32).
+template <int J>
+__device__ __forceinline__ unsigned xlane_xor(unsigned v) {
+  if constexpr (J == 1) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  else if constexpr (J == 2) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  else if constexpr (J == 8) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
+  else if constexpr (J < 32) return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (J << 10));
+  else return __shfl_xor(v, J, WAVE);
+}
+template <int J>
+__device__ __forceinline__ uint64_t bitonic_lane_stage(uint64_t v, int i, int k) {
+  const unsigned lo = xlane_xor<J>((unsigned)v), hi = xlane_xor<J>((unsigned)(v >> 32));
+  const uint64_t o = ((uint64_t)hi << 32) | lo;
+  const bool take_min = ((i & J) == 0) == ((i & k) == 0);
+  return take_min ? (o < v ? o : v) : (o > v ? o : v);
+}
+
+// Bitonic sort of n (power of two, n <= blockDim.x) uint64 keys, ascending, one key per thread in
+// registers: partner distances < 64 exchange across lanes (no barrier), larger ones through LDS,
+// ping-ponging between `key` and `tmp` so each such stage needs a single barrier.
+// For n = 1024: 45 cross-lane stages, 10 LDS stages.  Result in key[0, n).
+__device__ __forceinline__ void sort_u64_reg(uint64_t* key, uint64_t* tmp, int n) {
+  const int i = threadIdx.x;
+  uint64_t v = i < n ? key[i] : ~0ull;
+  int flip = 0;
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j >= WAVE; j >>= 1) {
+      uint64_t* buf = flip ? tmp : key;
+      flip ^= 1;
+      if (i < n) buf[i] = v;
+      __syncthreads();
+      const uint64_t o = i < n ? buf[i ^ j] : v;
+      const bool take_min = ((i & j) == 0) == ((i & k) == 0);
+      v = take_min ? (o < v ? o : v) : (o > v ? o : v);
     }
-    for (int i = n + threadIdx.x; i < n_pow2; i += blockDim.x) key[i] = ~0ull;
-    __syncthreads();
-  } else {
-    bitonic_sort_u64(key, n_pow2);
+    switch (k >= 64 ? 32 : k >> 1) {  // remaining distances 32..1 (wave-uniform)
+      case 32: v = bitonic_lane_stage<32>(v, i, k); [[fallthrough]];
+      case 16: v = bitonic_lane_stage<16>(v, i, k); [[fallthrough]];
+      case 8: v = bitonic_lane_stage<8>(v, i, k); [[fallthrough]];
+      case 4: v = bitonic_lane_stage<4>(v, i, k); [[fallthrough]];
+      case 2: v = bitonic_lane_stage<2>(v, i, k); [[fallthrough]];
+      default: v = bitonic_lane_stage<1>(v, i, k);
+    }
   }
+  __syncthreads();
+  if (i < n) key[i] = v;
+  __syncthreads();
+}
+
+// Sort n uint64 keys in LDS, ascending, by the whole block (key[n, n_pow2) padded with ~0 on
+// return): register bitonic when n_pow2 <= blockDim.x (`tmp` holds n_pow2 keys), LDS bitonic above.
+__device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, int n_pow2) {
+  for (int i = n + threadIdx.x; i < n_pow2; i += blockDim.x) key[i] = ~0ull;
+  __syncthreads();
+  if (n_pow2 <= (int)blockDim.x) sort_u64_reg(key, tmp, n_pow2);
+  else bitonic_sort_u64(key, n_pow2);
 }
 
 __host__ __device__ __forceinline__ int next_pow2(int v) {

@@ -113,8 +113,9 @@ __device__ __forceinline__ void ring_insert_block(int64_t* __restrict__ nbr, int
 }
 
 __host__ __device__ __forceinline__ size_t ring_insert_smem_bytes(int B) {
-  // keys + run starts (+ rank-sort scratch for 2B <= 1024)
-  return (size_t)next_pow2(2 * B) * 8 + (size_t)(2 * B + 2) * 4 + (2 * B <= 1024 ? (size_t)2 * B * 8 : 0);
+  // keys + run starts (+ register-sort ping-pong buffer for next_pow2(2B) <= 1024)
+  const int n = next_pow2(2 * B);
+  return (size_t)n * 8 + (size_t)(2 * B + 2) * 4 + (n <= 1024 ? (size_t)n * 8 : 0);
 }
 
 }  // namespace tgnx

@@ -39,7 +39,13 @@ constexpr int BWD_WAVES = TGNX_BWD_WAVES;  // waves per edge backward workgroup
 constexpr int GSEG = 64;      // workgroups of the segment backward kernel
 constexpr int MRR_SLOTS = 65536;  // per-batch MRR ring in buffers.mrr
 constexpr int BATCH_MAX = 2048;   // max events per batch (touch sort capacity 3 * BATCH_MAX in LDS)
-enum { MISC_RUNS = 0, MISC_KMAX = 1, MISC_WORDS = 16 };
+enum { MISC_RUNS = 0, MISC_KMAX = 1, MISC_STAMPS = 16, MISC_WORDS = TGNX_MISC_WORDS };
+#ifdef TGNX_TIMING  // phase timestamps of the single-workgroup kernels (measurement builds only)
+#define TGNX_STAMP(c, i) \
+  do { if (threadIdx.x == 0) reinterpret_cast<int64_t*>((c).misc + MISC_STAMPS)[i] = (int64_t)wall_clock64(); } while (0)
+#else
+#define TGNX_STAMP(c, i) do {} while (0)
+#endif
 
 // ------------------------------------------------------------------ layouts
 struct Lay {
@@ -258,10 +264,10 @@ __global__ void tgnn_advance(int64_t* ctl, int mode, int64_t batch_start, int64_
 // U = attn·W per head (exact collapse of EdgeGATConv's el/er/ee), predictor transposes/row sums.
 // Blocks [0, nb_dot): 64 outputs of U_e / U_l / U_r x 4 split-d waves (coalesced over outputs);
 // then 4 row sums per block (wave each, lanes over the row); then the two predictor transposes.
-__device__ __forceinline__ int collapse_dot_blocks(const Ctx& c) {
-  return (H * c.F + 63) / 64 + 2 * ((H * c.D + 63) / 64);
+__host__ __device__ inline int collapse_blocks(const Ctx& c) {
+  return (H * c.F + 63) / 64 + 2 * ((H * c.D + 63) / 64) + (3 * H + 2 * c.D + 3) / 4 + 64;
 }
-__global__ void __launch_bounds__(256) tgnn_collapse(Ctx c) {
+__device__ void collapse_body(const Ctx& c, const int bid, const int nblk) {
   __shared__ float part[4][64];
   const int D = c.D, F = c.F;
   const float* P = c.params;
@@ -270,9 +276,9 @@ __global__ void __launch_bounds__(256) tgnn_collapse(Ctx c) {
   const int nb_dot = nbe + 2 * nbl;
   const int nrow = 3 * H + 2 * D;
   const int nb_row = (nrow + 3) / 4;
-  if (blockIdx.x == 0)
+  if (bid == 0)
     for (int i = threadIdx.x; i < FMAX; i += blockDim.x) c.U[c.UL.ones + i] = 1.0f;
-  int b = blockIdx.x;
+  int b = bid;
   if (b < nb_dot) {
     int which, o;
     if (b < nbe) { which = 0; o = b * 64 + lane; }
@@ -318,7 +324,7 @@ __global__ void __launch_bounds__(256) tgnn_collapse(Ctx c) {
   }
   b -= nb_row;
   const int64_t nP = (int64_t)D * D;
-  for (int64_t x = (int64_t)b * blockDim.x + threadIdx.x; x < 2 * nP; x += (int64_t)(gridDim.x - nb_dot - nb_row) * blockDim.x) {
+  for (int64_t x = (int64_t)b * blockDim.x + threadIdx.x; x < 2 * nP; x += (int64_t)(nblk - nb_dot - nb_row) * blockDim.x) {
     const int which = (int)(x / nP);
     const int64_t z = x % nP;
     const int dd = (int)(z / D), o = (int)(z % D);
@@ -387,8 +393,9 @@ __global__ void tgnn_seg_count(Ctx c) {
 // order, and (train) each segment's in-edge count + the edge offsets, all from the sorted touches in
 // LDS.  Workgroup 1 meanwhile builds the ring insert plan (neighbor_loader.py:52-104) that
 // tgnn_finish applies with a wave per node.
+// Workgroup 2 computes the per-block max t and the stable block order.
 // LDS of workgroup 0: sorted keys [next_pow2(NT)] u64 | run starts [NT] | run id per touch [NT] |
-// rank-sort scratch [1024] u64.
+// register-sort ping-pong buffer [1024] u64.
 __host__ __device__ inline size_t assemble_smem_bytes(int Bmax) {
   const int NT = 3 * Bmax;
   return (size_t)next_pow2(NT) * 8 + (size_t)NT * 8 + 1024 * 8;
@@ -402,15 +409,39 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   if (blockIdx.x == 1) {  // ring insert plan
     if (B == 0 || B > c.Bmax) return;
+    TGNX_STAMP(c, 8);
     uint64_t* key;
     int* runs;
     const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs);
+    TGNX_STAMP(c, 9);
     for (int p = tid; p < 2 * B; p += T) c.rkeys[p] = key[p];
     for (int r = tid; r < U; r += T) c.rruns[r] = runs[r];
     if (tid == 0) {
       c.rruns[U] = 2 * B;
       c.misc[MISC_RUNS] = U;
     }
+    TGNX_STAMP(c, 10);
+    return;
+  }
+  if (blockIdx.x == 2) {  // per-block max t (eval's time_assoc[:] = max, model_utils.py:78), block order
+    if (B == 0 || B > c.Bmax) return;
+    const int64_t* blk = c.ev_blk + start;
+    const float* evt = c.ev_t + start;
+    uint64_t* key = reinterpret_cast<uint64_t*>(smem);
+    float* bmax = c.blkmax;
+    for (int b = tid; b < B; b += T) bmax[b] = -INFINITY;
+    __syncthreads();
+    for (int e = tid; e < B; e += T) atomicMax(&bmax[(int)blk[e]], evt[e]);
+    const int nb = next_pow2(B);
+    for (int p = tid; p < nb; p += T) key[p] = p < B ? (((uint64_t)blk[p] << 12) | (uint64_t)p) : ~0ull;
+    __syncthreads();
+    sort_u64(key, key + nb, B, nb);
+    for (int r = tid; r < B; r += T) {
+      const int e = (int)(key[r] & 4095u);
+      c.blk_rank[e] = r;
+      c.blk_order[r] = e;
+    }
+    if (tid == 0) c.misc[MISC_KMAX] = (int)(key[B - 1] >> 12);
     return;
   }
   if (B == 0) {
@@ -434,6 +465,7 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   int* run_start = reinterpret_cast<int*>(smem + (size_t)next_pow2(NTc) * 8);
   int* run_of = run_start + NTc;
   uint64_t* tmp = reinterpret_cast<uint64_t*>(run_of + NTc);
+  TGNX_STAMP(c, 0);
   if (TRAIN && c.gen_neg) {  // NegLinkSamplerDest.sample (neg_sampler.py:8-23), counter-based stream
     const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
     const uint64_t off = (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
@@ -459,7 +491,9 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     key[p] = k;
   }
   __syncthreads();
+  TGNX_STAMP(c, 1);
   sort_u64(key, tmp, NT, n);
+  TGNX_STAMP(c, 2);
   const int pc = (NT + T - 1) / T;
   const int p0 = tid * pc, p1 = min(NT, p0 + pc);
   // compacted s/p list (kind != 0), exclusive prefix over the sorted touches
@@ -475,6 +509,7 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     }
     if (tid == 0) c.sp_pref[NT] = tot;
   }
+  TGNX_STAMP(c, 3);
   // node runs -> node map; run id of every touch
   {
     int cnt = 0;
@@ -492,6 +527,7 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
       c.nodemap[knode(key[a])] = make_int4(gen, a, e - a, c.sp_pref[a]);
     }
   }
+  TGNX_STAMP(c, 4);
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
   const int nloc = hi - lo;
   const int S = nloc * (2 + c.Kn);
@@ -514,22 +550,9 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     }
   }
   __syncthreads();
-  // per-block max t (eval's time_assoc[:] = max, model_utils.py:78) and stable block order
-  float* bmax = c.blkmax;
-  for (int b = tid; b < B; b += T) bmax[b] = -INFINITY;
-  __syncthreads();
-  for (int e = tid; e < B; e += T) atomicMax(&bmax[(int)blk[e]], evt[e]);
-  const int nb = next_pow2(B);
-  for (int p = tid; p < nb; p += T) key[p] = p < B ? (((uint64_t)blk[p] << 12) | (uint64_t)p) : ~0ull;
-  __syncthreads();
-  sort_u64(key, tmp, B, nb);
-  for (int r = tid; r < B; r += T) {
-    const int e = (int)(key[r] & 4095u);
-    c.blk_rank[e] = r;
-    c.blk_order[r] = e;
-  }
-  if (tid == 0) c.misc[MISC_KMAX] = (int)(key[B - 1] >> 12);
-  if (TRAIN) {  // segment edge offsets
+  TGNX_STAMP(c, 5);
+  TGNX_STAMP(c, 6);
+  if (TRAIN) {  // segment edge offsets (seg_cnt written above by this workgroup)
     const int chunk = (S + T - 1) / T;
     const int r0 = tid * chunk, r1 = min(S, r0 + chunk);
     int s = 0;
@@ -556,6 +579,7 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     c.ctl[TGNX_CTL_S] = S;
     c.ctl[TGNX_CTL_E] = -1;   // counted by tgnn_seg_count / tgnn_seg_scan
   }
+  TGNX_STAMP(c, 7);
 }
 
 // exclusive scan of the edge counts (one workgroup) -> edge offsets
@@ -590,7 +614,7 @@ __global__ void __launch_bounds__(1024) tgnn_seg_scan(Ctx c) {
 
 // one thread per edge: source node, feature row, dt = t_edge - time_assoc[src] as of the block
 template <bool TRAIN>
-__global__ void tgnn_edge_meta(Ctx c) {
+__device__ void edge_meta_body(const Ctx& c, const int bid, const int nblk) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int S = (int)c.ctl[TGNX_CTL_S];
@@ -599,7 +623,7 @@ __global__ void tgnn_edge_meta(Ctx c) {
   const int lo_ev = (int)c.ctl[TGNX_CTL_LO], hi_ev = (int)c.ctl[TGNX_CTL_HI];
   const int gen = (int)c.ctl[TGNX_CTL_GEN];
   const float* evt = c.ev_t + start;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) {
+  for (int e = bid * blockDim.x + threadIdx.x; e < E; e += nblk * blockDim.x) {
     int lo = 0, hi = S;  // last w with eoff[w] <= e
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -642,6 +666,14 @@ __global__ void tgnn_edge_meta(Ctx c) {
     }
     c.meta[e] = m;
   }
+}
+
+// edge metadata and the collapsed weights (independent) in one launch: blocks [0, nmeta) then the
+// collapse blocks
+template <bool TRAIN>
+__global__ void __launch_bounds__(256) tgnn_meta_collapse(Ctx c, int nmeta) {
+  if ((int)blockIdx.x < nmeta) edge_meta_body<TRAIN>(c, blockIdx.x, nmeta);
+  else collapse_body(c, blockIdx.x - nmeta, gridDim.x - nmeta);
 }
 
 __device__ __forceinline__ const float* feat_row(const Ctx& c, int64_t frow) {
@@ -743,6 +775,9 @@ __device__ __forceinline__ float wave_sum8(const float (&v)[H], int lane) {
 // x_eh = U_e[h]·[efeat_e, drop(cos(w dt + b))] + U_l[h]·drop(mem[src]) + c_h   (model_utils.py:447-452
 // collapsed): a wave per edge, each lane's U columns held in registers across
 // edges, two gather sets ping-pong so one edge's loads are in flight during the other's math.
+template <bool TRAIN>
+__device__ void finish_body(const Ctx& c, const int bid, const int nblk);
+
 #ifndef TGNX_GFWD
 #define TGNX_GFWD 512
 #endif
@@ -750,6 +785,11 @@ constexpr int GFWD = TGNX_GFWD;
 template <int CF, int CT, bool DROP>
 __global__ void __launch_bounds__(256) tgnn_edge_fwd(Ctx c) {
   constexpr int NJ = CF + 2 * CT;
+  if ((int)blockIdx.x >= GFWD) {  // train: the batch's ring insert + time_assoc update (nothing after
+    // tgnn_edge_meta reads them; epoch_utils.py:304, model_utils.py:81-83) rides in this launch
+    finish_body<true>(c, blockIdx.x - GFWD, gridDim.x - GFWD);
+    return;
+  }
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int F = c.F, D = c.D, d = c.d;
@@ -804,7 +844,7 @@ __global__ void __launch_bounds__(256) tgnn_edge_fwd(Ctx c) {
     const float s = wave_sum8(acc, lane);
     if ((lane & 7) == 0) c.X[(int64_t)e * H + (lane >> 3)] = s + cst;
   };
-  const int stride = gridDim.x * 4;
+  const int stride = GFWD * 4;
   int e = blockIdx.x * 4 + wv;
   EdgeVals<CF, CT> A, Bv;
   if (e < E) edge_gather(c, e, cols, A);
@@ -820,19 +860,20 @@ __global__ void __launch_bounds__(256) tgnn_edge_fwd(Ctx c) {
   }
 }
 template <int CF>
-static void launch_edge_fwd_cf(const Ctx& c, hipStream_t s) {
+static void launch_edge_fwd_cf(const Ctx& c, int nfin, hipStream_t s) {
   const bool two = c.D > 64;
-  if (c.drop) two ? tgnn_edge_fwd<CF, 2, true><<<GFWD, 256, 0, s>>>(c) : tgnn_edge_fwd<CF, 1, true><<<GFWD, 256, 0, s>>>(c);
-  else two ? tgnn_edge_fwd<CF, 2, false><<<GFWD, 256, 0, s>>>(c) : tgnn_edge_fwd<CF, 1, false><<<GFWD, 256, 0, s>>>(c);
+  const int g = GFWD + nfin;
+  if (c.drop) two ? tgnn_edge_fwd<CF, 2, true><<<g, 256, 0, s>>>(c) : tgnn_edge_fwd<CF, 1, true><<<g, 256, 0, s>>>(c);
+  else two ? tgnn_edge_fwd<CF, 2, false><<<g, 256, 0, s>>>(c) : tgnn_edge_fwd<CF, 1, false><<<g, 256, 0, s>>>(c);
 }
-static void launch_edge_fwd(const Ctx& c, hipStream_t s) {
+static void launch_edge_fwd(const Ctx& c, int nfin, hipStream_t s) {
   switch ((c.d + 63) / 64) {
-    case 0: launch_edge_fwd_cf<0>(c, s); break;
-    case 1: launch_edge_fwd_cf<1>(c, s); break;
-    case 2: launch_edge_fwd_cf<2>(c, s); break;
-    case 3: launch_edge_fwd_cf<3>(c, s); break;
-    case 4: launch_edge_fwd_cf<4>(c, s); break;
-    default: launch_edge_fwd_cf<5>(c, s); break;
+    case 0: launch_edge_fwd_cf<0>(c, nfin, s); break;
+    case 1: launch_edge_fwd_cf<1>(c, nfin, s); break;
+    case 2: launch_edge_fwd_cf<2>(c, nfin, s); break;
+    case 3: launch_edge_fwd_cf<3>(c, nfin, s); break;
+    case 4: launch_edge_fwd_cf<4>(c, nfin, s); break;
+    default: launch_edge_fwd_cf<5>(c, nfin, s); break;
   }
 }
 
@@ -931,7 +972,7 @@ __global__ void __launch_bounds__(256) tgnn_seg_fwd(Ctx c) {
 // ------------------------------------------------------------------ backward
 // per segment: dx_eh from the saved logits (softmax + LeakyReLU + attn dropout backward),
 // d er -> dU_r partials (persistent waves, deterministic workgroup reduction)
-__global__ void __launch_bounds__(256) tgnn_seg_bwd(Ctx c) {
+__device__ void seg_bwd_body(const Ctx& c, const int bid, const int nblk) {
   extern __shared__ __attribute__((aligned(16))) float red[];
   const PLay PL = c.PL;
   for (int p = threadIdx.x; p < PL.total; p += blockDim.x) red[p] = 0.f;
@@ -950,7 +991,7 @@ __global__ void __launch_bounds__(256) tgnn_seg_bwd(Ctx c) {
     aUr[0][h] = aUr[1][h] = 0.f;
     acr[h] = 0.f;
   }
-  for (int w = blockIdx.x * 4 + wv; w < S; w += gridDim.x * 4) {
+  for (int w = bid * 4 + wv; w < S; w += nblk * 4) {
     const float g = c.seg_g[w];
     if (g == 0.f) continue;
     Seg s;
@@ -1017,7 +1058,7 @@ __global__ void __launch_bounds__(256) tgnn_seg_bwd(Ctx c) {
     }
     __syncthreads();
   }
-  float* slab = c.slabs_s + (int64_t)blockIdx.x * PL.total;
+  float* slab = c.slabs_s + (int64_t)bid * PL.total;
   for (int p = threadIdx.x; p < PL.total; p += blockDim.x) slab[p] = red[p];
 }
 
@@ -1322,7 +1363,7 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
 // (exact fp32, k-ordered fmaf chain).  Grid: 2 * ceil(D/16)^2 waves.
 __device__ void pred_reduce_vec_body(const Ctx& c, int y, int lane);
 
-__global__ void __launch_bounds__(256) tgnn_pred_reduce_mfma(Ctx c) {
+__device__ void pred_reduce_body(const Ctx& c, const int bid) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   __shared__ f32x4 part[4][64];
   const int B = (int)c.ctl[TGNX_CTL_B];
@@ -1330,12 +1371,12 @@ __global__ void __launch_bounds__(256) tgnn_pred_reduce_mfma(Ctx c) {
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
   const bool ok = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
   const int nt = (D + 15) / 16;
-  if ((int)blockIdx.x >= 2 * nt * nt) {  // trailing blocks: bias / output-layer / loss sums
-    pred_reduce_vec_body(c, ((int)blockIdx.x - 2 * nt * nt) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+  if (bid >= 2 * nt * nt) {  // trailing blocks: bias / output-layer / loss sums
+    pred_reduce_vec_body(c, (bid - 2 * nt * nt) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
     return;
   }
-  const int which = blockIdx.x / (nt * nt);
-  const int t = blockIdx.x % (nt * nt), tm = t / nt, tn = t % nt;
+  const int which = bid / (nt * nt);
+  const int t = bid % (nt * nt), tm = t / nt, tn = t % nt;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int S = 8 * D + 4;
   const int m = tm * 16 + (lane & 15), n = tn * 16 + (lane & 15), kk = lane >> 4;
@@ -1371,6 +1412,17 @@ __global__ void __launch_bounds__(256) tgnn_pred_reduce_mfma(Ctx c) {
     const int row = tm * 16 + (lane >> 4) * 4 + r;
     if (row < D && col < D) out[(int64_t)row * D + col] = acc[r];
   }
+}
+
+// segment backward (blocks [0, GSEG)) and the predictor weight reductions (the rest) in one launch:
+// both only need tgnn_pred_train's per-event rows
+__global__ void __launch_bounds__(256) tgnn_seg_bwd_pred(Ctx c) {
+  if ((int)blockIdx.x < GSEG) seg_bwd_body(c, blockIdx.x, GSEG);
+  else pred_reduce_body(c, blockIdx.x - GSEG);
+}
+__host__ __device__ inline int pred_reduce_blocks(int D) {
+  const int nt = (D + 15) / 16;
+  return 2 * nt * nt + (3 * D + 2 + 3) / 4;
 }
 
 // predictor bias / output-layer gradients and the batch loss: one wave per output, lanes over events
@@ -1477,6 +1529,10 @@ __global__ void tgnn_adam(Ctx c) {
   const double bc2 = 1.0 - pow((double)c.b2, (double)t);
   const float step = (float)(c.lr / bc1);
   const float bc2s = (float)sqrt(bc2);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // loss sum (slot after the parameters, all-reduced with them)
+    double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
+    *loss += (double)c.grads[c.L.total] * (double)B;
+  }
   for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < c.L.total; x += (int64_t)gridDim.x * blockDim.x) {
     const float g = c.grads[x];
     float m = c.am[x], v = c.av[x];
@@ -1489,16 +1545,17 @@ __global__ void tgnn_adam(Ctx c) {
   }
 }
 
-// End of a step (many workgroups): time_assoc of the touched nodes (model_utils.py:77-83), the ring
-// insert of the whole batch with a wave per node run of tgnn_assemble's plan, the loss sum.
+// Ring/time state update of a batch (many workgroups): time_assoc of the touched nodes
+// (model_utils.py:77-83) and the ring insert of the whole batch with a wave per node run of
+// tgnn_assemble's plan.
 template <bool TRAIN>
-__global__ void __launch_bounds__(256) tgnn_finish(Ctx c) {
+__device__ void finish_body(const Ctx& c, const int bid, const int nblk) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   const float* evt = c.ev_t + start;
   const int NT = TRAIN ? 3 * B : 2 * B;
-  const int gt = blockIdx.x * blockDim.x + threadIdx.x, gs = gridDim.x * blockDim.x;
+  const int gt = bid * blockDim.x + threadIdx.x, gs = nblk * blockDim.x;
   if (TRAIN) {  // final time_assoc = last assignment of each touched node
     for (int j = gt; j < NT; j += gs) {
       const uint64_t k = c.touches[j];
@@ -1512,17 +1569,18 @@ __global__ void __launch_bounds__(256) tgnn_finish(Ctx c) {
     }
   }
   const int U = c.misc[MISC_RUNS];
-  const int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int r = bid * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (r < U) {
     const int a = c.rruns[r];
     ring_merge_run(c.nbr, c.eid, c.rt, c.K, c.ev_src + start, c.ev_dst + start, evt, B, c.ctl[TGNX_CTL_CUR_EID],
                    c.assoc, c.rkeys, a, c.rruns[r + 1] - a, r, threadIdx.x & 63);
   }
-  if (TRAIN && gt == 0) {
-    double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
-    *loss += (double)c.grads[c.L.total] * (double)B;
-  }
 }
+template <bool TRAIN>
+__global__ void __launch_bounds__(256) tgnn_finish(Ctx c) {
+  finish_body<TRAIN>(c, blockIdx.x, gridDim.x);
+}
+__host__ __device__ inline int finish_blocks(int Bmax) { return (2 * Bmax + 3) / 4; }
 
 __global__ void tgnn_ta_fill(Ctx c) {
   const int B = (int)c.ctl[TGNX_CTL_B];
@@ -1787,7 +1845,7 @@ static int edge_grid(int64_t Ecap) {
 template <bool TRAIN>
 static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
   probe_begin(TGNX_K_ASSEMBLE, s);
-  tgnn_assemble<TRAIN><<<2, 1024, assemble_smem_bytes(c.Bmax), s>>>(c);
+  tgnn_assemble<TRAIN><<<3, 1024, assemble_smem_bytes(c.Bmax), s>>>(c);
   probe_end(TGNX_K_ASSEMBLE, s);
   TGNX_LAUNCH_CHECK("tgnn_assemble");
   if (!TRAIN) {
@@ -1796,17 +1854,15 @@ static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
     tgnn_seg_scan<<<1, 1024, 0, s>>>(c);
     TGNX_LAUNCH_CHECK("tgnn_seg_scan");
   }
-  probe_begin(TGNX_K_EDGE_META, s);
-  tgnn_edge_meta<TRAIN><<<edge_grid(c.Ecap) / 4 + 1, 256, 0, s>>>(c);
-  probe_end(TGNX_K_EDGE_META, s);
-  TGNX_LAUNCH_CHECK("tgnn_edge_meta");
-  {
-    const int nb = (H * c.F + 63) / 64 + 2 * ((H * c.D + 63) / 64) + (3 * H + 2 * c.D + 3) / 4 + 64;
-    tgnn_collapse<<<nb, 256, 0, s>>>(c);
-    TGNX_LAUNCH_CHECK("tgnn_collapse");
+  {  // edge metadata + collapsed weights (depends on the parameters only) in one launch
+    const int nmeta = edge_grid(c.Ecap) / 4 + 1;
+    probe_begin(TGNX_K_EDGE_META, s);
+    tgnn_meta_collapse<TRAIN><<<nmeta + collapse_blocks(c), 256, 0, s>>>(c, nmeta);
+    probe_end(TGNX_K_EDGE_META, s);
+    TGNX_LAUNCH_CHECK("tgnn_meta_collapse");
   }
   probe_begin(TGNX_K_EDGE_FWD, s);
-  launch_edge_fwd(c, s);
+  launch_edge_fwd(c, TRAIN ? finish_blocks(c.Bmax) : 0, s);
   probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgnn_edge_fwd");
   probe_begin(TGNX_K_SEG_FWD, s);
@@ -1819,11 +1875,10 @@ static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
 static int launch_backward(const Ctx& c, hipStream_t s) {
   const size_t shm = (size_t)c.PL.total * 4;
   probe_begin(TGNX_K_SEG_BWD, s);
-  tgnn_seg_bwd<<<GSEG, 256, shm, s>>>(c);
+  tgnn_seg_bwd_pred<<<GSEG + pred_reduce_blocks(c.D), 256, shm, s>>>(c);
   probe_end(TGNX_K_SEG_BWD, s);
-  TGNX_LAUNCH_CHECK("tgnn_seg_bwd");
+  TGNX_LAUNCH_CHECK("tgnn_seg_bwd_pred");
   probe_begin(TGNX_K_EDGE_BWD, s);
-  const int FD = c.F + c.D;
   launch_edge_bwd(c, s);
   probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgnn_edge_bwd");
@@ -1853,6 +1908,11 @@ int tgnx_tgnn_param_layout(const tgnx_tgnn_config* cfg, int64_t* off) {
 size_t tgnx_tgnn_ws_bytes(const tgnx_tgnn_config* cfg) {
   if (check_cfg(cfg)) return 0;
   return make_ws(cfg).total;
+}
+
+size_t tgnx_tgnn_ws_misc_offset(const tgnx_tgnn_config* cfg) {
+  if (check_cfg(cfg)) return 0;
+  return make_ws(cfg).misc;
 }
 
 int tgnx_tgnn_advance(int64_t* ctl, int32_t mode, int64_t batch_start, int64_t B, int64_t cur_e_id, int64_t split_lo,
@@ -1886,11 +1946,6 @@ int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers
   tgnn_pred_train<<<grid_for(Bmax, 4), 256, 0, s>>>(c);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgnn_pred_train");
-  {
-    const int nt = (c.D + 15) / 16;
-    tgnn_pred_reduce_mfma<<<2 * nt * nt + grid_for(3 * c.D + 2, 4), 256, 0, s>>>(c);
-    TGNX_LAUNCH_CHECK("tgnn_pred_reduce_mfma");
-  }
   rc = launch_backward(c, s);
   if (rc) return rc;
   {
@@ -1911,10 +1966,6 @@ int tgnx_tgnn_train_update(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers*
   tgnn_adam<<<grid_for(c.L.total, 256), 256, 0, s>>>(c);
   probe_end(TGNX_K_ADAM, s);
   TGNX_LAUNCH_CHECK("tgnn_adam");
-  probe_begin(TGNX_K_FINISH, s);
-  tgnn_finish<true><<<(2 * cfg->max_batch + 3) / 4, 256, 0, s>>>(c);
-  probe_end(TGNX_K_FINISH, s);
-  TGNX_LAUNCH_CHECK("tgnn_finish");
   return TGNX_OK;
 }
 
@@ -1940,7 +1991,7 @@ int tgnx_tgnn_eval_step(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* bu
   TGNX_LAUNCH_CHECK("tgnn_mrr");
   tgnn_ta_fill<<<grid_for(cfg->num_nodes, 256) < 4096 ? grid_for(cfg->num_nodes, 256) : 4096, 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgnn_ta_fill");
-  tgnn_finish<false><<<(2 * cfg->max_batch + 3) / 4, 256, 0, s>>>(c);
+  tgnn_finish<false><<<finish_blocks(cfg->max_batch), 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgnn_finish");
   return TGNX_OK;
 }

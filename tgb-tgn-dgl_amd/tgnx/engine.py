@@ -105,7 +105,8 @@ class TgnnEngine:
 
     def train_batch(self, src, dst, t, msg, blk, neg=None, dropout=True, update=True):
         """One train iteration on an explicit batch (epoch_utils.py:194-304).  update=False stops
-        after the gradients (no all-reduce, no Adam, no ring insert): see apply_update()."""
+        after the gradients (no all-reduce, no Adam; the ring insert / time_assoc update of the batch
+        already happened once the forward had read them): see apply_update()."""
         dev = self.dev
         src, dst, t, msg, blk = self._dev_batch(dev, src, dst, t, msg, blk)
         B = int(src.numel())
@@ -125,7 +126,7 @@ class TgnnEngine:
         return self.out_pos[:B], self.out_neg[:B], neg
 
     def apply_update(self, allreduce=True):
-        """All-reduce (world > 1), Adam, ring insert + time_assoc for the last train_batch."""
+        """All-reduce (world > 1) and Adam for the last train_batch."""
         buf, B = self._pending
         if allreduce:
             self._allreduce_grads()
