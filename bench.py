@@ -168,7 +168,8 @@ def main():
     bytes_edge = 20 + 4 * d + 4 * D + 4
     bytes_root = 4 * D + 4
     probes = {}
-    for name, kid in (("tgnn_edge_fwd", 1), ("tgnn_edge_bwd", 2), ("tgnn_seg_fwd", 6), ("tgnn_seg_bwd", 8)):
+    for name, kid in (("tgnn_edge_fwd", 1), ("tgnn_edge_bwd", 2), ("tgnn_seg_fwd", 6), ("tgnn_seg_bwd", 8),
+                      ("tgnn_pred_train", 4), ("tgnn_assemble", 3), ("tgnn_meta_collapse", 9), ("tgnn_adam", 7)):
         _lib.call("tgnx_probe_enable", kid)
         pe0, ps0 = eng.units()
         for _ in range(args.probe_steps):
@@ -188,7 +189,8 @@ def main():
         algo = edges * bytes_edge if name.startswith("tgnn_edge") else roots * bytes_root
         probes[name] = dict(avg_us=avg_ms * 1e3, launches=launches, edges=edges, roots=roots, bytes=algo,
                             gbs=algo / (avg_ms * 1e-3) / 1e9)
-    dom = max(probes, key=lambda k: probes[k]["avg_us"])
+    # roofline kernel: the slowest of the per-edge / per-segment kernels (the gather path of §8(d))
+    dom = max((k for k in probes if k.startswith(("tgnn_edge", "tgnn_seg"))), key=lambda k: probes[k]["avg_us"])
     pd = probes[dom]
 
     traffic = None

@@ -1258,48 +1258,82 @@ __global__ void __launch_bounds__(64 * RED_WAVES) tgnn_grad_reduce(Ctx c, int Ge
 __device__ __forceinline__ float softplus(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
 
 __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
-  __shared__ float se[4][3][DMAX];
+  // one workgroup per event; its 4 waves split the D-long contractions, LDS combines them in a
+  // fixed order, wave 0 finishes the event
+  __shared__ float se[3][DMAX];
+  __shared__ float part[4][3][DMAX];
   const int B = (int)c.ctl[TGNX_CTL_B];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
-  const int i = lo + blockIdx.x * 4 + wv;
+  const int i = lo + blockIdx.x;
+  if (B == 0 || i >= hi || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nloc = hi - lo;
-  const bool active = B > 0 && i < hi && c.ctl[TGNX_CTL_ERR] == 0;
   const int D = c.D;
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-  int blk = 0;
-  if (active) {
-    blk = (int)c.ev_blk[start + i];
+  const int blk = (int)c.ev_blk[start + i];
+  {
     const int64_t roots[3] = {c.ev_src[start + i], c.ev_dst[start + i], c.neg[start + i]};
-    const int segs[3] = {i - lo, nloc + i - lo, 2 * nloc + i - lo};
+    const float sv[3] = {c.seg_out[i - lo], c.seg_out[nloc + i - lo], c.seg_out[2 * nloc + i - lo]};
+    for (int x = tid; x < 3 * D; x += blockDim.x) {
+      const int r = x / D, dd = x % D;
+      float v = c.mem[roots[r] * D + dd];
+#ifndef TGNX_EXP_NOHASH
+      if (c.drop) v *= node_keep(c, seed, blk, roots[r], dd);
+#endif
+      se[r][dd] = v + sv[r];
+    }
+  }
+  __syncthreads();
+  const float* P = c.params;
+  {
+    // wave wv owns rows [d0, d0 + kc) of the contraction (kc <= DMAX / 4): all its weight loads are
+    // issued before any FMA, so one memory latency covers the chunk
+    constexpr int KC = DMAX / 4;
+    const int kc = (D + 3) / 4, d0 = wv * kc, n = min(D - d0, kc);
+    const float* WsT = c.U + c.UL.WsT;
+    const float* WdT = c.U + c.UL.WdT;
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const float sv = c.seg_out[segs[r]];
-      for (int dd = lane; dd < D; dd += 64) {
-        float v = c.mem[roots[r] * D + dd];
-        if (c.drop) v *= node_keep(c, seed, blk, roots[r], dd);
-        se[wv][r][dd] = v + sv;
+    for (int q = 0; q < 2; ++q) {
+      const int o = lane + 64 * q;
+      const int oc = o < D ? o : D - 1;
+      float ws[KC], wd[KC];
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        const int dd = d0 + (j < n ? j : 0);
+        ws[j] = WsT[dd * D + oc];
+        wd[j] = WdT[dd * D + oc];
+      }
+      float a = 0.f, b = 0.f, d2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        if (j < n) {
+          a += ws[j] * se[0][d0 + j];
+          b += wd[j] * se[1][d0 + j];
+          d2 += wd[j] * se[2][d0 + j];
+        }
+      }
+      if (o < D) {
+        part[wv][0][o] = a;
+        part[wv][1][o] = b;
+        part[wv][2][o] = d2;
       }
     }
   }
   __syncthreads();
-  if (!active) return;
-  const float* P = c.params;
+#ifdef TGNX_EXP_NOEPI
+  return;
+#endif
+  if (wv != 0) return;
   float hs[2], hp[2], hn[2];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int o = lane + 64 * q;
     float a = 0.f, b = 0.f, d2 = 0.f;
     if (o < D) {
-      a = P[c.L.bs + o]; b = P[c.L.bd + o]; d2 = b;
-      const float* WsT = c.U + c.UL.WsT;
-      const float* WdT = c.U + c.UL.WdT;
-      for (int dd = 0; dd < D; ++dd) {
-        a += WsT[dd * D + o] * se[wv][0][dd];
-        b += WdT[dd * D + o] * se[wv][1][dd];
-        d2 += WdT[dd * D + o] * se[wv][2][dd];
-      }
+      a = P[c.L.bs + o] + ((part[0][0][o] + part[1][0][o]) + (part[2][0][o] + part[3][0][o]));
+      b = P[c.L.bd + o] + ((part[0][1][o] + part[1][1][o]) + (part[2][1][o] + part[3][1][o]));
+      d2 = P[c.L.bd + o] + ((part[0][2][o] + part[1][2][o]) + (part[2][2][o] + part[3][2][o]));
     }
     hs[q] = a; hp[q] = b; hn[q] = d2;
   }
@@ -1334,11 +1368,11 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
       gp += dhp * c.U[c.UL.Wd1 + o];
       gn += dhn * c.U[c.UL.Wd1 + o];
       ev[0 * D + o] = A;
-      ev[1 * D + o] = se[wv][0][o];
+      ev[1 * D + o] = se[0][o];
       ev[2 * D + o] = dhp;
-      ev[3 * D + o] = se[wv][1][o];
+      ev[3 * D + o] = se[1][o];
       ev[4 * D + o] = dhn;
-      ev[5 * D + o] = se[wv][2][o];
+      ev[5 * D + o] = se[2][o];
       ev[6 * D + o] = hpos[q];
       ev[7 * D + o] = hneg[q];
     }
@@ -1520,28 +1554,47 @@ __device__ void grad_attn_body(const Ctx& c, int y, int lane) {
   }
 }
 
-// torch.optim.Adam (single-tensor form), bias corrections from the device step count
-__global__ void tgnn_adam(Ctx c) {
+// torch.optim.Adam (single-tensor form, same per-element operation order), bias corrections from
+// the device step count, computed once per workgroup; 4 parameters per thread.
+__device__ __forceinline__ void adam1(float g, float& m, float& v, float& p, float b1, float b2, float eps, float step,
+                                      float bc2s) {
+  m = m + (1.0f - b1) * (g - m);
+  v = v * b2 + (1.0f - b2) * g * g;
+  const float den = sqrtf(v) / bc2s + eps;
+  p -= step * (m / den);
+}
+__global__ void __launch_bounds__(256) tgnn_adam(Ctx c) {
+  __shared__ float sc[2];
   const int64_t B = c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
-  const double bc1 = 1.0 - pow((double)c.b1, (double)t);
-  const double bc2 = 1.0 - pow((double)c.b2, (double)t);
-  const float step = (float)(c.lr / bc1);
-  const float bc2s = (float)sqrt(bc2);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // loss sum (slot after the parameters, all-reduced with them)
-    double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
-    *loss += (double)c.grads[c.L.total] * (double)B;
+  if (threadIdx.x == 0) {
+    const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
+    const double bc1 = 1.0 - pow((double)c.b1, (double)t);
+    const double bc2 = 1.0 - pow((double)c.b2, (double)t);
+    sc[0] = (float)(c.lr / bc1);
+    sc[1] = (float)sqrt(bc2);
+    if (blockIdx.x == 0) {  // loss sum (slot after the parameters, all-reduced with them)
+      double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
+      *loss += (double)c.grads[c.L.total] * (double)B;
+    }
   }
-  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < c.L.total; x += (int64_t)gridDim.x * blockDim.x) {
-    const float g = c.grads[x];
-    float m = c.am[x], v = c.av[x];
-    m = m + (1.0f - c.b1) * (g - m);
-    v = v * c.b2 + (1.0f - c.b2) * g * g;
-    c.am[x] = m;
-    c.av[x] = v;
-    const float den = sqrtf(v) / bc2s + c.eps;
-    c.params[x] -= step * (m / den);
+  __syncthreads();
+  const float step = sc[0], bc2s = sc[1], b1 = c.b1, b2 = c.b2, eps = c.eps;
+  const int64_t n4 = c.L.total / 4;  // layout is padded to multiples of 4
+  float4* P4 = reinterpret_cast<float4*>(c.params);
+  float4* M4 = reinterpret_cast<float4*>(c.am);
+  float4* V4 = reinterpret_cast<float4*>(c.av);
+  const float4* G4 = reinterpret_cast<const float4*>(c.grads);
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n4; x += (int64_t)gridDim.x * blockDim.x) {
+    const float4 g = G4[x];
+    float4 m = M4[x], v = V4[x], p = P4[x];
+    adam1(g.x, m.x, v.x, p.x, b1, b2, eps, step, bc2s);
+    adam1(g.y, m.y, v.y, p.y, b1, b2, eps, step, bc2s);
+    adam1(g.z, m.z, v.z, p.z, b1, b2, eps, step, bc2s);
+    adam1(g.w, m.w, v.w, p.w, b1, b2, eps, step, bc2s);
+    M4[x] = m;
+    V4[x] = v;
+    P4[x] = p;
   }
 }
 
@@ -1943,7 +1996,7 @@ int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers
   rc = launch_forward<true>(c, 3 * (int64_t)Bmax, s);
   if (rc) return rc;
   probe_begin(TGNX_K_PRED, s);
-  tgnn_pred_train<<<grid_for(Bmax, 4), 256, 0, s>>>(c);
+  tgnn_pred_train<<<Bmax, 256, 0, s>>>(c);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgnn_pred_train");
   rc = launch_backward(c, s);
@@ -1963,7 +2016,7 @@ int tgnx_tgnn_train_update(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers*
   TGNX_CHECK_ARG(buf->grads && buf->adam_m && buf->adam_v, "tgnx_tgnn_train_update: null optimizer buffer");
   hipStream_t s = as_stream(stream);
   probe_begin(TGNX_K_ADAM, s);
-  tgnn_adam<<<grid_for(c.L.total, 256), 256, 0, s>>>(c);
+  tgnn_adam<<<grid_for(c.L.total / 4, 256), 256, 0, s>>>(c);
   probe_end(TGNX_K_ADAM, s);
   TGNX_LAUNCH_CHECK("tgnn_adam");
   return TGNX_OK;

@@ -13,11 +13,12 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /root/
 python3 - "$tag" <<'PY'
 import csv, sys
 rows = list(csv.DictReader(open(f"/root/repo/gpurun_out/{sys.argv[1]}_prof/run_kernel_stats.csv")))
+steps = max(int(r["Calls"]) for r in rows if "tgnn_assemble" in r["Name"])
 tot = 0
 for r in rows:
     c = int(r["Calls"]); a = float(r["AverageNs"]) / 1e3
     if c >= 400:
-        tot += a * c / 510
+        tot += a * c / steps
         print(f"{r['Name'][:50]:50s} {c:6d} {a:8.2f}us")
 print("per-step kernel sum %.1f us" % tot)
 PY
