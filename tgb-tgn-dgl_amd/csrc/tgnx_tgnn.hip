@@ -36,7 +36,7 @@ constexpr int TOUCH_MAX = 8192;
 #endif
 constexpr int GBWD = TGNX_GBWD;            // workgroups of the edge backward kernel (= partial slabs)
 constexpr int BWD_WAVES = TGNX_BWD_WAVES;  // waves per edge backward workgroup
-constexpr int GSEG = 64;      // workgroups of the segment backward kernel
+constexpr int GSEG = 160;     // workgroups of the segment backward kernel
 constexpr int MRR_SLOTS = 65536;  // per-batch MRR ring in buffers.mrr
 constexpr int BATCH_MAX = 2048;   // max events per batch (touch sort capacity 3 * BATCH_MAX in LDS)
 enum { MISC_RUNS = 0, MISC_KMAX = 1, MISC_STAMPS = 16, MISC_WORDS = TGNX_MISC_WORDS };
@@ -772,6 +772,52 @@ __device__ __forceinline__ float wave_sum8(const float (&v)[H], int lane) {
   return s;
 }
 
+// Segment kernels use lane l = 8 j + h: edge slot j (0..7) x head h.  Reductions over the edge
+// slots (lanes l ^ 8, l ^ 16, l ^ 32) and over the heads (l ^ 1, l ^ 2, l ^ 4) use DPP / swizzle.
+__device__ __forceinline__ float red_j_sum(float v) {
+  v += __uint_as_float(xlane_xor<8>(__float_as_uint(v)));
+  v += __uint_as_float(xlane_xor<16>(__float_as_uint(v)));
+  v += __uint_as_float(xlane_xor<32>(__float_as_uint(v)));
+  return v;
+}
+__device__ __forceinline__ float red_j_max(float v) {
+  v = fmaxf(v, __uint_as_float(xlane_xor<8>(__float_as_uint(v))));
+  v = fmaxf(v, __uint_as_float(xlane_xor<16>(__float_as_uint(v))));
+  v = fmaxf(v, __uint_as_float(xlane_xor<32>(__float_as_uint(v))));
+  return v;
+}
+__device__ __forceinline__ float red_h_sum(float v) {
+  v += __uint_as_float(xlane_xor<1>(__float_as_uint(v)));
+  v += __uint_as_float(xlane_xor<2>(__float_as_uint(v)));
+  v += __uint_as_float(xlane_xor<4>(__float_as_uint(v)));
+  return v;
+}
+// er_h = U_r[h]·drop(mem[root]) + c_r[h] (model_utils.py:588 collapsed) for the lane's head h:
+// dims dd = j + 8k, loads issued before the FMAs, then summed over the edge slots
+__device__ __forceinline__ float root_er8(const Ctx& c, const Seg& s, uint64_t seed, bool drop, int j, int h) {
+  constexpr int KD = DMAX / 8;
+  const int D = c.D;
+  const uint32_t nb = drop ? node_base(seed, s.blk, s.root) : 0u;
+  float mv[KD], uv[KD];
+#pragma unroll
+  for (int k = 0; k < KD; ++k) {
+    const int dd = min(j + 8 * k, D - 1);
+    mv[k] = c.mem[s.root * D + dd];
+    uv[k] = c.U[c.UL.Ur + h * D + dd];
+  }
+  float p = 0.f;
+#pragma unroll
+  for (int k = 0; k < KD; ++k) {
+    const int dd = j + 8 * k;
+    if (dd < D) {
+      float v = mv[k];
+      if (drop) v *= keep32(nb, (uint32_t)dd, c.pf, c.inv_kf);
+      p += uv[k] * v;
+    }
+  }
+  return red_j_sum(p) + c.U[c.UL.cr + h];
+}
+
 // x_eh = U_e[h]·[efeat_e, drop(cos(w dt + b))] + U_l[h]·drop(mem[src]) + c_h   (model_utils.py:447-452
 // collapsed): a wave per edge, each lane's U columns held in registers across
 // edges, two gather sets ping-pong so one edge's loads are in flight during the other's math.
@@ -883,35 +929,16 @@ __device__ __forceinline__ void load_x8(const float* p, float (&x)[H]) {
   x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
 }
 
-// er_h of a segment's root (model_utils.py:588): lanes over the memory dims
-__device__ __forceinline__ void root_er(const Ctx& c, const Seg& s, uint64_t seed, bool drop, int lane,
-                                       float (&er)[H], float (&nfr)[2]) {
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int dd = lane + 64 * q;
-    float v = dd < c.D ? c.mem[s.root * c.D + dd] : 0.f;
-    if (drop && dd < c.D) v *= node_keep(c, seed, s.blk, s.root, dd);
-    nfr[q] = v;
-  }
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-    float p = 0.f;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int dd = lane + 64 * q;
-      if (dd < c.D) p += c.U[c.UL.Ur + h * c.D + dd] * nfr[q];
-    }
-    er[h] = wave_sum(p) + c.U[c.UL.cr + h];
-  }
-}
 
 // per segment: LeakyReLU, edge softmax per head (model_utils.py:595-597), ft = Σ a·x, head mean
 template <bool TRAIN>
 __global__ void __launch_bounds__(256) tgnn_seg_fwd(Ctx c) {
+  // a wave per segment (lane = 8 edge slots x 8 heads): edge softmax with attention dropout and the
+  // head mean (model_utils.py:589-605 collapsed), online over chunks of 8 edges
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int S = (int)c.ctl[TGNX_CTL_S];
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, j = lane >> 3, h = lane & 7;
   const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (w >= S) return;
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
@@ -919,78 +946,83 @@ __global__ void __launch_bounds__(256) tgnn_seg_fwd(Ctx c) {
   seg_of(c, w, (int)c.ctl[TGNX_CTL_LO], (int)c.ctl[TGNX_CTL_HI], start, s);
   const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
   const bool drop = TRAIN && c.drop;
-  float er[H], nfr[2];
-  root_er(c, s, seed, drop, lane, er, nfr);
+  const float er = root_er8(c, s, seed, drop, j, h);
   const int e0 = c.seg_eoff[w], ne = c.seg_eoff[w + 1] - e0;
   const uint64_t sk = seg_key(s.blk, s.root);
-  float m[H], l[H], acc[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-    m[h] = -INFINITY; l[h] = 0.f; acc[h] = 0.f;
+  const float* __restrict__ X = c.X + (int64_t)e0 * H + h;
+  // each lane: online softmax over its edges o = j, j + 8, ... (no cross-lane traffic in the loop)
+  float m = -INFINITY, l = 0.f, acc = 0.f;
+#pragma unroll 4
+  for (int o = j; o < ne; o += 8) {
+    const float x = X[(int64_t)o * H];
+    float sc = x + er;
+    sc = sc > 0.f ? sc : 0.2f * sc;
+    const float mn = fmaxf(m, sc);
+    const float r = m == -INFINITY ? 0.f : expf(m - mn);
+    const float ex = expf(sc - mn);
+    float wgt = ex;
+    if (drop) wgt *= keep32(attn_base(seed, sk, o), (uint32_t)h, c.pa, c.inv_ka);
+    l = l * r + ex;
+    acc = acc * r + wgt * x;
+    m = mn;
   }
-  for (int base = 0; base < ne; base += 64) {
-    const int o = base + lane;
-    const bool ok = o < ne;
-    float x[H];
-    if (ok) load_x8(c.X + (int64_t)(e0 + o) * H, x);
-    const uint32_t ab = drop ? attn_base(seed, sk, o) : 0u;
+  // merge the 8 edge slots (lanes l ^ 8, ^ 16, ^ 32) in a fixed order
 #pragma unroll
-    for (int h = 0; h < H; ++h) {
-      float sc = -INFINITY;
-      if (ok) {
-        sc = x[h] + er[h];
-        sc = sc > 0.f ? sc : 0.2f * sc;
-      }
-      const float mn = fmaxf(m[h], wave_max(sc));
-      const float ex = ok ? expf(sc - mn) : 0.f;
-      float wgt = ex;
-      if (drop && ok) wgt *= keep32(ab, (uint32_t)h, c.pa, c.inv_ka);
-      const float r = expf(m[h] - mn);
-      l[h] = l[h] * r + wave_sum(ex);
-      acc[h] = acc[h] * r + wave_sum(ok ? wgt * x[h] : 0.f);
-      m[h] = mn;
+  for (int step = 0; step < 3; ++step) {
+    float mo, lo, ao;
+    if (step == 0) {
+      mo = __uint_as_float(xlane_xor<8>(__float_as_uint(m)));
+      lo = __uint_as_float(xlane_xor<8>(__float_as_uint(l)));
+      ao = __uint_as_float(xlane_xor<8>(__float_as_uint(acc)));
+    } else if (step == 1) {
+      mo = __uint_as_float(xlane_xor<16>(__float_as_uint(m)));
+      lo = __uint_as_float(xlane_xor<16>(__float_as_uint(l)));
+      ao = __uint_as_float(xlane_xor<16>(__float_as_uint(acc)));
+    } else {
+      mo = __uint_as_float(xlane_xor<32>(__float_as_uint(m)));
+      lo = __uint_as_float(xlane_xor<32>(__float_as_uint(l)));
+      ao = __uint_as_float(xlane_xor<32>(__float_as_uint(acc)));
     }
+    const float mn = fmaxf(m, mo);
+    const float r1 = m == -INFINITY ? 0.f : expf(m - mn);
+    const float r2 = mo == -INFINITY ? 0.f : expf(mo - mn);
+    l = l * r1 + lo * r2;  // fp addition commutes: both partners hold the same bits
+    acc = acc * r1 + ao * r2;
+    m = mn;
   }
-  float out = 0.f;
-  float st[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-    const float ft = acc[h] / l[h];
-    out += ft;
-    if (lane == h) {
-      st[0] = m[h]; st[1] = l[h]; st[2] = ft; st[3] = er[h];
-    }
-  }
+  const float ft = acc / l;
+  const float out = red_h_sum(ft);
   if (lane == 0) c.seg_out[w] = out * (1.0f / H);
-  if (TRAIN && lane < H) {
+  if (TRAIN && j == 0) {
     float* sp = c.seg_stats + (int64_t)w * 4 * H;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) sp[k * H + lane] = st[k];
+    sp[h] = m;
+    sp[H + h] = l;
+    sp[2 * H + h] = ft;
+    sp[3 * H + h] = er;
   }
 }
 
 // ------------------------------------------------------------------ backward
 // per segment: dx_eh from the saved logits (softmax + LeakyReLU + attn dropout backward),
 // d er -> dU_r partials (persistent waves, deterministic workgroup reduction)
+// Backward of tgnn_seg_fwd (a wave per segment, lane = 8 edge slots x 8 heads): dx of every edge
+// (-> DX), d er_h, and the partials of dU_r (= Σ der_h ⊗ drop(mem[root])) and dc_r, written as a
+// compact slab [H*D + H] per workgroup.
 __device__ void seg_bwd_body(const Ctx& c, const int bid, const int nblk) {
-  extern __shared__ __attribute__((aligned(16))) float red[];
-  const PLay PL = c.PL;
-  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) red[p] = 0.f;
-  __syncthreads();
+  constexpr int KD = DMAX / 8;
+  __shared__ float part[4][H * DMAX + H];
   const int B = (int)c.ctl[TGNX_CTL_B];
   const bool okb = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
   const int S = okb ? (int)c.ctl[TGNX_CTL_S] : 0;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, j = lane >> 3, h = lane & 7;
+  const int D = c.D;
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
   const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
   const bool drop = c.drop;
-  float aUr[2][H], acr[H];
+  float aUr[KD], acr = 0.f;
 #pragma unroll
-  for (int h = 0; h < H; ++h) {
-    aUr[0][h] = aUr[1][h] = 0.f;
-    acr[h] = 0.f;
-  }
+  for (int k = 0; k < KD; ++k) aUr[k] = 0.f;
   for (int w = bid * 4 + wv; w < S; w += nblk * 4) {
     const float g = c.seg_g[w];
     if (g == 0.f) continue;
@@ -998,68 +1030,50 @@ __device__ void seg_bwd_body(const Ctx& c, const int bid, const int nblk) {
     seg_of(c, w, lo, hi, start, s);
     const float gh = g * (1.0f / H);
     const float* sp = c.seg_stats + (int64_t)w * 4 * H;
-    float m[H], l[H], ft[H], er[H], der[H];
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      m[h] = sp[h]; l[h] = sp[H + h]; ft[h] = sp[2 * H + h]; er[h] = sp[3 * H + h]; der[h] = 0.f;
-    }
+    const float m = sp[h], l = sp[H + h], ft = sp[2 * H + h], er = sp[3 * H + h];
     const int e0 = c.seg_eoff[w], ne = c.seg_eoff[w + 1] - e0;
     const uint64_t sk = seg_key(s.blk, s.root);
-    for (int base = 0; base < ne; base += 64) {
-      const int o = base + lane;
-      const bool ok = o < ne;
-      float x[H], dx[H];
-      if (ok) load_x8(c.X + (int64_t)(e0 + o) * H, x);
-      const uint32_t ab = drop ? attn_base(seed, sk, o) : 0u;
-#pragma unroll
-      for (int h = 0; h < H; ++h) {
-        float ds = 0.f;
-        dx[h] = 0.f;
-        if (ok) {
-          float sc = x[h] + er[h];
-          const float lk = sc > 0.f ? 1.f : 0.2f;
-          sc = sc > 0.f ? sc : 0.2f * sc;
-          const float a = expf(sc - m[h]) / l[h];
-          const float mk = drop ? keep32(ab, (uint32_t)h, c.pa, c.inv_ka) : 1.f;
-          ds = a * gh * (x[h] * mk - ft[h]) * lk;
-          dx[h] = gh * a * mk + ds;
-        }
-        der[h] += wave_sum(ds);
-      }
-      if (ok) {
-        float4* dp = reinterpret_cast<float4*>(c.DX + (int64_t)(e0 + o) * H);
-        dp[0] = make_float4(dx[0], dx[1], dx[2], dx[3]);
-        dp[1] = make_float4(dx[4], dx[5], dx[6], dx[7]);
+    float der = 0.f;
+    const float* __restrict__ X = c.X + (int64_t)e0 * H + h;
+    float* __restrict__ DXp = c.DX + (int64_t)e0 * H + h;
+#pragma unroll 4
+    for (int o = j; o < ne; o += 8) {
+      {
+        const float x = X[(int64_t)o * H];
+        float sc = x + er;
+        const float lk = sc > 0.f ? 1.f : 0.2f;
+        sc = sc > 0.f ? sc : 0.2f * sc;
+        const float a = expf(sc - m) / l;
+        const float mk = drop ? keep32(attn_base(seed, sk, o), (uint32_t)h, c.pa, c.inv_ka) : 1.f;
+        const float ds = a * gh * (x * mk - ft) * lk;
+        DXp[(int64_t)o * H] = gh * a * mk + ds;
+        der += ds;
       }
     }
+    der = red_j_sum(der);
+    const uint32_t nb = drop ? node_base(seed, s.blk, s.root) : 0u;
+    float mv[KD];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int dd = lane + 64 * q;
-      float v = dd < c.D ? c.mem[s.root * c.D + dd] : 0.f;
-      if (drop && dd < c.D) v *= node_keep(c, seed, s.blk, s.root, dd);
+    for (int k = 0; k < KD; ++k) mv[k] = c.mem[s.root * D + min(j + 8 * k, D - 1)];
 #pragma unroll
-      for (int h = 0; h < H; ++h) aUr[q][h] += der[h] * v;
+    for (int k = 0; k < KD; ++k) {
+      float v = mv[k];
+      if (drop) v *= keep32(nb, (uint32_t)(j + 8 * k), c.pf, c.inv_kf);
+      aUr[k] += der * v;
     }
-#pragma unroll
-    for (int h = 0; h < H; ++h) acr[h] += der[h];
+    acr += der;
   }
-  for (int k = 0; k < 4; ++k) {
-    if (wv == k) {
+  float* pw = part[wv];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int dd = lane + 64 * q;
-        if (dd < c.D)
-#pragma unroll
-          for (int h = 0; h < H; ++h) red[PL.Ur + h * c.D + dd] += aUr[q][h];
-      }
-      if (lane == 0)
-#pragma unroll
-        for (int h = 0; h < H; ++h) red[PL.cr + h] += acr[h];
-    }
-    __syncthreads();
+  for (int k = 0; k < KD; ++k) {
+    const int dd = j + 8 * k;
+    if (dd < D) pw[h * D + dd] = aUr[k];
   }
-  float* slab = c.slabs_s + (int64_t)bid * PL.total;
-  for (int p = threadIdx.x; p < PL.total; p += blockDim.x) slab[p] = red[p];
+  if (j == 0) pw[H * D + h] = acr;
+  __syncthreads();
+  const int n = H * D + H;
+  float* slab = c.slabs_s + (int64_t)bid * n;
+  for (int p = threadIdx.x; p < n; p += blockDim.x) slab[p] = (part[0][p] + part[1][p]) + (part[2][p] + part[3][p]);
 }
 
 // dU_e, dU_l, dw, db, dc_e, dc_l partials of the edge terms (backward of tgnn_edge_fwd).
@@ -1234,15 +1248,20 @@ static void launch_edge_bwd(const Ctx& c, hipStream_t s) {
 constexpr int RED_WAVES = 16;
 __global__ void __launch_bounds__(64 * RED_WAVES) tgnn_grad_reduce(Ctx c, int Ge, int Gs) {
   __shared__ float acc[RED_WAVES][64];
-  const int P = c.PL.total;
+  const PLay PL = c.PL;
+  const int P = PL.total;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int p = blockIdx.x * 64 + lane;
+  // segment slabs are compact [dU_r (H*D) | dc_r (H)]
+  const int HD = H * c.D, ns = HD + H;
+  const int q = (p >= PL.Ur && p < PL.Ur + HD) ? p - PL.Ur : (p >= PL.cr && p < PL.cr + H) ? HD + (p - PL.cr) : -1;
   float s = 0.f;
   if (p < P) {
 #pragma unroll 4
     for (int g = wv; g < Ge; g += RED_WAVES) s += c.slabs[(int64_t)g * P + p];
+    if (q >= 0)
 #pragma unroll 4
-    for (int g = wv; g < Gs; g += RED_WAVES) s += c.slabs_s[(int64_t)g * P + p];
+      for (int g = wv; g < Gs; g += RED_WAVES) s += c.slabs_s[(int64_t)g * ns + q];
   }
   acc[wv][lane] = s;
   __syncthreads();
@@ -1781,7 +1800,7 @@ static WsLay make_ws(const tgnx_tgnn_config* cfg) {
   W.U = carve(off, (size_t)make_ulay(D, d).total * 4);
   W.evs = carve(off, (size_t)B * (8 * D + 4) * 4);
   W.slabs = carve(off, (size_t)GBWD * P * 4);
-  W.slabs_s = carve(off, (size_t)GSEG * P * 4);
+  W.slabs_s = carve(off, (size_t)GSEG * (H * D + H) * 4);
   W.red = carve(off, (size_t)P * 4);
   W.blkmax = carve(off, (size_t)B * 4);
   W.blk_rank = carve(off, (size_t)B * 4);
@@ -1926,9 +1945,8 @@ static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
 }
 
 static int launch_backward(const Ctx& c, hipStream_t s) {
-  const size_t shm = (size_t)c.PL.total * 4;
   probe_begin(TGNX_K_SEG_BWD, s);
-  tgnn_seg_bwd_pred<<<GSEG + pred_reduce_blocks(c.D), 256, shm, s>>>(c);
+  tgnn_seg_bwd_pred<<<GSEG + pred_reduce_blocks(c.D), 256, 0, s>>>(c);
   probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgnn_seg_bwd_pred");
   probe_begin(TGNX_K_EDGE_BWD, s);
