@@ -17,6 +17,7 @@ Modules exercised (file:line of the code that produced each fixture):
                  provides the imported names is put in sys.modules so the pure-torch classes
                  can be instantiated — no DGL op is ever called)
   msg.npz        modules/msg_func.py:12-18   IdentityMessage
+  link_pred.npz  modules/decoder.py:108-123  LinkPredictor (sigmoid output)
 """
 from __future__ import annotations
 
@@ -217,6 +218,20 @@ def capture_msg(seed):
                         te=te.numpy(), out=out.numpy(), out_channels=np.array([m.out_channels]))
 
 
+def capture_link_pred(seed):
+    """modules/decoder.py:108-123 LinkPredictor (sigmoid output): weights + inputs + outputs."""
+    from modules.decoder import LinkPredictor
+    torch.manual_seed(seed)
+    lp = LinkPredictor(6)
+    g = torch.Generator().manual_seed(seed + 1)
+    zs, zd = torch.randn(9, 6, generator=g), torch.randn(9, 6, generator=g)
+    with torch.no_grad():
+        out = lp(zs, zd)
+    sd = {k: v.numpy() for k, v in lp.state_dict().items()}
+    np.savez_compressed(os.path.join(HERE, "link_pred.npz"), zs=zs.numpy(), zd=zd.numpy(), out=out.numpy(),
+                        **{"p_" + k.replace(".", "__"): v for k, v in sd.items()})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -233,6 +248,7 @@ def main():
     capture_dataset(6)
     capture_model(7)
     capture_msg(8)
+    capture_link_pred(9)
     print("goldens written to", HERE)
 
 

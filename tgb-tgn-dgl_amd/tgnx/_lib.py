@@ -33,6 +33,9 @@ SIGNATURES = {
     "tgnx_tgnn_param_layout": (ctypes.c_int, [P, P]),
     "tgnx_tgnn_ws_bytes": (c_sz, [P]),
     "tgnx_tgnn_ws_misc_offset": (c_sz, [P]),
+    "tgnx_gemm_f32_ws_bytes": (c_sz, [c_i64, c_i64, c_i64]),
+    "tgnx_gemm_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, P, c_i64, c_i32, P, c_i64, c_i32, P, c_i64, P, c_i32, P, c_sz,
+                                     c_vp]),
     "tgnx_tgnn_advance": (ctypes.c_int, [P, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64,
                                          c_i32, c_vp]),
     "tgnx_tgnn_train_fwd_bwd": (ctypes.c_int, [P, P, c_i32, c_i32, c_vp]),
