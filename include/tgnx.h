@@ -222,6 +222,63 @@ int tgnx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, 
                   int64_t ldb, int32_t trans_b, float* C, int64_t ldc, const float* bias, int32_t accumulate,
                   void* ws, size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------- TGN memory path
+ * SURVEY §8 a14–a16 (the PyG TGN of the reference modules/ directory, wired as pyg_model_utils.py:10-36):
+ * TGNMemory (modules/memory_module.py:25-215) with IdentityMessage (msg_func.py:12-18) and
+ * Last/Mean aggregation (msg_agg.py:15-26), GRUCell memory update, GraphAttentionEmbedding over
+ * TransformerConv (emb_module.py:55-73, heads = 2, dropout on the attention), LinkPredictor
+ * (decoder.py:108-123, sigmoid output fed to BCE-with-logits as the reference's loop does).
+ * The sampler state is the LastNeighborLoader ring above; ctl is the tgnx_tgnn_advance block. */
+#define TGNX_TGN_NPARAM 21
+typedef struct {
+  int64_t num_nodes;
+  int64_t num_events;  /* rows of the event table (e_id space, message-store arena) */
+  int32_t ring, mem_dim, msg_dim, heads, max_batch, max_neg;
+  int32_t aggr;        /* 0 = LastAggregator, 1 = MeanAggregator */
+  float dropout, lr, beta1, beta2, eps;
+} tgnx_tgn_config;
+
+typedef struct {
+  const int64_t *ev_src, *ev_dst; /* event table [num_events] (e_id rows) */
+  const float *ev_t, *ev_msg;     /* [num_events], [num_events, msg_dim] */
+  int64_t* neg;                   /* train: [num_events] (written if gen_neg); eval: [num_events, Kn] */
+  const int64_t* dst_nodes;
+  int64_t n_dst;
+  int64_t *nbr, *eid;             /* LastNeighborLoader ring [N,K] */
+  float* rt;
+  int64_t* assoc;                 /* [N] */
+  float* memory;                  /* TGNMemory.memory [N, mem_dim] */
+  int64_t* last_update;           /* TGNMemory.last_update [N] */
+  int64_t* store;                 /* message stores: tgnx_tgn_store_words(cfg) int64, zero-filled once */
+  int32_t* node_gen;              /* int32[N], zero-filled once */
+  float *params, *grads, *adam_m, *adam_v; /* flat, tgnx_tgn_param_layout (+1 loss slot in grads) */
+  int64_t* ctl;                   /* int64[TGNX_CTL_WORDS] */
+  float *out_pos, *out_neg;       /* train: [B] sigmoid outputs; eval: [B], [B, Kn] */
+  double* mrr;                    /* eval: per-event reciprocal ranks of the last batch [B] */
+  void* ws;                       /* tgnx_tgn_ws_bytes(cfg), zero-filled once */
+} tgnx_tgn_buffers;
+
+int tgnx_tgn_param_layout(const tgnx_tgn_config* cfg, int64_t* offsets /* [TGNX_TGN_NPARAM+1] */);
+size_t tgnx_tgn_ws_bytes(const tgnx_tgn_config* cfg);
+size_t tgnx_tgn_store_words(const tgnx_tgn_config* cfg);
+/* memory = 0, last_update = 0, message stores empty (memory_module.py:106-110). */
+int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream);
+/* Train batch, part 1 (the canonical loop pyg_epoch_utils.py:106-137 carries commented out): negatives
+ * (gen_neg), sampler, memory(n_id) with the GRU update of every sampled node, embedding,
+ * link prediction, BCE, backward; then update_state (memory / last_update of src ∪ dst, message
+ * stores) and the ring insert.  Writes grads (+ loss slot). */
+int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg,
+                           int32_t dropout, void* stream);
+/* Train batch, part 2: Adam on the (possibly all-reduced) grads, loss sum. */
+int tgnx_tgn_train_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream);
+/* Eval batch (TGB tgbl link prediction): every event's [pos, Kn negatives] scored with the
+ * batch-start memory and ring, per-event reciprocal rank in buf->mrr, then update_state in eval
+ * order (store, then GRU update) and the ring insert. */
+int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t Kn, void* stream);
+/* train(False): update the memory of every node from its stored messages, clear the stores
+ * (memory_module.py:209-215). */
+int tgnx_tgn_flush(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

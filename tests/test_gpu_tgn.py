@@ -1,0 +1,123 @@
+"""GPU parity of the TGN memory path (SURVEY §8 a14–a16, tgnx_tgn_*) against the oracle restatement
+oracle/tgn_ref.py (PARITY UNPINNED for its torch_geometric / torch_scatter parts, see its header).
+
+Step by step on a small wiki-shaped stream with injected negatives and dropout off: link-prediction
+outputs, every parameter gradient, the TGNMemory state (memory, last_update) after update_state, the
+parameters after Adam; then flush (train(False)) and TGB-style eval scores / reciprocal ranks.
+Parameters, Adam moments and memory are resynchronised from the oracle after each compared step
+(fp32 reduction order differs; the comparison is per step).  Tolerances: outputs 2e-5 abs, memory
+1e-5 abs, gradients 2e-3 relative (L2) per tensor.  gnn.conv.lin_key.bias has an exactly zero
+gradient (q_i·b_k is the same for every edge of a centre, softmax is shift invariant): both sides
+hold rounding noise, checked to be negligible against lin_key.weight's gradient, and Adam turns that
+noise into lr-sized steps, so its parameters are excluded from the after-step comparison."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHIFT_INVARIANT = "gnn.conv.lin_key.bias"
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def _setup(aggr, N=300, B=50, d=16, D=32, nb=10, seed=3, max_neg=20):
+    from oracle.sampler_ref import RefLastNeighborLoader
+    from oracle.tgn_ref import RefTGN
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.synth import make_stream
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    s = make_stream("tgbl-wiki", seed=seed, num_events=B * nb, num_nodes=N, msg_dim=d)
+    torch.manual_seed(0)
+    ref = RefTGN(N, d, hidden=D, aggr=aggr, dropout=0.0)
+    opt_ref = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    dev = torch.device("cuda")
+    model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=max_neg, aggr=aggr, dropout=0.0)
+    model.load_reference_state(ref.state_dict())
+    opt = TgnAdam(model, 1e-3)
+    loader = LastNeighborLoader(N, 10, device=dev)
+    eng = TgnEngine(model, loader, dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32), msg=s.msg), opt,
+                    dst_nodes=s.dst_nodes)
+    eng.reset_state()
+    return s, ref, opt_ref, RefLastNeighborLoader(N, 10), model, opt, eng
+
+
+def _sync(ref, opt_ref, model, opt):
+    from tgnx.tgn import PARAM_ORDER
+    named = dict(ref.named_parameters())
+    with torch.no_grad():
+        for name in PARAM_ORDER:
+            o, n, _ = model._views[name]
+            p = named[name]
+            model.flat[o:o + n].copy_(p.detach().reshape(-1))
+            st = opt_ref.state.get(p, {})
+            if st:
+                opt.exp_avg[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                opt.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+        model.memory.memory.copy_(ref.memory.memory)
+        model.memory.last_update.copy_(ref.memory.last_update)
+
+
+@pytest.mark.parametrize("aggr", ["last", "mean"])
+def test_tgn_train_steps_and_eval_match_oracle(aggr):
+    from oracle.tgn_ref import eval_step, mrr_per_event, train_step
+    from tgnx.tgn import PARAM_ORDER
+    B = 50
+    s, ref, opt_ref, lref, model, opt, eng = _setup(aggr)
+    ev_t = torch.from_numpy(s.t.astype(np.float32))
+    ev_msg = torch.from_numpy(s.msg)
+    rng = np.random.default_rng(1)
+    named = dict(ref.named_parameters())
+    worst = {}
+    for st in range(7):
+        a = st * B
+        sl = slice(a, a + B)
+        src, pos = torch.from_numpy(s.src[sl]), torch.from_numpy(s.dst[sl])
+        neg = torch.from_numpy(rng.choice(s.dst_nodes, size=B))
+        loss, po, no = train_step(ref, opt_ref, lref, ev_t, ev_msg, src, pos, neg, ev_t[sl], ev_msg[sl])
+        pg, ng = eng.train_batch(a, B, neg=neg)
+        torch.cuda.synchronize()
+        eng.check()
+        assert torch.allclose(pg.cpu(), po, atol=2e-5), (st, (pg.cpu() - po).abs().max())
+        assert torch.allclose(ng.cpu(), no, atol=2e-5), (st, (ng.cpu() - no).abs().max())
+        assert abs(float(model.grad_flat[-1]) - loss) < 1e-5 * max(1.0, abs(loss))
+        g = model.grads_by_name()
+        for name in PARAM_ORDER:
+            if name == SHIFT_INVARIANT:
+                scale = float(named["gnn.conv.lin_key.weight"].grad.norm()) + 1e-12
+                assert float(g[name].norm()) < 1e-4 * scale and float(named[name].grad.norm()) < 1e-4 * scale
+                continue
+            r = _rel(g[name], named[name].grad)
+            worst[name] = max(worst.get(name, 0.0), r)
+            assert r < 2e-3, (st, name, r)
+        assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5), st
+        assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update), st
+        for name in PARAM_ORDER:
+            if name == SHIFT_INVARIANT:
+                continue
+            o, n, _ = model._views[name]
+            assert torch.allclose(model.flat[o:o + n].cpu(), named[name].detach().reshape(-1), atol=5e-6, rtol=1e-4), \
+                (st, name)
+        _sync(ref, opt_ref, model, opt)
+    # train(False): flush both, then a TGB-style eval batch
+    ref.memory.train(False)
+    eng.flush()
+    torch.cuda.synchronize()
+    assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5)
+    assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update)
+    a = 7 * B
+    sl = slice(a, a + B)
+    src, pos = torch.from_numpy(s.src[sl]), torch.from_numpy(s.dst[sl])
+    negs = torch.from_numpy(rng.choice(s.dst_nodes, size=(B, 20)))
+    po, no = eval_step(ref, lref, ev_t, ev_msg, src, pos, negs, ev_t[sl], ev_msg[sl])
+    pg, ngm, rr = eng.eval_batch(a, B, negs)
+    torch.cuda.synchronize()
+    eng.check()
+    assert torch.allclose(pg.cpu(), po, atol=2e-5)
+    assert torch.allclose(ngm.cpu(), no, atol=2e-5)
+    assert np.allclose(rr.cpu().numpy(), mrr_per_event(po, no), atol=1e-6)
+    assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5)
+    assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update)

@@ -23,13 +23,17 @@ struct GemmShape {
   int M, N, K, KC, S, tiles_m, tiles_n;  // capacities: the grid is sized from these
   const int *Mdev, *Ndev, *Kdev;         // optional runtime sizes on the device (<= capacities)
 };
+// S <= smax splits; split s handles k-chunks s, s + S, ... (so a large or device-sized K does not
+// need a proportional grid).
 inline GemmShape gemm_shape(int M, int N, int K, int KC, const int* Mdev = nullptr, const int* Ndev = nullptr,
-                            const int* Kdev = nullptr) {
+                            const int* Kdev = nullptr, int smax = 16) {
   GemmShape g;
   g.M = M; g.N = N; g.K = K;
   g.Mdev = Mdev; g.Ndev = Ndev; g.Kdev = Kdev;
   g.KC = KC > GKC ? GKC : KC;
   g.S = (K + g.KC - 1) / g.KC;
+  if (g.S > smax) g.S = smax;
+  if (g.S < 1) g.S = 1;
   g.tiles_m = (M + GT - 1) / GT;
   g.tiles_n = (N + GT - 1) / GT;
   return g;
@@ -75,26 +79,13 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
   const int Mr = g.Mdev ? min(*g.Mdev, g.M) : g.M;
   const int Nr = g.Ndev ? min(*g.Ndev, g.N) : g.N;
   const int Kr = g.Kdev ? min(*g.Kdev, g.K) : g.K;
-  const int Sr = max(1, (Kr + g.KC - 1) / g.KC);  // splits that exist at run time
+  const int nchunk = (Kr + g.KC - 1) / g.KC;
+  const int Sr = max(1, min(g.S, nchunk));  // splits with work at run time
   const int tiles = g.tiles_m * g.tiles_n;
   const int tile = bid % tiles, s = bid / tiles;
   const int tm = tile / g.tiles_n, tn = tile % g.tiles_n;
-  const int m0 = tm * GT, n0 = tn * GT, k0 = s * g.KC;
+  const int m0 = tm * GT, n0 = tn * GT;
   if (m0 >= Mr || n0 >= Nr || s >= Sr) return;  // all workgroups of such a tile / split leave together
-  const int kc = max(0, min(g.KC, Kr - k0));
-  // ---- one-phase operand load (A as As[k][m], B as Bs[k][n])
-  for (int x = tid; x < GKC * GT; x += 256) {
-    int r, kk;
-    if (AL::k_fast) { r = x / GKC; kk = x % GKC; } else { r = x % GT; kk = x / GT; }
-    As[kk][r] = (kk < kc && m0 + r < Mr) ? al(m0 + r, k0 + kk) : 0.f;
-  }
-  for (int x = tid; x < GKC * GT; x += 256) {
-    int r, kk;
-    if (BL::k_fast) { r = x / GKC; kk = x % GKC; } else { r = x % GT; kk = x / GT; }
-    Bs[kk][r] = (kk < kc && n0 + r < Nr) ? bl(n0 + r, k0 + kk) : 0.f;
-  }
-  __syncthreads();
-  // ---- MFMA: wave quadrant (wr, wc) of 32x32 = 2x2 tiles of 16x16
   const int wr = (wv >> 1) * 32, wc = (wv & 1) * 32;
   const int li = lane & 15, lk = lane >> 4;
   f32x4_t acc[2][2];
@@ -102,13 +93,31 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
-  for (int kk = 0; kk < kc; kk += 4) {
-    const float a0 = As[kk + lk][wr + li], a1 = As[kk + lk][wr + 16 + li];
-    const float b0 = Bs[kk + lk][wc + li], b1 = Bs[kk + lk][wc + 16 + li];
-    acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+  for (int ch = s; ch < max(nchunk, 1); ch += g.S) {
+    const int k0 = ch * g.KC;
+    const int kc = max(0, min(g.KC, Kr - k0));
+    if (ch > s) __syncthreads();  // previous chunk's MFMA reads done
+    // ---- one-phase operand load (A as As[k][m], B as Bs[k][n])
+    for (int x = tid; x < GKC * GT; x += 256) {
+      int r, kk;
+      if (AL::k_fast) { r = x / GKC; kk = x % GKC; } else { r = x % GT; kk = x / GT; }
+      As[kk][r] = (kk < kc && m0 + r < Mr) ? al(m0 + r, k0 + kk) : 0.f;
+    }
+    for (int x = tid; x < GKC * GT; x += 256) {
+      int r, kk;
+      if (BL::k_fast) { r = x / GKC; kk = x % GKC; } else { r = x % GT; kk = x / GT; }
+      Bs[kk][r] = (kk < kc && n0 + r < Nr) ? bl(n0 + r, k0 + kk) : 0.f;
+    }
+    __syncthreads();
+    // ---- MFMA: wave quadrant (wr, wc) of 32x32 = 2x2 tiles of 16x16
+    for (int kk = 0; kk < kc; kk += 4) {
+      const float a0 = As[kk + lk][wr + li], a1 = As[kk + lk][wr + 16 + li];
+      const float b0 = Bs[kk + lk][wc + li], b1 = Bs[kk + lk][wc + 16 + li];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
   }
   __syncthreads();  // As is reused as the output tile below
   float (*Ct)[GPAD] = As;

@@ -1,0 +1,1650 @@
+// TGN memory path on gfx950 (SURVEY §8 a14–a16): the PyG TGN of the reference's modules/ directory,
+// wired as pyg_model_utils.py:10-36, trained by the canonical loop pyg_epoch_utils.py:106-137 carries
+// commented out.  Reference semantics restated in oracle/tgn_ref.py (the checker).
+//
+// One train step (B events, ~13 launches, no host sync):
+//   tgn_mark        negatives, bitmaps of centres (src/pos/neg) and of every sampled node
+//   tgn_scan (3 WG) sorted unique centres + edge offsets + update list, sorted unique nodes + assoc
+//                   ‖ ring-insert plan ‖ message-store sort of the batch
+//   tgn_agg_emit    sampled edges (neighbor_loader.py:26-50 order) ‖ per node: stored messages ->
+//                   IdentityMessage -> Last/Mean aggregate, updated last_update (memory_module.py:152-207)
+//   GEMM G1 ‖ G3    GRUCell over [msg | memory] with the gate math in the epilogue ‖ lin_edge over
+//                   [cos(w Δt + b) | msg] gathered on the fly (the per-neighbour QKV contraction)
+//   GEMM G2         lin_query/key/value/skip of every sampled node
+//   tgn_attn_fwd    TransformerConv softmax + aggregation per centre (wave per centre)
+//   tgn_pred_train  LinkPredictor + BCE + backward rows per event
+//   tgn_attn_bwd    attention backward ‖ predictor bias / output-layer / loss reductions
+//   GEMMs           dW_edge ‖ dW_proj, dW_src/dst ‖ Δt-encoding grads, dZ0 (+ GRU backward epilogue),
+//                   dW_gru ‖ message-encoding grads
+//   tgn_adam, tgn_update (memory / last_update of src ∪ dst, message stores, ring merge)
+#include "tgnx_gemm.h"
+#include "tgnx_math.h"
+#include "tgnx_ring_dev.h"
+
+namespace tgnx {
+
+void probe_begin(int id, hipStream_t s);
+void probe_end(int id, hipStream_t s);
+
+namespace tgn {
+
+constexpr int TH = 2;        // TransformerConv heads (emb_module.py:66)
+constexpr int TDMAX = 128;   // memory / time / embedding dim capacity (C = D / 2 <= 64 lanes)
+constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touch keys)
+enum { CNT_R = 0, CNT_M = 1, CNT_E = 2, CNT_U = 3, CNT_RUNS = 4, CNT_SRUNS = 5, CNT_LIST = 6, CNT_WORDS = 16 };
+
+__host__ __device__ inline int64_t al4(int64_t x) { return (x + 3) & ~int64_t(3); }
+
+struct Lay {
+  int64_t te_w, te_b, w_ih, w_hh, b_ih, b_hh, wk, bk, wq, bq, wv, bv, we, wsk, bsk, lsw, lsb, ldw, ldb, lfw, lfb, total;
+};
+static Lay make_lay(int D, int d) {
+  const int64_t Qm = 3 * (int64_t)D + d, HC = D;
+  Lay L;
+  int64_t o = 0;
+  L.te_w = o; o += al4(D);
+  L.te_b = o; o += al4(D);
+  L.w_ih = o; o += al4(3 * D * Qm);
+  L.w_hh = o; o += al4(3 * (int64_t)D * D);
+  L.b_ih = o; o += al4(3 * D);
+  L.b_hh = o; o += al4(3 * D);
+  L.wk = o; o += al4(HC * D);
+  L.bk = o; o += al4(HC);
+  L.wq = o; o += al4(HC * D);
+  L.bq = o; o += al4(HC);
+  L.wv = o; o += al4(HC * D);
+  L.bv = o; o += al4(HC);
+  L.we = o; o += al4(HC * (D + d));
+  L.wsk = o; o += al4(HC * D);
+  L.bsk = o; o += al4(HC);
+  L.lsw = o; o += al4((int64_t)D * D);
+  L.lsb = o; o += al4(D);
+  L.ldw = o; o += al4((int64_t)D * D);
+  L.ldb = o; o += al4(D);
+  L.lfw = o; o += al4(D);
+  L.lfb = o; o += al4(1);
+  L.total = o;
+  return L;
+}
+
+struct Ctx {
+  int64_t N, nev, words;
+  int K, D, d, Qm, HC, C, aggr, Kn, drop, gen_neg;
+  float p, inv_keep, lr, b1, b2, eps;
+  const int64_t *ev_src, *ev_dst;
+  const float *ev_t, *ev_msg;
+  int64_t* neg;
+  const int64_t* dst_nodes;
+  int64_t n_dst;
+  int64_t *nbr, *eid;
+  float* rt;
+  int64_t* assoc;
+  float* mem;
+  int64_t* lu_buf;
+  int64_t* st;     // [4N] {s_off, s_cnt, d_off, d_cnt}
+  int64_t* arena;  // [2 * nev] event ids, batch at event start s occupies [2s, 2s + 2B)
+  int32_t* node_gen;
+  float *params, *grads, *am, *av;
+  int64_t* ctl;
+  float *out_pos, *out_neg;
+  double* mrr;
+  // workspace
+  uint32_t *cb, *nb;
+  int* cnt;
+  int64_t *cent, *nid, *upd;
+  int *cent_loc, *ceoff, *crank, *upd_loc;
+  int *e_j, *e_c;
+  int64_t* e_id;
+  float* e_t;
+  float *X, *trel, *lu;
+  int64_t* xw;
+  float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
+  float *dZc, *dP, *dE, *dG, *tgp;
+  float* gpart;
+  int* tick;
+  uint64_t *rkeys, *skeys;
+  int *rruns, *sruns;
+  int Bmax, Qcap, Rcap, Mcap, Ecap, Ucap, tgp_rows;
+  size_t gpart_floats;
+  Lay L;
+};
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float softplusf(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
+
+// ------------------------------------------------------------------ sampling (neighbor_loader.py:26-50)
+// K1: every query entry marks its node as a centre and its node + valid ring neighbours as sampled;
+// train negatives are drawn here (NegLinkSamplerDest, counter-based stream as in tgnx_tgnn);
+// src / pos nodes are stamped for the update list (memory_module.py:129).
+template <bool TRAIN>
+__global__ void tgn_mark(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int gen = (int)c.ctl[TGNX_CTL_GEN];
+  const int Kn = TRAIN ? 1 : c.Kn;
+  const int nq = B * (2 + Kn);
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+    int64_t v;
+    if (q < B) {
+      v = c.ev_src[start + q];
+      c.node_gen[v] = gen;
+    } else if (q < 2 * B) {
+      v = c.ev_dst[start + q - B];
+      c.node_gen[v] = gen;
+    } else if (TRAIN) {
+      const int i = q - 2 * B;
+      if (c.gen_neg) {
+        const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+        const uint64_t off = (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
+        const int64_t pd = c.ev_dst[start + i];
+        v = c.dst_nodes[0];
+        for (uint64_t attempt = 0; attempt < 64; ++attempt) {
+          const uint64_t h = hash4(seed, 0x6E656773ull, off + (uint64_t)i, attempt);
+          v = c.dst_nodes[(uint64_t)(((__uint128_t)(h >> 11) * (uint64_t)c.n_dst) >> 53)];
+          if (v != pd) break;
+        }
+        c.neg[start + i] = v;
+      } else {
+        v = c.neg[start + i];
+      }
+    } else {
+      const int x = q - 2 * B;
+      v = c.neg[(start + x / Kn) * Kn + x % Kn];
+    }
+    atomicOr(&c.cb[v >> 5], 1u << (v & 31));
+    atomicOr(&c.nb[v >> 5], 1u << (v & 31));
+    for (int j = 0; j < c.K; ++j) {
+      if (c.eid[v * c.K + j] >= 0) {
+        const int64_t u = c.nbr[v * c.K + j];
+        atomicOr(&c.nb[u >> 5], 1u << (u & 31));
+      }
+    }
+  }
+}
+
+// message-store plan of a batch: (node << 33 | dir << 32 | i), dir 0 = as source (msg_s_store),
+// 1 = as destination (msg_d_store); sorted, each (node, dir) run lists its events in batch order
+// (memory_module.py:188-191 with a stable sort).
+__device__ void store_plan_block(const Ctx& c, int B, int64_t start, unsigned char* smem, int* sh) {
+  const int n2 = 2 * B, n = next_pow2(n2);
+  uint64_t* key = reinterpret_cast<uint64_t*>(smem);
+  int* runs = reinterpret_cast<int*>(smem + (size_t)n * 8);
+  uint64_t* tmp = reinterpret_cast<uint64_t*>(smem + (size_t)n * 8 + (size_t)(n2 + 2) * 4 + 8);
+  for (int p = threadIdx.x; p < n; p += blockDim.x) {
+    uint64_t k = ~0ull;
+    if (p < n2) {
+      const int i = p < B ? p : p - B, dir = p < B ? 0 : 1;
+      const uint64_t node = (uint64_t)(dir == 0 ? c.ev_src[start + i] : c.ev_dst[start + i]);
+      k = (node << 33) | ((uint64_t)dir << 32) | (uint64_t)i;
+    }
+    key[p] = k;
+  }
+  __syncthreads();
+  sort_u64(key, tmp, n2, n);
+  const int T = blockDim.x, pc = (n2 + T - 1) / T;
+  const int p0 = threadIdx.x * pc, p1 = min(n2, p0 + pc);
+  int cntr = 0;
+  for (int p = p0; p < p1; ++p) cntr += (p == 0 || (key[p] >> 32) != (key[p - 1] >> 32));
+  int U;
+  int rid = block_excl_scan(cntr, sh, &U);
+  for (int p = p0; p < p1; ++p)
+    if (p == 0 || (key[p] >> 32) != (key[p - 1] >> 32)) runs[rid++] = p;
+  __syncthreads();
+  for (int p = threadIdx.x; p < n2; p += T) c.skeys[p] = key[p];
+  for (int r = threadIdx.x; r < U; r += T) c.sruns[r] = runs[r];
+  if (threadIdx.x == 0) {
+    c.sruns[U] = n2;
+    c.cnt[CNT_SRUNS] = U;
+  }
+}
+
+// K2 (3 workgroups): WG0 ordered bitmap walks -> centres (+ edge offsets, update list) and sampled
+// nodes (+ assoc, centre ranks); WG1 ring-insert plan; WG2 message-store plan.
+__host__ __device__ inline size_t tgn_scan_smem(int Bmax) {
+  const int n = next_pow2(2 * Bmax);
+  return (size_t)n * 16 + (size_t)(2 * Bmax + 4) * 4 + 64;
+}
+template <bool TRAIN>
+__global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int sh[20];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int tid = threadIdx.x, T = blockDim.x;
+  if (blockIdx.x == 1) {
+    uint64_t* key;
+    int* runs;
+    const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs);
+    for (int p = tid; p < 2 * B; p += T) c.rkeys[p] = key[p];
+    for (int r = tid; r < U; r += T) c.rruns[r] = runs[r];
+    if (tid == 0) {
+      c.rruns[U] = 2 * B;
+      c.cnt[CNT_RUNS] = U;
+    }
+    return;
+  }
+  if (blockIdx.x == 2) {
+    store_plan_block(c, B, start, smem, sh);
+    return;
+  }
+  const int gen = (int)c.ctl[TGNX_CTL_GEN];
+  const int64_t W = c.words;
+  const int64_t wc = (W + T - 1) / T, w0 = tid * wc, w1 = min(W, w0 + wc);
+  // centres: count, ring slots, update nodes
+  int nc = 0, ne = 0, nu = 0;
+  for (int64_t w = w0; w < w1; ++w) {
+    uint32_t m = c.cb[w];
+    while (m) {
+      const int b = __ffs(m) - 1;
+      m &= m - 1;
+      const int64_t v = (w << 5) + b;
+      ++nc;
+      for (int j = 0; j < c.K; ++j) ne += c.eid[v * c.K + j] >= 0;
+      nu += c.node_gen[v] == gen;
+    }
+  }
+  int R, E, U;
+  int rc = block_excl_scan(nc, sh, &R);
+  int re = block_excl_scan(ne, sh, &E);
+  int ru = block_excl_scan(nu, sh, &U);
+  const bool fits_c = R <= c.Rcap && E <= c.Ecap && U <= c.Ucap;
+  for (int64_t w = w0; w < w1; ++w) {
+    uint32_t m = c.cb[w];
+    if (!m) continue;
+    c.cb[w] = 0u;
+    while (m) {
+      const int b = __ffs(m) - 1;
+      m &= m - 1;
+      const int64_t v = (w << 5) + b;
+      int k = 0;
+      for (int j = 0; j < c.K; ++j) k += c.eid[v * c.K + j] >= 0;
+      if (fits_c) {
+        c.cent[rc] = v;
+        c.ceoff[rc] = re;
+        if (c.node_gen[v] == gen) c.upd[ru++] = v;
+      }
+      ++rc;
+      re += k;
+    }
+  }
+  // sampled nodes
+  int np = 0;
+  for (int64_t w = w0; w < w1; ++w) np += __popc(c.nb[w]);
+  int M;
+  int rank = block_excl_scan(np, sh, &M);
+  const bool fits = fits_c && M <= c.Mcap;
+  for (int64_t w = w0; w < w1; ++w) {
+    uint32_t m = c.nb[w];
+    if (!m) continue;
+    c.nb[w] = 0u;
+    while (m) {
+      const int b = __ffs(m) - 1;
+      m &= m - 1;
+      const int64_t v = (w << 5) + b;
+      if (fits) c.nid[rank] = v;
+      c.assoc[v] = rank;
+      ++rank;
+    }
+  }
+  if (!fits) {
+    if (tid == 0) c.ctl[TGNX_CTL_ERR] |= 4;
+    return;
+  }
+  for (int x = tid; x < M; x += T) c.crank[x] = -1;
+  __syncthreads();
+  for (int x = tid; x < R; x += T) {
+    const int loc = (int)c.assoc[c.cent[x]];
+    c.cent_loc[x] = loc;
+    c.crank[loc] = x;
+  }
+  for (int x = tid; x < U; x += T) c.upd_loc[x] = (int)c.assoc[c.upd[x]];
+  if (tid == 0) {
+    c.ceoff[R] = E;
+    c.cnt[CNT_R] = R;
+    c.cnt[CNT_M] = M;
+    c.cnt[CNT_E] = E;
+    c.cnt[CNT_U] = U;
+  }
+}
+
+// ------------------------------------------------------------------ messages (memory_module.py:152-207)
+// Aggregated message of node n (wave): IdentityMessage [mem[n], mem[other], raw, cos(w (t - lu[n]) + b)]
+// of its stored events, LastAggregator (first max t over [msg_s; msg_d], msg_agg.py:15-21) or
+// MeanAggregator (msg_agg.py:24-26); lu_new = max t (0 without messages, PyG scatter 'max').
+__device__ void agg_node(const Ctx& c, int64_t n, int m, int lane) {
+  const int D = c.D, d = c.d, Qm = c.Qm;
+  const int64_t so = c.st[4 * n], sc = c.st[4 * n + 1], dof = c.st[4 * n + 2], dc = c.st[4 * n + 3];
+  const int tot = (int)(sc + dc);
+  float* X = c.X + (int64_t)m * Qm;
+  const float* P = c.params;
+  if (tot == 0) {
+    for (int k = lane; k < Qm; k += 64) X[k] = 0.f;
+    if (lane == 0) {
+      c.xw[m] = -1;
+      c.trel[m] = 0.f;
+      c.lu[m] = 0.f;
+    }
+    return;
+  }
+  auto ev_of = [&](int k) -> int64_t { return k < sc ? c.arena[so + k] : c.arena[dof + (k - sc)]; };
+  const float lun = (float)c.lu_buf[n];
+  if (c.aggr == 0) {
+    float tb = -INFINITY;
+    int kb = 0x7fffffff;
+    for (int k = lane; k < tot; k += 64) {
+      const float t = c.ev_t[ev_of(k)];
+      if (t > tb) { tb = t; kb = k; }
+    }
+    const float tm = wave_max(tb);
+    int kk = tb == tm ? kb : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) kk = min(kk, __shfl_xor(kk, o, 64));
+    const int64_t e = ev_of(kk);
+    const int64_t other = kk < sc ? c.ev_dst[e] : c.ev_src[e];
+    const float tr = c.ev_t[e] - lun;
+    for (int k = lane; k < Qm; k += 64) {
+      float x;
+      if (k < D) x = c.mem[n * D + k];
+      else if (k < 2 * D) x = c.mem[other * D + (k - D)];
+      else if (k < 2 * D + d) x = c.ev_msg[e * d + (k - 2 * D)];
+      else {
+        const int q = k - 2 * D - d;
+        x = te_cos(fmaf(P[c.L.te_w + q], tr, P[c.L.te_b + q]));
+      }
+      X[k] = x;
+    }
+    if (lane == 0) {
+      c.xw[m] = e;
+      c.trel[m] = tr;
+      c.lu[m] = tm;
+    }
+  } else {
+    float tmax = -INFINITY;
+    for (int k = lane; k < Qm; k += 64) {
+      float s = 0.f;
+      for (int q = 0; q < tot; ++q) {  // event order: PyG scatter-sum order, then / count
+        const int64_t e = ev_of(q);
+        float x;
+        if (k < D) x = c.mem[n * D + k];
+        else if (k < 2 * D) x = c.mem[(q < sc ? c.ev_dst[e] : c.ev_src[e]) * D + (k - D)];
+        else if (k < 2 * D + d) x = c.ev_msg[e * d + (k - 2 * D)];
+        else {
+          const int qq = k - 2 * D - d;
+          x = te_cos(fmaf(P[c.L.te_w + qq], c.ev_t[e] - lun, P[c.L.te_b + qq]));
+        }
+        s += x;
+      }
+      X[k] = s / (float)tot;
+    }
+    for (int q = lane; q < tot; q += 64) tmax = fmaxf(tmax, c.ev_t[ev_of(q)]);
+    tmax = wave_max(tmax);
+    if (lane == 0) {
+      c.xw[m] = 1;
+      c.trel[m] = 0.f;
+      c.lu[m] = tmax;
+    }
+  }
+}
+
+// K3: blocks [0, nemit): sampled edges, thread per centre (centre-ascending, ring order = e_id
+// descending); the rest: mode 0 aggregation over the sampled nodes (train) + zeroing of the
+// backward accumulators, mode 1 last_update of the sampled nodes from the buffer (eval scoring),
+// mode 2 aggregation over a node list (eval update / flush; list == nullptr: nodes base + m).
+__global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nemit, const int64_t* list,
+                                                    const int* list_cnt, int n_host, int64_t base) {
+  if (mode != 2) {
+    const int B = (int)c.ctl[TGNX_CTL_B];
+    if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  }
+  if ((int)blockIdx.x < nemit) {
+    const int R = c.cnt[CNT_R];
+    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < R; x += nemit * blockDim.x) {
+      const int64_t v = c.cent[x];
+      int o = c.ceoff[x];
+      for (int j = 0; j < c.K; ++j) {
+        const int64_t e = c.eid[v * c.K + j];
+        if (e < 0) continue;
+        c.e_j[o] = (int)c.assoc[c.nbr[v * c.K + j]];
+        c.e_c[o] = x;
+        c.e_id[o] = e;
+        c.e_t[o] = c.rt[v * c.K + j];
+        ++o;
+      }
+    }
+    return;
+  }
+  const int bid = blockIdx.x - nemit, nb = gridDim.x - nemit;
+  const int lane = threadIdx.x & 63;
+  if (mode == 1) {
+    const int M = c.cnt[CNT_M];
+    for (int x = bid * blockDim.x + threadIdx.x; x < M; x += nb * blockDim.x) c.lu[x] = (float)c.lu_buf[c.nid[x]];
+    return;
+  }
+  if (mode == 0) {  // zero the atomically accumulated backward rows
+    const int M = c.cnt[CNT_M], R = c.cnt[CNT_R];
+    for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)M * 4 * c.HC; x += (int64_t)nb * blockDim.x)
+      c.dP[x] = 0.f;
+    for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R * c.HC; x += (int64_t)nb * blockDim.x)
+      c.dZc[x] = 0.f;
+  }
+  const int n = mode == 0 ? c.cnt[CNT_M] : (list_cnt ? *list_cnt : n_host);
+  for (int m = bid * 4 + (threadIdx.x >> 6); m < n; m += nb * 4) {
+    const int64_t v = mode == 0 ? c.nid[m] : (list ? list[m] : base + m);
+    agg_node(c, v, m, lane);
+  }
+}
+
+// ------------------------------------------------------------------ GEMM operands / epilogues
+// GRU input row m: [aggregated message (Qm) | memory of the node (D)]
+struct LoadGruA {
+  const float* X;
+  const float* mem;
+  const int64_t* list;  // node of row m (nullptr: base + m)
+  int64_t base;
+  int Qm, D;
+  static constexpr bool k_fast = true;
+  __device__ float operator()(int m, int k) const {
+    if (k < Qm) return X[(int64_t)m * Qm + k];
+    const int64_t v = list ? list[m] : base + m;
+    return mem[v * D + (k - Qm)];
+  }
+};
+// GRU weights with gates interleaved by unit: row 4j+g = (r, z, n_input, n_hidden) of unit j over
+// the columns [message | memory] (GRUCell weight_ih [3D, Qm], weight_hh [3D, D]).
+struct LoadGruW {
+  const float *wih, *whh;
+  int Qm, D;
+  static constexpr bool k_fast = true;
+  __device__ float operator()(int n, int k) const {
+    const int j = n >> 2, g = n & 3;
+    if (k < Qm) return g == 3 ? 0.f : wih[(int64_t)(g * D + j) * Qm + k];
+    return g == 2 ? 0.f : whh[(int64_t)((g == 3 ? 2 : g) * D + j) * D + (k - Qm)];
+  }
+};
+// GRUCell (torch gru_cell: r, z = σ(gi + gh), n = tanh(gi_n + r gh_n), h' = (h - n) z + n)
+struct EpiGru {
+  const float *bih, *bhh, *mem;
+  const int64_t* list;
+  int64_t base;
+  int D;
+  float *Z0, *gates;
+  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
+    for (int x = threadIdx.x; x < GT * (GT / 4); x += blockDim.x) {
+      const int r = x / (GT / 4), u = x % (GT / 4), m = m0 + r, j = n0 / 4 + u;
+      if (m >= M || 4 * j >= N) continue;
+      const float* row = Ct + r * GPAD + 4 * u;
+      const float pr = row[0] + (bih[j] + bhh[j]);
+      const float pz = row[1] + (bih[D + j] + bhh[D + j]);
+      const float gin = row[2] + bih[2 * D + j];
+      const float ghn = row[3] + bhh[2 * D + j];
+      const float rr = sigm(pr), zz = sigm(pz);
+      const float nn = tanhf(gin + rr * ghn);
+      const int64_t v = list ? list[m] : base + m;
+      const float h = mem[v * D + j];
+      Z0[(int64_t)m * D + j] = (h - nn) * zz + nn;
+      float4* gp = reinterpret_cast<float4*>(gates + ((int64_t)m * D + j) * 4);
+      *gp = make_float4(rr, zz, nn, ghn);
+    }
+  }
+};
+// TransformerConv edge attribute of sampled edge e: [cos(w (lu[src] - t_e) + b) | msg[e_id]]
+// (emb_module.py:69-72, rel_t = last_update[edge_index[0]] - t)
+struct LoadEdgeAttr {
+  const int* e_j;
+  const int64_t* e_id;
+  const float *e_t, *lu, *ev_msg, *tw, *tb;
+  int D, d;
+  static constexpr bool k_fast = true;
+  __device__ float operator()(int e, int k) const {
+    if (k < D) return te_cos(fmaf(tw[k], lu[e_j[e]] - e_t[e], tb[k]));
+    return ev_msg[e_id[e] * d + (k - D)];
+  }
+};
+// same operand with rows / columns swapped (B operand of dW_edge = dEᵀ EA)
+struct LoadEdgeAttrT {
+  LoadEdgeAttr a;
+  static constexpr bool k_fast = false;
+  __device__ float operator()(int n, int e) const { return a(e, n); }
+};
+// node-embedding input row m: train z0 (GRU output), eval memory[nid[m]] (memory_module.py:121-122)
+struct LoadZ {
+  const float* Z0;
+  const float* mem;
+  const int64_t* nid;
+  int D, eval;
+  static constexpr bool k_fast = true;
+  __device__ float operator()(int m, int k) const { return eval ? mem[nid[m] * D + k] : Z0[(int64_t)m * D + k]; }
+};
+// stacked [W_query; W_key; W_value; W_skip] rows (n / HC selects the linear)
+struct LoadProjW {
+  const float *wq, *wk, *wv, *ws;
+  int HC, D;
+  static constexpr bool k_fast = true;
+  __device__ float operator()(int n, int k) const {
+    const int g = n / HC, r = n % HC;
+    const float* w = g == 0 ? wq : g == 1 ? wk : g == 2 ? wv : ws;
+    return w[(int64_t)r * D + k];
+  }
+};
+struct EpiProj {
+  const float *bq, *bk, *bv, *bs;
+  float* P;
+  int HC;
+  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
+    for (int x = threadIdx.x; x < GT * GT; x += blockDim.x) {
+      const int r = x / GT, cc = x % GT, m = m0 + r, n = n0 + cc;
+      if (m >= M || n >= N) continue;
+      const int g = n / HC, q = n % HC;
+      const float* b = g == 0 ? bq : g == 1 ? bk : g == 2 ? bv : bs;
+      P[(int64_t)m * N + n] = Ct[r * GPAD + cc] + b[q];
+    }
+  }
+};
+
+// ------------------------------------------------------------------ attention (TransformerConv)
+// Wave per centre x (node row i): lane l < C holds channel l (head 0) and C + l (head 1).
+// P row = [q | k | v | skip] (lin_query / key / value / skip + biases); Ep row = lin_edge(edge_attr).
+// score_eh = (q_i · (k_j + e))_h / sqrt(C); alpha = PyG softmax (max-shifted, +1e-16); attention
+// dropout (train); out_i = Σ_e alpha~ (v_j + e) + skip_i.  Lane e keeps edge e's per-edge scalars.
+__device__ __forceinline__ float att_keep(const Ctx& c, uint64_t seed, int e, int h) {
+  return keep32(drop_base(seed, 7, (uint64_t)e, 0), (uint32_t)h, c.p, c.inv_keep);
+}
+template <bool TRAIN>
+__global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int R = c.cnt[CNT_R];
+  const int lane = threadIdx.x & 63;
+  const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (x >= R) return;
+  const int C = c.C, HC = c.HC;
+  const bool okl = lane < C;
+  const int l0 = okl ? lane : 0;
+  const int i = c.cent_loc[x];
+  const float* Pi = c.P + (int64_t)i * 4 * HC;
+  const float q0 = Pi[l0], q1 = Pi[C + l0];
+  const float sqc = sqrtf((float)C);
+  const int e0 = c.ceoff[x], ne = c.ceoff[x + 1] - e0;
+  float my0 = -INFINITY, my1 = -INFINITY;
+  for (int e = 0; e < ne; ++e) {
+    const float* Pj = c.P + (int64_t)c.e_j[e0 + e] * 4 * HC;
+    const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
+    float p0 = okl ? q0 * (Pj[HC + l0] + Ee[l0]) : 0.f;
+    float p1 = okl ? q1 * (Pj[HC + C + l0] + Ee[C + l0]) : 0.f;
+    p0 = wave_sum(p0) / sqc;
+    p1 = wave_sum(p1) / sqc;
+    if (lane == e) { my0 = p0; my1 = p1; }
+  }
+  const float mx0 = wave_max(my0), mx1 = wave_max(my1);
+  const float ex0 = lane < ne ? expf(my0 - mx0) : 0.f, ex1 = lane < ne ? expf(my1 - mx1) : 0.f;
+  const float a0 = ex0 / (wave_sum(ex0) + 1e-16f), a1 = ex1 / (wave_sum(ex1) + 1e-16f);
+  float t0 = a0, t1 = a1;
+  if (TRAIN && lane < ne) {
+    c.alpha[(int64_t)(e0 + lane) * 2] = a0;
+    c.alpha[(int64_t)(e0 + lane) * 2 + 1] = a1;
+    if (c.drop) {
+      const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+      t0 *= att_keep(c, seed, e0 + lane, 0);
+      t1 *= att_keep(c, seed, e0 + lane, 1);
+    }
+  }
+  float o0 = 0.f, o1 = 0.f;
+  for (int e = 0; e < ne; ++e) {
+    const float b0 = __shfl(t0, e, 64), b1 = __shfl(t1, e, 64);
+    const float* Pj = c.P + (int64_t)c.e_j[e0 + e] * 4 * HC;
+    const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
+    o0 += (Pj[2 * HC + l0] + Ee[l0]) * b0;
+    o1 += (Pj[2 * HC + C + l0] + Ee[C + l0]) * b1;
+  }
+  if (okl) {
+    c.Zc[(int64_t)x * HC + lane] = o0 + Pi[3 * HC + lane];
+    c.Zc[(int64_t)x * HC + C + lane] = o1 + Pi[3 * HC + C + lane];
+  }
+}
+
+// ------------------------------------------------------------------ link prediction (decoder.py:108-123)
+// Workgroup per event of this rank's slice: h = relu(lin_src(z_s) + lin_dst(z_d)), s = sigmoid(lin_final(h)),
+// loss = BCEWithLogits(s_pos, 1) + BCEWithLogits(s_neg, 0) (the reference feeds the sigmoid output to
+// BCEWithLogitsLoss), backward rows, dz rows accumulated into the centres' dZc.
+// evs row: zs | zp | zn | dhp | dhn | hp | hn (D each) | a_p a_n s_p s_n da_p da_n loss pad
+__host__ __device__ inline int evs_stride(int D) { return 7 * D + 8; }
+__global__ void __launch_bounds__(256) tgn_pred_train(Ctx c) {
+  __shared__ float z[3][TDMAX];
+  __shared__ float part[4][3][TDMAX];
+  __shared__ float dh[2][TDMAX];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
+  if (blockIdx.x == 0 && threadIdx.x == 0) c.cnt[CNT_LIST] = 3 * (hi - lo);
+  const int i = lo + blockIdx.x;
+  if (B == 0 || i >= hi || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int D = c.D;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int64_t roots[3] = {c.ev_src[start + i], c.ev_dst[start + i], c.neg[start + i]};
+  int cr[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) cr[r] = c.crank[c.assoc[roots[r]]];
+  for (int x = tid; x < 3 * D; x += blockDim.x) z[x / D][x % D] = c.Zc[(int64_t)cr[x / D] * D + x % D];
+  __syncthreads();
+  const float* P = c.params;
+  const float* Wsrc = P + c.L.lsw;
+  const float* Wdst = P + c.L.ldw;
+  const int kc = (D + 3) / 4, k0 = wv * kc, nk = min(D - k0, kc);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {  // lin_src(z_s), lin_dst(z_p), lin_dst(z_n): split contraction
+    const int o = lane + 64 * q;
+    if (o < D) {
+      float a = 0.f, b = 0.f, d2 = 0.f;
+      for (int k = 0; k < nk; ++k) {
+        const float ws = Wsrc[(int64_t)o * D + k0 + k], wd = Wdst[(int64_t)o * D + k0 + k];
+        a += ws * z[0][k0 + k];
+        b += wd * z[1][k0 + k];
+        d2 += wd * z[2][k0 + k];
+      }
+      part[wv][0][o] = a;
+      part[wv][1][o] = b;
+      part[wv][2][o] = d2;
+    }
+  }
+  __syncthreads();
+  float* ev = c.evs + (int64_t)i * evs_stride(D);
+  if (wv == 0) {
+    float hp[2], hn[2], zp = 0.f, zn = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int o = lane + 64 * q;
+      hp[q] = hn[q] = 0.f;
+      if (o < D) {
+        const float s = ((part[0][0][o] + part[1][0][o]) + (part[2][0][o] + part[3][0][o])) + P[c.L.lsb + o];
+        const float dp = ((part[0][1][o] + part[1][1][o]) + (part[2][1][o] + part[3][1][o])) + P[c.L.ldb + o];
+        const float dn = ((part[0][2][o] + part[1][2][o]) + (part[2][2][o] + part[3][2][o])) + P[c.L.ldb + o];
+        hp[q] = fmaxf(s + dp, 0.f);
+        hn[q] = fmaxf(s + dn, 0.f);
+        zp += P[c.L.lfw + o] * hp[q];
+        zn += P[c.L.lfw + o] * hn[q];
+      }
+    }
+    const float ap = wave_sum(zp) + P[c.L.lfb], an = wave_sum(zn) + P[c.L.lfb];
+    const float sp = sigm(ap), sn = sigm(an);
+    const float invB = 1.0f / (float)B;
+    const float dap = (sigm(sp) - 1.0f) * sp * (1.0f - sp) * invB;
+    const float dan = sigm(sn) * sn * (1.0f - sn) * invB;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int o = lane + 64 * q;
+      if (o < D) {
+        const float wf = P[c.L.lfw + o];
+        const float dhp = hp[q] > 0.f ? dap * wf : 0.f;
+        const float dhn = hn[q] > 0.f ? dan * wf : 0.f;
+        dh[0][o] = dhp;
+        dh[1][o] = dhn;
+        ev[o] = z[0][o];
+        ev[D + o] = z[1][o];
+        ev[2 * D + o] = z[2][o];
+        ev[3 * D + o] = dhp;
+        ev[4 * D + o] = dhn;
+        ev[5 * D + o] = hp[q];
+        ev[6 * D + o] = hn[q];
+      }
+    }
+    if (lane == 0) {
+      float* s = ev + 7 * D;
+      s[0] = ap; s[1] = an; s[2] = sp; s[3] = sn; s[4] = dap; s[5] = dan;
+      s[6] = (softplusf(-sp) + softplusf(sn)) * invB;
+      c.out_pos[i] = sp;
+      c.out_neg[i] = sn;
+    }
+  }
+  __syncthreads();
+  // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn (split over k, coalesced over o)
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int o = lane + 64 * q;
+    if (o < D) {
+      float a = 0.f, b = 0.f, d2 = 0.f;
+      for (int k = 0; k < nk; ++k) {
+        const int kk = k0 + k;
+        a += Wsrc[(int64_t)kk * D + o] * (dh[0][kk] + dh[1][kk]);
+        b += Wdst[(int64_t)kk * D + o] * dh[0][kk];
+        d2 += Wdst[(int64_t)kk * D + o] * dh[1][kk];
+      }
+      part[wv][0][o] = a;
+      part[wv][1][o] = b;
+      part[wv][2][o] = d2;
+    }
+  }
+  __syncthreads();
+  for (int x = tid; x < 3 * D; x += blockDim.x) {
+    const int r = x / D, o = x % D;
+    const float g = (part[0][r][o] + part[1][r][o]) + (part[2][r][o] + part[3][r][o]);
+    atomicAdd(&c.dZc[(int64_t)cr[r] * D + o], g);
+  }
+}
+
+// predictor bias / output-layer / loss reductions over this rank's events (wave per output)
+__device__ void lp_vec_body(const Ctx& c, int y, int lane) {
+  const int D = c.D;
+  if (y >= 3 * D + 2) return;
+  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
+  const bool ok = c.ctl[TGNX_CTL_B] > 0 && c.ctl[TGNX_CTL_ERR] == 0;
+  const int S = evs_stride(D);
+  float s = 0.f;
+  for (int i = lo + lane; i < hi && ok; i += 64) {
+    const float* ev = c.evs + (int64_t)i * S;
+    if (y < 2 * D) s += ev[3 * D + (y % D)] + ev[4 * D + (y % D)];
+    else if (y < 3 * D) s += ev[7 * D + 4] * ev[5 * D + (y - 2 * D)] + ev[7 * D + 5] * ev[6 * D + (y - 2 * D)];
+    else if (y == 3 * D) s += ev[7 * D + 4] + ev[7 * D + 5];
+    else s += ev[7 * D + 6];
+  }
+  s = wave_sum(s);
+  if (lane == 0) {
+    float* g = c.grads;
+    if (y < D) g[c.L.lsb + y] = s;
+    else if (y < 2 * D) g[c.L.ldb + y - D] = s;
+    else if (y < 3 * D) g[c.L.lfw + y - 2 * D] = s;
+    else if (y == 3 * D) g[c.L.lfb] = s;
+    else g[c.L.total] = s;  // batch loss slot
+  }
+}
+
+// Backward of tgn_attn_fwd (wave per centre) ‖ trailing blocks: lp_vec_body.
+__global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
+  if ((int)blockIdx.x >= ncb) {
+    lp_vec_body(c, ((int)blockIdx.x - ncb) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+    return;
+  }
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int R = c.cnt[CNT_R];
+  const int lane = threadIdx.x & 63;
+  const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (x >= R) return;
+  const int C = c.C, HC = c.HC;
+  const bool okl = lane < C;
+  const int l0 = okl ? lane : 0;
+  const int i = c.cent_loc[x];
+  const float* Pi = c.P + (int64_t)i * 4 * HC;
+  float* dPi = c.dP + (int64_t)i * 4 * HC;
+  const float q0 = Pi[l0], q1 = Pi[C + l0];
+  const float g0 = okl ? c.dZc[(int64_t)x * HC + lane] : 0.f, g1 = okl ? c.dZc[(int64_t)x * HC + C + lane] : 0.f;
+  const float sqc = sqrtf((float)C);
+  const int e0 = c.ceoff[x], ne = c.ceoff[x + 1] - e0;
+  const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+  float a0 = 0.f, a1 = 0.f, k0v = 1.f, k1v = 1.f;
+  if (lane < ne) {
+    a0 = c.alpha[(int64_t)(e0 + lane) * 2];
+    a1 = c.alpha[(int64_t)(e0 + lane) * 2 + 1];
+    if (c.drop) {
+      k0v = att_keep(c, seed, e0 + lane, 0);
+      k1v = att_keep(c, seed, e0 + lane, 1);
+    }
+  }
+  // d alpha~_eh = Σ_{ch in h} dout (v_j + e); d alpha = d alpha~ * keep
+  float da0 = 0.f, da1 = 0.f;
+  for (int e = 0; e < ne; ++e) {
+    const float* Pj = c.P + (int64_t)c.e_j[e0 + e] * 4 * HC;
+    const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
+    float p0 = okl ? g0 * (Pj[2 * HC + l0] + Ee[l0]) : 0.f;
+    float p1 = okl ? g1 * (Pj[2 * HC + C + l0] + Ee[C + l0]) : 0.f;
+    p0 = wave_sum(p0);
+    p1 = wave_sum(p1);
+    if (lane == e) { da0 = p0 * k0v; da1 = p1 * k1v; }
+  }
+  // softmax backward: d score = alpha (d alpha - Σ alpha d alpha)
+  const float s0 = wave_sum(a0 * da0), s1 = wave_sum(a1 * da1);
+  const float ds0 = a0 * (da0 - s0), ds1 = a1 * (da1 - s1);
+  const float t0 = a0 * k0v, t1 = a1 * k1v;
+  float dq0 = 0.f, dq1 = 0.f;
+  for (int e = 0; e < ne; ++e) {
+    const float d0 = __shfl(ds0, e, 64) / sqc, d1 = __shfl(ds1, e, 64) / sqc;
+    const float b0 = __shfl(t0, e, 64), b1 = __shfl(t1, e, 64);
+    const int j = c.e_j[e0 + e];
+    const float* Pj = c.P + (int64_t)j * 4 * HC;
+    const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
+    float* dPj = c.dP + (int64_t)j * 4 * HC;
+    float* dEe = c.dE + (int64_t)(e0 + e) * HC;
+    if (okl) {
+      dq0 += d0 * (Pj[HC + lane] + Ee[lane]);
+      dq1 += d1 * (Pj[HC + C + lane] + Ee[C + lane]);
+      const float dk0 = d0 * q0, dk1 = d1 * q1;
+      const float dv0 = b0 * g0, dv1 = b1 * g1;
+      dEe[lane] = dk0 + dv0;
+      dEe[C + lane] = dk1 + dv1;
+      atomicAdd(&dPj[HC + lane], dk0);
+      atomicAdd(&dPj[HC + C + lane], dk1);
+      atomicAdd(&dPj[2 * HC + lane], dv0);
+      atomicAdd(&dPj[2 * HC + C + lane], dv1);
+    }
+  }
+  if (okl) {
+    dPi[lane] = dq0;
+    dPi[C + lane] = dq1;
+    dPi[3 * HC + lane] = g0;
+    dPi[3 * HC + C + lane] = g1;
+  }
+}
+
+// ------------------------------------------------------------------ backward GEMM operands / epilogues
+// (n, m) -> z0[m][n], and 1 in the extra column n == D (bias gradient)
+struct LoadZ1T {
+  const float* Z0;
+  int D;
+  static constexpr bool k_fast = false;
+  __device__ float operator()(int n, int m) const { return n < D ? Z0[(int64_t)m * D + n] : 1.0f; }
+};
+struct EpiProjGrad {
+  float* g;
+  int64_t wq, bq, wk, bk, wv, bv, ws, bs;
+  int HC, D;
+  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
+    for (int x = threadIdx.x; x < GT * GT; x += blockDim.x) {
+      const int r = x / GT, cc = x % GT, row = m0 + r, n = n0 + cc;
+      if (row >= M || n >= N) continue;
+      const int gi = row / HC, q = row % HC;
+      const float v = Ct[r * GPAD + cc];
+      const int64_t W = gi == 0 ? wq : gi == 1 ? wk : gi == 2 ? wv : ws;
+      const int64_t Bb = gi == 0 ? bq : gi == 1 ? bk : gi == 2 ? bv : bs;
+      if (n < D) g[W + (int64_t)q * D + n] = v;
+      else g[Bb + q] = v;
+    }
+  }
+};
+// link predictor weight grads as one GEMM over 3 * nloc rows (block-diagonal K):
+// rows r < D: dW_src = Σ (dhp + dhn) zsᵀ ; rows r >= D: dW_dst = Σ dhp zpᵀ + dhn znᵀ
+struct LoadLpA {
+  const float* evs;
+  const int64_t* ctl;
+  int D, S;
+  static constexpr bool k_fast = false;
+  __device__ float operator()(int r, int k) const {
+    const int lo = (int)ctl[TGNX_CTL_LO], nloc = (int)(ctl[TGNX_CTL_HI] - ctl[TGNX_CTL_LO]);
+    const int blk = k / nloc, i = lo + k % nloc;
+    const float* ev = evs + (int64_t)i * S;
+    if (r < D) return blk == 0 ? ev[3 * D + r] + ev[4 * D + r] : 0.f;
+    return blk == 1 ? ev[3 * D + r - D] : blk == 2 ? ev[4 * D + r - D] : 0.f;
+  }
+};
+struct LoadLpB {
+  const float* evs;
+  const int64_t* ctl;
+  int D, S;
+  static constexpr bool k_fast = false;
+  __device__ float operator()(int n, int k) const {
+    const int lo = (int)ctl[TGNX_CTL_LO], nloc = (int)(ctl[TGNX_CTL_HI] - ctl[TGNX_CTL_LO]);
+    const int blk = k / nloc, i = lo + k % nloc;
+    return evs[(int64_t)i * S + blk * D + n];
+  }
+};
+struct EpiLpGrad {
+  float* g;
+  int64_t lsw, ldw;
+  int D;
+  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
+    for (int x = threadIdx.x; x < GT * GT; x += blockDim.x) {
+      const int r = x / GT, cc = x % GT, row = m0 + r, n = n0 + cc;
+      if (row >= M || n >= N) continue;
+      g[(row < D ? lsw + (int64_t)row * D : ldw + (int64_t)(row - D) * D) + n] = Ct[r * GPAD + cc];
+    }
+  }
+};
+// d(edge attr enc) -> Δt-encoding parameter grads: per 64-row tile, Σ_e darg Δt and Σ_e darg with
+// darg = -g sin(w Δt + b) (Δt = lu[src] - t_e), written to partial rows (summed in fixed order later)
+struct EpiTeEdge {
+  const int* e_j;
+  const float *e_t, *lu, *tw, *tb;
+  float* tgp;
+  int D, row0;
+  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
+    for (int cc = threadIdx.x; cc < GT; cc += blockDim.x) {
+      const int n = n0 + cc;
+      if (n >= N) continue;
+      float sw = 0.f, sb = 0.f;
+      for (int r = 0; r < GT && m0 + r < M; ++r) {
+        const int e = m0 + r;
+        const float dt = lu[e_j[e]] - e_t[e];
+        float sn, cs;
+        te_sincos(fmaf(tw[n], dt, tb[n]), sn, cs);
+        const float da = -Ct[r * GPAD + cc] * sn;
+        sw += da * dt;
+        sb += da;
+      }
+      tgp[(int64_t)(row0 + m0 / GT) * 2 * D + n] = sw;
+      tgp[(int64_t)(row0 + m0 / GT) * 2 * D + D + n] = sb;
+    }
+  }
+};
+// [W_query; W_key; W_value; W_skip] as the B operand of dz0 = dP W: element (n, k) = W_{k/HC}[k%HC][n]
+struct LoadProjWT {
+  const float *wq, *wk, *wv, *ws;
+  int HC, D;
+  static constexpr bool k_fast = false;
+  __device__ float operator()(int n, int k) const {
+    const int g = k / HC, r = k % HC;
+    const float* w = g == 0 ? wq : g == 1 ? wk : g == 2 ? wv : ws;
+    return w[(int64_t)r * D + n];
+  }
+};
+// GRUCell backward from dh' (memory is detached, so only the gate pre-activations get gradients):
+// dG[m][4j+g] = (d pre_r, d pre_z, d gi_n, d gh_n)
+struct EpiGruBwd {
+  const float *gates, *mem;
+  const int64_t* nid;
+  float* dG;
+  int D;
+  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
+    for (int x = threadIdx.x; x < GT * GT; x += blockDim.x) {
+      const int r = x / GT, cc = x % GT, m = m0 + r, j = n0 + cc;
+      if (m >= M || j >= N) continue;
+      const float dhp = Ct[r * GPAD + cc];
+      const float4 gt = *reinterpret_cast<const float4*>(gates + ((int64_t)m * D + j) * 4);
+      const float rr = gt.x, zz = gt.y, nn = gt.z, ghn = gt.w;
+      const float h = mem[nid[m] * D + j];
+      const float dn = dhp * (1.0f - zz), dz = dhp * (h - nn);
+      const float dpn = dn * (1.0f - nn * nn);
+      const float dr = dpn * ghn;
+      float4* o = reinterpret_cast<float4*>(dG + ((int64_t)m * D + j) * 4);
+      *o = make_float4(dr * rr * (1.0f - rr), dz * zz * (1.0f - zz), dpn, dpn * rr);
+    }
+  }
+};
+// [X | memory | 1] rows as the B operand of dW_gru = dGᵀ [X | H | 1]
+struct LoadGruAT1 {
+  const float* X;
+  const float* mem;
+  const int64_t* nid;
+  int Qm, D;
+  static constexpr bool k_fast = false;
+  __device__ float operator()(int n, int m) const {
+    if (n < Qm) return X[(int64_t)m * Qm + n];
+    if (n < Qm + D) return mem[nid[m] * D + (n - Qm)];
+    return 1.0f;
+  }
+};
+struct EpiGruWGrad {
+  float* g;
+  int64_t wih, whh, bih, bhh;
+  int Qm, D;
+  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
+    for (int x = threadIdx.x; x < GT * GT; x += blockDim.x) {
+      const int r = x / GT, cc = x % GT, row = m0 + r, n = n0 + cc;
+      if (row >= M || n >= N) continue;
+      const int j = row >> 2, gg = row & 3;
+      const float v = Ct[r * GPAD + cc];
+      if (n < Qm) {
+        if (gg < 3) g[wih + (int64_t)(gg * D + j) * Qm + n] = v;
+      } else if (n < Qm + D) {
+        if (gg != 2) g[whh + (int64_t)((gg == 3 ? 2 : gg) * D + j) * D + (n - Qm)] = v;
+      } else {
+        if (gg < 2) {
+          g[bih + gg * D + j] = v;
+          g[bhh + gg * D + j] = v;
+        } else if (gg == 2) {
+          g[bih + 2 * D + j] = v;
+        } else {
+          g[bhh + 2 * D + j] = v;
+        }
+      }
+    }
+  }
+};
+// encoding columns of W_ih as the B operand of dX_enc = dG W_cat[:, enc]: element (n, r = 4j+g)
+struct LoadGruWencT {
+  const float* wih;
+  int Qm, D, off;
+  static constexpr bool k_fast = false;
+  __device__ float operator()(int n, int r) const {
+    const int j = r >> 2, gg = r & 3;
+    return gg == 3 ? 0.f : wih[(int64_t)(gg * D + j) * Qm + off + n];
+  }
+};
+// message-encoding -> Δt-encoding parameter grads (Last: the winner's Δt; Mean: each stored
+// message's Δt with weight 1 / count), per 64-row tile partials
+struct EpiTeMsg {
+  Ctx c;
+  int row0;
+  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
+    const float* tw = c.params + c.L.te_w;
+    const float* tb = c.params + c.L.te_b;
+    const int D = c.D;
+    for (int cc = threadIdx.x; cc < GT; cc += blockDim.x) {
+      const int n = n0 + cc;
+      if (n >= N) continue;
+      float sw = 0.f, sb = 0.f;
+      for (int r = 0; r < GT && m0 + r < M; ++r) {
+        const int m = m0 + r;
+        if (c.xw[m] < 0) continue;
+        const float g = Ct[r * GPAD + cc];
+        if (c.aggr == 0) {
+          const float dt = c.trel[m];
+          float sn, cs;
+          te_sincos(fmaf(tw[n], dt, tb[n]), sn, cs);
+          const float da = -g * sn;
+          sw += da * dt;
+          sb += da;
+        } else {
+          const int64_t v = c.nid[m];
+          const int64_t so = c.st[4 * v], sc = c.st[4 * v + 1], dof = c.st[4 * v + 2], dc = c.st[4 * v + 3];
+          const float lun = (float)c.lu_buf[v];
+          const float gm = g / (float)(sc + dc);
+          for (int q = 0; q < sc + dc; ++q) {
+            const int64_t e = q < sc ? c.arena[so + q] : c.arena[dof + (q - sc)];
+            const float dt = c.ev_t[e] - lun;
+            float sn, cs;
+            te_sincos(fmaf(tw[n], dt, tb[n]), sn, cs);
+            const float da = -gm * sn;
+            sw += da * dt;
+            sb += da;
+          }
+        }
+      }
+      c.tgp[(int64_t)(row0 + m0 / GT) * 2 * D + n] = sw;
+      c.tgp[(int64_t)(row0 + m0 / GT) * 2 * D + D + n] = sb;
+    }
+  }
+};
+
+// Δt-encoding grads: fixed-order sum of the partial rows into grads (before any all-reduce)
+__global__ void tgn_te_reduce(Ctx c, int rows_edge, int rows_msg) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int D = c.D;
+  const int E = c.cnt[CNT_E], M = c.cnt[CNT_M];
+  const int re = min(rows_edge, (E + GT - 1) / GT), rm = min(rows_msg, (M + GT - 1) / GT);
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < 2 * D; x += gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int r = 0; r < re; ++r) s += c.tgp[(int64_t)r * 2 * D + x];
+    for (int r = 0; r < rm; ++r) s += c.tgp[(int64_t)(rows_edge + r) * 2 * D + x];
+    c.grads[(x < D ? c.L.te_w : c.L.te_b - D) + x] = s;
+  }
+}
+
+// ------------------------------------------------------------------ optimizer + state update
+__device__ __forceinline__ void adam1(float g, float& m, float& v, float& p, float b1, float b2, float eps, float step,
+                                      float bc2s) {
+  m = m + (1.0f - b1) * (g - m);
+  v = v * b2 + (1.0f - b2) * g * g;
+  const float den = sqrtf(v) / bc2s + eps;
+  p -= step * (m / den);
+}
+__global__ void __launch_bounds__(256) tgn_adam(Ctx c) {
+  __shared__ float sc[2];
+  const int64_t B = c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  if (threadIdx.x == 0) {
+    const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
+    sc[0] = (float)(c.lr / (1.0 - pow((double)c.b1, (double)t)));
+    sc[1] = (float)sqrt(1.0 - pow((double)c.b2, (double)t));
+    if (blockIdx.x == 0) *reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS) += (double)c.grads[c.L.total] * (double)B;
+  }
+  __syncthreads();
+  const float step = sc[0], bc2s = sc[1];
+  const int64_t n4 = c.L.total / 4;
+  float4* P4 = reinterpret_cast<float4*>(c.params);
+  float4* M4 = reinterpret_cast<float4*>(c.am);
+  float4* V4 = reinterpret_cast<float4*>(c.av);
+  const float4* G4 = reinterpret_cast<const float4*>(c.grads);
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n4; x += (int64_t)gridDim.x * blockDim.x) {
+    const float4 g = G4[x];
+    float4 m = M4[x], v = V4[x], p = P4[x];
+    adam1(g.x, m.x, v.x, p.x, c.b1, c.b2, c.eps, step, bc2s);
+    adam1(g.y, m.y, v.y, p.y, c.b1, c.b2, c.eps, step, bc2s);
+    adam1(g.z, m.z, v.z, p.z, c.b1, c.b2, c.eps, step, bc2s);
+    adam1(g.w, m.w, v.w, p.w, c.b1, c.b2, c.eps, step, bc2s);
+    M4[x] = m;
+    V4[x] = v;
+    P4[x] = p;
+  }
+}
+
+// update_state pieces (memory_module.py:126-150, :180-191) and the ring insert, by block range:
+// [0, nmem): memory / last_update of the update list from the GRU rows (wave per node; train rows
+// are the sampled nodes' rows via assoc, eval / flush rows are list positions);
+// [nmem, nmem + nst): message stores of the batch; the rest: ring merge, wave per node run.
+__global__ void __launch_bounds__(256) tgn_update(Ctx c, int nmem, int nst, int mem_mode, const int64_t* list,
+                                                  const int* list_cnt, int n_host, int64_t base) {
+  const int lane = threadIdx.x & 63;
+  if ((int)blockIdx.x < nmem) {
+    if (mem_mode == 0 && (c.ctl[TGNX_CTL_B] == 0 || c.ctl[TGNX_CTL_ERR] != 0)) return;
+    const int n = list_cnt ? *list_cnt : n_host;
+    for (int u = blockIdx.x * 4 + (threadIdx.x >> 6); u < n; u += nmem * 4) {
+      const int64_t v = list ? list[u] : base + u;
+      const int m = mem_mode == 0 ? c.upd_loc[u] : u;
+      for (int k = lane; k < c.D; k += 64) c.mem[v * c.D + k] = c.Z0[(int64_t)m * c.D + k];
+      if (lane == 0) c.lu_buf[v] = (int64_t)c.lu[m];
+    }
+    return;
+  }
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  if ((int)blockIdx.x < nmem + nst) {
+    const int bid = blockIdx.x - nmem;
+    const int n2 = 2 * B, U = c.cnt[CNT_SRUNS];
+    const int64_t ab = 2 * start;  // arena slot of this batch
+    for (int p = bid * blockDim.x + threadIdx.x; p < n2; p += nst * blockDim.x)
+      c.arena[ab + p] = start + (int64_t)(c.skeys[p] & 0xFFFFFFFFull);
+    for (int r = bid * blockDim.x + threadIdx.x; r < U; r += nst * blockDim.x) {
+      const int a = c.sruns[r], len = c.sruns[r + 1] - a;
+      const uint64_t k = c.skeys[a];
+      const int64_t v = (int64_t)(k >> 33);
+      const int dir = (int)((k >> 32) & 1u);
+      c.st[4 * v + 2 * dir] = ab + a;
+      c.st[4 * v + 2 * dir + 1] = len;
+    }
+    return;
+  }
+  const int r = (blockIdx.x - nmem - nst) * 4 + (threadIdx.x >> 6);
+  if (r < c.cnt[CNT_RUNS]) {
+    const int a = c.rruns[r];
+    ring_merge_run(c.nbr, c.eid, c.rt, c.K, c.ev_src + start, c.ev_dst + start, c.ev_t + start, B,
+                   c.ctl[TGNX_CTL_CUR_EID], c.assoc, c.rkeys, a, c.rruns[r + 1] - a, r, lane);
+  }
+}
+}  // namespace tgn
+}  // namespace tgnx
+
+// ================================================================== host side
+namespace tgnx {
+namespace tgn {
+
+__global__ void tgn_reset_kernel(float* mem, int64_t nm, int64_t* lu, int64_t* st, int64_t N) {
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < nm; x += (int64_t)gridDim.x * blockDim.x) mem[x] = 0.f;
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < N; x += (int64_t)gridDim.x * blockDim.x) {
+    lu[x] = 0;
+    st[4 * x] = st[4 * x + 1] = st[4 * x + 2] = st[4 * x + 3] = 0;
+  }
+}
+__global__ void tgn_clear_store(int64_t* st, int64_t N) {
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < N; x += (int64_t)gridDim.x * blockDim.x)
+    st[4 * x + 1] = st[4 * x + 3] = 0;
+}
+
+// eval scoring: workgroup per event, threads over its [pos, negatives] candidates:
+// s = sigmoid(lin_final(relu(Hs[src] + Hd[cand]))) (Hs / Hd = lin_src / lin_dst of the centres),
+// then the TGB rank rule: rank = 0.5 (#neg > pos + #neg >= pos) + 1.
+__global__ void __launch_bounds__(256) tgn_score(Ctx c) {
+  __shared__ float hs[TDMAX], wf[TDMAX];
+  __shared__ float spos;
+  __shared__ int cnt2[2];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int i = blockIdx.x;
+  if (B == 0 || i >= B || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int D = c.D, Kn = c.Kn, tid = threadIdx.x;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int cs = c.crank[c.assoc[c.ev_src[start + i]]];
+  for (int k = tid; k < D; k += blockDim.x) {
+    hs[k] = c.Hs[(int64_t)cs * D + k];
+    wf[k] = c.params[c.L.lfw + k];
+  }
+  if (tid == 0) cnt2[0] = cnt2[1] = 0;
+  __syncthreads();
+  const float bf = c.params[c.L.lfb];
+  auto score = [&](int64_t node) {
+    const float* hd = c.Hd + (int64_t)c.crank[c.assoc[node]] * D;
+    float a = 0.f;
+    for (int k = 0; k < D; ++k) a += wf[k] * fmaxf(hs[k] + hd[k], 0.f);
+    return sigm(a + bf);
+  };
+  if (tid == 0) {
+    spos = score(c.ev_dst[start + i]);
+    c.out_pos[i] = spos;
+  }
+  __syncthreads();
+  const float sp = spos;
+  int opt = 0, pes = 0;
+  for (int q = tid; q < Kn; q += blockDim.x) {
+    const float s = score(c.neg[(start + i) * Kn + q]);
+    c.out_neg[(int64_t)i * Kn + q] = s;
+    opt += s > sp;
+    pes += s >= sp;
+  }
+  atomicAdd(&cnt2[0], opt);
+  atomicAdd(&cnt2[1], pes);
+  __syncthreads();
+  if (tid == 0) c.mrr[i] = 1.0 / (0.5 * ((double)cnt2[0] + (double)cnt2[1]) + 1.0);
+}
+
+static size_t carve(size_t& off, size_t bytes) {
+  size_t o = off;
+  off += (bytes + 255) & ~size_t(255);
+  return o;
+}
+struct Caps {
+  int B, Kn, Qtr, Qcap, Rtr, Rcap, Mtr, Mcap, Etr, Ecap, Ucap, Qm, D, d, HC;
+  int64_t N;
+};
+static Caps make_caps(const tgnx_tgn_config* cfg) {
+  Caps k;
+  k.N = cfg->num_nodes;
+  k.B = cfg->max_batch;
+  k.Kn = cfg->max_neg < 1 ? 1 : cfg->max_neg;
+  k.D = cfg->mem_dim;
+  k.d = cfg->msg_dim;
+  k.HC = k.D;
+  k.Qm = 3 * k.D + k.d;
+  const int K = cfg->ring;
+  auto cap = [&](int64_t x) { return (int)(x < k.N ? x : k.N); };
+  k.Qtr = 3 * k.B;
+  k.Qcap = k.B * (2 + k.Kn);
+  if (k.Qcap < k.Qtr) k.Qcap = k.Qtr;
+  k.Rtr = cap(k.Qtr);
+  k.Rcap = cap(k.Qcap);
+  k.Mtr = cap((int64_t)k.Rtr * (K + 1));
+  k.Mcap = cap((int64_t)k.Rcap * (K + 1));
+  k.Etr = k.Rtr * K;
+  k.Ecap = k.Rcap * K;
+  k.Ucap = cap(2 * (int64_t)k.B);
+  return k;
+}
+// the GEMMs of a step (capacities), for partial-buffer sizing
+static void gemm_caps(const Caps& k, GemmShape* g, int& n) {
+  n = 0;
+  g[n++] = gemm_shape(k.Mcap, 4 * k.D, k.Qm + k.D, GKC);           // G1
+  g[n++] = gemm_shape(k.Ecap, k.HC, k.D + k.d, GKC);                // G3
+  g[n++] = gemm_shape(k.Mcap, 4 * k.HC, k.D, GKC);                  // G2
+  g[n++] = gemm_shape(k.HC, k.D + k.d, k.Etr, GKC);                 // G5
+  g[n++] = gemm_shape(4 * k.HC, k.D + 1, k.Mtr, GKC);               // G6
+  g[n++] = gemm_shape(2 * k.D, k.D, 3 * k.B, GKC);                  // link predictor
+  g[n++] = gemm_shape(k.Etr, k.D, k.HC, GKC);                       // G5b
+  g[n++] = gemm_shape(k.Mtr, k.D, 4 * k.HC, GKC);                   // G7
+  g[n++] = gemm_shape(4 * k.D, k.Qm + k.D + 1, k.Mtr, GKC);         // G8
+  g[n++] = gemm_shape(k.Mtr, k.D, 4 * k.D, GKC);                    // G9
+  g[n++] = gemm_shape(k.Rcap, k.D, k.D, GKC);                       // Hs / Hd
+}
+struct WsLay {
+  size_t cb, nb, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
+      Ep, alpha, Zc, evs, Hs, Hd, dZc, dP, dE, dG, tgp, gpart, tick, rkeys, rruns, skeys, sruns, total;
+  size_t gpart_floats;
+  int ntick, tgp_rows;
+};
+static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
+  WsLay W;
+  size_t off = 0;
+  const int64_t words = (k.N + 31) / 32 + 1;
+  const int D = k.D, HC = k.HC;
+  W.cb = carve(off, words * 4);
+  W.nb = carve(off, words * 4);
+  W.cnt = carve(off, CNT_WORDS * 4);
+  W.cent = carve(off, (size_t)k.Rcap * 8);
+  W.cent_loc = carve(off, (size_t)k.Rcap * 4);
+  W.ceoff = carve(off, (size_t)(k.Rcap + 1) * 4);
+  W.crank = carve(off, (size_t)k.Mcap * 4);
+  W.upd_loc = carve(off, (size_t)k.Ucap * 4);
+  W.nid = carve(off, (size_t)k.Mcap * 8);
+  W.upd = carve(off, (size_t)k.Ucap * 8);
+  W.e_j = carve(off, (size_t)k.Ecap * 4);
+  W.e_c = carve(off, (size_t)k.Ecap * 4);
+  W.e_id = carve(off, (size_t)k.Ecap * 8);
+  W.e_t = carve(off, (size_t)k.Ecap * 4);
+  W.X = carve(off, (size_t)k.Mcap * k.Qm * 4);
+  W.trel = carve(off, (size_t)k.Mcap * 4);
+  W.lu = carve(off, (size_t)k.Mcap * 4);
+  W.xw = carve(off, (size_t)k.Mcap * 8);
+  W.gates = carve(off, (size_t)k.Mcap * 4 * D * 4);
+  W.Z0 = carve(off, (size_t)k.Mcap * D * 4);
+  W.P = carve(off, (size_t)k.Mcap * 4 * HC * 4);
+  W.Ep = carve(off, (size_t)k.Ecap * HC * 4);
+  W.alpha = carve(off, (size_t)k.Etr * TH * 4);
+  W.Zc = carve(off, (size_t)k.Rcap * HC * 4);
+  W.evs = carve(off, (size_t)k.B * evs_stride(D) * 4);
+  W.Hs = carve(off, (size_t)k.Rcap * D * 4);
+  W.Hd = carve(off, (size_t)k.Rcap * D * 4);
+  W.dZc = carve(off, (size_t)k.Rtr * HC * 4);
+  W.dP = carve(off, (size_t)k.Mtr * 4 * HC * 4);
+  W.dE = carve(off, (size_t)k.Etr * HC * 4);
+  W.dG = carve(off, (size_t)k.Mtr * 4 * D * 4);
+  W.tgp_rows = (k.Etr + GT - 1) / GT + (k.Mtr + GT - 1) / GT;
+  W.tgp = carve(off, (size_t)W.tgp_rows * 2 * D * 4);
+  GemmShape g[16];
+  int n;
+  gemm_caps(k, g, n);
+  size_t pf = 0;
+  int nt = 1;
+  for (int i = 0; i < n; ++i) {
+    pf = std::max(pf, gemm_partial_floats(g[i]));
+    nt = std::max(nt, g[i].tiles_m * g[i].tiles_n);
+  }
+  W.gpart_floats = pf;
+  W.ntick = nt;
+  W.gpart = carve(off, 2 * pf * 4 + 64);
+  W.tick = carve(off, (size_t)2 * nt * 4);
+  const int n2 = 2 * k.B;
+  W.rkeys = carve(off, (size_t)n2 * 8);
+  W.rruns = carve(off, (size_t)(n2 + 2) * 4);
+  W.skeys = carve(off, (size_t)n2 * 8);
+  W.sruns = carve(off, (size_t)(n2 + 2) * 4);
+  W.total = off;
+  return W;
+}
+
+static int check_cfg(const tgnx_tgn_config* cfg) {
+  TGNX_CHECK_ARG(cfg, "tgn: null config");
+  TGNX_CHECK_ARG(cfg->heads == TH, "tgn: heads must be %d (emb_module.py:66), got %d", TH, cfg->heads);
+  TGNX_CHECK_ARG(cfg->mem_dim > 0 && cfg->mem_dim <= TDMAX && cfg->mem_dim % TH == 0,
+                 "tgn: mem_dim must be even and <= %d", TDMAX);
+  TGNX_CHECK_ARG(cfg->msg_dim >= 0 && cfg->msg_dim <= 4096, "tgn: bad msg_dim");
+  TGNX_CHECK_ARG(cfg->ring > 0 && cfg->ring <= KMAX, "tgn: ring size must be in [1, %d]", KMAX);
+  TGNX_CHECK_ARG(cfg->max_batch > 0 && cfg->max_batch <= 2048, "tgn: max_batch must be in [1, 2048]");
+  TGNX_CHECK_ARG(cfg->num_nodes > 0 && cfg->num_nodes < (1ll << 31), "tgn: bad num_nodes");
+  TGNX_CHECK_ARG(cfg->num_events > 0, "tgn: bad num_events");
+  TGNX_CHECK_ARG(cfg->aggr == 0 || cfg->aggr == 1, "tgn: aggr must be 0 (last) or 1 (mean)");
+  TGNX_CHECK_ARG(cfg->dropout >= 0.f && cfg->dropout < 1.f, "tgn: bad dropout");
+  return TGNX_OK;
+}
+
+static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int Kn, Ctx& c, Caps& k, WsLay& W) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(b && b->ctl && b->ws && b->params && b->memory && b->last_update && b->store && b->node_gen &&
+                     b->nbr && b->eid && b->rt && b->assoc && b->ev_src && b->ev_dst && b->ev_t && b->ev_msg,
+                 "tgn: null buffer");
+  k = make_caps(cfg);
+  W = make_ws(cfg, k);
+  memset(&c, 0, sizeof(c));
+  c.N = cfg->num_nodes;
+  c.nev = cfg->num_events;
+  c.words = (c.N + 31) / 32 + 1;
+  c.K = cfg->ring;
+  c.D = cfg->mem_dim;
+  c.d = cfg->msg_dim;
+  c.Qm = k.Qm;
+  c.HC = k.HC;
+  c.C = k.HC / TH;
+  c.aggr = cfg->aggr;
+  c.Kn = Kn;
+  c.p = cfg->dropout;
+  c.inv_keep = 1.0f / (1.0f - cfg->dropout);
+  c.lr = cfg->lr;
+  c.b1 = cfg->beta1;
+  c.b2 = cfg->beta2;
+  c.eps = cfg->eps;
+  c.ev_src = b->ev_src;
+  c.ev_dst = b->ev_dst;
+  c.ev_t = b->ev_t;
+  c.ev_msg = b->ev_msg;
+  c.neg = b->neg;
+  c.dst_nodes = b->dst_nodes;
+  c.n_dst = b->n_dst;
+  c.nbr = b->nbr;
+  c.eid = b->eid;
+  c.rt = b->rt;
+  c.assoc = b->assoc;
+  c.mem = b->memory;
+  c.lu_buf = b->last_update;
+  c.st = b->store;
+  c.arena = b->store + 4 * c.N;
+  c.node_gen = b->node_gen;
+  c.params = b->params;
+  c.grads = b->grads;
+  c.am = b->adam_m;
+  c.av = b->adam_v;
+  c.ctl = b->ctl;
+  c.out_pos = b->out_pos;
+  c.out_neg = b->out_neg;
+  c.mrr = b->mrr;
+  char* ws = reinterpret_cast<char*>(b->ws);
+  c.cb = reinterpret_cast<uint32_t*>(ws + W.cb);
+  c.nb = reinterpret_cast<uint32_t*>(ws + W.nb);
+  c.cnt = reinterpret_cast<int*>(ws + W.cnt);
+  c.cent = reinterpret_cast<int64_t*>(ws + W.cent);
+  c.cent_loc = reinterpret_cast<int*>(ws + W.cent_loc);
+  c.ceoff = reinterpret_cast<int*>(ws + W.ceoff);
+  c.crank = reinterpret_cast<int*>(ws + W.crank);
+  c.upd_loc = reinterpret_cast<int*>(ws + W.upd_loc);
+  c.nid = reinterpret_cast<int64_t*>(ws + W.nid);
+  c.upd = reinterpret_cast<int64_t*>(ws + W.upd);
+  c.e_j = reinterpret_cast<int*>(ws + W.e_j);
+  c.e_c = reinterpret_cast<int*>(ws + W.e_c);
+  c.e_id = reinterpret_cast<int64_t*>(ws + W.e_id);
+  c.e_t = reinterpret_cast<float*>(ws + W.e_t);
+  c.X = reinterpret_cast<float*>(ws + W.X);
+  c.trel = reinterpret_cast<float*>(ws + W.trel);
+  c.lu = reinterpret_cast<float*>(ws + W.lu);
+  c.xw = reinterpret_cast<int64_t*>(ws + W.xw);
+  c.gates = reinterpret_cast<float*>(ws + W.gates);
+  c.Z0 = reinterpret_cast<float*>(ws + W.Z0);
+  c.P = reinterpret_cast<float*>(ws + W.P);
+  c.Ep = reinterpret_cast<float*>(ws + W.Ep);
+  c.alpha = reinterpret_cast<float*>(ws + W.alpha);
+  c.Zc = reinterpret_cast<float*>(ws + W.Zc);
+  c.evs = reinterpret_cast<float*>(ws + W.evs);
+  c.Hs = reinterpret_cast<float*>(ws + W.Hs);
+  c.Hd = reinterpret_cast<float*>(ws + W.Hd);
+  c.dZc = reinterpret_cast<float*>(ws + W.dZc);
+  c.dP = reinterpret_cast<float*>(ws + W.dP);
+  c.dE = reinterpret_cast<float*>(ws + W.dE);
+  c.dG = reinterpret_cast<float*>(ws + W.dG);
+  c.tgp = reinterpret_cast<float*>(ws + W.tgp);
+  c.gpart = reinterpret_cast<float*>(ws + W.gpart);
+  c.tick = reinterpret_cast<int*>(ws + W.tick);
+  c.rkeys = reinterpret_cast<uint64_t*>(ws + W.rkeys);
+  c.rruns = reinterpret_cast<int*>(ws + W.rruns);
+  c.skeys = reinterpret_cast<uint64_t*>(ws + W.skeys);
+  c.sruns = reinterpret_cast<int*>(ws + W.sruns);
+  c.Bmax = k.B;
+  c.Qcap = k.Qcap;
+  c.Rcap = k.Rcap;
+  c.Mcap = k.Mcap;
+  c.Ecap = k.Ecap;
+  c.Ucap = k.Ucap;
+  c.tgp_rows = W.tgp_rows;
+  c.gpart_floats = W.gpart_floats;
+  c.L = make_lay(c.D, c.d);
+  return TGNX_OK;
+}
+
+static inline int gridn(int64_t n, int per, int cap = 4096) {
+  int64_t g = (n + per - 1) / per;
+  if (g < 1) g = 1;
+  return (int)(g < cap ? g : cap);
+}
+
+// the GRU of a node list (eval update / flush): messages -> GRUCell (X, Z0 rows 0..n)
+static void gru_list(const Ctx& c, const Caps& k, const int64_t* list, const int* list_cnt, int n_host, int64_t base,
+                     int mcap, hipStream_t s) {
+  const float* P = c.params;
+  tgn_agg_emit<<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
+  const GemmShape g1 = gemm_shape(mcap, 4 * c.D, c.Qm + c.D, GKC, list_cnt);
+  gemm_launch(g1, LoadGruA{c.X, c.mem, list, base, c.Qm, c.D}, LoadGruW{P + c.L.w_ih, P + c.L.w_hh, c.Qm, c.D},
+              EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, list, base, c.D, c.Z0, c.gates}, c.gpart, c.tick, s);
+}
+
+}  // namespace tgn
+}  // namespace tgnx
+
+using namespace tgnx;
+using namespace tgnx::tgn;
+
+extern "C" {
+
+int tgnx_tgn_param_layout(const tgnx_tgn_config* cfg, int64_t* off) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(off, "tgnx_tgn_param_layout: null output");
+  const Lay L = make_lay(cfg->mem_dim, cfg->msg_dim);
+  const int64_t v[TGNX_TGN_NPARAM + 1] = {L.te_w, L.te_b, L.w_ih, L.w_hh, L.b_ih, L.b_hh, L.wk, L.bk,
+                                          L.wq,   L.bq,   L.wv,   L.bv,   L.we,   L.wsk,  L.bsk, L.lsw,
+                                          L.lsb,  L.ldw,  L.ldb,  L.lfw,  L.lfb,  L.total};
+  for (int i = 0; i <= TGNX_TGN_NPARAM; ++i) off[i] = v[i];
+  return TGNX_OK;
+}
+
+size_t tgnx_tgn_ws_bytes(const tgnx_tgn_config* cfg) {
+  if (check_cfg(cfg)) return 0;
+  return make_ws(cfg, make_caps(cfg)).total;
+}
+
+size_t tgnx_tgn_store_words(const tgnx_tgn_config* cfg) {
+  if (check_cfg(cfg)) return 0;
+  return (size_t)(4 * cfg->num_nodes + 2 * cfg->num_events);
+}
+
+int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(buf && buf->memory && buf->last_update && buf->store, "tgnx_tgn_reset_state: null buffer");
+  const int64_t N = cfg->num_nodes;
+  tgn_reset_kernel<<<gridn(N * cfg->mem_dim, 256), 256, 0, as_stream(stream)>>>(buf->memory, N * cfg->mem_dim,
+                                                                                 buf->last_update, buf->store, N);
+  TGNX_LAUNCH_CHECK("tgn_reset");
+  return TGNX_OK;
+}
+
+int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
+                           void* stream) {
+  Ctx c;
+  Caps k;
+  WsLay W;
+  int rc = make_ctx(cfg, buf, 1, c, k, W);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(buf->neg && buf->grads && buf->out_pos && buf->out_neg, "tgnx_tgn_train_fwd_bwd: null buffer");
+  TGNX_CHECK_ARG(!gen_neg || (buf->dst_nodes && buf->n_dst > 0), "tgnx_tgn_train_fwd_bwd: no destination set");
+  c.gen_neg = gen_neg ? 1 : 0;
+  c.drop = dropout && cfg->dropout > 0.f;
+  hipStream_t s = as_stream(stream);
+  const float* P = c.params;
+  float* G = c.grads;
+  float *p0 = c.gpart, *p1 = c.gpart + c.gpart_floats;
+  int *t0 = c.tick, *t1 = c.tick + W.ntick;
+  const int D = c.D, HC = c.HC, Qm = c.Qm, d = c.d;
+  tgn_mark<true><<<gridn(3 * k.B, 256), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgn_mark");
+  tgn_scan<true><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
+  TGNX_LAUNCH_CHECK("tgn_scan");
+  const int nemit = gridn(k.Rtr, 256);
+  tgn_agg_emit<<<nemit + gridn(k.Mtr, 4, 2048), 256, 0, s>>>(c, 0, nemit, nullptr, nullptr, 0, 0);
+  TGNX_LAUNCH_CHECK("tgn_agg_emit");
+  // GRU over every sampled node ‖ lin_edge over every sampled edge
+  const LoadEdgeAttr ea{c.e_j, c.e_id, c.e_t, c.lu, c.ev_msg, P + c.L.te_w, P + c.L.te_b, D, d};
+  gemm2_launch(gemm_shape(k.Mtr, 4 * D, Qm + D, GKC, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D},
+               LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
+               EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, p0, t0,
+               gemm_shape(k.Etr, HC, D + d, GKC, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
+               EpiStore{c.Ep, nullptr, HC, 0}, p1, t1, s);
+  TGNX_LAUNCH_CHECK("tgn_gru_edge");
+  gemm_launch(gemm_shape(k.Mtr, 4 * HC, D, GKC, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
+              LoadProjW{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
+              EpiProj{P + c.L.bq, P + c.L.bk, P + c.L.bv, P + c.L.bsk, c.P, HC}, p0, t0, s);
+  TGNX_LAUNCH_CHECK("tgn_proj");
+  tgn_attn_fwd<true><<<gridn(k.Rtr, 4), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgn_attn_fwd");
+  tgn_pred_train<<<k.B, 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgn_pred_train");
+  const int ncb = gridn(k.Rtr, 4);
+  tgn_attn_bwd<<<ncb + gridn(3 * D + 2, 4), 256, 0, s>>>(c, ncb);
+  TGNX_LAUNCH_CHECK("tgn_attn_bwd");
+  gemm2_launch(gemm_shape(HC, D + d, k.Etr, GKC, nullptr, nullptr, c.cnt + CNT_E), LoadKRow{c.dE, HC, k.Etr, HC},
+               LoadEdgeAttrT{ea}, EpiStore{G + c.L.we, nullptr, D + d, 0}, p0, t0,
+               gemm_shape(4 * HC, D + 1, k.Mtr, GKC, nullptr, nullptr, c.cnt + CNT_M), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC},
+               LoadZ1T{c.Z0, D},
+               EpiProjGrad{G, c.L.wq, c.L.bq, c.L.wk, c.L.bk, c.L.wv, c.L.bv, c.L.wsk, c.L.bsk, HC, D}, p1, t1, s);
+  TGNX_LAUNCH_CHECK("tgn_wgrad1");
+  const int rows_edge = (k.Etr + GT - 1) / GT, rows_msg = (k.Mtr + GT - 1) / GT;
+  gemm2_launch(gemm_shape(2 * D, D, 3 * k.B, GKC, nullptr, nullptr, c.cnt + CNT_LIST),
+               LoadLpA{c.evs, c.ctl, D, evs_stride(D)}, LoadLpB{c.evs, c.ctl, D, evs_stride(D)},
+               EpiLpGrad{G, c.L.lsw, c.L.ldw, D}, p0, t0, gemm_shape(k.Etr, D, HC, GKC, c.cnt + CNT_E),
+               LoadRowK{c.dE, k.Etr, HC, HC}, LoadKRow{P + c.L.we, D, HC, D + d},
+               EpiTeEdge{c.e_j, c.e_t, c.lu, P + c.L.te_w, P + c.L.te_b, c.tgp, D, 0}, p1, t1, s);
+  TGNX_LAUNCH_CHECK("tgn_wgrad2");
+  gemm_launch(gemm_shape(k.Mtr, D, 4 * HC, GKC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
+              LoadProjWT{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
+              EpiGruBwd{c.gates, c.mem, c.nid, c.dG, D}, p0, t0, s);
+  TGNX_LAUNCH_CHECK("tgn_dz0");
+  gemm2_launch(gemm_shape(4 * D, Qm + D + 1, k.Mtr, GKC, nullptr, nullptr, c.cnt + CNT_M),
+               LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D},
+               EpiGruWGrad{G, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, Qm, D}, p0, t0,
+               gemm_shape(k.Mtr, D, 4 * D, GKC, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
+               LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c, rows_edge}, p1, t1, s);
+  TGNX_LAUNCH_CHECK("tgn_wgrad3");
+  tgn_te_reduce<<<1, 256, 0, s>>>(c, rows_edge, rows_msg);
+  TGNX_LAUNCH_CHECK("tgn_te_reduce");
+  // update_state (train order: memory of src ∪ dst from this step's GRU rows, then the stores), insert
+  const int nmem = gridn(k.Ucap, 4, 1024), nst = gridn(2 * k.B, 256), nring = gridn(2 * k.B, 4);
+  tgn_update<<<nmem + nst + nring, 256, 0, s>>>(c, nmem, nst, 0, c.upd, c.cnt + CNT_U, 0, 0);
+  TGNX_LAUNCH_CHECK("tgn_update");
+  return TGNX_OK;
+}
+
+int tgnx_tgn_train_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream) {
+  Ctx c;
+  Caps k;
+  WsLay W;
+  int rc = make_ctx(cfg, buf, 1, c, k, W);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(buf->grads && buf->adam_m && buf->adam_v, "tgnx_tgn_train_update: null optimizer buffer");
+  tgn_adam<<<gridn(c.L.total / 4, 256), 256, 0, as_stream(stream)>>>(c);
+  TGNX_LAUNCH_CHECK("tgn_adam");
+  return TGNX_OK;
+}
+
+int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t Kn, void* stream) {
+  Ctx c;
+  Caps k;
+  WsLay W;
+  TGNX_CHECK_ARG(cfg && Kn >= 1 && Kn <= (cfg->max_neg < 1 ? 1 : cfg->max_neg), "tgnx_tgn_eval_step: Kn out of range");
+  int rc = make_ctx(cfg, buf, Kn, c, k, W);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(buf->neg && buf->out_pos && buf->out_neg && buf->mrr, "tgnx_tgn_eval_step: null buffer");
+  hipStream_t s = as_stream(stream);
+  const float* P = c.params;
+  float *p0 = c.gpart, *p1 = c.gpart + c.gpart_floats;
+  int *t0 = c.tick, *t1 = c.tick + W.ntick;
+  const int D = c.D, HC = c.HC, d = c.d;
+  const int Rq = (int)std::min<int64_t>(c.N, (int64_t)k.B * (2 + Kn));
+  const int Mq = (int)std::min<int64_t>(c.N, (int64_t)Rq * (c.K + 1));
+  const int Eq = Rq * c.K;
+  tgn_mark<false><<<gridn((int64_t)k.B * (2 + Kn), 256), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgn_mark");
+  tgn_scan<false><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
+  TGNX_LAUNCH_CHECK("tgn_scan");
+  const int nemit = gridn(Rq, 256);
+  tgn_agg_emit<<<nemit + gridn(Mq, 256), 256, 0, s>>>(c, 1, nemit, nullptr, nullptr, 0, 0);
+  TGNX_LAUNCH_CHECK("tgn_emit");
+  const LoadEdgeAttr ea{c.e_j, c.e_id, c.e_t, c.lu, c.ev_msg, P + c.L.te_w, P + c.L.te_b, D, d};
+  gemm2_launch(gemm_shape(Eq, HC, D + d, GKC, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
+               EpiStore{c.Ep, nullptr, HC, 0}, p0, t0, gemm_shape(Mq, 4 * HC, D, GKC, c.cnt + CNT_M),
+               LoadZ{c.Z0, c.mem, c.nid, D, 1}, LoadProjW{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
+               EpiProj{P + c.L.bq, P + c.L.bk, P + c.L.bv, P + c.L.bsk, c.P, HC}, p1, t1, s);
+  TGNX_LAUNCH_CHECK("tgn_edge_proj");
+  tgn_attn_fwd<false><<<gridn(Rq, 4, 1 << 20), 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgn_attn_fwd");
+  gemm2_launch(gemm_shape(Rq, D, D, GKC, c.cnt + CNT_R), LoadRowK{c.Zc, Rq, D, D}, LoadRowK{P + c.L.lsw, D, D, D},
+               EpiStore{c.Hs, P + c.L.lsb, D, 0}, p0, t0, gemm_shape(Rq, D, D, GKC, c.cnt + CNT_R),
+               LoadRowK{c.Zc, Rq, D, D}, LoadRowK{P + c.L.ldw, D, D, D}, EpiStore{c.Hd, P + c.L.ldb, D, 0}, p1, t1, s);
+  TGNX_LAUNCH_CHECK("tgn_lin_src_dst");
+  tgn_score<<<k.B, 256, 0, s>>>(c);
+  TGNX_LAUNCH_CHECK("tgn_score");
+  // update_state in eval order: stores first, then the GRU of src ∪ dst; ring insert
+  const int nst = gridn(2 * k.B, 256), nring = gridn(2 * k.B, 4);
+  tgn_update<<<nst + nring, 256, 0, s>>>(c, 0, nst, 1, nullptr, nullptr, 0, 0);
+  TGNX_LAUNCH_CHECK("tgn_store_insert");
+  gru_list(c, k, c.upd, c.cnt + CNT_U, 0, 0, k.Ucap, s);
+  TGNX_LAUNCH_CHECK("tgn_gru_update");
+  tgn_update<<<gridn(k.Ucap, 4, 1024), 256, 0, s>>>(c, gridn(k.Ucap, 4, 1024), 0, 1, c.upd, c.cnt + CNT_U, 0, 0);
+  TGNX_LAUNCH_CHECK("tgn_memory_write");
+  return TGNX_OK;
+}
+
+int tgnx_tgn_flush(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream) {
+  Ctx c;
+  Caps k;
+  WsLay W;
+  int rc = make_ctx(cfg, buf, 1, c, k, W);
+  if (rc) return rc;
+  hipStream_t s = as_stream(stream);
+  const int chunk = k.Mcap;
+  for (int64_t base = 0; base < c.N; base += chunk) {
+    const int n = (int)std::min<int64_t>(chunk, c.N - base);
+    gru_list(c, k, nullptr, nullptr, n, base, n, s);
+    TGNX_LAUNCH_CHECK("tgn_flush_gru");
+    tgn_update<<<gridn(n, 4, 1024), 256, 0, s>>>(c, gridn(n, 4, 1024), 0, 1, nullptr, nullptr, n, base);
+    TGNX_LAUNCH_CHECK("tgn_flush_write");
+  }
+  tgn_clear_store<<<gridn(c.N, 256), 256, 0, s>>>(c.st, c.N);
+  TGNX_LAUNCH_CHECK("tgn_clear_store");
+  return TGNX_OK;
+}
+
+}  // extern "C"

@@ -33,6 +33,14 @@ SIGNATURES = {
     "tgnx_tgnn_param_layout": (ctypes.c_int, [P, P]),
     "tgnx_tgnn_ws_bytes": (c_sz, [P]),
     "tgnx_tgnn_ws_misc_offset": (c_sz, [P]),
+    "tgnx_tgn_param_layout": (ctypes.c_int, [P, P]),
+    "tgnx_tgn_ws_bytes": (c_sz, [P]),
+    "tgnx_tgn_store_words": (c_sz, [P]),
+    "tgnx_tgn_reset_state": (ctypes.c_int, [P, P, c_vp]),
+    "tgnx_tgn_train_fwd_bwd": (ctypes.c_int, [P, P, c_i32, c_i32, c_vp]),
+    "tgnx_tgn_train_update": (ctypes.c_int, [P, P, c_vp]),
+    "tgnx_tgn_eval_step": (ctypes.c_int, [P, P, c_i32, c_vp]),
+    "tgnx_tgn_flush": (ctypes.c_int, [P, P, c_vp]),
     "tgnx_gemm_f32_ws_bytes": (c_sz, [c_i64, c_i64, c_i64]),
     "tgnx_gemm_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, P, c_i64, c_i32, P, c_i64, c_i32, P, c_i64, P, c_i32, P, c_sz,
                                      c_vp]),

@@ -1,0 +1,305 @@
+"""The TGN memory path (SURVEY §8 a14–a16) behind the reference's PyG surface.
+
+`getModel` / `getOptimizer` mirror pyg_model_utils.py:10-43: the returned dict has 'memory' (TGNMemory:
+time_enc + GRUCell, memory / last_update buffers, message stores), 'gnn' (GraphAttentionEmbedding:
+TransformerConv, sharing memory.time_enc) and 'link_pred' (LinkPredictor); state_dict keys are the
+reference's (`memory.gru.weight_ih`, `gnn.conv.lin_key.weight`, `link_pred.lin_final.bias`, ...).  Every
+trainable tensor is a view into one flat fp32 device buffer (`tgnx_tgn_param_layout`); the step runs in
+libtgnx (TgnEngine below), there is no torch-op path.
+
+Initialisation as the reference's modules: TimeEncoder = Linear(1, D) (torch default), GRUCell
+U(-1/sqrt(D), 1/sqrt(D)), PyG Linear (kaiming_uniform a=sqrt(5) -> U(-1/sqrt(in), 1/sqrt(in)), bias the
+same bound), LinkPredictor torch Linear defaults; memory / last_update zero (memory_module.py:106-110).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+P = ctypes.c_void_p
+
+PARAM_ORDER = [  # flat-buffer order = tgnx_tgn_param_layout
+    "memory.time_enc.lin.weight", "memory.time_enc.lin.bias",
+    "memory.gru.weight_ih", "memory.gru.weight_hh", "memory.gru.bias_ih", "memory.gru.bias_hh",
+    "gnn.conv.lin_key.weight", "gnn.conv.lin_key.bias", "gnn.conv.lin_query.weight", "gnn.conv.lin_query.bias",
+    "gnn.conv.lin_value.weight", "gnn.conv.lin_value.bias", "gnn.conv.lin_edge.weight",
+    "gnn.conv.lin_skip.weight", "gnn.conv.lin_skip.bias",
+    "link_pred.lin_src.weight", "link_pred.lin_src.bias", "link_pred.lin_dst.weight", "link_pred.lin_dst.bias",
+    "link_pred.lin_final.weight", "link_pred.lin_final.bias",
+]
+
+
+class TgnConfig(ctypes.Structure):
+    _fields_ = [("num_nodes", ctypes.c_int64), ("num_events", ctypes.c_int64), ("ring", ctypes.c_int32),
+                ("mem_dim", ctypes.c_int32), ("msg_dim", ctypes.c_int32), ("heads", ctypes.c_int32),
+                ("max_batch", ctypes.c_int32), ("max_neg", ctypes.c_int32), ("aggr", ctypes.c_int32),
+                ("dropout", ctypes.c_float), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
+                ("beta2", ctypes.c_float), ("eps", ctypes.c_float)]
+
+
+class TgnBuffers(ctypes.Structure):
+    _fields_ = [("ev_src", P), ("ev_dst", P), ("ev_t", P), ("ev_msg", P), ("neg", P), ("dst_nodes", P),
+                ("n_dst", ctypes.c_int64), ("nbr", P), ("eid", P), ("rt", P), ("assoc", P), ("memory", P),
+                ("last_update", P), ("store", P), ("node_gen", P), ("params", P), ("grads", P), ("adam_m", P),
+                ("adam_v", P), ("ctl", P), ("out_pos", P), ("out_neg", P), ("mrr", P), ("ws", P)]
+
+
+def param_shapes(D: int, d: int) -> dict:
+    Q = 3 * D + d
+    s = {"memory.time_enc.lin.weight": (D, 1), "memory.time_enc.lin.bias": (D,),
+         "memory.gru.weight_ih": (3 * D, Q), "memory.gru.weight_hh": (3 * D, D),
+         "memory.gru.bias_ih": (3 * D,), "memory.gru.bias_hh": (3 * D,),
+         "gnn.conv.lin_edge.weight": (D, D + d),
+         "link_pred.lin_src.weight": (D, D), "link_pred.lin_src.bias": (D,),
+         "link_pred.lin_dst.weight": (D, D), "link_pred.lin_dst.bias": (D,),
+         "link_pred.lin_final.weight": (1, D), "link_pred.lin_final.bias": (1,)}
+    for k in ("key", "query", "value", "skip"):
+        s[f"gnn.conv.lin_{k}.weight"] = (D, D)
+        s[f"gnn.conv.lin_{k}.bias"] = (D,)
+    return s
+
+
+def reference_init(D: int, d: int, generator=None) -> dict:
+    g = generator
+
+    def unif(shape, bound):
+        return (torch.rand(shape, generator=g) * 2 - 1) * bound
+
+    out = {}
+    for name, shape in param_shapes(D, d).items():
+        if name.startswith("memory.time_enc"):
+            bound = 1.0                                   # Linear(1, D): fan_in = 1
+        elif name.startswith("memory.gru"):
+            bound = 1.0 / math.sqrt(D)                    # GRUCell.reset_parameters
+        elif name == "gnn.conv.lin_edge.weight":
+            bound = 1.0 / math.sqrt(D + d)
+        else:
+            bound = 1.0 / math.sqrt(D)                    # fan_in D (conv / predictor linears)
+        out[name] = unif(shape, bound)
+    return out
+
+
+class _Holder(nn.Module):
+    pass
+
+
+class TGNModel(nn.Module):
+    """memory + gnn + link_pred of pyg_model_utils.py:10-36 over one flat parameter buffer."""
+
+    def __init__(self, num_nodes, num_events, msg_dim, hidden_dim, device, ring=10, max_batch=2048, max_neg=1,
+                 aggr="last", dropout=0.1, generator=None):
+        super().__init__()
+        dev = _lib.require_device(device)
+        D, d = int(hidden_dim), int(msg_dim)
+        self.num_nodes, self.num_events, self.D, self.d = int(num_nodes), int(num_events), D, d
+        self.cfg = TgnConfig(num_nodes=num_nodes, num_events=num_events, ring=ring, mem_dim=D, msg_dim=d, heads=2,
+                             max_batch=max_batch, max_neg=max_neg, aggr=0 if aggr == "last" else 1, dropout=dropout,
+                             lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8)
+        off = (ctypes.c_int64 * 22)()
+        _lib.call("tgnx_tgn_param_layout", ctypes.byref(self.cfg), off)
+        self.offsets = list(off)
+        total = self.offsets[-1]
+        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.grad_flat = torch.zeros(total + 1, dtype=torch.float32, device=dev)    # + batch-loss slot
+        shapes = param_shapes(D, d)
+        init = reference_init(D, d, generator)
+        self.memory = _Holder()
+        self.memory.time_enc = _Holder()
+        self.memory.time_enc.lin = _Holder()
+        self.memory.gru = _Holder()
+        self.gnn = _Holder()
+        self.gnn.conv = _Holder()
+        for k in ("key", "query", "value", "edge", "skip"):
+            setattr(self.gnn.conv, f"lin_{k}", _Holder())
+        self.link_pred = _Holder()
+        for k in ("src", "dst", "final"):
+            setattr(self.link_pred, f"lin_{k}", _Holder())
+        self._views = {}
+        for name, o in zip(PARAM_ORDER, self.offsets[:-1]):
+            n = int(np.prod(shapes[name]))
+            view = self.flat[o:o + n].view(shapes[name])
+            view.copy_(init[name].to(dev))
+            mod = self
+            parts = name.split(".")
+            for part in parts[:-1]:
+                mod = getattr(mod, part)
+            setattr(mod, parts[-1], nn.Parameter(view))
+            self._views[name] = (o, n, shapes[name])
+        self.gnn.time_enc = self.memory.time_enc                           # shared (pyg_model_utils.py:27)
+        # TGNMemory buffers (memory_module.py:80-83) and the message stores
+        self.memory.register_buffer("memory", torch.zeros(num_nodes, D, device=dev))
+        self.memory.register_buffer("last_update", torch.zeros(num_nodes, dtype=torch.long, device=dev))
+        words = _lib.lib().tgnx_tgn_store_words(ctypes.byref(self.cfg))
+        if words == 0:
+            raise RuntimeError(f"tgnx_tgn_store_words: {_lib.lib().tgnx_last_error().decode()}")
+        self.store = torch.zeros(int(words), dtype=torch.long, device=dev)
+        self.node_gen = torch.zeros(num_nodes, dtype=torch.int32, device=dev)
+
+    @property
+    def device(self):
+        return self.flat.device
+
+    def trainable_count(self) -> int:
+        return sum(n for _, n, _ in self._views.values())
+
+    def load_reference_state(self, sd: dict) -> None:
+        with torch.no_grad():
+            for name, (o, n, _) in self._views.items():
+                self.flat[o:o + n].copy_(sd[name].reshape(-1).to(self.flat.device))
+
+    def grads_by_name(self) -> dict:
+        return {name: self.grad_flat[o:o + n].view(s) for name, (o, n, s) in self._views.items()}
+
+    def forward(self, *a, **k):
+        raise RuntimeError("tgnx TGN runs through tgnx.tgn.TgnEngine / pyg_epoch_utils (the fused HIP step)")
+
+
+class TgnAdam(torch.optim.Optimizer):
+    """torch.optim.Adam over set(memory) | set(gnn) | set(link_pred) (pyg_model_utils.py:38-43); the
+    update runs on the device (tgnx_tgn_train_update)."""
+
+    def __init__(self, model: TGNModel, lr: float):
+        super().__init__([p for p in model.parameters() if p.requires_grad], dict(lr=lr, betas=(0.9, 0.999), eps=1e-8))
+        self.model = model
+        model.cfg.lr = float(lr)
+        self.exp_avg = torch.zeros_like(model.flat)
+        self.exp_avg_sq = torch.zeros_like(model.flat)
+
+    def zero_grad(self, set_to_none: bool = True):
+        pass
+
+    def step(self, closure=None):
+        raise RuntimeError("TgnAdam.step runs inside the TGN train step (tgnx_tgn_train_update)")
+
+
+def _p(t):
+    return 0 if t is None else t.data_ptr()
+
+
+class TgnEngine:
+    """Owns the workspace of one TGN model + one neighbour ring over a resident event table
+    (src, dst, t, msg rows = e_id)."""
+
+    def __init__(self, model: TGNModel, loader, events: dict, optimizer: TgnAdam | None = None,
+                 dst_nodes=None, seed: int = 0, rank: int = 0, world: int = 1):
+        self.model, self.loader, self.opt = model, loader, optimizer
+        self.dev = model.device
+        cfg = model.cfg
+        if cfg.ring != loader.size:
+            cfg.ring = loader.size
+        self.cfg = cfg
+        ev = {k: torch.as_tensor(v) for k, v in events.items()}
+        self.src = ev["src"].to(self.dev, torch.long).contiguous()
+        self.dst = ev["dst"].to(self.dev, torch.long).contiguous()
+        self.t = ev["t"].to(self.dev, torch.float32).contiguous()
+        self.msg = ev["msg"].to(self.dev, torch.float32).contiguous()
+        if self.src.numel() > cfg.num_events:
+            raise ValueError("event table larger than cfg.num_events")
+        nb = _lib.lib().tgnx_tgn_ws_bytes(ctypes.byref(cfg))
+        if nb == 0:
+            raise RuntimeError(f"tgnx_tgn_ws_bytes: {_lib.lib().tgnx_last_error().decode()}")
+        self.ws = torch.zeros(nb, dtype=torch.uint8, device=self.dev)
+        self.ctl = torch.zeros(16, dtype=torch.int64, device=self.dev)
+        self.neg_train = torch.zeros(cfg.num_events, dtype=torch.long, device=self.dev)
+        self.out_pos = torch.zeros(cfg.max_batch, dtype=torch.float32, device=self.dev)
+        self.out_neg = torch.zeros(cfg.max_batch * max(cfg.max_neg, 1), dtype=torch.float32, device=self.dev)
+        self.mrr = torch.zeros(cfg.max_batch, dtype=torch.float64, device=self.dev)
+        self.dst_nodes = None if dst_nodes is None else torch.as_tensor(dst_nodes).to(self.dev, torch.long).contiguous()
+        self.seed, self.rank, self.world = int(seed), int(rank), int(world)
+        if optimizer is None:
+            self.adam_m, self.adam_v = torch.zeros_like(model.flat), torch.zeros_like(model.flat)
+        else:
+            self.adam_m, self.adam_v = optimizer.exp_avg, optimizer.exp_avg_sq
+
+    def _buffers(self, neg_ptr: int) -> TgnBuffers:
+        m, ld = self.model, self.loader
+        b = TgnBuffers()
+        b.ev_src, b.ev_dst, b.ev_t, b.ev_msg = _p(self.src), _p(self.dst), _p(self.t), _p(self.msg)
+        b.neg = neg_ptr
+        b.dst_nodes = _p(self.dst_nodes)
+        b.n_dst = 0 if self.dst_nodes is None else self.dst_nodes.numel()
+        b.nbr, b.eid, b.rt, b.assoc = _p(ld.neighbors), _p(ld.e_id), _p(ld.t), _p(ld._assoc)
+        b.memory, b.last_update = _p(m.memory.memory), _p(m.memory.last_update)
+        b.store, b.node_gen = _p(m.store), _p(m.node_gen)
+        b.params, b.grads, b.adam_m, b.adam_v = _p(m.flat), _p(m.grad_flat), _p(self.adam_m), _p(self.adam_v)
+        b.ctl, b.out_pos, b.out_neg, b.mrr, b.ws = _p(self.ctl), _p(self.out_pos), _p(self.out_neg), _p(self.mrr), _p(self.ws)
+        return b
+
+    def _stream(self):
+        return _lib.stream(self.dev)
+
+    def advance(self, batch_start: int, B: int, train: bool):
+        _lib.call("tgnx_tgnn_advance", _p(self.ctl), 0, batch_start, B, batch_start, 0, 0, 1, self.rank, self.world,
+                  self.seed, 1 if train else 0, self._stream())
+
+    # ------------------------------------------------------------------ state
+    def reset_state(self):
+        """memory_module.reset_state + neighbor_loader.reset_state (pyg_epoch_utils.py:15-16)."""
+        b = self._buffers(0)
+        _lib.call("tgnx_tgn_reset_state", ctypes.byref(self.cfg), ctypes.byref(b), self._stream())
+        self.loader.reset_state()
+
+    def flush(self):
+        """TGNMemory.train(False) (memory_module.py:209-215)."""
+        b = self._buffers(0)
+        _lib.call("tgnx_tgn_flush", ctypes.byref(self.cfg), ctypes.byref(b), self._stream())
+
+    # ------------------------------------------------------------------ steps
+    def train_batch(self, start: int, B: int, neg=None, dropout: bool = True, update: bool = True):
+        """One TGN train batch over events [start, start + B).  neg: LongTensor[B] to inject, or None to
+        draw on the device.  Returns (sigmoid(pos), sigmoid(neg)) views."""
+        if neg is not None:
+            self.neg_train[start:start + B].copy_(torch.as_tensor(neg).to(self.dev, torch.long))
+        self.advance(start, B, True)
+        b = self._buffers(_p(self.neg_train))
+        _lib.call("tgnx_tgn_train_fwd_bwd", ctypes.byref(self.cfg), ctypes.byref(b), 0 if neg is not None else 1,
+                  1 if dropout else 0, self._stream())
+        self._pending = b
+        if update:
+            self.apply_update()
+        return self.out_pos[:B], self.out_neg[:B]
+
+    def apply_update(self, allreduce: bool = True):
+        if allreduce and self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.model.grad_flat)
+        _lib.call("tgnx_tgn_train_update", ctypes.byref(self.cfg), ctypes.byref(self._pending), self._stream())
+
+    def eval_batch(self, start: int, B: int, negs):
+        """TGB-style eval batch: negs LongTensor[B, Kn].  Returns (pos [B], neg [B, Kn], rr [B])."""
+        negs = torch.as_tensor(negs).to(self.dev, torch.long).contiguous()
+        Kn = negs.shape[1]
+        if Kn > self.cfg.max_neg:
+            raise ValueError(f"{Kn} negatives > max_neg {self.cfg.max_neg}")
+        self.advance(start, B, False)
+        # the kernels index neg[(start + i) * Kn + c]: shift the base pointer by start rows
+        b = self._buffers(negs.data_ptr() - start * Kn * 8)
+        _lib.call("tgnx_tgn_eval_step", ctypes.byref(self.cfg), ctypes.byref(b), Kn, self._stream())
+        self._keep = negs
+        return self.out_pos[:B], self.out_neg[:B * Kn].view(B, Kn), self.mrr[:B]
+
+    def loss_sum(self) -> float:
+        return float(self.ctl[12:13].view(torch.float64).item())
+
+    def check(self):
+        err = int(self.ctl[11].item())
+        if err:
+            raise RuntimeError(f"tgnx TGN step error flags {err:#x} (batch or sampled set beyond capacity)")
+
+
+def getModel(feature_dim, hidden_dim, num_nodes, device, num_events=None, **kw):
+    """pyg_model_utils.py:10-36; num_events sizes the message-store arena (the event table's rows)."""
+    if num_events is None:
+        raise ValueError("tgnx getModel (PyG TGN) needs num_events (rows of the event table)")
+    m = TGNModel(num_nodes, num_events, feature_dim, hidden_dim, device, **kw)
+    return {"memory": m.memory, "gnn": m.gnn, "link_pred": m.link_pred, "model": m}
+
+
+def getOptimizer(model, lr):
+    return TgnAdam(model["model"], lr)
