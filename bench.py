@@ -4,9 +4,12 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A step is one train batch of the running reference path (epoch_utils.py:186-315):
-negatives, sampler read, all dependency blocks of the batch (model_utils.py:68-157),
-predictor + BCE, backward, Adam, neighbour-ring insert.  Synthetic wiki-shaped stream
+A step is one train batch.  Headline (--model tgn, the north star): the TGN memory path
+(modules/memory_module.py + msg_func/msg_agg + emb_module TransformerConv + decoder LinkPredictor,
+the loop pyg_epoch_utils.py:106-137 comments out): negatives, sampler, GRU memory update of every
+sampled node, attention embedding, link prediction + BCE, backward, Adam, update_state + ring
+insert.  Secondary (--model tgnn): the running DGL path (epoch_utils.py:186-315, all dependency
+blocks of the batch).  Synthetic wiki-shaped stream
 (TGB data is not downloadable here), events resident in HBM.
 Data-parallel: the global batch is B·N events, every rank replays the ring/time state of the
 whole batch and computes its 1/N of the rows; gradients are all-reduced over RCCL (weak scaling).
@@ -80,27 +83,8 @@ def cpu_baseline(stream, B, budget_s=15.0, max_batches=40):
                       f"wiki-shaped stream, B={B}, K=10, dropout 0.6 (reference epoch 1), torch CPU threads={cores}"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--batch", type=int, default=200, help="events per GPU per step")
-    ap.add_argument("--dataset", default="tgbl-wiki")
-    ap.add_argument("--no-dropout", action="store_true", help="train mode without dropout (reference epochs >= 2)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--probe-steps", type=int, default=100)
-    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+def run_tgnn(args, world, rank, dev):
+    """The running reference path (model_utils.TGNN, DGL EdgeGATConv block loop)."""
 
     from tgnx import _lib
     from tgnx.engine import TgnnEngine
@@ -205,7 +189,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(stream, args.batch)
 
-    if rank == 0:
+    if True:
         out = {
             "metric": "temporal edges/sec on tgbl-wiki TGN (train step)",
             "value": round(args.steps * Bg / elapsed, 1),
@@ -237,6 +221,225 @@ def main():
             "cpu_baseline": cpu,
             "loss_sum": round(loss, 4),
         }
+        return out
+
+
+
+def cpu_baseline_tgn(stream, B, budget_s=15.0, max_batches=40):
+    """Oracle restatement of the TGN memory path (oracle/tgn_ref.py) on the same stream, bounded sample."""
+    sys.path.insert(0, ROOT)
+    from oracle.sampler_ref import RefLastNeighborLoader
+    from oracle.tgn_ref import RefTGN, train_step
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+    torch.set_num_threads(cores)
+    N, d = stream.shape.num_nodes, stream.shape.msg_dim
+    torch.manual_seed(0)
+    model = RefTGN(N, d, hidden=100, aggr="last", dropout=0.1)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    loader = RefLastNeighborLoader(N, 10)
+    ev_t = torch.from_numpy(stream.t.astype(np.float32))
+    ev_msg = torch.from_numpy(stream.msg)
+    rng = np.random.default_rng(0)
+    n, t_total = 0, 0.0
+    while n < max_batches and t_total < budget_s:
+        sl = slice(n * B, (n + 1) * B)
+        src, dst = torch.from_numpy(stream.src[sl]), torch.from_numpy(stream.dst[sl])
+        neg = torch.from_numpy(rng.choice(stream.dst_nodes, size=src.shape[0]))
+        t0 = time.perf_counter()
+        train_step(model, opt, loader, ev_t, ev_msg, src, dst, neg, ev_t[sl], ev_msg[sl])
+        dt = time.perf_counter() - t0
+        if n > 0:
+            t_total += dt
+        n += 1
+    timed = max(n - 1, 1)
+    return {"value": round(timed * B / max(t_total, 1e-9), 2), "unit": "events/s", "cores": cores, "kind": "port",
+            "sample": f"oracle TGN restatement (oracle/tgn_ref.py: TGNMemory + GRU + TransformerConv + LinkPredictor), "
+                      f"train batches 2..{n} of the same wiki-shaped stream, B={B}, K=10, last aggregation, "
+                      f"torch CPU threads={cores}"}
+
+
+def run_tgn(args, world, rank, dev):
+    """The TGN memory path (north star; SURVEY §8 a14–a16): TGNMemory + GRU, TransformerConv, LinkPredictor."""
+    from tgnx import _lib
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.synth import SHAPES, make_stream
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+
+    shape = SHAPES[args.dataset]
+    stream = make_stream(shape, seed=0)
+    N, d, D, K = shape.num_nodes, shape.msg_dim, 100, 10
+    Bg = args.batch * world
+    g = torch.Generator().manual_seed(0)
+    model = TGNModel(N, stream.num_events, d, D, dev, ring=K, max_batch=Bg, max_neg=1,
+                     aggr="mean" if args.aggr == "mean" else "last", dropout=0.0 if args.no_dropout else 0.1,
+                     generator=g)
+    opt = TgnAdam(model, 1e-4)
+    loader = LastNeighborLoader(N, K, device=dev)
+    eng = TgnEngine(model, loader, dict(src=stream.src, dst=stream.dst, t=stream.t.astype(np.float32), msg=stream.msg),
+                    opt, dst_nodes=np.unique(stream.dst), seed=1234, rank=rank, world=world)
+    eng.bind_resident(0, stream.train_end, Bg, dropout=not args.no_dropout)
+    nb_epoch = math.ceil(stream.train_end / Bg)
+    counter = {"i": 0}
+    use_graph = not args.no_graph
+    eng.begin_epoch()
+    if use_graph:
+        eng.capture_resident()
+
+    def step(eager=False):
+        if counter["i"] % nb_epoch == 0 and counter["i"] > 0:
+            eng.begin_epoch()
+        if use_graph and not eager:
+            eng.replay_resident()
+        else:
+            eng.resident_train_step()
+        counter["i"] += 1
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    eng.check()
+    loss = eng.loss_sum()
+    assert math.isfinite(loss), "non-finite loss"
+
+    # live per-launch timing (HIP events on the launch stream), units from the device counters
+    Qm = 3 * D + d
+    probes = {}
+    spec = (("tgn_gru_edge", 1), ("tgn_attn_fwd", 6), ("tgn_attn_bwd", 8), ("tgn_wgrad_edge_proj", 2),
+            ("tgn_agg_emit", 9), ("tgn_scan", 3), ("tgn_pred_train", 4), ("tgn_update", 5), ("tgn_adam", 7))
+    for name, kid in spec:
+        _lib.call("tgnx_probe_enable", kid)
+        pe0, pm0 = eng.units()
+        for _ in range(args.probe_steps):
+            step(eager=True)
+        barrier()
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        _lib.call("tgnx_probe_read", ctypes.byref(ms), ctypes.byref(n))
+        _lib.call("tgnx_probe_enable", 0)
+        pe1, pm1 = eng.units()
+        launches = max(int(n.value), 1)
+        avg_ms = ms.value / launches
+        E = (pe1 - pe0) / launches
+        M = (pm1 - pm0) / launches
+        # algorithmic bytes per launch (DESIGN.md §TGN): edges carry the §8(d) per-sampled-edge record
+        # (ring entry 20 + msg row 4d + neighbour memory / projections 4D + Δt 4); nodes carry their
+        # message gather (2 memory rows + msg row + Δt) and GRU rows (X 4Qm, memory 4D, z 4D, gates 16D)
+        per_edge = 20 + 4 * d + 4 * D + 4
+        if name == "tgn_gru_edge":
+            algo = M * (4 * Qm + 4 * D + 4 * D + 16 * D) + E * (4 * d + 12 + 4 * D)
+        elif name in ("tgn_attn_fwd", "tgn_attn_bwd"):
+            algo = E * (12 * D + 8) + M * 0
+        elif name == "tgn_wgrad_edge_proj":
+            algo = E * (4 * D + 4 * d + 12) + M * (16 * D + 4 * D)
+        elif name == "tgn_agg_emit":
+            algo = M * (8 * D + 4 * d + 40 + 4 * Qm) + E * (per_edge + 4)
+        else:
+            algo = 0.0
+        probes[name] = dict(avg_us=avg_ms * 1e3, edges=E, nodes=M, bytes=algo,
+                            gbs=(algo / (avg_ms * 1e-3) / 1e9) if algo else None)
+    dom = max((k for k in probes if probes[k]["bytes"]), key=lambda k: probes[k]["avg_us"])
+    pd = probes[dom]
+    flops_gru_edge = None
+    if "tgn_gru_edge" in probes:
+        q = probes["tgn_gru_edge"]
+        flops_gru_edge = 2 * q["nodes"] * (Qm + D) * 4 * D + 2 * q["edges"] * (D + d) * D
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(dom, {}).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_tgn(stream, args.batch)
+    return {
+        "metric": "temporal edges/sec on tgbl-wiki TGN (train step)",
+        "value": round(args.steps * Bg / elapsed, 1),
+        "unit": "events/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic tgbl-wiki-shaped stream (SURVEY.md §8d), events resident in HBM",
+        "config": {"workload": f"{args.dataset} TGN memory path (TGNMemory + GRUCell, IdentityMessage + "
+                               f"{'Mean' if args.aggr == 'mean' else 'Last'}Aggregator, TransformerConv heads=2, "
+                               f"LinkPredictor), batch {args.batch}/GPU, {K} temporal neighbours, D=100, d={d}, "
+                               f"attention dropout {'off' if args.no_dropout else '0.1'}",
+                   "global_batch": Bg, "parallelism": f"dp{world}",
+                   "launch": "hip-graph replay per step" if use_graph else "eager",
+                   "sampled_edges_per_step": round(probes[dom]["edges"], 1),
+                   "sampled_nodes_per_step": round(probes[dom]["nodes"], 1)},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(pd["gbs"], 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(pd["gbs"] / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "avg_launch_us": round(pd["avg_us"], 3), "algo_bytes_per_launch": round(pd["bytes"]),
+                     "bytes_model": "DESIGN.md §TGN: per sampled edge 20 + 4d + 4D + 4 (SURVEY §8d) plus per-node "
+                                    "message / GRU rows; tgn_gru_edge also " +
+                                    (f"{flops_gru_edge / (probes['tgn_gru_edge']['avg_us'] * 1e-6) / 1e12:.3f} "
+                                     f"TFLOP/s fp32 MFMA" if flops_gru_edge else "")},
+        "kernels_us": {k: round(v["avg_us"], 3) for k, v in probes.items()},
+        "cpu_baseline": cpu,
+        "loss_sum": round(loss, 4),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--batch", type=int, default=200, help="events per GPU per step")
+    ap.add_argument("--dataset", default="tgbl-wiki")
+    ap.add_argument("--model", choices=["tgn", "tgnn"], default="tgn",
+                    help="tgn: the TGN memory path (north star, headline); tgnn: the running DGL block-loop path")
+    ap.add_argument("--aggr", choices=["last", "mean"], default="last")
+    ap.add_argument("--only", action="store_true", help="skip the secondary path")
+    ap.add_argument("--no-dropout", action="store_true", help="train mode without dropout")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe-steps", type=int, default=100)
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    run = {"tgn": run_tgn, "tgnn": run_tgnn}
+    out = run[args.model](args, world, rank, dev)
+    if not args.only:
+        other = "tgnn" if args.model == "tgn" else "tgn"
+        sec = run[other](args, world, rank, dev)
+        out["secondary_path"] = {"model": other, "workload": sec["config"]["workload"], "value": sec["value"],
+                                 "unit": sec["unit"], "ms_per_step": sec["ms_per_step"],
+                                 "roofline": sec["roofline"], "kernels_us": sec["kernels_us"],
+                                 "cpu_baseline": sec["cpu_baseline"]}
+    if rank == 0:
         print(json.dumps(out))
     if world > 1:
         torch.distributed.destroy_process_group()

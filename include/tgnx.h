@@ -212,10 +212,10 @@ int tgnx_tgnn_eval_step(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* bu
                         int32_t tile_quirk, void* stream);
 
 /* ---------------------------------------------------------------- dense fp32 GEMM
- * C[M,N] = op(A) op(B) (+ bias[N]) (+ C if accumulate) on v_mfma_f32_16x16x4_f32, split-K with a
- * deterministic fixed-order reduction.  op(A)(m,k) = trans_a ? A[k*lda+m] : A[m*lda+k];
- * op(B)(k,n) = trans_b ? B[n*ldb+k] : B[k*ldb+n].  `ws` holds tgnx_gemm_f32_ws_bytes(M,N,K) bytes,
- * zero-filled once (tickets return to zero).  Used by the TGN memory path (modules: Linear /
+ * C[M,N] = op(A) op(B) (+ bias[N]) (+ C if accumulate) on v_mfma_f32_16x16x4_f32; K > 256 runs
+ * split-K with a fixed-order (deterministic) fixup launch.  op(A)(m,k) = trans_a ? A[k*lda+m] : A[m*lda+k];
+ * op(B)(k,n) = trans_b ? B[n*ldb+k] : B[k*ldb+n].  `ws` holds tgnx_gemm_f32_ws_bytes(M,N,K) bytes
+ * (split partials).  Used by the TGN memory path (modules: Linear /
  * GRUCell / TransformerConv contractions); exported for tests. */
 size_t tgnx_gemm_f32_ws_bytes(int64_t M, int64_t N, int64_t K);
 int tgnx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, int32_t trans_a, const float* B,

@@ -100,12 +100,10 @@ struct Ctx {
   int64_t* xw;
   float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
   float *dZc, *dP, *dE, *dG, *tgp;
-  float* gpart;
-  int* tick;
+  float *pA, *pB, *pC, *pD;  // split-K partials of the deferred weight-gradient GEMMs
   uint64_t *rkeys, *skeys;
   int *rruns, *sruns;
   int Bmax, Qcap, Rcap, Mcap, Ecap, Ucap, tgp_rows;
-  size_t gpart_floats;
   Lay L;
 };
 
@@ -306,6 +304,8 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
     c.cnt[CNT_M] = M;
     c.cnt[CNT_E] = E;
     c.cnt[CNT_U] = U;
+    c.ctl[TGNX_CTL_SUM_E] += E;
+    c.ctl[TGNX_CTL_SUM_S] += M;
   }
 }
 
@@ -1045,20 +1045,26 @@ struct EpiTeMsg {
   }
 };
 
-// Δt-encoding grads: fixed-order sum of the partial rows into grads (before any all-reduce)
-__global__ void tgn_te_reduce(Ctx c, int rows_edge, int rows_msg) {
-  const int B = (int)c.ctl[TGNX_CTL_B];
-  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int D = c.D;
-  const int E = c.cnt[CNT_E], M = c.cnt[CNT_M];
-  const int re = min(rows_edge, (E + GT - 1) / GT), rm = min(rows_msg, (M + GT - 1) / GT);
-  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < 2 * D; x += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int r = 0; r < re; ++r) s += c.tgp[(int64_t)r * 2 * D + x];
-    for (int r = 0; r < rm; ++r) s += c.tgp[(int64_t)(rows_edge + r) * 2 * D + x];
-    c.grads[(x < D ? c.L.te_w : c.L.te_b - D) + x] = s;
+// Δt-encoding grads: fixed-order sum of the partial rows into grads (before any all-reduce); rides
+// as the tail block of the weight-gradient fixup launch
+struct TeReduceTail {
+  Ctx c;
+  int rows_edge, rows_msg;
+  __device__ void operator()(int bid) const {
+    if (bid != 0) return;
+    const int B = (int)c.ctl[TGNX_CTL_B];
+    if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+    const int D = c.D;
+    const int E = c.cnt[CNT_E], M = c.cnt[CNT_M];
+    const int re = min(rows_edge, (E + GT - 1) / GT), rm = min(rows_msg, (M + GT - 1) / GT);
+    for (int x = threadIdx.x; x < 2 * D; x += blockDim.x) {
+      float s = 0.f;
+      for (int r = 0; r < re; ++r) s += c.tgp[(int64_t)r * 2 * D + x];
+      for (int r = 0; r < rm; ++r) s += c.tgp[(int64_t)(rows_edge + r) * 2 * D + x];
+      c.grads[(x < D ? c.L.te_w : c.L.te_b - D) + x] = s;
+    }
   }
-}
+};
 
 // ------------------------------------------------------------------ optimizer + state update
 __device__ __forceinline__ void adam1(float g, float& m, float& v, float& p, float b1, float b2, float eps, float step,
@@ -1238,26 +1244,15 @@ static Caps make_caps(const tgnx_tgn_config* cfg) {
   k.Ucap = cap(2 * (int64_t)k.B);
   return k;
 }
-// the GEMMs of a step (capacities), for partial-buffer sizing
-static void gemm_caps(const Caps& k, GemmShape* g, int& n) {
-  n = 0;
-  g[n++] = gemm_shape(k.Mcap, 4 * k.D, k.Qm + k.D, GKC);           // G1
-  g[n++] = gemm_shape(k.Ecap, k.HC, k.D + k.d, GKC);                // G3
-  g[n++] = gemm_shape(k.Mcap, 4 * k.HC, k.D, GKC);                  // G2
-  g[n++] = gemm_shape(k.HC, k.D + k.d, k.Etr, GKC);                 // G5
-  g[n++] = gemm_shape(4 * k.HC, k.D + 1, k.Mtr, GKC);               // G6
-  g[n++] = gemm_shape(2 * k.D, k.D, 3 * k.B, GKC);                  // link predictor
-  g[n++] = gemm_shape(k.Etr, k.D, k.HC, GKC);                       // G5b
-  g[n++] = gemm_shape(k.Mtr, k.D, 4 * k.HC, GKC);                   // G7
-  g[n++] = gemm_shape(4 * k.D, k.Qm + k.D + 1, k.Mtr, GKC);         // G8
-  g[n++] = gemm_shape(k.Mtr, k.D, 4 * k.D, GKC);                    // G9
-  g[n++] = gemm_shape(k.Rcap, k.D, k.D, GKC);                       // Hs / Hd
-}
+// the deferred (split-K) weight-gradient GEMMs of a train step
+static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split(k.HC, k.D + k.d, k.Etr, GKC, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, 32); }
+static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_split(4 * k.HC, k.D + 1, k.Mtr, GKC, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, 16); }
+static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split(2 * k.D, k.D, 3 * k.B, GKC, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, 16); }
+static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split(4 * k.D, k.Qm + k.D + 1, k.Mtr, GKC, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, 16); }
 struct WsLay {
   size_t cb, nb, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
-      Ep, alpha, Zc, evs, Hs, Hd, dZc, dP, dE, dG, tgp, gpart, tick, rkeys, rruns, skeys, sruns, total;
-  size_t gpart_floats;
-  int ntick, tgp_rows;
+      Ep, alpha, Zc, evs, Hs, Hd, dZc, dP, dE, dG, tgp, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, total;
+  int tgp_rows;
 };
 static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   WsLay W;
@@ -1297,19 +1292,10 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.dG = carve(off, (size_t)k.Mtr * 4 * D * 4);
   W.tgp_rows = (k.Etr + GT - 1) / GT + (k.Mtr + GT - 1) / GT;
   W.tgp = carve(off, (size_t)W.tgp_rows * 2 * D * 4);
-  GemmShape g[16];
-  int n;
-  gemm_caps(k, g, n);
-  size_t pf = 0;
-  int nt = 1;
-  for (int i = 0; i < n; ++i) {
-    pf = std::max(pf, gemm_partial_floats(g[i]));
-    nt = std::max(nt, g[i].tiles_m * g[i].tiles_n);
-  }
-  W.gpart_floats = pf;
-  W.ntick = nt;
-  W.gpart = carve(off, 2 * pf * 4 + 64);
-  W.tick = carve(off, (size_t)2 * nt * 4);
+  W.pA = carve(off, gemm_partial_floats(shp_dWe(k, nullptr)) * 4);
+  W.pB = carve(off, gemm_partial_floats(shp_dWp(k, nullptr)) * 4);
+  W.pC = carve(off, gemm_partial_floats(shp_dWlp(k, nullptr)) * 4);
+  W.pD = carve(off, gemm_partial_floats(shp_dWg(k, nullptr)) * 4);
   const int n2 = 2 * k.B;
   W.rkeys = carve(off, (size_t)n2 * 8);
   W.rruns = carve(off, (size_t)(n2 + 2) * 4);
@@ -1417,8 +1403,10 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.dE = reinterpret_cast<float*>(ws + W.dE);
   c.dG = reinterpret_cast<float*>(ws + W.dG);
   c.tgp = reinterpret_cast<float*>(ws + W.tgp);
-  c.gpart = reinterpret_cast<float*>(ws + W.gpart);
-  c.tick = reinterpret_cast<int*>(ws + W.tick);
+  c.pA = reinterpret_cast<float*>(ws + W.pA);
+  c.pB = reinterpret_cast<float*>(ws + W.pB);
+  c.pC = reinterpret_cast<float*>(ws + W.pC);
+  c.pD = reinterpret_cast<float*>(ws + W.pD);
   c.rkeys = reinterpret_cast<uint64_t*>(ws + W.rkeys);
   c.rruns = reinterpret_cast<int*>(ws + W.rruns);
   c.skeys = reinterpret_cast<uint64_t*>(ws + W.skeys);
@@ -1430,7 +1418,6 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.Ecap = k.Ecap;
   c.Ucap = k.Ucap;
   c.tgp_rows = W.tgp_rows;
-  c.gpart_floats = W.gpart_floats;
   c.L = make_lay(c.D, c.d);
   return TGNX_OK;
 }
@@ -1448,7 +1435,7 @@ static void gru_list(const Ctx& c, const Caps& k, const int64_t* list, const int
   tgn_agg_emit<<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
   const GemmShape g1 = gemm_shape(mcap, 4 * c.D, c.Qm + c.D, GKC, list_cnt);
   gemm_launch(g1, LoadGruA{c.X, c.mem, list, base, c.Qm, c.D}, LoadGruW{P + c.L.w_ih, P + c.L.w_hh, c.Qm, c.D},
-              EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, list, base, c.D, c.Z0, c.gates}, c.gpart, c.tick, s);
+              EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, list, base, c.D, c.Z0, c.gates}, nullptr, s);
 }
 
 }  // namespace tgn
@@ -1506,63 +1493,78 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   hipStream_t s = as_stream(stream);
   const float* P = c.params;
   float* G = c.grads;
-  float *p0 = c.gpart, *p1 = c.gpart + c.gpart_floats;
-  int *t0 = c.tick, *t1 = c.tick + W.ntick;
   const int D = c.D, HC = c.HC, Qm = c.Qm, d = c.d;
   tgn_mark<true><<<gridn(3 * k.B, 256), 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_mark");
+  probe_begin(TGNX_K_ASSEMBLE, s);
   tgn_scan<true><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
+  probe_end(TGNX_K_ASSEMBLE, s);
   TGNX_LAUNCH_CHECK("tgn_scan");
   const int nemit = gridn(k.Rtr, 256);
+  probe_begin(TGNX_K_EDGE_META, s);
   tgn_agg_emit<<<nemit + gridn(k.Mtr, 4, 2048), 256, 0, s>>>(c, 0, nemit, nullptr, nullptr, 0, 0);
+  probe_end(TGNX_K_EDGE_META, s);
   TGNX_LAUNCH_CHECK("tgn_agg_emit");
   // GRU over every sampled node ‖ lin_edge over every sampled edge
   const LoadEdgeAttr ea{c.e_j, c.e_id, c.e_t, c.lu, c.ev_msg, P + c.L.te_w, P + c.L.te_b, D, d};
+  probe_begin(TGNX_K_EDGE_FWD, s);
   gemm2_launch(gemm_shape(k.Mtr, 4 * D, Qm + D, GKC, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D},
                LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
-               EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, p0, t0,
+               EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, nullptr,
                gemm_shape(k.Etr, HC, D + d, GKC, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
-               EpiStore{c.Ep, nullptr, HC, 0}, p1, t1, s);
+               EpiStore{c.Ep, nullptr, HC, 0}, nullptr, s);
+  probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgn_gru_edge");
   gemm_launch(gemm_shape(k.Mtr, 4 * HC, D, GKC, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
               LoadProjW{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
-              EpiProj{P + c.L.bq, P + c.L.bk, P + c.L.bv, P + c.L.bsk, c.P, HC}, p0, t0, s);
+              EpiProj{P + c.L.bq, P + c.L.bk, P + c.L.bv, P + c.L.bsk, c.P, HC}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_proj");
+  probe_begin(TGNX_K_SEG_FWD, s);
   tgn_attn_fwd<true><<<gridn(k.Rtr, 4), 256, 0, s>>>(c);
+  probe_end(TGNX_K_SEG_FWD, s);
   TGNX_LAUNCH_CHECK("tgn_attn_fwd");
+  probe_begin(TGNX_K_PRED, s);
   tgn_pred_train<<<k.B, 256, 0, s>>>(c);
+  probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
   const int ncb = gridn(k.Rtr, 4);
+  probe_begin(TGNX_K_SEG_BWD, s);
   tgn_attn_bwd<<<ncb + gridn(3 * D + 2, 4), 256, 0, s>>>(c, ncb);
+  probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_attn_bwd");
-  gemm2_launch(gemm_shape(HC, D + d, k.Etr, GKC, nullptr, nullptr, c.cnt + CNT_E), LoadKRow{c.dE, HC, k.Etr, HC},
-               LoadEdgeAttrT{ea}, EpiStore{G + c.L.we, nullptr, D + d, 0}, p0, t0,
-               gemm_shape(4 * HC, D + 1, k.Mtr, GKC, nullptr, nullptr, c.cnt + CNT_M), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC},
-               LoadZ1T{c.Z0, D},
-               EpiProjGrad{G, c.L.wq, c.L.bq, c.L.wk, c.L.bk, c.L.wv, c.L.bv, c.L.wsk, c.L.bsk, HC, D}, p1, t1, s);
+  // weight gradients (deferred split-K) ‖ ...
+  const EpiStore e_dWe{G + c.L.we, nullptr, D + d, 0};
+  const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.wk, c.L.bk, c.L.wv, c.L.bv, c.L.wsk, c.L.bsk, HC, D};
+  const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D};
+  const EpiGruWGrad e_dWg{G, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, Qm, D};
+  probe_begin(TGNX_K_EDGE_BWD, s);
+  gemm2_launch(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, e_dWe, c.pA, shp_dWp(k, c.cnt),
+               LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, e_dWp, c.pB, s);
+  probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad1");
   const int rows_edge = (k.Etr + GT - 1) / GT, rows_msg = (k.Mtr + GT - 1) / GT;
-  gemm2_launch(gemm_shape(2 * D, D, 3 * k.B, GKC, nullptr, nullptr, c.cnt + CNT_LIST),
-               LoadLpA{c.evs, c.ctl, D, evs_stride(D)}, LoadLpB{c.evs, c.ctl, D, evs_stride(D)},
-               EpiLpGrad{G, c.L.lsw, c.L.ldw, D}, p0, t0, gemm_shape(k.Etr, D, HC, GKC, c.cnt + CNT_E),
-               LoadRowK{c.dE, k.Etr, HC, HC}, LoadKRow{P + c.L.we, D, HC, D + d},
-               EpiTeEdge{c.e_j, c.e_t, c.lu, P + c.L.te_w, P + c.L.te_b, c.tgp, D, 0}, p1, t1, s);
+  gemm2_launch(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)}, LoadLpB{c.evs, c.ctl, D, evs_stride(D)},
+               e_dWlp, c.pC, gemm_shape(k.Etr, D, HC, GKC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
+               LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, P + c.L.te_w, P + c.L.te_b, c.tgp, D, 0},
+               nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad2");
   gemm_launch(gemm_shape(k.Mtr, D, 4 * HC, GKC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
               LoadProjWT{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
-              EpiGruBwd{c.gates, c.mem, c.nid, c.dG, D}, p0, t0, s);
+              EpiGruBwd{c.gates, c.mem, c.nid, c.dG, D}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_dz0");
-  gemm2_launch(gemm_shape(4 * D, Qm + D + 1, k.Mtr, GKC, nullptr, nullptr, c.cnt + CNT_M),
-               LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D},
-               EpiGruWGrad{G, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, Qm, D}, p0, t0,
-               gemm_shape(k.Mtr, D, 4 * D, GKC, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
-               LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c, rows_edge}, p1, t1, s);
+  gemm2_launch(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, e_dWg,
+               c.pD, gemm_shape(k.Mtr, D, 4 * D, GKC, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
+               LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c, rows_edge}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
-  tgn_te_reduce<<<1, 256, 0, s>>>(c, rows_edge, rows_msg);
-  TGNX_LAUNCH_CHECK("tgn_te_reduce");
+  gemm_fixup_launch(1, TeReduceTail{c, rows_edge, rows_msg}, s, GemmFix<EpiStore>{shp_dWe(k, c.cnt), c.pA, e_dWe},
+                    GemmFix<EpiProjGrad>{shp_dWp(k, c.cnt), c.pB, e_dWp}, GemmFix<EpiLpGrad>{shp_dWlp(k, c.cnt), c.pC, e_dWlp},
+                    GemmFix<EpiGruWGrad>{shp_dWg(k, c.cnt), c.pD, e_dWg});
+  TGNX_LAUNCH_CHECK("tgn_wgrad_fixup");
   // update_state (train order: memory of src ∪ dst from this step's GRU rows, then the stores), insert
   const int nmem = gridn(k.Ucap, 4, 1024), nst = gridn(2 * k.B, 256), nring = gridn(2 * k.B, 4);
+  probe_begin(TGNX_K_FINISH, s);
   tgn_update<<<nmem + nst + nring, 256, 0, s>>>(c, nmem, nst, 0, c.upd, c.cnt + CNT_U, 0, 0);
+  probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgn_update");
   return TGNX_OK;
 }
@@ -1574,7 +1576,9 @@ int tgnx_tgn_train_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* bu
   int rc = make_ctx(cfg, buf, 1, c, k, W);
   if (rc) return rc;
   TGNX_CHECK_ARG(buf->grads && buf->adam_m && buf->adam_v, "tgnx_tgn_train_update: null optimizer buffer");
+  probe_begin(TGNX_K_ADAM, as_stream(stream));
   tgn_adam<<<gridn(c.L.total / 4, 256), 256, 0, as_stream(stream)>>>(c);
+  probe_end(TGNX_K_ADAM, as_stream(stream));
   TGNX_LAUNCH_CHECK("tgn_adam");
   return TGNX_OK;
 }
@@ -1589,8 +1593,6 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   TGNX_CHECK_ARG(buf->neg && buf->out_pos && buf->out_neg && buf->mrr, "tgnx_tgn_eval_step: null buffer");
   hipStream_t s = as_stream(stream);
   const float* P = c.params;
-  float *p0 = c.gpart, *p1 = c.gpart + c.gpart_floats;
-  int *t0 = c.tick, *t1 = c.tick + W.ntick;
   const int D = c.D, HC = c.HC, d = c.d;
   const int Rq = (int)std::min<int64_t>(c.N, (int64_t)k.B * (2 + Kn));
   const int Mq = (int)std::min<int64_t>(c.N, (int64_t)Rq * (c.K + 1));
@@ -1604,15 +1606,15 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   TGNX_LAUNCH_CHECK("tgn_emit");
   const LoadEdgeAttr ea{c.e_j, c.e_id, c.e_t, c.lu, c.ev_msg, P + c.L.te_w, P + c.L.te_b, D, d};
   gemm2_launch(gemm_shape(Eq, HC, D + d, GKC, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
-               EpiStore{c.Ep, nullptr, HC, 0}, p0, t0, gemm_shape(Mq, 4 * HC, D, GKC, c.cnt + CNT_M),
+               EpiStore{c.Ep, nullptr, HC, 0}, nullptr, gemm_shape(Mq, 4 * HC, D, GKC, c.cnt + CNT_M),
                LoadZ{c.Z0, c.mem, c.nid, D, 1}, LoadProjW{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
-               EpiProj{P + c.L.bq, P + c.L.bk, P + c.L.bv, P + c.L.bsk, c.P, HC}, p1, t1, s);
+               EpiProj{P + c.L.bq, P + c.L.bk, P + c.L.bv, P + c.L.bsk, c.P, HC}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_edge_proj");
   tgn_attn_fwd<false><<<gridn(Rq, 4, 1 << 20), 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_attn_fwd");
   gemm2_launch(gemm_shape(Rq, D, D, GKC, c.cnt + CNT_R), LoadRowK{c.Zc, Rq, D, D}, LoadRowK{P + c.L.lsw, D, D, D},
-               EpiStore{c.Hs, P + c.L.lsb, D, 0}, p0, t0, gemm_shape(Rq, D, D, GKC, c.cnt + CNT_R),
-               LoadRowK{c.Zc, Rq, D, D}, LoadRowK{P + c.L.ldw, D, D, D}, EpiStore{c.Hd, P + c.L.ldb, D, 0}, p1, t1, s);
+               EpiStore{c.Hs, P + c.L.lsb, D, 0}, nullptr, gemm_shape(Rq, D, D, GKC, c.cnt + CNT_R),
+               LoadRowK{c.Zc, Rq, D, D}, LoadRowK{P + c.L.ldw, D, D, D}, EpiStore{c.Hd, P + c.L.ldb, D, 0}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_lin_src_dst");
   tgn_score<<<k.B, 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_score");

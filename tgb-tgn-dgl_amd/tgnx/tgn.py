@@ -284,6 +284,77 @@ class TgnEngine:
         self._keep = negs
         return self.out_pos[:B], self.out_neg[:B * Kn].view(B, Kn), self.mrr[:B]
 
+    # ------------------------------------------------------------------ resident (graph-capturable)
+    def bind_resident(self, split_lo: int, split_hi: int, batch: int, dropout: bool = True):
+        """Consecutive batches of `batch` events over [split_lo, split_hi), negatives drawn on the
+        device; the batch cursor lives in the control block (no host arguments change per step)."""
+        self._res = (int(split_lo), int(split_hi), int(batch))
+        self._res_drop = 1 if dropout else 0
+        self._res_buf = self._buffers(_p(self.neg_train))
+        L = _lib.lib()
+        self._f = (L.tgnx_tgnn_advance, L.tgnx_tgn_train_fwd_bwd, L.tgnx_tgn_train_update)
+        self._cfg_ref, self._buf_ref = ctypes.byref(self.cfg), ctypes.byref(self._res_buf)
+        self._ctl_p = ctypes.c_void_p(self.ctl.data_ptr())
+
+    def begin_epoch(self):
+        """pyg_epoch_utils.py:11-16: memory reset_state + neighbor_loader reset_state; cursor to 0."""
+        self.reset_state()
+        self.ctl[10] = 0
+
+    def _pre(self):
+        adv, fb, _ = self._f
+        lo, hi, batch = self._res
+        st = self._stream()
+        rc = adv(self._ctl_p, 1, 0, 0, 0, lo, hi, batch, self.rank, self.world, self.seed, 1, st)
+        rc |= fb(self._cfg_ref, self._buf_ref, 1, self._res_drop, st)
+        if rc:
+            raise RuntimeError(f"tgnx TGN resident step failed: {_lib.lib().tgnx_last_error().decode()}")
+
+    def _post(self):
+        if self._f[2](self._cfg_ref, self._buf_ref, self._stream()):
+            raise RuntimeError(f"tgnx TGN resident update failed: {_lib.lib().tgnx_last_error().decode()}")
+
+    def _allreduce(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.model.grad_flat)
+
+    def resident_train_step(self):
+        self._pre()
+        self._allreduce()
+        self._post()
+
+    def capture_resident(self):
+        """One resident step as HIP graph(s) (world > 1: the all-reduce stays eager between them)."""
+        torch.cuda.synchronize(self.dev)
+        saved = self.ctl.clone()
+        if self.world == 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._pre()
+                self._post()
+            self._graphs = (g, None)
+        else:
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                self._pre()
+            with torch.cuda.graph(g2):
+                self._post()
+            self._graphs = (g1, g2)
+        torch.cuda.synchronize(self.dev)
+        self.ctl.copy_(saved)
+
+    def replay_resident(self):
+        g1, g2 = self._graphs
+        g1.replay()
+        if g2 is not None:
+            self._allreduce()
+            g2.replay()
+
+    def units(self):
+        """(sum of sampled edges, sum of sampled nodes) since the last reset."""
+        return int(self.ctl[13]), int(self.ctl[14])
+
     def loss_sum(self) -> float:
         return float(self.ctl[12:13].view(torch.float64).item())
 
