@@ -100,6 +100,8 @@ struct Ctx {
   int64_t* xw;
   float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
   float *dZc, *dP, *dE, *dG, *tgp;
+  float *encE, *sinE;  // per sampled edge: cos / sin of the Δt encoding argument [E][D]
+  float *s0m, *s1m;    // per GRU row: (mean over its messages of) sin(arg), sin(arg) Δt  [M][D]
   float *pA, *pB, *pC, *pD;  // split-K partials of the deferred weight-gradient GEMMs
   uint64_t *rkeys, *skeys;
   int *rruns, *sruns;
@@ -313,7 +315,7 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
 // Aggregated message of node n (wave): IdentityMessage [mem[n], mem[other], raw, cos(w (t - lu[n]) + b)]
 // of its stored events, LastAggregator (first max t over [msg_s; msg_d], msg_agg.py:15-21) or
 // MeanAggregator (msg_agg.py:24-26); lu_new = max t (0 without messages, PyG scatter 'max').
-__device__ void agg_node(const Ctx& c, int64_t n, int m, int lane) {
+__device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
   const int D = c.D, d = c.d, Qm = c.Qm;
   const int64_t so = c.st[4 * n], sc = c.st[4 * n + 1], dof = c.st[4 * n + 2], dc = c.st[4 * n + 3];
   const int tot = (int)(sc + dc);
@@ -321,6 +323,8 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane) {
   const float* P = c.params;
   if (tot == 0) {
     for (int k = lane; k < Qm; k += 64) X[k] = 0.f;
+    if (grad)
+      for (int q = lane; q < D; q += 64) c.s0m[(int64_t)m * D + q] = c.s1m[(int64_t)m * D + q] = 0.f;
     if (lane == 0) {
       c.xw[m] = -1;
       c.trel[m] = 0.f;
@@ -351,7 +355,12 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane) {
       else if (k < 2 * D + d) x = c.ev_msg[e * d + (k - 2 * D)];
       else {
         const int q = k - 2 * D - d;
-        x = te_cos(fmaf(P[c.L.te_w + q], tr, P[c.L.te_b + q]));
+        float sn;
+        te_sincos(fmaf(P[c.L.te_w + q], tr, P[c.L.te_b + q]), sn, x);
+        if (grad) {
+          c.s0m[(int64_t)m * D + q] = sn;
+          c.s1m[(int64_t)m * D + q] = sn * tr;
+        }
       }
       X[k] = x;
     }
@@ -363,7 +372,7 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane) {
   } else {
     float tmax = -INFINITY;
     for (int k = lane; k < Qm; k += 64) {
-      float s = 0.f;
+      float s = 0.f, s0 = 0.f, s1 = 0.f;
       for (int q = 0; q < tot; ++q) {  // event order: PyG scatter-sum order, then / count
         const int64_t e = ev_of(q);
         float x;
@@ -372,11 +381,20 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane) {
         else if (k < 2 * D + d) x = c.ev_msg[e * d + (k - 2 * D)];
         else {
           const int qq = k - 2 * D - d;
-          x = te_cos(fmaf(P[c.L.te_w + qq], c.ev_t[e] - lun, P[c.L.te_b + qq]));
+          const float dt = c.ev_t[e] - lun;
+          float sn;
+          te_sincos(fmaf(P[c.L.te_w + qq], dt, P[c.L.te_b + qq]), sn, x);
+          s0 += sn;
+          s1 += sn * dt;
         }
         s += x;
       }
       X[k] = s / (float)tot;
+      if (grad && k >= 2 * D + d) {
+        const int qq = k - 2 * D - d;
+        c.s0m[(int64_t)m * D + qq] = s0 / (float)tot;
+        c.s1m[(int64_t)m * D + qq] = s1 / (float)tot;
+      }
     }
     for (int q = lane; q < tot; q += 64) tmax = fmaxf(tmax, c.ev_t[ev_of(q)]);
     tmax = wave_max(tmax);
@@ -388,11 +406,24 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane) {
   }
 }
 
+// last_update the GRU step gives node u (memory_module.py:175-176): max t over its stored messages, 0
+// without messages (PyG scatter 'max' fill); wave-uniform
+__device__ float store_tmax(const Ctx& c, int64_t u, int lane) {
+  const int64_t so = c.st[4 * u], sc = c.st[4 * u + 1], dof = c.st[4 * u + 2], dc = c.st[4 * u + 3];
+  const int tot = (int)(sc + dc);
+  if (tot == 0) return 0.f;
+  float tb = -INFINITY;
+  for (int k = lane; k < tot; k += 64) tb = fmaxf(tb, c.ev_t[k < sc ? c.arena[so + k] : c.arena[dof + (k - sc)]]);
+  return wave_max(tb);
+}
+
 // K3: blocks [0, nemit): sampled edges, thread per centre (centre-ascending, ring order = e_id
-// descending); the rest: mode 0 aggregation over the sampled nodes (train) + zeroing of the
-// backward accumulators, mode 1 last_update of the sampled nodes from the buffer (eval scoring),
-// mode 2 aggregation over a node list (eval update / flush; list == nullptr: nodes base + m).
-__global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nemit, const int64_t* list,
+// descending); [nemit, nemit + nenc): the Δt encoding of every sampled edge, wave per centre
+// (cos -> the lin_edge operand, sin -> its backward; emb_module.py:69-72, rel_t = last_update[src] - t);
+// the rest: mode 0 aggregation over the sampled nodes (train) + zeroing of the backward
+// accumulators, mode 1 last_update of the sampled nodes from the buffer (eval scoring), mode 2
+// aggregation over a node list (eval update / flush; list == nullptr: nodes base + m).
+__global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nemit, int nenc, const int64_t* list,
                                                     const int* list_cnt, int n_host, int64_t base) {
   if (mode != 2) {
     const int B = (int)c.ctl[TGNX_CTL_B];
@@ -415,8 +446,36 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nemit, 
     }
     return;
   }
-  const int bid = blockIdx.x - nemit, nb = gridDim.x - nemit;
   const int lane = threadIdx.x & 63;
+  if ((int)blockIdx.x < nemit + nenc) {
+    const int R = c.cnt[CNT_R], D = c.D;
+    const float* tw = c.params + c.L.te_w;
+    const float* tb = c.params + c.L.te_b;
+    for (int x = (blockIdx.x - nemit) * 4 + (threadIdx.x >> 6); x < R; x += nenc * 4) {
+      const int64_t v = c.cent[x];
+      int o = c.ceoff[x];
+      for (int j = 0; j < c.K; ++j) {
+        if (c.eid[v * c.K + j] < 0) continue;
+        const int64_t u = c.nbr[v * c.K + j];
+        const float lu = mode == 0 ? store_tmax(c, u, lane) : (float)c.lu_buf[u];
+        const float dt = lu - c.rt[v * c.K + j];
+        for (int q = lane; q < D; q += 64) {
+          const float a = fmaf(tw[q], dt, tb[q]);
+          if (mode == 0) {
+            float sn, cs;
+            te_sincos(a, sn, cs);
+            c.encE[(int64_t)o * D + q] = cs;
+            c.sinE[(int64_t)o * D + q] = sn;
+          } else {
+            c.encE[(int64_t)o * D + q] = te_cos(a);
+          }
+        }
+        ++o;
+      }
+    }
+    return;
+  }
+  const int bid = blockIdx.x - nemit - nenc, nb = gridDim.x - nemit - nenc;
   if (mode == 1) {
     const int M = c.cnt[CNT_M];
     for (int x = bid * blockDim.x + threadIdx.x; x < M; x += nb * blockDim.x) c.lu[x] = (float)c.lu_buf[c.nid[x]];
@@ -432,7 +491,7 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nemit, 
   const int n = mode == 0 ? c.cnt[CNT_M] : (list_cnt ? *list_cnt : n_host);
   for (int m = bid * 4 + (threadIdx.x >> 6); m < n; m += nb * 4) {
     const int64_t v = mode == 0 ? c.nid[m] : (list ? list[m] : base + m);
-    agg_node(c, v, m, lane);
+    agg_node(c, v, m, lane, mode == 0);
   }
 }
 
@@ -470,11 +529,12 @@ struct EpiGru {
   int64_t base;
   int D;
   float *Z0, *gates;
-  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
-    for (int x = threadIdx.x; x < GT * (GT / 4); x += blockDim.x) {
-      const int r = x / (GT / 4), u = x % (GT / 4), m = m0 + r, j = n0 / 4 + u;
-      if (m >= M || 4 * j >= N) continue;
-      const float* row = Ct + r * GPAD + 4 * u;
+  __device__ void operator()(const GemmTile& t) const {
+    const int q4 = t.tn / 4;
+    for (int x = threadIdx.x; x < t.tm * q4; x += blockDim.x) {
+      const int r = x / q4, u = x % q4, m = t.m0 + r, j = t.n0 / 4 + u;
+      if (m >= t.M || 4 * j >= t.N) continue;
+      const float* row = t.c + r * t.pitch + 4 * u;
       const float pr = row[0] + (bih[j] + bhh[j]);
       const float pz = row[1] + (bih[D + j] + bhh[D + j]);
       const float gin = row[2] + bih[2 * D + j];
@@ -492,13 +552,13 @@ struct EpiGru {
 // TransformerConv edge attribute of sampled edge e: [cos(w (lu[src] - t_e) + b) | msg[e_id]]
 // (emb_module.py:69-72, rel_t = last_update[edge_index[0]] - t)
 struct LoadEdgeAttr {
-  const int* e_j;
+  const float* enc;  // cos(w rel_t + b) rows, written by tgn_agg_emit
   const int64_t* e_id;
-  const float *e_t, *lu, *ev_msg, *tw, *tb;
+  const float* ev_msg;
   int D, d;
   static constexpr bool k_fast = true;
   __device__ float operator()(int e, int k) const {
-    if (k < D) return te_cos(fmaf(tw[k], lu[e_j[e]] - e_t[e], tb[k]));
+    if (k < D) return enc[(int64_t)e * D + k];
     return ev_msg[e_id[e] * d + (k - D)];
   }
 };
@@ -532,13 +592,14 @@ struct EpiProj {
   const float *bq, *bk, *bv, *bs;
   float* P;
   int HC;
-  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
-    for (int x = threadIdx.x; x < GT * GT; x += blockDim.x) {
-      const int r = x / GT, cc = x % GT, m = m0 + r, n = n0 + cc;
+  __device__ void operator()(const GemmTile& t) const {
+    const int M = t.M, N = t.N;
+    for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
+      const int r = x / t.tn, cc = x % t.tn, m = t.m0 + r, n = t.n0 + cc;
       if (m >= M || n >= N) continue;
       const int g = n / HC, q = n % HC;
       const float* b = g == 0 ? bq : g == 1 ? bk : g == 2 ? bv : bs;
-      P[(int64_t)m * N + n] = Ct[r * GPAD + cc] + b[q];
+      P[(int64_t)m * N + n] = t(r, cc) + b[q];
     }
   }
 };
@@ -838,12 +899,12 @@ struct EpiProjGrad {
   float* g;
   int64_t wq, bq, wk, bk, wv, bv, ws, bs;
   int HC, D;
-  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
-    for (int x = threadIdx.x; x < GT * GT; x += blockDim.x) {
-      const int r = x / GT, cc = x % GT, row = m0 + r, n = n0 + cc;
-      if (row >= M || n >= N) continue;
+  __device__ void operator()(const GemmTile& t) const {
+    for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
+      const int r = x / t.tn, cc = x % t.tn, row = t.m0 + r, n = t.n0 + cc;
+      if (row >= t.M || n >= t.N) continue;
       const int gi = row / HC, q = row % HC;
-      const float v = Ct[r * GPAD + cc];
+      const float v = t(r, cc);
       const int64_t W = gi == 0 ? wq : gi == 1 ? wk : gi == 2 ? wv : ws;
       const int64_t Bb = gi == 0 ? bq : gi == 1 ? bk : gi == 2 ? bv : bs;
       if (n < D) g[W + (int64_t)q * D + n] = v;
@@ -881,37 +942,77 @@ struct EpiLpGrad {
   float* g;
   int64_t lsw, ldw;
   int D;
-  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
-    for (int x = threadIdx.x; x < GT * GT; x += blockDim.x) {
-      const int r = x / GT, cc = x % GT, row = m0 + r, n = n0 + cc;
-      if (row >= M || n >= N) continue;
-      g[(row < D ? lsw + (int64_t)row * D : ldw + (int64_t)(row - D) * D) + n] = Ct[r * GPAD + cc];
+  __device__ void operator()(const GemmTile& t) const {
+    for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
+      const int r = x / t.tn, cc = x % t.tn, row = t.m0 + r, n = t.n0 + cc;
+      if (row >= t.M || n >= t.N) continue;
+      g[(row < D ? lsw + (int64_t)row * D : ldw + (int64_t)(row - D) * D) + n] = t(r, cc);
     }
   }
 };
-// d(edge attr enc) -> Δt-encoding parameter grads: per 64-row tile, Σ_e darg Δt and Σ_e darg with
-// darg = -g sin(w Δt + b) (Δt = lu[src] - t_e), written to partial rows (summed in fixed order later)
+// Δt-encoding parameter grads from a tile of d(encoding) (dA): per row-tile partials
+//   tgp[row][n] = Σ_r -dA[r][n] S1[r][n],  tgp[row][D + n] = Σ_r -dA[r][n] S0[r][n]
+// (S0 = sin(w Δt + b), S1 = S0 Δt, precomputed), summed in fixed order by TeReduceTail.
+__device__ __forceinline__ void te_tile_grad(const GemmTile& t, const float* S0, const float* S1, float* tgp,
+                                             int D) {
+  const int groups = blockDim.x / t.tn;
+  const int cc = threadIdx.x % t.tn, g = threadIdx.x / t.tn, n = t.n0 + cc;
+  float sw = 0.f, sb = 0.f;
+  if (g < groups && n < t.N)
+    for (int r = g; r < t.tm && t.m0 + r < t.M; r += groups) {
+      const int64_t o = (int64_t)(t.m0 + r) * D + n;
+      const float da = -t(r, cc);
+      sw += da * S1[o];
+      sb += da * S0[o];
+    }
+  float* red = t.scratch;  // [2][groups][tn]
+  if (g < groups) {
+    red[g * t.tn + cc] = sw;
+    red[(groups + g) * t.tn + cc] = sb;
+  }
+  __syncthreads();
+  if (threadIdx.x < t.tn && n < t.N) {
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < groups; ++q) {
+      a += red[q * t.tn + cc];
+      b += red[(groups + q) * t.tn + cc];
+    }
+    tgp[(int64_t)t.tile_row() * 2 * D + n] = a;
+    tgp[(int64_t)t.tile_row() * 2 * D + D + n] = b;
+  }
+}
+// d(edge attr enc) of the sampled edges; S1 = sin Δt formed here from lu / e_t
 struct EpiTeEdge {
   const int* e_j;
-  const float *e_t, *lu, *tw, *tb;
+  const float *e_t, *lu, *sinE;
   float* tgp;
-  int D, row0;
-  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
-    for (int cc = threadIdx.x; cc < GT; cc += blockDim.x) {
-      const int n = n0 + cc;
-      if (n >= N) continue;
-      float sw = 0.f, sb = 0.f;
-      for (int r = 0; r < GT && m0 + r < M; ++r) {
-        const int e = m0 + r;
+  int D;
+  __device__ void operator()(const GemmTile& t) const {
+    const int groups = blockDim.x / t.tn;
+    const int cc = threadIdx.x % t.tn, g = threadIdx.x / t.tn, n = t.n0 + cc;
+    float sw = 0.f, sb = 0.f;
+    if (g < groups && n < t.N)
+      for (int r = g; r < t.tm && t.m0 + r < t.M; r += groups) {
+        const int e = t.m0 + r;
         const float dt = lu[e_j[e]] - e_t[e];
-        float sn, cs;
-        te_sincos(fmaf(tw[n], dt, tb[n]), sn, cs);
-        const float da = -Ct[r * GPAD + cc] * sn;
+        const float da = -t(r, cc) * sinE[(int64_t)e * D + n];
         sw += da * dt;
         sb += da;
       }
-      tgp[(int64_t)(row0 + m0 / GT) * 2 * D + n] = sw;
-      tgp[(int64_t)(row0 + m0 / GT) * 2 * D + D + n] = sb;
+    float* red = t.scratch;
+    if (g < groups) {
+      red[g * t.tn + cc] = sw;
+      red[(groups + g) * t.tn + cc] = sb;
+    }
+    __syncthreads();
+    if (threadIdx.x < t.tn && n < t.N) {
+      float a = 0.f, b = 0.f;
+      for (int q = 0; q < groups; ++q) {
+        a += red[q * t.tn + cc];
+        b += red[(groups + q) * t.tn + cc];
+      }
+      tgp[(int64_t)t.tile_row() * 2 * D + n] = a;
+      tgp[(int64_t)t.tile_row() * 2 * D + D + n] = b;
     }
   }
 };
@@ -933,11 +1034,11 @@ struct EpiGruBwd {
   const int64_t* nid;
   float* dG;
   int D;
-  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
-    for (int x = threadIdx.x; x < GT * GT; x += blockDim.x) {
-      const int r = x / GT, cc = x % GT, m = m0 + r, j = n0 + cc;
-      if (m >= M || j >= N) continue;
-      const float dhp = Ct[r * GPAD + cc];
+  __device__ void operator()(const GemmTile& t) const {
+    for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
+      const int r = x / t.tn, cc = x % t.tn, m = t.m0 + r, j = t.n0 + cc;
+      if (m >= t.M || j >= t.N) continue;
+      const float dhp = t(r, cc);
       const float4 gt = *reinterpret_cast<const float4*>(gates + ((int64_t)m * D + j) * 4);
       const float rr = gt.x, zz = gt.y, nn = gt.z, ghn = gt.w;
       const float h = mem[nid[m] * D + j];
@@ -966,12 +1067,12 @@ struct EpiGruWGrad {
   float* g;
   int64_t wih, whh, bih, bhh;
   int Qm, D;
-  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
-    for (int x = threadIdx.x; x < GT * GT; x += blockDim.x) {
-      const int r = x / GT, cc = x % GT, row = m0 + r, n = n0 + cc;
-      if (row >= M || n >= N) continue;
+  __device__ void operator()(const GemmTile& t) const {
+    for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
+      const int r = x / t.tn, cc = x % t.tn, row = t.m0 + r, n = t.n0 + cc;
+      if (row >= t.M || n >= t.N) continue;
       const int j = row >> 2, gg = row & 3;
-      const float v = Ct[r * GPAD + cc];
+      const float v = t(r, cc);
       if (n < Qm) {
         if (gg < 3) g[wih + (int64_t)(gg * D + j) * Qm + n] = v;
       } else if (n < Qm + D) {
@@ -1000,49 +1101,12 @@ struct LoadGruWencT {
   }
 };
 // message-encoding -> Δt-encoding parameter grads (Last: the winner's Δt; Mean: each stored
-// message's Δt with weight 1 / count), per 64-row tile partials
+// message's Δt with weight 1 / count, folded into s0m / s1m by agg_node), per row-tile partials
 struct EpiTeMsg {
-  Ctx c;
-  int row0;
-  __device__ void operator()(const float* Ct, int m0, int n0, int M, int N) const {
-    const float* tw = c.params + c.L.te_w;
-    const float* tb = c.params + c.L.te_b;
-    const int D = c.D;
-    for (int cc = threadIdx.x; cc < GT; cc += blockDim.x) {
-      const int n = n0 + cc;
-      if (n >= N) continue;
-      float sw = 0.f, sb = 0.f;
-      for (int r = 0; r < GT && m0 + r < M; ++r) {
-        const int m = m0 + r;
-        if (c.xw[m] < 0) continue;
-        const float g = Ct[r * GPAD + cc];
-        if (c.aggr == 0) {
-          const float dt = c.trel[m];
-          float sn, cs;
-          te_sincos(fmaf(tw[n], dt, tb[n]), sn, cs);
-          const float da = -g * sn;
-          sw += da * dt;
-          sb += da;
-        } else {
-          const int64_t v = c.nid[m];
-          const int64_t so = c.st[4 * v], sc = c.st[4 * v + 1], dof = c.st[4 * v + 2], dc = c.st[4 * v + 3];
-          const float lun = (float)c.lu_buf[v];
-          const float gm = g / (float)(sc + dc);
-          for (int q = 0; q < sc + dc; ++q) {
-            const int64_t e = q < sc ? c.arena[so + q] : c.arena[dof + (q - sc)];
-            const float dt = c.ev_t[e] - lun;
-            float sn, cs;
-            te_sincos(fmaf(tw[n], dt, tb[n]), sn, cs);
-            const float da = -gm * sn;
-            sw += da * dt;
-            sb += da;
-          }
-        }
-      }
-      c.tgp[(int64_t)(row0 + m0 / GT) * 2 * D + n] = sw;
-      c.tgp[(int64_t)(row0 + m0 / GT) * 2 * D + D + n] = sb;
-    }
-  }
+  const float *s0m, *s1m;
+  float* tgp;
+  int D, row0;
+  __device__ void operator()(const GemmTile& t) const { te_tile_grad(t, s0m, s1m, tgp + (int64_t)row0 * 2 * D, D); }
 };
 
 // Δt-encoding grads: fixed-order sum of the partial rows into grads (before any all-reduce); rides
@@ -1056,7 +1120,7 @@ struct TeReduceTail {
     if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
     const int D = c.D;
     const int E = c.cnt[CNT_E], M = c.cnt[CNT_M];
-    const int re = min(rows_edge, (E + GT - 1) / GT), rm = min(rows_msg, (M + GT - 1) / GT);
+    const int re = min(rows_edge, (E + G32::TM - 1) / G32::TM), rm = min(rows_msg, (M + G32::TM - 1) / G32::TM);
     for (int x = threadIdx.x; x < 2 * D; x += blockDim.x) {
       float s = 0.f;
       for (int r = 0; r < re; ++r) s += c.tgp[(int64_t)r * 2 * D + x];
@@ -1245,13 +1309,14 @@ static Caps make_caps(const tgnx_tgn_config* cfg) {
   return k;
 }
 // the deferred (split-K) weight-gradient GEMMs of a train step
-static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split(k.HC, k.D + k.d, k.Etr, GKC, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, 32); }
-static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_split(4 * k.HC, k.D + 1, k.Mtr, GKC, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, 16); }
-static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split(2 * k.D, k.D, 3 * k.B, GKC, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, 16); }
-static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split(4 * k.D, k.Qm + k.D + 1, k.Mtr, GKC, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, 16); }
+static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(k.HC, k.D + k.d, k.Etr, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, 8); }
+static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.HC, k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, 4); }
+static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, 5); }
+static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, 4); }
 struct WsLay {
   size_t cb, nb, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
-      Ep, alpha, Zc, evs, Hs, Hd, dZc, dP, dE, dG, tgp, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, total;
+      Ep, alpha, Zc, evs, Hs, Hd, dZc, dP, dE, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
+      total;
   int tgp_rows;
 };
 static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
@@ -1290,8 +1355,12 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.dP = carve(off, (size_t)k.Mtr * 4 * HC * 4);
   W.dE = carve(off, (size_t)k.Etr * HC * 4);
   W.dG = carve(off, (size_t)k.Mtr * 4 * D * 4);
-  W.tgp_rows = (k.Etr + GT - 1) / GT + (k.Mtr + GT - 1) / GT;
+  W.tgp_rows = (k.Etr + G32::TM - 1) / G32::TM + (k.Mtr + G32::TM - 1) / G32::TM;
   W.tgp = carve(off, (size_t)W.tgp_rows * 2 * D * 4);
+  W.encE = carve(off, (size_t)k.Ecap * D * 4);
+  W.sinE = carve(off, (size_t)k.Etr * D * 4);
+  W.s0m = carve(off, (size_t)k.Mtr * D * 4);
+  W.s1m = carve(off, (size_t)k.Mtr * D * 4);
   W.pA = carve(off, gemm_partial_floats(shp_dWe(k, nullptr)) * 4);
   W.pB = carve(off, gemm_partial_floats(shp_dWp(k, nullptr)) * 4);
   W.pC = carve(off, gemm_partial_floats(shp_dWlp(k, nullptr)) * 4);
@@ -1403,6 +1472,10 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.dE = reinterpret_cast<float*>(ws + W.dE);
   c.dG = reinterpret_cast<float*>(ws + W.dG);
   c.tgp = reinterpret_cast<float*>(ws + W.tgp);
+  c.encE = reinterpret_cast<float*>(ws + W.encE);
+  c.sinE = reinterpret_cast<float*>(ws + W.sinE);
+  c.s0m = reinterpret_cast<float*>(ws + W.s0m);
+  c.s1m = reinterpret_cast<float*>(ws + W.s1m);
   c.pA = reinterpret_cast<float*>(ws + W.pA);
   c.pB = reinterpret_cast<float*>(ws + W.pB);
   c.pC = reinterpret_cast<float*>(ws + W.pC);
@@ -1432,9 +1505,9 @@ static inline int gridn(int64_t n, int per, int cap = 4096) {
 static void gru_list(const Ctx& c, const Caps& k, const int64_t* list, const int* list_cnt, int n_host, int64_t base,
                      int mcap, hipStream_t s) {
   const float* P = c.params;
-  tgn_agg_emit<<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
-  const GemmShape g1 = gemm_shape(mcap, 4 * c.D, c.Qm + c.D, GKC, list_cnt);
-  gemm_launch(g1, LoadGruA{c.X, c.mem, list, base, c.Qm, c.D}, LoadGruW{P + c.L.w_ih, P + c.L.w_hh, c.Qm, c.D},
+  tgn_agg_emit<<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, 0, list, list_cnt, n_host, base);
+  const GemmShape g1 = gemm_shape<G32>(mcap, 4 * c.D, c.Qm + c.D, list_cnt);
+  gemm_launch<G32>(g1, LoadGruA{c.X, c.mem, list, base, c.Qm, c.D}, LoadGruW{P + c.L.w_ih, P + c.L.w_hh, c.Qm, c.D},
               EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, list, base, c.D, c.Z0, c.gates}, nullptr, s);
 }
 
@@ -1500,22 +1573,22 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   tgn_scan<true><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
   probe_end(TGNX_K_ASSEMBLE, s);
   TGNX_LAUNCH_CHECK("tgn_scan");
-  const int nemit = gridn(k.Rtr, 256);
+  const int nemit = gridn(k.Rtr, 256), nenc = gridn(k.Rtr, 4, 2048);
   probe_begin(TGNX_K_EDGE_META, s);
-  tgn_agg_emit<<<nemit + gridn(k.Mtr, 4, 2048), 256, 0, s>>>(c, 0, nemit, nullptr, nullptr, 0, 0);
+  tgn_agg_emit<<<nemit + nenc + gridn(k.Mtr, 4, 2048), 256, 0, s>>>(c, 0, nemit, nenc, nullptr, nullptr, 0, 0);
   probe_end(TGNX_K_EDGE_META, s);
   TGNX_LAUNCH_CHECK("tgn_agg_emit");
   // GRU over every sampled node ‖ lin_edge over every sampled edge
-  const LoadEdgeAttr ea{c.e_j, c.e_id, c.e_t, c.lu, c.ev_msg, P + c.L.te_w, P + c.L.te_b, D, d};
+  const LoadEdgeAttr ea{c.encE, c.e_id, c.ev_msg, D, d};
   probe_begin(TGNX_K_EDGE_FWD, s);
-  gemm2_launch(gemm_shape(k.Mtr, 4 * D, Qm + D, GKC, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D},
+  gemm2_launch<G32, G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D},
                LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
                EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, nullptr,
-               gemm_shape(k.Etr, HC, D + d, GKC, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
+               gemm_shape<G32>(k.Etr, HC, D + d, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
                EpiStore{c.Ep, nullptr, HC, 0}, nullptr, s);
   probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgn_gru_edge");
-  gemm_launch(gemm_shape(k.Mtr, 4 * HC, D, GKC, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
+  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
               LoadProjW{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
               EpiProj{P + c.L.bq, P + c.L.bk, P + c.L.bv, P + c.L.bsk, c.P, HC}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_proj");
@@ -1538,27 +1611,27 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D};
   const EpiGruWGrad e_dWg{G, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, Qm, D};
   probe_begin(TGNX_K_EDGE_BWD, s);
-  gemm2_launch(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, e_dWe, c.pA, shp_dWp(k, c.cnt),
+  gemm2_launch<G32, G32>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, e_dWe, c.pA, shp_dWp(k, c.cnt),
                LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, e_dWp, c.pB, s);
   probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad1");
-  const int rows_edge = (k.Etr + GT - 1) / GT, rows_msg = (k.Mtr + GT - 1) / GT;
-  gemm2_launch(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)}, LoadLpB{c.evs, c.ctl, D, evs_stride(D)},
-               e_dWlp, c.pC, gemm_shape(k.Etr, D, HC, GKC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
-               LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, P + c.L.te_w, P + c.L.te_b, c.tgp, D, 0},
+  const int rows_edge = (k.Etr + G32::TM - 1) / G32::TM, rows_msg = (k.Mtr + G32::TM - 1) / G32::TM;
+  gemm2_launch<G32, G32>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)}, LoadLpB{c.evs, c.ctl, D, evs_stride(D)},
+               e_dWlp, c.pC, gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
+               LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
                nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad2");
-  gemm_launch(gemm_shape(k.Mtr, D, 4 * HC, GKC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
+  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
               LoadProjWT{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
               EpiGruBwd{c.gates, c.mem, c.nid, c.dG, D}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_dz0");
-  gemm2_launch(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, e_dWg,
-               c.pD, gemm_shape(k.Mtr, D, 4 * D, GKC, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
-               LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c, rows_edge}, nullptr, s);
+  gemm2_launch<G32, G32>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, e_dWg,
+               c.pD, gemm_shape<G32>(k.Mtr, D, 4 * D, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
+               LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
-  gemm_fixup_launch(1, TeReduceTail{c, rows_edge, rows_msg}, s, GemmFix<EpiStore>{shp_dWe(k, c.cnt), c.pA, e_dWe},
-                    GemmFix<EpiProjGrad>{shp_dWp(k, c.cnt), c.pB, e_dWp}, GemmFix<EpiLpGrad>{shp_dWlp(k, c.cnt), c.pC, e_dWlp},
-                    GemmFix<EpiGruWGrad>{shp_dWg(k, c.cnt), c.pD, e_dWg});
+  gemm_fixup_launch(1, TeReduceTail{c, rows_edge, rows_msg}, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
+                    gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
+                    gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg));
   TGNX_LAUNCH_CHECK("tgn_wgrad_fixup");
   // update_state (train order: memory of src ∪ dst from this step's GRU rows, then the stores), insert
   const int nmem = gridn(k.Ucap, 4, 1024), nst = gridn(2 * k.B, 256), nring = gridn(2 * k.B, 4);
@@ -1601,19 +1674,19 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   TGNX_LAUNCH_CHECK("tgn_mark");
   tgn_scan<false><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_scan");
-  const int nemit = gridn(Rq, 256);
-  tgn_agg_emit<<<nemit + gridn(Mq, 256), 256, 0, s>>>(c, 1, nemit, nullptr, nullptr, 0, 0);
+  const int nemit = gridn(Rq, 256), nenc = gridn(Rq, 4, 4096);
+  tgn_agg_emit<<<nemit + nenc + gridn(Mq, 256), 256, 0, s>>>(c, 1, nemit, nenc, nullptr, nullptr, 0, 0);
   TGNX_LAUNCH_CHECK("tgn_emit");
-  const LoadEdgeAttr ea{c.e_j, c.e_id, c.e_t, c.lu, c.ev_msg, P + c.L.te_w, P + c.L.te_b, D, d};
-  gemm2_launch(gemm_shape(Eq, HC, D + d, GKC, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
-               EpiStore{c.Ep, nullptr, HC, 0}, nullptr, gemm_shape(Mq, 4 * HC, D, GKC, c.cnt + CNT_M),
+  const LoadEdgeAttr ea{c.encE, c.e_id, c.ev_msg, D, d};
+  gemm2_launch<G32, G32>(gemm_shape<G32>(Eq, HC, D + d, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
+               EpiStore{c.Ep, nullptr, HC, 0}, nullptr, gemm_shape<G32>(Mq, 4 * HC, D, c.cnt + CNT_M),
                LoadZ{c.Z0, c.mem, c.nid, D, 1}, LoadProjW{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
                EpiProj{P + c.L.bq, P + c.L.bk, P + c.L.bv, P + c.L.bsk, c.P, HC}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_edge_proj");
   tgn_attn_fwd<false><<<gridn(Rq, 4, 1 << 20), 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_attn_fwd");
-  gemm2_launch(gemm_shape(Rq, D, D, GKC, c.cnt + CNT_R), LoadRowK{c.Zc, Rq, D, D}, LoadRowK{P + c.L.lsw, D, D, D},
-               EpiStore{c.Hs, P + c.L.lsb, D, 0}, nullptr, gemm_shape(Rq, D, D, GKC, c.cnt + CNT_R),
+  gemm2_launch<G32, G32>(gemm_shape<G32>(Rq, D, D, c.cnt + CNT_R), LoadRowK{c.Zc, Rq, D, D}, LoadRowK{P + c.L.lsw, D, D, D},
+               EpiStore{c.Hs, P + c.L.lsb, D, 0}, nullptr, gemm_shape<G32>(Rq, D, D, c.cnt + CNT_R),
                LoadRowK{c.Zc, Rq, D, D}, LoadRowK{P + c.L.ldw, D, D, D}, EpiStore{c.Hd, P + c.L.ldb, D, 0}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_lin_src_dst");
   tgn_score<<<k.B, 256, 0, s>>>(c);
