@@ -17,6 +17,7 @@
 //     kernel boundary that orders the partials here.
 #pragma once
 #include "tgnx_common.h"
+#include <type_traits>
 
 namespace tgnx {
 
@@ -25,14 +26,18 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 template <int TM_, int TN_, int KC_>
 struct GemmCfg {
   static constexpr int TM = TM_, TN = TN_, KC = KC_;
-  static constexpr int FM = TM / 32, FN = TN / 32;      // 16x16 MFMA tiles per wave (2x2 waves)
-  static constexpr int PA = TM + 1, PB = TN + 1;         // LDS pitches (conflict-free stash)
+  static constexpr int FM = TM / 32, FN = TN / 32;  // 16x16 MFMA tiles per wave (2x2 waves)
+  static constexpr int PK = KC + 4;                  // LDS row pitch of the k-contiguous operand rows
+  static constexpr int PB = TN + 1;                  // LDS pitch of the C tile
   static constexpr int LA = TM * KC / 256, LB = TN * KC / 256;  // operand elements per thread per chunk
-  static constexpr int SMEM = KC * (PA + PB);            // floats (operands; the C tile reuses them)
-  static_assert(TM % 32 == 0 && TN % 32 == 0 && (TM * KC) % 256 == 0 && (TN * KC) % 256 == 0, "tile");
+  static constexpr int SMEM = (TM + TN) * PK;        // floats (operands; the C tile reuses them)
+  static_assert(TM % 32 == 0 && TN % 32 == 0 && KC % 16 == 0 && LA % 4 == 0 && LB % 4 == 0, "tile");
   static_assert(TM * (TN + 1) + 512 <= SMEM, "C tile + epilogue scratch must fit the operand LDS");
 };
-using G32 = GemmCfg<32, 32, 128>;  // the TGN step's GEMMs
+#ifndef TGNX_G32_KC
+#define TGNX_G32_KC 128
+#endif
+using G32 = GemmCfg<32, 32, TGNX_G32_KC>;  // the TGN step's GEMMs
 using G64 = GemmCfg<64, 64, 64>;   // large-M GEMMs (eval scoring)
 
 struct GemmShape {
@@ -74,14 +79,21 @@ inline size_t gemm_partial_floats(const GemmShape& g) {
 // bounds), plus `static constexpr bool k_fast` (true when consecutive k are consecutive in memory)
 // to pick the coalesced thread -> element mapping.
 //
-// Epilogue concept: `void operator()(const GemmTile& t) const`, run by all 256 threads of the
-// workgroup; t(r, cc) is C[m0 + r][n0 + cc] for r < tm, cc < tn, M / N the runtime bounds.
+// Epilogue concept: `template <class T> void operator()(const T& t) const` with T a GemmTile<TM, TN>,
+// run by all 256 threads of the workgroup; t(r, cc) is C[m0 + r][n0 + cc] for r < tm, cc < tn, M / N
+// the runtime bounds.  The tile shape is compile-time so epilogues can issue every gather of the
+// tile before their first store (the compiler cannot hoist loads over stores that may alias).
+template <int TM_, int TN_>
 struct GemmTile {
+  static constexpr int tm = TM_, tn = TN_, pitch = TN_ + 1, per = TM_ * TN_ / 256;  // elements per thread
   const float* c;
-  int pitch, tm, tn, m0, n0, M, N;
+  int m0, n0, M, N;
   float* scratch;  // >= 512 floats of LDS past the tile, free for the epilogue
   __device__ float operator()(int r, int cc) const { return c[r * pitch + cc]; }
   __device__ int tile_row() const { return m0 / tm; }
+  // element i of this thread: tile row / column
+  __device__ static int row_of(int i) { return (threadIdx.x + 256 * i) / tn; }
+  __device__ static int col_of(int i) { return (threadIdx.x + 256 * i) % tn; }
 };
 
 // Row-major operand: element (r, k) at p[r * ld + k]  (k_fast)
@@ -113,11 +125,19 @@ __device__ __forceinline__ GemmRt gemm_runtime(const GemmShape& g) {
   return r;
 }
 
-// element mapping of a chunk load: thread tid, item i -> (row r, chunk column kk)
+// element mapping of a chunk load: thread tid, item i -> (row r, chunk column kk).  k-fast operands:
+// consecutive threads take consecutive k (coalesced loads, conflict-free b32 LDS stores); r-fast
+// operands: consecutive threads take consecutive rows and each thread 4 consecutive k (coalesced
+// loads per k, one b128 LDS store).
 template <bool KFAST, int ROWS, int KC>
 __device__ __forceinline__ void gemm_map(int tid, int i, int& r, int& kk) {
-  const int x = tid + 256 * i;
-  if (KFAST) { r = x / KC; kk = x % KC; } else { r = x % ROWS; kk = x / ROWS; }
+  if (KFAST) {
+    const int x = tid + 256 * i;
+    r = x / KC; kk = x % KC;
+  } else {
+    const int x = tid + 256 * (i >> 2);
+    r = x % ROWS; kk = 4 * (x / ROWS) + (i & 3);
+  }
 }
 
 // One workgroup of a GEMM (`bid` in [0, gemm_blocks(g))); `smem` holds CFG::SMEM floats.
@@ -126,9 +146,9 @@ template <class CFG, class AL, class BL, class EPI>
 __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, const BL& bl, const EPI& epi, float* part,
                                           int bid, float* smem) {
   constexpr int TM = CFG::TM, TN = CFG::TN, KC = CFG::KC, FM = CFG::FM, FN = CFG::FN;
-  constexpr int PA = CFG::PA, PB = CFG::PB, LA = CFG::LA, LB = CFG::LB;
-  float* As = smem;            // [KC][PA]
-  float* Bs = smem + KC * PA;  // [KC][PB]
+  constexpr int PK = CFG::PK, PB = CFG::PB, LA = CFG::LA, LB = CFG::LB;
+  float* As = smem;            // [TM][PK]: row m, k contiguous
+  float* Bs = smem + TM * PK;  // [TN][PK]: row n, k contiguous
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const GemmRt rt = gemm_runtime<CFG>(g);
   const int tiles = g.tiles_m * g.tiles_n;
@@ -159,38 +179,58 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
       rb[i] = (kk < kc && n0 + r < rt.Nr) ? bl(n0 + r, k0 + kk) : 0.f;
     }
   };
+  auto stash1 = [&](float* S, const float* rv, auto kfast, auto rows, auto cnt) {
+    constexpr int ROWS = decltype(rows)::value, CNT = decltype(cnt)::value;
+    if constexpr (decltype(kfast)::value) {
+#pragma unroll
+      for (int i = 0; i < CNT; ++i) {
+        int r, kk;
+        gemm_map<true, ROWS, KC>(tid, i, r, kk);
+        S[r * PK + kk] = rv[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < CNT; i += 4) {
+        int r, kk;
+        gemm_map<false, ROWS, KC>(tid, i, r, kk);
+        *reinterpret_cast<f32x4_t*>(S + r * PK + kk) = f32x4_t{rv[i], rv[i + 1], rv[i + 2], rv[i + 3]};
+      }
+    }
+  };
   auto stash = [&]() {
+    stash1(As, ra, std::integral_constant<bool, AL::k_fast>{}, std::integral_constant<int, TM>{},
+           std::integral_constant<int, LA>{});
+    stash1(Bs, rb, std::integral_constant<bool, BL::k_fast>{}, std::integral_constant<int, TN>{},
+           std::integral_constant<int, LB>{});
+  };
+  // k permutation inside a 16-deep slab: MFMA step q of lane (li, lk) takes k = 4 lk + q, so each
+  // lane's operands for 4 steps are one b128 LDS read (same permutation for A and B)
+  auto slab = [&](int kk, f32x4_t* a, f32x4_t* b) {
 #pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      int r, kk;
-      gemm_map<AL::k_fast, TM, KC>(tid, i, r, kk);
-      As[kk * PA + r] = ra[i];
-    }
+    for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const f32x4_t*>(As + (wr + 16 * i + li) * PK + kk + 4 * lk);
 #pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      int r, kk;
-      gemm_map<BL::k_fast, TN, KC>(tid, i, r, kk);
-      Bs[kk * PB + r] = rb[i];
-    }
+    for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const f32x4_t*>(Bs + (wc + 16 * j + li) * PK + kk + 4 * lk);
   };
   const int last = max(rt.nchunk, 1);
   fetch(s);
   stash();
   __syncthreads();
   for (int ch = s; ch < last; ch += g.S) {
-    const int kc = max(0, min(KC, rt.Kr - ch * KC));
     const bool more = ch + g.S < last;
     if (more) fetch(ch + g.S);  // next chunk in flight during this chunk's MFMAs
-    for (int kk = 0; kk < kc; kk += 4) {
-      float a[FM], b[FN];
+    f32x4_t a[2][FM], b[2][FN];
+    slab(0, a[0], b[0]);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = As[(kk + lk) * PA + wr + 16 * i + li];
+    for (int it = 0; it < KC / 16; ++it) {
+      const int cur = it & 1;
+      if (it + 1 < KC / 16) slab(16 * (it + 1), a[cur ^ 1], b[cur ^ 1]);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = Bs[(kk + lk) * PB + wc + 16 * j + li];
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][i][q], b[cur][j][q], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
     if (more) {
@@ -214,7 +254,7 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
 #pragma unroll
       for (int r = 0; r < 4; ++r) Ct[(wr + 16 * i + lk * 4 + r) * PB + wc + 16 * j + li] = acc[i][j][r];
   __syncthreads();
-  epi(GemmTile{Ct, PB, TM, TN, m0, n0, rt.Mr, rt.Nr, smem + TM * PB});
+  epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, smem + TM * PB});
 }
 
 template <class CFG, class AL, class BL, class EPI>
@@ -269,7 +309,7 @@ __device__ void gemm_fix_tile(const GemmFix<CFG, EPI>& f, int tile, float* smem)
       for (int r = 0; r < 4; ++r) Ct[(wr + 16 * i + lk * 4 + r) * PB + wc + 16 * j + li] = sum[r];
     }
   __syncthreads();
-  f.epi(GemmTile{Ct, PB, TM, TN, m0, n0, rt.Mr, rt.Nr, smem + TM * PB});
+  f.epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, smem + TM * PB});
 }
 template <class CFG, class EPI>
 __device__ __forceinline__ bool gemm_fix_dispatch(const GemmFix<CFG, EPI>& f, int& bid, float* smem) {
@@ -303,14 +343,19 @@ struct EpiStore {
   float* C;
   const float* bias;
   int ldc, accumulate;
-  __device__ void operator()(const GemmTile& t) const {
-    for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
-      const int r = x / t.tn, cc = x % t.tn, m = t.m0 + r, n = t.n0 + cc;
-      if (m < t.M && n < t.N) {
-        float v = t(r, cc) + (bias ? bias[n] : 0.f);
-        float* o = C + (int64_t)m * ldc + n;
-        *o = accumulate ? *o + v : v;
-      }
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    float v[T::per];
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) {
+      const int r = T::row_of(i), cc = T::col_of(i), m = t.m0 + r, n = t.n0 + cc;
+      const bool ok = m < t.M && n < t.N;
+      v[i] = t(r, cc) + ((ok && bias) ? bias[n] : 0.f) + ((ok && accumulate) ? C[(int64_t)m * ldc + n] : 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) {
+      const int r = T::row_of(i), cc = T::col_of(i), m = t.m0 + r, n = t.n0 + cc;
+      if (m < t.M && n < t.N) C[(int64_t)m * ldc + n] = v[i];
     }
   }
 };

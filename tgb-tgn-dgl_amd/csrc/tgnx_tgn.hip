@@ -90,6 +90,7 @@ struct Ctx {
   double* mrr;
   // workspace
   uint32_t *cb, *nb;
+  int* kval;  // [N] valid ring slots of a centre (written by tgn_mark for this batch's centres)
   int* cnt;
   int64_t *cent, *nid, *upd;
   int *cent_loc, *ceoff, *crank, *upd_loc;
@@ -115,7 +116,8 @@ __device__ __forceinline__ float softplusf(float x) { return fmaxf(x, 0.f) + log
 // ------------------------------------------------------------------ sampling (neighbor_loader.py:26-50)
 // K1: every query entry marks its node as a centre and its node + valid ring neighbours as sampled;
 // train negatives are drawn here (NegLinkSamplerDest, counter-based stream as in tgnx_tgnn);
-// src / pos nodes are stamped for the update list (memory_module.py:129).
+// src / pos nodes are stamped for the update list (memory_module.py:129).  16 lanes per entry, one
+// ring slot each (all slot loads in flight at once); the entry's valid-slot count goes to kval[v].
 template <bool TRAIN>
 __global__ void tgn_mark(Ctx c) {
   const int B = (int)c.ctl[TGNX_CTL_B];
@@ -124,14 +126,14 @@ __global__ void tgn_mark(Ctx c) {
   const int gen = (int)c.ctl[TGNX_CTL_GEN];
   const int Kn = TRAIN ? 1 : c.Kn;
   const int nq = B * (2 + Kn);
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+  const int sl = threadIdx.x & 15, grp = (threadIdx.x & 63) >> 4;
+  const int gstride = (gridDim.x * blockDim.x) >> 4;
+  for (int q = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; q < nq; q += gstride) {
     int64_t v;
     if (q < B) {
       v = c.ev_src[start + q];
-      c.node_gen[v] = gen;
     } else if (q < 2 * B) {
       v = c.ev_dst[start + q - B];
-      c.node_gen[v] = gen;
     } else if (TRAIN) {
       const int i = q - 2 * B;
       if (c.gen_neg) {
@@ -144,7 +146,7 @@ __global__ void tgn_mark(Ctx c) {
           v = c.dst_nodes[(uint64_t)(((__uint128_t)(h >> 11) * (uint64_t)c.n_dst) >> 53)];
           if (v != pd) break;
         }
-        c.neg[start + i] = v;
+        if (sl == 0) c.neg[start + i] = v;
       } else {
         v = c.neg[start + i];
       }
@@ -152,13 +154,21 @@ __global__ void tgn_mark(Ctx c) {
       const int x = q - 2 * B;
       v = c.neg[(start + x / Kn) * Kn + x % Kn];
     }
-    atomicOr(&c.cb[v >> 5], 1u << (v & 31));
-    atomicOr(&c.nb[v >> 5], 1u << (v & 31));
-    for (int j = 0; j < c.K; ++j) {
-      if (c.eid[v * c.K + j] >= 0) {
+    int k = 0;
+    for (int j0 = 0; j0 < c.K; j0 += 16) {
+      const int j = j0 + sl;
+      const bool ok = j < c.K && c.eid[v * c.K + j] >= 0;
+      if (ok) {  // plain read first: hub words are hit by many lanes, most find the bit set
         const int64_t u = c.nbr[v * c.K + j];
-        atomicOr(&c.nb[u >> 5], 1u << (u & 31));
+        if (!(c.nb[u >> 5] & (1u << (u & 31)))) atomicOr(&c.nb[u >> 5], 1u << (u & 31));
       }
+      k += __popcll((__ballot(ok) >> (16 * grp)) & 0xFFFFull);
+    }
+    if (sl == 0) {
+      if (q < 2 * B) c.node_gen[v] = gen;
+      c.kval[v] = k;
+      if (!(c.cb[v >> 5] & (1u << (v & 31)))) atomicOr(&c.cb[v >> 5], 1u << (v & 31));
+      if (!(c.nb[v >> 5] & (1u << (v & 31)))) atomicOr(&c.nb[v >> 5], 1u << (v & 31));
     }
   }
 }
@@ -232,53 +242,27 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
   const int gen = (int)c.ctl[TGNX_CTL_GEN];
   const int64_t W = c.words;
   const int64_t wc = (W + T - 1) / T, w0 = tid * wc, w1 = min(W, w0 + wc);
-  // centres: count, ring slots, update nodes
-  int nc = 0, ne = 0, nu = 0;
+  // pass 1: centres (sorted) and sampled nodes (sorted, + assoc) from the bitmaps; no other loads
+  int nc = 0, np = 0;
   for (int64_t w = w0; w < w1; ++w) {
-    uint32_t m = c.cb[w];
-    while (m) {
-      const int b = __ffs(m) - 1;
-      m &= m - 1;
-      const int64_t v = (w << 5) + b;
-      ++nc;
-      for (int j = 0; j < c.K; ++j) ne += c.eid[v * c.K + j] >= 0;
-      nu += c.node_gen[v] == gen;
-    }
+    nc += __popc(c.cb[w]);
+    np += __popc(c.nb[w]);
   }
-  int R, E, U;
+  int R, M;
   int rc = block_excl_scan(nc, sh, &R);
-  int re = block_excl_scan(ne, sh, &E);
-  int ru = block_excl_scan(nu, sh, &U);
-  const bool fits_c = R <= c.Rcap && E <= c.Ecap && U <= c.Ucap;
+  int rank = block_excl_scan(np, sh, &M);
+  const bool fits = R <= c.Rcap && M <= c.Mcap;
   for (int64_t w = w0; w < w1; ++w) {
     uint32_t m = c.cb[w];
-    if (!m) continue;
-    c.cb[w] = 0u;
+    if (m) c.cb[w] = 0u;
     while (m) {
       const int b = __ffs(m) - 1;
       m &= m - 1;
-      const int64_t v = (w << 5) + b;
-      int k = 0;
-      for (int j = 0; j < c.K; ++j) k += c.eid[v * c.K + j] >= 0;
-      if (fits_c) {
-        c.cent[rc] = v;
-        c.ceoff[rc] = re;
-        if (c.node_gen[v] == gen) c.upd[ru++] = v;
-      }
+      if (fits) c.cent[rc] = (w << 5) + b;
       ++rc;
-      re += k;
     }
-  }
-  // sampled nodes
-  int np = 0;
-  for (int64_t w = w0; w < w1; ++w) np += __popc(c.nb[w]);
-  int M;
-  int rank = block_excl_scan(np, sh, &M);
-  const bool fits = fits_c && M <= c.Mcap;
-  for (int64_t w = w0; w < w1; ++w) {
-    uint32_t m = c.nb[w];
-    if (!m) continue;
-    c.nb[w] = 0u;
+    m = c.nb[w];
+    if (m) c.nb[w] = 0u;
     while (m) {
       const int b = __ffs(m) - 1;
       m &= m - 1;
@@ -293,13 +277,33 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
     return;
   }
   for (int x = tid; x < M; x += T) c.crank[x] = -1;
+  __threadfence_block();
   __syncthreads();
-  for (int x = tid; x < R; x += T) {
-    const int loc = (int)c.assoc[c.cent[x]];
+  // pass 2: per centre (contiguous chunk per thread) ring-slot count and update stamp -> edge
+  // offsets and the update list (memory_module.py:129 src ∪ dst, sorted)
+  const int xc = (R + T - 1) / T, x0 = min(R, tid * xc), x1 = min(R, x0 + xc);
+  int ne = 0, nu = 0;
+  for (int x = x0; x < x1; ++x) {
+    const int64_t v = c.cent[x];
+    ne += c.kval[v];
+    nu += c.node_gen[v] == gen;
+  }
+  int E, U;
+  int re = block_excl_scan(ne, sh, &E);
+  int ru = block_excl_scan(nu, sh, &U);
+  for (int x = x0; x < x1; ++x) {
+    const int64_t v = c.cent[x];
+    const int loc = (int)c.assoc[v];
+    c.ceoff[x] = re;
+    re += c.kval[v];
     c.cent_loc[x] = loc;
     c.crank[loc] = x;
+    if (c.node_gen[v] == gen) {
+      c.upd[ru] = v;
+      c.upd_loc[ru] = loc;
+      ++ru;
+    }
   }
-  for (int x = tid; x < U; x += T) c.upd_loc[x] = (int)c.assoc[c.upd[x]];
   if (tid == 0) {
     c.ceoff[R] = E;
     c.cnt[CNT_R] = R;
@@ -529,7 +533,8 @@ struct EpiGru {
   int64_t base;
   int D;
   float *Z0, *gates;
-  __device__ void operator()(const GemmTile& t) const {
+  template <class T>
+  __device__ void operator()(const T& t) const {
     const int q4 = t.tn / 4;
     for (int x = threadIdx.x; x < t.tm * q4; x += blockDim.x) {
       const int r = x / q4, u = x % q4, m = t.m0 + r, j = t.n0 / 4 + u;
@@ -592,14 +597,20 @@ struct EpiProj {
   const float *bq, *bk, *bv, *bs;
   float* P;
   int HC;
-  __device__ void operator()(const GemmTile& t) const {
-    const int M = t.M, N = t.N;
-    for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
-      const int r = x / t.tn, cc = x % t.tn, m = t.m0 + r, n = t.n0 + cc;
-      if (m >= M || n >= N) continue;
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    float v[T::per];
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) {
+      const int n = t.n0 + T::col_of(i);
       const int g = n / HC, q = n % HC;
       const float* b = g == 0 ? bq : g == 1 ? bk : g == 2 ? bv : bs;
-      P[(int64_t)m * N + n] = t(r, cc) + b[q];
+      v[i] = t(T::row_of(i), T::col_of(i)) + (n < t.N ? b[q] : 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) {
+      const int m = t.m0 + T::row_of(i), n = t.n0 + T::col_of(i);
+      if (m < t.M && n < t.N) P[(int64_t)m * t.N + n] = v[i];
     }
   }
 };
@@ -899,7 +910,8 @@ struct EpiProjGrad {
   float* g;
   int64_t wq, bq, wk, bk, wv, bv, ws, bs;
   int HC, D;
-  __device__ void operator()(const GemmTile& t) const {
+  template <class T>
+  __device__ void operator()(const T& t) const {
     for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
       const int r = x / t.tn, cc = x % t.tn, row = t.m0 + r, n = t.n0 + cc;
       if (row >= t.M || n >= t.N) continue;
@@ -942,7 +954,8 @@ struct EpiLpGrad {
   float* g;
   int64_t lsw, ldw;
   int D;
-  __device__ void operator()(const GemmTile& t) const {
+  template <class T>
+  __device__ void operator()(const T& t) const {
     for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
       const int r = x / t.tn, cc = x % t.tn, row = t.m0 + r, n = t.n0 + cc;
       if (row >= t.M || n >= t.N) continue;
@@ -953,7 +966,8 @@ struct EpiLpGrad {
 // Δt-encoding parameter grads from a tile of d(encoding) (dA): per row-tile partials
 //   tgp[row][n] = Σ_r -dA[r][n] S1[r][n],  tgp[row][D + n] = Σ_r -dA[r][n] S0[r][n]
 // (S0 = sin(w Δt + b), S1 = S0 Δt, precomputed), summed in fixed order by TeReduceTail.
-__device__ __forceinline__ void te_tile_grad(const GemmTile& t, const float* S0, const float* S1, float* tgp,
+template <class T>
+__device__ __forceinline__ void te_tile_grad(const T& t, const float* S0, const float* S1, float* tgp,
                                              int D) {
   const int groups = blockDim.x / t.tn;
   const int cc = threadIdx.x % t.tn, g = threadIdx.x / t.tn, n = t.n0 + cc;
@@ -987,18 +1001,29 @@ struct EpiTeEdge {
   const float *e_t, *lu, *sinE;
   float* tgp;
   int D;
-  __device__ void operator()(const GemmTile& t) const {
-    const int groups = blockDim.x / t.tn;
-    const int cc = threadIdx.x % t.tn, g = threadIdx.x / t.tn, n = t.n0 + cc;
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    constexpr int groups = 256 / T::tn, per = T::tm / groups;
+    const int cc = threadIdx.x % T::tn, g = threadIdx.x / T::tn, n = t.n0 + cc;
+    int ej[per];
+    float et[per], sn[per], dt[per];
+#pragma unroll
+    for (int i = 0; i < per; ++i) {
+      const int e = t.m0 + g + groups * i;
+      const bool ok = e < t.M && n < t.N;
+      ej[i] = ok ? e_j[e] : 0;
+      et[i] = ok ? e_t[e] : 0.f;
+      sn[i] = ok ? sinE[(int64_t)e * D + n] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < per; ++i) dt[i] = lu[ej[i]] - et[i];
     float sw = 0.f, sb = 0.f;
-    if (g < groups && n < t.N)
-      for (int r = g; r < t.tm && t.m0 + r < t.M; r += groups) {
-        const int e = t.m0 + r;
-        const float dt = lu[e_j[e]] - e_t[e];
-        const float da = -t(r, cc) * sinE[(int64_t)e * D + n];
-        sw += da * dt;
-        sb += da;
-      }
+#pragma unroll
+    for (int i = 0; i < per; ++i) {
+      const float da = -t(g + groups * i, cc) * sn[i];
+      sw += da * dt[i];
+      sb += da;
+    }
     float* red = t.scratch;
     if (g < groups) {
       red[g * t.tn + cc] = sw;
@@ -1034,15 +1059,27 @@ struct EpiGruBwd {
   const int64_t* nid;
   float* dG;
   int D;
-  __device__ void operator()(const GemmTile& t) const {
-    for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
-      const int r = x / t.tn, cc = x % t.tn, m = t.m0 + r, j = t.n0 + cc;
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    int64_t node[T::per];
+    float4 gt[T::per];
+    float h[T::per];
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) {  // gathers first (no stores in between)
+      const int m = t.m0 + T::row_of(i), j = t.n0 + T::col_of(i);
+      const bool ok = m < t.M && j < t.N;
+      node[i] = ok ? nid[m] : 0;
+      gt[i] = ok ? *reinterpret_cast<const float4*>(gates + ((int64_t)m * D + j) * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) h[i] = mem[node[i] * D + t.n0 + T::col_of(i)];
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) {
+      const int r = T::row_of(i), cc = T::col_of(i), m = t.m0 + r, j = t.n0 + cc;
       if (m >= t.M || j >= t.N) continue;
       const float dhp = t(r, cc);
-      const float4 gt = *reinterpret_cast<const float4*>(gates + ((int64_t)m * D + j) * 4);
-      const float rr = gt.x, zz = gt.y, nn = gt.z, ghn = gt.w;
-      const float h = mem[nid[m] * D + j];
-      const float dn = dhp * (1.0f - zz), dz = dhp * (h - nn);
+      const float rr = gt[i].x, zz = gt[i].y, nn = gt[i].z, ghn = gt[i].w;
+      const float dn = dhp * (1.0f - zz), dz = dhp * (h[i] - nn);
       const float dpn = dn * (1.0f - nn * nn);
       const float dr = dpn * ghn;
       float4* o = reinterpret_cast<float4*>(dG + ((int64_t)m * D + j) * 4);
@@ -1067,7 +1104,8 @@ struct EpiGruWGrad {
   float* g;
   int64_t wih, whh, bih, bhh;
   int Qm, D;
-  __device__ void operator()(const GemmTile& t) const {
+  template <class T>
+  __device__ void operator()(const T& t) const {
     for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
       const int r = x / t.tn, cc = x % t.tn, row = t.m0 + r, n = t.n0 + cc;
       if (row >= t.M || n >= t.N) continue;
@@ -1106,7 +1144,8 @@ struct EpiTeMsg {
   const float *s0m, *s1m;
   float* tgp;
   int D, row0;
-  __device__ void operator()(const GemmTile& t) const { te_tile_grad(t, s0m, s1m, tgp + (int64_t)row0 * 2 * D, D); }
+  template <class T>
+  __device__ void operator()(const T& t) const { te_tile_grad(t, s0m, s1m, tgp + (int64_t)row0 * 2 * D, D); }
 };
 
 // Δt-encoding grads: fixed-order sum of the partial rows into grads (before any all-reduce); rides
@@ -1314,7 +1353,7 @@ static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_spli
 static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, 5); }
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, 4); }
 struct WsLay {
-  size_t cb, nb, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
+  size_t cb, nb, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
       Ep, alpha, Zc, evs, Hs, Hd, dZc, dP, dE, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
       total;
   int tgp_rows;
@@ -1326,6 +1365,7 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   const int D = k.D, HC = k.HC;
   W.cb = carve(off, words * 4);
   W.nb = carve(off, words * 4);
+  W.kval = carve(off, (size_t)k.N * 4);
   W.cnt = carve(off, CNT_WORDS * 4);
   W.cent = carve(off, (size_t)k.Rcap * 8);
   W.cent_loc = carve(off, (size_t)k.Rcap * 4);
@@ -1442,6 +1482,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   char* ws = reinterpret_cast<char*>(b->ws);
   c.cb = reinterpret_cast<uint32_t*>(ws + W.cb);
   c.nb = reinterpret_cast<uint32_t*>(ws + W.nb);
+  c.kval = reinterpret_cast<int*>(ws + W.kval);
   c.cnt = reinterpret_cast<int*>(ws + W.cnt);
   c.cent = reinterpret_cast<int64_t*>(ws + W.cent);
   c.cent_loc = reinterpret_cast<int*>(ws + W.cent_loc);
@@ -1567,7 +1608,7 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   const float* P = c.params;
   float* G = c.grads;
   const int D = c.D, HC = c.HC, Qm = c.Qm, d = c.d;
-  tgn_mark<true><<<gridn(3 * k.B, 256), 256, 0, s>>>(c);
+  tgn_mark<true><<<gridn(3 * k.B * 16, 256), 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_mark");
   probe_begin(TGNX_K_ASSEMBLE, s);
   tgn_scan<true><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
@@ -1670,7 +1711,7 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   const int Rq = (int)std::min<int64_t>(c.N, (int64_t)k.B * (2 + Kn));
   const int Mq = (int)std::min<int64_t>(c.N, (int64_t)Rq * (c.K + 1));
   const int Eq = Rq * c.K;
-  tgn_mark<false><<<gridn((int64_t)k.B * (2 + Kn), 256), 256, 0, s>>>(c);
+  tgn_mark<false><<<gridn((int64_t)k.B * (2 + Kn) * 16, 256), 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_mark");
   tgn_scan<false><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_scan");

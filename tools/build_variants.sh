@@ -1,17 +1,21 @@
 #!/bin/bash
-# Build libtgnx.so variants of tgnx_tgnn.hip with extra -D flags for kernel-geometry timing
-# experiments: tools/build_variants.sh name "-DFOO=1 ..." [name "flags"]...  -> build_var/<name>/libtgnx.so
+# Build libtgnx.so variants with extra -D flags for kernel-geometry timing experiments:
+#   tools/build_variants.sh name "-DFOO=1 ..." [name "flags"]...  -> build_var/<name>/libtgnx.so
+# (every csrc/*.hip recompiled with the flags; select one at run time with TGNX_LIB=...)
 set -e
 cd "$(dirname "$0")/../tgb-tgn-dgl_amd"
 make -s -j8
-OTHERS=$(ls build/*.o | grep -v tgnx_tgnn.o)
+rm -rf ../build_var
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   mkdir -p ../build_var/$name
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -Wno-unused-result $flags \
-    -c csrc/tgnx_tgnn.hip -o ../build_var/$name/tgnx_tgnn.o &
+  for src in csrc/*.hip; do
+    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -Wno-unused-result $flags \
+      -c $src -o ../build_var/$name/$(basename $src .hip).o &
+  done
+  cp build/tgnx_host.o ../build_var/$name/
 done
 wait
 for d in ../build_var/*/; do
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $d/libtgnx.so $d/tgnx_tgnn.o $OTHERS
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $d/libtgnx.so $d/*.o
 done
