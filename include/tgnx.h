@@ -256,7 +256,12 @@ typedef struct {
   float *out_pos, *out_neg;       /* train: [B] sigmoid outputs; eval: [B], [B, Kn] */
   double* mrr;                    /* eval: per-event reciprocal ranks of the last batch [B] */
   void* ws;                       /* tgnx_tgn_ws_bytes(cfg), zero-filled once */
+  float* xrows;                   /* data parallel (ctl world > 1): [xcap, TGNX_TGN_ROW(mem_dim)] rows this
+                                     rank's step updated, for the all-gather; NULL at world 1 */
+  int64_t xcap;                   /* >= 2 * ceil(max_batch / world) */
 } tgnx_tgn_buffers;
+/* exchanged memory row: int32 node (-1 = unused slot), int64 last_update (lo, hi words), pad, memory[D] */
+#define TGNX_TGN_ROW(D) ((D) + 4)
 
 int tgnx_tgn_param_layout(const tgnx_tgn_config* cfg, int64_t* offsets /* [TGNX_TGN_NPARAM+1] */);
 size_t tgnx_tgn_ws_bytes(const tgnx_tgn_config* cfg);
@@ -266,9 +271,18 @@ int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf
 /* Train batch, part 1 (the canonical loop pyg_epoch_utils.py:106-137 carries commented out): negatives
  * (gen_neg), sampler, memory(n_id) with the GRU update of every sampled node, embedding,
  * link prediction, BCE, backward; then update_state (memory / last_update of src ∪ dst, message
- * stores) and the ring insert.  Writes grads (+ loss slot). */
+ * stores) and the ring insert.  Writes grads (+ loss slot).
+ * Data parallel (ctl rank / world from tgnx_tgnn_advance): the roots, GRU, embedding, prediction and
+ * loss cover this rank's event slice only (grads are its share of the global-batch mean; sum them
+ * across ranks); message stores and the ring insert replay the whole global batch (replicated);
+ * the memory rows this rank updated are packed into buf->xrows for the all-gather. */
 int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg,
                            int32_t dropout, void* stream);
+/* Data parallel: write the all-gathered rows of every rank (rows [nrows, TGNX_TGN_ROW(mem_dim)], slots
+ * with node -1 skipped) into memory / last_update.  Ranks that updated the same node computed the
+ * same row (same replicated inputs), so the order does not matter. */
+int tgnx_tgn_apply_rows(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, const float* rows, int64_t nrows,
+                        void* stream);
 /* Train batch, part 2: Adam on the (possibly all-reduced) grads, loss sum. */
 int tgnx_tgn_train_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream);
 /* Eval batch (TGB tgbl link prediction): every event's [pos, Kn negatives] scored with the

@@ -266,6 +266,68 @@ def train_step(model: RefTGN, opt, loader, ev_t, ev_msg, src, pos, neg, t, msg):
     return float(loss.detach()), pos_out.detach().view(-1), neg_out.detach().view(-1)
 
 
+def train_step_dp(model: RefTGN, opt, loader, ev_t, ev_msg, src, pos, neg, t, msg, rank: int, world: int):
+    """train_step decomposed over `world` ranks the way the HIP step shards it: rank r
+    takes the events [B r / W, B (r + 1) / W) as roots (memory(n_id), embedding, prediction, its share
+    of the global-batch mean loss); gradients are summed with an all-reduce; the message stores and the
+    ring insert replay the whole global batch on every rank; the GRU rows of the slice's src ∪ dst are
+    exchanged with an all-gather of (node, last_update, memory) and written by every rank.  Returns
+    (global loss, pos_out, neg_out of the slice)."""
+    import torch.distributed as dist
+    B = src.numel()
+    lo, hi = B * rank // world, B * (rank + 1) // world
+    s_src, s_pos, s_neg = src[lo:hi], pos[lo:hi], neg[lo:hi]
+    model.train()
+    opt.zero_grad()
+    n_id = torch.cat([s_src, s_pos, s_neg]).unique()
+    n_id, ei, e_id, _ = loader(n_id.numpy())
+    n_id, ei, e_id = torch.from_numpy(n_id), torch.from_numpy(ei), torch.from_numpy(e_id)
+    assoc = torch.zeros(model.memory.num_nodes, dtype=torch.long)
+    assoc[n_id] = torch.arange(n_id.size(0))
+    z, last_update = model.memory(n_id)
+    z = model.gnn(z, last_update, ei, ev_t[e_id], ev_msg[e_id])
+    pos_out = model.link_pred(z[assoc[s_src]], z[assoc[s_pos]])
+    neg_out = model.link_pred(z[assoc[s_src]], z[assoc[s_neg]])
+    bce = nn.functional.binary_cross_entropy_with_logits
+    loss = (bce(pos_out, torch.ones_like(pos_out), reduction="sum")
+            + bce(neg_out, torch.zeros_like(neg_out), reduction="sum")) / B
+    mem = model.memory
+    u = torch.cat([s_src, s_pos]).unique()
+    with torch.no_grad():
+        m_u, lu_u = mem._get_updated_memory(u)                          # before this batch's stores
+    mem._update_msg_store(src, pos, t, msg, mem.msg_s_store)
+    mem._update_msg_store(pos, src, t, msg, mem.msg_d_store)
+    loader.insert(src.numpy(), pos.numpy(), t.numpy())
+    loss.backward()
+    lt = loss.detach().clone()
+    if world > 1:
+        for p in model.parameters():
+            if p.grad is not None:
+                dist.all_reduce(p.grad)
+        dist.all_reduce(lt)
+    opt.step()
+    cap = 2 * (-(-B // world))
+    node = torch.full((cap,), -1, dtype=torch.long)
+    node[:u.numel()] = u
+    lu = torch.zeros(cap, dtype=torch.long)
+    lu[:u.numel()] = lu_u.long()
+    rows = torch.zeros(cap, mem.memory_dim)
+    rows[:u.numel()] = m_u.detach()
+    if world > 1:
+        g_node = [torch.empty_like(node) for _ in range(world)]
+        g_lu = [torch.empty_like(lu) for _ in range(world)]
+        g_rows = [torch.empty_like(rows) for _ in range(world)]
+        dist.all_gather(g_node, node)
+        dist.all_gather(g_lu, lu)
+        dist.all_gather(g_rows, rows)
+        node, lu, rows = torch.cat(g_node), torch.cat(g_lu), torch.cat(g_rows)
+    ok = node >= 0
+    with torch.no_grad():
+        mem.memory[node[ok]] = rows[ok]
+        mem.last_update[node[ok]] = lu[ok]
+    return float(lt), pos_out.detach().view(-1), neg_out.detach().view(-1)
+
+
 @torch.no_grad()
 def eval_step(model: RefTGN, loader, ev_t, ev_msg, src, pos, negs, t, msg):
     """TGB-style eval of one batch: every event's [pos, negs...] scored against the batch-start

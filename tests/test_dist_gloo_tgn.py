@@ -1,0 +1,102 @@
+"""World-size-2 `gloo` test (CPU) of the TGN memory path's data-parallel decomposition (SURVEY §8e,
+the scheme tgnx_tgn_train_fwd_bwd / tgnx_tgn_apply_rows implement): per-rank event slices as roots,
+all-reduced gradients, replicated message stores / ring insert, and an all-gather of the GRU-updated
+memory rows (oracle.tgn_ref.train_step_dp), against the single-process canonical step
+(oracle.tgn_ref.train_step) on the same global batches:
+  * lr = 0 (parameters fixed): losses, every step's summed gradients, memory and last_update;
+  * lr = 1e-3: losses and parameters after every step.  Memory is not compared here: the gradient
+    sums differ in fp order (~1e-7), and the time encoding multiplies a weight difference by Δt
+    (~1e6 s on the unix-scale streams), which moves cos(w Δt + b) by up to ~1e-4 — the precision
+    sensitivity SURVEY §7 notes, not a decomposition error (the lr = 0 case pins the decomposition)."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(rank, world, port, out_dir, steps, aggr, lr):
+    import sys
+    for p in (ROOT, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from oracle.sampler_ref import RefLastNeighborLoader
+    from oracle.tgn_ref import RefTGN, train_step, train_step_dp
+    from tgnx.synth import make_stream
+
+    torch.set_num_threads(1)
+    if world > 1:
+        os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    N, B, d, D = 200, 40, 8, 16
+    s = make_stream("tgbl-wiki", seed=5, num_events=B * steps, num_nodes=N, msg_dim=d)
+    torch.manual_seed(0)
+    model = RefTGN(N, d, hidden=D, aggr=aggr, dropout=0.0)
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    loader = RefLastNeighborLoader(N, 10)
+    ev_t = torch.from_numpy(s.t.astype(np.float32))
+    ev_msg = torch.from_numpy(s.msg)
+    rng = np.random.default_rng(7)
+    losses, mems, lus, grads = [], [], [], []
+    for st in range(steps):
+        sl = slice(st * B, (st + 1) * B)
+        src, pos = torch.from_numpy(s.src[sl]), torch.from_numpy(s.dst[sl])
+        neg = torch.from_numpy(rng.choice(s.dst_nodes, size=B))
+        if world == 1:
+            loss, _, _ = train_step(model, opt, loader, ev_t, ev_msg, src, pos, neg, ev_t[sl], ev_msg[sl])
+        else:
+            loss, _, _ = train_step_dp(model, opt, loader, ev_t, ev_msg, src, pos, neg, ev_t[sl], ev_msg[sl], rank,
+                                       world)
+        losses.append(loss)
+        grads.append(np.concatenate([p.grad.detach().reshape(-1).numpy() for p in model.parameters()]))
+        mems.append(model.memory.memory.detach().clone().numpy())
+        lus.append(model.memory.last_update.clone().numpy())
+    params = {k: v.detach().numpy() for k, v in model.named_parameters()}
+    np.savez(os.path.join(out_dir, f"r{rank}_w{world}.npz"), losses=np.array(losses), mem=np.stack(mems),
+             lu=np.stack(lus), grads=np.stack(grads), **params)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _check(aggr, lr):
+    steps = 4
+    with tempfile.TemporaryDirectory() as td:
+        _run(0, 1, 0, td, steps, aggr, lr)
+        mp.spawn(_run, args=(2, _free_port(), td, steps, aggr, lr), nprocs=2, join=True)
+        ref = np.load(os.path.join(td, "r0_w1.npz"))
+        for r in (0, 1):
+            got = np.load(os.path.join(td, f"r{r}_w2.npz"))
+            np.testing.assert_allclose(got["losses"], ref["losses"], rtol=1e-5, atol=1e-6)
+            if lr == 0:
+                np.testing.assert_array_equal(got["lu"], ref["lu"])
+                np.testing.assert_allclose(got["mem"], ref["mem"], rtol=0, atol=1e-6)
+                for st in range(steps):
+                    g, gr = got["grads"][st], ref["grads"][st]
+                    assert np.linalg.norm(g - gr) <= 1e-5 * np.linalg.norm(gr) + 1e-9, st
+            for k in ref.files:
+                if k in ("losses", "mem", "lu", "grads"):
+                    continue
+                np.testing.assert_allclose(got[k], ref[k], rtol=0, atol=5e-6, err_msg=k)
+
+
+def test_tgn_dp_gloo_world2_last():
+    _check("last", 0.0)
+    _check("last", 1e-3)
+
+
+def test_tgn_dp_gloo_world2_mean():
+    _check("mean", 0.0)
+    _check("mean", 1e-3)

@@ -88,6 +88,8 @@ struct Ctx {
   int64_t* ctl;
   float *out_pos, *out_neg;
   double* mrr;
+  float* xrows;  // data parallel: this rank's updated memory rows (TGNX_TGN_ROW layout), or nullptr
+  int xcap;
   // workspace
   uint32_t *cb, *nb;
   int* kval;  // [N] valid ring slots of a centre (written by tgn_mark for this batch's centres)
@@ -125,17 +127,19 @@ __global__ void tgn_mark(Ctx c) {
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   const int gen = (int)c.ctl[TGNX_CTL_GEN];
   const int Kn = TRAIN ? 1 : c.Kn;
-  const int nq = B * (2 + Kn);
+  // train: this rank's event slice [lo, lo + nl) (data parallel; the whole batch at world 1)
+  const int lo = TRAIN ? (int)c.ctl[TGNX_CTL_LO] : 0, nl = TRAIN ? (int)(c.ctl[TGNX_CTL_HI] - c.ctl[TGNX_CTL_LO]) : B;
+  const int nq = nl * (2 + Kn);
   const int sl = threadIdx.x & 15, grp = (threadIdx.x & 63) >> 4;
   const int gstride = (gridDim.x * blockDim.x) >> 4;
   for (int q = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; q < nq; q += gstride) {
     int64_t v;
-    if (q < B) {
-      v = c.ev_src[start + q];
-    } else if (q < 2 * B) {
-      v = c.ev_dst[start + q - B];
+    if (q < nl) {
+      v = c.ev_src[start + lo + q];
+    } else if (q < 2 * nl) {
+      v = c.ev_dst[start + lo + q - nl];
     } else if (TRAIN) {
-      const int i = q - 2 * B;
+      const int i = lo + q - 2 * nl;
       if (c.gen_neg) {
         const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
         const uint64_t off = (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
@@ -151,7 +155,7 @@ __global__ void tgn_mark(Ctx c) {
         v = c.neg[start + i];
       }
     } else {
-      const int x = q - 2 * B;
+      const int x = q - 2 * nl;
       v = c.neg[(start + x / Kn) * Kn + x % Kn];
     }
     int k = 0;
@@ -165,7 +169,7 @@ __global__ void tgn_mark(Ctx c) {
       k += __popcll((__ballot(ok) >> (16 * grp)) & 0xFFFFull);
     }
     if (sl == 0) {
-      if (q < 2 * B) c.node_gen[v] = gen;
+      if (q < 2 * nl) c.node_gen[v] = gen;
       c.kval[v] = k;
       if (!(c.cb[v >> 5] & (1u << (v & 31)))) atomicOr(&c.cb[v >> 5], 1u << (v & 31));
       if (!(c.nb[v >> 5] & (1u << (v & 31)))) atomicOr(&c.nb[v >> 5], 1u << (v & 31));
@@ -620,8 +624,9 @@ struct EpiProj {
 // P row = [q | k | v | skip] (lin_query / key / value / skip + biases); Ep row = lin_edge(edge_attr).
 // score_eh = (q_i · (k_j + e))_h / sqrt(C); alpha = PyG softmax (max-shifted, +1e-16); attention
 // dropout (train); out_i = Σ_e alpha~ (v_j + e) + skip_i.  Lane e keeps edge e's per-edge scalars.
-__device__ __forceinline__ float att_keep(const Ctx& c, uint64_t seed, int e, int h) {
-  return keep32(drop_base(seed, 7, (uint64_t)e, 0), (uint32_t)h, c.p, c.inv_keep);
+// keyed by (centre node, neighbour e_id): the same mask whichever rank / batch position samples the edge
+__device__ __forceinline__ float att_keep(const Ctx& c, uint64_t seed, int x, int e, int h) {
+  return keep32(drop_base(seed, 7, (uint64_t)c.cent[x], (uint64_t)c.e_id[e]), (uint32_t)h, c.p, c.inv_keep);
 }
 template <bool TRAIN>
 __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
@@ -658,8 +663,8 @@ __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
     c.alpha[(int64_t)(e0 + lane) * 2 + 1] = a1;
     if (c.drop) {
       const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-      t0 *= att_keep(c, seed, e0 + lane, 0);
-      t1 *= att_keep(c, seed, e0 + lane, 1);
+      t0 *= att_keep(c, seed, x, e0 + lane, 0);
+      t1 *= att_keep(c, seed, x, e0 + lane, 1);
     }
   }
   float o0 = 0.f, o1 = 0.f;
@@ -849,8 +854,8 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
     a0 = c.alpha[(int64_t)(e0 + lane) * 2];
     a1 = c.alpha[(int64_t)(e0 + lane) * 2 + 1];
     if (c.drop) {
-      k0v = att_keep(c, seed, e0 + lane, 0);
-      k1v = att_keep(c, seed, e0 + lane, 1);
+      k0v = att_keep(c, seed, x, e0 + lane, 0);
+      k1v = att_keep(c, seed, x, e0 + lane, 1);
     }
   }
   // d alpha~_eh = Σ_{ch in h} dout (v_j + e); d alpha = d alpha~ * keep
@@ -1217,12 +1222,35 @@ __global__ void __launch_bounds__(256) tgn_update(Ctx c, int nmem, int nst, int 
   if ((int)blockIdx.x < nmem) {
     if (mem_mode == 0 && (c.ctl[TGNX_CTL_B] == 0 || c.ctl[TGNX_CTL_ERR] != 0)) return;
     const int n = list_cnt ? *list_cnt : n_host;
+    const int RW = TGNX_TGN_ROW(c.D);
+    float* xr = mem_mode == 0 ? c.xrows : nullptr;
+    if (xr && n > c.xcap) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) c.ctl[TGNX_CTL_ERR] |= 8;
+      return;
+    }
     for (int u = blockIdx.x * 4 + (threadIdx.x >> 6); u < n; u += nmem * 4) {
       const int64_t v = list ? list[u] : base + u;
       const int m = mem_mode == 0 ? c.upd_loc[u] : u;
-      for (int k = lane; k < c.D; k += 64) c.mem[v * c.D + k] = c.Z0[(int64_t)m * c.D + k];
-      if (lane == 0) c.lu_buf[v] = (int64_t)c.lu[m];
+      const int64_t luv = (int64_t)c.lu[m];
+      for (int k = lane; k < c.D; k += 64) {
+        const float z = c.Z0[(int64_t)m * c.D + k];
+        c.mem[v * c.D + k] = z;
+        if (xr) xr[(int64_t)u * RW + 4 + k] = z;
+      }
+      if (lane == 0) {
+        c.lu_buf[v] = luv;
+        if (xr) {
+          int* h = reinterpret_cast<int*>(xr + (int64_t)u * RW);
+          h[0] = (int)v;
+          h[1] = (int)(uint32_t)((uint64_t)luv & 0xFFFFFFFFull);
+          h[2] = (int)(uint32_t)((uint64_t)luv >> 32);
+          h[3] = 0;
+        }
+      }
     }
+    if (xr)  // unused slots
+      for (int u = n + blockIdx.x * blockDim.x + threadIdx.x; u < c.xcap; u += nmem * blockDim.x)
+        reinterpret_cast<int*>(xr + (int64_t)u * RW)[0] = -1;
     return;
   }
   const int B = (int)c.ctl[TGNX_CTL_B];
@@ -1249,6 +1277,20 @@ __global__ void __launch_bounds__(256) tgn_update(Ctx c, int nmem, int nst, int 
     const int a = c.rruns[r];
     ring_merge_run(c.nbr, c.eid, c.rt, c.K, c.ev_src + start, c.ev_dst + start, c.ev_t + start, B,
                    c.ctl[TGNX_CTL_CUR_EID], c.assoc, c.rkeys, a, c.rruns[r + 1] - a, r, lane);
+  }
+}
+
+// data parallel: the all-gathered memory rows of every rank -> memory / last_update (wave per row)
+__global__ void __launch_bounds__(256) tgn_apply_rows(float* mem, int64_t* lu, const float* rows, int64_t nrows, int D,
+                                                      int64_t N) {
+  const int lane = threadIdx.x & 63, RW = TGNX_TGN_ROW(D);
+  for (int64_t u = blockIdx.x * 4 + (threadIdx.x >> 6); u < nrows; u += (int64_t)gridDim.x * 4) {
+    const float* row = rows + u * RW;
+    const int* h = reinterpret_cast<const int*>(row);
+    const int v = h[0];
+    if (v < 0 || v >= N) continue;
+    for (int k = lane; k < D; k += 64) mem[(int64_t)v * D + k] = row[4 + k];
+    if (lane == 0) lu[v] = (int64_t)(((uint64_t)(uint32_t)h[2] << 32) | (uint64_t)(uint32_t)h[1]);
   }
 }
 }  // namespace tgn
@@ -1479,6 +1521,9 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.out_pos = b->out_pos;
   c.out_neg = b->out_neg;
   c.mrr = b->mrr;
+  c.xrows = b->xrows;
+  c.xcap = b->xrows ? (int)std::min<int64_t>(b->xcap, 1 << 30) : 0;
+  TGNX_CHECK_ARG(!b->xrows || b->xcap > 0, "tgn: xrows without xcap");
   char* ws = reinterpret_cast<char*>(b->ws);
   c.cb = reinterpret_cast<uint32_t*>(ws + W.cb);
   c.nb = reinterpret_cast<uint32_t*>(ws + W.nb);
@@ -1680,6 +1725,19 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   tgn_update<<<nmem + nst + nring, 256, 0, s>>>(c, nmem, nst, 0, c.upd, c.cnt + CNT_U, 0, 0);
   probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgn_update");
+  return TGNX_OK;
+}
+
+int tgnx_tgn_apply_rows(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, const float* rows, int64_t nrows,
+                        void* stream) {
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(buf && buf->memory && buf->last_update, "tgnx_tgn_apply_rows: null buffer");
+  TGNX_CHECK_ARG(nrows >= 0 && (nrows == 0 || rows), "tgnx_tgn_apply_rows: bad rows");
+  if (nrows == 0) return TGNX_OK;
+  tgn_apply_rows<<<gridn(nrows, 4, 4096), 256, 0, as_stream(stream)>>>(buf->memory, buf->last_update, rows, nrows,
+                                                                        cfg->mem_dim, cfg->num_nodes);
+  TGNX_LAUNCH_CHECK("tgn_apply_rows");
   return TGNX_OK;
 }
 

@@ -47,7 +47,8 @@ class TgnBuffers(ctypes.Structure):
     _fields_ = [("ev_src", P), ("ev_dst", P), ("ev_t", P), ("ev_msg", P), ("neg", P), ("dst_nodes", P),
                 ("n_dst", ctypes.c_int64), ("nbr", P), ("eid", P), ("rt", P), ("assoc", P), ("memory", P),
                 ("last_update", P), ("store", P), ("node_gen", P), ("params", P), ("grads", P), ("adam_m", P),
-                ("adam_v", P), ("ctl", P), ("out_pos", P), ("out_neg", P), ("mrr", P), ("ws", P)]
+                ("adam_v", P), ("ctl", P), ("out_pos", P), ("out_neg", P), ("mrr", P), ("ws", P), ("xrows", P),
+                ("xcap", ctypes.c_int64)]
 
 
 def param_shapes(D: int, d: int) -> dict:
@@ -216,6 +217,14 @@ class TgnEngine:
             self.adam_m, self.adam_v = torch.zeros_like(model.flat), torch.zeros_like(model.flat)
         else:
             self.adam_m, self.adam_v = optimizer.exp_avg, optimizer.exp_avg_sq
+        # data parallel: each rank's GRU-updated memory rows [node | last_update | memory],
+        # all-gathered over RCCL after the step and written by every rank (tgnx_tgn_apply_rows)
+        self.xrows = self.xgather = None
+        if self.world > 1:
+            self.xcap = min(cfg.num_nodes, 2 * (-(-cfg.max_batch // self.world)))
+            rw = cfg.mem_dim + 4
+            self.xrows = torch.zeros(self.xcap, rw, dtype=torch.float32, device=self.dev)
+            self.xgather = torch.zeros(self.world * self.xcap, rw, dtype=torch.float32, device=self.dev)
 
     def _buffers(self, neg_ptr: int) -> TgnBuffers:
         m, ld = self.model, self.loader
@@ -229,6 +238,7 @@ class TgnEngine:
         b.store, b.node_gen = _p(m.store), _p(m.node_gen)
         b.params, b.grads, b.adam_m, b.adam_v = _p(m.flat), _p(m.grad_flat), _p(self.adam_m), _p(self.adam_v)
         b.ctl, b.out_pos, b.out_neg, b.mrr, b.ws = _p(self.ctl), _p(self.out_pos), _p(self.out_neg), _p(self.mrr), _p(self.ws)
+        b.xrows, b.xcap = _p(self.xrows), (0 if self.xrows is None else self.xcap)
         return b
 
     def _stream(self):
@@ -267,9 +277,20 @@ class TgnEngine:
 
     def apply_update(self, allreduce: bool = True):
         if allreduce and self.world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(self.model.grad_flat)
+            self._exchange()
+        if self.world > 1:
+            self._apply_rows(self._pending)
         _lib.call("tgnx_tgn_train_update", ctypes.byref(self.cfg), ctypes.byref(self._pending), self._stream())
+
+    def _exchange(self):
+        """The step's collectives: gradient sum (all-reduce) and the touched memory rows (all-gather)."""
+        import torch.distributed as dist
+        dist.all_reduce(self.model.grad_flat)
+        dist.all_gather_into_tensor(self.xgather, self.xrows)
+
+    def _apply_rows(self, b):
+        _lib.call("tgnx_tgn_apply_rows", ctypes.byref(self.cfg), ctypes.byref(b), _p(self.xgather),
+                  self.xgather.shape[0], self._stream())
 
     def eval_batch(self, start: int, B: int, negs):
         """TGB-style eval batch: negs LongTensor[B, Kn].  Returns (pos [B], neg [B, Kn], rr [B])."""
@@ -292,7 +313,7 @@ class TgnEngine:
         self._res_drop = 1 if dropout else 0
         self._res_buf = self._buffers(_p(self.neg_train))
         L = _lib.lib()
-        self._f = (L.tgnx_tgnn_advance, L.tgnx_tgn_train_fwd_bwd, L.tgnx_tgn_train_update)
+        self._f = (L.tgnx_tgnn_advance, L.tgnx_tgn_train_fwd_bwd, L.tgnx_tgn_train_update, L.tgnx_tgn_apply_rows)
         self._cfg_ref, self._buf_ref = ctypes.byref(self.cfg), ctypes.byref(self._res_buf)
         self._ctl_p = ctypes.c_void_p(self.ctl.data_ptr())
 
@@ -302,7 +323,7 @@ class TgnEngine:
         self.ctl[10] = 0
 
     def _pre(self):
-        adv, fb, _ = self._f
+        adv, fb = self._f[:2]
         lo, hi, batch = self._res
         st = self._stream()
         rc = adv(self._ctl_p, 1, 0, 0, 0, lo, hi, batch, self.rank, self.world, self.seed, 1, st)
@@ -311,13 +332,18 @@ class TgnEngine:
             raise RuntimeError(f"tgnx TGN resident step failed: {_lib.lib().tgnx_last_error().decode()}")
 
     def _post(self):
-        if self._f[2](self._cfg_ref, self._buf_ref, self._stream()):
+        st = self._stream()
+        rc = 0
+        if self.world > 1:
+            rc |= self._f[3](self._cfg_ref, self._buf_ref, ctypes.c_void_p(self.xgather.data_ptr()),
+                             ctypes.c_int64(self.xgather.shape[0]), st)
+        rc |= self._f[2](self._cfg_ref, self._buf_ref, st)
+        if rc:
             raise RuntimeError(f"tgnx TGN resident update failed: {_lib.lib().tgnx_last_error().decode()}")
 
     def _allreduce(self):
         if self.world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(self.model.grad_flat)
+            self._exchange()
 
     def resident_train_step(self):
         self._pre()
@@ -325,7 +351,7 @@ class TgnEngine:
         self._post()
 
     def capture_resident(self):
-        """One resident step as HIP graph(s) (world > 1: the all-reduce stays eager between them)."""
+        """One resident step as HIP graph(s) (world > 1: the collectives stay eager between them)."""
         torch.cuda.synchronize(self.dev)
         saved = self.ctl.clone()
         if self.world == 1:
