@@ -1,10 +1,11 @@
 """Entry script with the reference's CLI (pyg-mem-tgn.py --data <name> --config <yml>).
 
-Runs the running reference path (TGNN, dependency-block batching) on the fused HIP step:
-train + validation MRR per epoch, wall-clock per phase.  Extra flags: --epochs overrides
-train.epoch (the reference's 3000 is a run length, not a smoke test), --batch overrides
-train.batch_size.  Data: a TGB dataset name (synthetic stream of that shape; no network
-here) or an .npz with src/dst/t/msg, see tgnx/data.py.
+Runs the running reference path (TGNN, dependency-block batching; --path dgl, the default) or the
+PyG TGN memory path (--path pyg: pyg_model_utils + the canonical loop in pyg_epoch_utils, the
+import swap at pyg-mem-tgn.py:23-25) on the fused HIP step: train + validation MRR per epoch,
+wall-clock per phase.  Extra flags: --epochs overrides train.epoch (the reference's 3000 is a run
+length, not a smoke test), --batch overrides train.batch_size.  Data: a TGB dataset name
+(synthetic stream of that shape; no network here) or an .npz with src/dst/t/msg, see tgnx/data.py.
 """
 import argparse
 import os
@@ -15,8 +16,6 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 import torch  # noqa: E402
 
-from epoch_utils import test, train  # noqa: E402
-from model_utils import getModel, getOptimizer  # noqa: E402
 from neg_sampler import NegLinkSamplerDest  # noqa: E402
 from neighbor_loader import LastNeighborLoader  # noqa: E402
 from utils import getDataWithDependecyBlock, parse_config  # noqa: E402
@@ -28,7 +27,14 @@ def main():
     ap.add_argument("--config", type=str, default=os.path.join(os.path.dirname(__file__), "config", "TGN.yml"))
     ap.add_argument("--epochs", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--path", choices=["dgl", "pyg"], default="dgl", help="#change based on dgl/pyg")
     args = ap.parse_args()
+    if args.path == "dgl":
+        from epoch_utils import test, train
+        from model_utils import getModel, getOptimizer
+    else:
+        from pyg_epoch_utils import test, train
+        from pyg_model_utils import getModel, getOptimizer
 
     device = torch.device("cuda")
     sample_param, memory_param, gnn_param, train_param = parse_config(args.config)
@@ -39,8 +45,12 @@ def main():
     neg_dest_sampler = NegLinkSamplerDest(torch.unique(data.dst), device=device)
     neighbor_loader = LastNeighborLoader(data.num_nodes, size=sample_param["neighbor"][0], device=device)
     assoc = torch.empty(data.num_nodes, dtype=torch.long, device=device)
-    model = getModel(data.msg.shape[1], gnn_param["dim_out"], data.num_nodes, device, gnn_param=gnn_param,
-                     ring=sample_param["neighbor"][0], max_batch=train_param["batch_size"])
+    if args.path == "dgl":
+        model = getModel(data.msg.shape[1], gnn_param["dim_out"], data.num_nodes, device, gnn_param=gnn_param,
+                         ring=sample_param["neighbor"][0], max_batch=train_param["batch_size"])
+    else:
+        model = getModel(data.msg.shape[1], gnn_param["dim_out"], data.num_nodes, device,
+                         ring=sample_param["neighbor"][0], max_batch=train_param["batch_size"])
     optimizer = getOptimizer(model, train_param["lr"])
     criterion = torch.nn.BCEWithLogitsLoss()
     t_start = time.time()

@@ -98,7 +98,8 @@ class TGNModel(nn.Module):
         super().__init__()
         dev = _lib.require_device(device)
         D, d = int(hidden_dim), int(msg_dim)
-        self.num_nodes, self.num_events, self.D, self.d = int(num_nodes), int(num_events), D, d
+        num_events = max(int(num_events or 0), 1)
+        self.num_nodes, self.num_events, self.D, self.d = int(num_nodes), num_events, D, d
         self.cfg = TgnConfig(num_nodes=num_nodes, num_events=num_events, ring=ring, mem_dim=D, msg_dim=d, heads=2,
                              max_batch=max_batch, max_neg=max_neg, aggr=0 if aggr == "last" else 1, dropout=dropout,
                              lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8)
@@ -136,11 +137,24 @@ class TGNModel(nn.Module):
         # TGNMemory buffers (memory_module.py:80-83) and the message stores
         self.memory.register_buffer("memory", torch.zeros(num_nodes, D, device=dev))
         self.memory.register_buffer("last_update", torch.zeros(num_nodes, dtype=torch.long, device=dev))
+        self.store = None
+        self.ensure_events(max(int(num_events or 0), 1))
+        self.node_gen = torch.zeros(num_nodes, dtype=torch.int32, device=dev)
+
+    def ensure_events(self, n: int) -> None:
+        """Size the message-store arena for an event table of n rows (the reference's getModel does
+        not know the stream length; the engine calls this when it binds the table)."""
+        if self.store is not None and n <= self.cfg.num_events:
+            return
+        self.cfg.num_events = int(n)
+        self.num_events = int(n)
         words = _lib.lib().tgnx_tgn_store_words(ctypes.byref(self.cfg))
         if words == 0:
             raise RuntimeError(f"tgnx_tgn_store_words: {_lib.lib().tgnx_last_error().decode()}")
-        self.store = torch.zeros(int(words), dtype=torch.long, device=dev)
-        self.node_gen = torch.zeros(num_nodes, dtype=torch.int32, device=dev)
+        old = self.store
+        self.store = torch.zeros(int(words), dtype=torch.long, device=self.flat.device)
+        if old is not None:   # per-node {off, cnt} words first; arena offsets stay valid
+            self.store[:old.numel()].copy_(old)
 
     @property
     def device(self):
@@ -196,6 +210,7 @@ class TgnEngine:
             cfg.ring = loader.size
         self.cfg = cfg
         ev = {k: torch.as_tensor(v) for k, v in events.items()}
+        model.ensure_events(int(ev["src"].numel()))
         self.src = ev["src"].to(self.dev, torch.long).contiguous()
         self.dst = ev["dst"].to(self.dev, torch.long).contiguous()
         self.t = ev["t"].to(self.dev, torch.float32).contiguous()
@@ -225,6 +240,22 @@ class TgnEngine:
             rw = cfg.mem_dim + 4
             self.xrows = torch.zeros(self.xcap, rw, dtype=torch.float32, device=self.dev)
             self.xgather = torch.zeros(self.world * self.xcap, rw, dtype=torch.float32, device=self.dev)
+
+    def ensure_neg(self, kn: int) -> None:
+        """Grow the workspace for eval batches with kn negatives per event (TGB: ~999 on tgbl-wiki)."""
+        if kn <= self.cfg.max_neg:
+            return
+        torch.cuda.synchronize(self.dev)
+        self.cfg.max_neg = int(kn)
+        nb = _lib.lib().tgnx_tgn_ws_bytes(ctypes.byref(self.cfg))
+        if nb == 0:
+            raise RuntimeError(f"tgnx_tgn_ws_bytes: {_lib.lib().tgnx_last_error().decode()}")
+        self.ws = torch.zeros(nb, dtype=torch.uint8, device=self.dev)   # scratch only: zero = initial state
+        self.out_neg = torch.zeros(self.cfg.max_batch * kn, dtype=torch.float32, device=self.dev)
+        if hasattr(self, "_res_buf"):
+            self._res_buf = self._buffers(_p(self.neg_train))
+            self._buf_ref = ctypes.byref(self._res_buf)
+        self._graphs = None                                   # captured pointers are stale
 
     def _buffers(self, neg_ptr: int) -> TgnBuffers:
         m, ld = self.model, self.loader
@@ -296,8 +327,7 @@ class TgnEngine:
         """TGB-style eval batch: negs LongTensor[B, Kn].  Returns (pos [B], neg [B, Kn], rr [B])."""
         negs = torch.as_tensor(negs).to(self.dev, torch.long).contiguous()
         Kn = negs.shape[1]
-        if Kn > self.cfg.max_neg:
-            raise ValueError(f"{Kn} negatives > max_neg {self.cfg.max_neg}")
+        self.ensure_neg(Kn)
         self.advance(start, B, False)
         # the kernels index neg[(start + i) * Kn + c]: shift the base pointer by start rows
         b = self._buffers(negs.data_ptr() - start * Kn * 8)
@@ -391,9 +421,9 @@ class TgnEngine:
 
 
 def getModel(feature_dim, hidden_dim, num_nodes, device, num_events=None, **kw):
-    """pyg_model_utils.py:10-36; num_events sizes the message-store arena (the event table's rows)."""
-    if num_events is None:
-        raise ValueError("tgnx getModel (PyG TGN) needs num_events (rows of the event table)")
+    """pyg_model_utils.py:10-36.  num_events (optional) pre-sizes the message-store arena; otherwise the
+    engine sizes it when it binds the event table.  Extra keywords: ring, max_batch, max_neg, aggr,
+    dropout (TGNModel)."""
     m = TGNModel(num_nodes, num_events, feature_dim, hidden_dim, device, **kw)
     return {"memory": m.memory, "gnn": m.gnn, "link_pred": m.link_pred, "model": m}
 
