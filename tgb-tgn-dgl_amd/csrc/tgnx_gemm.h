@@ -23,9 +23,10 @@ namespace tgnx {
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-template <int TM_, int TN_, int KC_>
+template <int TM_, int TN_, int KC_, int PF_ = 1>
 struct GemmCfg {
   static constexpr int TM = TM_, TN = TN_, KC = KC_;
+  static constexpr int PF = PF_;  // k-chunks whose global loads are in flight ahead of the MFMAs
   static constexpr int FM = TM / 32, FN = TN / 32;  // 16x16 MFMA tiles per wave (2x2 waves)
   static constexpr int PK = KC + 4;                  // LDS row pitch of the k-contiguous operand rows
   static constexpr int PB = TN + 1;                  // LDS pitch of the C tile
@@ -37,7 +38,10 @@ struct GemmCfg {
 #ifndef TGNX_G32_KC
 #define TGNX_G32_KC 128
 #endif
-using G32 = GemmCfg<32, 32, TGNX_G32_KC>;  // the TGN step's GEMMs
+#ifndef TGNX_G32_PF
+#define TGNX_G32_PF 1
+#endif
+using G32 = GemmCfg<32, 32, TGNX_G32_KC, TGNX_G32_PF>;  // the TGN step's GEMMs
 using G64 = GemmCfg<64, 64, 64>;   // large-M GEMMs (eval scoring)
 
 struct GemmShape {
@@ -70,7 +74,8 @@ inline GemmShape gemm_shape_split(int M, int N, int K, const int* Mdev, const in
   g.deferred = 1;
   return g;
 }
-__host__ __device__ inline int gemm_blocks(const GemmShape& g) { return g.tiles_m * g.tiles_n * g.S; }
+// grid of a GEMM: tiles x splits, padded to a multiple of the 8 XCDs (see gemm_work)
+__host__ __device__ inline int gemm_blocks(const GemmShape& g) { return (g.tiles_m * g.tiles_n * g.S + 7) & ~7; }
 inline size_t gemm_partial_floats(const GemmShape& g) {
   return g.deferred ? (size_t)g.tiles_m * g.tiles_n * g.S * g.tm * g.tn : 0;
 }
@@ -140,6 +145,36 @@ __device__ __forceinline__ void gemm_map(int tid, int i, int& r, int& kk) {
   }
 }
 
+// XCD-aware work mapping.  Workgroups are dispatched round-robin over the 8 XCDs (bid % 8) and each
+// XCD has its own L2, so with a plain bid -> tile order every XCD fetches all of A and all of B from
+// the fabric (PMC: 16.7 MB per launch for the GRU GEMM against ~4 MB algorithmic).  Here XCD x takes
+// the contiguous run [x T/8, (x+1) T/8) of a grouped tile order (GROUP m-tiles per column sweep), so
+// it touches ~T/8 tiles packed in a GROUP x (T/8/GROUP) rectangle.  Splits are the slowest index.
+// The order is laid over the RUNTIME tile counts (capacities are worst-case: 6,600 rows against
+// ~415 at run time would put every live tile on one XCD); partial-buffer offsets stay in capacity
+// tile numbering.
+constexpr int GEMM_GROUP = 4;
+struct GemmWork {
+  int tile, s, tm, tn;
+  bool ok;
+};
+template <int TM, int TN>
+__device__ __forceinline__ GemmWork gemm_work(const GemmShape& g, int Mr, int Nr, int Sr, int bid) {
+  GemmWork w;
+  const int tmr = (Mr + TM - 1) / TM, tnr = (Nr + TN - 1) / TN;
+  const int tiles = tmr * tnr, T = tiles * Sr, per = (T + 7) >> 3;
+  const int L = (bid & 7) * per + (bid >> 3);
+  w.ok = (bid >> 3) < per && L < T && tiles > 0;
+  const int s = w.ok ? L / tiles : 0, tl = w.ok ? L - s * tiles : 0;
+  const int gw = GEMM_GROUP * max(tnr, 1), grp = tl / gw, m_first = grp * GEMM_GROUP;
+  const int gsz = max(1, min(tmr - m_first, GEMM_GROUP)), r = tl - grp * gw;
+  w.s = s;
+  w.tm = m_first + r % gsz;
+  w.tn = r / gsz;
+  w.tile = w.tm * g.tiles_n + w.tn;
+  return w;
+}
+
 // One workgroup of a GEMM (`bid` in [0, gemm_blocks(g))); `smem` holds CFG::SMEM floats.
 // A kernel may host several GEMMs by dispatching on block ranges.
 template <class CFG, class AL, class BL, class EPI>
@@ -151,11 +186,10 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
   float* Bs = smem + TM * PK;  // [TN][PK]: row n, k contiguous
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const GemmRt rt = gemm_runtime<CFG>(g);
-  const int tiles = g.tiles_m * g.tiles_n;
-  const int tile = bid % tiles, s = bid / tiles;
-  const int tmi = tile / g.tiles_n, tni = tile % g.tiles_n;
-  const int m0 = tmi * TM, n0 = tni * TN;
-  if (m0 >= rt.Mr || n0 >= rt.Nr || s >= rt.Sr) return;  // the fixup skips such tiles / splits too
+  const GemmWork wk = gemm_work<TM, TN>(g, rt.Mr, rt.Nr, rt.Sr, bid);
+  const int tile = wk.tile, s = wk.s;
+  const int m0 = wk.tm * TM, n0 = wk.tn * TN;
+  if (!wk.ok || m0 >= rt.Mr || n0 >= rt.Nr || s >= rt.Sr) return;  // the fixup skips such tiles / splits too
   const int wr = (wv >> 1) * (TM / 2), wc = (wv & 1) * (TN / 2);
   const int li = lane & 15, lk = lane >> 4;
   f32x4_t acc[FM][FN];
@@ -163,20 +197,22 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
-  float ra[LA], rb[LB];
-  auto fetch = [&](int ch) {  // chunk ch -> registers (every load in flight at once)
+  constexpr int PF = CFG::PF;
+  float ra[PF][LA], rb[PF][LB];
+  // chunk ch -> register slot p (every load of the slot in flight at once)
+  auto fetch = [&](float* fa, float* fb, int ch) {
     const int k0 = ch * KC, kc = max(0, min(KC, rt.Kr - k0));
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       int r, kk;
       gemm_map<AL::k_fast, TM, KC>(tid, i, r, kk);
-      ra[i] = (kk < kc && m0 + r < rt.Mr) ? al(m0 + r, k0 + kk) : 0.f;
+      fa[i] = (kk < kc && m0 + r < rt.Mr) ? al(m0 + r, k0 + kk) : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       int r, kk;
       gemm_map<BL::k_fast, TN, KC>(tid, i, r, kk);
-      rb[i] = (kk < kc && n0 + r < rt.Nr) ? bl(n0 + r, k0 + kk) : 0.f;
+      fb[i] = (kk < kc && n0 + r < rt.Nr) ? bl(n0 + r, k0 + kk) : 0.f;
     }
   };
   auto stash1 = [&](float* S, const float* rv, auto kfast, auto rows, auto cnt) {
@@ -197,10 +233,10 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
       }
     }
   };
-  auto stash = [&]() {
-    stash1(As, ra, std::integral_constant<bool, AL::k_fast>{}, std::integral_constant<int, TM>{},
+  auto stash = [&](const float* fa, const float* fb) {
+    stash1(As, fa, std::integral_constant<bool, AL::k_fast>{}, std::integral_constant<int, TM>{},
            std::integral_constant<int, LA>{});
-    stash1(Bs, rb, std::integral_constant<bool, BL::k_fast>{}, std::integral_constant<int, TN>{},
+    stash1(Bs, fb, std::integral_constant<bool, BL::k_fast>{}, std::integral_constant<int, TN>{},
            std::integral_constant<int, LB>{});
   };
   // k permutation inside a 16-deep slab: MFMA step q of lane (li, lk) takes k = 4 lk + q, so each
@@ -211,13 +247,7 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
 #pragma unroll
     for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const f32x4_t*>(Bs + (wc + 16 * j + li) * PK + kk + 4 * lk);
   };
-  const int last = max(rt.nchunk, 1);
-  fetch(s);
-  stash();
-  __syncthreads();
-  for (int ch = s; ch < last; ch += g.S) {
-    const bool more = ch + g.S < last;
-    if (more) fetch(ch + g.S);  // next chunk in flight during this chunk's MFMAs
+  auto mfma_chunk = [&]() {
     f32x4_t a[2][FM], b[2][FN];
     slab(0, a[0], b[0]);
 #pragma unroll
@@ -232,10 +262,24 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][i][q], b[cur][j][q], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
-    if (more) {
-      stash();
-      __syncthreads();
+  };
+  // PF-deep pipeline: the loads of the next PF chunks of this split are in flight while a chunk
+  // is stashed and multiplied (PF = 4 at KC = 128: every load of a K <= 512 GEMM issued up front)
+  const int last = max(rt.nchunk, 1);
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (s + p * g.S < last) fetch(ra[p], rb[p], s + p * g.S);
+  for (int c0 = s; c0 < last; c0 += PF * g.S) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int ch = c0 + p * g.S;
+      if (ch < last) {
+        stash(ra[p], rb[p]);
+        __syncthreads();
+        if (ch + PF * g.S < last) fetch(ra[p], rb[p], ch + PF * g.S);
+        mfma_chunk();
+        __syncthreads();
+      }
     }
   }
   if (g.deferred) {  // partial tile in register layout, summed by gemm_fixup_kernel

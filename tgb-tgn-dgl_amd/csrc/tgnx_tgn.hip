@@ -35,8 +35,12 @@ enum { CNT_R = 0, CNT_M = 1, CNT_E = 2, CNT_U = 3, CNT_RUNS = 4, CNT_SRUNS = 5, 
 
 __host__ __device__ inline int64_t al4(int64_t x) { return (x + 3) & ~int64_t(3); }
 
+// Flat parameter buffer.  The four node projections of TransformerConv (query, key, value, skip) sit
+// at a fixed stride (pw weights, pb biases) so kernels address projection g as base + g * stride:
+// a 4-way pointer select was lowered to a scratch-memory lookup table inside the GEMM loaders.
 struct Lay {
   int64_t te_w, te_b, w_ih, w_hh, b_ih, b_hh, wk, bk, wq, bq, wv, bv, we, wsk, bsk, lsw, lsb, ldw, ldb, lfw, lfb, total;
+  int64_t pw, pb;  // projection strides: wq + g pw, bq + g pb for g = query, key, value, skip
 };
 static Lay make_lay(int D, int d) {
   const int64_t Qm = 3 * (int64_t)D + d, HC = D;
@@ -48,15 +52,17 @@ static Lay make_lay(int D, int d) {
   L.w_hh = o; o += al4(3 * (int64_t)D * D);
   L.b_ih = o; o += al4(3 * D);
   L.b_hh = o; o += al4(3 * D);
-  L.wk = o; o += al4(HC * D);
-  L.bk = o; o += al4(HC);
-  L.wq = o; o += al4(HC * D);
-  L.bq = o; o += al4(HC);
-  L.wv = o; o += al4(HC * D);
-  L.bv = o; o += al4(HC);
+  L.pw = al4(HC * D);
+  L.pb = al4(HC);
+  L.wq = o; o += L.pw;
+  L.wk = o; o += L.pw;
+  L.wv = o; o += L.pw;
+  L.wsk = o; o += L.pw;
+  L.bq = o; o += L.pb;
+  L.bk = o; o += L.pb;
+  L.bv = o; o += L.pb;
+  L.bsk = o; o += L.pb;
   L.we = o; o += al4(HC * (D + d));
-  L.wsk = o; o += al4(HC * D);
-  L.bsk = o; o += al4(HC);
   L.lsw = o; o += al4((int64_t)D * D);
   L.lsb = o; o += al4(D);
   L.ldw = o; o += al4((int64_t)D * D);
@@ -588,17 +594,18 @@ struct LoadZ {
 };
 // stacked [W_query; W_key; W_value; W_skip] rows (n / HC selects the linear)
 struct LoadProjW {
-  const float *wq, *wk, *wv, *ws;
+  const float* w;  // wq; projection g at w + g * pw
+  int64_t pw;
   int HC, D;
   static constexpr bool k_fast = true;
   __device__ float operator()(int n, int k) const {
     const int g = n / HC, r = n % HC;
-    const float* w = g == 0 ? wq : g == 1 ? wk : g == 2 ? wv : ws;
-    return w[(int64_t)r * D + k];
+    return w[g * pw + (int64_t)r * D + k];
   }
 };
 struct EpiProj {
-  const float *bq, *bk, *bv, *bs;
+  const float* b;  // bq; projection g at b + g * pb
+  int64_t pb;
   float* P;
   int HC;
   template <class T>
@@ -608,8 +615,7 @@ struct EpiProj {
     for (int i = 0; i < T::per; ++i) {
       const int n = t.n0 + T::col_of(i);
       const int g = n / HC, q = n % HC;
-      const float* b = g == 0 ? bq : g == 1 ? bk : g == 2 ? bv : bs;
-      v[i] = t(T::row_of(i), T::col_of(i)) + (n < t.N ? b[q] : 0.f);
+      v[i] = t(T::row_of(i), T::col_of(i)) + (n < t.N ? b[g * pb + q] : 0.f);
     }
 #pragma unroll
     for (int i = 0; i < T::per; ++i) {
@@ -913,7 +919,7 @@ struct LoadZ1T {
 };
 struct EpiProjGrad {
   float* g;
-  int64_t wq, bq, wk, bk, wv, bv, ws, bs;
+  int64_t wq, bq, pw, pb;  // projection gi: weights wq + gi pw, bias bq + gi pb
   int HC, D;
   template <class T>
   __device__ void operator()(const T& t) const {
@@ -922,10 +928,8 @@ struct EpiProjGrad {
       if (row >= t.M || n >= t.N) continue;
       const int gi = row / HC, q = row % HC;
       const float v = t(r, cc);
-      const int64_t W = gi == 0 ? wq : gi == 1 ? wk : gi == 2 ? wv : ws;
-      const int64_t Bb = gi == 0 ? bq : gi == 1 ? bk : gi == 2 ? bv : bs;
-      if (n < D) g[W + (int64_t)q * D + n] = v;
-      else g[Bb + q] = v;
+      if (n < D) g[wq + gi * pw + (int64_t)q * D + n] = v;
+      else g[bq + gi * pb + q] = v;
     }
   }
 };
@@ -1048,13 +1052,13 @@ struct EpiTeEdge {
 };
 // [W_query; W_key; W_value; W_skip] as the B operand of dz0 = dP W: element (n, k) = W_{k/HC}[k%HC][n]
 struct LoadProjWT {
-  const float *wq, *wk, *wv, *ws;
+  const float* w;  // wq; projection g at w + g * pw
+  int64_t pw;
   int HC, D;
   static constexpr bool k_fast = false;
   __device__ float operator()(int n, int k) const {
     const int g = k / HC, r = k % HC;
-    const float* w = g == 0 ? wq : g == 1 ? wk : g == 2 ? wv : ws;
-    return w[(int64_t)r * D + n];
+    return w[g * pw + (int64_t)r * D + n];
   }
 };
 // GRUCell backward from dh' (memory is detached, so only the gate pre-activations get gradients):
@@ -1675,8 +1679,8 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgn_gru_edge");
   gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
-              LoadProjW{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
-              EpiProj{P + c.L.bq, P + c.L.bk, P + c.L.bv, P + c.L.bsk, c.P, HC}, nullptr, s);
+              LoadProjW{P + c.L.wq, c.L.pw, HC, D},
+              EpiProj{P + c.L.bq, c.L.pb, c.P, HC}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_proj");
   probe_begin(TGNX_K_SEG_FWD, s);
   tgn_attn_fwd<true><<<gridn(k.Rtr, 4), 256, 0, s>>>(c);
@@ -1693,7 +1697,7 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   TGNX_LAUNCH_CHECK("tgn_attn_bwd");
   // weight gradients (deferred split-K) ‖ ...
   const EpiStore e_dWe{G + c.L.we, nullptr, D + d, 0};
-  const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.wk, c.L.bk, c.L.wv, c.L.bv, c.L.wsk, c.L.bsk, HC, D};
+  const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D};
   const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D};
   const EpiGruWGrad e_dWg{G, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, Qm, D};
   probe_begin(TGNX_K_EDGE_BWD, s);
@@ -1708,7 +1712,7 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
                nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad2");
   gemm_launch<G32>(gemm_shape<G32>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
-              LoadProjWT{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
+              LoadProjWT{P + c.L.wq, c.L.pw, HC, D},
               EpiGruBwd{c.gates, c.mem, c.nid, c.dG, D}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_dz0");
   gemm2_launch<G32, G32>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, e_dWg,
@@ -1779,8 +1783,8 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   const LoadEdgeAttr ea{c.encE, c.e_id, c.ev_msg, D, d};
   gemm2_launch<G32, G32>(gemm_shape<G32>(Eq, HC, D + d, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
                EpiStore{c.Ep, nullptr, HC, 0}, nullptr, gemm_shape<G32>(Mq, 4 * HC, D, c.cnt + CNT_M),
-               LoadZ{c.Z0, c.mem, c.nid, D, 1}, LoadProjW{P + c.L.wq, P + c.L.wk, P + c.L.wv, P + c.L.wsk, HC, D},
-               EpiProj{P + c.L.bq, P + c.L.bk, P + c.L.bv, P + c.L.bsk, c.P, HC}, nullptr, s);
+               LoadZ{c.Z0, c.mem, c.nid, D, 1}, LoadProjW{P + c.L.wq, c.L.pw, HC, D},
+               EpiProj{P + c.L.bq, c.L.pb, c.P, HC}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_edge_proj");
   tgn_attn_fwd<false><<<gridn(Rq, 4, 1 << 20), 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_attn_fwd");
