@@ -1,0 +1,103 @@
+"""CPU tests of the TGN memory path's host surface (no GPU): the oracle pinned by the reference's own
+module outputs (tests/golden/msg.npz: modules/msg_func.py IdentityMessage; tests/golden/link_pred.npz:
+modules/decoder.py LinkPredictor), the aggregation semantics the kernels follow, and
+the C ABI's host-side entry points (parameter layout against the reference's parameter shapes,
+workspace / store sizing, argument rejection)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+
+def test_identity_message_matches_reference(golden):
+    from oracle.tgn_ref import identity_message
+    z = golden("msg.npz")
+    out = identity_message(*(torch.from_numpy(z[k]) for k in ("zs", "zd", "raw", "te")))
+    np.testing.assert_array_equal(out.numpy(), z["out"])
+    assert out.shape[1] == int(z["out_channels"][0])
+
+
+def test_link_predictor_matches_reference(golden):
+    from oracle.tgn_ref import RefLinkPredictor
+    z = golden("link_pred.npz")
+    lp = RefLinkPredictor(6)
+    sd = {k[2:].replace("__", "."): torch.from_numpy(z[k]) for k in z.files if k.startswith("p_")}
+    lp.load_state_dict(sd)
+    with torch.no_grad():
+        out = lp(torch.from_numpy(z["zs"]), torch.from_numpy(z["zd"]))
+    np.testing.assert_allclose(out.numpy(), z["out"], rtol=0, atol=1e-7)
+
+
+def test_last_aggregator_ties_and_empty_rows():
+    """LastAggregator (msg_agg.py:15-21): the message at the max t per node, ties -> the first
+    message (torch_scatter CPU), nodes without messages -> zeros; last_update fill 0."""
+    from oracle.tgn_ref import last_aggregate, mean_aggregate, scatter_max_first
+    msg = torch.arange(12, dtype=torch.float32).view(6, 2)
+    idx = torch.tensor([0, 2, 0, 2, 2, 0])
+    t = torch.tensor([5, 3, 5, 7, 7, 1])          # node 0: tie at t=5 (rows 0, 2); node 2: tie at 7 (rows 3, 4)
+    out = last_aggregate(msg, idx, t, 4)
+    np.testing.assert_array_equal(out.numpy(), np.array([[0, 1], [0, 0], [6, 7], [0, 0]], dtype=np.float32))
+    mx, arg = scatter_max_first(t, idx, 4)
+    np.testing.assert_array_equal(mx.numpy(), [5, 0, 7, 0])
+    np.testing.assert_array_equal(arg.numpy(), [0, 6, 3, 6])
+    mean = mean_aggregate(msg, idx, t, 4)
+    np.testing.assert_allclose(mean.numpy(), [[(0 + 4 + 10) / 3, (1 + 5 + 11) / 3], [0, 0],
+                                              [(2 + 6 + 8) / 3, (3 + 7 + 9) / 3], [0, 0]], rtol=1e-6)
+
+
+def _cfg(N=9227, E=157474, D=100, d=172, B=200, kn=1, aggr=0, heads=2):
+    from tgnx.tgn import TgnConfig
+    return TgnConfig(num_nodes=N, num_events=E, ring=10, mem_dim=D, msg_dim=d, heads=heads, max_batch=B, max_neg=kn,
+                     aggr=aggr, dropout=0.1, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8)
+
+
+@pytest.mark.parametrize("D,d", [(100, 172), (100, 1), (32, 16), (6, 2)])
+def test_param_layout_matches_reference_shapes(D, d):
+    """tgnx_tgn_param_layout: one slot per reference parameter (pyg_model_utils.py:10-36 modules),
+    sized as the reference's shapes, 16-B aligned, disjoint; the projection stride invariant."""
+    from oracle.tgn_ref import RefTGN
+    from tgnx import _lib
+    from tgnx.tgn import PARAM_ORDER, param_shapes
+    cfg = _cfg(D=D, d=d)
+    off = (ctypes.c_int64 * 22)()
+    _lib.call("tgnx_tgn_param_layout", ctypes.byref(cfg), off)
+    off = list(off)
+    ref = {k: tuple(v.shape) for k, v in RefTGN(50, d, hidden=D).named_parameters()}
+    shapes = param_shapes(D, d)
+    assert set(ref) == set(PARAM_ORDER) and all(ref[k] == shapes[k] for k in PARAM_ORDER)
+    spans = sorted((off[i], off[i] + int(np.prod(shapes[k]))) for i, k in enumerate(PARAM_ORDER))
+    for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
+        assert a1 <= b0
+    assert all(o % 4 == 0 for o in off[:-1]) and spans[-1][1] <= off[-1]
+    o = dict(zip(PARAM_ORDER, off))
+    w = [o[f"gnn.conv.lin_{k}.weight"] for k in ("query", "key", "value", "skip")]
+    b = [o[f"gnn.conv.lin_{k}.bias"] for k in ("query", "key", "value", "skip")]
+    assert len({y - x for x, y in zip(w, w[1:])}) == 1 and len({y - x for x, y in zip(b, b[1:])}) == 1
+
+
+def test_workspace_and_store_sizing():
+    from tgnx import _lib
+    L = _lib.lib()
+    cfg = _cfg()
+    assert L.tgnx_tgn_store_words(ctypes.byref(cfg)) == 4 * cfg.num_nodes + 2 * cfg.num_events
+    ws1 = L.tgnx_tgn_ws_bytes(ctypes.byref(cfg))
+    assert ws1 > 0
+    big = _cfg(kn=999)                                        # TGB eval negatives grow the workspace
+    assert L.tgnx_tgn_ws_bytes(ctypes.byref(big)) > ws1
+    review = _cfg(N=352637, E=4873540, d=1, kn=100, aggr=1)
+    assert 0 < L.tgnx_tgn_ws_bytes(ctypes.byref(review)) < (8 << 30)
+
+
+@pytest.mark.parametrize("field,value,msg", [("heads", 8, b"heads"), ("mem_dim", 101, b"mem_dim"),
+                                             ("max_batch", 5000, b"max_batch"), ("aggr", 3, b"aggr"),
+                                             ("ring", 0, b"ring")])
+def test_config_rejections(field, value, msg):
+    from tgnx import _lib
+    L = _lib.lib()
+    cfg = _cfg()
+    setattr(cfg, field, value)
+    assert L.tgnx_tgn_ws_bytes(ctypes.byref(cfg)) == 0
+    off = (ctypes.c_int64 * 22)()
+    assert L.tgnx_tgn_param_layout(ctypes.byref(cfg), off) != 0
+    assert msg in L.tgnx_last_error()

@@ -36,7 +36,7 @@ struct GemmCfg {
   static_assert(TM * (TN + 1) + 512 <= SMEM, "C tile + epilogue scratch must fit the operand LDS");
 };
 #ifndef TGNX_G32_KC
-#define TGNX_G32_KC 128
+#define TGNX_G32_KC 64
 #endif
 #ifndef TGNX_G32_PF
 #define TGNX_G32_PF 1
@@ -80,9 +80,15 @@ inline size_t gemm_partial_floats(const GemmShape& g) {
   return g.deferred ? (size_t)g.tiles_m * g.tiles_n * g.S * g.tm * g.tn : 0;
 }
 
-// Loader concept: `float operator()(int m_or_n, int k) const` (called only inside the runtime
-// bounds), plus `static constexpr bool k_fast` (true when consecutive k are consecutive in memory)
-// to pick the coalesced thread -> element mapping.
+// Loader concept: `static constexpr bool k_fast` (true when consecutive k are consecutive in memory,
+// picks the coalesced thread -> element mapping) and either
+//   * `float operator()(int m_or_n, int k) const` — a load whose address needs no other load, or
+//   * a two-phase gather: `using Idx`, `static constexpr bool row_idx`, `Idx index(int r, int k)`
+//     (the index loads: node ids, event ids, ...) and `float load(const Idx&, int r, int k)`.
+// The body issues every index load of a chunk before any data load (row_idx: once per tile, before
+// the K loop).  A data load whose address depends on an index load in the same batch would force
+// `s_waitcnt vmcnt(0)` per element — vmcnt retires in issue order — and serialise the chunk.
+// Loaders are called with in-range (clamped) r and k; out-of-range elements are zeroed afterwards.
 //
 // Epilogue concept: `template <class T> void operator()(const T& t) const` with T a GemmTile<TM, TN>,
 // run by all 256 threads of the workgroup; t(r, cc) is C[m0 + r][n0 + cc] for r < tm, cc < tn, M / N
@@ -101,19 +107,40 @@ struct GemmTile {
   __device__ static int col_of(int i) { return (threadIdx.x + 256 * i) % tn; }
 };
 
-// Row-major operand: element (r, k) at p[r * ld + k]  (k_fast)
+// Loaded values are never selected against at load time (`c ? v : 0.f` lets the compiler sink the
+// load into a branch whose join waits on it): the body zeroes out-of-range elements when it stashes
+// them, and loaders express constant entries arithmetically (v * 0/1 + c).
+__device__ __forceinline__ float f01(bool b) { return b ? 1.0f : 0.0f; }
+
+template <class L, class = void>
+struct LoaderTraits {  // plain loader
+  using Idx = int;
+  static constexpr bool row_idx = true;
+  __device__ static Idx index(const L&, int, int) { return 0; }
+  __device__ static float load(const L& l, const Idx&, int r, int k) { return l(r, k); }
+};
+template <class L>
+struct LoaderTraits<L, std::void_t<typename L::Idx>> {  // two-phase gather
+  using Idx = typename L::Idx;
+  static constexpr bool row_idx = L::row_idx;
+  __device__ static Idx index(const L& l, int r, int k) { return l.index(r, k); }
+  __device__ static float load(const L& l, const Idx& i, int r, int k) { return l.load(i, r, k); }
+};
+
+// Row-major operand: element (r, k) at p[r * ld + k]  (k_fast).  rows x ks bound the buffer (the body
+// clamps r, k to the GEMM's runtime bounds, which every call site keeps within it).
 struct LoadRowK {
   const float* p;
   int rows, ks, ld;
   static constexpr bool k_fast = true;
-  __device__ float operator()(int r, int k) const { return (r < rows && k < ks) ? p[(int64_t)r * ld + k] : 0.f; }
+  __device__ float operator()(int r, int k) const { return p[(int64_t)min(r, rows - 1) * ld + min(k, ks - 1)]; }
 };
 // Transposed operand: element (r, k) at p[k * ld + r]  (r fast)
 struct LoadKRow {
   const float* p;
   int rows, ks, ld;
   static constexpr bool k_fast = false;
-  __device__ float operator()(int r, int k) const { return (r < rows && k < ks) ? p[(int64_t)k * ld + r] : 0.f; }
+  __device__ float operator()(int r, int k) const { return p[(int64_t)min(k, ks - 1) * ld + min(r, rows - 1)]; }
 };
 
 struct GemmRt {
@@ -153,7 +180,10 @@ __device__ __forceinline__ void gemm_map(int tid, int i, int& r, int& kk) {
 // The order is laid over the RUNTIME tile counts (capacities are worst-case: 6,600 rows against
 // ~415 at run time would put every live tile on one XCD); partial-buffer offsets stay in capacity
 // tile numbering.
-constexpr int GEMM_GROUP = 4;
+#ifndef TGNX_GEMM_GROUP
+#define TGNX_GEMM_GROUP 4
+#endif
+constexpr int GEMM_GROUP = TGNX_GEMM_GROUP;
 struct GemmWork {
   int tile, s, tm, tn;
   bool ok;
@@ -200,44 +230,77 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
   constexpr int PF = CFG::PF;
   float ra[PF][LA], rb[PF][LB];
   // chunk ch -> register slot p (every load of the slot in flight at once)
-  auto fetch = [&](float* fa, float* fb, int ch) {
-    const int k0 = ch * KC, kc = max(0, min(KC, rt.Kr - k0));
+  using TA = LoaderTraits<AL>;
+  using TB = LoaderTraits<BL>;
+  typename TA::Idx ia[LA];
+  typename TB::Idx ib[LB];
+  const int mlast = rt.Mr - 1, nlast = rt.Nr - 1, klast = max(rt.Kr - 1, 0);
+  // index phase (every index load of the operand issued before any data load)
+  auto index_a = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       int r, kk;
       gemm_map<AL::k_fast, TM, KC>(tid, i, r, kk);
-      fa[i] = (kk < kc && m0 + r < rt.Mr) ? al(m0 + r, k0 + kk) : 0.f;
+      ia[i] = TA::index(al, min(m0 + r, mlast), min(k0 + kk, klast));
+    }
+  };
+  auto index_b = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      int r, kk;
+      gemm_map<BL::k_fast, TN, KC>(tid, i, r, kk);
+      ib[i] = TB::index(bl, min(n0 + r, nlast), min(k0 + kk, klast));
+    }
+  };
+  if (TA::row_idx) index_a(0);
+  if (TB::row_idx) index_b(0);
+  // chunk ch -> registers: clamped in-range loads (out-of-range elements are zeroed in stash)
+  auto fetch = [&](float* fa, float* fb, int ch) {
+    const int k0 = ch * KC, kc = max(0, min(KC, rt.Kr - k0));
+    if (!TA::row_idx) index_a(k0);
+    if (!TB::row_idx) index_b(k0);
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      int r, kk;
+      gemm_map<AL::k_fast, TM, KC>(tid, i, r, kk);
+      fa[i] = TA::load(al, ia[i], min(m0 + r, mlast), min(k0 + kk, klast));
     }
 #pragma unroll
     for (int i = 0; i < LB; ++i) {
       int r, kk;
       gemm_map<BL::k_fast, TN, KC>(tid, i, r, kk);
-      fb[i] = (kk < kc && n0 + r < rt.Nr) ? bl(n0 + r, k0 + kk) : 0.f;
+      fb[i] = TB::load(bl, ib[i], min(n0 + r, nlast), min(k0 + kk, klast));
     }
   };
-  auto stash1 = [&](float* S, const float* rv, auto kfast, auto rows, auto cnt) {
+  // registers -> LDS, zeroing elements outside the runtime bounds (rlast: last valid row of the tile
+  // origin r0; kc: valid k of the chunk)
+  auto stash1 = [&](float* S, const float* rv, auto kfast, auto rows, auto cnt, int r0, int rlast, int kc) {
     constexpr int ROWS = decltype(rows)::value, CNT = decltype(cnt)::value;
     if constexpr (decltype(kfast)::value) {
 #pragma unroll
       for (int i = 0; i < CNT; ++i) {
         int r, kk;
         gemm_map<true, ROWS, KC>(tid, i, r, kk);
-        S[r * PK + kk] = rv[i];
+        S[r * PK + kk] = (kk < kc && r0 + r <= rlast) ? rv[i] : 0.f;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < CNT; i += 4) {
         int r, kk;
         gemm_map<false, ROWS, KC>(tid, i, r, kk);
-        *reinterpret_cast<f32x4_t*>(S + r * PK + kk) = f32x4_t{rv[i], rv[i + 1], rv[i + 2], rv[i + 3]};
+        const bool rok = r0 + r <= rlast;
+        *reinterpret_cast<f32x4_t*>(S + r * PK + kk) =
+            f32x4_t{(rok && kk < kc) ? rv[i] : 0.f, (rok && kk + 1 < kc) ? rv[i + 1] : 0.f,
+                    (rok && kk + 2 < kc) ? rv[i + 2] : 0.f, (rok && kk + 3 < kc) ? rv[i + 3] : 0.f};
       }
     }
   };
-  auto stash = [&](const float* fa, const float* fb) {
+  auto stash = [&](const float* fa, const float* fb, int ch) {
+    const int kc = max(0, min(KC, rt.Kr - ch * KC));
     stash1(As, fa, std::integral_constant<bool, AL::k_fast>{}, std::integral_constant<int, TM>{},
-           std::integral_constant<int, LA>{});
+           std::integral_constant<int, LA>{}, m0, mlast, kc);
     stash1(Bs, fb, std::integral_constant<bool, BL::k_fast>{}, std::integral_constant<int, TN>{},
-           std::integral_constant<int, LB>{});
+           std::integral_constant<int, LB>{}, n0, nlast, kc);
   };
   // k permutation inside a 16-deep slab: MFMA step q of lane (li, lk) takes k = 4 lk + q, so each
   // lane's operands for 4 steps are one b128 LDS read (same permutation for A and B)
@@ -274,7 +337,7 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
     for (int p = 0; p < PF; ++p) {
       const int ch = c0 + p * g.S;
       if (ch < last) {
-        stash(ra[p], rb[p]);
+        stash(ra[p], rb[p], ch);
         __syncthreads();
         if (ch + PF * g.S < last) fetch(ra[p], rb[p], ch + PF * g.S);
         mfma_chunk();

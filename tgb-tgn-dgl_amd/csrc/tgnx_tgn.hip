@@ -514,14 +514,21 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nemit, 
 struct LoadGruA {
   const float* X;
   const float* mem;
-  const int64_t* list;  // node of row m (nullptr: base + m)
+  const int64_t* list;  // node of row m; with `ident`, rows are nodes base + m (list: any valid array)
   int64_t base;
-  int Qm, D;
+  int Qm, D, ident;
   static constexpr bool k_fast = true;
-  __device__ float operator()(int m, int k) const {
-    if (k < Qm) return X[(int64_t)m * Qm + k];
-    const int64_t v = list ? list[m] : base + m;
-    return mem[v * D + (k - Qm)];
+  using Idx = int64_t;  // the row's node (hoisted out of the K loop)
+  static constexpr bool row_idx = true;
+  // unconditional load + select: a branch here merges the loaded value in a phi, i.e. one
+  // s_waitcnt per element
+  __device__ Idx index(int m, int) const {
+    const int64_t v = list[m];
+    return ident ? base + m : v;
+  }
+  __device__ float load(Idx v, int m, int k) const {
+    const float* p = k < Qm ? X + (int64_t)m * Qm + k : mem + v * D + (k - Qm);
+    return *p;
   }
 };
 // GRU weights with gates interleaved by unit: row 4j+g = (r, z, n_input, n_hidden) of unit j over
@@ -530,10 +537,13 @@ struct LoadGruW {
   const float *wih, *whh;
   int Qm, D;
   static constexpr bool k_fast = true;
-  __device__ float operator()(int n, int k) const {
+  __device__ float operator()(int n, int k) const {  // branch-free
     const int j = n >> 2, g = n & 3;
-    if (k < Qm) return g == 3 ? 0.f : wih[(int64_t)(g * D + j) * Qm + k];
-    return g == 2 ? 0.f : whh[(int64_t)((g == 3 ? 2 : g) * D + j) * D + (k - Qm)];
+    const bool ih = k < Qm;
+    const int gr = ih ? min(g, 2) : (g == 3 ? 2 : g);  // weight row block (clamped: always a valid row)
+    const bool zero = ih ? g == 3 : g == 2;
+    const float* p = ih ? wih + (int64_t)(gr * D + j) * Qm + k : whh + (int64_t)(gr * D + j) * D + (k - Qm);
+    return *p * f01(!zero);
   }
 };
 // GRUCell (torch gru_cell: r, z = σ(gi + gh), n = tanh(gi_n + r gh_n), h' = (h - n) z + n)
@@ -572,16 +582,22 @@ struct LoadEdgeAttr {
   const float* ev_msg;
   int D, d;
   static constexpr bool k_fast = true;
-  __device__ float operator()(int e, int k) const {
-    if (k < D) return enc[(int64_t)e * D + k];
-    return ev_msg[e_id[e] * d + (k - D)];
+  using Idx = int64_t;  // the edge's event id (msg row)
+  static constexpr bool row_idx = true;
+  __device__ Idx index(int e, int) const { return e_id[e]; }
+  __device__ float load(Idx id, int e, int k) const {
+    const float* p = k < D ? enc + (int64_t)e * D + k : ev_msg + id * d + (k - D);
+    return *p;
   }
 };
 // same operand with rows / columns swapped (B operand of dW_edge = dEᵀ EA)
 struct LoadEdgeAttrT {
   LoadEdgeAttr a;
   static constexpr bool k_fast = false;
-  __device__ float operator()(int n, int e) const { return a(e, n); }
+  using Idx = int64_t;  // k = edge: the index changes per chunk
+  static constexpr bool row_idx = false;
+  __device__ Idx index(int, int e) const { return a.e_id[e]; }
+  __device__ float load(Idx id, int n, int e) const { return a.load(id, e, n); }
 };
 // node-embedding input row m: train z0 (GRU output), eval memory[nid[m]] (memory_module.py:121-122)
 struct LoadZ {
@@ -590,7 +606,16 @@ struct LoadZ {
   const int64_t* nid;
   int D, eval;
   static constexpr bool k_fast = true;
-  __device__ float operator()(int m, int k) const { return eval ? mem[nid[m] * D + k] : Z0[(int64_t)m * D + k]; }
+  using Idx = int64_t;
+  static constexpr bool row_idx = true;
+  __device__ Idx index(int m, int) const {
+    const int64_t v = nid[m];
+    return eval ? v : 0;
+  }
+  __device__ float load(Idx v, int m, int k) const {
+    const float* p = eval ? mem + v * D + k : Z0 + (int64_t)m * D + k;
+    return *p;
+  }
 };
 // stacked [W_query; W_key; W_value; W_skip] rows (n / HC selects the linear)
 struct LoadProjW {
@@ -915,7 +940,9 @@ struct LoadZ1T {
   const float* Z0;
   int D;
   static constexpr bool k_fast = false;
-  __device__ float operator()(int n, int m) const { return n < D ? Z0[(int64_t)m * D + n] : 1.0f; }
+  __device__ float operator()(int n, int m) const {
+    return Z0[(int64_t)m * D + min(n, D - 1)] * f01(n < D) + f01(n >= D);
+  }
 };
 struct EpiProjGrad {
   float* g;
@@ -941,11 +968,13 @@ struct LoadLpA {
   int D, S;
   static constexpr bool k_fast = false;
   __device__ float operator()(int r, int k) const {
-    const int lo = (int)ctl[TGNX_CTL_LO], nloc = (int)(ctl[TGNX_CTL_HI] - ctl[TGNX_CTL_LO]);
+    const int lo = (int)ctl[TGNX_CTL_LO], nloc = max(1, (int)(ctl[TGNX_CTL_HI] - ctl[TGNX_CTL_LO]));
     const int blk = k / nloc, i = lo + k % nloc;
     const float* ev = evs + (int64_t)i * S;
-    if (r < D) return blk == 0 ? ev[3 * D + r] + ev[4 * D + r] : 0.f;
-    return blk == 1 ? ev[3 * D + r - D] : blk == 2 ? ev[4 * D + r - D] : 0.f;
+    const bool src = r < D;
+    const int o = src ? r : r - D;
+    const float a = ev[3 * D + o], b = ev[4 * D + o];   // dhp, dhn
+    return src ? (blk == 0 ? a + b : 0.f) : (blk == 1 ? a : blk == 2 ? b : 0.f);
   }
 };
 struct LoadLpB {
@@ -954,7 +983,7 @@ struct LoadLpB {
   int D, S;
   static constexpr bool k_fast = false;
   __device__ float operator()(int n, int k) const {
-    const int lo = (int)ctl[TGNX_CTL_LO], nloc = (int)(ctl[TGNX_CTL_HI] - ctl[TGNX_CTL_LO]);
+    const int lo = (int)ctl[TGNX_CTL_LO], nloc = max(1, (int)(ctl[TGNX_CTL_HI] - ctl[TGNX_CTL_LO]));
     const int blk = k / nloc, i = lo + k % nloc;
     return evs[(int64_t)i * S + blk * D + n];
   }
@@ -1103,10 +1132,13 @@ struct LoadGruAT1 {
   const int64_t* nid;
   int Qm, D;
   static constexpr bool k_fast = false;
-  __device__ float operator()(int n, int m) const {
-    if (n < Qm) return X[(int64_t)m * Qm + n];
-    if (n < Qm + D) return mem[nid[m] * D + (n - Qm)];
-    return 1.0f;
+  using Idx = int64_t;  // k = sampled node: its id, per chunk
+  static constexpr bool row_idx = false;
+  __device__ Idx index(int, int m) const { return nid[m]; }
+  __device__ float load(Idx v, int n, int m) const {
+    const bool x = n < Qm, one = n >= Qm + D;
+    const float* p = x ? X + (int64_t)m * Qm + n : mem + v * D + min(n - Qm, D - 1);
+    return *p * f01(!one) + f01(one);
   }
 };
 struct EpiGruWGrad {
@@ -1144,7 +1176,7 @@ struct LoadGruWencT {
   static constexpr bool k_fast = false;
   __device__ float operator()(int n, int r) const {
     const int j = r >> 2, gg = r & 3;
-    return gg == 3 ? 0.f : wih[(int64_t)(gg * D + j) * Qm + off + n];
+    return wih[(int64_t)(min(gg, 2) * D + j) * Qm + off + n] * f01(gg != 3);
   }
 };
 // message-encoding -> Δt-encoding parameter grads (Last: the winner's Δt; Mean: each stored
@@ -1597,7 +1629,8 @@ static void gru_list(const Ctx& c, const Caps& k, const int64_t* list, const int
   const float* P = c.params;
   tgn_agg_emit<<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, 0, list, list_cnt, n_host, base);
   const GemmShape g1 = gemm_shape<G32>(mcap, 4 * c.D, c.Qm + c.D, list_cnt);
-  gemm_launch<G32>(g1, LoadGruA{c.X, c.mem, list, base, c.Qm, c.D}, LoadGruW{P + c.L.w_ih, P + c.L.w_hh, c.Qm, c.D},
+  gemm_launch<G32>(g1, LoadGruA{c.X, c.mem, list ? list : c.nid, base, c.Qm, c.D, list ? 0 : 1},
+                   LoadGruW{P + c.L.w_ih, P + c.L.w_hh, c.Qm, c.D},
               EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, list, base, c.D, c.Z0, c.gates}, nullptr, s);
 }
 
@@ -1671,11 +1704,32 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   // GRU over every sampled node ‖ lin_edge over every sampled edge
   const LoadEdgeAttr ea{c.encE, c.e_id, c.ev_msg, D, d};
   probe_begin(TGNX_K_EDGE_FWD, s);
-  gemm2_launch<G32, G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D},
+#ifdef TGNX_SPLIT_GRU  // timing experiment: the two GEMMs as separate launches
+#if TGNX_SPLIT_GRU == 2   // (timing only) plain A operand
+  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadRowK{c.X, k.Mtr, Qm + D, Qm},
+                   LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
+                   EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, nullptr, s);
+#elif TGNX_SPLIT_GRU == 3  // (timing only) plain B operand
+  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
+                   LoadRowK{P + c.L.w_ih, 4 * D, Qm + D, Qm},
+                   EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, nullptr, s);
+#elif TGNX_SPLIT_GRU == 4  // (timing only) plain epilogue
+  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
+                   LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D}, EpiStore{c.gates, nullptr, 4 * D, 0}, nullptr, s);
+#else
+  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
+                   LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
+                   EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, nullptr, s);
+#endif
+  gemm_launch<G32>(gemm_shape<G32>(k.Etr, HC, D + d, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
+                   EpiStore{c.Ep, nullptr, HC, 0}, nullptr, s);
+#else
+  gemm2_launch<G32, G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
                LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
                EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, nullptr,
                gemm_shape<G32>(k.Etr, HC, D + d, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
                EpiStore{c.Ep, nullptr, HC, 0}, nullptr, s);
+#endif
   probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgn_gru_edge");
   gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},

@@ -5,10 +5,10 @@
 set -e
 cd "$(dirname "$0")/../tgb-tgn-dgl_amd"
 make -s -j8
-rm -rf ../build_var
+# (only the named variants are rebuilt; others in build_var/ are kept)
 while [ $# -ge 2 ]; do
-  name=$1; flags=$2; shift 2
-  mkdir -p ../build_var/$name
+  name=$1; flags=$2; shift 2; BUILT="$BUILT ../build_var/$name/"
+  rm -rf ../build_var/$name; mkdir -p ../build_var/$name
   for src in csrc/*.hip; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -Wno-unused-result $flags \
       -c $src -o ../build_var/$name/$(basename $src .hip).o &
@@ -16,6 +16,6 @@ while [ $# -ge 2 ]; do
   cp build/tgnx_host.o ../build_var/$name/
 done
 wait
-for d in ../build_var/*/; do
+for d in $BUILT; do
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $d/libtgnx.so $d/*.o
 done
