@@ -329,10 +329,37 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
 // Aggregated message of node n (wave): IdentityMessage [mem[n], mem[other], raw, cos(w (t - lu[n]) + b)]
 // of its stored events, LastAggregator (first max t over [msg_s; msg_d], msg_agg.py:15-21) or
 // MeanAggregator (msg_agg.py:24-26); lu_new = max t (0 without messages, PyG scatter 'max').
+// Loads are batched: each 64-event chunk of the store is fetched lane-parallel (event id, other
+// endpoint, t) and broadcast by shuffles; the X row is filled 8 columns per lane at a time from
+// selected addresses (unconditional loads, encoding columns blended arithmetically).
+__device__ __forceinline__ int64_t shfl_i64(int64_t v, int src) {
+  return (int64_t)(((uint64_t)(uint32_t)__shfl((int)(v >> 32), src, 64) << 32) |
+                   (uint64_t)(uint32_t)__shfl((int)v, src, 64));
+}
+// stored event k of node n (k < sc: as source, else as destination): id, other endpoint, t
+struct StoreView {
+  int64_t so, sc, dof, tot;
+};
+__device__ __forceinline__ StoreView store_view(const Ctx& c, int64_t n) {
+  StoreView s;
+  s.so = c.st[4 * n];
+  s.sc = c.st[4 * n + 1];
+  s.dof = c.st[4 * n + 2];
+  s.tot = s.sc + c.st[4 * n + 3];
+  return s;
+}
+__device__ __forceinline__ void store_event(const Ctx& c, const StoreView& s, int64_t k, int64_t& e, int64_t& other,
+                                            float& t) {
+  const int64_t kk = max((int64_t)0, min(k, s.tot - 1));
+  const bool src = kk < s.sc;
+  e = *(src ? c.arena + s.so + kk : c.arena + s.dof + (kk - s.sc));
+  other = *(src ? c.ev_dst + e : c.ev_src + e);
+  t = c.ev_t[e];
+}
 __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
-  const int D = c.D, d = c.d, Qm = c.Qm;
-  const int64_t so = c.st[4 * n], sc = c.st[4 * n + 1], dof = c.st[4 * n + 2], dc = c.st[4 * n + 3];
-  const int tot = (int)(sc + dc);
+  const int D = c.D, d = c.d, Qm = c.Qm, enc0 = 2 * D + d;
+  const StoreView sv = store_view(c, n);
+  const int tot = (int)sv.tot;
   float* X = c.X + (int64_t)m * Qm;
   const float* P = c.params;
   if (tot == 0) {
@@ -346,37 +373,58 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
     }
     return;
   }
-  auto ev_of = [&](int k) -> int64_t { return k < sc ? c.arena[so + k] : c.arena[dof + (k - sc)]; };
   const float lun = (float)c.lu_buf[n];
+  const float* rowN = c.mem + n * D;
   if (c.aggr == 0) {
+    // winner: max t, first index in [msg_s; msg_d] order
     float tb = -INFINITY;
     int kb = 0x7fffffff;
-    for (int k = lane; k < tot; k += 64) {
-      const float t = c.ev_t[ev_of(k)];
-      if (t > tb) { tb = t; kb = k; }
+    int64_t eb = 0, ob = 0;
+    for (int k0 = 0; k0 < tot; k0 += 64) {
+      int64_t e, o;
+      float tt;
+      store_event(c, sv, k0 + lane, e, o, tt);
+      if (k0 + lane < tot && tt > tb) {
+        tb = tt;
+        kb = k0 + lane;
+        eb = e;
+        ob = o;
+      }
     }
     const float tm = wave_max(tb);
     int kk = tb == tm ? kb : 0x7fffffff;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) kk = min(kk, __shfl_xor(kk, o, 64));
-    const int64_t e = ev_of(kk);
-    const int64_t other = kk < sc ? c.ev_dst[e] : c.ev_src[e];
-    const float tr = c.ev_t[e] - lun;
-    for (int k = lane; k < Qm; k += 64) {
-      float x;
-      if (k < D) x = c.mem[n * D + k];
-      else if (k < 2 * D) x = c.mem[other * D + (k - D)];
-      else if (k < 2 * D + d) x = c.ev_msg[e * d + (k - 2 * D)];
-      else {
-        const int q = k - 2 * D - d;
-        float sn;
-        te_sincos(fmaf(P[c.L.te_w + q], tr, P[c.L.te_b + q]), sn, x);
-        if (grad) {
-          c.s0m[(int64_t)m * D + q] = sn;
-          c.s1m[(int64_t)m * D + q] = sn * tr;
-        }
+    const int wl = __ffsll(__ballot(kb == kk)) - 1;
+    const int64_t e = shfl_i64(eb, wl), other = shfl_i64(ob, wl);
+    const float tr = tm - lun;
+    const float* rowO = c.mem + other * D;
+    const float* raw = c.ev_msg + e * d;
+    for (int k0 = lane; k0 < Qm; k0 += 64 * 8) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = min(k0 + 64 * i, Qm - 1);
+        const float* p = k < D ? rowN + k : k < 2 * D ? rowO + (k - D) : k < enc0 ? raw + (k - 2 * D) : rowN;
+        v[i] = *p;
       }
-      X[k] = x;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = k0 + 64 * i;
+        if (k >= Qm) continue;
+        const bool enc = k >= enc0;
+        float cs = 0.f;
+        if (enc) {
+          const int q = k - enc0;
+          float sn;
+          te_sincos(fmaf(P[c.L.te_w + q], tr, P[c.L.te_b + q]), sn, cs);
+          if (grad) {
+            c.s0m[(int64_t)m * D + q] = sn;
+            c.s1m[(int64_t)m * D + q] = sn * tr;
+          }
+        }
+        X[k] = v[i] * f01(!enc) + cs;
+      }
     }
     if (lane == 0) {
       c.xw[m] = e;
@@ -384,33 +432,56 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
       c.lu[m] = tm;
     }
   } else {
+    // mean over the stored events in event order (PyG scatter-sum order, then / count)
+    const float inv = 1.0f / (float)tot;
     float tmax = -INFINITY;
-    for (int k = lane; k < Qm; k += 64) {
-      float s = 0.f, s0 = 0.f, s1 = 0.f;
-      for (int q = 0; q < tot; ++q) {  // event order: PyG scatter-sum order, then / count
-        const int64_t e = ev_of(q);
-        float x;
-        if (k < D) x = c.mem[n * D + k];
-        else if (k < 2 * D) x = c.mem[(q < sc ? c.ev_dst[e] : c.ev_src[e]) * D + (k - D)];
-        else if (k < 2 * D + d) x = c.ev_msg[e * d + (k - 2 * D)];
-        else {
-          const int qq = k - 2 * D - d;
-          const float dt = c.ev_t[e] - lun;
-          float sn;
-          te_sincos(fmaf(P[c.L.te_w + qq], dt, P[c.L.te_b + qq]), sn, x);
-          s0 += sn;
-          s1 += sn * dt;
+    for (int k0 = 0; k0 < Qm; k0 += 64 * 8) {
+      float s[8], s0[8], s1[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] = s0[i] = s1[i] = 0.f;
+      for (int q0 = 0; q0 < tot; q0 += 64) {
+        int64_t e_l, o_l;
+        float t_l;
+        store_event(c, sv, q0 + lane, e_l, o_l, t_l);
+        if (k0 == 0 && q0 + lane < tot) tmax = fmaxf(tmax, t_l);
+        const int nq = min(64, tot - q0);
+        for (int q = 0; q < nq; ++q) {
+          const int64_t e = shfl_i64(e_l, q), o = shfl_i64(o_l, q);
+          const float dt = __shfl(t_l, q, 64) - lun;
+          float v[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int k = min(k0 + lane + 64 * i, Qm - 1);
+            const float* p = k < D ? rowN + k : k < 2 * D ? c.mem + o * D + (k - D)
+                                                  : k < enc0 ? c.ev_msg + e * d + (k - 2 * D) : rowN;
+            v[i] = *p;
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int k = k0 + lane + 64 * i;
+            const bool enc = k >= enc0 && k < Qm;
+            float cs = 0.f, sn = 0.f;
+            if (enc) {
+              const int qq = k - enc0;
+              te_sincos(fmaf(P[c.L.te_w + qq], dt, P[c.L.te_b + qq]), sn, cs);
+            }
+            s[i] += v[i] * f01(!enc) + cs;
+            s0[i] += sn;
+            s1[i] += sn * dt;
+          }
         }
-        s += x;
       }
-      X[k] = s / (float)tot;
-      if (grad && k >= 2 * D + d) {
-        const int qq = k - 2 * D - d;
-        c.s0m[(int64_t)m * D + qq] = s0 / (float)tot;
-        c.s1m[(int64_t)m * D + qq] = s1 / (float)tot;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = k0 + lane + 64 * i;
+        if (k >= Qm) continue;
+        X[k] = s[i] / (float)tot;
+        if (grad && k >= enc0) {
+          c.s0m[(int64_t)m * D + (k - enc0)] = s0[i] * inv;
+          c.s1m[(int64_t)m * D + (k - enc0)] = s1[i] * inv;
+        }
       }
     }
-    for (int q = lane; q < tot; q += 64) tmax = fmaxf(tmax, c.ev_t[ev_of(q)]);
     tmax = wave_max(tmax);
     if (lane == 0) {
       c.xw[m] = 1;
@@ -423,73 +494,76 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
 // last_update the GRU step gives node u (memory_module.py:175-176): max t over its stored messages, 0
 // without messages (PyG scatter 'max' fill); wave-uniform
 __device__ float store_tmax(const Ctx& c, int64_t u, int lane) {
-  const int64_t so = c.st[4 * u], sc = c.st[4 * u + 1], dof = c.st[4 * u + 2], dc = c.st[4 * u + 3];
-  const int tot = (int)(sc + dc);
-  if (tot == 0) return 0.f;
+  const StoreView sv = store_view(c, u);
+  if (sv.tot == 0) return 0.f;
   float tb = -INFINITY;
-  for (int k = lane; k < tot; k += 64) tb = fmaxf(tb, c.ev_t[k < sc ? c.arena[so + k] : c.arena[dof + (k - sc)]]);
+  for (int64_t k0 = 0; k0 < sv.tot; k0 += 64) {
+    const int64_t kk = min(k0 + lane, sv.tot - 1);
+    const int64_t e = *(kk < sv.sc ? c.arena + sv.so + kk : c.arena + sv.dof + (kk - sv.sc));
+    tb = fmaxf(tb, c.ev_t[e]);   // clamped duplicates of the last event do not change the max
+  }
   return wave_max(tb);
 }
 
-// K3: blocks [0, nemit): sampled edges, thread per centre (centre-ascending, ring order = e_id
-// descending); [nemit, nemit + nenc): the Δt encoding of every sampled edge, wave per centre
-// (cos -> the lin_edge operand, sin -> its backward; emb_module.py:69-72, rel_t = last_update[src] - t);
-// the rest: mode 0 aggregation over the sampled nodes (train) + zeroing of the backward
+// K3: blocks [0, nedge): one wave per (centre x, ring slot j) — the sampled edge record (centre-
+// ascending, ring order = e_id descending, neighbor_loader.py:26-50; output slot = the centre's edge
+// offset + valid slots before j, by ballot) and its Δt encoding (cos -> the lin_edge operand, sin ->
+// its backward; emb_module.py:69-72, rel_t = last_update[src] - t, with last_update as the GRU step
+// gives it: the max t of the neighbour's stored messages, 0 without any).  Every load of a wave
+// depends on at most the previous round (ring row; neighbour; its store; arena; t).
+// The rest: mode 0 aggregation over the sampled nodes (train) + zeroing of the backward
 // accumulators, mode 1 last_update of the sampled nodes from the buffer (eval scoring), mode 2
 // aggregation over a node list (eval update / flush; list == nullptr: nodes base + m).
-__global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nemit, int nenc, const int64_t* list,
+__global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, const int64_t* list,
                                                     const int* list_cnt, int n_host, int64_t base) {
   if (mode != 2) {
     const int B = (int)c.ctl[TGNX_CTL_B];
     if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   }
-  if ((int)blockIdx.x < nemit) {
-    const int R = c.cnt[CNT_R];
-    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < R; x += nemit * blockDim.x) {
-      const int64_t v = c.cent[x];
-      int o = c.ceoff[x];
-      for (int j = 0; j < c.K; ++j) {
-        const int64_t e = c.eid[v * c.K + j];
-        if (e < 0) continue;
-        c.e_j[o] = (int)c.assoc[c.nbr[v * c.K + j]];
-        c.e_c[o] = x;
-        c.e_id[o] = e;
-        c.e_t[o] = c.rt[v * c.K + j];
-        ++o;
-      }
-    }
-    return;
-  }
   const int lane = threadIdx.x & 63;
-  if ((int)blockIdx.x < nemit + nenc) {
-    const int R = c.cnt[CNT_R], D = c.D;
+  if ((int)blockIdx.x < nedge) {
+    const int R = c.cnt[CNT_R], K = c.K, D = c.D;
     const float* tw = c.params + c.L.te_w;
     const float* tb = c.params + c.L.te_b;
-    for (int x = (blockIdx.x - nemit) * 4 + (threadIdx.x >> 6); x < R; x += nenc * 4) {
+    for (int pr = blockIdx.x * 4 + (threadIdx.x >> 6); pr < R * K; pr += nedge * 4) {
+      const int x = pr / K, j = pr - x * K;
       const int64_t v = c.cent[x];
-      int o = c.ceoff[x];
-      for (int j = 0; j < c.K; ++j) {
-        if (c.eid[v * c.K + j] < 0) continue;
-        const int64_t u = c.nbr[v * c.K + j];
-        const float lu = mode == 0 ? store_tmax(c, u, lane) : (float)c.lu_buf[u];
-        const float dt = lu - c.rt[v * c.K + j];
-        for (int q = lane; q < D; q += 64) {
-          const float a = fmaf(tw[q], dt, tb[q]);
-          if (mode == 0) {
-            float sn, cs;
-            te_sincos(a, sn, cs);
-            c.encE[(int64_t)o * D + q] = cs;
-            c.sinE[(int64_t)o * D + q] = sn;
-          } else {
-            c.encE[(int64_t)o * D + q] = te_cos(a);
-          }
+      const int ls = min(lane, K - 1);
+      const int64_t e_l = c.eid[v * K + ls];
+      const int64_t u_l = c.nbr[v * K + ls];
+      const float t_l = c.rt[v * K + ls];
+      const uint64_t valid = __ballot(lane < K && e_l >= 0);
+      if (!((valid >> j) & 1ull)) continue;
+      const int o = c.ceoff[x] + __popcll(valid & ((1ull << j) - 1ull));
+      const int64_t e = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(e_l >> 32), j, 64) << 32) |
+                                  (uint64_t)(uint32_t)__shfl((int)e_l, j, 64));
+      const int64_t u = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(u_l >> 32), j, 64) << 32) |
+                                  (uint64_t)(uint32_t)__shfl((int)u_l, j, 64));
+      const float te = __shfl(t_l, j, 64);
+      const int ju = (int)c.assoc[u];
+      const float lu = mode == 0 ? store_tmax(c, u, lane) : (float)c.lu_buf[u];
+      if (lane == 0) {
+        c.e_j[o] = ju;
+        c.e_c[o] = x;
+        c.e_id[o] = e;
+        c.e_t[o] = te;
+      }
+      const float dt = lu - te;
+      for (int q = lane; q < D; q += 64) {
+        const float a = fmaf(tw[q], dt, tb[q]);
+        if (mode == 0) {
+          float sn, cs;
+          te_sincos(a, sn, cs);
+          c.encE[(int64_t)o * D + q] = cs;
+          c.sinE[(int64_t)o * D + q] = sn;
+        } else {
+          c.encE[(int64_t)o * D + q] = te_cos(a);
         }
-        ++o;
       }
     }
     return;
   }
-  const int bid = blockIdx.x - nemit - nenc, nb = gridDim.x - nemit - nenc;
+  const int bid = blockIdx.x - nedge, nb = gridDim.x - nedge;
   if (mode == 1) {
     const int M = c.cnt[CNT_M];
     for (int x = bid * blockDim.x + threadIdx.x; x < M; x += nb * blockDim.x) c.lu[x] = (float)c.lu_buf[c.nid[x]];
@@ -1627,7 +1701,7 @@ static inline int gridn(int64_t n, int per, int cap = 4096) {
 static void gru_list(const Ctx& c, const Caps& k, const int64_t* list, const int* list_cnt, int n_host, int64_t base,
                      int mcap, hipStream_t s) {
   const float* P = c.params;
-  tgn_agg_emit<<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, 0, list, list_cnt, n_host, base);
+  tgn_agg_emit<<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
   const GemmShape g1 = gemm_shape<G32>(mcap, 4 * c.D, c.Qm + c.D, list_cnt);
   gemm_launch<G32>(g1, LoadGruA{c.X, c.mem, list ? list : c.nid, base, c.Qm, c.D, list ? 0 : 1},
                    LoadGruW{P + c.L.w_ih, P + c.L.w_hh, c.Qm, c.D},
@@ -1696,9 +1770,9 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   tgn_scan<true><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
   probe_end(TGNX_K_ASSEMBLE, s);
   TGNX_LAUNCH_CHECK("tgn_scan");
-  const int nemit = gridn(k.Rtr, 256), nenc = gridn(k.Rtr, 4, 2048);
+  const int nedge = gridn((int64_t)k.Rtr * c.K, 4, 4096);
   probe_begin(TGNX_K_EDGE_META, s);
-  tgn_agg_emit<<<nemit + nenc + gridn(k.Mtr, 4, 2048), 256, 0, s>>>(c, 0, nemit, nenc, nullptr, nullptr, 0, 0);
+  tgn_agg_emit<<<nedge + gridn(k.Mtr, 4, 2048), 256, 0, s>>>(c, 0, nedge, nullptr, nullptr, 0, 0);
   probe_end(TGNX_K_EDGE_META, s);
   TGNX_LAUNCH_CHECK("tgn_agg_emit");
   // GRU over every sampled node ‖ lin_edge over every sampled edge
@@ -1831,8 +1905,8 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   TGNX_LAUNCH_CHECK("tgn_mark");
   tgn_scan<false><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_scan");
-  const int nemit = gridn(Rq, 256), nenc = gridn(Rq, 4, 4096);
-  tgn_agg_emit<<<nemit + nenc + gridn(Mq, 256), 256, 0, s>>>(c, 1, nemit, nenc, nullptr, nullptr, 0, 0);
+  const int nedge = gridn((int64_t)Rq * c.K, 4, 4096);
+  tgn_agg_emit<<<nedge + gridn(Mq, 256), 256, 0, s>>>(c, 1, nedge, nullptr, nullptr, 0, 0);
   TGNX_LAUNCH_CHECK("tgn_emit");
   const LoadEdgeAttr ea{c.encE, c.e_id, c.ev_msg, D, d};
   gemm2_launch<G32, G32>(gemm_shape<G32>(Eq, HC, D + d, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
