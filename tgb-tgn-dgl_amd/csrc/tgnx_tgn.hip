@@ -733,6 +733,7 @@ struct EpiProj {
 __device__ __forceinline__ float att_keep(const Ctx& c, uint64_t seed, int x, int e, int h) {
   return keep32(drop_base(seed, 7, (uint64_t)c.cent[x], (uint64_t)c.e_id[e]), (uint32_t)h, c.p, c.inv_keep);
 }
+constexpr int ATT_EB = 16;  // edges whose neighbour rows are loaded in one batch (ring K <= 32: <= 2 batches)
 template <bool TRAIN>
 __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
   const int B = (int)c.ctl[TGNX_CTL_B];
@@ -742,22 +743,31 @@ __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
   const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (x >= R) return;
   const int C = c.C, HC = c.HC;
-  const bool okl = lane < C;
-  const int l0 = okl ? lane : 0;
+  const float on = f01(lane < C);
+  const int l0 = min(lane, C - 1);
   const int i = c.cent_loc[x];
   const float* Pi = c.P + (int64_t)i * 4 * HC;
   const float q0 = Pi[l0], q1 = Pi[C + l0];
   const float sqc = sqrtf((float)C);
   const int e0 = c.ceoff[x], ne = c.ceoff[x + 1] - e0;
+  const int jl = c.e_j[e0 + min(lane, max(ne - 1, 0))];   // lane e: the neighbour row of edge e
   float my0 = -INFINITY, my1 = -INFINITY;
-  for (int e = 0; e < ne; ++e) {
-    const float* Pj = c.P + (int64_t)c.e_j[e0 + e] * 4 * HC;
-    const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
-    float p0 = okl ? q0 * (Pj[HC + l0] + Ee[l0]) : 0.f;
-    float p1 = okl ? q1 * (Pj[HC + C + l0] + Ee[C + l0]) : 0.f;
-    p0 = wave_sum(p0) / sqc;
-    p1 = wave_sum(p1) / sqc;
-    if (lane == e) { my0 = p0; my1 = p1; }
+  for (int b = 0; b < ne; b += ATT_EB) {
+    float k0[ATT_EB], k1[ATT_EB];
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {  // all loads of the batch in flight
+      const int e = min(b + u, ne - 1);
+      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
+      k0[u] = Pj[HC + l0] + Ee[l0];
+      k1[u] = Pj[HC + C + l0] + Ee[C + l0];
+    }
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      if (b + u >= ne) break;
+      const float p0 = wave_sum(q0 * k0[u] * on) / sqc, p1 = wave_sum(q1 * k1[u] * on) / sqc;
+      if (lane == b + u) { my0 = p0; my1 = p1; }
+    }
   }
   const float mx0 = wave_max(my0), mx1 = wave_max(my1);
   const float ex0 = lane < ne ? expf(my0 - mx0) : 0.f, ex1 = lane < ne ? expf(my1 - mx1) : 0.f;
@@ -773,14 +783,24 @@ __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
     }
   }
   float o0 = 0.f, o1 = 0.f;
-  for (int e = 0; e < ne; ++e) {
-    const float b0 = __shfl(t0, e, 64), b1 = __shfl(t1, e, 64);
-    const float* Pj = c.P + (int64_t)c.e_j[e0 + e] * 4 * HC;
-    const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
-    o0 += (Pj[2 * HC + l0] + Ee[l0]) * b0;
-    o1 += (Pj[2 * HC + C + l0] + Ee[C + l0]) * b1;
+  for (int b = 0; b < ne; b += ATT_EB) {
+    float v0[ATT_EB], v1[ATT_EB];
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      const int e = min(b + u, ne - 1);
+      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
+      v0[u] = Pj[2 * HC + l0] + Ee[l0];
+      v1[u] = Pj[2 * HC + C + l0] + Ee[C + l0];
+    }
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      if (b + u >= ne) break;
+      o0 += v0[u] * __shfl(t0, b + u, 64);
+      o1 += v1[u] * __shfl(t1, b + u, 64);
+    }
   }
-  if (okl) {
+  if (lane < C) {
     c.Zc[(int64_t)x * HC + lane] = o0 + Pi[3 * HC + lane];
     c.Zc[(int64_t)x * HC + C + lane] = o1 + Pi[3 * HC + C + lane];
   }
@@ -945,59 +965,80 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
   if (x >= R) return;
   const int C = c.C, HC = c.HC;
   const bool okl = lane < C;
-  const int l0 = okl ? lane : 0;
+  const float on = f01(okl);
+  const int l0 = min(lane, C - 1);
   const int i = c.cent_loc[x];
   const float* Pi = c.P + (int64_t)i * 4 * HC;
   float* dPi = c.dP + (int64_t)i * 4 * HC;
   const float q0 = Pi[l0], q1 = Pi[C + l0];
-  const float g0 = okl ? c.dZc[(int64_t)x * HC + lane] : 0.f, g1 = okl ? c.dZc[(int64_t)x * HC + C + lane] : 0.f;
+  const float g0 = c.dZc[(int64_t)x * HC + l0] * on, g1 = c.dZc[(int64_t)x * HC + C + l0] * on;
   const float sqc = sqrtf((float)C);
   const int e0 = c.ceoff[x], ne = c.ceoff[x + 1] - e0;
+  const int le = e0 + min(lane, max(ne - 1, 0));
+  const int jl = c.e_j[le];
   const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-  float a0 = 0.f, a1 = 0.f, k0v = 1.f, k1v = 1.f;
-  if (lane < ne) {
-    a0 = c.alpha[(int64_t)(e0 + lane) * 2];
-    a1 = c.alpha[(int64_t)(e0 + lane) * 2 + 1];
-    if (c.drop) {
-      k0v = att_keep(c, seed, x, e0 + lane, 0);
-      k1v = att_keep(c, seed, x, e0 + lane, 1);
-    }
+  const float al0 = c.alpha[(int64_t)le * 2], al1 = c.alpha[(int64_t)le * 2 + 1];
+  const float a0 = lane < ne ? al0 : 0.f, a1 = lane < ne ? al1 : 0.f;
+  float k0v = 1.f, k1v = 1.f;
+  if (lane < ne && c.drop) {
+    k0v = att_keep(c, seed, x, e0 + lane, 0);
+    k1v = att_keep(c, seed, x, e0 + lane, 1);
   }
   // d alpha~_eh = Σ_{ch in h} dout (v_j + e); d alpha = d alpha~ * keep
   float da0 = 0.f, da1 = 0.f;
-  for (int e = 0; e < ne; ++e) {
-    const float* Pj = c.P + (int64_t)c.e_j[e0 + e] * 4 * HC;
-    const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
-    float p0 = okl ? g0 * (Pj[2 * HC + l0] + Ee[l0]) : 0.f;
-    float p1 = okl ? g1 * (Pj[2 * HC + C + l0] + Ee[C + l0]) : 0.f;
-    p0 = wave_sum(p0);
-    p1 = wave_sum(p1);
-    if (lane == e) { da0 = p0 * k0v; da1 = p1 * k1v; }
+  for (int b = 0; b < ne; b += ATT_EB) {
+    float v0[ATT_EB], v1[ATT_EB];
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      const int e = min(b + u, ne - 1);
+      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
+      v0[u] = Pj[2 * HC + l0] + Ee[l0];
+      v1[u] = Pj[2 * HC + C + l0] + Ee[C + l0];
+    }
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      if (b + u >= ne) break;
+      const float p0 = wave_sum(g0 * v0[u]), p1 = wave_sum(g1 * v1[u]);
+      if (lane == b + u) { da0 = p0 * k0v; da1 = p1 * k1v; }
+    }
   }
   // softmax backward: d score = alpha (d alpha - Σ alpha d alpha)
   const float s0 = wave_sum(a0 * da0), s1 = wave_sum(a1 * da1);
   const float ds0 = a0 * (da0 - s0), ds1 = a1 * (da1 - s1);
   const float t0 = a0 * k0v, t1 = a1 * k1v;
   float dq0 = 0.f, dq1 = 0.f;
-  for (int e = 0; e < ne; ++e) {
-    const float d0 = __shfl(ds0, e, 64) / sqc, d1 = __shfl(ds1, e, 64) / sqc;
-    const float b0 = __shfl(t0, e, 64), b1 = __shfl(t1, e, 64);
-    const int j = c.e_j[e0 + e];
-    const float* Pj = c.P + (int64_t)j * 4 * HC;
-    const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
-    float* dPj = c.dP + (int64_t)j * 4 * HC;
-    float* dEe = c.dE + (int64_t)(e0 + e) * HC;
-    if (okl) {
-      dq0 += d0 * (Pj[HC + lane] + Ee[lane]);
-      dq1 += d1 * (Pj[HC + C + lane] + Ee[C + lane]);
-      const float dk0 = d0 * q0, dk1 = d1 * q1;
-      const float dv0 = b0 * g0, dv1 = b1 * g1;
-      dEe[lane] = dk0 + dv0;
-      dEe[C + lane] = dk1 + dv1;
-      atomicAdd(&dPj[HC + lane], dk0);
-      atomicAdd(&dPj[HC + C + lane], dk1);
-      atomicAdd(&dPj[2 * HC + lane], dv0);
-      atomicAdd(&dPj[2 * HC + C + lane], dv1);
+  for (int b = 0; b < ne; b += ATT_EB) {
+    float kk0[ATT_EB], kk1[ATT_EB];
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      const int e = min(b + u, ne - 1);
+      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
+      kk0[u] = Pj[HC + l0] + Ee[l0];
+      kk1[u] = Pj[HC + C + l0] + Ee[C + l0];
+    }
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      const int e = b + u;
+      if (e >= ne) break;
+      const float d0 = __shfl(ds0, e, 64) / sqc, d1 = __shfl(ds1, e, 64) / sqc;
+      const float b0 = __shfl(t0, e, 64), b1 = __shfl(t1, e, 64);
+      const int j = __shfl(jl, e, 64);
+      float* dPj = c.dP + (int64_t)j * 4 * HC;
+      float* dEe = c.dE + (int64_t)(e0 + e) * HC;
+      dq0 += d0 * kk0[u];
+      dq1 += d1 * kk1[u];
+      if (okl) {
+        const float dk0 = d0 * q0, dk1 = d1 * q1;
+        const float dv0 = b0 * g0, dv1 = b1 * g1;
+        dEe[lane] = dk0 + dv0;
+        dEe[C + lane] = dk1 + dv1;
+        atomicAdd(&dPj[HC + lane], dk0);
+        atomicAdd(&dPj[HC + C + lane], dk1);
+        atomicAdd(&dPj[2 * HC + lane], dv0);
+        atomicAdd(&dPj[2 * HC + C + lane], dv1);
+      }
     }
   }
   if (okl) {
