@@ -407,10 +407,19 @@ __device__ void gemm_fix_tile(const GemmFix<CFG, EPI>& f, int tile, float* smem)
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
+      // every split's partial in flight at once (clamped loads, masked sum; split order fixed)
+      constexpr int SU = 8;
       f32x4_t sum = {0.f, 0.f, 0.f, 0.f};
-      for (int q = 0; q < rt.Sr; ++q) {
-        const f32x4_t* pq = reinterpret_cast<const f32x4_t*>(f.part + ((size_t)tile * f.g.S + q) * TM * TN);
-        sum += pq[((wv * FM + i) * FN + j) * 64 + lane];
+      for (int q0 = 0; q0 < rt.Sr; q0 += SU) {
+        f32x4_t pv[SU];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int q = min(q0 + u, rt.Sr - 1);
+          pv[u] = reinterpret_cast<const f32x4_t*>(f.part + ((size_t)tile * f.g.S + q) * TM * TN)
+              [((wv * FM + i) * FN + j) * 64 + lane];
+        }
+#pragma unroll
+        for (int u = 0; u < SU; ++u) sum += pv[u] * f01(q0 + u < rt.Sr);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) Ct[(wr + 16 * i + lk * 4 + r) * PB + wc + 16 * j + li] = sum[r];

@@ -1309,18 +1309,36 @@ struct EpiTeMsg {
 struct TeReduceTail {
   Ctx c;
   int rows_edge, rows_msg;
+  // tail block b: columns [64 b, 64 b + 64) of the 2D (w, b) gradients; wave w sums the rows
+  // [w R / 4, (w + 1) R / 4) with 8 loads in flight, the 4 wave sums combine in fixed order
   __device__ void operator()(int bid) const {
-    if (bid != 0) return;
+    __shared__ float red[4][64];
+    const int D = c.D, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int x = bid * 64 + lane;
+    if (bid * 64 >= 2 * D) return;
     const int B = (int)c.ctl[TGNX_CTL_B];
     if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-    const int D = c.D;
     const int E = c.cnt[CNT_E], M = c.cnt[CNT_M];
     const int re = min(rows_edge, (E + G32::TM - 1) / G32::TM), rm = min(rows_msg, (M + G32::TM - 1) / G32::TM);
-    for (int x = threadIdx.x; x < 2 * D; x += blockDim.x) {
-      float s = 0.f;
-      for (int r = 0; r < re; ++r) s += c.tgp[(int64_t)r * 2 * D + x];
-      for (int r = 0; r < rm; ++r) s += c.tgp[(int64_t)(rows_edge + r) * 2 * D + x];
-      c.grads[(x < D ? c.L.te_w : c.L.te_b - D) + x] = s;
+    const int R = re + rm, r0 = wv * R / 4, r1 = (wv + 1) * R / 4;
+    const int xc = min(x, 2 * D - 1);
+    float s = 0.f;
+    for (int r = r0; r < r1; r += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int rr = min(r + u, r1 - 1);
+        const int row = rr < re ? rr : rows_edge + (rr - re);
+        v[u] = c.tgp[(int64_t)row * 2 * D + xc];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u] * f01(r + u < r1);
+    }
+    red[wv][lane] = s;
+    __syncthreads();
+    if (wv == 0 && x < 2 * D) {
+      const float tot = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+      c.grads[(x < D ? c.L.te_w : c.L.te_b - D) + x] = tot;
     }
   }
 };
@@ -1888,7 +1906,7 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
                c.pD, gemm_shape<G32>(k.Mtr, D, 4 * D, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
                LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
-  gemm_fixup_launch(1, TeReduceTail{c, rows_edge, rows_msg}, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
+  gemm_fixup_launch((2 * D + 63) / 64, TeReduceTail{c, rows_edge, rows_msg}, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
                     gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
                     gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg));
   TGNX_LAUNCH_CHECK("tgn_wgrad_fixup");
