@@ -222,6 +222,30 @@ int tgnx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, 
                   int64_t ldb, int32_t trans_b, float* C, int64_t ldc, const float* bias, int32_t accumulate,
                   void* ws, size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------- t-CSR temporal graph
+ * TGL's ext_full.npz (indptr int64[N+1], indices int64[nnz], eid int64[nnz], ts fp32[nnz]) that
+ * utils.py:73 loads (generated by tgb_gen_graph.py, README.md:5, absent from the reference) and TGL's
+ * "recent" neighbour sampler (its C++ sampler_core, README.md:2, also absent).  Rows are ordered by
+ * event id (= time order for a chronological stream; *chrono = 0 reports a stream whose t decreases
+ * somewhere, for which only the event-id cutoff is meaningful).  Parity unpinned for TGL itself; the
+ * event-id cutoff is pinned by the reference's LastNeighborLoader goldens. */
+size_t tgnx_tcsr_build_ws_bytes(int64_t num_events, int32_t add_reverse);
+/* events (src[e], dst[e], t[e]), e = event id; add_reverse: also the (dst -> src) entry (TGL
+ * --add_reverse; LastNeighborLoader inserts both directions).  nnz = E or 2E; nnz < 2^31. */
+int tgnx_tcsr_build(const int64_t* src, const int64_t* dst, const float* t, int64_t num_events, int64_t num_nodes,
+                    int32_t add_reverse, int64_t* indptr, int64_t* indices, int64_t* eid, float* ts, int32_t* chrono,
+                    void* ws, size_t ws_bytes, void* stream);
+/* For each root q: the K most recent row entries before the cutoff, newest first, into
+ * out_*[q*K + j] (j < out_cnt[q]; the rest nbr = eid = -1, t = -1):
+ *   mode 0: eid < cut (cut_eid[q], or cut_eid_all when cut_eid is NULL) — LastNeighborLoader's ring
+ *           row at a batch start when cut = the batch's first event id (neighbor_loader.py:52-104);
+ *   mode 1: ts < cut_t[q] (TGL: strictly before the root's timestamp).
+ * out_cnt may be NULL. */
+int tgnx_tcsr_sample(const int64_t* indptr, const int64_t* indices, const int64_t* eid, const float* ts,
+                     int64_t num_nodes, int32_t K, const int64_t* roots, int64_t Q, int32_t mode, const int64_t* cut_eid,
+                     int64_t cut_eid_all, const float* cut_t, int64_t* out_nbr, int64_t* out_eid, float* out_t,
+                     int32_t* out_cnt, void* stream);
+
 /* ---------------------------------------------------------------- TGN memory path
  * SURVEY §8 a14–a16 (the PyG TGN of the reference modules/ directory, wired as pyg_model_utils.py:10-36):
  * TGNMemory (modules/memory_module.py:25-215) with IdentityMessage (msg_func.py:12-18) and

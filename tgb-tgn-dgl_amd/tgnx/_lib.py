@@ -42,6 +42,9 @@ SIGNATURES = {
     "tgnx_tgn_eval_step": (ctypes.c_int, [P, P, c_i32, c_vp]),
     "tgnx_tgn_flush": (ctypes.c_int, [P, P, c_vp]),
     "tgnx_tgn_apply_rows": (ctypes.c_int, [P, P, P, c_i64, c_vp]),
+    "tgnx_tcsr_build_ws_bytes": (c_sz, [c_i64, c_i32]),
+    "tgnx_tcsr_build": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i32, P, P, P, P, P, P, c_sz, c_vp]),
+    "tgnx_tcsr_sample": (ctypes.c_int, [P, P, P, P, c_i64, c_i32, P, c_i64, c_i32, P, c_i64, P, P, P, P, P, c_vp]),
     "tgnx_gemm_f32_ws_bytes": (c_sz, [c_i64, c_i64, c_i64]),
     "tgnx_gemm_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, P, c_i64, c_i32, P, c_i64, c_i32, P, c_i64, P, c_i32, P, c_sz,
                                      c_vp]),
