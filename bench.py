@@ -323,8 +323,8 @@ def run_tgn(args, world, rank, dev):
     # live per-launch timing (HIP events on the launch stream), units from the device counters
     Qm = 3 * D + d
     probes = {}
-    spec = (("tgn_gru_edge", 1), ("tgn_attn_fwd", 6), ("tgn_attn_bwd", 8), ("tgn_wgrad_edge_proj", 2),
-            ("tgn_agg_emit", 9), ("tgn_scan", 3), ("tgn_pred_train", 4), ("tgn_update", 5), ("tgn_adam", 7))
+    spec = (("tgn_gru_edge", 1), ("tgn_attn_fwd", 6), ("tgn_attn_bwd", 8), ("tgn_wgrad_dz0", 2),
+            ("tgn_agg_emit", 9), ("tgn_scan", 3), ("tgn_pred_train", 4), ("tgn_fixup_update", 5), ("tgn_adam", 7))
     for name, kid in spec:
         _lib.call("tgnx_probe_enable", kid)
         pe0, pm0 = eng.units()
@@ -347,8 +347,9 @@ def run_tgn(args, world, rank, dev):
             algo = M * (4 * Qm + 4 * D + 4 * D + 16 * D) + E * (4 * d + 12 + 4 * D)
         elif name in ("tgn_attn_fwd", "tgn_attn_bwd"):
             algo = E * (12 * D + 8) + M * 0
-        elif name == "tgn_wgrad_edge_proj":
-            algo = E * (4 * D + 4 * d + 12) + M * (16 * D + 4 * D)
+        elif name == "tgn_wgrad_dz0":
+            # dW_edge (dE + edge attrs), dEnc W_e (dE again), dW_proj (dP + z0), dz0 (dP, gates, memory, dG out)
+            algo = E * (4 * D + 4 * (D + d) + 12 + 4 * D) + M * (16 * D + 4 * D + 16 * D + 16 * D + 8 * D + 16 * D)
         elif name == "tgn_agg_emit":
             algo = M * (8 * D + 4 * d + 40 + 4 * Qm) + E * (per_edge + 4)
         else:

@@ -17,6 +17,7 @@
 //     kernel boundary that orders the partials here.
 #pragma once
 #include "tgnx_common.h"
+#include <algorithm>
 #include <type_traits>
 
 namespace tgnx {
@@ -379,6 +380,44 @@ __global__ void __launch_bounds__(256) gemm2_kernel(GemmShape g1, AL1 a1, BL1 b1
   const int n1 = gemm_blocks(g1);
   if ((int)blockIdx.x < n1) gemm_body<C1>(g1, a1, b1, e1, p1, blockIdx.x, smem);
   else gemm_body<C2>(g2, a2, b2, e2, p2, blockIdx.x - n1, smem);
+}
+
+// Any number of independent GEMMs in one launch (block ranges in argument order; every range is a
+// multiple of 8 blocks, so each GEMM keeps its XCD grouping).
+template <class CFG, class AL, class BL, class EPI>
+struct GemmJob {
+  using Cfg = CFG;
+  GemmShape g;
+  AL al;
+  BL bl;
+  EPI epi;
+  float* part;
+};
+template <class CFG, class AL, class BL, class EPI>
+inline GemmJob<CFG, AL, BL, EPI> gemm_job(const GemmShape& g, const AL& al, const BL& bl, const EPI& epi, float* part) {
+  return GemmJob<CFG, AL, BL, EPI>{g, al, bl, epi, part};
+}
+template <class J>
+__device__ __forceinline__ bool gemm_job_dispatch(const J& j, int& bid, float* smem) {
+  const int nb = gemm_blocks(j.g);
+  if (bid < nb) {
+    gemm_body<typename J::Cfg>(j.g, j.al, j.bl, j.epi, j.part, bid, smem);
+    return true;
+  }
+  bid -= nb;
+  return false;
+}
+template <class... J>
+__global__ void __launch_bounds__(256) gemmN_kernel(J... j) {
+  constexpr int SM = std::max({J::Cfg::SMEM...});
+  __shared__ __attribute__((aligned(16))) float smem[SM];
+  int bid = blockIdx.x;
+  (void)(gemm_job_dispatch(j, bid, smem) || ...);
+}
+template <class... J>
+static inline void gemmN_launch(hipStream_t s, const J&... j) {
+  const int nb = (gemm_blocks(j.g) + ... + 0);
+  if (nb > 0) gemmN_kernel<J...><<<nb, 256, 0, s>>>(j...);
 }
 
 // ---------------------------------------------------------------- split-K fixup

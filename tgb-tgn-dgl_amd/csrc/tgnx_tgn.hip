@@ -1305,7 +1305,7 @@ struct EpiTeMsg {
 };
 
 // Δt-encoding grads: fixed-order sum of the partial rows into grads (before any all-reduce); rides
-// as the tail block of the weight-gradient fixup launch
+// as the tail blocks of the weight-gradient fixup launch (TrainTail below)
 struct TeReduceTail {
   Ctx c;
   int rows_edge, rows_msg;
@@ -1385,19 +1385,19 @@ __global__ void __launch_bounds__(256) tgn_adam(Ctx c) {
 // [0, nmem): memory / last_update of the update list from the GRU rows (wave per node; train rows
 // are the sampled nodes' rows via assoc, eval / flush rows are list positions);
 // [nmem, nmem + nst): message stores of the batch; the rest: ring merge, wave per node run.
-__global__ void __launch_bounds__(256) tgn_update(Ctx c, int nmem, int nst, int mem_mode, const int64_t* list,
-                                                  const int* list_cnt, int n_host, int64_t base) {
+__device__ void update_body(const Ctx& c, int blk, int nmem, int nst, int mem_mode, const int64_t* list,
+                            const int* list_cnt, int n_host, int64_t base) {
   const int lane = threadIdx.x & 63;
-  if ((int)blockIdx.x < nmem) {
+  if (blk < nmem) {
     if (mem_mode == 0 && (c.ctl[TGNX_CTL_B] == 0 || c.ctl[TGNX_CTL_ERR] != 0)) return;
     const int n = list_cnt ? *list_cnt : n_host;
     const int RW = TGNX_TGN_ROW(c.D);
     float* xr = mem_mode == 0 ? c.xrows : nullptr;
     if (xr && n > c.xcap) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) c.ctl[TGNX_CTL_ERR] |= 8;
+      if (blk == 0 && threadIdx.x == 0) c.ctl[TGNX_CTL_ERR] |= 8;
       return;
     }
-    for (int u = blockIdx.x * 4 + (threadIdx.x >> 6); u < n; u += nmem * 4) {
+    for (int u = blk * 4 + (threadIdx.x >> 6); u < n; u += nmem * 4) {
       const int64_t v = list ? list[u] : base + u;
       const int m = mem_mode == 0 ? c.upd_loc[u] : u;
       const int64_t luv = (int64_t)c.lu[m];
@@ -1418,15 +1418,15 @@ __global__ void __launch_bounds__(256) tgn_update(Ctx c, int nmem, int nst, int 
       }
     }
     if (xr)  // unused slots
-      for (int u = n + blockIdx.x * blockDim.x + threadIdx.x; u < c.xcap; u += nmem * blockDim.x)
+      for (int u = n + blk * blockDim.x + threadIdx.x; u < c.xcap; u += nmem * blockDim.x)
         reinterpret_cast<int*>(xr + (int64_t)u * RW)[0] = -1;
     return;
   }
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
-  if ((int)blockIdx.x < nmem + nst) {
-    const int bid = blockIdx.x - nmem;
+  if (blk < nmem + nst) {
+    const int bid = blk - nmem;
     const int n2 = 2 * B, U = c.cnt[CNT_SRUNS];
     const int64_t ab = 2 * start;  // arena slot of this batch
     for (int p = bid * blockDim.x + threadIdx.x; p < n2; p += nst * blockDim.x)
@@ -1441,13 +1441,29 @@ __global__ void __launch_bounds__(256) tgn_update(Ctx c, int nmem, int nst, int 
     }
     return;
   }
-  const int r = (blockIdx.x - nmem - nst) * 4 + (threadIdx.x >> 6);
+  const int r = (blk - nmem - nst) * 4 + (threadIdx.x >> 6);
   if (r < c.cnt[CNT_RUNS]) {
     const int a = c.rruns[r];
     ring_merge_run(c.nbr, c.eid, c.rt, c.K, c.ev_src + start, c.ev_dst + start, c.ev_t + start, B,
                    c.ctl[TGNX_CTL_CUR_EID], c.assoc, c.rkeys, a, c.rruns[r + 1] - a, r, lane);
   }
 }
+
+__global__ void __launch_bounds__(256) tgn_update(Ctx c, int nmem, int nst, int mem_mode, const int64_t* list,
+                                                  const int* list_cnt, int n_host, int64_t base) {
+  update_body(c, blockIdx.x, nmem, nst, mem_mode, list, list_cnt, n_host, base);
+}
+
+// tail blocks of the train step's fixup launch: the Δt-encoding reduction (nte blocks), then
+// update_state + ring insert (update_body: nothing in the fixup reads memory, stores or the ring)
+struct TrainTail {
+  TeReduceTail te;
+  int nte, nmem, nst;
+  __device__ void operator()(int bid) const {
+    if (bid < nte) te(bid);
+    else update_body(te.c, bid - nte, nmem, nst, 0, te.c.upd, te.c.cnt + CNT_U, 0, 0);
+  }
+};
 
 // data parallel: the all-gathered memory rows of every rank -> memory / last_update (wave per row)
 __global__ void __launch_bounds__(256) tgn_apply_rows(float* mem, int64_t* lu, const float* rows, int64_t nrows, int D,
@@ -1887,35 +1903,36 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D};
   const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D};
   const EpiGruWGrad e_dWg{G, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, Qm, D};
-  probe_begin(TGNX_K_EDGE_BWD, s);
-  gemm2_launch<G32, G32>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, e_dWe, c.pA, shp_dWp(k, c.cnt),
-               LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, e_dWp, c.pB, s);
-  probe_end(TGNX_K_EDGE_BWD, s);
-  TGNX_LAUNCH_CHECK("tgn_wgrad1");
+  // one launch: dW_edge, dW_proj, dW_src/dst (deferred split-K) ‖ dEnc·W_e (Δt partials) ‖ dz0 = dP W
+  // with the GRU backward in its epilogue — all read only what attn_bwd / pred_train produced
   const int rows_edge = (k.Etr + G32::TM - 1) / G32::TM, rows_msg = (k.Mtr + G32::TM - 1) / G32::TM;
-  gemm2_launch<G32, G32>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)}, LoadLpB{c.evs, c.ctl, D, evs_stride(D)},
-               e_dWlp, c.pC, gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
-               LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
-               nullptr, s);
-  TGNX_LAUNCH_CHECK("tgn_wgrad2");
-  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
-              LoadProjWT{P + c.L.wq, c.L.pw, HC, D},
-              EpiGruBwd{c.gates, c.mem, c.nid, c.dG, D}, nullptr, s);
-  TGNX_LAUNCH_CHECK("tgn_dz0");
+  probe_begin(TGNX_K_EDGE_BWD, s);
+  gemmN_launch(s, gemm_job<G32>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, e_dWe, c.pA),
+               gemm_job<G32>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, e_dWp, c.pB),
+               gemm_job<G32>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
+                             LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, e_dWlp, c.pC),
+               gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
+                             LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
+                             (float*)nullptr),
+               gemm_job<G32>(gemm_shape<G32>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
+                             LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, EpiGruBwd{c.gates, c.mem, c.nid, c.dG, D},
+                             (float*)nullptr));
+  probe_end(TGNX_K_EDGE_BWD, s);
+  TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
   gemm2_launch<G32, G32>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, e_dWg,
                c.pD, gemm_shape<G32>(k.Mtr, D, 4 * D, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
                LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
-  gemm_fixup_launch((2 * D + 63) / 64, TeReduceTail{c, rows_edge, rows_msg}, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
-                    gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
-                    gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg));
-  TGNX_LAUNCH_CHECK("tgn_wgrad_fixup");
-  // update_state (train order: memory of src ∪ dst from this step's GRU rows, then the stores), insert
+  // split-K sums + epilogues ‖ Δt reduction ‖ update_state (train order: memory of src ∪ dst from
+  // this step's GRU rows, then the stores) + ring insert, one launch
+  const int nte = (2 * D + 63) / 64;
   const int nmem = gridn(k.Ucap, 4, 1024), nst = gridn(2 * k.B, 256), nring = gridn(2 * k.B, 4);
   probe_begin(TGNX_K_FINISH, s);
-  tgn_update<<<nmem + nst + nring, 256, 0, s>>>(c, nmem, nst, 0, c.upd, c.cnt + CNT_U, 0, 0);
+  gemm_fixup_launch(nte + nmem + nst + nring, TrainTail{TeReduceTail{c, rows_edge, rows_msg}, nte, nmem, nst}, s,
+                    gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe), gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp),
+                    gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp), gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg));
   probe_end(TGNX_K_FINISH, s);
-  TGNX_LAUNCH_CHECK("tgn_update");
+  TGNX_LAUNCH_CHECK("tgn_fixup_update");
   return TGNX_OK;
 }
 

@@ -17,7 +17,7 @@ KEYS = {
     "tgn_attn_fwd": ["tgn_attn_fwd"],
     "tgn_attn_bwd": ["tgn_attn_bwd"],
     "tgn_agg_emit": ["tgn_agg_emit"],
-    "tgn_wgrad_edge_proj": ["LoadEdgeAttrT", "LoadZ1T"],
+    "tgn_wgrad_dz0": ["gemmN_kernel", "LoadEdgeAttrT", "LoadProjWT"],
     "tgnn_edge_fwd": ["tgnn_edge_fwd"],
     "tgnn_edge_bwd": ["tgnn_edge_bwd"],
     "tgnn_seg_fwd": ["tgnn_seg_fwd"],
