@@ -43,6 +43,10 @@ struct GemmCfg {
 #define TGNX_G32_PF 1
 #endif
 using G32 = GemmCfg<32, 32, TGNX_G32_KC, TGNX_G32_PF>;  // the TGN step's GEMMs
+#ifndef TGNX_G32L_KC
+#define TGNX_G32L_KC 64
+#endif
+using G32L = GemmCfg<32, 32, TGNX_G32L_KC, 1>;  // long-K direct GEMMs (GRU, dz0, dX_enc): fewer chunks
 using G64 = GemmCfg<64, 64, 64>;   // large-M GEMMs (eval scoring)
 
 struct GemmShape {

@@ -1777,8 +1777,8 @@ static void gru_list(const Ctx& c, const Caps& k, const int64_t* list, const int
                      int mcap, hipStream_t s) {
   const float* P = c.params;
   tgn_agg_emit<<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
-  const GemmShape g1 = gemm_shape<G32>(mcap, 4 * c.D, c.Qm + c.D, list_cnt);
-  gemm_launch<G32>(g1, LoadGruA{c.X, c.mem, list ? list : c.nid, base, c.Qm, c.D, list ? 0 : 1},
+  const GemmShape g1 = gemm_shape<G32L>(mcap, 4 * c.D, c.Qm + c.D, list_cnt);
+  gemm_launch<G32L>(g1, LoadGruA{c.X, c.mem, list ? list : c.nid, base, c.Qm, c.D, list ? 0 : 1},
                    LoadGruW{P + c.L.w_ih, P + c.L.w_hh, c.Qm, c.D},
               EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, list, base, c.D, c.Z0, c.gates}, nullptr, s);
 }
@@ -1873,7 +1873,7 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   gemm_launch<G32>(gemm_shape<G32>(k.Etr, HC, D + d, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
                    EpiStore{c.Ep, nullptr, HC, 0}, nullptr, s);
 #else
-  gemm2_launch<G32, G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
+  gemm2_launch<G32L, G32>(gemm_shape<G32L>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
                LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
                EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, nullptr,
                gemm_shape<G32>(k.Etr, HC, D + d, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
@@ -1914,13 +1914,13 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
                gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
                              LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
                              (float*)nullptr),
-               gemm_job<G32>(gemm_shape<G32>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
+               gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
                              LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, EpiGruBwd{c.gates, c.mem, c.nid, c.dG, D},
                              (float*)nullptr));
   probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
-  gemm2_launch<G32, G32>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, e_dWg,
-               c.pD, gemm_shape<G32>(k.Mtr, D, 4 * D, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
+  gemm2_launch<G32, G32L>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, e_dWg,
+               c.pD, gemm_shape<G32L>(k.Mtr, D, 4 * D, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
                LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
   // split-K sums + epilogues ‖ Δt reduction ‖ update_state (train order: memory of src ∪ dst from

@@ -599,59 +599,59 @@ __global__ void __launch_bounds__(1024) tgnn_seg_scan(Ctx c) {
   }
 }
 
-// one thread per edge: source node, feature row, dt = t_edge - time_assoc[src] as of the block
+// per edge: source node, feature row, dt = t_edge - time_assoc[src] as of the block
 template <bool TRAIN>
 __device__ void edge_meta_body(const Ctx& c, const int bid, const int nblk) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int S = (int)c.ctl[TGNX_CTL_S];
-  const int E = (int)c.ctl[TGNX_CTL_E];
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   const int lo_ev = (int)c.ctl[TGNX_CTL_LO], hi_ev = (int)c.ctl[TGNX_CTL_HI];
   const int gen = (int)c.ctl[TGNX_CTL_GEN];
   const float* evt = c.ev_t + start;
-  for (int e = bid * blockDim.x + threadIdx.x; e < E; e += nblk * blockDim.x) {
-    int lo = 0, hi = S;  // last w with eoff[w] <= e
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (c.seg_eoff[mid] <= e) lo = mid; else hi = mid;
-    }
-    const int w = lo;
-    const int o = e - c.seg_eoff[w];
+  const int lane = threadIdx.x & 63;
+  // wave per segment, lanes over its edges: the segment's root / block / edge range are loaded once
+  // per wave (an edge-parallel layout needed a dependent binary search over the segment offsets)
+  for (int w = bid * 4 + (threadIdx.x >> 6); w < S; w += nblk * 4) {
     Seg s;
     seg_of(c, w, lo_ev, hi_ev, start, s);
-    const int nring = c.seg_cnt[w] & 255;
-    EdgeMeta m;
-    float bt;
-    if (o < nring) {
-      const int64_t idx = s.root * c.K + o;
-      m.u = c.nbr[idx];
-      m.frow = c.eid[idx];
-      bt = c.rt[idx];
-    } else if (o == nring) {
-      m.u = s.root;
-      m.frow = -1;
-      bt = 0.f;
-    } else {
-      const uint64_t k = c.sp_keys[c.nodemap[s.root].w + (o - nring - 1)];
-      const int ev = kev(k);
-      m.u = kkind(k) == 2 ? c.ev_dst[start + ev] : c.ev_src[start + ev];
-      m.frow = -(start + ev) - 2;
-      bt = evt[ev];
+    const int cntw = c.seg_cnt[w];
+    const int nring = cntw & 255;
+    const int e0 = c.seg_eoff[w], ne = c.seg_eoff[w + 1] - e0;
+    const int spw = c.nodemap[s.root].w;
+    for (int o = lane; o < ne; o += 64) {
+      EdgeMeta m;
+      float bt;
+      if (o < nring) {
+        const int64_t idx = s.root * c.K + o;
+        m.u = c.nbr[idx];
+        m.frow = c.eid[idx];
+        bt = c.rt[idx];
+      } else if (o == nring) {
+        m.u = s.root;
+        m.frow = -1;
+        bt = 0.f;
+      } else {
+        const uint64_t k = c.sp_keys[spw + (o - nring - 1)];
+        const int ev = kev(k);
+        m.u = kkind(k) == 2 ? c.ev_dst[start + ev] : c.ev_src[start + ev];
+        m.frow = -(start + ev) - 2;
+        bt = evt[ev];
+      }
+      m.dt = bt - ta_at<TRAIN>(c, m.u, s.blk, gen, evt);
+      m.seg = w;
+      m.o = o;
+      m.blk = s.blk;
+      m.root = s.root;
+      if (c.drop) {
+        const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+        m.eb = efeat_base(seed, seg_key(s.blk, s.root), o);
+        m.nb = node_base(seed, s.blk, m.u);
+      } else {
+        m.eb = m.nb = 0u;
+      }
+      c.meta[e0 + o] = m;
     }
-    m.dt = bt - ta_at<TRAIN>(c, m.u, s.blk, gen, evt);
-    m.seg = w;
-    m.o = o;
-    m.blk = s.blk;
-    m.root = s.root;
-    if (c.drop) {
-      const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-      m.eb = efeat_base(seed, seg_key(s.blk, s.root), o);
-      m.nb = node_base(seed, s.blk, m.u);
-    } else {
-      m.eb = m.nb = 0u;
-    }
-    c.meta[e] = m;
   }
 }
 
@@ -1879,7 +1879,7 @@ static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
     TGNX_LAUNCH_CHECK("tgnn_seg_scan");
   }
   {  // edge metadata + collapsed weights (depends on the parameters only) in one launch
-    const int nmeta = edge_grid(c.Ecap) / 4 + 1;
+    const int nmeta = (int)std::min<int64_t>(4096, (Scap + 3) / 4);  // wave per segment
     probe_begin(TGNX_K_EDGE_META, s);
     tgnn_meta_collapse<TRAIN><<<nmeta + collapse_blocks(c), 256, 0, s>>>(c, nmeta);
     probe_end(TGNX_K_EDGE_META, s);
