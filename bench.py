@@ -369,6 +369,27 @@ def run_tgn(args, world, rank, dev):
             traffic = json.load(open(pmc)).get(dom, {}).get("bytes_per_launch")
         except Exception:
             traffic = None
+    # validation pass on the device (TGNMemory.train(False) flush, then TGB-style scoring of the first
+    # val batches against the dataset's negative count): exercises the eval path at full size; MRR
+    # parity against the oracle is tests/test_gpu_tgn.py (bench may not run the oracle outside its
+    # cpu_baseline leg)
+    from tgnx.synth import eval_negatives
+    nval = min(10, max(1, (stream.val_end - stream.train_end) // args.batch))
+    negs = eval_negatives(stream, "val", shape.num_neg_eval)
+    eng.flush()
+    torch.cuda.synchronize()
+    tv = time.perf_counter()
+    rrs = []
+    for i in range(nval):
+        a = stream.train_end + i * args.batch
+        _, _, rr = eng.eval_batch(a, args.batch, torch.from_numpy(negs[i * args.batch:(i + 1) * args.batch]))
+        rrs.append(rr.clone())
+    torch.cuda.synchronize()
+    tv = time.perf_counter() - tv
+    eng.check()
+    val = {"mrr": round(float(torch.stack(rrs).mean()), 5), "batches": nval, "negatives": int(shape.num_neg_eval),
+           "events_per_s": round(nval * args.batch / tv, 1), "note": "synthetic stream, mid-epoch state; "
+           "eval-path smoke at full size (MRR parity vs the oracle: tests/test_gpu_tgn.py)"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_tgn(stream, args.batch)
@@ -402,6 +423,7 @@ def run_tgn(args, world, rank, dev):
                                      f"TFLOP/s fp32 MFMA" if flops_gru_edge else "")},
         "kernels_us": {k: round(v["avg_us"], 3) for k, v in probes.items()},
         "cpu_baseline": cpu,
+        "val_eval_gpu": val,
         "loss_sum": round(loss, 4),
     }
 
