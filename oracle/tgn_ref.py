@@ -205,18 +205,27 @@ class RefTransformerConv(nn.Module):
 
 
 class RefGraphAttentionEmbedding(nn.Module):
-    """modules/emb_module.py:55-73."""
+    """modules/emb_module.py:55-73.  layers = 2 is the build's 2-hop extension (SURVEY §8d comment
+    config, "no reference parity"): conv2(conv1(x)) over the same 2-hop edge set (the sampler called
+    on the 1-hop node set), sharing the edge attributes; no activation between the layers."""
 
-    def __init__(self, in_channels, out_channels, msg_dim, time_enc, dropout=0.1):
+    def __init__(self, in_channels, out_channels, msg_dim, time_enc, dropout=0.1, layers=1):
         super().__init__()
         self.time_enc = time_enc
         self.conv = RefTransformerConv(in_channels, out_channels // 2, 2, dropout, msg_dim + time_enc.out_channels)
+        if layers == 2:
+            self.conv2 = RefTransformerConv(out_channels, out_channels // 2, 2, dropout,
+                                            msg_dim + time_enc.out_channels)
+        self.layers = layers
 
     def forward(self, x, last_update, edge_index, t, msg):
         rel_t = last_update[edge_index[0]] - t
         rel_t_enc = self.time_enc(rel_t.to(x.dtype))
         edge_attr = torch.cat([rel_t_enc, msg], dim=-1)
-        return self.conv(x, edge_index, edge_attr)
+        h = self.conv(x, edge_index, edge_attr)
+        if self.layers == 2:
+            h = self.conv2(h, edge_index, edge_attr)
+        return h
 
 
 class RefLinkPredictor(nn.Module):
@@ -236,11 +245,21 @@ class RefLinkPredictor(nn.Module):
 class RefTGN(nn.Module):
     """pyg_model_utils.py:10-36: memory + gnn (sharing memory.time_enc) + link_pred."""
 
-    def __init__(self, num_nodes, msg_dim, hidden=100, aggr="last", dropout=0.1):
+    def __init__(self, num_nodes, msg_dim, hidden=100, aggr="last", dropout=0.1, layers=1):
         super().__init__()
         self.memory = RefTGNMemory(num_nodes, msg_dim, hidden, hidden, aggr)
-        self.gnn = RefGraphAttentionEmbedding(hidden, hidden, msg_dim, self.memory.time_enc, dropout)
+        self.gnn = RefGraphAttentionEmbedding(hidden, hidden, msg_dim, self.memory.time_enc, dropout, layers)
         self.link_pred = RefLinkPredictor(hidden)
+        self.layers = layers
+
+
+def sample_hops(model: RefTGN, loader, n_id):
+    """1 hop: loader(n_id); 2 hops (layers = 2): loader(loader(n_id).nodes) — the edges into every
+    1-hop node, whose node set contains the 1-hop set."""
+    n_id, ei, e_id, _ = loader(np.asarray(n_id))
+    if model.layers == 2:
+        n_id, ei, e_id, _ = loader(n_id)
+    return torch.from_numpy(n_id), torch.from_numpy(ei), torch.from_numpy(e_id)
 
 
 def train_step(model: RefTGN, opt, loader, ev_t, ev_msg, src, pos, neg, t, msg):
@@ -248,9 +267,7 @@ def train_step(model: RefTGN, opt, loader, ev_t, ev_msg, src, pos, neg, t, msg):
     ev_t / ev_msg: the stream's t / msg (rows = e_id).  Returns (loss, pos_out, neg_out)."""
     model.train()
     opt.zero_grad()
-    n_id = torch.cat([src, pos, neg]).unique()
-    n_id, ei, e_id, _ = loader(n_id.numpy())
-    n_id, ei, e_id = torch.from_numpy(n_id), torch.from_numpy(ei), torch.from_numpy(e_id)
+    n_id, ei, e_id = sample_hops(model, loader, torch.cat([src, pos, neg]).unique().numpy())
     assoc = torch.zeros(model.memory.num_nodes, dtype=torch.long)
     assoc[n_id] = torch.arange(n_id.size(0))
     z, last_update = model.memory(n_id)
@@ -279,9 +296,7 @@ def train_step_dp(model: RefTGN, opt, loader, ev_t, ev_msg, src, pos, neg, t, ms
     s_src, s_pos, s_neg = src[lo:hi], pos[lo:hi], neg[lo:hi]
     model.train()
     opt.zero_grad()
-    n_id = torch.cat([s_src, s_pos, s_neg]).unique()
-    n_id, ei, e_id, _ = loader(n_id.numpy())
-    n_id, ei, e_id = torch.from_numpy(n_id), torch.from_numpy(ei), torch.from_numpy(e_id)
+    n_id, ei, e_id = sample_hops(model, loader, torch.cat([s_src, s_pos, s_neg]).unique().numpy())
     assoc = torch.zeros(model.memory.num_nodes, dtype=torch.long)
     assoc[n_id] = torch.arange(n_id.size(0))
     z, last_update = model.memory(n_id)
@@ -334,9 +349,7 @@ def eval_step(model: RefTGN, loader, ev_t, ev_msg, src, pos, negs, t, msg):
     memory / ring state, then update_state + insert.  Returns (pos_out [B], neg_out [B, K'])."""
     model.eval()
     cand = torch.cat([pos.view(-1, 1), negs], dim=1)            # [B, 1 + K']
-    n_id = torch.cat([src, cand.reshape(-1)]).unique()
-    n_id, ei, e_id, _ = loader(n_id.numpy())
-    n_id, ei, e_id = torch.from_numpy(n_id), torch.from_numpy(ei), torch.from_numpy(e_id)
+    n_id, ei, e_id = sample_hops(model, loader, torch.cat([src, cand.reshape(-1)]).unique().numpy())
     assoc = torch.zeros(model.memory.num_nodes, dtype=torch.long)
     assoc[n_id] = torch.arange(n_id.size(0))
     z, last_update = model.memory(n_id)

@@ -101,3 +101,47 @@ def test_config_rejections(field, value, msg):
     off = (ctypes.c_int64 * 22)()
     assert L.tgnx_tgn_param_layout(ctypes.byref(cfg), off) != 0
     assert msg in L.tgnx_last_error()
+
+
+def test_two_hop_oracle_reduces_to_one_hop():
+    """The 2-hop extension (oracle RefTGN(layers=2)): with conv2 the identity (value weights 0, skip = I)
+    the 2-hop scores equal the 1-hop model's on the same stream — the 2-hop node set, assoc and the
+    layer-1 outputs of the roots are consistent with the 1-hop path."""
+    from oracle.sampler_ref import RefLastNeighborLoader
+    from oracle.tgn_ref import RefTGN, eval_step, train_step
+    torch.manual_seed(0)
+    N, d, D, B = 60, 5, 8, 16
+    rng = np.random.default_rng(0)
+    E = 6 * B
+    src, dst = torch.from_numpy(rng.integers(0, N, E)), torch.from_numpy(rng.integers(0, N, E))
+    t = torch.from_numpy(np.sort(rng.random(E) * 100).astype(np.float32))
+    msg = torch.randn(E, d)
+    m1 = RefTGN(N, d, hidden=D, dropout=0.0)
+    m2 = RefTGN(N, d, hidden=D, dropout=0.0, layers=2)
+    sd = m1.state_dict()
+    with torch.no_grad():
+        for k, v in m2.state_dict().items():
+            if k in sd:
+                v.copy_(sd[k])
+        c2 = m2.gnn.conv2
+        for lin in (c2.lin_query, c2.lin_key, c2.lin_value, c2.lin_edge):
+            lin.weight.zero_()
+            if lin.bias is not None:
+                lin.bias.zero_()
+        c2.lin_skip.weight.copy_(torch.eye(D))
+        c2.lin_skip.bias.zero_()
+    l1, l2 = RefLastNeighborLoader(N, 3), RefLastNeighborLoader(N, 3)
+    o1 = torch.optim.SGD(m1.parameters(), lr=0.0)
+    o2 = torch.optim.SGD(m2.parameters(), lr=0.0)
+    for b in range(E // B - 1):
+        sl = slice(b * B, (b + 1) * B)
+        neg = torch.from_numpy(rng.integers(0, N, B))
+        a = train_step(m1, o1, l1, t, msg, src[sl], dst[sl], neg, t[sl], msg[sl])
+        c = train_step(m2, o2, l2, t, msg, src[sl], dst[sl], neg, t[sl], msg[sl])
+        torch.testing.assert_close(a[1], c[1], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(a[2], c[2], rtol=1e-5, atol=1e-6)
+    sl = slice(E - B, E)
+    negs = torch.from_numpy(rng.integers(0, N, (B, 4)))
+    a = eval_step(m1, l1, t, msg, src[sl], dst[sl], negs, t[sl], msg[sl])
+    c = eval_step(m2, l2, t, msg, src[sl], dst[sl], negs, t[sl], msg[sl])
+    torch.testing.assert_close(a[1], c[1], rtol=1e-5, atol=1e-6)
