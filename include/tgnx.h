@@ -254,12 +254,18 @@ int tgnx_tcsr_sample(const int64_t* indptr, const int64_t* indices, const int64_
  * (decoder.py:108-123, sigmoid output fed to BCE-with-logits as the reference's loop does).
  * The sampler state is the LastNeighborLoader ring above; ctl is the tgnx_tgnn_advance block. */
 #define TGNX_TGN_NPARAM 21
+/* layers = 2 (SURVEY §8d comment config, "2-hop temporal attention"; the build's extension, no
+ * reference parity): the sampler is called again on the 1-hop node set and a second TransformerConv
+ * `gnn.conv2` (same shapes as `gnn.conv`) runs on the first one's output; its 9 tensors follow the
+ * 21 above in the layout (lin_key w/b, lin_query w/b, lin_value w/b, lin_edge w, lin_skip w/b). */
+#define TGNX_TGN_NPARAM2 30
 typedef struct {
   int64_t num_nodes;
   int64_t num_events;  /* rows of the event table (e_id space, message-store arena) */
   int32_t ring, mem_dim, msg_dim, heads, max_batch, max_neg;
   int32_t aggr;        /* 0 = LastAggregator, 1 = MeanAggregator */
   float dropout, lr, beta1, beta2, eps;
+  int32_t layers;      /* 1 (emb_module.py:55-73) or 2 (2-hop: conv2(conv1(x)) over the 2-hop sample) */
 } tgnx_tgn_config;
 
 typedef struct {
@@ -287,7 +293,8 @@ typedef struct {
 /* exchanged memory row: int32 node (-1 = unused slot), int64 last_update (lo, hi words), pad, memory[D] */
 #define TGNX_TGN_ROW(D) ((D) + 4)
 
-int tgnx_tgn_param_layout(const tgnx_tgn_config* cfg, int64_t* offsets /* [TGNX_TGN_NPARAM+1] */);
+int tgnx_tgn_param_layout(const tgnx_tgn_config* cfg,
+                          int64_t* offsets /* [TGNX_TGN_NPARAM+1], layers = 2: [TGNX_TGN_NPARAM2+1] */);
 size_t tgnx_tgn_ws_bytes(const tgnx_tgn_config* cfg);
 size_t tgnx_tgn_store_words(const tgnx_tgn_config* cfg);
 /* memory = 0, last_update = 0, message stores empty (memory_module.py:106-110). */

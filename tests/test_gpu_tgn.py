@@ -16,7 +16,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-SHIFT_INVARIANT = "gnn.conv.lin_key.bias"
+SHIFT_INVARIANT = {"gnn.conv.lin_key.bias": "gnn.conv.lin_key.weight", "gnn.conv2.lin_key.bias": "gnn.conv2.lin_key.weight"}
 
 
 def _rel(a, b):
@@ -24,7 +24,7 @@ def _rel(a, b):
     return float((a - b).norm() / (b.norm() + 1e-12))
 
 
-def _setup(aggr, N=300, B=50, d=16, D=32, nb=10, seed=3, max_neg=20):
+def _setup(aggr, N=300, B=50, d=16, D=32, nb=10, seed=3, max_neg=20, layers=1):
     from oracle.sampler_ref import RefLastNeighborLoader
     from oracle.tgn_ref import RefTGN
     from tgnx.sampler import LastNeighborLoader
@@ -32,10 +32,11 @@ def _setup(aggr, N=300, B=50, d=16, D=32, nb=10, seed=3, max_neg=20):
     from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
     s = make_stream("tgbl-wiki", seed=seed, num_events=B * nb, num_nodes=N, msg_dim=d)
     torch.manual_seed(0)
-    ref = RefTGN(N, d, hidden=D, aggr=aggr, dropout=0.0)
+    ref = RefTGN(N, d, hidden=D, aggr=aggr, dropout=0.0, layers=layers)
     opt_ref = torch.optim.Adam(ref.parameters(), lr=1e-3)
     dev = torch.device("cuda")
-    model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=max_neg, aggr=aggr, dropout=0.0)
+    model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=max_neg, aggr=aggr, dropout=0.0,
+                     layers=layers)
     model.load_reference_state(ref.state_dict())
     opt = TgnAdam(model, 1e-3)
     loader = LastNeighborLoader(N, 10, device=dev)
@@ -46,10 +47,9 @@ def _setup(aggr, N=300, B=50, d=16, D=32, nb=10, seed=3, max_neg=20):
 
 
 def _sync(ref, opt_ref, model, opt):
-    from tgnx.tgn import PARAM_ORDER
     named = dict(ref.named_parameters())
     with torch.no_grad():
-        for name in PARAM_ORDER:
+        for name in model.param_order:
             o, n, _ = model._views[name]
             p = named[name]
             model.flat[o:o + n].copy_(p.detach().reshape(-1))
@@ -61,12 +61,13 @@ def _sync(ref, opt_ref, model, opt):
         model.memory.last_update.copy_(ref.memory.last_update)
 
 
-@pytest.mark.parametrize("aggr", ["last", "mean"])
-def test_tgn_train_steps_and_eval_match_oracle(aggr):
+@pytest.mark.parametrize("aggr,layers", [("last", 1), ("mean", 1), ("last", 2), ("mean", 2)])
+def test_tgn_train_steps_and_eval_match_oracle(aggr, layers):
+    """layers = 2: the 2-hop extension (oracle RefTGN(layers=2); no reference parity possible)."""
     from oracle.tgn_ref import eval_step, mrr_per_event, train_step
-    from tgnx.tgn import PARAM_ORDER
     B = 50
-    s, ref, opt_ref, lref, model, opt, eng = _setup(aggr)
+    s, ref, opt_ref, lref, model, opt, eng = _setup(aggr, layers=layers)
+    PARAM_ORDER = model.param_order
     ev_t = torch.from_numpy(s.t.astype(np.float32))
     ev_msg = torch.from_numpy(s.msg)
     rng = np.random.default_rng(1)
@@ -86,8 +87,8 @@ def test_tgn_train_steps_and_eval_match_oracle(aggr):
         assert abs(float(model.grad_flat[-1]) - loss) < 1e-5 * max(1.0, abs(loss))
         g = model.grads_by_name()
         for name in PARAM_ORDER:
-            if name == SHIFT_INVARIANT:
-                scale = float(named["gnn.conv.lin_key.weight"].grad.norm()) + 1e-12
+            if name in SHIFT_INVARIANT:
+                scale = float(named[SHIFT_INVARIANT[name]].grad.norm()) + 1e-12
                 assert float(g[name].norm()) < 1e-4 * scale and float(named[name].grad.norm()) < 1e-4 * scale
                 continue
             r = _rel(g[name], named[name].grad)
@@ -96,7 +97,7 @@ def test_tgn_train_steps_and_eval_match_oracle(aggr):
         assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5), st
         assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update), st
         for name in PARAM_ORDER:
-            if name == SHIFT_INVARIANT:
+            if name in SHIFT_INVARIANT:
                 continue
             o, n, _ = model._views[name]
             assert torch.allclose(model.flat[o:o + n].cpu(), named[name].detach().reshape(-1), atol=5e-6, rtol=1e-4), \

@@ -46,34 +46,55 @@ def test_last_aggregator_ties_and_empty_rows():
                                               [(2 + 6 + 8) / 3, (3 + 7 + 9) / 3], [0, 0]], rtol=1e-6)
 
 
-def _cfg(N=9227, E=157474, D=100, d=172, B=200, kn=1, aggr=0, heads=2):
+def _cfg(N=9227, E=157474, D=100, d=172, B=200, kn=1, aggr=0, heads=2, layers=1):
     from tgnx.tgn import TgnConfig
     return TgnConfig(num_nodes=N, num_events=E, ring=10, mem_dim=D, msg_dim=d, heads=heads, max_batch=B, max_neg=kn,
-                     aggr=aggr, dropout=0.1, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8)
+                     aggr=aggr, dropout=0.1, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8, layers=layers)
 
 
+@pytest.mark.parametrize("layers", [1, 2])
 @pytest.mark.parametrize("D,d", [(100, 172), (100, 1), (32, 16), (6, 2)])
-def test_param_layout_matches_reference_shapes(D, d):
-    """tgnx_tgn_param_layout: one slot per reference parameter (pyg_model_utils.py:10-36 modules),
-    sized as the reference's shapes, 16-B aligned, disjoint; the projection stride invariant."""
+def test_param_layout_matches_reference_shapes(D, d, layers):
+    """tgnx_tgn_param_layout: one slot per reference parameter (pyg_model_utils.py:10-36 modules; layers = 2
+    adds the oracle's gnn.conv2), sized as the reference's shapes, 16-B aligned, disjoint; the projection
+    stride invariant (the same stride for conv2)."""
     from oracle.tgn_ref import RefTGN
     from tgnx import _lib
-    from tgnx.tgn import PARAM_ORDER, param_shapes
-    cfg = _cfg(D=D, d=d)
-    off = (ctypes.c_int64 * 22)()
+    from tgnx.tgn import PARAM_ORDER, PARAM_ORDER2, param_shapes
+    order = PARAM_ORDER2 if layers == 2 else PARAM_ORDER
+    cfg = _cfg(D=D, d=d, layers=layers)
+    off = (ctypes.c_int64 * (len(order) + 1))()
     _lib.call("tgnx_tgn_param_layout", ctypes.byref(cfg), off)
     off = list(off)
-    ref = {k: tuple(v.shape) for k, v in RefTGN(50, d, hidden=D).named_parameters()}
-    shapes = param_shapes(D, d)
-    assert set(ref) == set(PARAM_ORDER) and all(ref[k] == shapes[k] for k in PARAM_ORDER)
-    spans = sorted((off[i], off[i] + int(np.prod(shapes[k]))) for i, k in enumerate(PARAM_ORDER))
+    ref = {k: tuple(v.shape) for k, v in RefTGN(50, d, hidden=D, layers=layers).named_parameters()}
+    shapes = param_shapes(D, d, layers)
+    assert set(ref) == set(order) and all(ref[k] == shapes[k] for k in order)
+    spans = sorted((off[i], off[i] + int(np.prod(shapes[k]))) for i, k in enumerate(order))
     for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
         assert a1 <= b0
     assert all(o % 4 == 0 for o in off[:-1]) and spans[-1][1] <= off[-1]
-    o = dict(zip(PARAM_ORDER, off))
-    w = [o[f"gnn.conv.lin_{k}.weight"] for k in ("query", "key", "value", "skip")]
-    b = [o[f"gnn.conv.lin_{k}.bias"] for k in ("query", "key", "value", "skip")]
-    assert len({y - x for x, y in zip(w, w[1:])}) == 1 and len({y - x for x, y in zip(b, b[1:])}) == 1
+    o = dict(zip(order, off))
+    strides = set()
+    for cv in (("conv", "conv2") if layers == 2 else ("conv",)):
+        w = [o[f"gnn.{cv}.lin_{k}.weight"] for k in ("query", "key", "value", "skip")]
+        b = [o[f"gnn.{cv}.lin_{k}.bias"] for k in ("query", "key", "value", "skip")]
+        assert len({y - x for x, y in zip(w, w[1:])}) == 1 and len({y - x for x, y in zip(b, b[1:])}) == 1
+        strides.add((w[1] - w[0], b[1] - b[0]))
+    assert len(strides) == 1
+
+
+def test_two_hop_workspace_sizing():
+    """layers = 2 sizes the outer sample up to (K + 1)x the 1-hop one; the comment-shaped config (B = 600)
+    fits comfortably in one MI355X's HBM."""
+    from tgnx import _lib
+    L = _lib.lib()
+    one = L.tgnx_tgn_ws_bytes(ctypes.byref(_cfg()))
+    two = L.tgnx_tgn_ws_bytes(ctypes.byref(_cfg(layers=2)))
+    assert two > 2 * one                                   # capped by N = 9,227 here
+    comment = _cfg(N=994790, E=44314507, d=2, B=600, kn=1, layers=2)
+    assert 0 < L.tgnx_tgn_ws_bytes(ctypes.byref(comment)) < (16 << 30)
+    bad = _cfg(layers=3)
+    assert L.tgnx_tgn_ws_bytes(ctypes.byref(bad)) == 0 and b"layers" in L.tgnx_last_error()
 
 
 def test_workspace_and_store_sizing():

@@ -41,8 +41,10 @@ __host__ __device__ inline int64_t al4(int64_t x) { return (x + 3) & ~int64_t(3)
 struct Lay {
   int64_t te_w, te_b, w_ih, w_hh, b_ih, b_hh, wk, bk, wq, bq, wv, bv, we, wsk, bsk, lsw, lsb, ldw, ldb, lfw, lfb, total;
   int64_t pw, pb;  // projection strides: wq + g pw, bq + g pb for g = query, key, value, skip
+  // layers = 2: gnn.conv2 (same shapes, same fixed-stride projection block), after lin_final.bias
+  int64_t wk2, bk2, wq2, bq2, wv2, bv2, we2, wsk2, bsk2;
 };
-static Lay make_lay(int D, int d) {
+static Lay make_lay(int D, int d, int layers) {
   const int64_t Qm = 3 * (int64_t)D + d, HC = D;
   Lay L;
   int64_t o = 0;
@@ -54,21 +56,27 @@ static Lay make_lay(int D, int d) {
   L.b_hh = o; o += al4(3 * D);
   L.pw = al4(HC * D);
   L.pb = al4(HC);
-  L.wq = o; o += L.pw;
-  L.wk = o; o += L.pw;
-  L.wv = o; o += L.pw;
-  L.wsk = o; o += L.pw;
-  L.bq = o; o += L.pb;
-  L.bk = o; o += L.pb;
-  L.bv = o; o += L.pb;
-  L.bsk = o; o += L.pb;
-  L.we = o; o += al4(HC * (D + d));
+  auto proj = [&](int64_t& wq, int64_t& wk, int64_t& wv, int64_t& wsk, int64_t& bq, int64_t& bk, int64_t& bv,
+                  int64_t& bsk, int64_t& we) {
+    wq = o; o += L.pw;
+    wk = o; o += L.pw;
+    wv = o; o += L.pw;
+    wsk = o; o += L.pw;
+    bq = o; o += L.pb;
+    bk = o; o += L.pb;
+    bv = o; o += L.pb;
+    bsk = o; o += L.pb;
+    we = o; o += al4(HC * (D + d));
+  };
+  proj(L.wq, L.wk, L.wv, L.wsk, L.bq, L.bk, L.bv, L.bsk, L.we);
   L.lsw = o; o += al4((int64_t)D * D);
   L.lsb = o; o += al4(D);
   L.ldw = o; o += al4((int64_t)D * D);
   L.ldb = o; o += al4(D);
   L.lfw = o; o += al4(D);
   L.lfb = o; o += al4(1);
+  if (layers == 2) proj(L.wq2, L.wk2, L.wv2, L.wsk2, L.bq2, L.bk2, L.bv2, L.bsk2, L.we2);
+  else L.wq2 = L.wk2 = L.wv2 = L.wsk2 = L.bq2 = L.bk2 = L.bv2 = L.bsk2 = L.we2 = 0;
   L.total = o;
   return L;
 }
@@ -116,7 +124,24 @@ struct Ctx {
   int *rruns, *sruns;
   int Bmax, Qcap, Rcap, Mcap, Ecap, Ucap, tgp_rows;
   Lay L;
+  // ---- 2-hop (layers = 2).  The arrays above then describe the OUTER sample: centres = the 1-hop node
+  // set (roots ∪ their ring neighbours, sorted), nodes = the 2-hop set; gnn.conv runs over it and
+  // writes Zc = h1 per centre.  The ROOT level (gnn.conv2 over the roots' own ring rows, whose
+  // neighbours are all outer centres) has its own lists; `root_view` swaps them into a Ctx so the
+  // attention kernels run unchanged on either level.
+  int layers;
+  int rsel;        // cnt word holding this view's centre count (CNT_R; root view: CNT_R1)
+  int att_salt;    // attention-dropout stream (conv: 7, conv2: 9)
+  uint32_t* rb;    // roots bitmap
+  int* x2r;        // [outer centre] -> root index or -1 (nullptr at layers = 1)
+  int64_t* cent1;  // roots (sorted)
+  int *r_x2, *ceoff1;                // root -> its outer-centre index (row of P2 / h1); root edge offsets
+  int *e1_j, *e1_e2;                 // root edge -> neighbour's outer-centre index; -> outer edge index
+  int64_t* e1_id;                    // root edge -> event id
+  float *P2, *Ep2, *alpha1, *Zr, *dZr, *dP2, *dE2, *pE, *pF;
+  int R1cap, E1cap, tgp_e1;          // tgp rows of the root edges start at tgp_e1
 };
+constexpr int CNT_R1 = 7, CNT_E1 = 8;
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ float softplusf(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
@@ -171,6 +196,29 @@ __global__ void tgn_mark(Ctx c) {
       if (ok) {  // plain read first: hub words are hit by many lanes, most find the bit set
         const int64_t u = c.nbr[v * c.K + j];
         if (!(c.nb[u >> 5] & (1u << (u & 31)))) atomicOr(&c.nb[u >> 5], 1u << (u & 31));
+        if (c.layers == 2) {
+          // 2 hops: the neighbour is an outer centre; its own ring neighbours are sampled nodes
+          // (the lane walks u's ring row, all K slot loads issued before the marking)
+          if (!(c.cb[u >> 5] & (1u << (u & 31)))) atomicOr(&c.cb[u >> 5], 1u << (u & 31));
+          int ku = 0;
+          for (int i0 = 0; i0 < c.K; i0 += 8) {
+            int64_t ev[8], w[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const int ii = min(i0 + i, c.K - 1);
+              ev[i] = c.eid[u * c.K + ii];
+              w[i] = c.nbr[u * c.K + ii];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              if (i0 + i >= c.K || ev[i] < 0) continue;
+              ++ku;
+              const int64_t x = w[i];
+              if (!(c.nb[x >> 5] & (1u << (x & 31)))) atomicOr(&c.nb[x >> 5], 1u << (x & 31));
+            }
+          }
+          c.kval[u] = ku;
+        }
       }
       k += __popcll((__ballot(ok) >> (16 * grp)) & 0xFFFFull);
     }
@@ -179,6 +227,7 @@ __global__ void tgn_mark(Ctx c) {
       c.kval[v] = k;
       if (!(c.cb[v >> 5] & (1u << (v & 31)))) atomicOr(&c.cb[v >> 5], 1u << (v & 31));
       if (!(c.nb[v >> 5] & (1u << (v & 31)))) atomicOr(&c.nb[v >> 5], 1u << (v & 31));
+      if (c.layers == 2 && !(c.rb[v >> 5] & (1u << (v & 31)))) atomicOr(&c.rb[v >> 5], 1u << (v & 31));
     }
   }
 }
@@ -308,6 +357,7 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
     re += c.kval[v];
     c.cent_loc[x] = loc;
     c.crank[loc] = x;
+    if (c.x2r) c.x2r[x] = -1;
     if (c.node_gen[v] == gen) {
       c.upd[ru] = v;
       c.upd_loc[ru] = loc;
@@ -322,6 +372,49 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
     c.cnt[CNT_U] = U;
     c.ctl[TGNX_CTL_SUM_E] += E;
     c.ctl[TGNX_CTL_SUM_S] += M;
+  }
+  if (c.layers != 2) return;
+  // pass 3 (2 hops): the roots (sorted) from their bitmap -> root index, outer-centre index (crank is
+  // complete after the barrier), root edge offsets (a root's edges are its outer edge range)
+  __threadfence_block();
+  __syncthreads();
+  int nr = 0, nre = 0;
+  for (int64_t w = w0; w < w1; ++w) {
+    uint32_t m = c.rb[w];
+    nr += __popc(m);
+    while (m) {
+      const int b = __ffs(m) - 1;
+      m &= m - 1;
+      nre += c.kval[(w << 5) + b];
+    }
+  }
+  int R1, E1;
+  int r1 = block_excl_scan(nr, sh, &R1);
+  int e1 = block_excl_scan(nre, sh, &E1);
+  if (R1 > c.R1cap) {
+    if (tid == 0) c.ctl[TGNX_CTL_ERR] |= 4;
+    return;
+  }
+  for (int64_t w = w0; w < w1; ++w) {
+    uint32_t m = c.rb[w];
+    if (m) c.rb[w] = 0u;
+    while (m) {
+      const int b = __ffs(m) - 1;
+      m &= m - 1;
+      const int64_t v = (w << 5) + b;
+      const int x2 = c.crank[c.assoc[v]];
+      c.cent1[r1] = v;
+      c.r_x2[r1] = x2;
+      c.x2r[x2] = r1;
+      c.ceoff1[r1] = e1;
+      e1 += c.kval[v];
+      ++r1;
+    }
+  }
+  if (tid == 0) {
+    c.ceoff1[R1] = E1;
+    c.cnt[CNT_R1] = R1;
+    c.cnt[CNT_E1] = E1;
   }
 }
 
@@ -548,6 +641,15 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
         c.e_id[o] = e;
         c.e_t[o] = te;
       }
+      if (c.x2r && lane == 1) {  // 2 hops: a root's edges are its outer edges, same slot order
+        const int x1 = c.x2r[x];
+        if (x1 >= 0) {
+          const int o1 = c.ceoff1[x1] + (o - c.ceoff[x]);
+          c.e1_j[o1] = c.crank[ju];
+          c.e1_e2[o1] = o;
+          c.e1_id[o1] = e;
+        }
+      }
       const float dt = lu - te;
       for (int q = lane; q < D; q += 64) {
         const float a = fmaf(tw[q], dt, tb[q]);
@@ -573,8 +675,17 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
     const int M = c.cnt[CNT_M], R = c.cnt[CNT_R];
     for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)M * 4 * c.HC; x += (int64_t)nb * blockDim.x)
       c.dP[x] = 0.f;
-    for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R * c.HC; x += (int64_t)nb * blockDim.x)
-      c.dZc[x] = 0.f;
+    if (c.layers == 2) {  // root level: dZr (predictor rows), dP2 (conv2 projections of the outer centres);
+                          // dZc = dh1 is written whole by a GEMM
+      const int R1 = c.cnt[CNT_R1];
+      for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R * 4 * c.HC; x += (int64_t)nb * blockDim.x)
+        c.dP2[x] = 0.f;
+      for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R1 * c.HC; x += (int64_t)nb * blockDim.x)
+        c.dZr[x] = 0.f;
+    } else {
+      for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R * c.HC; x += (int64_t)nb * blockDim.x)
+        c.dZc[x] = 0.f;
+    }
   }
   const int n = mode == 0 ? c.cnt[CNT_M] : (list_cnt ? *list_cnt : n_host);
   for (int m = bid * 4 + (threadIdx.x >> 6); m < n; m += nb * 4) {
@@ -673,6 +784,35 @@ struct LoadEdgeAttrT {
   __device__ Idx index(int, int e) const { return a.e_id[e]; }
   __device__ float load(Idx id, int n, int e) const { return a.load(id, e, n); }
 };
+// 2 hops: the edge attribute of root edge e = that of its outer edge e1_e2[e] (same Δt encoding row,
+// same message row); both index loads are independent
+struct EdgeRef {
+  int64_t id;
+  int e2;
+};
+struct LoadEdgeAttrMap {
+  const float* enc;
+  const int64_t* e1_id;
+  const int* e1_e2;
+  const float* ev_msg;
+  int D, d;
+  static constexpr bool k_fast = true;
+  using Idx = EdgeRef;
+  static constexpr bool row_idx = true;
+  __device__ Idx index(int e, int) const { return EdgeRef{e1_id[e], e1_e2[e]}; }
+  __device__ float load(const Idx& r, int, int k) const {
+    const float* p = k < D ? enc + (int64_t)r.e2 * D + k : ev_msg + r.id * d + (k - D);
+    return *p;
+  }
+};
+struct LoadEdgeAttrMapT {
+  LoadEdgeAttrMap a;
+  static constexpr bool k_fast = false;
+  using Idx = EdgeRef;
+  static constexpr bool row_idx = false;
+  __device__ Idx index(int, int e) const { return a.index(e, 0); }
+  __device__ float load(const Idx& r, int n, int e) const { return a.load(r, e, n); }
+};
 // node-embedding input row m: train z0 (GRU output), eval memory[nid[m]] (memory_module.py:121-122)
 struct LoadZ {
   const float* Z0;
@@ -731,14 +871,15 @@ struct EpiProj {
 // dropout (train); out_i = Σ_e alpha~ (v_j + e) + skip_i.  Lane e keeps edge e's per-edge scalars.
 // keyed by (centre node, neighbour e_id): the same mask whichever rank / batch position samples the edge
 __device__ __forceinline__ float att_keep(const Ctx& c, uint64_t seed, int x, int e, int h) {
-  return keep32(drop_base(seed, 7, (uint64_t)c.cent[x], (uint64_t)c.e_id[e]), (uint32_t)h, c.p, c.inv_keep);
+  return keep32(drop_base(seed, (uint64_t)c.att_salt, (uint64_t)c.cent[x], (uint64_t)c.e_id[e]), (uint32_t)h, c.p,
+                c.inv_keep);
 }
 constexpr int ATT_EB = 16;  // edges whose neighbour rows are loaded in one batch (ring K <= 32: <= 2 batches)
 template <bool TRAIN>
 __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int R = c.cnt[CNT_R];
+  const int R = c.cnt[c.rsel];
   const int lane = threadIdx.x & 63;
   const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (x >= R) return;
@@ -806,6 +947,12 @@ __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
   }
 }
 
+// row of a root's embedding: its centre index (2 hops: its root index, via the outer centre)
+__device__ __forceinline__ int root_row(const Ctx& c, int64_t v) {
+  const int x = c.crank[c.assoc[v]];
+  return c.x2r ? c.x2r[x] : x;
+}
+
 // ------------------------------------------------------------------ link prediction (decoder.py:108-123)
 // Workgroup per event of this rank's slice: h = relu(lin_src(z_s) + lin_dst(z_d)), s = sigmoid(lin_final(h)),
 // loss = BCEWithLogits(s_pos, 1) + BCEWithLogits(s_neg, 0) (the reference feeds the sigmoid output to
@@ -827,7 +974,7 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c) {
   const int64_t roots[3] = {c.ev_src[start + i], c.ev_dst[start + i], c.neg[start + i]};
   int cr[3];
 #pragma unroll
-  for (int r = 0; r < 3; ++r) cr[r] = c.crank[c.assoc[roots[r]]];
+  for (int r = 0; r < 3; ++r) cr[r] = root_row(c, roots[r]);
   for (int x = tid; x < 3 * D; x += blockDim.x) z[x / D][x % D] = c.Zc[(int64_t)cr[x / D] * D + x % D];
   __syncthreads();
   const float* P = c.params;
@@ -959,7 +1106,7 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
   }
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int R = c.cnt[CNT_R];
+  const int R = c.cnt[c.rsel];
   const int lane = threadIdx.x & 63;
   const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (x >= R) return;
@@ -1149,24 +1296,32 @@ __device__ __forceinline__ void te_tile_grad(const T& t, const float* S0, const 
   }
 }
 // d(edge attr enc) of the sampled edges; S1 = sin Δt formed here from lu / e_t
+// (map != nullptr: rows are root edges, their Δt data that of the outer edge map[e]; partial rows from row0)
 struct EpiTeEdge {
   const int* e_j;
   const float *e_t, *lu, *sinE;
   float* tgp;
   int D;
+  const int* map = nullptr;
+  int row0 = 0;
   template <class T>
   __device__ void operator()(const T& t) const {
     constexpr int groups = 256 / T::tn, per = T::tm / groups;
     const int cc = threadIdx.x % T::tn, g = threadIdx.x / T::tn, n = t.n0 + cc;
-    int ej[per];
+    int ej[per], e2[per];
     float et[per], sn[per], dt[per];
 #pragma unroll
     for (int i = 0; i < per; ++i) {
       const int e = t.m0 + g + groups * i;
+      e2[i] = map ? map[min(e, t.M - 1)] : e;
+    }
+#pragma unroll
+    for (int i = 0; i < per; ++i) {
+      const int e = t.m0 + g + groups * i;
       const bool ok = e < t.M && n < t.N;
-      ej[i] = ok ? e_j[e] : 0;
-      et[i] = ok ? e_t[e] : 0.f;
-      sn[i] = ok ? sinE[(int64_t)e * D + n] : 0.f;
+      ej[i] = ok ? e_j[e2[i]] : 0;
+      et[i] = ok ? e_t[e2[i]] : 0.f;
+      sn[i] = ok ? sinE[(int64_t)e2[i] * D + n] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < per; ++i) dt[i] = lu[ej[i]] - et[i];
@@ -1189,8 +1344,8 @@ struct EpiTeEdge {
         a += red[q * t.tn + cc];
         b += red[(groups + q) * t.tn + cc];
       }
-      tgp[(int64_t)t.tile_row() * 2 * D + n] = a;
-      tgp[(int64_t)t.tile_row() * 2 * D + D + n] = b;
+      tgp[(int64_t)(row0 + t.tile_row()) * 2 * D + n] = a;
+      tgp[(int64_t)(row0 + t.tile_row()) * 2 * D + D + n] = b;
     }
   }
 };
@@ -1320,7 +1475,9 @@ struct TeReduceTail {
     if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
     const int E = c.cnt[CNT_E], M = c.cnt[CNT_M];
     const int re = min(rows_edge, (E + G32::TM - 1) / G32::TM), rm = min(rows_msg, (M + G32::TM - 1) / G32::TM);
-    const int R = re + rm, r0 = wv * R / 4, r1 = (wv + 1) * R / 4;
+    // 2 hops: the root edges' rows (conv2's lin_edge) follow at tgp_e1
+    const int re1 = c.layers == 2 ? min(c.tgp_rows - c.tgp_e1, (c.cnt[CNT_E1] + G32::TM - 1) / G32::TM) : 0;
+    const int R = re + rm + re1, r0 = wv * R / 4, r1 = (wv + 1) * R / 4;
     const int xc = min(x, 2 * D - 1);
     float s = 0.f;
     for (int r = r0; r < r1; r += 8) {
@@ -1328,7 +1485,7 @@ struct TeReduceTail {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int rr = min(r + u, r1 - 1);
-        const int row = rr < re ? rr : rows_edge + (rr - re);
+        const int row = rr < re ? rr : rr < re + rm ? rows_edge + (rr - re) : c.tgp_e1 + (rr - re - rm);
         v[u] = c.tgp[(int64_t)row * 2 * D + xc];
       }
 #pragma unroll
@@ -1509,7 +1666,7 @@ __global__ void __launch_bounds__(256) tgn_score(Ctx c) {
   if (B == 0 || i >= B || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int D = c.D, Kn = c.Kn, tid = threadIdx.x;
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
-  const int cs = c.crank[c.assoc[c.ev_src[start + i]]];
+  const int cs = root_row(c, c.ev_src[start + i]);
   for (int k = tid; k < D; k += blockDim.x) {
     hs[k] = c.Hs[(int64_t)cs * D + k];
     wf[k] = c.params[c.L.lfw + k];
@@ -1518,7 +1675,7 @@ __global__ void __launch_bounds__(256) tgn_score(Ctx c) {
   __syncthreads();
   const float bf = c.params[c.L.lfb];
   auto score = [&](int64_t node) {
-    const float* hd = c.Hd + (int64_t)c.crank[c.assoc[node]] * D;
+    const float* hd = c.Hd + (int64_t)root_row(c, node) * D;
     float a = 0.f;
     for (int k = 0; k < D; ++k) a += wf[k] * fmaxf(hs[k] + hd[k], 0.f);
     return sigm(a + bf);
@@ -1549,8 +1706,10 @@ static size_t carve(size_t& off, size_t bytes) {
 }
 struct Caps {
   int B, Kn, Qtr, Qcap, Rtr, Rcap, Mtr, Mcap, Etr, Ecap, Ucap, Qm, D, d, HC;
+  int layers, R1tr, R1cap, E1tr, E1cap;  // 2 hops: root level (R*/E*/M* above: the outer sample)
   int64_t N;
 };
+static int cfg_layers(const tgnx_tgn_config* cfg) { return cfg->layers == 2 ? 2 : 1; }
 static Caps make_caps(const tgnx_tgn_config* cfg) {
   Caps k;
   k.N = cfg->num_nodes;
@@ -1565,25 +1724,36 @@ static Caps make_caps(const tgnx_tgn_config* cfg) {
   k.Qtr = 3 * k.B;
   k.Qcap = k.B * (2 + k.Kn);
   if (k.Qcap < k.Qtr) k.Qcap = k.Qtr;
-  k.Rtr = cap(k.Qtr);
-  k.Rcap = cap(k.Qcap);
+  k.layers = cfg_layers(cfg);
+  k.R1tr = cap(k.Qtr);
+  k.R1cap = cap(k.Qcap);
+  k.Rtr = k.layers == 2 ? cap((int64_t)k.R1tr * (K + 1)) : k.R1tr;
+  k.Rcap = k.layers == 2 ? cap((int64_t)k.R1cap * (K + 1)) : k.R1cap;
   k.Mtr = cap((int64_t)k.Rtr * (K + 1));
   k.Mcap = cap((int64_t)k.Rcap * (K + 1));
   k.Etr = k.Rtr * K;
   k.Ecap = k.Rcap * K;
+  k.E1tr = k.layers == 2 ? k.R1tr * K : 0;
+  k.E1cap = k.layers == 2 ? k.R1cap * K : 0;
   k.Ucap = cap(2 * (int64_t)k.B);
   return k;
 }
+// split count of a long-K weight-gradient GEMM: ~2k rows of K per split (2-hop edge sets are ~10x the
+// 1-hop ones), at least 8
+static int ksplit(int K, int smin) { return std::max(smin, std::min(64, K / 2048)); }
 // the deferred (split-K) weight-gradient GEMMs of a train step
-static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(k.HC, k.D + k.d, k.Etr, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, 8); }
-static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.HC, k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, 4); }
+static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(k.HC, k.D + k.d, k.Etr, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, ksplit(k.Etr, 8)); }
+static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.HC, k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
+// 2 hops: conv2's projections (K = outer centres) and lin_edge (K = root edges)
+static GemmShape shp_dWp2(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.HC, k.D + 1, k.Rtr, nullptr, nullptr, cnt ? cnt + CNT_R : nullptr, ksplit(k.Rtr, 4)); }
+static GemmShape shp_dWe2(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(k.HC, k.D + k.d, k.E1tr, nullptr, nullptr, cnt ? cnt + CNT_E1 : nullptr, ksplit(k.E1tr, 8)); }
 static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, 5); }
-static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, 4); }
+static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
 struct WsLay {
   size_t cb, nb, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
       Ep, alpha, Zc, evs, Hs, Hd, dZc, dP, dE, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
-      total;
-  int tgp_rows;
+      rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF, total;
+  int tgp_rows, tgp_e1;
 };
 static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   WsLay W;
@@ -1622,7 +1792,8 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.dP = carve(off, (size_t)k.Mtr * 4 * HC * 4);
   W.dE = carve(off, (size_t)k.Etr * HC * 4);
   W.dG = carve(off, (size_t)k.Mtr * 4 * D * 4);
-  W.tgp_rows = (k.Etr + G32::TM - 1) / G32::TM + (k.Mtr + G32::TM - 1) / G32::TM;
+  W.tgp_e1 = (k.Etr + G32::TM - 1) / G32::TM + (k.Mtr + G32::TM - 1) / G32::TM;
+  W.tgp_rows = W.tgp_e1 + (k.E1tr + G32::TM - 1) / G32::TM;
   W.tgp = carve(off, (size_t)W.tgp_rows * 2 * D * 4);
   W.encE = carve(off, (size_t)k.Ecap * D * 4);
   W.sinE = carve(off, (size_t)k.Etr * D * 4);
@@ -1637,6 +1808,25 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.rruns = carve(off, (size_t)(n2 + 2) * 4);
   W.skeys = carve(off, (size_t)n2 * 8);
   W.sruns = carve(off, (size_t)(n2 + 2) * 4);
+  const bool two = k.layers == 2;
+  const size_t R1 = two ? k.R1cap : 0, E1 = k.E1cap, R2 = two ? k.Rcap : 0;
+  W.rb = carve(off, two ? words * 4 : 0);
+  W.x2r = carve(off, R2 * 4);
+  W.cent1 = carve(off, R1 * 8);
+  W.r_x2 = carve(off, R1 * 4);
+  W.ceoff1 = carve(off, (R1 + 1) * 4);
+  W.e1_j = carve(off, E1 * 4);
+  W.e1_e2 = carve(off, E1 * 4);
+  W.e1_id = carve(off, E1 * 8);
+  W.P2 = carve(off, R2 * 4 * HC * 4);
+  W.Ep2 = carve(off, E1 * HC * 4);
+  W.alpha1 = carve(off, (size_t)k.E1tr * TH * 4);
+  W.Zr = carve(off, R1 * HC * 4);
+  W.dZr = carve(off, (two ? (size_t)k.R1tr : 0) * HC * 4);
+  W.dP2 = carve(off, (two ? (size_t)k.Rtr : 0) * 4 * HC * 4);
+  W.dE2 = carve(off, (size_t)k.E1tr * HC * 4);
+  W.pE = carve(off, two ? gemm_partial_floats(shp_dWp2(k, nullptr)) * 4 : 0);
+  W.pF = carve(off, two ? gemm_partial_floats(shp_dWe2(k, nullptr)) * 4 : 0);
   W.total = off;
   return W;
 }
@@ -1653,6 +1843,7 @@ static int check_cfg(const tgnx_tgn_config* cfg) {
   TGNX_CHECK_ARG(cfg->num_events > 0, "tgn: bad num_events");
   TGNX_CHECK_ARG(cfg->aggr == 0 || cfg->aggr == 1, "tgn: aggr must be 0 (last) or 1 (mean)");
   TGNX_CHECK_ARG(cfg->dropout >= 0.f && cfg->dropout < 1.f, "tgn: bad dropout");
+  TGNX_CHECK_ARG(cfg->layers >= 0 && cfg->layers <= 2, "tgn: layers must be 1 or 2, got %d", cfg->layers);
   return TGNX_OK;
 }
 
@@ -1762,8 +1953,54 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.Ecap = k.Ecap;
   c.Ucap = k.Ucap;
   c.tgp_rows = W.tgp_rows;
-  c.L = make_lay(c.D, c.d);
+  c.L = make_lay(c.D, c.d, k.layers);
+  c.layers = k.layers;
+  c.rsel = CNT_R;
+  c.att_salt = 7;
+  if (k.layers == 2) {
+    c.rb = reinterpret_cast<uint32_t*>(ws + W.rb);
+    c.x2r = reinterpret_cast<int*>(ws + W.x2r);
+    c.cent1 = reinterpret_cast<int64_t*>(ws + W.cent1);
+    c.r_x2 = reinterpret_cast<int*>(ws + W.r_x2);
+    c.ceoff1 = reinterpret_cast<int*>(ws + W.ceoff1);
+    c.e1_j = reinterpret_cast<int*>(ws + W.e1_j);
+    c.e1_e2 = reinterpret_cast<int*>(ws + W.e1_e2);
+    c.e1_id = reinterpret_cast<int64_t*>(ws + W.e1_id);
+    c.P2 = reinterpret_cast<float*>(ws + W.P2);
+    c.Ep2 = reinterpret_cast<float*>(ws + W.Ep2);
+    c.alpha1 = reinterpret_cast<float*>(ws + W.alpha1);
+    c.Zr = reinterpret_cast<float*>(ws + W.Zr);
+    c.dZr = reinterpret_cast<float*>(ws + W.dZr);
+    c.dP2 = reinterpret_cast<float*>(ws + W.dP2);
+    c.dE2 = reinterpret_cast<float*>(ws + W.dE2);
+    c.pE = reinterpret_cast<float*>(ws + W.pE);
+    c.pF = reinterpret_cast<float*>(ws + W.pF);
+    c.R1cap = k.R1cap;
+    c.E1cap = k.E1cap;
+    c.tgp_e1 = W.tgp_e1;
+  }
   return TGNX_OK;
+}
+
+// 2 hops: the root level as a Ctx for the attention / prediction kernels — centres = roots, node rows =
+// outer centres (P2 = conv2's projections of h1), edges = the roots' ring rows, output Zr
+static Ctx root_view(const Ctx& c) {
+  Ctx r = c;
+  r.cent = c.cent1;
+  r.cent_loc = c.r_x2;
+  r.ceoff = c.ceoff1;
+  r.e_j = c.e1_j;
+  r.e_id = c.e1_id;
+  r.P = c.P2;
+  r.Ep = c.Ep2;
+  r.alpha = c.alpha1;
+  r.Zc = c.Zr;
+  r.dZc = c.dZr;
+  r.dP = c.dP2;
+  r.dE = c.dE2;
+  r.rsel = CNT_R1;
+  r.att_salt = 9;
+  return r;
 }
 
 static inline int gridn(int64_t n, int per, int cap = 4096) {
@@ -1795,11 +2032,14 @@ int tgnx_tgn_param_layout(const tgnx_tgn_config* cfg, int64_t* off) {
   int rc = check_cfg(cfg);
   if (rc) return rc;
   TGNX_CHECK_ARG(off, "tgnx_tgn_param_layout: null output");
-  const Lay L = make_lay(cfg->mem_dim, cfg->msg_dim);
-  const int64_t v[TGNX_TGN_NPARAM + 1] = {L.te_w, L.te_b, L.w_ih, L.w_hh, L.b_ih, L.b_hh, L.wk, L.bk,
-                                          L.wq,   L.bq,   L.wv,   L.bv,   L.we,   L.wsk,  L.bsk, L.lsw,
-                                          L.lsb,  L.ldw,  L.ldb,  L.lfw,  L.lfb,  L.total};
-  for (int i = 0; i <= TGNX_TGN_NPARAM; ++i) off[i] = v[i];
+  const int layers = cfg_layers(cfg);
+  const Lay L = make_lay(cfg->mem_dim, cfg->msg_dim, layers);
+  const int64_t v[TGNX_TGN_NPARAM2] = {L.te_w, L.te_b, L.w_ih, L.w_hh, L.b_ih, L.b_hh, L.wk,  L.bk,  L.wq,  L.bq,
+                                       L.wv,   L.bv,   L.we,   L.wsk,  L.bsk,  L.lsw,  L.lsb, L.ldw, L.ldb, L.lfw,
+                                       L.lfb,  L.wk2,  L.bk2,  L.wq2,  L.bq2,  L.wv2,  L.bv2, L.we2, L.wsk2, L.bsk2};
+  const int np = layers == 2 ? TGNX_TGN_NPARAM2 : TGNX_TGN_NPARAM;
+  for (int i = 0; i < np; ++i) off[i] = v[i];
+  off[np] = L.total;
   return TGNX_OK;
 }
 
@@ -1850,35 +2090,23 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   tgn_agg_emit<<<nedge + gridn(k.Mtr, 4, 2048), 256, 0, s>>>(c, 0, nedge, nullptr, nullptr, 0, 0);
   probe_end(TGNX_K_EDGE_META, s);
   TGNX_LAUNCH_CHECK("tgn_agg_emit");
-  // GRU over every sampled node ‖ lin_edge over every sampled edge
+  // GRU over every sampled node ‖ lin_edge over every sampled edge (‖ 2 hops: conv2's lin_edge over the
+  // root edges)
   const LoadEdgeAttr ea{c.encE, c.e_id, c.ev_msg, D, d};
+  const bool two = k.layers == 2;
+  const LoadEdgeAttrMap ea1{c.encE, c.e1_id, c.e1_e2, c.ev_msg, D, d};
+  const auto j_gru = gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
+                                    LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
+                                    EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, (float*)nullptr);
+  const auto j_edge = gemm_job<G32>(gemm_shape<G32>(k.Etr, HC, D + d, c.cnt + CNT_E), ea,
+                                    LoadRowK{P + c.L.we, HC, D + d, D + d}, EpiStore{c.Ep, nullptr, HC, 0}, (float*)nullptr);
   probe_begin(TGNX_K_EDGE_FWD, s);
-#ifdef TGNX_SPLIT_GRU  // timing experiment: the two GEMMs as separate launches
-#if TGNX_SPLIT_GRU == 2   // (timing only) plain A operand
-  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadRowK{c.X, k.Mtr, Qm + D, Qm},
-                   LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
-                   EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, nullptr, s);
-#elif TGNX_SPLIT_GRU == 3  // (timing only) plain B operand
-  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
-                   LoadRowK{P + c.L.w_ih, 4 * D, Qm + D, Qm},
-                   EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, nullptr, s);
-#elif TGNX_SPLIT_GRU == 4  // (timing only) plain epilogue
-  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
-                   LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D}, EpiStore{c.gates, nullptr, 4 * D, 0}, nullptr, s);
-#else
-  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
-                   LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
-                   EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, nullptr, s);
-#endif
-  gemm_launch<G32>(gemm_shape<G32>(k.Etr, HC, D + d, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
-                   EpiStore{c.Ep, nullptr, HC, 0}, nullptr, s);
-#else
-  gemm2_launch<G32L, G32>(gemm_shape<G32L>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
-               LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
-               EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, nullptr,
-               gemm_shape<G32>(k.Etr, HC, D + d, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
-               EpiStore{c.Ep, nullptr, HC, 0}, nullptr, s);
-#endif
+  if (two)
+    gemmN_launch(s, j_gru, j_edge,
+                 gemm_job<G32>(gemm_shape<G32>(k.E1tr, HC, D + d, c.cnt + CNT_E1), ea1,
+                               LoadRowK{P + c.L.we2, HC, D + d, D + d}, EpiStore{c.Ep2, nullptr, HC, 0}, (float*)nullptr));
+  else
+    gemmN_launch(s, j_gru, j_edge);
   probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgn_gru_edge");
   gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
@@ -1886,16 +2114,44 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
               EpiProj{P + c.L.bq, c.L.pb, c.P, HC}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_proj");
   probe_begin(TGNX_K_SEG_FWD, s);
-  tgn_attn_fwd<true><<<gridn(k.Rtr, 4), 256, 0, s>>>(c);
+  tgn_attn_fwd<true><<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c);
   probe_end(TGNX_K_SEG_FWD, s);
   TGNX_LAUNCH_CHECK("tgn_attn_fwd");
+  const Ctx cr = two ? root_view(c) : c;  // the level the predictor reads
+  if (two) {  // conv2 over the roots: projections of h1 (rows = outer centres), attention per root
+    gemm_launch<G32>(gemm_shape<G32>(k.Rtr, 4 * HC, HC, c.cnt + CNT_R), LoadRowK{c.Zc, k.Rtr, HC, HC},
+                     LoadProjW{P + c.L.wq2, c.L.pw, HC, HC}, EpiProj{P + c.L.bq2, c.L.pb, c.P2, HC}, nullptr, s);
+    TGNX_LAUNCH_CHECK("tgn_proj2");
+    tgn_attn_fwd<true><<<gridn(k.R1tr, 4, 1 << 20), 256, 0, s>>>(cr);
+    TGNX_LAUNCH_CHECK("tgn_attn_fwd2");
+  }
   probe_begin(TGNX_K_PRED, s);
-  tgn_pred_train<<<k.B, 256, 0, s>>>(c);
+  tgn_pred_train<<<k.B, 256, 0, s>>>(cr);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
-  const int ncb = gridn(k.Rtr, 4);
   probe_begin(TGNX_K_SEG_BWD, s);
-  tgn_attn_bwd<<<ncb + gridn(3 * D + 2, 4), 256, 0, s>>>(c, ncb);
+  if (two) {
+    // conv2 backward (‖ predictor reductions) -> dP2, dE2; then dh1 = dP2 [Wq2; Wk2; Wv2; Wsk2] ‖ dW_proj2,
+    // dW_edge2 (deferred) ‖ conv2's lin_edge -> Δt-encoding partials; then conv backward from dh1
+    const int ncb1 = gridn(k.R1tr, 4, 1 << 20);
+    tgn_attn_bwd<<<ncb1 + gridn(3 * D + 2, 4), 256, 0, s>>>(cr, ncb1);
+    TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
+    gemmN_launch(s,
+                 gemm_job<G32L>(gemm_shape<G32L>(k.Rtr, HC, 4 * HC, c.cnt + CNT_R), LoadRowK{c.dP2, k.Rtr, 4 * HC, 4 * HC},
+                                LoadProjWT{P + c.L.wq2, c.L.pw, HC, HC}, EpiStore{c.dZc, nullptr, HC, 0}, (float*)nullptr),
+                 gemm_job<G32>(shp_dWp2(k, c.cnt), LoadKRow{c.dP2, 4 * HC, k.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
+                               EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC}, c.pE),
+                 gemm_job<G32>(shp_dWe2(k, c.cnt), LoadKRow{c.dE2, HC, k.E1tr, HC}, LoadEdgeAttrMapT{ea1},
+                               EpiStore{G + c.L.we2, nullptr, D + d, 0}, c.pF),
+                 gemm_job<G32>(gemm_shape<G32>(k.E1tr, D, HC, c.cnt + CNT_E1), LoadRowK{c.dE2, k.E1tr, HC, HC},
+                               LoadKRow{P + c.L.we2, D, HC, D + d},
+                               EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, c.e1_e2, c.tgp_e1}, (float*)nullptr));
+    TGNX_LAUNCH_CHECK("tgn_dh1");
+    tgn_attn_bwd<<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c, gridn(k.Rtr, 4, 1 << 20));
+  } else {
+    const int ncb = gridn(k.Rtr, 4, 1 << 20);
+    tgn_attn_bwd<<<ncb + gridn(3 * D + 2, 4), 256, 0, s>>>(c, ncb);
+  }
   probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_attn_bwd");
   // weight gradients (deferred split-K) ‖ ...
@@ -1927,10 +2183,18 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   // this step's GRU rows, then the stores) + ring insert, one launch
   const int nte = (2 * D + 63) / 64;
   const int nmem = gridn(k.Ucap, 4, 1024), nst = gridn(2 * k.B, 256), nring = gridn(2 * k.B, 4);
+  const TrainTail tail{TeReduceTail{c, rows_edge, rows_msg}, nte, nmem, nst};
   probe_begin(TGNX_K_FINISH, s);
-  gemm_fixup_launch(nte + nmem + nst + nring, TrainTail{TeReduceTail{c, rows_edge, rows_msg}, nte, nmem, nst}, s,
-                    gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe), gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp),
-                    gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp), gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg));
+  if (two)
+    gemm_fixup_launch(nte + nmem + nst + nring, tail, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
+                      gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
+                      gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg),
+                      gemm_fix<G32>(shp_dWp2(k, c.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC}),
+                      gemm_fix<G32>(shp_dWe2(k, c.cnt), c.pF, EpiStore{G + c.L.we2, nullptr, D + d, 0}));
+  else
+    gemm_fixup_launch(nte + nmem + nst + nring, tail, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
+                      gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
+                      gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg));
   probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgn_fixup_update");
   return TGNX_OK;
@@ -1974,9 +2238,11 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   hipStream_t s = as_stream(stream);
   const float* P = c.params;
   const int D = c.D, HC = c.HC, d = c.d;
-  const int Rq = (int)std::min<int64_t>(c.N, (int64_t)k.B * (2 + Kn));
+  const bool two = k.layers == 2;
+  const int R1q = (int)std::min<int64_t>(c.N, (int64_t)k.B * (2 + Kn));  // roots
+  const int Rq = two ? (int)std::min<int64_t>(c.N, (int64_t)R1q * (c.K + 1)) : R1q;  // (outer) centres
   const int Mq = (int)std::min<int64_t>(c.N, (int64_t)Rq * (c.K + 1));
-  const int Eq = Rq * c.K;
+  const int Eq = Rq * c.K, E1q = two ? R1q * c.K : 0;
   tgn_mark<false><<<gridn((int64_t)k.B * (2 + Kn) * 16, 256), 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_mark");
   tgn_scan<false><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
@@ -1985,18 +2251,35 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   tgn_agg_emit<<<nedge + gridn(Mq, 256), 256, 0, s>>>(c, 1, nedge, nullptr, nullptr, 0, 0);
   TGNX_LAUNCH_CHECK("tgn_emit");
   const LoadEdgeAttr ea{c.encE, c.e_id, c.ev_msg, D, d};
-  gemm2_launch<G32, G32>(gemm_shape<G32>(Eq, HC, D + d, c.cnt + CNT_E), ea, LoadRowK{P + c.L.we, HC, D + d, D + d},
-               EpiStore{c.Ep, nullptr, HC, 0}, nullptr, gemm_shape<G32>(Mq, 4 * HC, D, c.cnt + CNT_M),
-               LoadZ{c.Z0, c.mem, c.nid, D, 1}, LoadProjW{P + c.L.wq, c.L.pw, HC, D},
-               EpiProj{P + c.L.bq, c.L.pb, c.P, HC}, nullptr, s);
+  const auto j_edge = gemm_job<G32>(gemm_shape<G32>(Eq, HC, D + d, c.cnt + CNT_E), ea,
+                                    LoadRowK{P + c.L.we, HC, D + d, D + d}, EpiStore{c.Ep, nullptr, HC, 0}, (float*)nullptr);
+  const auto j_proj = gemm_job<G32>(gemm_shape<G32>(Mq, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 1},
+                                    LoadProjW{P + c.L.wq, c.L.pw, HC, D}, EpiProj{P + c.L.bq, c.L.pb, c.P, HC},
+                                    (float*)nullptr);
+  if (two)
+    gemmN_launch(s, j_edge, j_proj,
+                 gemm_job<G32>(gemm_shape<G32>(E1q, HC, D + d, c.cnt + CNT_E1),
+                               LoadEdgeAttrMap{c.encE, c.e1_id, c.e1_e2, c.ev_msg, D, d},
+                               LoadRowK{P + c.L.we2, HC, D + d, D + d}, EpiStore{c.Ep2, nullptr, HC, 0}, (float*)nullptr));
+  else
+    gemmN_launch(s, j_edge, j_proj);
   TGNX_LAUNCH_CHECK("tgn_edge_proj");
   tgn_attn_fwd<false><<<gridn(Rq, 4, 1 << 20), 256, 0, s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_attn_fwd");
-  gemm2_launch<G32, G32>(gemm_shape<G32>(Rq, D, D, c.cnt + CNT_R), LoadRowK{c.Zc, Rq, D, D}, LoadRowK{P + c.L.lsw, D, D, D},
-               EpiStore{c.Hs, P + c.L.lsb, D, 0}, nullptr, gemm_shape<G32>(Rq, D, D, c.cnt + CNT_R),
-               LoadRowK{c.Zc, Rq, D, D}, LoadRowK{P + c.L.ldw, D, D, D}, EpiStore{c.Hd, P + c.L.ldb, D, 0}, nullptr, s);
+  const Ctx cr = two ? root_view(c) : c;
+  if (two) {
+    gemm_launch<G32>(gemm_shape<G32>(Rq, 4 * HC, HC, c.cnt + CNT_R), LoadRowK{c.Zc, Rq, HC, HC},
+                     LoadProjW{P + c.L.wq2, c.L.pw, HC, HC}, EpiProj{P + c.L.bq2, c.L.pb, c.P2, HC}, nullptr, s);
+    TGNX_LAUNCH_CHECK("tgn_proj2");
+    tgn_attn_fwd<false><<<gridn(R1q, 4, 1 << 20), 256, 0, s>>>(cr);
+    TGNX_LAUNCH_CHECK("tgn_attn_fwd2");
+  }
+  gemm2_launch<G32, G32>(gemm_shape<G32>(R1q, D, D, c.cnt + cr.rsel), LoadRowK{cr.Zc, R1q, D, D},
+               LoadRowK{P + c.L.lsw, D, D, D}, EpiStore{c.Hs, P + c.L.lsb, D, 0}, nullptr,
+               gemm_shape<G32>(R1q, D, D, c.cnt + cr.rsel), LoadRowK{cr.Zc, R1q, D, D}, LoadRowK{P + c.L.ldw, D, D, D},
+               EpiStore{c.Hd, P + c.L.ldb, D, 0}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_lin_src_dst");
-  tgn_score<<<k.B, 256, 0, s>>>(c);
+  tgn_score<<<k.B, 256, 0, s>>>(cr);
   TGNX_LAUNCH_CHECK("tgn_score");
   // update_state in eval order: stores first, then the GRU of src ∪ dst; ring insert
   const int nst = gridn(2 * k.B, 256), nring = gridn(2 * k.B, 4);

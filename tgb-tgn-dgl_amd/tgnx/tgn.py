@@ -33,6 +33,12 @@ PARAM_ORDER = [  # flat-buffer order = tgnx_tgn_param_layout
     "link_pred.lin_src.weight", "link_pred.lin_src.bias", "link_pred.lin_dst.weight", "link_pred.lin_dst.bias",
     "link_pred.lin_final.weight", "link_pred.lin_final.bias",
 ]
+# layers = 2 (2-hop temporal attention, SURVEY §8d comment config): gnn.conv2 after the 21 above
+PARAM_ORDER2 = PARAM_ORDER + [
+    "gnn.conv2.lin_key.weight", "gnn.conv2.lin_key.bias", "gnn.conv2.lin_query.weight", "gnn.conv2.lin_query.bias",
+    "gnn.conv2.lin_value.weight", "gnn.conv2.lin_value.bias", "gnn.conv2.lin_edge.weight",
+    "gnn.conv2.lin_skip.weight", "gnn.conv2.lin_skip.bias",
+]
 
 
 class TgnConfig(ctypes.Structure):
@@ -40,7 +46,7 @@ class TgnConfig(ctypes.Structure):
                 ("mem_dim", ctypes.c_int32), ("msg_dim", ctypes.c_int32), ("heads", ctypes.c_int32),
                 ("max_batch", ctypes.c_int32), ("max_neg", ctypes.c_int32), ("aggr", ctypes.c_int32),
                 ("dropout", ctypes.c_float), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
-                ("beta2", ctypes.c_float), ("eps", ctypes.c_float)]
+                ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("layers", ctypes.c_int32)]
 
 
 class TgnBuffers(ctypes.Structure):
@@ -51,7 +57,7 @@ class TgnBuffers(ctypes.Structure):
                 ("xcap", ctypes.c_int64)]
 
 
-def param_shapes(D: int, d: int) -> dict:
+def param_shapes(D: int, d: int, layers: int = 1) -> dict:
     Q = 3 * D + d
     s = {"memory.time_enc.lin.weight": (D, 1), "memory.time_enc.lin.bias": (D,),
          "memory.gru.weight_ih": (3 * D, Q), "memory.gru.weight_hh": (3 * D, D),
@@ -60,25 +66,28 @@ def param_shapes(D: int, d: int) -> dict:
          "link_pred.lin_src.weight": (D, D), "link_pred.lin_src.bias": (D,),
          "link_pred.lin_dst.weight": (D, D), "link_pred.lin_dst.bias": (D,),
          "link_pred.lin_final.weight": (1, D), "link_pred.lin_final.bias": (1,)}
-    for k in ("key", "query", "value", "skip"):
-        s[f"gnn.conv.lin_{k}.weight"] = (D, D)
-        s[f"gnn.conv.lin_{k}.bias"] = (D,)
+    convs = ("conv", "conv2") if layers == 2 else ("conv",)
+    for cv in convs:
+        for k in ("key", "query", "value", "skip"):
+            s[f"gnn.{cv}.lin_{k}.weight"] = (D, D)
+            s[f"gnn.{cv}.lin_{k}.bias"] = (D,)
+        s[f"gnn.{cv}.lin_edge.weight"] = (D, D + d)
     return s
 
 
-def reference_init(D: int, d: int, generator=None) -> dict:
+def reference_init(D: int, d: int, generator=None, layers: int = 1) -> dict:
     g = generator
 
     def unif(shape, bound):
         return (torch.rand(shape, generator=g) * 2 - 1) * bound
 
     out = {}
-    for name, shape in param_shapes(D, d).items():
+    for name, shape in param_shapes(D, d, layers).items():
         if name.startswith("memory.time_enc"):
             bound = 1.0                                   # Linear(1, D): fan_in = 1
         elif name.startswith("memory.gru"):
             bound = 1.0 / math.sqrt(D)                    # GRUCell.reset_parameters
-        elif name == "gnn.conv.lin_edge.weight":
+        elif name.endswith("lin_edge.weight"):
             bound = 1.0 / math.sqrt(D + d)
         else:
             bound = 1.0 / math.sqrt(D)                    # fan_in D (conv / predictor linears)
@@ -94,7 +103,7 @@ class TGNModel(nn.Module):
     """memory + gnn + link_pred of pyg_model_utils.py:10-36 over one flat parameter buffer."""
 
     def __init__(self, num_nodes, num_events, msg_dim, hidden_dim, device, ring=10, max_batch=2048, max_neg=1,
-                 aggr="last", dropout=0.1, generator=None):
+                 aggr="last", dropout=0.1, generator=None, layers=1):
         super().__init__()
         dev = _lib.require_device(device)
         D, d = int(hidden_dim), int(msg_dim)
@@ -102,28 +111,36 @@ class TGNModel(nn.Module):
         self.num_nodes, self.num_events, self.D, self.d = int(num_nodes), num_events, D, d
         self.cfg = TgnConfig(num_nodes=num_nodes, num_events=num_events, ring=ring, mem_dim=D, msg_dim=d, heads=2,
                              max_batch=max_batch, max_neg=max_neg, aggr=0 if aggr == "last" else 1, dropout=dropout,
-                             lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8)
-        off = (ctypes.c_int64 * 22)()
+                             lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8, layers=int(layers))
+        if layers not in (1, 2):
+            raise ValueError(f"layers must be 1 or 2, got {layers}")
+        self.layers = int(layers)
+        order = PARAM_ORDER2 if layers == 2 else PARAM_ORDER
+        self.param_order = order
+        off = (ctypes.c_int64 * (len(order) + 1))()
         _lib.call("tgnx_tgn_param_layout", ctypes.byref(self.cfg), off)
         self.offsets = list(off)
         total = self.offsets[-1]
         self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
         self.grad_flat = torch.zeros(total + 1, dtype=torch.float32, device=dev)    # + batch-loss slot
-        shapes = param_shapes(D, d)
-        init = reference_init(D, d, generator)
+        shapes = param_shapes(D, d, layers)
+        init = reference_init(D, d, generator, layers)
         self.memory = _Holder()
         self.memory.time_enc = _Holder()
         self.memory.time_enc.lin = _Holder()
         self.memory.gru = _Holder()
         self.gnn = _Holder()
         self.gnn.conv = _Holder()
-        for k in ("key", "query", "value", "edge", "skip"):
-            setattr(self.gnn.conv, f"lin_{k}", _Holder())
+        if layers == 2:
+            self.gnn.conv2 = _Holder()
+        for cv in (("conv", "conv2") if layers == 2 else ("conv",)):
+            for k in ("key", "query", "value", "edge", "skip"):
+                setattr(getattr(self.gnn, cv), f"lin_{k}", _Holder())
         self.link_pred = _Holder()
         for k in ("src", "dst", "final"):
             setattr(self.link_pred, f"lin_{k}", _Holder())
         self._views = {}
-        for name, o in zip(PARAM_ORDER, self.offsets[:-1]):
+        for name, o in zip(order, self.offsets[:-1]):
             n = int(np.prod(shapes[name]))
             view = self.flat[o:o + n].view(shapes[name])
             view.copy_(init[name].to(dev))
