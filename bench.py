@@ -276,7 +276,7 @@ def run_tgn(args, world, rank, dev):
     g = torch.Generator().manual_seed(0)
     model = TGNModel(N, stream.num_events, d, D, dev, ring=K, max_batch=Bg, max_neg=1,
                      aggr="mean" if args.aggr == "mean" else "last", dropout=0.0 if args.no_dropout else 0.1,
-                     generator=g)
+                     generator=g, layers=args.layers)
     opt = TgnAdam(model, 1e-4)
     loader = LastNeighborLoader(N, K, device=dev)
     eng = TgnEngine(model, loader, dict(src=stream.src, dst=stream.dst, t=stream.t.astype(np.float32), msg=stream.msg),
@@ -375,7 +375,7 @@ def run_tgn(args, world, rank, dev):
     # cpu_baseline leg)
     from tgnx.synth import eval_negatives
     nval = min(10, max(1, (stream.val_end - stream.train_end) // args.batch))
-    negs = eval_negatives(stream, "val", shape.num_neg_eval)
+    negs = eval_negatives(stream, "val", shape.num_neg_eval, limit=nval * args.batch)
     eng.flush()
     torch.cuda.synchronize()
     tv = time.perf_counter()
@@ -405,13 +405,16 @@ def run_tgn(args, world, rank, dev):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic tgbl-wiki-shaped stream (SURVEY.md §8d), events resident in HBM",
+        "data": f"synthetic {args.dataset}-shaped stream (SURVEY.md §8d), events resident in HBM",
         "config": {"workload": f"{args.dataset} TGN memory path (TGNMemory + GRUCell, IdentityMessage + "
-                               f"{'Mean' if args.aggr == 'mean' else 'Last'}Aggregator, TransformerConv heads=2, "
+                               f"{'Mean' if args.aggr == 'mean' else 'Last'}Aggregator, "
+                               f"{'2-hop temporal attention (conv2(conv1)), ' if args.layers == 2 else ''}"
+                               f"TransformerConv heads=2, "
                                f"LinkPredictor), batch {args.batch}/GPU, {K} temporal neighbours, D=100, d={d}, "
                                f"attention dropout {'off' if args.no_dropout else '0.1'}",
                    "global_batch": Bg, "parallelism": f"dp{world}",
                    "launch": "hip-graph replay per step" if use_graph else "eager",
+                   "layers": args.layers,
                    "sampled_edges_per_step": round(probes[dom]["edges"], 1),
                    "sampled_nodes_per_step": round(probes[dom]["nodes"], 1)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(pd["gbs"], 2), "peak": HBM_PEAK_GBS,
@@ -438,6 +441,8 @@ def main():
     ap.add_argument("--model", choices=["tgn", "tgnn"], default="tgn",
                     help="tgn: the TGN memory path (north star, headline); tgnn: the running DGL block-loop path")
     ap.add_argument("--aggr", choices=["last", "mean"], default="last")
+    ap.add_argument("--layers", type=int, choices=[1, 2], default=1,
+                    help="TGN attention hops (2: the comment config's 2-hop temporal attention)")
     ap.add_argument("--only", action="store_true", help="skip the secondary path")
     ap.add_argument("--no-dropout", action="store_true", help="train mode without dropout")
     ap.add_argument("--no-cpu-baseline", action="store_true")

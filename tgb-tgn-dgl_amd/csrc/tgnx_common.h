@@ -92,6 +92,37 @@ __device__ __forceinline__ int block_excl_scan(int v, int* sh, int* total) {
   return r;
 }
 
+// Two exclusive scans sharing the barriers of one.  `sh` must hold >= 40 ints of LDS.
+__device__ __forceinline__ void block_excl_scan2(int a, int b, int* sh, int* ra, int* rb, int* ta, int* tb) {
+  const int l = lane_id();
+  const int w = threadIdx.x / WAVE;
+  const int nw = (blockDim.x + WAVE - 1) / WAVE;
+  const int ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+  if (l == WAVE - 1) {
+    sh[w] = ia;
+    sh[20 + w] = ib;
+  }
+  __syncthreads();
+  if (w == 0) {
+    const int s = (l < nw) ? sh[l] : 0, t = (l < nw) ? sh[20 + l] : 0;
+    const int si = wave_incl_scan(s), ti = wave_incl_scan(t);
+    if (l < nw) {
+      sh[l] = si - s;
+      sh[20 + l] = ti - t;
+    }
+    if (l == nw - 1) {
+      sh[16] = si;
+      sh[36] = ti;
+    }
+  }
+  __syncthreads();
+  *ra = ia - a + sh[w];
+  *rb = ib - b + sh[20 + w];
+  *ta = sh[16];
+  *tb = sh[36];
+  __syncthreads();
+}
+
 // In-LDS bitonic sort of n (power of two) uint64 keys, ascending, by the whole block.
 __device__ __forceinline__ void bitonic_sort_u64(uint64_t* key, int n) {
   for (int k = 2; k <= n; k <<= 1) {

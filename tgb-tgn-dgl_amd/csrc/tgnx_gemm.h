@@ -79,8 +79,17 @@ inline GemmShape gemm_shape_split(int M, int N, int K, const int* Mdev, const in
   g.deferred = 1;
   return g;
 }
-// grid of a GEMM: tiles x splits, padded to a multiple of the 8 XCDs (see gemm_work)
-__host__ __device__ inline int gemm_blocks(const GemmShape& g) { return (g.tiles_m * g.tiles_n * g.S + 7) & ~7; }
+// grid of a GEMM: tiles x splits of the CAPACITY shape, padded to a multiple of the 8 XCDs (see gemm_work),
+// capped: capacities are worst cases (a 2-hop sample is sized for 2e5 rows and runs ~1e3), and
+// dispatching 1e5 workgroups that exit at once cost ~80 us per launch; a workgroup loops over the
+// runtime work in strides of the grid instead (gemm_body).
+#ifndef TGNX_GEMM_GRID_CAP
+#define TGNX_GEMM_GRID_CAP 2048
+#endif
+__host__ __device__ inline int gemm_blocks(const GemmShape& g) {
+  const int full = (g.tiles_m * g.tiles_n * g.S + 7) & ~7;
+  return full < TGNX_GEMM_GRID_CAP ? full : TGNX_GEMM_GRID_CAP;
+}
 inline size_t gemm_partial_floats(const GemmShape& g) {
   return g.deferred ? (size_t)g.tiles_m * g.tiles_n * g.S * g.tm * g.tn : 0;
 }
@@ -210,17 +219,15 @@ __device__ __forceinline__ GemmWork gemm_work(const GemmShape& g, int Mr, int Nr
   return w;
 }
 
-// One workgroup of a GEMM (`bid` in [0, gemm_blocks(g))); `smem` holds CFG::SMEM floats.
-// A kernel may host several GEMMs by dispatching on block ranges.
+// One work item (virtual block `bid` of the XCD-grouped order) of a GEMM; `smem` holds CFG::SMEM floats.
 template <class CFG, class AL, class BL, class EPI>
-__device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, const BL& bl, const EPI& epi, float* part,
-                                          int bid, float* smem) {
+__device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, const AL& al, const BL& bl,
+                                          const EPI& epi, float* part, int bid, float* smem) {
   constexpr int TM = CFG::TM, TN = CFG::TN, KC = CFG::KC, FM = CFG::FM, FN = CFG::FN;
   constexpr int PK = CFG::PK, PB = CFG::PB, LA = CFG::LA, LB = CFG::LB;
   float* As = smem;            // [TM][PK]: row m, k contiguous
   float* Bs = smem + TM * PK;  // [TN][PK]: row n, k contiguous
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const GemmRt rt = gemm_runtime<CFG>(g);
   const GemmWork wk = gemm_work<TM, TN>(g, rt.Mr, rt.Nr, rt.Sr, bid);
   const int tile = wk.tile, s = wk.s;
   const int m0 = wk.tm * TM, n0 = wk.tn * TN;
@@ -367,6 +374,19 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
       for (int r = 0; r < 4; ++r) Ct[(wr + 16 * i + lk * 4 + r) * PB + wc + 16 * j + li] = acc[i][j][r];
   __syncthreads();
   epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, smem + TM * PB});
+}
+// Workgroup `bid` in [0, gemm_blocks(g)) of a GEMM: the virtual blocks bid, bid + grid, ... that carry
+// runtime work.  A kernel may host several GEMMs by dispatching on block ranges.
+template <class CFG, class AL, class BL, class EPI>
+__device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, const BL& bl, const EPI& epi, float* part,
+                                          int bid, float* smem) {
+  const GemmRt rt = gemm_runtime<CFG>(g);
+  const int tmr = (rt.Mr + CFG::TM - 1) / CFG::TM, tnr = (rt.Nr + CFG::TN - 1) / CFG::TN;
+  const int per = (tmr * tnr * rt.Sr + 7) >> 3, grid = gemm_blocks(g);
+  for (int vb = bid; vb < 8 * per; vb += grid) {
+    gemm_tile<CFG>(g, rt, al, bl, epi, part, vb, smem);
+    __syncthreads();
+  }
 }
 
 template <class CFG, class AL, class BL, class EPI>

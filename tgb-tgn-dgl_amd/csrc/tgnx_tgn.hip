@@ -105,7 +105,9 @@ struct Ctx {
   float* xrows;  // data parallel: this rank's updated memory rows (TGNX_TGN_ROW layout), or nullptr
   int xcap;
   // workspace
-  uint32_t *cb, *nb;
+  uint32_t *cb, *nb;       // centre / sampled-node bitmaps over N
+  uint32_t *cbs, *nbs, *rbs;  // their summaries (bit per word)
+  int *cl, *nl, *rl;       // tgn_scan: nonzero word lists
   int* kval;  // [N] valid ring slots of a centre (written by tgn_mark for this batch's centres)
   int* cnt;
   int64_t *cent, *nid, *upd;
@@ -147,6 +149,18 @@ __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x))
 __device__ __forceinline__ float softplusf(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
 
 // ------------------------------------------------------------------ sampling (neighbor_loader.py:26-50)
+// Node sets are bitmaps over N with a summary level (bit per bitmap word, set by the lane whose atomicOr
+// found the word empty), so tgn_scan visits only the words that hold nodes: O(sampled + N / 1024)
+// instead of O(N / 32) per batch (a single-workgroup walk of a 1M-node bitmap took ~40 us per pass).
+// Plain read first: hub words are hit by many lanes, most find the bit set.
+__device__ __forceinline__ void mark_node(uint32_t* bm, uint32_t* sum, int64_t v) {
+  const int64_t w = v >> 5;
+  const uint32_t bit = 1u << (v & 31);
+  if (!(bm[w] & bit)) {
+    if (atomicOr(&bm[w], bit) == 0u) atomicOr(&sum[w >> 5], 1u << (w & 31));
+  }
+}
+
 // K1: every query entry marks its node as a centre and its node + valid ring neighbours as sampled;
 // train negatives are drawn here (NegLinkSamplerDest, counter-based stream as in tgnx_tgnn);
 // src / pos nodes are stamped for the update list (memory_module.py:129).  16 lanes per entry, one
@@ -195,11 +209,11 @@ __global__ void tgn_mark(Ctx c) {
       const bool ok = j < c.K && c.eid[v * c.K + j] >= 0;
       if (ok) {  // plain read first: hub words are hit by many lanes, most find the bit set
         const int64_t u = c.nbr[v * c.K + j];
-        if (!(c.nb[u >> 5] & (1u << (u & 31)))) atomicOr(&c.nb[u >> 5], 1u << (u & 31));
+        mark_node(c.nb, c.nbs, u);
         if (c.layers == 2) {
           // 2 hops: the neighbour is an outer centre; its own ring neighbours are sampled nodes
           // (the lane walks u's ring row, all K slot loads issued before the marking)
-          if (!(c.cb[u >> 5] & (1u << (u & 31)))) atomicOr(&c.cb[u >> 5], 1u << (u & 31));
+          mark_node(c.cb, c.cbs, u);
           int ku = 0;
           for (int i0 = 0; i0 < c.K; i0 += 8) {
             int64_t ev[8], w[8];
@@ -214,7 +228,7 @@ __global__ void tgn_mark(Ctx c) {
               if (i0 + i >= c.K || ev[i] < 0) continue;
               ++ku;
               const int64_t x = w[i];
-              if (!(c.nb[x >> 5] & (1u << (x & 31)))) atomicOr(&c.nb[x >> 5], 1u << (x & 31));
+              mark_node(c.nb, c.nbs, x);
             }
           }
           c.kval[u] = ku;
@@ -225,9 +239,9 @@ __global__ void tgn_mark(Ctx c) {
     if (sl == 0) {
       if (q < 2 * nl) c.node_gen[v] = gen;
       c.kval[v] = k;
-      if (!(c.cb[v >> 5] & (1u << (v & 31)))) atomicOr(&c.cb[v >> 5], 1u << (v & 31));
-      if (!(c.nb[v >> 5] & (1u << (v & 31)))) atomicOr(&c.nb[v >> 5], 1u << (v & 31));
-      if (c.layers == 2 && !(c.rb[v >> 5] & (1u << (v & 31)))) atomicOr(&c.rb[v >> 5], 1u << (v & 31));
+      mark_node(c.cb, c.cbs, v);
+      mark_node(c.nb, c.nbs, v);
+      if (c.layers == 2) mark_node(c.rb, c.rbs, v);
     }
   }
 }
@@ -268,6 +282,34 @@ __device__ void store_plan_block(const Ctx& c, int B, int64_t start, unsigned ch
   }
 }
 
+// the indices of the nonzero words of two bitmaps, ascending, from their summaries (cleared); whole block
+__device__ void occupied_words2(uint32_t* sa, uint32_t* sb, int64_t words, int* la, int* lb, int* sh, int* na,
+                                int* nb) {
+  const int T = blockDim.x;
+  const int64_t SW = (words + 31) >> 5, sc = (SW + T - 1) / T, s0 = min(SW, threadIdx.x * sc), s1 = min(SW, s0 + sc);
+  int ca = 0, cb = 0;
+  for (int64_t i = s0; i < s1; ++i) {
+    ca += __popc(sa[i]);
+    cb += sb ? __popc(sb[i]) : 0;
+  }
+  int oa, ob;
+  block_excl_scan2(ca, cb, sh, &oa, &ob, na, nb);
+  auto emit = [&](uint32_t* sum, int* list, int o) {
+    for (int64_t i = s0; i < s1; ++i) {
+      uint32_t m = sum[i];
+      if (!m) continue;
+      sum[i] = 0u;
+      while (m) {
+        const int b = __ffs(m) - 1;
+        m &= m - 1;
+        list[o++] = (int)((i << 5) + b);
+      }
+    }
+  };
+  emit(sa, la, oa);
+  if (sb) emit(sb, lb, ob);
+}
+
 // K2 (3 workgroups): WG0 ordered bitmap walks -> centres (+ edge offsets, update list) and sampled
 // nodes (+ assoc, centre ranks); WG1 ring-insert plan; WG2 message-store plan.
 __host__ __device__ inline size_t tgn_scan_smem(int Bmax) {
@@ -277,7 +319,7 @@ __host__ __device__ inline size_t tgn_scan_smem(int Bmax) {
 template <bool TRAIN>
 __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ int sh[20];
+  __shared__ int sh[40];
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
@@ -299,19 +341,40 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
     return;
   }
   const int gen = (int)c.ctl[TGNX_CTL_GEN];
-  const int64_t W = c.words;
-  const int64_t wc = (W + T - 1) / T, w0 = tid * wc, w1 = min(W, w0 + wc);
-  // pass 1: centres (sorted) and sampled nodes (sorted, + assoc) from the bitmaps; no other loads
-  int nc = 0, np = 0;
-  for (int64_t w = w0; w < w1; ++w) {
-    nc += __popc(c.cb[w]);
-    np += __popc(c.nb[w]);
+  // pass 0: the words each thread walks.  Small graphs (<= 2 words per thread): contiguous word ranges
+  // (summaries just cleared); large graphs: the nonzero words in word order, from the summaries
+  const bool direct = c.words <= 2 * (int64_t)T;
+  int ncw, nnw, nrw = 0;
+  if (direct) {
+    ncw = nnw = (int)c.words;
+    if (c.layers == 2) nrw = (int)c.words;
+    const int64_t SW = (c.words + 31) >> 5;
+    for (int64_t i = tid; i < SW; i += T) {
+      c.cbs[i] = c.nbs[i] = 0u;
+      if (c.layers == 2) c.rbs[i] = 0u;
+    }
+  } else {
+    occupied_words2(c.cbs, c.nbs, c.words, c.cl, c.nl, sh, &ncw, &nnw);
+    if (c.layers == 2) {
+      int unused;
+      occupied_words2(c.rbs, nullptr, c.words, c.rl, nullptr, sh, &nrw, &unused);
+    }
+    __threadfence_block();
+    __syncthreads();
   }
-  int R, M;
-  int rc = block_excl_scan(nc, sh, &R);
-  int rank = block_excl_scan(np, sh, &M);
+  auto word = [&](const int* list, int i) -> int64_t { return direct ? (int64_t)i : (int64_t)list[i]; };
+  // pass 1: centres (sorted) and sampled nodes (sorted, + assoc): thread t takes a contiguous run of each
+  // word list; block scans give the ranks; words are cleared
+  const int cq = (ncw + T - 1) / T, c0 = min(ncw, tid * cq), c1 = min(ncw, c0 + cq);
+  const int nq = (nnw + T - 1) / T, n0 = min(nnw, tid * nq), n1 = min(nnw, n0 + nq);
+  int nc = 0, np = 0;
+  for (int i = c0; i < c1; ++i) nc += __popc(c.cb[word(c.cl, i)]);
+  for (int i = n0; i < n1; ++i) np += __popc(c.nb[word(c.nl, i)]);
+  int R, M, rc, rank;
+  block_excl_scan2(nc, np, sh, &rc, &rank, &R, &M);
   const bool fits = R <= c.Rcap && M <= c.Mcap;
-  for (int64_t w = w0; w < w1; ++w) {
+  for (int i = c0; i < c1; ++i) {
+    const int64_t w = word(c.cl, i);
     uint32_t m = c.cb[w];
     if (m) c.cb[w] = 0u;
     while (m) {
@@ -320,7 +383,10 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
       if (fits) c.cent[rc] = (w << 5) + b;
       ++rc;
     }
-    m = c.nb[w];
+  }
+  for (int i = n0; i < n1; ++i) {
+    const int64_t w = word(c.nl, i);
+    uint32_t m = c.nb[w];
     if (m) c.nb[w] = 0u;
     while (m) {
       const int b = __ffs(m) - 1;
@@ -333,6 +399,7 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
   }
   if (!fits) {
     if (tid == 0) c.ctl[TGNX_CTL_ERR] |= 4;
+    for (int i = tid; i < nrw; i += T) c.rb[word(c.rl, i)] = 0u;  // leave every bitmap empty
     return;
   }
   for (int x = tid; x < M; x += T) c.crank[x] = -1;
@@ -347,9 +414,8 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
     ne += c.kval[v];
     nu += c.node_gen[v] == gen;
   }
-  int E, U;
-  int re = block_excl_scan(ne, sh, &E);
-  int ru = block_excl_scan(nu, sh, &U);
+  int E, U, re, ru;
+  block_excl_scan2(ne, nu, sh, &re, &ru, &E, &U);
   for (int x = x0; x < x1; ++x) {
     const int64_t v = c.cent[x];
     const int loc = (int)c.assoc[v];
@@ -378,8 +444,10 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
   // complete after the barrier), root edge offsets (a root's edges are its outer edge range)
   __threadfence_block();
   __syncthreads();
+  const int rq = (nrw + T - 1) / T, q0 = min(nrw, tid * rq), q1 = min(nrw, q0 + rq);
   int nr = 0, nre = 0;
-  for (int64_t w = w0; w < w1; ++w) {
+  for (int i = q0; i < q1; ++i) {
+    const int64_t w = word(c.rl, i);
     uint32_t m = c.rb[w];
     nr += __popc(m);
     while (m) {
@@ -388,14 +456,15 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
       nre += c.kval[(w << 5) + b];
     }
   }
-  int R1, E1;
-  int r1 = block_excl_scan(nr, sh, &R1);
-  int e1 = block_excl_scan(nre, sh, &E1);
+  int R1, E1, r1, e1;
+  block_excl_scan2(nr, nre, sh, &r1, &e1, &R1, &E1);
   if (R1 > c.R1cap) {
     if (tid == 0) c.ctl[TGNX_CTL_ERR] |= 4;
+    for (int i = tid; i < nrw; i += T) c.rb[word(c.rl, i)] = 0u;
     return;
   }
-  for (int64_t w = w0; w < w1; ++w) {
+  for (int i = q0; i < q1; ++i) {
+    const int64_t w = word(c.rl, i);
     uint32_t m = c.rb[w];
     if (m) c.rb[w] = 0u;
     while (m) {
@@ -1750,7 +1819,7 @@ static GemmShape shp_dWe2(const Caps& k, const int* cnt) { return gemm_shape_spl
 static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, 5); }
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
 struct WsLay {
-  size_t cb, nb, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
+  size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
       Ep, alpha, Zc, evs, Hs, Hd, dZc, dP, dE, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
       rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF, total;
   int tgp_rows, tgp_e1;
@@ -1762,6 +1831,11 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   const int D = k.D, HC = k.HC;
   W.cb = carve(off, words * 4);
   W.nb = carve(off, words * 4);
+  const int64_t swords = (words + 31) / 32 + 1;
+  W.cbs = carve(off, swords * 4);
+  W.nbs = carve(off, swords * 4);
+  W.cl = carve(off, words * 4);
+  W.nl = carve(off, words * 4);
   W.kval = carve(off, (size_t)k.N * 4);
   W.cnt = carve(off, CNT_WORDS * 4);
   W.cent = carve(off, (size_t)k.Rcap * 8);
@@ -1811,6 +1885,8 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   const bool two = k.layers == 2;
   const size_t R1 = two ? k.R1cap : 0, E1 = k.E1cap, R2 = two ? k.Rcap : 0;
   W.rb = carve(off, two ? words * 4 : 0);
+  W.rbs = carve(off, two ? swords * 4 : 0);
+  W.rl = carve(off, two ? words * 4 : 0);
   W.x2r = carve(off, R2 * 4);
   W.cent1 = carve(off, R1 * 8);
   W.r_x2 = carve(off, R1 * 4);
@@ -1903,6 +1979,10 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   char* ws = reinterpret_cast<char*>(b->ws);
   c.cb = reinterpret_cast<uint32_t*>(ws + W.cb);
   c.nb = reinterpret_cast<uint32_t*>(ws + W.nb);
+  c.cbs = reinterpret_cast<uint32_t*>(ws + W.cbs);
+  c.nbs = reinterpret_cast<uint32_t*>(ws + W.nbs);
+  c.cl = reinterpret_cast<int*>(ws + W.cl);
+  c.nl = reinterpret_cast<int*>(ws + W.nl);
   c.kval = reinterpret_cast<int*>(ws + W.kval);
   c.cnt = reinterpret_cast<int*>(ws + W.cnt);
   c.cent = reinterpret_cast<int64_t*>(ws + W.cent);
@@ -1959,6 +2039,8 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.att_salt = 7;
   if (k.layers == 2) {
     c.rb = reinterpret_cast<uint32_t*>(ws + W.rb);
+    c.rbs = reinterpret_cast<uint32_t*>(ws + W.rbs);
+    c.rl = reinterpret_cast<int*>(ws + W.rl);
     c.x2r = reinterpret_cast<int*>(ws + W.x2r);
     c.cent1 = reinterpret_cast<int64_t*>(ws + W.cent1);
     c.r_x2 = reinterpret_cast<int*>(ws + W.r_x2);

@@ -117,13 +117,16 @@ def make_stream(shape: StreamShape | str, seed: int = 0, num_events: int | None 
 
 
 def eval_negatives(stream: TemporalStream, split: str, num_neg: int | None = None,
-                   seed: int = 1) -> np.ndarray:
+                   seed: int = 1, limit: int | None = None) -> np.ndarray:
     """Per-positive eval negatives drawn from the destination set, excluding the positive.
 
-    Stands in for TGB's precomputed `*_ns.pkl` (`epoch_utils.py:43`): Long[E_split, num_neg].
+    Stands in for TGB's precomputed `*_ns.pkl` (`epoch_utils.py:43`): Long[E_split, num_neg]
+    (the split's first `limit` events only, if given).
     """
     sl = stream.split(split)
     pos = stream.dst[sl]
+    if limit is not None:
+        pos = pos[:limit]
     k = stream.shape.num_neg_eval if num_neg is None else num_neg
     rng = np.random.default_rng(seed + (0 if split == "val" else 7919))
     cand = stream.dst_nodes
