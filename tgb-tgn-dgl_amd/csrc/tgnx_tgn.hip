@@ -14,6 +14,7 @@
 //   tgn_attn_fwd    TransformerConv softmax + aggregation per centre (wave per centre)
 //   tgn_pred_train  LinkPredictor + BCE + backward rows per event
 //   tgn_attn_bwd    attention backward ‖ predictor bias / output-layer / loss reductions
+//   tgn_kv_reduce   per-edge dk / dv summed into the neighbours' dP rows (sorted runs, no hub contention)
 //   GEMMs           dW_edge ‖ dW_proj, dW_src/dst ‖ Δt-encoding grads, dZ0 (+ GRU backward epilogue),
 //                   dW_gru ‖ message-encoding grads
 //   tgn_adam, tgn_update (memory / last_update of src ∪ dst, message stores, ring merge)
@@ -119,6 +120,7 @@ struct Ctx {
   int64_t* xw;
   float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
   float *dZc, *dP, *dE, *dG, *tgp;
+  float* dKV;  // per edge [dk | dv] of the attention backward [E][2 HC] (tgn_kv_reduce sums them into dP)
   float *encE, *sinE;  // per sampled edge: cos / sin of the Δt encoding argument [E][D]
   float *s0m, *s1m;    // per GRU row: (mean over its messages of) sin(arg), sin(arg) Δt  [M][D]
   float *pA, *pB, *pC, *pD;  // split-K partials of the deferred weight-gradient GEMMs
@@ -1168,6 +1170,10 @@ __device__ void lp_vec_body(const Ctx& c, int y, int lane) {
 }
 
 // Backward of tgn_attn_fwd (wave per centre) ‖ trailing blocks: lp_vec_body.
+// dk / dv of an edge belong to its neighbour's row of dP.  They are stored per edge (dKV, plain
+// coalesced stores) and summed into dP by tgn_kv_reduce: a hub neighbour is shared by most centres (a
+// wiki-shaped hub user sits in ~40 % of the page rings), and per-edge global atomics on its row
+// serialised at the L2 (attn_bwd 36 us, 15 us without them).
 __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
   if ((int)blockIdx.x >= ncb) {
     lp_vec_body(c, ((int)blockIdx.x - ncb) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
@@ -1240,9 +1246,8 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
       if (e >= ne) break;
       const float d0 = __shfl(ds0, e, 64) / sqc, d1 = __shfl(ds1, e, 64) / sqc;
       const float b0 = __shfl(t0, e, 64), b1 = __shfl(t1, e, 64);
-      const int j = __shfl(jl, e, 64);
-      float* dPj = c.dP + (int64_t)j * 4 * HC;
       float* dEe = c.dE + (int64_t)(e0 + e) * HC;
+      float* dKe = c.dKV + (int64_t)(e0 + e) * 2 * HC;  // [dk (HC) | dv (HC)]
       dq0 += d0 * kk0[u];
       dq1 += d1 * kk1[u];
       if (okl) {
@@ -1250,10 +1255,10 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
         const float dv0 = b0 * g0, dv1 = b1 * g1;
         dEe[lane] = dk0 + dv0;
         dEe[C + lane] = dk1 + dv1;
-        atomicAdd(&dPj[HC + lane], dk0);
-        atomicAdd(&dPj[HC + C + lane], dk1);
-        atomicAdd(&dPj[2 * HC + lane], dv0);
-        atomicAdd(&dPj[2 * HC + C + lane], dv1);
+        dKe[lane] = dk0;
+        dKe[C + lane] = dk1;
+        dKe[HC + lane] = dv0;
+        dKe[HC + C + lane] = dv1;
       }
     }
   }
@@ -1262,6 +1267,77 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
     dPi[C + lane] = dq1;
     dPi[3 * HC + lane] = g0;
     dPi[3 * HC + C + lane] = g1;
+  }
+}
+
+// dP[j][k | v columns] += Σ over edges e with neighbour j of dKV[e] (the zeroed accumulators of
+// agg_emit).  Workgroup per chunk of KVR_CH consecutive edges, sorted by neighbour in LDS (rank by
+// counting); each wave takes KVR_CH / 4 sorted edges, loads all their rows at once (lanes over columns)
+// and sums runs of equal neighbours in registers: one global atomic per (wave, neighbour run, column),
+// so a hub row sees a few atomics per chunk instead of one per edge.  (Merging in LDS with ds_add_f32
+// instead ran at about one element per two clocks per CU: slower than the contention it removed.)
+constexpr int KVR_CH = 64;            // edges per workgroup
+constexpr int KVR_PW = KVR_CH / 4;    // sorted edges per wave
+__global__ void __launch_bounds__(256) tgn_kv_reduce(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int E = c.ceoff[c.cnt[c.rsel]];
+  const int eb = blockIdx.x * KVR_CH;
+  if (eb >= E) return;  // whole workgroup
+  const int ne = min(KVR_CH, E - eb);
+  const int HC = c.HC, H2 = 2 * HC;
+  __shared__ int sj[KVR_CH], sorder[KVR_CH];
+  const int t = threadIdx.x;
+  if (t < KVR_CH) sj[t] = t < ne ? c.e_j[eb + t] : INT_MAX;
+  __syncthreads();
+  if (t < ne) {  // stable rank of (neighbour, edge)
+    const int key = sj[t];
+    int r = 0;
+    for (int u = 0; u < ne; ++u) {
+      const int ju = sj[u];
+      r += (ju < key) || (ju == key && u < t);
+    }
+    sorder[r] = t;
+  }
+  __syncthreads();
+  const int w = t >> 6, lane = t & 63;
+  const int i0 = w * KVR_PW;
+  if (i0 >= ne) return;
+  const int n = min(KVR_PW, ne - i0);
+  int jj[KVR_PW], er[KVR_PW];
+#pragma unroll
+  for (int u = 0; u < KVR_PW; ++u) {
+    const int e = sorder[i0 + min(u, n - 1)];
+    jj[u] = sj[e];
+    er[u] = eb + e;
+  }
+  for (int c0 = 0; c0 < H2; c0 += 256) {  // 4 columns per lane per pass (one pass at HC <= 128)
+    float v[KVR_PW][4];
+#pragma unroll
+    for (int u = 0; u < KVR_PW; ++u)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) v[u][p] = c.dKV[(int64_t)er[u] * H2 + min(c0 + lane + 64 * p, H2 - 1)];
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int jc = jj[0];
+#pragma unroll
+    for (int u = 0; u < KVR_PW; ++u) {
+      const bool in = u < n;
+      if (in && jj[u] != jc) {  // wave-uniform run boundary
+        float* dst = c.dP + (int64_t)jc * 4 * HC + HC + c0 + lane;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          if (c0 + lane + 64 * p < H2) atomicAdd(dst + 64 * p, a[p]);
+          a[p] = 0.f;
+        }
+        jc = jj[u];
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) a[p] += in ? v[u][p] : 0.f;
+    }
+    float* dst = c.dP + (int64_t)jc * 4 * HC + HC + c0 + lane;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      if (c0 + lane + 64 * p < H2) atomicAdd(dst + 64 * p, a[p]);
   }
 }
 
@@ -1820,7 +1896,7 @@ static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_spl
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
-      Ep, alpha, Zc, evs, Hs, Hd, dZc, dP, dE, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
+      Ep, alpha, Zc, evs, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
       rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF, total;
   int tgp_rows, tgp_e1;
 };
@@ -1865,6 +1941,7 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.dZc = carve(off, (size_t)k.Rtr * HC * 4);
   W.dP = carve(off, (size_t)k.Mtr * 4 * HC * 4);
   W.dE = carve(off, (size_t)k.Etr * HC * 4);
+  W.dKV = carve(off, (size_t)(k.Etr > k.E1tr ? k.Etr : k.E1tr) * 2 * HC * 4);  // both levels (used in turn)
   W.dG = carve(off, (size_t)k.Mtr * 4 * D * 4);
   W.tgp_e1 = (k.Etr + G32::TM - 1) / G32::TM + (k.Mtr + G32::TM - 1) / G32::TM;
   W.tgp_rows = W.tgp_e1 + (k.E1tr + G32::TM - 1) / G32::TM;
@@ -2012,6 +2089,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.dZc = reinterpret_cast<float*>(ws + W.dZc);
   c.dP = reinterpret_cast<float*>(ws + W.dP);
   c.dE = reinterpret_cast<float*>(ws + W.dE);
+  c.dKV = reinterpret_cast<float*>(ws + W.dKV);
   c.dG = reinterpret_cast<float*>(ws + W.dG);
   c.tgp = reinterpret_cast<float*>(ws + W.tgp);
   c.encE = reinterpret_cast<float*>(ws + W.encE);
@@ -2218,6 +2296,8 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     const int ncb1 = gridn(k.R1tr, 4, 1 << 20);
     tgn_attn_bwd<<<ncb1 + gridn(3 * D + 2, 4), 256, 0, s>>>(cr, ncb1);
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
+    tgn_kv_reduce<<<gridn(k.E1tr, KVR_CH, 1 << 20), 256, 0, s>>>(cr);
+    TGNX_LAUNCH_CHECK("tgn_kv_reduce2");
     gemmN_launch(s,
                  gemm_job<G32L>(gemm_shape<G32L>(k.Rtr, HC, 4 * HC, c.cnt + CNT_R), LoadRowK{c.dP2, k.Rtr, 4 * HC, 4 * HC},
                                 LoadProjWT{P + c.L.wq2, c.L.pw, HC, HC}, EpiStore{c.dZc, nullptr, HC, 0}, (float*)nullptr),
@@ -2234,8 +2314,10 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     const int ncb = gridn(k.Rtr, 4, 1 << 20);
     tgn_attn_bwd<<<ncb + gridn(3 * D + 2, 4), 256, 0, s>>>(c, ncb);
   }
-  probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_attn_bwd");
+  tgn_kv_reduce<<<gridn(k.Etr, KVR_CH, 1 << 20), 256, 0, s>>>(c);
+  probe_end(TGNX_K_SEG_BWD, s);
+  TGNX_LAUNCH_CHECK("tgn_kv_reduce");
   // weight gradients (deferred split-K) ‖ ...
   const EpiStore e_dWe{G + c.L.we, nullptr, D + d, 0};
   const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D};

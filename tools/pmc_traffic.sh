@@ -1,19 +1,17 @@
 #!/bin/bash
-# HBM-side traffic per kernel launch from rocprofv3 PMC counters, collected as
-# /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3 PMC slots) prescribes: FETCH_SIZE and
-# WRITE_SIZE in separate passes (they do not fit one TCC pass), no trace domains besides the
-# kernel dispatches.  Writes gpurun_out/<tag>_pmc_{fetch,write}/ and gpurun_out/<tag>_pmc_traffic.json
-# (merge into profiles/pmc_traffic.json with tools/pmc_summarize.py after the call; only gpurun_out/
-# comes back from the box).
-#   tools/pmc_traffic.sh <tag> [model]
-tag=${1:-pmc}; model=${2:-tgn}
-cd /tmp && export TMPDIR=/tmp
+# On the GPU box: HBM traffic per launch of the bench's probed kernels from PMC counters, one counter per
+# rocprofv3 pass (FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2: they cannot share a pass), eager launches.
+#   tools/pmc_traffic.sh <tag>  ->  gpurun_out/<tag>_pmc/{tgn,tgnn}_{fetch,write}/run_counter_collection.csv
+#                                   and gpurun_out/<tag>_pmc_traffic.json (tools/pmc_summary.py)
+tag=${1:-pmc}
 R=/root/repo
-for c in FETCH_SIZE WRITE_SIZE; do
-  lc=$(echo $c | cut -d_ -f1 | tr A-Z a-z)
-  timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d $R/gpurun_out/${tag}_pmc_$lc -o run -- \
-    python3 $R/bench.py --model $model --only --steps 20 --warmup 5 --no-cpu-baseline --no-graph --probe-steps 1 \
-    > $R/gpurun_out/${tag}_pmc_$lc.log 2>&1 || exit $?
+cd /tmp && export TMPDIR=/tmp
+for model in tgn tgnn; do
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    sub=$(echo $ctr | cut -d_ -f1 | tr A-Z a-z)
+    timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/${tag}_pmc/${model}_${sub} -o run -- \
+      python3 $R/bench.py --model $model --only --no-graph --steps 30 --warmup 5 --probe-steps 1 --no-cpu-baseline \
+      > $R/gpurun_out/${tag}_pmc_${model}_${sub}.log 2>&1 || exit $?
+  done
 done
-python3 $R/tools/pmc_summarize.py $R/gpurun_out/${tag}_pmc_fetch $R/gpurun_out/${tag}_pmc_write \
-  $R/gpurun_out/${tag}_pmc_traffic.json
+python3 $R/tools/pmc_summary.py $R/gpurun_out/${tag}_pmc > $R/gpurun_out/${tag}_pmc_traffic.json
