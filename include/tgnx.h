@@ -287,10 +287,13 @@ typedef struct {
   double* mrr;                    /* eval: per-event reciprocal ranks of the last batch [B] */
   void* ws;                       /* tgnx_tgn_ws_bytes(cfg), zero-filled once */
   float* xrows;                   /* data parallel (ctl world > 1): [xcap, TGNX_TGN_ROW(mem_dim)] rows this
-                                     rank's step updated, for the all-gather; NULL at world 1 */
+                                     rank's step updated, exchanged after the step; NULL at
+                                     world 1 */
   int64_t xcap;                   /* >= 2 * ceil(max_batch / world) */
 } tgnx_tgn_buffers;
-/* exchanged memory row: int32 node (-1 = unused slot), int64 last_update (lo, hi words), pad, memory[D] */
+/* exchanged memory row, all fields floats holding exact integers so that the row survives a SUM exchange
+ * (one all-reduce over [gradients | every rank's row slots, zero but the sender's] is the all-gather):
+ * node (-1 = unused slot; num_nodes < 2^24), last_update bits 0-23, 24-47, 48-63, memory[D] */
 #define TGNX_TGN_ROW(D) ((D) + 4)
 
 int tgnx_tgn_param_layout(const tgnx_tgn_config* cfg,
@@ -309,10 +312,11 @@ int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf
  * the memory rows this rank updated are packed into buf->xrows for the all-gather. */
 int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg,
                            int32_t dropout, void* stream);
-/* Data parallel: write the all-gathered rows of every rank (rows [nrows, TGNX_TGN_ROW(mem_dim)], slots
- * with node -1 skipped) into memory / last_update.  Ranks that updated the same node computed the
- * same row (same replicated inputs), so the order does not matter. */
-int tgnx_tgn_apply_rows(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, const float* rows, int64_t nrows,
+/* Data parallel: write the exchanged rows of every rank (rows [nrows, TGNX_TGN_ROW(mem_dim)], slots
+ * with node -1 skipped) into memory / last_update, then zero `rows` (ready for the next summing
+ * exchange).  Ranks that updated the same node computed the same row (same replicated inputs), so the
+ * order does not matter. */
+int tgnx_tgn_apply_rows(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, float* rows, int64_t nrows,
                         void* stream);
 /* Train batch, part 2: Adam on the (possibly all-reduced) grads, loss sum. */
 int tgnx_tgn_train_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream);

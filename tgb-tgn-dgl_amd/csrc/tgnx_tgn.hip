@@ -1683,6 +1683,16 @@ __global__ void __launch_bounds__(256) tgn_adam(Ctx c) {
   }
 }
 
+// data-parallel row header (TGNX_TGN_ROW): node, last_update as floats holding exact integers < 2^24
+// (node; last_update bits 0-23, 24-47, 48-63), so that the rows survive the summing exchange (the
+// all-reduce that carries them adds only zeros to them).  Unused slot: node -1.
+__device__ __forceinline__ void xrow_header(float* h, int64_t v, int64_t luv) {
+  const uint64_t b = (uint64_t)luv;
+  h[0] = (float)v;
+  h[1] = (float)(uint32_t)(b & 0xFFFFFFull);
+  h[2] = (float)(uint32_t)((b >> 24) & 0xFFFFFFull);
+  h[3] = (float)(uint32_t)(b >> 48);
+}
 // update_state pieces (memory_module.py:126-150, :180-191) and the ring insert, by block range:
 // [0, nmem): memory / last_update of the update list from the GRU rows (wave per node; train rows
 // are the sampled nodes' rows via assoc, eval / flush rows are list positions);
@@ -1710,18 +1720,11 @@ __device__ void update_body(const Ctx& c, int blk, int nmem, int nst, int mem_mo
       }
       if (lane == 0) {
         c.lu_buf[v] = luv;
-        if (xr) {
-          int* h = reinterpret_cast<int*>(xr + (int64_t)u * RW);
-          h[0] = (int)v;
-          h[1] = (int)(uint32_t)((uint64_t)luv & 0xFFFFFFFFull);
-          h[2] = (int)(uint32_t)((uint64_t)luv >> 32);
-          h[3] = 0;
-        }
+        if (xr) xrow_header(xr + (int64_t)u * RW, v, luv);
       }
     }
     if (xr)  // unused slots
-      for (int u = n + blk * blockDim.x + threadIdx.x; u < c.xcap; u += nmem * blockDim.x)
-        reinterpret_cast<int*>(xr + (int64_t)u * RW)[0] = -1;
+      for (int u = n + blk * blockDim.x + threadIdx.x; u < c.xcap; u += nmem * blockDim.x) xr[(int64_t)u * RW] = -1.f;
     return;
   }
   const int B = (int)c.ctl[TGNX_CTL_B];
@@ -1767,17 +1770,23 @@ struct TrainTail {
   }
 };
 
-// data parallel: the all-gathered memory rows of every rank -> memory / last_update (wave per row)
-__global__ void __launch_bounds__(256) tgn_apply_rows(float* mem, int64_t* lu, const float* rows, int64_t nrows, int D,
+// data parallel: the exchanged memory rows of every rank -> memory / last_update (wave per row); the
+// rows are zeroed after use (the next step's exchange sums every rank's slot into them)
+__global__ void __launch_bounds__(256) tgn_apply_rows(float* mem, int64_t* lu, float* rows, int64_t nrows, int D,
                                                       int64_t N) {
   const int lane = threadIdx.x & 63, RW = TGNX_TGN_ROW(D);
   for (int64_t u = blockIdx.x * 4 + (threadIdx.x >> 6); u < nrows; u += (int64_t)gridDim.x * 4) {
-    const float* row = rows + u * RW;
-    const int* h = reinterpret_cast<const int*>(row);
-    const int v = h[0];
-    if (v < 0 || v >= N) continue;
-    for (int k = lane; k < D; k += 64) mem[(int64_t)v * D + k] = row[4 + k];
-    if (lane == 0) lu[v] = (int64_t)(((uint64_t)(uint32_t)h[2] << 32) | (uint64_t)(uint32_t)h[1]);
+    float* row = rows + u * RW;
+    const float h0 = row[0], h1 = row[1], h2 = row[2], h3 = row[3];
+    const int64_t v = (int64_t)h0;
+    const bool ok = h0 >= 0.f && v < N;
+    for (int k = lane; k < D; k += 64) {
+      if (ok) mem[v * D + k] = row[4 + k];
+      row[4 + k] = 0.f;
+    }
+    if (lane < 4) row[lane] = 0.f;
+    if (ok && lane == 0)
+      lu[v] = (int64_t)((uint64_t)(uint32_t)h1 | ((uint64_t)(uint32_t)h2 << 24) | ((uint64_t)(uint32_t)h3 << 48));
   }
 }
 }  // namespace tgn
@@ -2053,6 +2062,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.xrows = b->xrows;
   c.xcap = b->xrows ? (int)std::min<int64_t>(b->xcap, 1 << 30) : 0;
   TGNX_CHECK_ARG(!b->xrows || b->xcap > 0, "tgn: xrows without xcap");
+  TGNX_CHECK_ARG(!b->xrows || cfg->num_nodes < (1ll << 24), "tgn: data-parallel row exchange needs num_nodes < 2^24");
   char* ws = reinterpret_cast<char*>(b->ws);
   c.cb = reinterpret_cast<uint32_t*>(ws + W.cb);
   c.nb = reinterpret_cast<uint32_t*>(ws + W.nb);
@@ -2364,7 +2374,7 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   return TGNX_OK;
 }
 
-int tgnx_tgn_apply_rows(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, const float* rows, int64_t nrows,
+int tgnx_tgn_apply_rows(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, float* rows, int64_t nrows,
                         void* stream) {
   int rc = check_cfg(cfg);
   if (rc) return rc;

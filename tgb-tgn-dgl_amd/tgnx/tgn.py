@@ -210,6 +210,19 @@ class TgnAdam(torch.optim.Optimizer):
         raise RuntimeError("TgnAdam.step runs inside the TGN train step (tgnx_tgn_train_update)")
 
 
+def row_header(v: int, lu: int) -> list:
+    """Header of an exchanged memory row (include/tgnx.h TGNX_TGN_ROW; written on the device by the
+    update step): node, last_update bits 0-23 / 24-47 / 48-63, each a float holding an exact integer."""
+    b = int(lu) & 0xFFFFFFFFFFFFFFFF
+    return [float(v), float(b & 0xFFFFFF), float((b >> 24) & 0xFFFFFF), float(b >> 48)]
+
+
+def row_decode(h) -> tuple:
+    """(node, last_update) of an exchanged row header (node -1: unused slot)."""
+    b = int(h[1]) | (int(h[2]) << 24) | (int(h[3]) << 48)
+    return int(h[0]), b - (1 << 64) if b >= 1 << 63 else b
+
+
 def _p(t):
     return 0 if t is None else t.data_ptr()
 
@@ -249,14 +262,21 @@ class TgnEngine:
             self.adam_m, self.adam_v = torch.zeros_like(model.flat), torch.zeros_like(model.flat)
         else:
             self.adam_m, self.adam_v = optimizer.exp_avg, optimizer.exp_avg_sq
-        # data parallel: each rank's GRU-updated memory rows [node | last_update | memory],
-        # all-gathered over RCCL after the step and written by every rank (tgnx_tgn_apply_rows)
-        self.xrows = self.xgather = None
+        # data parallel: each rank's GRU-updated memory rows [node | last_update | memory]
+        # travel with the gradients in ONE all-reduce over RCCL: the exchange buffer is [gradients |
+        # world x xcap rows]; a rank writes only its own row slot (exact small-integer floats, the
+        # other slots zero), so the sum of the row part is the all-gather.  tgnx_tgn_apply_rows writes
+        # them into memory / last_update on every rank and zeroes the slots for the next step.
+        self.xrows = self.xgather = self.comm = None
         if self.world > 1:
             self.xcap = min(cfg.num_nodes, 2 * (-(-cfg.max_batch // self.world)))
             rw = cfg.mem_dim + 4
-            self.xrows = torch.zeros(self.xcap, rw, dtype=torch.float32, device=self.dev)
-            self.xgather = torch.zeros(self.world * self.xcap, rw, dtype=torch.float32, device=self.dev)
+            G = model.grad_flat.numel()
+            self.comm = torch.zeros(G + self.world * self.xcap * rw, dtype=torch.float32, device=self.dev)
+            self.comm[:G].copy_(model.grad_flat)
+            model.grad_flat = self.comm[:G]          # the kernels' gradient buffer heads the exchange buffer
+            self.xgather = self.comm[G:].view(self.world * self.xcap, rw)
+            self.xrows = self.xgather[self.rank * self.xcap:(self.rank + 1) * self.xcap]
 
     def ensure_neg(self, kn: int) -> None:
         """Grow the workspace for eval batches with kn negatives per event (TGB: ~999 on tgbl-wiki)."""
@@ -331,10 +351,10 @@ class TgnEngine:
         _lib.call("tgnx_tgn_train_update", ctypes.byref(self.cfg), ctypes.byref(self._pending), self._stream())
 
     def _exchange(self):
-        """The step's collectives: gradient sum (all-reduce) and the touched memory rows (all-gather)."""
+        """The step's one collective: gradient sum and the touched memory rows of every rank (an
+        all-gather carried by the same all-reduce, see __init__)."""
         import torch.distributed as dist
-        dist.all_reduce(self.model.grad_flat)
-        dist.all_gather_into_tensor(self.xgather, self.xrows)
+        dist.all_reduce(self.comm)
 
     def _apply_rows(self, b):
         _lib.call("tgnx_tgn_apply_rows", ctypes.byref(self.cfg), ctypes.byref(b), _p(self.xgather),
