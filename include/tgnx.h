@@ -312,6 +312,11 @@ int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf
  * the memory rows this rank updated are packed into buf->xrows for the all-gather. */
 int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg,
                            int32_t dropout, void* stream);
+/* Train batch in one call at world 1: tgnx_tgn_train_fwd_bwd with Adam folded into the gradient writers
+ * (every gradient element's writer also updates its parameter / adam_m / adam_v), equal to fwd_bwd +
+ * tgnx_tgn_train_update (grads are still written).  Refused with xrows set (data parallel). */
+int tgnx_tgn_train_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
+                        void* stream);
 /* Data parallel: write the exchanged rows of every rank (rows [nrows, TGNX_TGN_ROW(mem_dim)], slots
  * with node -1 skipped) into memory / last_update, then zero `rows` (ready for the next summing
  * exchange).  Ranks that updated the same node computed the same row (same replicated inputs), so the

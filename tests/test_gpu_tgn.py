@@ -122,3 +122,40 @@ def test_tgn_train_steps_and_eval_match_oracle(aggr, layers):
     assert np.allclose(rr.cpu().numpy(), mrr_per_event(po, no), atol=1e-6)
     assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5)
     assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update)
+
+
+@pytest.mark.parametrize("layers", [1, 2])
+def test_tgn_fused_adam_step_equals_fwd_bwd_plus_update(layers):
+    """tgnx_tgn_train_step (Adam folded into the gradient writers) against tgnx_tgn_train_fwd_bwd +
+    tgnx_tgn_train_update on twin engines, device negatives and attention dropout on.  The gradient
+    atomics (dz rows, neighbour k/v sums) make the two runs' gradients differ in the last bits, so
+    the states are resynchronised after every step and compared per step: outputs 1e-5 abs;
+    parameters and Adam moments per tensor 1e-4 relative (the shift-invariant lin_key.bias, whose
+    gradient is pure rounding noise, excluded); memory 1e-5 abs; loss sums 1e-5 relative."""
+    engines = []
+    for fused in (True, False):
+        s, ref, opt_ref, lref, model, opt, eng = _setup("last", layers=layers)
+        model.cfg.dropout = 0.1
+        eng.fuse_adam = fused
+        engines.append((model, opt, eng))
+    (m1, o1, e1), (m2, o2, e2) = engines
+    B = 50
+    for st in range(6):
+        outs = [e.train_batch(st * B, B, neg=None, dropout=True, update=True) for e in (e1, e2)]
+        torch.cuda.synchronize()
+        e1.check()
+        e2.check()
+        assert torch.allclose(outs[0][0], outs[1][0], atol=1e-5) and torch.allclose(outs[0][1], outs[1][1], atol=1e-5)
+        for name in m1.param_order:
+            if name in SHIFT_INVARIANT:
+                continue
+            o, n, _ = m1._views[name]
+            for a, b in ((m1.flat, m2.flat), (o1.exp_avg, o2.exp_avg), (o1.exp_avg_sq, o2.exp_avg_sq)):
+                assert _rel(a[o:o + n], b[o:o + n]) < 1e-4, (st, name)
+        assert torch.allclose(m1.memory.memory, m2.memory.memory, atol=1e-5), st
+        assert abs(e1.loss_sum() - e2.loss_sum()) <= 1e-5 * abs(e2.loss_sum()), st
+        with torch.no_grad():   # resynchronise: the next step starts from identical states
+            m1.flat.copy_(m2.flat)
+            o1.exp_avg.copy_(o2.exp_avg)
+            o1.exp_avg_sq.copy_(o2.exp_avg_sq)
+            m1.memory.memory.copy_(m2.memory.memory)

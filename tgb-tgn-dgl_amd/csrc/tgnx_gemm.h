@@ -539,6 +539,13 @@ struct EpiStore {
   }
 };
 
+// epilogue of a deferred split-K job (its partials are summed and finished by gemm_fixup_kernel): never
+// called, and keeps the finishing epilogue's fields out of the GEMM kernel's arguments
+struct EpiDeferred {
+  template <class T>
+  __device__ void operator()(const T&) const {}
+};
+
 template <class CFG, class AL, class BL, class EPI>
 static inline void gemm_launch(const GemmShape& g, const AL& al, const BL& bl, const EPI& epi, float* part,
                                hipStream_t s) {

@@ -82,6 +82,59 @@ static Lay make_lay(int D, int d, int layers) {
   return L;
 }
 
+__device__ __forceinline__ void adam1(float g, float& m, float& v, float& p, float b1, float b2, float eps, float step,
+                                      float bc2s) {
+  m = m + (1.0f - b1) * (g - m);
+  v = v * b2 + (1.0f - b2) * g * g;
+  const float den = sqrtf(v) / bc2s + eps;
+  p -= step * (m / den);
+}
+
+// Adam folded into the gradient writers (tgnx_tgn_train_step, world 1): the writer of a gradient
+// element also applies the update to its parameter, so no separate optimizer pass re-reads the
+// 4 buffers.  p == nullptr: plain gradient store (tgnx_tgn_train_fwd_bwd; data parallel).  The step
+// scalars (lr / (1 - b1^t), sqrt(1 - b2^t)) are written to ctl[TGNX_CTL_ADAM_SC] by tgn_pred_train.
+constexpr int TGNX_CTL_ADAM_SC = 15;
+struct AdamFuse {
+  float *p = nullptr, *m = nullptr, *v = nullptr;
+  const int64_t* ctl = nullptr;
+  float b1 = 0.f, b2 = 0.f, eps = 0.f;
+  // n gradient elements (idx < 0: none) of one thread: every load issued before any store (the
+  // buffers may alias as far as the compiler knows, so interleaving would serialise the elements)
+  template <int N>
+  __device__ __forceinline__ void put_n(float* g, const int64_t (&idx)[N], const float (&val)[N]) const {
+    if (!p) {
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if (idx[i] >= 0) g[idx[i]] = val[i];
+      return;
+    }
+    float mm[N], vv[N], pp[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int64_t j = idx[i] >= 0 ? idx[i] : 0;
+      mm[i] = m[j];
+      vv[i] = v[j];
+      pp[i] = p[j];
+    }
+    const float* sc = reinterpret_cast<const float*>(ctl + TGNX_CTL_ADAM_SC);
+    const float s0 = sc[0], s1 = sc[1];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      if (idx[i] < 0) continue;
+      adam1(val[i], mm[i], vv[i], pp[i], b1, b2, eps, s0, s1);
+      g[idx[i]] = val[i];
+      m[idx[i]] = mm[i];
+      v[idx[i]] = vv[i];
+      p[idx[i]] = pp[i];
+    }
+  }
+  __device__ __forceinline__ void put(float* g, int64_t i, float val) const {
+    const int64_t ix[1] = {i};
+    const float vx[1] = {val};
+    put_n<1>(g, ix, vx);
+  }
+};
 struct Ctx {
   int64_t N, nev, words;
   int K, D, d, Qm, HC, C, aggr, Kn, drop, gen_neg;
@@ -120,6 +173,7 @@ struct Ctx {
   int64_t* xw;
   float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
   float *dZc, *dP, *dE, *dG, *tgp;
+  AdamFuse adf;  // fused optimizer (tgnx_tgn_train_step) or plain gradient stores
   float* dKV;  // per edge [dk | dv] of the attention backward [E][2 HC] (tgn_kv_reduce sums them into dP)
   float *encE, *sinE;  // per sampled edge: cos / sin of the Δt encoding argument [E][D]
   float *s0m, *s1m;    // per GRU row: (mean over its messages of) sin(arg), sin(arg) Δt  [M][D]
@@ -1036,7 +1090,15 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c) {
   __shared__ float dh[2][TDMAX];
   const int B = (int)c.ctl[TGNX_CTL_B];
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
-  if (blockIdx.x == 0 && threadIdx.x == 0) c.cnt[CNT_LIST] = 3 * (hi - lo);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    c.cnt[CNT_LIST] = 3 * (hi - lo);
+    if (c.adf.p) {  // fused Adam: this step's scalars for the gradient writers (tgn_adam computes them itself)
+      const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
+      float* sc = reinterpret_cast<float*>(c.ctl + TGNX_CTL_ADAM_SC);
+      sc[0] = (float)(c.lr / (1.0 - pow((double)c.b1, (double)t)));
+      sc[1] = (float)sqrt(1.0 - pow((double)c.b2, (double)t));
+    }
+  }
   const int i = lo + blockIdx.x;
   if (B == 0 || i >= hi || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1161,11 +1223,15 @@ __device__ void lp_vec_body(const Ctx& c, int y, int lane) {
   s = wave_sum(s);
   if (lane == 0) {
     float* g = c.grads;
-    if (y < D) g[c.L.lsb + y] = s;
-    else if (y < 2 * D) g[c.L.ldb + y - D] = s;
-    else if (y < 3 * D) g[c.L.lfw + y - 2 * D] = s;
-    else if (y == 3 * D) g[c.L.lfb] = s;
-    else g[c.L.total] = s;  // batch loss slot
+    if (y < D) c.adf.put(g, c.L.lsb + y, s);
+    else if (y < 2 * D) c.adf.put(g, c.L.ldb + y - D, s);
+    else if (y < 3 * D) c.adf.put(g, c.L.lfw + y - 2 * D, s);
+    else if (y == 3 * D) c.adf.put(g, c.L.lfb, s);
+    else {
+      g[c.L.total] = s;  // batch loss slot
+      if (c.adf.p && ok)  // fused step: the running loss sum tgn_adam keeps otherwise
+        *reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS) += (double)s * (double)c.ctl[TGNX_CTL_B];
+    }
   }
 }
 
@@ -1355,16 +1421,42 @@ struct EpiProjGrad {
   float* g;
   int64_t wq, bq, pw, pb;  // projection gi: weights wq + gi pw, bias bq + gi pb
   int HC, D;
+  AdamFuse af;
   template <class T>
   __device__ void operator()(const T& t) const {
-    for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
-      const int r = x / t.tn, cc = x % t.tn, row = t.m0 + r, n = t.n0 + cc;
-      if (row >= t.M || n >= t.N) continue;
+    constexpr int NI = (T::tm * T::tn + 255) / 256;
+    int64_t ix[NI];
+    float vx[NI];
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int x = threadIdx.x + 256 * it;
+      const int r = x / T::tn, cc = x % T::tn, row = t.m0 + r, n = t.n0 + cc;
+      const bool ok = x < T::tm * T::tn && row < t.M && n < t.N;
       const int gi = row / HC, q = row % HC;
-      const float v = t(r, cc);
-      if (n < D) g[wq + gi * pw + (int64_t)q * D + n] = v;
-      else g[bq + gi * pb + q] = v;
+      vx[it] = ok ? t(r, cc) : 0.f;
+      ix[it] = !ok ? -1 : n < D ? wq + gi * pw + (int64_t)q * D + n : bq + gi * pb + q;
     }
+    af.put_n(g, ix, vx);
+  }
+};
+// plain row-major weight gradient (lin_edge): g[off + m ldc + n]
+struct EpiGradStore {
+  float* g;
+  int64_t off;
+  int ldc;
+  AdamFuse af;
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    int64_t ix[T::per];
+    float vx[T::per];
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) {
+      const int r = T::row_of(i), cc = T::col_of(i), m = t.m0 + r, n = t.n0 + cc;
+      const bool ok = m < t.M && n < t.N;
+      vx[i] = ok ? t(r, cc) : 0.f;
+      ix[i] = ok ? off + (int64_t)m * ldc + n : -1;
+    }
+    af.put_n(g, ix, vx);
   }
 };
 // link predictor weight grads as one GEMM over 3 * nloc rows (block-diagonal K):
@@ -1399,13 +1491,21 @@ struct EpiLpGrad {
   float* g;
   int64_t lsw, ldw;
   int D;
+  AdamFuse af;
   template <class T>
   __device__ void operator()(const T& t) const {
-    for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
-      const int r = x / t.tn, cc = x % t.tn, row = t.m0 + r, n = t.n0 + cc;
-      if (row >= t.M || n >= t.N) continue;
-      g[(row < D ? lsw + (int64_t)row * D : ldw + (int64_t)(row - D) * D) + n] = t(r, cc);
+    constexpr int NI = (T::tm * T::tn + 255) / 256;
+    int64_t ix[NI];
+    float vx[NI];
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int x = threadIdx.x + 256 * it;
+      const int r = x / T::tn, cc = x % T::tn, row = t.m0 + r, n = t.n0 + cc;
+      const bool ok = x < T::tm * T::tn && row < t.M && n < t.N;
+      vx[it] = ok ? t(r, cc) : 0.f;
+      ix[it] = ok ? (row < D ? lsw + (int64_t)row * D : ldw + (int64_t)(row - D) * D) + n : -1;
     }
+    af.put_n(g, ix, vx);
   }
 };
 // Δt-encoding parameter grads from a tile of d(encoding) (dA): per row-tile partials
@@ -1560,28 +1660,37 @@ struct EpiGruWGrad {
   float* g;
   int64_t wih, whh, bih, bhh;
   int Qm, D;
+  AdamFuse af;
   template <class T>
   __device__ void operator()(const T& t) const {
-    for (int x = threadIdx.x; x < t.tm * t.tn; x += blockDim.x) {
-      const int r = x / t.tn, cc = x % t.tn, row = t.m0 + r, n = t.n0 + cc;
-      if (row >= t.M || n >= t.N) continue;
+    constexpr int NI = (T::tm * T::tn + 255) / 256;
+    int64_t ix[2 * NI];  // the (r, z) bias columns feed both b_ih and b_hh
+    float vx[2 * NI];
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int x = threadIdx.x + 256 * it;
+      const int r = x / T::tn, cc = x % T::tn, row = t.m0 + r, n = t.n0 + cc;
+      const bool ok = x < T::tm * T::tn && row < t.M && n < t.N;
       const int j = row >> 2, gg = row & 3;
-      const float v = t(r, cc);
-      if (n < Qm) {
-        if (gg < 3) g[wih + (int64_t)(gg * D + j) * Qm + n] = v;
-      } else if (n < Qm + D) {
-        if (gg != 2) g[whh + (int64_t)((gg == 3 ? 2 : gg) * D + j) * D + (n - Qm)] = v;
-      } else {
-        if (gg < 2) {
-          g[bih + gg * D + j] = v;
-          g[bhh + gg * D + j] = v;
-        } else if (gg == 2) {
-          g[bih + 2 * D + j] = v;
+      const float v = ok ? t(r, cc) : 0.f;
+      int64_t a = -1, b = -1;
+      if (ok) {
+        if (n < Qm) {
+          if (gg < 3) a = wih + (int64_t)(gg * D + j) * Qm + n;
+        } else if (n < Qm + D) {
+          if (gg != 2) a = whh + (int64_t)((gg == 3 ? 2 : gg) * D + j) * D + (n - Qm);
+        } else if (gg < 2) {
+          a = bih + gg * D + j;
+          b = bhh + gg * D + j;
         } else {
-          g[bhh + 2 * D + j] = v;
+          a = gg == 2 ? bih + 2 * D + j : bhh + 2 * D + j;
         }
       }
+      ix[2 * it] = a;
+      ix[2 * it + 1] = b;
+      vx[2 * it] = vx[2 * it + 1] = v;
     }
+    af.put_n(g, ix, vx);
   }
 };
 // encoding columns of W_ih as the B operand of dX_enc = dG W_cat[:, enc]: element (n, r = 4j+g)
@@ -1640,19 +1749,12 @@ struct TeReduceTail {
     __syncthreads();
     if (wv == 0 && x < 2 * D) {
       const float tot = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-      c.grads[(x < D ? c.L.te_w : c.L.te_b - D) + x] = tot;
+      c.adf.put(c.grads, (x < D ? c.L.te_w : c.L.te_b - D) + x, tot);
     }
   }
 };
 
 // ------------------------------------------------------------------ optimizer + state update
-__device__ __forceinline__ void adam1(float g, float& m, float& v, float& p, float b1, float b2, float eps, float step,
-                                      float bc2s) {
-  m = m + (1.0f - b1) * (g - m);
-  v = v * b2 + (1.0f - b2) * g * g;
-  const float den = sqrtf(v) / bc2s + eps;
-  p -= step * (m / den);
-}
 __global__ void __launch_bounds__(256) tgn_adam(Ctx c) {
   __shared__ float sc[2];
   const int64_t B = c.ctl[TGNX_CTL_B];
@@ -2234,14 +2336,25 @@ int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf
   return TGNX_OK;
 }
 
-int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
-                           void* stream) {
+static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
+                           void* stream, bool fuse_adam) {
   Ctx c;
   Caps k;
   WsLay W;
   int rc = make_ctx(cfg, buf, 1, c, k, W);
   if (rc) return rc;
   TGNX_CHECK_ARG(buf->neg && buf->grads && buf->out_pos && buf->out_neg, "tgnx_tgn_train_fwd_bwd: null buffer");
+  if (fuse_adam) {
+    TGNX_CHECK_ARG(buf->adam_m && buf->adam_v, "tgnx_tgn_train_step: null optimizer buffer");
+    TGNX_CHECK_ARG(!buf->xrows, "tgnx_tgn_train_step: data parallel steps all-reduce before Adam (fwd_bwd + update)");
+    c.adf.p = c.params;
+    c.adf.m = c.am;
+    c.adf.v = c.av;
+    c.adf.ctl = c.ctl;
+    c.adf.b1 = c.b1;
+    c.adf.b2 = c.b2;
+    c.adf.eps = c.eps;
+  }
   TGNX_CHECK_ARG(!gen_neg || (buf->dst_nodes && buf->n_dst > 0), "tgnx_tgn_train_fwd_bwd: no destination set");
   c.gen_neg = gen_neg ? 1 : 0;
   c.drop = dropout && cfg->dropout > 0.f;
@@ -2312,9 +2425,9 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
                  gemm_job<G32L>(gemm_shape<G32L>(k.Rtr, HC, 4 * HC, c.cnt + CNT_R), LoadRowK{c.dP2, k.Rtr, 4 * HC, 4 * HC},
                                 LoadProjWT{P + c.L.wq2, c.L.pw, HC, HC}, EpiStore{c.dZc, nullptr, HC, 0}, (float*)nullptr),
                  gemm_job<G32>(shp_dWp2(k, c.cnt), LoadKRow{c.dP2, 4 * HC, k.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
-                               EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC}, c.pE),
+                               EpiDeferred{}, c.pE),
                  gemm_job<G32>(shp_dWe2(k, c.cnt), LoadKRow{c.dE2, HC, k.E1tr, HC}, LoadEdgeAttrMapT{ea1},
-                               EpiStore{G + c.L.we2, nullptr, D + d, 0}, c.pF),
+                               EpiDeferred{}, c.pF),
                  gemm_job<G32>(gemm_shape<G32>(k.E1tr, D, HC, c.cnt + CNT_E1), LoadRowK{c.dE2, k.E1tr, HC, HC},
                                LoadKRow{P + c.L.we2, D, HC, D + d},
                                EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, c.e1_e2, c.tgp_e1}, (float*)nullptr));
@@ -2329,18 +2442,18 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_kv_reduce");
   // weight gradients (deferred split-K) ‖ ...
-  const EpiStore e_dWe{G + c.L.we, nullptr, D + d, 0};
-  const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D};
-  const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D};
-  const EpiGruWGrad e_dWg{G, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, Qm, D};
+  const EpiGradStore e_dWe{G, c.L.we, D + d, c.adf};
+  const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D, c.adf};
+  const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D, c.adf};
+  const EpiGruWGrad e_dWg{G, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, Qm, D, c.adf};
   // one launch: dW_edge, dW_proj, dW_src/dst (deferred split-K) ‖ dEnc·W_e (Δt partials) ‖ dz0 = dP W
   // with the GRU backward in its epilogue — all read only what attn_bwd / pred_train produced
   const int rows_edge = (k.Etr + G32::TM - 1) / G32::TM, rows_msg = (k.Mtr + G32::TM - 1) / G32::TM;
   probe_begin(TGNX_K_EDGE_BWD, s);
-  gemmN_launch(s, gemm_job<G32>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, e_dWe, c.pA),
-               gemm_job<G32>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, e_dWp, c.pB),
+  gemmN_launch(s, gemm_job<G32>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, EpiDeferred{}, c.pA),
+               gemm_job<G32>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB),
                gemm_job<G32>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
-                             LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, e_dWlp, c.pC),
+                             LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, EpiDeferred{}, c.pC),
                gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
                              LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
                              (float*)nullptr),
@@ -2349,7 +2462,7 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
                              (float*)nullptr));
   probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
-  gemm2_launch<G32, G32L>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, e_dWg,
+  gemm2_launch<G32, G32L>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{},
                c.pD, gemm_shape<G32L>(k.Mtr, D, 4 * D, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
                LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
@@ -2363,8 +2476,8 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     gemm_fixup_launch(nte + nmem + nst + nring, tail, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
                       gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
                       gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg),
-                      gemm_fix<G32>(shp_dWp2(k, c.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC}),
-                      gemm_fix<G32>(shp_dWe2(k, c.cnt), c.pF, EpiStore{G + c.L.we2, nullptr, D + d, 0}));
+                      gemm_fix<G32>(shp_dWp2(k, c.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC, c.adf}),
+                      gemm_fix<G32>(shp_dWe2(k, c.cnt), c.pF, EpiGradStore{G, c.L.we2, D + d, c.adf}));
   else
     gemm_fixup_launch(nte + nmem + nst + nring, tail, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
                       gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
@@ -2372,6 +2485,16 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgn_fixup_update");
   return TGNX_OK;
+}
+
+int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
+                           void* stream) {
+  return train_step_impl(cfg, buf, gen_neg, dropout, stream, false);
+}
+
+int tgnx_tgn_train_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
+                        void* stream) {
+  return train_step_impl(cfg, buf, gen_neg, dropout, stream, true);
 }
 
 int tgnx_tgn_apply_rows(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, float* rows, int64_t nrows,

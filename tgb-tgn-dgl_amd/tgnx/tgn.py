@@ -258,6 +258,7 @@ class TgnEngine:
         self.mrr = torch.zeros(cfg.max_batch, dtype=torch.float64, device=self.dev)
         self.dst_nodes = None if dst_nodes is None else torch.as_tensor(dst_nodes).to(self.dev, torch.long).contiguous()
         self.seed, self.rank, self.world = int(seed), int(rank), int(world)
+        self.fuse_adam = True
         if optimizer is None:
             self.adam_m, self.adam_v = torch.zeros_like(model.flat), torch.zeros_like(model.flat)
         else:
@@ -336,12 +337,18 @@ class TgnEngine:
             self.neg_train[start:start + B].copy_(torch.as_tensor(neg).to(self.dev, torch.long))
         self.advance(start, B, True)
         b = self._buffers(_p(self.neg_train))
-        _lib.call("tgnx_tgn_train_fwd_bwd", ctypes.byref(self.cfg), ctypes.byref(b), 0 if neg is not None else 1,
-                  1 if dropout else 0, self._stream())
+        fused = update and self._fused()
+        _lib.call("tgnx_tgn_train_step" if fused else "tgnx_tgn_train_fwd_bwd", ctypes.byref(self.cfg), ctypes.byref(b),
+                  0 if neg is not None else 1, 1 if dropout else 0, self._stream())
         self._pending = b
-        if update:
+        if update and not fused:
             self.apply_update()
         return self.out_pos[:B], self.out_neg[:B]
+
+    def _fused(self) -> bool:
+        """Adam folded into the step's gradient writers (tgnx_tgn_train_step): world 1 only, since data
+        parallel steps all-reduce the gradients before the update."""
+        return self.fuse_adam and self.world == 1
 
     def apply_update(self, allreduce: bool = True):
         if allreduce and self.world > 1:
@@ -380,7 +387,9 @@ class TgnEngine:
         self._res_drop = 1 if dropout else 0
         self._res_buf = self._buffers(_p(self.neg_train))
         L = _lib.lib()
-        self._f = (L.tgnx_tgnn_advance, L.tgnx_tgn_train_fwd_bwd, L.tgnx_tgn_train_update, L.tgnx_tgn_apply_rows)
+        self._res_fused = self._fused()
+        self._f = (L.tgnx_tgnn_advance, L.tgnx_tgn_train_step if self._res_fused else L.tgnx_tgn_train_fwd_bwd,
+                   L.tgnx_tgn_train_update, L.tgnx_tgn_apply_rows)
         self._cfg_ref, self._buf_ref = ctypes.byref(self.cfg), ctypes.byref(self._res_buf)
         self._ctl_p = ctypes.c_void_p(self.ctl.data_ptr())
 
@@ -404,7 +413,8 @@ class TgnEngine:
         if self.world > 1:
             rc |= self._f[3](self._cfg_ref, self._buf_ref, ctypes.c_void_p(self.xgather.data_ptr()),
                              ctypes.c_int64(self.xgather.shape[0]), st)
-        rc |= self._f[2](self._cfg_ref, self._buf_ref, st)
+        if not self._res_fused:   # fused step: Adam already applied
+            rc |= self._f[2](self._cfg_ref, self._buf_ref, st)
         if rc:
             raise RuntimeError(f"tgnx TGN resident update failed: {_lib.lib().tgnx_last_error().decode()}")
 
