@@ -3,8 +3,9 @@
 `getDataWithDependecyBlock(name, train_param)` returns the same 7-tuple as the
 reference (utils.py:25,67): (data, train_dl, val_dl, test_dl, neg_sampler,
 evaluator, metric).  TGB datasets cannot be downloaded here, so `name` is either
-  * a TGB dataset name (tgbl-wiki / -review / -coin / -comment): a synthetic stream
-    with that dataset's published shape (tgnx.synth; TGNX_SYNTH_EVENTS scales it down), or
+  * a TGB dataset name (tgbl-wiki / -review / -coin / -comment): the dataset on disk under
+    $TGNX_TGB_ROOT (default "datasets", as utils.py:29) in py-tgb's raw layout (tgnx.tgb_io), else a
+    synthetic stream with that dataset's published shape (tgnx.synth; TGNX_SYNTH_EVENTS scales it down), or
   * a path to an .npz holding src, dst, t, msg (+ optional val_neg / test_neg).
 Loaders iterate host batches exactly like the reference's DataLoader (dicts of
 src/dst/t/msg/b/idx, t cast to float32 — temporal_dataset.py:34-57) and also carry
@@ -26,6 +27,7 @@ import yaml
 
 from . import _lib
 from .synth import SHAPES, eval_negatives, make_stream
+from .tgb_io import load_tgb, uniform_negatives
 
 
 def parse_config(f):
@@ -177,6 +179,17 @@ def _load(name: str):
         return src, dst, t, msg, tr, va, negs, None
     if name not in SHAPES:
         raise ValueError(f"unknown dataset {name!r}: give a TGB name {sorted(SHAPES)} or an .npz path")
+    # a TGB dataset on disk (utils.py:29 reads datasets/<name>): raw edge list or the tgnx cache
+    disk = load_tgb(name, root=os.environ.get("TGNX_TGB_ROOT", "datasets"),
+                    allow_pickle=os.environ.get("TGNX_TGB_ALLOW_PICKLE") == "1")
+    if disk is not None:
+        src, dst, t, msg, tr, va, negs = disk
+        kneg = int(os.environ.get("TGNX_EVAL_NEGS", str(SHAPES[name].num_neg_eval)))
+        if "val_neg" not in negs:
+            negs["val_neg"] = uniform_negatives(dst, tr, va, kneg, seed=1)
+        if "test_neg" not in negs:
+            negs["test_neg"] = uniform_negatives(dst, va, len(t), kneg, seed=2)
+        return src, dst, t, msg, tr, va, negs, None
     ev = os.environ.get("TGNX_SYNTH_EVENTS")
     s = make_stream(SHAPES[name], seed=int(os.environ.get("TGNX_SYNTH_SEED", "0")),
                     num_events=int(ev) if ev else None)

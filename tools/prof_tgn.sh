@@ -10,7 +10,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpu
 python3 - $R/gpurun_out/${tag}_prof <<'PY'
 import csv, glob, sys
 rows = list(csv.DictReader(open(glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0])))
-steps = max(int(r["Calls"]) for r in rows if "tgn_adam" in r["Name"])
+steps = max(int(r["Calls"]) for r in rows if "tgn_pred_train" in r["Name"])
 tot = 0
 for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
     c = int(r["Calls"]); a = float(r["AverageNs"]) / 1e3
