@@ -46,7 +46,10 @@ using G32 = GemmCfg<32, 32, TGNX_G32_KC, TGNX_G32_PF>;  // the TGN step's GEMMs
 #ifndef TGNX_G32L_KC
 #define TGNX_G32L_KC 64
 #endif
-using G32L = GemmCfg<32, 32, TGNX_G32L_KC, 1>;  // long-K direct GEMMs (GRU, dz0, dX_enc): fewer chunks
+#ifndef TGNX_G32L_PF
+#define TGNX_G32L_PF 1
+#endif
+using G32L = GemmCfg<32, 32, TGNX_G32L_KC, TGNX_G32L_PF>;  // long-K direct GEMMs (GRU, dz0, dX_enc): fewer chunks
 using G64 = GemmCfg<64, 64, 64>;   // large-M GEMMs (eval scoring)
 
 struct GemmShape {

@@ -221,19 +221,27 @@ __device__ __forceinline__ void mark_node(uint32_t* bm, uint32_t* sum, int64_t v
 // train negatives are drawn here (NegLinkSamplerDest, counter-based stream as in tgnx_tgnn);
 // src / pos nodes are stamped for the update list (memory_module.py:129).  16 lanes per entry, one
 // ring slot each (all slot loads in flight at once); the entry's valid-slot count goes to kval[v].
+__device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh);
 template <bool TRAIN>
-__global__ void tgn_mark(Ctx c) {
+__global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  if ((int)blockIdx.x >= nmark) {  // train: ring-insert / message-store plans (1024 threads)
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int sh[40];
+    plan_blocks(c, (int)blockIdx.x - nmark, B, start, smem, sh);
+    return;
+  }
+  if (threadIdx.x >= 256) return;  // marking runs 256-thread groups
   const int gen = (int)c.ctl[TGNX_CTL_GEN];
   const int Kn = TRAIN ? 1 : c.Kn;
   // train: this rank's event slice [lo, lo + nl) (data parallel; the whole batch at world 1)
   const int lo = TRAIN ? (int)c.ctl[TGNX_CTL_LO] : 0, nl = TRAIN ? (int)(c.ctl[TGNX_CTL_HI] - c.ctl[TGNX_CTL_LO]) : B;
   const int nq = nl * (2 + Kn);
   const int sl = threadIdx.x & 15, grp = (threadIdx.x & 63) >> 4;
-  const int gstride = (gridDim.x * blockDim.x) >> 4;
-  for (int q = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; q < nq; q += gstride) {
+  const int gstride = (nmark * 256) >> 4;
+  for (int q = (blockIdx.x * 256 + threadIdx.x) >> 4; q < nq; q += gstride) {
     int64_t v;
     if (q < nl) {
       v = c.ev_src[start + lo + q];
@@ -372,15 +380,12 @@ __host__ __device__ inline size_t tgn_scan_smem(int Bmax) {
   const int n = next_pow2(2 * Bmax);
   return (size_t)n * 16 + (size_t)(2 * Bmax + 4) * 4 + 64;
 }
-template <bool TRAIN>
-__global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ int sh[40];
-  const int B = (int)c.ctl[TGNX_CTL_B];
-  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+
+// the batch's ring-insert plan (which = 0) and message-store plan (which = 1); they read only the batch's
+// events, so the train step runs them as two extra 1024-thread workgroups of tgn_mark
+__device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh) {
   const int tid = threadIdx.x, T = blockDim.x;
-  if (blockIdx.x == 1) {
+  if (which == 0) {
     uint64_t* key;
     int* runs;
     const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs);
@@ -390,10 +395,20 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
       c.rruns[U] = 2 * B;
       c.cnt[CNT_RUNS] = U;
     }
-    return;
-  }
-  if (blockIdx.x == 2) {
+  } else {
     store_plan_block(c, B, start, smem, sh);
+  }
+}
+template <bool TRAIN>
+__global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int sh[40];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  const int tid = threadIdx.x, T = blockDim.x;
+  if (blockIdx.x >= 1) {  // eval: the plans ride here (train: in tgn_mark)
+    plan_blocks(c, (int)blockIdx.x - 1, B, start, smem, sh);
     return;
   }
   const int gen = (int)c.ctl[TGNX_CTL_GEN];
@@ -1356,10 +1371,11 @@ __global__ void __launch_bounds__(256) tgn_kv_reduce(Ctx c) {
   const int t = threadIdx.x;
   if (t < KVR_CH) sj[t] = t < ne ? c.e_j[eb + t] : INT_MAX;
   __syncthreads();
-  if (t < ne) {  // stable rank of (neighbour, edge)
+  if (t < ne) {  // stable rank of (neighbour, edge); padding keys (INT_MAX, past ne) rank after every edge
     const int key = sj[t];
     int r = 0;
-    for (int u = 0; u < ne; ++u) {
+#pragma unroll 16
+    for (int u = 0; u < KVR_CH; ++u) {
       const int ju = sj[u];
       r += (ju < key) || (ju == key && u < t);
     }
@@ -2362,10 +2378,13 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   const float* P = c.params;
   float* G = c.grads;
   const int D = c.D, HC = c.HC, Qm = c.Qm, d = c.d;
-  tgn_mark<true><<<gridn(3 * k.B * 16, 256), 256, 0, s>>>(c);
+  {
+    const int nmark = gridn(3 * k.B * 16, 256);
+    tgn_mark<true><<<nmark + 2, 1024, tgn_scan_smem(k.B), s>>>(c, nmark);
+  }
   TGNX_LAUNCH_CHECK("tgn_mark");
   probe_begin(TGNX_K_ASSEMBLE, s);
-  tgn_scan<true><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
+  tgn_scan<true><<<1, 1024, 0, s>>>(c);  // plans: in tgn_mark
   probe_end(TGNX_K_ASSEMBLE, s);
   TGNX_LAUNCH_CHECK("tgn_scan");
   const int nedge = gridn((int64_t)k.Rtr * c.K, 4, 4096);
@@ -2540,7 +2559,10 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   const int Rq = two ? (int)std::min<int64_t>(c.N, (int64_t)R1q * (c.K + 1)) : R1q;  // (outer) centres
   const int Mq = (int)std::min<int64_t>(c.N, (int64_t)Rq * (c.K + 1));
   const int Eq = Rq * c.K, E1q = two ? R1q * c.K : 0;
-  tgn_mark<false><<<gridn((int64_t)k.B * (2 + Kn) * 16, 256), 256, 0, s>>>(c);
+  {
+    const int nmark = gridn((int64_t)k.B * (2 + Kn) * 16, 256);
+    tgn_mark<false><<<nmark, 256, 0, s>>>(c, nmark);
+  }
   TGNX_LAUNCH_CHECK("tgn_mark");
   tgn_scan<false><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_scan");
