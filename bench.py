@@ -325,6 +325,8 @@ def run_tgn(args, world, rank, dev):
     probes = {}
     spec = (("tgn_gru_edge", 1), ("tgn_attn_fwd", 6), ("tgn_attn_bwd", 8), ("tgn_wgrad_dz0", 2),
             ("tgn_agg_emit", 9), ("tgn_scan", 3), ("tgn_pred_train", 4), ("tgn_fixup_update", 5), ("tgn_adam", 7))
+    if getattr(eng, "_res_fused", False):   # world 1: Adam rides in the gradient writers (no tgn_adam launch)
+        spec = tuple(x for x in spec if x[0] != "tgn_adam")
     for name, kid in spec:
         _lib.call("tgnx_probe_enable", kid)
         pe0, pm0 = eng.units()

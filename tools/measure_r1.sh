@@ -12,4 +12,6 @@ cd $R
 timeout -k 10 400 python bench.py --model tgn --only --dataset tgbl-review --aggr mean --steps 300 --warmup 30 \
   --no-cpu-baseline --probe-steps 20 > gpurun_out/m_review.json 2> gpurun_out/m_review.err || exit $?
 timeout -k 10 500 python bench.py --model tgn --only --dataset tgbl-coin --steps 300 --warmup 30 --no-cpu-baseline \
-  --probe-steps 20 > gpurun_out/m_coin.json 2> gpurun_out/m_coin.err
+  --probe-steps 20 > gpurun_out/m_coin.json 2> gpurun_out/m_coin.err || exit $?
+timeout -k 10 400 python bench.py --model tgn --only --dataset tgbl-comment --batch 600 --layers 2 --steps 100 --warmup 20 \
+  --no-cpu-baseline --probe-steps 20 > gpurun_out/m_comment2.json 2> gpurun_out/m_comment2.err

@@ -13,7 +13,7 @@ KERNELS = {
     "tgn_gru_edge": ("gemmN_kernel", "LoadGruA,"),
     "tgn_wgrad_dz0": ("gemmN_kernel", "LoadEdgeAttrT"),
     "tgn_attn_fwd": ("tgn_attn_fwd<true>",),
-    "tgn_attn_bwd": ("tgn_attn_bwd",),
+    "tgn_attn_bwd": [("tgn_attn_bwd",), ("tgn_kv_reduce",)],   # the probe brackets both launches
     "tgn_agg_emit": ("tgn_agg_emit",),
     "tgn_scan": ("tgn_scan<true>",),
     "tgn_mark": ("tgn_mark<true>",),
@@ -51,18 +51,24 @@ def main(d):
         if not f or not w:
             continue
         fe, wr = load(f[0]), load(w[0])
-        for probe, keys in KERNELS.items():
+        for probe, sel in KERNELS.items():
             if not probe.startswith(model + "_"):
                 continue
-            fn = [n for n in fe if match(n, keys)]
-            wn = [n for n in wr if match(n, keys)]
-            if not fn or not wn:
-                continue
-            fv = [v for n in fn for v in fe[n]]
-            wv = [v for n in wn for v in wr[n]]
-            fkb, wkb = sum(fv) / len(fv), sum(wv) / len(wv)
-            res[probe] = {"fetch_kb": round(fkb, 2), "write_kb": round(wkb, 2), "launches": len(fv),
-                          "bytes_per_launch": int((2 * fkb + wkb) * 1024)}
+            fkb = wkb = 0.0
+            launches = None
+            for keys in (sel if isinstance(sel, list) else [sel]):   # several kernels: per-launch sums
+                fn = [n for n in fe if match(n, keys)]
+                wn = [n for n in wr if match(n, keys)]
+                if not fn or not wn:
+                    break
+                fv = [v for n in fn for v in fe[n]]
+                wv = [v for n in wn for v in wr[n]]
+                fkb += sum(fv) / len(fv)
+                wkb += sum(wv) / len(wv)
+                launches = len(fv) if launches is None else min(launches, len(fv))
+            else:
+                res[probe] = {"fetch_kb": round(fkb, 2), "write_kb": round(wkb, 2), "launches": launches,
+                              "bytes_per_launch": int((2 * fkb + wkb) * 1024)}
     print(json.dumps(res, indent=1))
 
 
