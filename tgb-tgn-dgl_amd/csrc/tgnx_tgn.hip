@@ -665,42 +665,55 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
       c.lu[m] = tm;
     }
   } else {
-    // mean over the stored events in event order (PyG scatter-sum order, then / count)
+    // mean over the stored events in event order (PyG scatter-sum order, then / count).  Messages are
+    // taken AGG_MB at a time with all their row loads in flight (a hub node stores ~100 messages of its
+    // last batch: one load round per message made agg_emit 83 us on the review-shaped stream)
+    constexpr int AGG_MB = 4;
     const float inv = 1.0f / (float)tot;
     float tmax = -INFINITY;
     for (int k0 = 0; k0 < Qm; k0 += 64 * 8) {
-      float s[8], s0[8], s1[8];
+      float s[8], s0[8], s1[8], tw[8], tb[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) s[i] = s0[i] = s1[i] = 0.f;
+      for (int i = 0; i < 8; ++i) {
+        s[i] = s0[i] = s1[i] = 0.f;
+        const int qq = min(max(k0 + lane + 64 * i - enc0, 0), D - 1);  // encoding weights of this column
+        tw[i] = P[c.L.te_w + qq];
+        tb[i] = P[c.L.te_b + qq];
+      }
       for (int q0 = 0; q0 < tot; q0 += 64) {
         int64_t e_l, o_l;
         float t_l;
         store_event(c, sv, q0 + lane, e_l, o_l, t_l);
         if (k0 == 0 && q0 + lane < tot) tmax = fmaxf(tmax, t_l);
         const int nq = min(64, tot - q0);
-        for (int q = 0; q < nq; ++q) {
-          const int64_t e = shfl_i64(e_l, q), o = shfl_i64(o_l, q);
-          const float dt = __shfl(t_l, q, 64) - lun;
-          float v[8];
+        for (int qb = 0; qb < nq; qb += AGG_MB) {
+          float v[AGG_MB][8], dt[AGG_MB];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int k = min(k0 + lane + 64 * i, Qm - 1);
-            const float* p = k < D ? rowN + k : k < 2 * D ? c.mem + o * D + (k - D)
-                                                  : k < enc0 ? c.ev_msg + e * d + (k - 2 * D) : rowN;
-            v[i] = *p;
+          for (int u = 0; u < AGG_MB; ++u) {
+            const int q = min(qb + u, nq - 1);
+            const int64_t e = shfl_i64(e_l, q), o = shfl_i64(o_l, q);
+            dt[u] = __shfl(t_l, q, 64) - lun;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const int k = min(k0 + lane + 64 * i, Qm - 1);
+              const float* p = k < D ? rowN + k : k < 2 * D ? c.mem + o * D + (k - D)
+                                                    : k < enc0 ? c.ev_msg + e * d + (k - 2 * D) : rowN;
+              v[u][i] = *p;
+            }
           }
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int k = k0 + lane + 64 * i;
-            const bool enc = k >= enc0 && k < Qm;
-            float cs = 0.f, sn = 0.f;
-            if (enc) {
-              const int qq = k - enc0;
-              te_sincos(fmaf(P[c.L.te_w + qq], dt, P[c.L.te_b + qq]), sn, cs);
+          for (int u = 0; u < AGG_MB; ++u) {
+            if (qb + u >= nq) break;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const int k = k0 + lane + 64 * i;
+              const bool enc = k >= enc0 && k < Qm;
+              float cs = 0.f, sn = 0.f;
+              if (enc) te_sincos(fmaf(tw[i], dt[u], tb[i]), sn, cs);
+              s[i] += v[u][i] * f01(!enc) + cs;
+              s0[i] += sn;
+              s1[i] += sn * dt[u];
             }
-            s[i] += v[i] * f01(!enc) + cs;
-            s0[i] += sn;
-            s1[i] += sn * dt;
           }
         }
       }
@@ -721,6 +734,118 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
       c.trel[m] = 0.f;
       c.lu[m] = tmax;
     }
+  }
+}
+
+// MeanAggregator for one node by a whole workgroup (train step): the node's stored messages are split
+// into 4 contiguous ranges, one per wave, and the partial sums combine in LDS in wave order.  A hub node
+// of the review-shaped stream stores ~100-200 messages of its last batch; one wave evaluating D
+// time-encoding sin/cos pairs per message ran 84 us (agg_emit), all other waves done long before.
+__device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m) {
+  __shared__ float red[4][3][8][64];
+  __shared__ float rmax[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int D = c.D, d = c.d, Qm = c.Qm, enc0 = 2 * D + d;
+  const StoreView sv = store_view(c, n);
+  const int tot = (int)sv.tot;
+  float* X = c.X + (int64_t)m * Qm;
+  if (tot == 0) {  // workgroup-uniform
+    if (w == 0) {
+      for (int k = lane; k < Qm; k += 64) X[k] = 0.f;
+      for (int q = lane; q < D; q += 64) c.s0m[(int64_t)m * D + q] = c.s1m[(int64_t)m * D + q] = 0.f;
+      if (lane == 0) {
+        c.xw[m] = -1;
+        c.trel[m] = 0.f;
+        c.lu[m] = 0.f;
+      }
+    }
+    return;
+  }
+  const float lun = (float)c.lu_buf[n];
+  const float* rowN = c.mem + n * D;
+  const float* P = c.params;
+  const int qa = w * tot / 4, qe = (w + 1) * tot / 4;  // this wave's messages (event order)
+  constexpr int AGG_MB = 4;
+  const float inv = 1.0f / (float)tot;
+  float tmax = -INFINITY;
+  for (int k0 = 0; k0 < Qm; k0 += 64 * 8) {
+    float s[8], s0[8], s1[8], tw[8], tb[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s[i] = s0[i] = s1[i] = 0.f;
+      const int qq = min(max(k0 + lane + 64 * i - enc0, 0), D - 1);
+      tw[i] = P[c.L.te_w + qq];
+      tb[i] = P[c.L.te_b + qq];
+    }
+    for (int q0 = qa; q0 < qe; q0 += 64) {
+      int64_t e_l, o_l;
+      float t_l;
+      store_event(c, sv, q0 + lane, e_l, o_l, t_l);
+      if (k0 == 0 && q0 + lane < qe) tmax = fmaxf(tmax, t_l);
+      const int nq = min(64, qe - q0);
+      for (int qb = 0; qb < nq; qb += AGG_MB) {
+        float v[AGG_MB][8], dt[AGG_MB];
+#pragma unroll
+        for (int u = 0; u < AGG_MB; ++u) {
+          const int q = min(qb + u, nq - 1);
+          const int64_t e = shfl_i64(e_l, q), o = shfl_i64(o_l, q);
+          dt[u] = __shfl(t_l, q, 64) - lun;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int k = min(k0 + lane + 64 * i, Qm - 1);
+            const float* p = k < D ? rowN + k : k < 2 * D ? c.mem + o * D + (k - D)
+                                                  : k < enc0 ? c.ev_msg + e * d + (k - 2 * D) : rowN;
+            v[u][i] = *p;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < AGG_MB; ++u) {
+          if (qb + u >= nq) break;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int k = k0 + lane + 64 * i;
+            const bool enc = k >= enc0 && k < Qm;
+            float cs = 0.f, sn = 0.f;
+            if (enc) te_sincos(fmaf(tw[i], dt[u], tb[i]), sn, cs);
+            s[i] += v[u][i] * f01(!enc) + cs;
+            s0[i] += sn;
+            s1[i] += sn * dt[u];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[w][0][i][lane] = s[i];
+      red[w][1][i][lane] = s0[i];
+      red[w][2][i][lane] = s1[i];
+    }
+    if (k0 == 0) {
+      const float wm = wave_max(tmax);
+      if (lane == 0) rmax[w] = wm;
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = k0 + lane + 64 * i;
+        if (k >= Qm) continue;
+        const float a = ((red[0][0][i][lane] + red[1][0][i][lane]) + red[2][0][i][lane]) + red[3][0][i][lane];
+        X[k] = a / (float)tot;
+        if (k >= enc0) {
+          const float b0 = ((red[0][1][i][lane] + red[1][1][i][lane]) + red[2][1][i][lane]) + red[3][1][i][lane];
+          const float b1 = ((red[0][2][i][lane] + red[1][2][i][lane]) + red[2][2][i][lane]) + red[3][2][i][lane];
+          c.s0m[(int64_t)m * D + (k - enc0)] = b0 * inv;
+          c.s1m[(int64_t)m * D + (k - enc0)] = b1 * inv;
+        }
+      }
+      if (k0 == 0 && lane == 0) {
+        c.xw[m] = 1;
+        c.trel[m] = 0.f;
+        c.lu[m] = fmaxf(fmaxf(rmax[0], rmax[1]), fmaxf(rmax[2], rmax[3]));
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -828,6 +953,10 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
     }
   }
   const int n = mode == 0 ? c.cnt[CNT_M] : (list_cnt ? *list_cnt : n_host);
+  if (mode == 0 && c.aggr == 1) {  // train, MeanAggregator: a workgroup per node (hub nodes store many messages)
+    for (int m = bid; m < n; m += nb) agg_node_mean_wg(c, c.nid[m], m);
+    return;
+  }
   for (int m = bid * 4 + (threadIdx.x >> 6); m < n; m += nb * 4) {
     const int64_t v = mode == 0 ? c.nid[m] : (list ? list[m] : base + m);
     agg_node(c, v, m, lane, mode == 0);
