@@ -347,11 +347,15 @@ def run_tgn(args, world, rank, dev):
         per_edge = 20 + 4 * d + 4 * D + 4
         if name == "tgn_gru_edge":
             algo = M * (4 * Qm + 4 * D + 4 * D + 16 * D) + E * (4 * d + 12 + 4 * D)
-        elif name in ("tgn_attn_fwd", "tgn_attn_bwd"):
-            algo = E * (12 * D + 8) + M * 0
+        elif name == "tgn_attn_fwd":
+            algo = E * (12 * D + 8)
+        elif name == "tgn_attn_bwd":
+            # attention backward; then, in one launch, the (dk, dv) sums (dKV rows in, dP k/v columns out)
+            # beside dW_edge (dE + edge attrs) and dEnc W_e (dE again)
+            algo = E * (12 * D + 8) + E * (8 * D + 8 * D) + E * (4 * D + 4 * (D + d) + 12 + 4 * D)
         elif name == "tgn_wgrad_dz0":
-            # dW_edge (dE + edge attrs), dEnc W_e (dE again), dW_proj (dP + z0), dz0 (dP, gates, memory, dG out)
-            algo = E * (4 * D + 4 * (D + d) + 12 + 4 * D) + M * (16 * D + 4 * D + 16 * D + 16 * D + 8 * D + 16 * D)
+            # dW_proj (dP + z0), dz0 (dP, gates, memory, dG out)
+            algo = M * (16 * D + 4 * D + 16 * D + 16 * D + 8 * D + 16 * D)
         elif name == "tgn_agg_emit":
             algo = M * (8 * D + 4 * d + 40 + 4 * Qm) + E * (per_edge + 4)
         else:

@@ -434,6 +434,28 @@ __device__ __forceinline__ bool gemm_job_dispatch(const J& j, int& bid, float* s
   bid -= nb;
   return false;
 }
+// a non-GEMM piece of work riding in a gemmN launch: nb 256-thread workgroups running f(bid, smem)
+template <class F>
+struct BlockJob {
+  struct Cfg {
+    static constexpr int SMEM = 4;
+  };
+  F f;
+  int nb;
+};
+template <class F>
+__device__ __forceinline__ bool gemm_job_dispatch(const BlockJob<F>& j, int& bid, float* smem) {
+  if (bid < j.nb) {
+    j.f(bid, smem);
+    return true;
+  }
+  bid -= j.nb;
+  return false;
+}
+template <class J>
+inline int job_blocks(const J& j) { return gemm_blocks(j.g); }
+template <class F>
+inline int job_blocks(const BlockJob<F>& j) { return j.nb; }
 template <class... J>
 __global__ void __launch_bounds__(256) gemmN_kernel(J... j) {
   constexpr int SM = std::max({J::Cfg::SMEM...});
@@ -443,7 +465,7 @@ __global__ void __launch_bounds__(256) gemmN_kernel(J... j) {
 }
 template <class... J>
 static inline void gemmN_launch(hipStream_t s, const J&... j) {
-  const int nb = (gemm_blocks(j.g) + ... + 0);
+  const int nb = (job_blocks(j) + ... + 0);
   if (nb > 0) gemmN_kernel<J...><<<nb, 256, 0, s>>>(j...);
 }
 

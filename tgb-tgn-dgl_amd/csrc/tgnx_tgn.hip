@@ -15,8 +15,8 @@
 //   tgn_pred_train  LinkPredictor + BCE + backward rows per event
 //   tgn_attn_bwd    attention backward ‖ predictor bias / output-layer / loss reductions
 //   tgn_kv_reduce   per-edge dk / dv summed into the neighbours' dP rows (sorted runs, no hub contention)
-//   GEMMs           dW_edge ‖ dW_proj, dW_src/dst ‖ Δt-encoding grads, dZ0 (+ GRU backward epilogue),
-//                   dW_gru ‖ message-encoding grads
+//                   ‖ dW_edge, dEnc·W_e (the GEMMs that need only dE)
+//   GEMMs           dW_proj, dW_src/dst ‖ dZ0 (+ GRU backward epilogue); dW_gru ‖ message-encoding grads
 //   tgn_adam, tgn_update (memory / last_update of src ∪ dst, message stores, ring merge)
 #include "tgnx_gemm.h"
 #include "tgnx_math.h"
@@ -1488,11 +1488,11 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
 // instead ran at about one element per two clocks per CU: slower than the contention it removed.)
 constexpr int KVR_CH = 64;            // edges per workgroup
 constexpr int KVR_PW = KVR_CH / 4;    // sorted edges per wave
-__global__ void __launch_bounds__(256) tgn_kv_reduce(Ctx c) {
+__device__ void kv_reduce_body(const Ctx& c, int bid) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int E = c.ceoff[c.cnt[c.rsel]];
-  const int eb = blockIdx.x * KVR_CH;
+  const int eb = bid * KVR_CH;
   if (eb >= E) return;  // whole workgroup
   const int ne = min(KVR_CH, E - eb);
   const int HC = c.HC, H2 = 2 * HC;
@@ -1551,6 +1551,13 @@ __global__ void __launch_bounds__(256) tgn_kv_reduce(Ctx c) {
       if (c0 + lane + 64 * p < H2) atomicAdd(dst + 64 * p, a[p]);
   }
 }
+
+__global__ void __launch_bounds__(256) tgn_kv_reduce(Ctx c) { kv_reduce_body(c, blockIdx.x); }
+// the same work as a BlockJob of a gemmN launch (beside the GEMMs that need only dE, see the train step)
+struct KvReduceJob {
+  Ctx c;
+  __device__ void operator()(int bid, float*) const { kv_reduce_body(c, bid); }
+};
 
 // ------------------------------------------------------------------ backward GEMM operands / epilogues
 // (n, m) -> z0[m][n], and 1 in the extra column n == D (bias gradient)
@@ -2586,25 +2593,29 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     tgn_attn_bwd<<<ncb + gridn(3 * D + 2, 4), 256, 0, s>>>(c, ncb);
   }
   TGNX_LAUNCH_CHECK("tgn_attn_bwd");
-  tgn_kv_reduce<<<gridn(k.Etr, KVR_CH, 1 << 20), 256, 0, s>>>(c);
-  probe_end(TGNX_K_SEG_BWD, s);
-  TGNX_LAUNCH_CHECK("tgn_kv_reduce");
-  // weight gradients (deferred split-K) ‖ ...
+  // k / v sums into dP ‖ the GEMMs that need only dE: dW_edge (deferred split-K) and dEnc·W_e (Δt
+  // partials of the sampled edges).  Jobs of one gemmN launch add up rather than overlap (measured:
+  // the five backward jobs in one launch took 28 us, dz0 alone 16), while kv_reduce leaves most CUs
+  // idle: the dE-only GEMMs fill them here instead of lengthening the dP launch below.
   const EpiGradStore e_dWe{G, c.L.we, D + d, c.adf};
+  gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(k.Etr, KVR_CH, 1 << 20)},
+               gemm_job<G32>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, EpiDeferred{}, c.pA),
+               gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
+                             LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
+                             (float*)nullptr));
+  probe_end(TGNX_K_SEG_BWD, s);
+  TGNX_LAUNCH_CHECK("tgn_kv_reduce_dE");
+  // weight gradients (deferred split-K) ‖ ...
   const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D, c.adf};
   const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D, c.adf};
   const EpiGruWGrad e_dWg{G, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, Qm, D, c.adf};
-  // one launch: dW_edge, dW_proj, dW_src/dst (deferred split-K) ‖ dEnc·W_e (Δt partials) ‖ dz0 = dP W
-  // with the GRU backward in its epilogue — all read only what attn_bwd / pred_train produced
+  // one launch: dW_proj, dW_src/dst (deferred split-K) ‖ dz0 = dP W with the GRU backward in its
+  // epilogue — all read only what attn_bwd / kv_reduce / pred_train produced
   const int rows_edge = (k.Etr + G32::TM - 1) / G32::TM, rows_msg = (k.Mtr + G32::TM - 1) / G32::TM;
   probe_begin(TGNX_K_EDGE_BWD, s);
-  gemmN_launch(s, gemm_job<G32>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, EpiDeferred{}, c.pA),
-               gemm_job<G32>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB),
+  gemmN_launch(s, gemm_job<G32>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB),
                gemm_job<G32>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
                              LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, EpiDeferred{}, c.pC),
-               gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
-                             LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
-                             (float*)nullptr),
                gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
                              LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, EpiGruBwd{c.gates, c.mem, c.nid, c.dG, D},
                              (float*)nullptr));
