@@ -370,7 +370,9 @@ def run_tgn(args, world, rank, dev):
         flops_gru_edge = 2 * q["nodes"] * (Qm + D) * 4 * D + 2 * q["edges"] * (D + d) * D
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    # the PMC passes (tools/pmc_traffic.sh) run the default workload: wiki-shaped, 1 hop, last aggregation
+    pmc_workload = args.dataset == "tgbl-wiki" and args.layers == 1 and args.aggr == "last" and args.batch == 200
+    if os.path.exists(pmc) and pmc_workload:
         try:
             traffic = json.load(open(pmc)).get(dom, {}).get("bytes_per_launch")
         except Exception:
