@@ -2574,18 +2574,19 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     const int ncb1 = gridn(k.R1tr, 4, 1 << 20);
     tgn_attn_bwd<<<ncb1 + gridn(3 * D + 2, 4), 256, 0, s>>>(cr, ncb1);
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
-    tgn_kv_reduce<<<gridn(k.E1tr, KVR_CH, 1 << 20), 256, 0, s>>>(cr);
-    TGNX_LAUNCH_CHECK("tgn_kv_reduce2");
-    gemmN_launch(s,
-                 gemm_job<G32L>(gemm_shape<G32L>(k.Rtr, HC, 4 * HC, c.cnt + CNT_R), LoadRowK{c.dP2, k.Rtr, 4 * HC, 4 * HC},
-                                LoadProjWT{P + c.L.wq2, c.L.pw, HC, HC}, EpiStore{c.dZc, nullptr, HC, 0}, (float*)nullptr),
-                 gemm_job<G32>(shp_dWp2(k, c.cnt), LoadKRow{c.dP2, 4 * HC, k.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
-                               EpiDeferred{}, c.pE),
+    // conv2's (dk, dv) sums ‖ its dE2-only GEMMs (as in the 1-hop step below), then dh1 ‖ dW_proj2
+    gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{cr}, gridn(k.E1tr, KVR_CH, 1 << 20)},
                  gemm_job<G32>(shp_dWe2(k, c.cnt), LoadKRow{c.dE2, HC, k.E1tr, HC}, LoadEdgeAttrMapT{ea1},
                                EpiDeferred{}, c.pF),
                  gemm_job<G32>(gemm_shape<G32>(k.E1tr, D, HC, c.cnt + CNT_E1), LoadRowK{c.dE2, k.E1tr, HC, HC},
                                LoadKRow{P + c.L.we2, D, HC, D + d},
                                EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, c.e1_e2, c.tgp_e1}, (float*)nullptr));
+    TGNX_LAUNCH_CHECK("tgn_kv_reduce2");
+    gemmN_launch(s,
+                 gemm_job<G32L>(gemm_shape<G32L>(k.Rtr, HC, 4 * HC, c.cnt + CNT_R), LoadRowK{c.dP2, k.Rtr, 4 * HC, 4 * HC},
+                                LoadProjWT{P + c.L.wq2, c.L.pw, HC, HC}, EpiStore{c.dZc, nullptr, HC, 0}, (float*)nullptr),
+                 gemm_job<G32>(shp_dWp2(k, c.cnt), LoadKRow{c.dP2, 4 * HC, k.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
+                               EpiDeferred{}, c.pE));
     TGNX_LAUNCH_CHECK("tgn_dh1");
     tgn_attn_bwd<<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c, gridn(k.Rtr, 4, 1 << 20));
   } else {
