@@ -741,7 +741,7 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
 // into 4 contiguous ranges, one per wave, and the partial sums combine in LDS in wave order.  A hub node
 // of the review-shaped stream stores ~100-200 messages of its last batch; one wave evaluating D
 // time-encoding sin/cos pairs per message ran 84 us (agg_emit), all other waves done long before.
-__device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m) {
+__device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m, bool grad) {
   __shared__ float red[4][3][8][64];
   __shared__ float rmax[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -752,7 +752,8 @@ __device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m) {
   if (tot == 0) {  // workgroup-uniform
     if (w == 0) {
       for (int k = lane; k < Qm; k += 64) X[k] = 0.f;
-      for (int q = lane; q < D; q += 64) c.s0m[(int64_t)m * D + q] = c.s1m[(int64_t)m * D + q] = 0.f;
+      if (grad)
+        for (int q = lane; q < D; q += 64) c.s0m[(int64_t)m * D + q] = c.s1m[(int64_t)m * D + q] = 0.f;
       if (lane == 0) {
         c.xw[m] = -1;
         c.trel[m] = 0.f;
@@ -832,7 +833,7 @@ __device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m) {
         if (k >= Qm) continue;
         const float a = ((red[0][0][i][lane] + red[1][0][i][lane]) + red[2][0][i][lane]) + red[3][0][i][lane];
         X[k] = a / (float)tot;
-        if (k >= enc0) {
+        if (grad && k >= enc0) {
           const float b0 = ((red[0][1][i][lane] + red[1][1][i][lane]) + red[2][1][i][lane]) + red[3][1][i][lane];
           const float b1 = ((red[0][2][i][lane] + red[1][2][i][lane]) + red[2][2][i][lane]) + red[3][2][i][lane];
           c.s0m[(int64_t)m * D + (k - enc0)] = b0 * inv;
@@ -953,8 +954,9 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
     }
   }
   const int n = mode == 0 ? c.cnt[CNT_M] : (list_cnt ? *list_cnt : n_host);
-  if (mode == 0 && c.aggr == 1) {  // train, MeanAggregator: a workgroup per node (hub nodes store many messages)
-    for (int m = bid; m < n; m += nb) agg_node_mean_wg(c, c.nid[m], m);
+  if (c.aggr == 1 && (mode == 0 || list)) {  // MeanAggregator, train / eval update: a workgroup per node (hub
+                                             // nodes store many messages); the all-node flush stays wave-per-node
+    for (int m = bid; m < n; m += nb) agg_node_mean_wg(c, mode == 0 ? c.nid[m] : list[m], m, mode == 0);
     return;
   }
   for (int m = bid * 4 + (threadIdx.x >> 6); m < n; m += nb * 4) {
