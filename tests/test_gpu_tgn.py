@@ -159,3 +159,64 @@ def test_tgn_fused_adam_step_equals_fwd_bwd_plus_update(layers):
             o1.exp_avg.copy_(o2.exp_avg)
             o1.exp_avg_sq.copy_(o2.exp_avg_sq)
             m1.memory.memory.copy_(m2.memory.memory)
+
+
+def test_tgn_mean_hub_node_matches_oracle():
+    """MeanAggregator over a hub: one node is the source of EVERY event of a 300-event batch, so in the
+    next batch its stored messages (300) are split over the four waves of its workgroup, each wave
+    running more than one 64-message round (agg_node_mean_wg), in the train step and in the eval
+    update.  Outputs, gradients, memory and last_update against the oracle as in the main test."""
+    from oracle.sampler_ref import RefLastNeighborLoader
+    from oracle.tgn_ref import RefTGN, eval_step, train_step
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.synth import make_stream
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    N, B, d, D, nb = 400, 300, 8, 32, 4
+    s = make_stream("tgbl-wiki", seed=5, num_events=B * nb, num_nodes=N, msg_dim=d)
+    hub = int(s.src[0])
+    s.src[:] = hub                      # the hub is every event's source
+    torch.manual_seed(0)
+    ref = RefTGN(N, d, hidden=D, aggr="mean", dropout=0.0)
+    opt_ref = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    dev = torch.device("cuda")
+    model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=5, aggr="mean", dropout=0.0)
+    model.load_reference_state(ref.state_dict())
+    opt = TgnAdam(model, 1e-3)
+    eng = TgnEngine(model, LastNeighborLoader(N, 10, device=dev),
+                    dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32), msg=s.msg), opt, dst_nodes=s.dst_nodes)
+    eng.reset_state()
+    lref = RefLastNeighborLoader(N, 10)
+    ev_t, ev_msg = torch.from_numpy(s.t.astype(np.float32)), torch.from_numpy(s.msg)
+    rng = np.random.default_rng(2)
+    named = dict(ref.named_parameters())
+    for st in range(nb - 1):
+        sl = slice(st * B, (st + 1) * B)
+        src, pos = torch.from_numpy(s.src[sl]), torch.from_numpy(s.dst[sl])
+        neg = torch.from_numpy(rng.choice(s.dst_nodes, size=B))
+        loss, po, no = train_step(ref, opt_ref, lref, ev_t, ev_msg, src, pos, neg, ev_t[sl], ev_msg[sl])
+        pg, ng = eng.train_batch(st * B, B, neg=neg)
+        torch.cuda.synchronize()
+        eng.check()
+        assert torch.allclose(pg.cpu(), po, atol=2e-5) and torch.allclose(ng.cpu(), no, atol=2e-5), st
+        g = model.grads_by_name()
+        for name in model.param_order:
+            if name in SHIFT_INVARIANT:
+                continue
+            assert _rel(g[name], named[name].grad) < 2e-3, (st, name)
+        assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5), st
+        assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update), st
+        _sync(ref, opt_ref, model, opt)
+    # eval batch (scores with the batch-start state, then the eval update aggregates the hub again)
+    ref.memory.train(False)
+    eng.flush()
+    a = (nb - 1) * B
+    sl = slice(a, a + B)
+    src, pos = torch.from_numpy(s.src[sl]), torch.from_numpy(s.dst[sl])
+    negs = torch.from_numpy(rng.choice(s.dst_nodes, size=(B, 5)))
+    po, no = eval_step(ref, lref, ev_t, ev_msg, src, pos, negs, ev_t[sl], ev_msg[sl])
+    pg, ngm, rr = eng.eval_batch(a, B, negs)
+    torch.cuda.synchronize()
+    eng.check()
+    assert torch.allclose(pg.cpu(), po, atol=2e-5) and torch.allclose(ngm.cpu(), no, atol=2e-5)
+    assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5)
+    assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update)
