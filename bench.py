@@ -323,7 +323,7 @@ def run_tgn(args, world, rank, dev):
     # live per-launch timing (HIP events on the launch stream), units from the device counters
     Qm = 3 * D + d
     probes = {}
-    spec = (("tgn_gru_edge", 1), ("tgn_attn_fwd", 6), ("tgn_attn_bwd", 8), ("tgn_wgrad_dz0", 2),
+    spec = (("tgn_gru_edge", 1), ("tgn_attn_fwd", 6), ("tgn_attn_bwd", 8), ("tgn_kv_dE", 10), ("tgn_wgrad_dz0", 2),
             ("tgn_agg_emit", 9), ("tgn_scan", 3), ("tgn_pred_train", 4), ("tgn_fixup_update", 5), ("tgn_adam", 7))
     if getattr(eng, "_res_fused", False):   # world 1: Adam rides in the gradient writers (no tgn_adam launch)
         spec = tuple(x for x in spec if x[0] != "tgn_adam")
@@ -350,9 +350,11 @@ def run_tgn(args, world, rank, dev):
         elif name == "tgn_attn_fwd":
             algo = E * (12 * D + 8)
         elif name == "tgn_attn_bwd":
-            # attention backward; then, in one launch, the (dk, dv) sums (dKV rows in, dP k/v columns out)
-            # beside dW_edge (dE + edge attrs) and dEnc W_e (dE again)
-            algo = E * (12 * D + 8) + E * (8 * D + 8 * D) + E * (4 * D + 4 * (D + d) + 12 + 4 * D)
+            algo = E * (12 * D + 8)
+        elif name == "tgn_kv_dE":
+            # the (dk, dv) sums (dKV rows in, dP k/v columns out) beside dW_edge (dE + edge attrs) and
+            # dEnc W_e (dE again)
+            algo = E * (8 * D + 8 * D) + E * (4 * D + 4 * (D + d) + 12 + 4 * D)
         elif name == "tgn_wgrad_dz0":
             # dW_proj (dP + z0), dz0 (dP, gates, memory, dG out)
             algo = M * (16 * D + 4 * D + 16 * D + 16 * D + 8 * D + 16 * D)

@@ -97,6 +97,7 @@ int tgnx_block_ids_host(const int64_t* src, const int64_t* dst, int64_t num_even
 #define TGNX_K_ADAM 7
 #define TGNX_K_SEG_BWD 8        /* tgnn_seg_bwd */
 #define TGNX_K_EDGE_META 9      /* tgnn_edge_meta */
+#define TGNX_K_KV 10             /* TGN: kv_reduce ‖ dW_edge ‖ dEnc·W_e launch */
 int tgnx_probe_enable(int32_t kernel_id);
 int tgnx_probe_read(double* total_ms, int64_t* launches);
 

@@ -2595,18 +2595,20 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     const int ncb = gridn(k.Rtr, 4, 1 << 20);
     tgn_attn_bwd<<<ncb + gridn(3 * D + 2, 4), 256, 0, s>>>(c, ncb);
   }
+  probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_attn_bwd");
   // k / v sums into dP ‖ the GEMMs that need only dE: dW_edge (deferred split-K) and dEnc·W_e (Δt
   // partials of the sampled edges).  Jobs of one gemmN launch add up rather than overlap (measured:
   // the five backward jobs in one launch took 28 us, dz0 alone 16), while kv_reduce leaves most CUs
   // idle: the dE-only GEMMs fill them here instead of lengthening the dP launch below.
   const EpiGradStore e_dWe{G, c.L.we, D + d, c.adf};
+  probe_begin(TGNX_K_KV, s);
   gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(k.Etr, KVR_CH, 1 << 20)},
                gemm_job<G32>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, EpiDeferred{}, c.pA),
                gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
                              LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
                              (float*)nullptr));
-  probe_end(TGNX_K_SEG_BWD, s);
+  probe_end(TGNX_K_KV, s);
   TGNX_LAUNCH_CHECK("tgn_kv_reduce_dE");
   // weight gradients (deferred split-K) ‖ ...
   const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D, c.adf};

@@ -13,7 +13,8 @@ KERNELS = {
     "tgn_gru_edge": ("gemmN_kernel", "LoadGruA,"),
     "tgn_wgrad_dz0": ("gemmN_kernel", "LoadZ1T", "EpiGruBwd"),
     "tgn_attn_fwd": ("tgn_attn_fwd<true>",),
-    "tgn_attn_bwd": [("tgn_attn_bwd",), ("gemmN_kernel", "KvReduceJob")],   # the probe brackets both launches
+    "tgn_attn_bwd": ("tgn_attn_bwd",),
+    "tgn_kv_dE": ("gemmN_kernel", "KvReduceJob"),
     "tgn_agg_emit": ("tgn_agg_emit",),
     "tgn_scan": ("tgn_scan<true>",),
     "tgn_mark": ("tgn_mark<true>",),
