@@ -318,6 +318,13 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
  * tgnx_tgn_train_update (grads are still written).  Refused with xrows set (data parallel). */
 int tgnx_tgn_train_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
                         void* stream);
+/* tgnx_tgn_train_step of the next batch of a resident split, with the batch cursor folded in: the
+ * same as tgnx_tgnn_advance(ctl, mode 1, ..., split_lo, split_hi, batch, rank, world, base_seed,
+ * train 1) followed by tgnx_tgn_train_step(gen_neg 1), one launch fewer (the step counters NB / GEN /
+ * ADAM_T advance in the step's last launch).  World 1 (Adam is folded in as well). */
+int tgnx_tgn_train_step_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                                 int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
+                                 int32_t dropout, void* stream);
 /* Data parallel: write the exchanged rows of every rank (rows [nrows, TGNX_TGN_ROW(mem_dim)], slots
  * with node -1 skipped) into memory / last_update, then zero `rows` (ready for the next summing
  * exchange).  Ranks that updated the same node computed the same row (same replicated inputs), so the

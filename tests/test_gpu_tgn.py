@@ -220,3 +220,43 @@ def test_tgn_mean_hub_node_matches_oracle():
     assert torch.allclose(pg.cpu(), po, atol=2e-5) and torch.allclose(ngm.cpu(), no, atol=2e-5)
     assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5)
     assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update)
+
+
+def test_tgn_resident_folded_cursor_equals_advance_plus_step():
+    """Resident world-1 steps with the batch cursor folded into tgn_mark (tgnx_tgn_train_step_resident)
+    against tgnx_tgnn_advance + tgnx_tgn_train_step on a twin engine, device negatives and attention
+    dropout on: the step counters and batch descriptor in ctl must match exactly after every step;
+    outputs, parameters and memory within the fused-Adam test's tolerances (resynchronised per step)."""
+    engines = []
+    for fold in (True, False):
+        s, ref, opt_ref, lref, model, opt, eng = _setup("last")
+        model.cfg.dropout = 0.1
+        eng.fold_cursor = fold
+        eng.bind_resident(0, 7 * 50 + 20, 50, dropout=True)   # the last batch is partial (20 events)
+        eng.begin_epoch()
+        engines.append((model, opt, eng))
+    (m1, o1, e1), (m2, o2, e2) = engines
+    for st in range(9):                                        # 8 batches, then one past the split (B = 0)
+        for e in (e1, e2):
+            e.resident_train_step()
+        torch.cuda.synchronize()
+        e1.check()
+        e2.check()
+        for w in (0, 1, 2, 3, 4, 7, 8, 9, 10):                 # start, cur e_id, B, GEN, ADAM_T, LO, HI, SEED, NB
+            assert int(e1.ctl[w]) == int(e2.ctl[w]), (st, w, int(e1.ctl[w]), int(e2.ctl[w]))
+        assert torch.equal(e1.neg_train, e2.neg_train), st
+        B = int(e1.ctl[2])
+        if B:
+            assert torch.allclose(e1.out_pos[:B], e2.out_pos[:B], atol=1e-5), st
+        for name in m1.param_order:
+            if name in SHIFT_INVARIANT:
+                continue
+            o, n, _ = m1._views[name]
+            assert _rel(m1.flat[o:o + n], m2.flat[o:o + n]) < 1e-4, (st, name)
+        assert torch.allclose(m1.memory.memory, m2.memory.memory, atol=1e-5), st
+        assert abs(e1.loss_sum() - e2.loss_sum()) <= 1e-5 * max(1.0, abs(e2.loss_sum())), st
+        with torch.no_grad():
+            m1.flat.copy_(m2.flat)
+            o1.exp_avg.copy_(o2.exp_avg)
+            o1.exp_avg_sq.copy_(o2.exp_avg_sq)
+            m1.memory.memory.copy_(m2.memory.memory)

@@ -103,7 +103,9 @@ struct AdamFuse {
   // buffers may alias as far as the compiler knows, so interleaving would serialise the elements)
   template <int N>
   __device__ __forceinline__ void put_n(float* g, const int64_t (&idx)[N], const float (&val)[N]) const {
-    if (!p) {
+    // no update for an empty batch (a resident cursor past the split): the split-K fixup still finishes
+    // the previous step's partials, as tgn_adam skips B = 0
+    if (!p || ctl[TGNX_CTL_B] == 0 || ctl[TGNX_CTL_ERR] != 0) {
 #pragma unroll
       for (int i = 0; i < N; ++i)
         if (idx[i] >= 0) g[idx[i]] = val[i];
@@ -173,6 +175,12 @@ struct Ctx {
   int64_t* xw;
   float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
   float *dZc, *dP, *dE, *dG, *tgp;
+  // resident batch cursor folded into tgn_mark (tgnx_tgn_train_step_resident): mark derives the batch
+  // descriptor from the step counters, the step's last launch advances them
+  int adv = 0;
+  int64_t adv_lo = 0, adv_hi = 0, adv_batch = 0;
+  int adv_rank = 0, adv_world = 1;
+  uint64_t adv_seed = 0;
   AdamFuse adf;  // fused optimizer (tgnx_tgn_train_step) or plain gradient stores
   float* dKV;  // per edge [dk | dv] of the attention backward [E][2 HC] (tgn_kv_reduce sums them into dP)
   float *encE, *sinE;  // per sampled edge: cos / sin of the Δt encoding argument [E][D]
@@ -224,9 +232,25 @@ __device__ __forceinline__ void mark_node(uint32_t* bm, uint32_t* sum, int64_t v
 __device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh);
 template <bool TRAIN>
 __global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
-  const int B = (int)c.ctl[TGNX_CTL_B];
+  int B;
+  int64_t start;
+  if (TRAIN && c.adv) {  // tgnn_advance (mode 1) restated: every block from the unchanged step counters
+    const int64_t nb = c.ctl[TGNX_CTL_NB];
+    start = c.adv_lo + nb * c.adv_batch;
+    B = start >= c.adv_hi ? 0 : (int)min(c.adv_hi - start, c.adv_batch);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the descriptor for the later launches (no block here reads it)
+      c.ctl[TGNX_CTL_BATCH_START] = start;
+      c.ctl[TGNX_CTL_B] = B;
+      c.ctl[TGNX_CTL_CUR_EID] = start;
+      c.ctl[TGNX_CTL_LO] = (int64_t)B * c.adv_rank / c.adv_world;
+      c.ctl[TGNX_CTL_HI] = (int64_t)B * (c.adv_rank + 1) / c.adv_world;
+      c.ctl[TGNX_CTL_SEED] = (int64_t)(mix64(c.adv_seed ^ mix64((uint64_t)(nb + 1))) >> 1);
+    }
+  } else {
+    B = (int)c.ctl[TGNX_CTL_B];
+    start = c.ctl[TGNX_CTL_BATCH_START];
+  }
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   if ((int)blockIdx.x >= nmark) {  // train: ring-insert / message-store plans (1024 threads)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ int sh[40];
@@ -234,10 +258,12 @@ __global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
     return;
   }
   if (threadIdx.x >= 256) return;  // marking runs 256-thread groups
-  const int gen = (int)c.ctl[TGNX_CTL_GEN];
+  const bool adv = TRAIN && c.adv;
+  const int gen = (int)c.ctl[TGNX_CTL_GEN] + (adv ? 1 : 0);
   const int Kn = TRAIN ? 1 : c.Kn;
   // train: this rank's event slice [lo, lo + nl) (data parallel; the whole batch at world 1)
-  const int lo = TRAIN ? (int)c.ctl[TGNX_CTL_LO] : 0, nl = TRAIN ? (int)(c.ctl[TGNX_CTL_HI] - c.ctl[TGNX_CTL_LO]) : B;
+  const int lo = !TRAIN ? 0 : adv ? B * c.adv_rank / c.adv_world : (int)c.ctl[TGNX_CTL_LO];
+  const int nl = !TRAIN ? B : adv ? B * (c.adv_rank + 1) / c.adv_world - lo : (int)(c.ctl[TGNX_CTL_HI] - c.ctl[TGNX_CTL_LO]);
   const int nq = nl * (2 + Kn);
   const int sl = threadIdx.x & 15, grp = (threadIdx.x & 63) >> 4;
   const int gstride = (nmark * 256) >> 4;
@@ -250,8 +276,9 @@ __global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
     } else if (TRAIN) {
       const int i = lo + q - 2 * nl;
       if (c.gen_neg) {
-        const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-        const uint64_t off = (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
+        const uint64_t seed = adv ? (mix64(c.adv_seed ^ mix64((uint64_t)(c.ctl[TGNX_CTL_NB] + 1))) >> 1)
+                                  : (uint64_t)c.ctl[TGNX_CTL_SEED];
+        const uint64_t off = adv ? (uint64_t)start : (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
         const int64_t pd = c.ev_dst[start + i];
         v = c.dst_nodes[0];
         for (uint64_t attempt = 0; attempt < 64; ++attempt) {
@@ -411,7 +438,7 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
     plan_blocks(c, (int)blockIdx.x - 1, B, start, smem, sh);
     return;
   }
-  const int gen = (int)c.ctl[TGNX_CTL_GEN];
+  const int gen = (int)c.ctl[TGNX_CTL_GEN] + (c.adv ? 1 : 0);  // cursor folded into mark: counters advance at the end
   // pass 0: the words each thread walks.  Small graphs (<= 2 words per thread): contiguous word ranges
   // (summaries just cleared); large graphs: the nonzero words in word order, from the summaries
   const bool direct = c.words <= 2 * (int64_t)T;
@@ -1239,7 +1266,7 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     c.cnt[CNT_LIST] = 3 * (hi - lo);
     if (c.adf.p) {  // fused Adam: this step's scalars for the gradient writers (tgn_adam computes them itself)
-      const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
+      const int64_t t = c.ctl[TGNX_CTL_ADAM_T] + (c.adv ? 1 : 0);
       float* sc = reinterpret_cast<float*>(c.ctl + TGNX_CTL_ADAM_SC);
       sc[0] = (float)(c.lr / (1.0 - pow((double)c.b1, (double)t)));
       sc[1] = (float)sqrt(1.0 - pow((double)c.b2, (double)t));
@@ -2019,8 +2046,17 @@ __global__ void __launch_bounds__(256) tgn_update(Ctx c, int nmem, int nst, int 
 // update_state + ring insert (update_body: nothing in the fixup reads memory, stores or the ring)
 struct TrainTail {
   TeReduceTail te;
-  int nte, nmem, nst;
+  int nte, nmem, nst, ninc;  // ninc: index of the step-counter block (folded cursor), -1 without
   __device__ void operator()(int bid) const {
+    if (bid == ninc) {  // what tgnn_advance did at the start of the step (no other block reads these)
+      if (threadIdx.x == 0) {
+        int64_t* ctl = te.c.ctl;
+        ctl[TGNX_CTL_GEN] += 1;
+        ctl[TGNX_CTL_NB] += 1;
+        if (ctl[TGNX_CTL_B] > 0) ctl[TGNX_CTL_ADAM_T] += 1;
+      }
+      return;
+    }
     if (bid < nte) te(bid);
     else update_body(te.c, bid - nte, nmem, nst, 0, te.c.upd, te.c.cnt + CNT_U, 0, 0);
   }
@@ -2490,13 +2526,30 @@ int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf
   return TGNX_OK;
 }
 
+struct AdvArgs {
+  int64_t lo, hi, batch;
+  int rank, world;
+  uint64_t seed;
+};
 static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
-                           void* stream, bool fuse_adam) {
+                           void* stream, bool fuse_adam, const AdvArgs* adv = nullptr) {
   Ctx c;
   Caps k;
   WsLay W;
   int rc = make_ctx(cfg, buf, 1, c, k, W);
   if (rc) return rc;
+  if (adv) {
+    TGNX_CHECK_ARG(adv->batch > 0 && adv->batch <= cfg->max_batch && adv->world >= 1 && adv->rank >= 0 &&
+                       adv->rank < adv->world && adv->lo >= 0 && adv->hi >= adv->lo,
+                   "tgnx_tgn_train_step_resident: bad cursor arguments");
+    c.adv = 1;
+    c.adv_lo = adv->lo;
+    c.adv_hi = adv->hi;
+    c.adv_batch = adv->batch;
+    c.adv_rank = adv->rank;
+    c.adv_world = adv->world;
+    c.adv_seed = adv->seed;
+  }
   TGNX_CHECK_ARG(buf->neg && buf->grads && buf->out_pos && buf->out_neg, "tgnx_tgn_train_fwd_bwd: null buffer");
   if (fuse_adam) {
     TGNX_CHECK_ARG(buf->adam_m && buf->adam_v, "tgnx_tgn_train_step: null optimizer buffer");
@@ -2634,16 +2687,17 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   // this step's GRU rows, then the stores) + ring insert, one launch
   const int nte = (2 * D + 63) / 64;
   const int nmem = gridn(k.Ucap, 4, 1024), nst = gridn(2 * k.B, 256), nring = gridn(2 * k.B, 4);
-  const TrainTail tail{TeReduceTail{c, rows_edge, rows_msg}, nte, nmem, nst};
+  const int ninc = c.adv ? nte + nmem + nst + nring : -1;
+  const TrainTail tail{TeReduceTail{c, rows_edge, rows_msg}, nte, nmem, nst, ninc};
   probe_begin(TGNX_K_FINISH, s);
   if (two)
-    gemm_fixup_launch(nte + nmem + nst + nring, tail, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
+    gemm_fixup_launch(nte + nmem + nst + nring + (c.adv ? 1 : 0), tail, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
                       gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
                       gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg),
                       gemm_fix<G32>(shp_dWp2(k, c.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC, c.adf}),
                       gemm_fix<G32>(shp_dWe2(k, c.cnt), c.pF, EpiGradStore{G, c.L.we2, D + d, c.adf}));
   else
-    gemm_fixup_launch(nte + nmem + nst + nring, tail, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
+    gemm_fixup_launch(nte + nmem + nst + nring + (c.adv ? 1 : 0), tail, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
                       gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
                       gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg));
   probe_end(TGNX_K_FINISH, s);
@@ -2659,6 +2713,13 @@ int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
 int tgnx_tgn_train_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
                         void* stream) {
   return train_step_impl(cfg, buf, gen_neg, dropout, stream, true);
+}
+
+int tgnx_tgn_train_step_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                                 int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
+                                 int32_t dropout, void* stream) {
+  const AdvArgs a{split_lo, split_hi, batch, rank, world, base_seed};
+  return train_step_impl(cfg, buf, 1, dropout, stream, true, &a);
 }
 
 int tgnx_tgn_apply_rows(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, float* rows, int64_t nrows,

@@ -259,6 +259,7 @@ class TgnEngine:
         self.dst_nodes = None if dst_nodes is None else torch.as_tensor(dst_nodes).to(self.dev, torch.long).contiguous()
         self.seed, self.rank, self.world = int(seed), int(rank), int(world)
         self.fuse_adam = True
+        self.fold_cursor = True   # resident world-1 steps: tgnx_tgn_train_step_resident
         if optimizer is None:
             self.adam_m, self.adam_v = torch.zeros_like(model.flat), torch.zeros_like(model.flat)
         else:
@@ -402,8 +403,12 @@ class TgnEngine:
         adv, fb = self._f[:2]
         lo, hi, batch = self._res
         st = self._stream()
-        rc = adv(self._ctl_p, 1, 0, 0, 0, lo, hi, batch, self.rank, self.world, self.seed, 1, st)
-        rc |= fb(self._cfg_ref, self._buf_ref, 1, self._res_drop, st)
+        if self._res_fused and self.fold_cursor:   # world 1: cursor folded into the step's first launch
+            rc = _lib.lib().tgnx_tgn_train_step_resident(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank,
+                                                         self.world, self.seed, self._res_drop, st)
+        else:
+            rc = adv(self._ctl_p, 1, 0, 0, 0, lo, hi, batch, self.rank, self.world, self.seed, 1, st)
+            rc |= fb(self._cfg_ref, self._buf_ref, 1, self._res_drop, st)
         if rc:
             raise RuntimeError(f"tgnx TGN resident step failed: {_lib.lib().tgnx_last_error().decode()}")
 
