@@ -325,6 +325,11 @@ int tgnx_tgn_train_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf,
 int tgnx_tgn_train_step_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
                                  int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
                                  int32_t dropout, void* stream);
+/* Data parallel form: tgnx_tgn_train_fwd_bwd with the folded cursor (the exchange, tgnx_tgn_apply_rows and
+ * tgnx_tgn_train_update follow; the counters have advanced when train_update reads ADAM_T). */
+int tgnx_tgn_train_fwd_bwd_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                                    int64_t split_hi, int64_t batch, int32_t rank, int32_t world,
+                                    uint64_t base_seed, int32_t dropout, void* stream);
 /* Data parallel: write the exchanged rows of every rank (rows [nrows, TGNX_TGN_ROW(mem_dim)], slots
  * with node -1 skipped) into memory / last_update, then zero `rows` (ready for the next summing
  * exchange).  Ranks that updated the same node computed the same row (same replicated inputs), so the

@@ -2722,6 +2722,13 @@ int tgnx_tgn_train_step_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buff
   return train_step_impl(cfg, buf, 1, dropout, stream, true, &a);
 }
 
+int tgnx_tgn_train_fwd_bwd_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                                    int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
+                                    int32_t dropout, void* stream) {
+  const AdvArgs a{split_lo, split_hi, batch, rank, world, base_seed};
+  return train_step_impl(cfg, buf, 1, dropout, stream, false, &a);
+}
+
 int tgnx_tgn_apply_rows(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, float* rows, int64_t nrows,
                         void* stream) {
   int rc = check_cfg(cfg);

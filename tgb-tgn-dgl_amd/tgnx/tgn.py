@@ -403,9 +403,9 @@ class TgnEngine:
         adv, fb = self._f[:2]
         lo, hi, batch = self._res
         st = self._stream()
-        if self._res_fused and self.fold_cursor:   # world 1: cursor folded into the step's first launch
-            rc = _lib.lib().tgnx_tgn_train_step_resident(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank,
-                                                         self.world, self.seed, self._res_drop, st)
+        if self.fold_cursor:   # the batch cursor folded into the step's first launch
+            f = _lib.lib().tgnx_tgn_train_step_resident if self._res_fused else _lib.lib().tgnx_tgn_train_fwd_bwd_resident
+            rc = f(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank, self.world, self.seed, self._res_drop, st)
         else:
             rc = adv(self._ctl_p, 1, 0, 0, 0, lo, hi, batch, self.rank, self.world, self.seed, 1, st)
             rc |= fb(self._cfg_ref, self._buf_ref, 1, self._res_drop, st)
