@@ -100,6 +100,13 @@ int tgnx_block_ids_host(const int64_t* src, const int64_t* dst, int64_t num_even
 #define TGNX_K_KV 10             /* TGN: kv_reduce ‖ dW_edge ‖ dEnc·W_e launch */
 int tgnx_probe_enable(int32_t kernel_id);
 int tgnx_probe_read(double* total_ms, int64_t* launches);
+/* Workgroup timeline stamps (diagnostic; measurement only): a library built with -DTGNX_STAMPS records, for
+ * wave 0 of every workgroup of the TGN step's kernels, {start, end} (s_memrealtime ticks, 100 MHz), kernel
+ * id, block and XCC as 32-byte records into `buf`: 64 shards (by block) of cap / 64 records, shard s at
+ * record s * (cap / 64); tgnx_stamps_count returns the fullest shard's count (tools/stamps.py).  buf = NULL
+ * stops recording.  Without the flag: tgnx_stamps_set returns TGNX_EINVAL and tgnx_stamps_count -1. */
+int tgnx_stamps_set(void* buf, uint32_t cap);
+int64_t tgnx_stamps_count(void);
 
 
 /* ------------------------------------------------------------------------

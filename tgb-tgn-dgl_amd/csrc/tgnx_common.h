@@ -33,6 +33,37 @@ void set_error(const char* fmt, ...);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ---------------------------------------------------------------- wave timeline stamps (diagnostic build)
+// Built with -DTGNX_STAMPS: every instrumented kernel's waves record {start, end} (s_memrealtime, 100 MHz),
+// the kernel id, block and XCC into a buffer set by tgnx_stamps_set (tools/stamps.py reads it).  Without the
+// flag TGNX_STAMP(k) is empty and the buffer entry points return TGNX_EINVAL.
+#ifdef TGNX_STAMPS
+struct StampRec {
+  unsigned long long t0, t1;
+  unsigned kid, blk, xcc, wave;
+};
+static __device__ StampRec* g_stamp_buf;
+static __device__ unsigned g_stamp_cap;             // records per shard
+static __device__ unsigned g_stamp_cnt[64 * 32];    // 64 shards (by block), one 128-B line each
+struct StampScope {  // wave 0 of each workgroup records
+  unsigned long long t0;
+  unsigned kid;
+  __device__ explicit StampScope(unsigned k) : t0(__builtin_amdgcn_s_memrealtime()), kid(k) {}
+  __device__ ~StampScope() {
+    if (threadIdx.x == 0 && g_stamp_buf) {
+      const unsigned sh = blockIdx.x & 63, i = atomicAdd(&g_stamp_cnt[sh * 32], 1u);
+      if (i < g_stamp_cap)
+        g_stamp_buf[(size_t)sh * g_stamp_cap + i] =
+            StampRec{t0, __builtin_amdgcn_s_memrealtime(), kid, blockIdx.x,
+                     (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20), 0u};
+    }
+  }
+};
+#define TGNX_STAMP(k) ::tgnx::StampScope tgnx_stamp_scope_(k)
+#else
+#define TGNX_STAMP(k)
+#endif
+
 // ---------------------------------------------------------------- counter-based RNG
 // splitmix64 finaliser: statistically strong, stateless, identical in every replay.
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {

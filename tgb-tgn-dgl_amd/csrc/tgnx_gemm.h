@@ -394,6 +394,7 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
 
 template <class CFG, class AL, class BL, class EPI>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmShape g, AL al, BL bl, EPI epi, float* part) {
+  TGNX_STAMP(20);
   __shared__ __attribute__((aligned(16))) float smem[CFG::SMEM];
   gemm_body<CFG>(g, al, bl, epi, part, blockIdx.x, smem);
 }
@@ -402,6 +403,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmShape g, AL al, BL bl, EP
 template <class C1, class C2, class AL1, class BL1, class EP1, class AL2, class BL2, class EP2>
 __global__ void __launch_bounds__(256) gemm2_kernel(GemmShape g1, AL1 a1, BL1 b1, EP1 e1, float* p1, GemmShape g2,
                                                     AL2 a2, BL2 b2, EP2 e2, float* p2) {
+  TGNX_STAMP(21);
   constexpr int SM = C1::SMEM > C2::SMEM ? C1::SMEM : C2::SMEM;
   __shared__ __attribute__((aligned(16))) float smem[SM];
   const int n1 = gemm_blocks(g1);
@@ -458,6 +460,7 @@ template <class F>
 inline int job_blocks(const BlockJob<F>& j) { return j.nb; }
 template <class... J>
 __global__ void __launch_bounds__(256) gemmN_kernel(J... j) {
+  TGNX_STAMP(22);
   constexpr int SM = std::max({J::Cfg::SMEM...});
   __shared__ __attribute__((aligned(16))) float smem[SM];
   int bid = blockIdx.x;
@@ -534,6 +537,7 @@ constexpr int GEMM_FIX_SMEM = 64 * 65 + 512;  // floats: the largest C tile (G64
 // call `tail(bid)` (extra reductions that ride in the same launch).
 template <class TAIL, class... F>
 __global__ void __launch_bounds__(256) gemm_fixup_kernel(TAIL tail, F... f) {
+  TGNX_STAMP(23);
   __shared__ __attribute__((aligned(16))) float smem[GEMM_FIX_SMEM];
   int bid = blockIdx.x;
   if (!(gemm_fix_dispatch(f, bid, smem) || ...)) tail(bid);

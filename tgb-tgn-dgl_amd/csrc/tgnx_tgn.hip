@@ -232,6 +232,7 @@ __device__ __forceinline__ void mark_node(uint32_t* bm, uint32_t* sum, int64_t v
 __device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh);
 template <bool TRAIN>
 __global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
+  TGNX_STAMP(1);
   int B;
   int64_t start;
   if (TRAIN && c.adv) {  // tgnn_advance (mode 1) restated: every block from the unchanged step counters
@@ -428,6 +429,7 @@ __device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsig
 }
 template <bool TRAIN>
 __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
+  TGNX_STAMP(2);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int sh[40];
   const int B = (int)c.ctl[TGNX_CTL_B];
@@ -902,6 +904,7 @@ __device__ float store_tmax(const Ctx& c, int64_t u, int lane) {
 // aggregation over a node list (eval update / flush; list == nullptr: nodes base + m).
 __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, const int64_t* list,
                                                     const int* list_cnt, int n_host, int64_t base) {
+  TGNX_STAMP(3);
   if (mode != 2) {
     const int B = (int)c.ctl[TGNX_CTL_B];
     if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
@@ -1175,6 +1178,7 @@ __device__ __forceinline__ float att_keep(const Ctx& c, uint64_t seed, int x, in
 constexpr int ATT_EB = 16;  // edges whose neighbour rows are loaded in one batch (ring K <= 32: <= 2 batches)
 template <bool TRAIN>
 __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
+  TGNX_STAMP(4);
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int R = c.cnt[c.rsel];
@@ -1258,6 +1262,7 @@ __device__ __forceinline__ int root_row(const Ctx& c, int64_t v) {
 // evs row: zs | zp | zn | dhp | dhn | hp | hn (D each) | a_p a_n s_p s_n da_p da_n loss pad
 __host__ __device__ inline int evs_stride(int D) { return 7 * D + 8; }
 __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c) {
+  TGNX_STAMP(5);
   __shared__ float z[3][TDMAX];
   __shared__ float part[4][3][TDMAX];
   __shared__ float dh[2][TDMAX];
@@ -1414,6 +1419,7 @@ __device__ void lp_vec_body(const Ctx& c, int y, int lane) {
 // wiki-shaped hub user sits in ~40 % of the page rings), and per-edge global atomics on its row
 // serialised at the L2 (attn_bwd 36 us, 15 us without them).
 __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
+  TGNX_STAMP(6);
   if ((int)blockIdx.x >= ncb) {
     lp_vec_body(c, ((int)blockIdx.x - ncb) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
     return;
@@ -1937,6 +1943,7 @@ struct TeReduceTail {
 
 // ------------------------------------------------------------------ optimizer + state update
 __global__ void __launch_bounds__(256) tgn_adam(Ctx c) {
+  TGNX_STAMP(7);
   __shared__ float sc[2];
   const int64_t B = c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
@@ -2842,6 +2849,41 @@ int tgnx_tgn_flush(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void
   tgn_clear_store<<<gridn(c.N, 256), 256, 0, s>>>(c.st, c.N);
   TGNX_LAUNCH_CHECK("tgn_clear_store");
   return TGNX_OK;
+}
+
+
+// wave timeline stamps (diagnostic build, see tgnx_common.h)
+int tgnx_stamps_set(void* buf, uint32_t cap) {
+#ifdef TGNX_STAMPS
+  StampRec* b = reinterpret_cast<StampRec*>(buf);
+  const unsigned per = cap / 64;
+  static unsigned z[64 * 32];
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_buf), &b, sizeof b) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_cap), &per, sizeof per) != hipSuccess ||
+      hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_cnt), z, sizeof z) != hipSuccess) {
+    set_error("tgnx_stamps_set: symbol copy failed");
+    return TGNX_EHIP;
+  }
+  return TGNX_OK;
+#else
+  (void)buf;
+  (void)cap;
+  set_error("tgnx_stamps_set: library built without TGNX_STAMPS");
+  return TGNX_EINVAL;
+#endif
+}
+
+// records per shard (64 shards of cap / 64 records each; shard s holds records [s * cap/64, ...))
+int64_t tgnx_stamps_count(void) {
+#ifdef TGNX_STAMPS
+  unsigned n[64 * 32];
+  if (hipMemcpyFromSymbol(n, HIP_SYMBOL(g_stamp_cnt), sizeof n) != hipSuccess) return -1;
+  unsigned mx = 0;
+  for (int s = 0; s < 64; ++s) mx = n[s * 32] > mx ? n[s * 32] : mx;
+  return mx;
+#else
+  return -1;
+#endif
 }
 
 }  // extern "C"

@@ -1,0 +1,507 @@
+// GEMM lab (not part of libtgnx): times candidate fp32 MFMA GEMM cores at the TGN step's shapes in
+// isolation, each launch inside a captured graph of back-to-back launches (the step's setting).
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I tgb-tgn-dgl_amd/csrc tools/gemm_lab.hip -o build_var/gemm_lab
+// Shapes: the GRU GEMM (A = gathered [X | memory] rows, M ~ 415, N = 4D = 400, K = 572) and lin_edge
+// (M ~ 1415, N = 100, K = 272).  A is gathered by a row index (two-phase loader), B is a weight matrix.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "tgnx_gemm.h"
+
+namespace tgnx {
+void set_error(const char*, ...) {}
+}
+using namespace tgnx;
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e = (x);                                                              \
+    if (e != hipSuccess) {                                                           \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));       \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+// A(m, k) = X[idx[m]][k] (two-phase gather, row index hoisted)
+struct LoadGather {
+  const float* X;
+  const int* idx;
+  int K;
+  static constexpr bool k_fast = true;
+  using Idx = int;
+  static constexpr bool row_idx = true;
+  __device__ Idx index(int m, int) const { return idx[m]; }
+  __device__ float load(Idx v, int, int k) const { return X[(int64_t)v * K + k]; }
+};
+
+// ------------------------------------------------------------------ candidate: wave-split-K, registers
+// One TMxTN tile per workgroup; wave w owns the 16-deep k-slabs w, w + 4, ...; operands go straight from
+// global memory to registers in the MFMA layout (lane (li, lk) of 16x16x4 step q takes k = 4 lk + q), PD
+// slabs in flight; no LDS or barrier in the K loop; the four waves' partial tiles are summed through LDS
+// in wave order at the end.
+template <int TM, int TN, int PD, class AL, class BL, class EPI>
+__global__ void __launch_bounds__(256) gemmw_kernel(GemmShape g, AL al, BL bl, EPI epi) {
+  constexpr int FM = TM / 16, FN = TN / 16, PB = TN + 1;
+  __shared__ __attribute__((aligned(16))) float red[4 * TM * PB + TM * PB + 512];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, lk = lane >> 4;
+  const int Mr = g.Mdev ? min(*g.Mdev, g.M) : g.M, Nr = g.N, Kr = g.K;
+  const int tnr = (Nr + TN - 1) / TN, tmr = (Mr + TM - 1) / TM;
+  const int tiles = tmr * tnr;
+  for (int t = blockIdx.x; t < tiles; t += gridDim.x) {
+    const int m0 = (t / tnr) * TM, n0 = (t % tnr) * TN;
+    using TA = LoaderTraits<AL>;
+    using TB = LoaderTraits<BL>;
+    typename TA::Idx ia[FM];
+    typename TB::Idx ib[FN];
+    const int mlast = Mr - 1, nlast = Nr - 1, klast = Kr - 1;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) ia[i] = TA::index(al, min(m0 + 16 * i + li, mlast), 0);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) ib[j] = TB::index(bl, min(n0 + 16 * j + li, nlast), 0);
+    const int nslab = (Kr + 15) >> 4;
+    const int nmy = nslab > wv ? (nslab - wv + 3) >> 2 : 0;  // slabs of this wave
+    f32x4_t acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+    float ra[PD][FM][4], rb[PD][FN][4];
+    auto fetch = [&](int p, int s) {  // slab s of this wave (clamped: a valid slab is always loaded)
+      const int k0 = 16 * (wv + 4 * min(s, max(nmy - 1, 0)));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          ra[p][i][q] = TA::load(al, ia[i], min(m0 + 16 * i + li, mlast), min(k0 + 4 * lk + q, klast));
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          rb[p][j][q] = TB::load(bl, ib[j], min(n0 + 16 * j + li, nlast), min(k0 + 4 * lk + q, klast));
+    };
+    auto mfma = [&](int p, int s) {
+      const int k0 = 16 * (wv + 4 * s);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float km = f01(k0 + 4 * lk + q <= klast);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[p][i][q] * km, rb[p][j][q], acc[i][j], 0, 0, 0);
+      }
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p) fetch(p, p);
+    for (int s0 = 0; s0 < nmy; s0 += PD) {
+#pragma unroll
+      for (int p = 0; p < PD; ++p) {
+        if (s0 + p < nmy) mfma(p, s0 + p);
+        fetch(p, s0 + p + PD);
+      }
+    }
+    float* mine = red + wv * TM * PB;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mine[(16 * i + 4 * lk + r) * PB + 16 * j + li] = acc[i][j][r];
+    __syncthreads();
+    float* Ct = red + 4 * TM * PB;
+    for (int x = tid; x < TM * TN; x += 256) {
+      const int r = x / TN, cc = x % TN, o = r * PB + cc;
+      Ct[o] = ((red[o] + red[TM * PB + o]) + red[2 * TM * PB + o]) + red[3 * TM * PB + o];
+    }
+    __syncthreads();
+    epi(GemmTile<TM, TN>{Ct, m0, n0, Mr, Nr, Ct + TM * PB});
+    __syncthreads();
+  }
+}
+
+
+// ------------------------------------------------------------------ candidate: base core, 16-B loads
+// As gemm_tile, but k-fast operands are fetched 4 consecutive k per lane (global_load_dwordx4) and stashed
+// with ds_write_b128.  Loader: `float4 load4(Idx, r, k)` (k % 4 == 0, the 4 elements contiguous, 16-B
+// aligned, in bounds).
+struct LoadGather4 : LoadGather {
+  __device__ float4 load4(Idx v, int, int k) const { return *reinterpret_cast<const float4*>(X + (int64_t)v * K + k); }
+};
+struct LoadRowK4 : LoadRowK {
+  using Idx = int;
+  static constexpr bool row_idx = true;
+  __device__ Idx index(int, int) const { return 0; }
+  __device__ float load(Idx, int r, int k) const { return p[(int64_t)r * ld + k]; }
+  __device__ float4 load4(Idx, int r, int k) const { return *reinterpret_cast<const float4*>(p + (int64_t)r * ld + k); }
+};
+template <class CFG, bool UNC, bool SB, class AL, class BL, class EPI>
+__global__ void __launch_bounds__(256) gemm4_kernel(GemmShape g, AL al, BL bl, EPI epi) {
+  constexpr int TM = CFG::TM, TN = CFG::TN, KC = CFG::KC, FM = CFG::FM, FN = CFG::FN;
+  constexpr int PK = CFG::PK, PB = CFG::PB, PF = CFG::PF;
+  constexpr int VA = TM * KC / 1024, VB = TN * KC / 1024;  // float4 per thread per chunk
+  __shared__ __attribute__((aligned(16))) float smem[CFG::SMEM];
+  float* As = smem;
+  float* Bs = smem + TM * PK;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const GemmRt rt = gemm_runtime<CFG>(g);
+  const int tmr = (rt.Mr + TM - 1) / TM, tnr = (rt.Nr + TN - 1) / TN;
+  const int per = (tmr * tnr + 7) >> 3, grid = gridDim.x;
+  for (int vb = blockIdx.x; vb < 8 * per; vb += grid) {
+    const GemmWork wk = gemm_work<TM, TN>(g, rt.Mr, rt.Nr, 1, vb);
+    const int m0 = wk.tm * TM, n0 = wk.tn * TN;
+    if (!wk.ok || m0 >= rt.Mr || n0 >= rt.Nr) continue;
+    const int wr = (wv >> 1) * (TM / 2), wc = (wv & 1) * (TN / 2);
+    const int li = lane & 15, lk = lane >> 4;
+    f32x4_t acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+    using TA = LoaderTraits<AL>;
+    using TB = LoaderTraits<BL>;
+    typename TA::Idx ia[VA];
+    typename TB::Idx ib[VB];
+    const int mlast = rt.Mr - 1, nlast = rt.Nr - 1;
+    const int k4last = (rt.Kr - 1) & ~3;  // last in-bounds 4-group start (rows padded to a multiple of 4)
+#pragma unroll
+    for (int i = 0; i < VA; ++i) {
+      const int x = tid + 256 * i, r = x / (KC / 4);
+      ia[i] = TA::index(al, min(m0 + r, mlast), 0);
+    }
+#pragma unroll
+    for (int i = 0; i < VB; ++i) {
+      const int x = tid + 256 * i, r = x / (KC / 4);
+      ib[i] = TB::index(bl, min(n0 + r, nlast), 0);
+    }
+    float4 ra[PF][VA], rb[PF][VB];
+    auto fetch = [&](float4* fa, float4* fb, int ch) {
+      const int k0 = ch * KC;
+#pragma unroll
+      for (int i = 0; i < VA; ++i) {
+        const int x = tid + 256 * i, r = x / (KC / 4), kk = 4 * (x % (KC / 4));
+        fa[i] = al.load4(ia[i], min(m0 + r, mlast), min(k0 + kk, k4last));
+      }
+#pragma unroll
+      for (int i = 0; i < VB; ++i) {
+        const int x = tid + 256 * i, r = x / (KC / 4), kk = 4 * (x % (KC / 4));
+        fb[i] = bl.load4(ib[i], min(n0 + r, nlast), min(k0 + kk, k4last));
+      }
+    };
+    auto stash = [&](const float4* fa, const float4* fb, int ch) {
+      const int kc = max(0, min(KC, rt.Kr - ch * KC));
+#pragma unroll
+      for (int i = 0; i < VA; ++i) {
+        const int x = tid + 256 * i, r = x / (KC / 4), kk = 4 * (x % (KC / 4));
+        const bool rok = m0 + r <= mlast;
+        *reinterpret_cast<f32x4_t*>(As + r * PK + kk) =
+            f32x4_t{(rok && kk < kc) ? fa[i].x : 0.f, (rok && kk + 1 < kc) ? fa[i].y : 0.f,
+                    (rok && kk + 2 < kc) ? fa[i].z : 0.f, (rok && kk + 3 < kc) ? fa[i].w : 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < VB; ++i) {
+        const int x = tid + 256 * i, r = x / (KC / 4), kk = 4 * (x % (KC / 4));
+        const bool rok = n0 + r <= nlast;
+        *reinterpret_cast<f32x4_t*>(Bs + r * PK + kk) =
+            f32x4_t{(rok && kk < kc) ? fb[i].x : 0.f, (rok && kk + 1 < kc) ? fb[i].y : 0.f,
+                    (rok && kk + 2 < kc) ? fb[i].z : 0.f, (rok && kk + 3 < kc) ? fb[i].w : 0.f};
+      }
+    };
+    auto slab = [&](int kk, f32x4_t* a, f32x4_t* b) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const f32x4_t*>(As + (wr + 16 * i + li) * PK + kk + 4 * lk);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const f32x4_t*>(Bs + (wc + 16 * j + li) * PK + kk + 4 * lk);
+    };
+    f32x4_t acc2[FM][FN];  // second accumulator chain (odd slabs): halves the dependent MFMA latency
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc2[i][j] = {0.f, 0.f, 0.f, 0.f};
+    auto mfma_chunk = [&]() {
+      f32x4_t a[2][FM], b[2][FN];
+      slab(0, a[0], b[0]);
+#pragma unroll
+      for (int it = 0; it < KC / 16; ++it) {
+        const int cur = it & 1;
+        if (it + 1 < KC / 16) slab(16 * (it + 1), a[cur ^ 1], b[cur ^ 1]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+              if (q & 1) acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][i][q], b[cur][j][q], acc2[i][j], 0, 0, 0);
+              else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur][i][q], b[cur][j][q], acc[i][j], 0, 0, 0);
+            }
+      }
+    };
+    const int last = max(rt.nchunk, 1);
+    if constexpr (UNC) {  // unconditional pipeline: every stage loads (clamped chunk) and multiplies
+#pragma unroll
+      for (int p = 0; p < PF; ++p) fetch(ra[p], rb[p], min(p, last - 1));
+      for (int c0 = 0; c0 < last; c0 += PF) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+          const int ch = c0 + p;
+          stash(ra[p], rb[p], ch);  // ch >= last: kc = 0, zeros
+          __syncthreads();
+          fetch(ra[p], rb[p], min(ch + PF, last - 1));
+          if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+          mfma_chunk();
+          if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+          __syncthreads();
+        }
+      }
+    } else {
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+      if (p < last) fetch(ra[p], rb[p], p);
+    for (int c0 = 0; c0 < last; c0 += PF) {
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        const int ch = c0 + p;
+        if (ch < last) {
+          stash(ra[p], rb[p], ch);
+          __syncthreads();
+          if (ch + PF < last) fetch(ra[p], rb[p], ch + PF);
+          mfma_chunk();
+          __syncthreads();
+        }
+      }
+    }
+    }
+    float* Ct = smem;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Ct[(wr + 16 * i + lk * 4 + r) * PB + wc + 16 * j + li] = acc[i][j][r] + acc2[i][j][r];
+    __syncthreads();
+    epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, smem + TM * PB});
+    __syncthreads();
+  }
+}
+
+// ---- per-workgroup timeline: {start, end} (s_memrealtime, 100 MHz), HW_ID, XCC_ID
+struct Stamp {
+  unsigned long long t0, t1;
+  unsigned hw, xcc;
+};
+__device__ __forceinline__ void stamp_begin(unsigned long long& t0) { t0 = __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void stamp_end(Stamp* st, unsigned long long t0) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Stamp s;
+    s.t0 = t0;
+    s.t1 = __builtin_amdgcn_s_memrealtime();
+    s.hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    s.xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    st[blockIdx.x] = s;
+  }
+}
+template <class C1, class C2, class AL1, class BL1, class EP1, class AL2, class BL2, class EP2>
+__global__ void __launch_bounds__(256) gemm2_stamp(GemmShape g1, AL1 a1, BL1 b1, EP1 e1, GemmShape g2, AL2 a2, BL2 b2,
+                                                   EP2 e2, Stamp* st) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  unsigned long long t0;
+  stamp_begin(t0);
+  const int n1 = gemm_blocks(g1);
+  if ((int)blockIdx.x < n1) gemm_body<C1>(g1, a1, b1, e1, nullptr, blockIdx.x, smem);
+  else gemm_body<C2>(g2, a2, b2, e2, nullptr, blockIdx.x - n1, smem);
+  stamp_end(st, t0);
+}
+
+__global__ void empty_kernel(int* p) {
+  if (p && threadIdx.x == 1000) p[0] = 1;
+}
+
+__global__ void ref_gemm(const float* X, const int* idx, const float* W, float* C, int M, int N, int K) {
+  const int m = blockIdx.y, n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double s = 0;
+  for (int k = 0; k < K; ++k) s += (double)X[(int64_t)idx[m] * K + k] * W[(int64_t)n * K + k];
+  C[(int64_t)m * N + n] = (float)s;
+}
+
+template <class F>
+static float time_graph(F launch, hipStream_t st, int reps = 20, int iters = 30) {
+  hipGraph_t gr;
+  hipGraphExec_t ex;
+  CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+  for (int r = 0; r < reps; ++r) launch();
+  CK(hipStreamEndCapture(st, &gr));
+  CK(hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0));
+  for (int w = 0; w < 3; ++w) CK(hipGraphLaunch(ex, st));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0, st));
+  for (int i = 0; i < iters; ++i) CK(hipGraphLaunch(ex, st));
+  CK(hipEventRecord(e1, st));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  CK(hipGraphExecDestroy(ex));
+  CK(hipGraphDestroy(gr));
+  return ms * 1e3f / (reps * iters);
+}
+
+int main(int argc, char** argv) {
+  struct Shape {
+    const char* name;
+    int M, N, K, rows;
+  };
+  const Shape shapes[] = {{"gru", 415, 400, 572, 9227}, {"lin_edge", 1415, 100, 272, 200000}, {"dz0", 415, 100, 400, 415}};
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  {
+    const float us = time_graph([&] { empty_kernel<<<256, 256, 0, st>>>(nullptr); }, st);
+    printf("empty kernel (256 WGs): %.2f us per launch\n", us);
+    const float us1 = time_graph([&] { empty_kernel<<<1, 64, 0, st>>>(nullptr); }, st);
+    printf("empty kernel (1 WG): %.2f us per launch\n", us1);
+  }
+  for (const Shape& sh : shapes) {
+    const int M = sh.M, N = sh.N, K = sh.K;
+    std::vector<float> hX((size_t)sh.rows * K), hW((size_t)N * K);
+    std::vector<int> hidx(M);
+    srand(1);
+    for (auto& v : hX) v = (rand() / (float)RAND_MAX) - 0.5f;
+    for (auto& v : hW) v = (rand() / (float)RAND_MAX) - 0.5f;
+    for (int m = 0; m < M; ++m) hidx[m] = (int)(((int64_t)m * 7919 + 13) % sh.rows);
+    float *X, *W, *C, *Cref;
+    int* idx;
+    CK(hipMalloc(&X, hX.size() * 4));
+    CK(hipMalloc(&W, hW.size() * 4));
+    CK(hipMalloc(&C, (size_t)M * N * 4));
+    CK(hipMalloc(&Cref, (size_t)M * N * 4));
+    CK(hipMalloc(&idx, M * 4));
+    CK(hipMemcpy(X, hX.data(), hX.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(W, hW.data(), hW.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(idx, hidx.data(), M * 4, hipMemcpyHostToDevice));
+    ref_gemm<<<dim3((N + 63) / 64, M), 64, 0, st>>>(X, idx, W, Cref, M, N, K);
+    CK(hipStreamSynchronize(st));
+    std::vector<float> href((size_t)M * N), hc((size_t)M * N);
+    CK(hipMemcpy(href.data(), Cref, href.size() * 4, hipMemcpyDeviceToHost));
+    const LoadGather al{X, idx, K};
+    const LoadRowK bl{W, N, K, K};
+    const EpiStore epi{C, nullptr, N, 0};
+    auto check = [&](const char* name, float us) {
+      CK(hipMemcpy(hc.data(), C, hc.size() * 4, hipMemcpyDeviceToHost));
+      double md = 0;
+      for (size_t i = 0; i < hc.size(); ++i) md = std::max(md, (double)fabsf(hc[i] - href[i]));
+      printf("%-9s %-34s %7.2f us  %6.2f TFLOP/s  maxdiff %.2e\n", sh.name, name, us, 2.0 * M * N * K / us / 1e6, md);
+      CK(hipMemset(C, 0, (size_t)M * N * 4));
+    };
+    auto base = [&](auto cfg, const char* name) {
+      using CFG = decltype(cfg);
+      const GemmShape g = gemm_shape<CFG>(M, N, K);
+      const float us = time_graph([&] { gemm_kernel<CFG><<<gemm_blocks(g), 256, 0, st>>>(g, al, bl, epi, nullptr); }, st);
+      check(name, us);
+    };
+    base(GemmCfg<32, 32, 64, 1>{}, "base 32x32 KC64 PF1");
+    base(GemmCfg<32, 32, 32, 2>{}, "base 32x32 KC32 PF2");
+    base(GemmCfg<32, 32, 128, 1>{}, "base 32x32 KC128 PF1");
+    const LoadGather4 al4{{X, idx, K}};
+    const LoadRowK4 bl4{{W, N, K, K}};
+    auto v4 = [&](auto cfg, const char* name) {
+      using CFG = decltype(cfg);
+      const GemmShape g = gemm_shape<CFG>(M, N, K);
+      const float us = time_graph([&] { gemm4_kernel<CFG, false, false><<<gemm_blocks(g), 256, 0, st>>>(g, al4, bl4, epi); }, st);
+      check(name, us);
+      const float u2 = time_graph([&] { gemm4_kernel<CFG, true, false><<<gemm_blocks(g), 256, 0, st>>>(g, al4, bl4, epi); }, st);
+      char nm[64];
+      snprintf(nm, sizeof nm, "%s unc", name);
+      check(nm, u2);
+      const float u3 = time_graph([&] { gemm4_kernel<CFG, true, true><<<gemm_blocks(g), 256, 0, st>>>(g, al4, bl4, epi); }, st);
+      snprintf(nm, sizeof nm, "%s unc+sb", name);
+      check(nm, u3);
+    };
+    if (K % 4 == 0) {
+      v4(GemmCfg<32, 32, 64, 1>{}, "v4 32x32 KC64 PF1");
+      v4(GemmCfg<32, 32, 64, 2>{}, "v4 32x32 KC64 PF2");
+      v4(GemmCfg<32, 32, 128, 1>{}, "v4 32x32 KC128 PF1");
+      v4(GemmCfg<32, 32, 128, 2>{}, "v4 32x32 KC128 PF2");
+      v4(GemmCfg<32, 32, 32, 4>{}, "v4 32x32 KC32 PF4");
+      v4(GemmCfg<32, 32, 64, 3>{}, "v4 32x32 KC64 PF3");
+      v4(GemmCfg<32, 32, 32, 2>{}, "v4 32x32 KC32 PF2");
+    }
+    auto wsk = [&](auto tm, auto tn, auto pd, const char* name) {
+      constexpr int TM = decltype(tm)::value, TN = decltype(tn)::value, PD = decltype(pd)::value;
+      const GemmShape g = gemm_shape<GemmCfg<32, 32, 64>>(M, N, K);
+      const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN);
+      const float us = time_graph([&] { gemmw_kernel<TM, TN, PD><<<tiles, 256, 0, st>>>(g, al, bl, epi); }, st);
+      check(name, us);
+    };
+    using I16 = std::integral_constant<int, 16>;
+    using I32 = std::integral_constant<int, 32>;
+    using I64 = std::integral_constant<int, 64>;
+    wsk(I32{}, I32{}, std::integral_constant<int, 2>{}, "wsplitK 32x32 PD2");
+    CK(hipFree(X));
+    CK(hipFree(W));
+    CK(hipFree(C));
+    CK(hipFree(Cref));
+    CK(hipFree(idx));
+  }
+
+  // ---- GRU || lin_edge in one launch: does the dispatcher pile workgroups onto a few CUs?
+  {
+    const int M1 = 415, N1 = 400, K1 = 572, R1 = 9227, M2 = 1415, N2 = 100, K2 = 272, R2 = 200000;
+    float *X1, *W1, *C1, *X2, *W2, *C2;
+    int *i1, *i2;
+    CK(hipMalloc(&X1, (size_t)R1 * K1 * 4)); CK(hipMalloc(&W1, (size_t)N1 * K1 * 4)); CK(hipMalloc(&C1, (size_t)M1 * N1 * 4));
+    CK(hipMalloc(&X2, (size_t)R2 * K2 * 4)); CK(hipMalloc(&W2, (size_t)N2 * K2 * 4)); CK(hipMalloc(&C2, (size_t)M2 * N2 * 4));
+    CK(hipMalloc(&i1, M1 * 4)); CK(hipMalloc(&i2, M2 * 4));
+    CK(hipMemset(X1, 0, (size_t)R1 * K1 * 4)); CK(hipMemset(W1, 0, (size_t)N1 * K1 * 4));
+    CK(hipMemset(X2, 0, (size_t)R2 * K2 * 4)); CK(hipMemset(W2, 0, (size_t)N2 * K2 * 4));
+    std::vector<int> h1(M1), h2(M2);
+    for (int m = 0; m < M1; ++m) h1[m] = (int)(((int64_t)m * 7919 + 13) % R1);
+    for (int m = 0; m < M2; ++m) h2[m] = (int)(((int64_t)m * 104729 + 7) % R2);
+    CK(hipMemcpy(i1, h1.data(), M1 * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(i2, h2.data(), M2 * 4, hipMemcpyHostToDevice));
+    using C = GemmCfg<32, 32, 64, 1>;
+    const GemmShape g1 = gemm_shape<C>(M1, N1, K1), g2 = gemm_shape<C>(M2, N2, K2);
+    const LoadGather a1{X1, i1, K1}, a2{X2, i2, K2};
+    const LoadRowK b1{W1, N1, K1, K1}, b2{W2, N2, K2, K2};
+    const EpiStore e1{C1, nullptr, N1, 0}, e2{C2, nullptr, N2, 0};
+    const int nb1 = gemm_blocks(g1), nb2 = gemm_blocks(g2), nb = nb1 + nb2;
+    Stamp* st_d;
+    CK(hipMalloc(&st_d, nb * sizeof(Stamp)));
+    std::vector<Stamp> hs(nb);
+    auto kern = gemm2_stamp<C, C, LoadGather, LoadRowK, EpiStore, LoadGather, LoadRowK, EpiStore>;
+    CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    for (int lds_kb : {18, 40, 80, 150}) {
+      const size_t lds = (size_t)lds_kb * 1024;
+      for (int which = 0; which < 3; ++which) {  // 0: both, 1: GRU only, 2: lin_edge only
+        const GemmShape z = gemm_shape<C>(0, 1, 1);
+        const GemmShape ga = which == 2 ? z : g1, gb = which == 1 ? z : g2;
+        const int n = gemm_blocks(ga) + gemm_blocks(gb);
+        const float us = time_graph([&] { kern<<<n, 256, lds, st>>>(ga, a1, b1, e1, gb, a2, b2, e2, st_d); }, st);
+        kern<<<n, 256, lds, st>>>(ga, a1, b1, e1, gb, a2, b2, e2, st_d);
+        CK(hipStreamSynchronize(st));
+        CK(hipMemcpy(hs.data(), st_d, n * sizeof(Stamp), hipMemcpyDeviceToHost));
+        unsigned long long tmin = ~0ull, tmax = 0, smax = 0;
+        double dsum = 0, dmax = 0;
+        std::vector<int> cu(4096, 0);
+        for (int b = 0; b < n; ++b) {
+          tmin = std::min(tmin, hs[b].t0); tmax = std::max(tmax, hs[b].t1); smax = std::max(smax, hs[b].t0);
+          const double d = (hs[b].t1 - hs[b].t0) * 0.01;
+          dsum += d; dmax = std::max(dmax, d);
+          const unsigned h = hs[b].hw, key = ((hs[b].xcc & 7) << 9) | (((h >> 13) & 7) << 6) | (((h >> 12) & 1) << 5) | ((h >> 8) & 15);
+          cu[key]++;
+        }
+        int used = 0, mx = 0;
+        for (int v : cu) { used += v > 0; mx = std::max(mx, v); }
+        printf("gru||edge lds %3d KB %-9s %3d WGs: graph %6.2f us | span %5.2f us, last start +%5.2f, WG dur avg %5.2f max %5.2f | CUs used %3d, max WGs/CU %d\n",
+               lds_kb, which == 0 ? "both" : which == 1 ? "gru" : "lin_edge", n, us, (tmax - tmin) * 0.01, (smax - tmin) * 0.01,
+               dsum / n, dmax, used, mx);
+      }
+    }
+  }
+  return 0;
+}
