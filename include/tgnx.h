@@ -327,13 +327,22 @@ int tgnx_tgn_train_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf,
                         void* stream);
 /* tgnx_tgn_train_step of the next batch of a resident split, with the batch cursor folded in: the
  * same as tgnx_tgnn_advance(ctl, mode 1, ..., split_lo, split_hi, batch, rank, world, base_seed,
- * train 1) followed by tgnx_tgn_train_step(gen_neg 1), one launch fewer (the step counters NB / GEN /
- * ADAM_T advance in the step's last launch).  World 1 (Adam is folded in as well). */
+ * train 1) followed by tgnx_tgn_train_step(gen_neg 1), one launch fewer.  World 1 only (Adam is folded
+ * in as well; world > 1 is refused), split_hi <= num_events.
+ * ctl words, in stream order: the step's first launch writes the batch descriptor (BATCH_START, B,
+ * CUR_EID, LO, HI, SEED) from the unchanged counters; the step's LAST launch advances NB, GEN and (when
+ * B > 0) ADAM_T.  So once the call's work has completed, ctl equals what advance + step leave; between
+ * the two (e.g. a kernel of the caller's own, enqueued in between) the counters still hold the previous
+ * step's values, whereas tgnx_tgnn_advance has already advanced them. */
 int tgnx_tgn_train_step_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
                                  int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
                                  int32_t dropout, void* stream);
 /* Data parallel form: tgnx_tgn_train_fwd_bwd with the folded cursor (the exchange, tgnx_tgn_apply_rows and
- * tgnx_tgn_train_update follow; the counters have advanced when train_update reads ADAM_T). */
+ * tgnx_tgn_train_update follow).  ctl words as for tgnx_tgn_train_step_resident: the descriptor is written
+ * by the first launch, NB / GEN / ADAM_T advance in the last launch of THIS call, so they have advanced
+ * by the time the exchange and tgnx_tgn_train_update (which reads ADAM_T) run — the same values the
+ * advance + fwd_bwd path gives them.  Test: tests/test_gpu_tgn_dp.py (per rank, folded vs advance +
+ * fwd_bwd). */
 int tgnx_tgn_train_fwd_bwd_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
                                     int64_t split_hi, int64_t batch, int32_t rank, int32_t world,
                                     uint64_t base_seed, int32_t dropout, void* stream);

@@ -79,3 +79,83 @@ def test_tgn_data_parallel_matches_single(aggr, layers):
             (st, float((r0.model.memory.memory - e1.model.memory.memory).abs().max()))
         assert torch.equal(r0.model.store, e1.model.store), st
         assert torch.equal(r0.loader.neighbors, e1.loader.neighbors) and torch.equal(r0.loader.e_id, e1.loader.e_id)
+
+
+def _rel(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def test_tgn_dp_resident_folded_cursor_per_rank():
+    """Data-parallel resident steps (world = 2, one device) with the batch cursor folded into the first
+    launch (tgnx_tgn_train_fwd_bwd_resident) against tgnx_tgnn_advance + tgnx_tgn_train_fwd_bwd, per rank,
+    through the summing exchange, apply_rows and Adam (lr 1e-3, so an ADAM_T off by one shows in the
+    parameters): ctl words, the rank's negatives, gradients and packed memory rows after fwd_bwd; memory,
+    last_update, parameters and moments after the update.  The split ends with a partial batch (20
+    events) and the last step runs one batch past the split (B = 0: nothing may change).  Parameters
+    and memory are re-synchronised from the unfolded twin after each compared step (the dz atomics make
+    the gradients order-dependent at the last bits)."""
+    from oracle.tgn_ref import RefTGN
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.synth import make_stream
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    N, B, d, D = 400, 64, 16, 32
+    s = make_stream("tgbl-wiki", seed=9, num_events=B * 9, num_nodes=N, msg_dim=d)
+    torch.manual_seed(0)
+    sd = RefTGN(N, d, hidden=D, aggr="last", dropout=0.1).state_dict()
+    dev = torch.device("cuda")
+    ev = dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32), msg=s.msg)
+    split_hi = 7 * B + 20
+    eng = {}
+    for fold in (True, False):
+        for rank in (0, 1):
+            model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=1, aggr="last", dropout=0.1)
+            model.load_reference_state(sd)
+            e = TgnEngine(model, LastNeighborLoader(N, 10, device=dev), ev, TgnAdam(model, 1e-3),
+                          dst_nodes=s.dst_nodes, seed=77, rank=rank, world=2)
+            e.fold_cursor = fold
+            e.bind_resident(0, split_hi, B, dropout=True)
+            e.begin_epoch()
+            eng[fold, rank] = e
+    for st in range(9):
+        for e in eng.values():
+            e._pre()
+        torch.cuda.synchronize()
+        for e in eng.values():
+            e.check()
+        for rank in (0, 1):
+            f, u = eng[True, rank], eng[False, rank]
+            for w in (0, 1, 2, 3, 4, 7, 8, 9, 10):   # start, cur e_id, B, GEN, ADAM_T, LO, HI, SEED, NB
+                assert int(f.ctl[w]) == int(u.ctl[w]), (st, rank, w, int(f.ctl[w]), int(u.ctl[w]))
+            Bst = int(u.ctl[2])
+            assert Bst == (B if st < 7 else 20 if st == 7 else 0), (st, Bst)
+            assert torch.equal(f.neg_train, u.neg_train), (st, rank)
+            G = f.model.grad_flat.numel()
+            if Bst:
+                assert _rel(f.comm[:G - 1], u.comm[:G - 1]) < 1e-5, (st, rank)
+                assert abs(float(f.comm[G - 1]) - float(u.comm[G - 1])) < 1e-5, (st, rank)
+            assert torch.equal(f.xrows, u.xrows), (st, rank)  # node headers and GRU rows (deterministic GEMM)
+        # the exchange (all-reduce = sum over ranks), per twin set
+        for fold in (True, False):
+            tot = eng[fold, 0].comm + eng[fold, 1].comm
+            for rank in (0, 1):
+                eng[fold, rank].comm.copy_(tot)
+        for e in eng.values():
+            e._post()
+        torch.cuda.synchronize()
+        for rank in (0, 1):
+            f, u = eng[True, rank], eng[False, rank]
+            fm, um = f.model, u.model
+            assert torch.equal(fm.memory.last_update, um.memory.last_update), (st, rank)
+            assert torch.allclose(fm.memory.memory, um.memory.memory, atol=1e-6), (st, rank)
+            assert _rel(fm.flat, um.flat) < 1e-6, (st, rank)
+            assert _rel(f.adam_m, u.adam_m) < 1e-5 and _rel(f.adam_v, u.adam_v) < 1e-5, (st, rank)
+            assert abs(f.loss_sum() - u.loss_sum()) <= 1e-6 * max(1.0, abs(u.loss_sum())), (st, rank)
+            assert torch.equal(f.loader.e_id, u.loader.e_id) and torch.equal(f.model.store, u.model.store), (st, rank)
+        assert torch.equal(eng[True, 0].model.memory.memory, eng[True, 1].model.memory.memory), st
+        for rank in (0, 1):   # re-synchronise the folded twin
+            f, u = eng[True, rank], eng[False, rank]
+            with torch.no_grad():
+                f.model.flat.copy_(u.model.flat)
+                f.adam_m.copy_(u.adam_m)
+                f.adam_v.copy_(u.adam_v)
+                f.model.memory.memory.copy_(u.model.memory.memory)

@@ -47,21 +47,27 @@ static __device__ unsigned g_stamp_cap;             // records per shard
 static __device__ unsigned g_stamp_cnt[64 * 32];    // 64 shards (by block), one 128-B line each
 struct StampScope {  // wave 0 of each workgroup records
   unsigned long long t0;
-  unsigned kid;
+  unsigned kid, mid = 0;  // two checkpoints: ticks since t0 (16 bits each) at TGNX_STAMP_AT(0 / 1)
   __device__ explicit StampScope(unsigned k) : t0(__builtin_amdgcn_s_memrealtime()), kid(k) {}
+  __device__ void at(int slot) {
+    const unsigned d = (unsigned)min(__builtin_amdgcn_s_memrealtime() - t0, 0xFFFFull);
+    mid = slot ? (mid & 0xFFFFu) | (d << 16) : (mid & 0xFFFF0000u) | d;
+  }
   __device__ ~StampScope() {
     if (threadIdx.x == 0 && g_stamp_buf) {
       const unsigned sh = blockIdx.x & 63, i = atomicAdd(&g_stamp_cnt[sh * 32], 1u);
       if (i < g_stamp_cap)
         g_stamp_buf[(size_t)sh * g_stamp_cap + i] =
             StampRec{t0, __builtin_amdgcn_s_memrealtime(), kid, blockIdx.x,
-                     (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20), 0u};
+                     (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20), mid};
     }
   }
 };
 #define TGNX_STAMP(k) ::tgnx::StampScope tgnx_stamp_scope_(k)
+#define TGNX_STAMP_AT(slot) tgnx_stamp_scope_.at(slot)
 #else
 #define TGNX_STAMP(k)
+#define TGNX_STAMP_AT(slot)
 #endif
 
 // ---------------------------------------------------------------- counter-based RNG

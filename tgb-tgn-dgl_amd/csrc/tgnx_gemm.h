@@ -86,8 +86,10 @@ inline GemmShape gemm_shape_split(int M, int N, int K, const int* Mdev, const in
 // capped: capacities are worst cases (a 2-hop sample is sized for 2e5 rows and runs ~1e3), and
 // dispatching 1e5 workgroups that exit at once cost ~80 us per launch; a workgroup loops over the
 // runtime work in strides of the grid instead (gemm_body).
+// (idle workgroups past the runtime tiles hold dispatch slots: 2048 -> 1024 shortened the step ~7 us on
+// the wiki shape, stamps timeline; 512 lengthened the dW_gru launch, whose ~940 split blocks are all busy)
 #ifndef TGNX_GEMM_GRID_CAP
-#define TGNX_GEMM_GRID_CAP 2048
+#define TGNX_GEMM_GRID_CAP 1024
 #endif
 __host__ __device__ inline int gemm_blocks(const GemmShape& g) {
   const int full = (g.tiles_m * g.tiles_n * g.S + 7) & ~7;

@@ -172,6 +172,7 @@ struct Ctx {
   int64_t* e_id;
   float* e_t;
   float *X, *trel, *lu;
+  int* evr;  // [3 B] centre row of each root (src, dst, neg) of this rank's events (tgn_agg_emit)
   int64_t* xw;
   float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
   float *dZc, *dP, *dE, *dG, *tgp;
@@ -197,6 +198,7 @@ struct Ctx {
   // attention kernels run unchanged on either level.
   int layers;
   int rsel;        // cnt word holding this view's centre count (CNT_R; root view: CNT_R1)
+  int ccap;        // rows of this view's centre arrays (cent_loc; ceoff has ccap + 1): Rcap, root view R1cap
   int att_salt;    // attention-dropout stream (conv: 7, conv2: 9)
   uint32_t* rb;    // roots bitmap
   int* x2r;        // [outer centre] -> root index or -1 (nullptr at layers = 1)
@@ -210,6 +212,13 @@ struct Ctx {
 constexpr int CNT_R1 = 7, CNT_E1 = 8;
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// e / d for 0 <= e < 2^22, 0 < d (inv = 1.0f / d): float estimate, corrected to the exact quotient
+__device__ __forceinline__ int div_small(int e, int d, float inv) {
+  int q = (int)((float)e * inv);
+  q -= q * d > e;
+  q += (q + 1) * d <= e;
+  return q;
+}
 __device__ __forceinline__ float softplusf(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
 
 // ------------------------------------------------------------------ sampling (neighbor_loader.py:26-50)
@@ -893,6 +902,12 @@ __device__ float store_tmax(const Ctx& c, int64_t u, int lane) {
   return wave_max(tb);
 }
 
+// row of a root's embedding: its centre index (2 hops: its root index, via the outer centre)
+__device__ __forceinline__ int root_row(const Ctx& c, int64_t v) {
+  const int x = c.crank[c.assoc[v]];
+  return c.x2r ? c.x2r[x] : x;
+}
+
 // K3: blocks [0, nedge): one wave per (centre x, ring slot j) — the sampled edge record (centre-
 // ascending, ring order = e_id descending, neighbor_loader.py:26-50; output slot = the centre's edge
 // offset + valid slots before j, by ballot) and its Δt encoding (cos -> the lin_edge operand, sin ->
@@ -903,18 +918,32 @@ __device__ float store_tmax(const Ctx& c, int64_t u, int lane) {
 // accumulators, mode 1 last_update of the sampled nodes from the buffer (eval scoring), mode 2
 // aggregation over a node list (eval update / flush; list == nullptr: nodes base + m).
 __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, const int64_t* list,
-                                                    const int* list_cnt, int n_host, int64_t base) {
+                                                    const int* list_cnt, int n_host, int64_t base, int nevb = 0) {
   TGNX_STAMP(3);
   if (mode != 2) {
     const int B = (int)c.ctl[TGNX_CTL_B];
     if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   }
   const int lane = threadIdx.x & 63;
-  if ((int)blockIdx.x < nedge) {
+  if ((int)blockIdx.x < nevb) {  // train: the centre row of every root of this rank's events, so that
+                                 // tgn_pred_train starts from one index load (root_row: assoc -> rank)
+    const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
+    const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+    for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < 3 * (hi - lo); x += nevb * blockDim.x) {
+      const int i = lo + x / 3, r = x % 3;
+      const int64_t* src = r == 0 ? c.ev_src : r == 1 ? c.ev_dst : c.neg;
+      c.evr[x] = root_row(c, src[start + i]);
+    }
+    return;
+  }
+  // then the node part (its workgroups run longest: hub nodes' stores), the sampled-edge part in the last
+  // nedge blocks; both loop over their runtime work in strides of their block count
+  const int nnode = gridDim.x - nedge - nevb;
+  if ((int)blockIdx.x >= nevb + nnode) {
     const int R = c.cnt[CNT_R], K = c.K, D = c.D;
     const float* tw = c.params + c.L.te_w;
     const float* tb = c.params + c.L.te_b;
-    for (int pr = blockIdx.x * 4 + (threadIdx.x >> 6); pr < R * K; pr += nedge * 4) {
+    for (int pr = ((int)blockIdx.x - nevb - nnode) * 4 + (threadIdx.x >> 6); pr < R * K; pr += nedge * 4) {
       const int x = pr / K, j = pr - x * K;
       const int64_t v = c.cent[x];
       const int ls = min(lane, K - 1);
@@ -961,7 +990,7 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
     }
     return;
   }
-  const int bid = blockIdx.x - nedge, nb = gridDim.x - nedge;
+  const int bid = blockIdx.x - nevb, nb = nnode;
   if (mode == 1) {
     const int M = c.cnt[CNT_M];
     for (int x = bid * blockDim.x + threadIdx.x; x < M; x += nb * blockDim.x) c.lu[x] = (float)c.lu_buf[c.nid[x]];
@@ -1132,6 +1161,9 @@ struct LoadZ {
     return *p;
   }
 };
+// row n < 4 HC of the stacked projections [q; k; v; skip] -> (linear g, row r): compares, not an integer
+// division (a ~40-instruction routine per element inside the GEMM loaders' K loop)
+__device__ __forceinline__ int proj_g(int n, int HC) { return (n >= HC) + (n >= 2 * HC) + (n >= 3 * HC); }
 // stacked [W_query; W_key; W_value; W_skip] rows (n / HC selects the linear)
 struct LoadProjW {
   const float* w;  // wq; projection g at w + g * pw
@@ -1139,7 +1171,7 @@ struct LoadProjW {
   int HC, D;
   static constexpr bool k_fast = true;
   __device__ float operator()(int n, int k) const {
-    const int g = n / HC, r = n % HC;
+    const int g = proj_g(n, HC), r = n - g * HC;
     return w[g * pw + (int64_t)r * D + k];
   }
 };
@@ -1154,7 +1186,7 @@ struct EpiProj {
 #pragma unroll
     for (int i = 0; i < T::per; ++i) {
       const int n = t.n0 + T::col_of(i);
-      const int g = n / HC, q = n % HC;
+      const int g = proj_g(n, HC), q = n - g * HC;
       v[i] = t(T::row_of(i), T::col_of(i)) + (n < t.N ? b[g * pb + q] : 0.f);
     }
 #pragma unroll
@@ -1176,24 +1208,84 @@ __device__ __forceinline__ float att_keep(const Ctx& c, uint64_t seed, int x, in
                 c.inv_keep);
 }
 constexpr int ATT_EB = 16;  // edges whose neighbour rows are loaded in one batch (ring K <= 32: <= 2 batches)
+// A centre with 1..ATT_EB edges: the k, v and edge rows of every edge and the centre's skip row are
+// issued as one round (each edge row loaded once for k + e and v + e); same arithmetic as the batched
+// loop of tgn_attn_fwd.
+template <bool TRAIN>
+__device__ __forceinline__ void attn_fwd_one(const Ctx& c, int x, int lane, float on, int l0, const float* Pi,
+                                             float q0, float q1, float sqc, int e0, int ne, int jl) {
+  const int C = c.C, HC = c.HC;
+  float k0[ATT_EB], k1[ATT_EB], v0[ATT_EB], v1[ATT_EB];
+#pragma unroll
+  for (int u = 0; u < ATT_EB; ++u) {
+    const int e = min(u, ne - 1);
+    const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+    const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
+    const float ea = Ee[l0], eb = Ee[C + l0];
+    k0[u] = Pj[HC + l0] + ea;
+    k1[u] = Pj[HC + C + l0] + eb;
+    v0[u] = Pj[2 * HC + l0] + ea;
+    v1[u] = Pj[2 * HC + C + l0] + eb;
+  }
+  const float sk0 = Pi[3 * HC + l0], sk1 = Pi[3 * HC + C + l0];
+  float my0 = -INFINITY, my1 = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < ATT_EB; ++u) {
+    if (u >= ne) break;
+    const float p0 = wave_sum(q0 * k0[u] * on) / sqc, p1 = wave_sum(q1 * k1[u] * on) / sqc;
+    if (lane == u) { my0 = p0; my1 = p1; }
+  }
+  const float mx0 = wave_max(my0), mx1 = wave_max(my1);
+  const float ex0 = lane < ne ? expf(my0 - mx0) : 0.f, ex1 = lane < ne ? expf(my1 - mx1) : 0.f;
+  const float a0 = ex0 / (wave_sum(ex0) + 1e-16f), a1 = ex1 / (wave_sum(ex1) + 1e-16f);
+  float t0 = a0, t1 = a1;
+  if (TRAIN && lane < ne) {
+    c.alpha[(int64_t)(e0 + lane) * 2] = a0;
+    c.alpha[(int64_t)(e0 + lane) * 2 + 1] = a1;
+    if (c.drop) {
+      const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+      t0 *= att_keep(c, seed, x, e0 + lane, 0);
+      t1 *= att_keep(c, seed, x, e0 + lane, 1);
+    }
+  }
+  float o0 = 0.f, o1 = 0.f;
+#pragma unroll
+  for (int u = 0; u < ATT_EB; ++u) {
+    if (u >= ne) break;
+    o0 += v0[u] * __shfl(t0, u, 64);
+    o1 += v1[u] * __shfl(t1, u, 64);
+  }
+  if (lane < C) {
+    c.Zc[(int64_t)x * HC + lane] = o0 + sk0;
+    c.Zc[(int64_t)x * HC + C + lane] = o1 + sk1;
+  }
+}
 template <bool TRAIN>
 __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
   TGNX_STAMP(4);
-  const int B = (int)c.ctl[TGNX_CTL_B];
-  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int R = c.cnt[c.rsel];
   const int lane = threadIdx.x & 63;
   const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (x >= R) return;
+  // one round for the batch descriptor, the centre count and the centre's row / edge range: the centre
+  // arrays hold ccap rows (ceoff ccap + 1), so the read is clamped, and discarded past the runtime count
+  const int xc = min(x, max(c.ccap - 1, 0));
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int64_t err = c.ctl[TGNX_CTL_ERR];
+  const int R = c.cnt[c.rsel];
+  const int i = c.cent_loc[xc];
+  const int e0 = c.ceoff[xc], e1 = c.ceoff[xc + 1];
+  if (B == 0 || err != 0 || x >= R) return;
   const int C = c.C, HC = c.HC;
   const float on = f01(lane < C);
   const int l0 = min(lane, C - 1);
-  const int i = c.cent_loc[x];
   const float* Pi = c.P + (int64_t)i * 4 * HC;
   const float q0 = Pi[l0], q1 = Pi[C + l0];
   const float sqc = sqrtf((float)C);
-  const int e0 = c.ceoff[x], ne = c.ceoff[x + 1] - e0;
+  const int ne = e1 - e0;
   const int jl = c.e_j[e0 + min(lane, max(ne - 1, 0))];   // lane e: the neighbour row of edge e
+  if (ne > 0 && ne <= ATT_EB) {  // every ring of K <= 16: k, v and edge rows of all edges in one round
+    attn_fwd_one<TRAIN>(c, x, lane, on, l0, Pi, q0, q1, sqc, e0, ne, jl);
+    return;
+  }
   float my0 = -INFINITY, my1 = -INFINITY;
   for (int b = 0; b < ne; b += ATT_EB) {
     float k0[ATT_EB], k1[ATT_EB];
@@ -1249,11 +1341,6 @@ __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
   }
 }
 
-// row of a root's embedding: its centre index (2 hops: its root index, via the outer centre)
-__device__ __forceinline__ int root_row(const Ctx& c, int64_t v) {
-  const int x = c.crank[c.assoc[v]];
-  return c.x2r ? c.x2r[x] : x;
-}
 
 // ------------------------------------------------------------------ link prediction (decoder.py:108-123)
 // Workgroup per event of this rank's slice: h = relu(lin_src(z_s) + lin_dst(z_d)), s = sigmoid(lin_final(h)),
@@ -1261,54 +1348,152 @@ __device__ __forceinline__ int root_row(const Ctx& c, int64_t v) {
 // BCEWithLogitsLoss), backward rows, dz rows accumulated into the centres' dZc.
 // evs row: zs | zp | zn | dhp | dhn | hp | hn (D each) | a_p a_n s_p s_n da_p da_n loss pad
 __host__ __device__ inline int evs_stride(int D) { return 7 * D + 8; }
+// Wave roles until the first barrier: wave 0 loads the roots' centre rows (written per event by
+// tgn_agg_emit, in the ctl round) and their Zc rows; waves 1-3 stage lin_src / lin_dst (LDS, pitch D + 1:
+// conflict-free rows and columns)
+// and the bias / output-layer vectors.  vmcnt retires in issue order, so a chain load queued behind the
+// 80 KB of weights in the same wave would wait for all of them; separate waves keep separate queues.
+// (Read from global memory directly, the forward's W[o][k] with lanes over o touched 64 cache lines per
+// load instruction.)
+__host__ __device__ inline size_t tgn_pred_smem(int D) { return (size_t)2 * D * (D + 1) * sizeof(float); }
+constexpr int PRED_SU = 16;  // float4 per staging thread per matrix per round (D <= 110: one round)
 __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c) {
   TGNX_STAMP(5);
-  __shared__ float z[3][TDMAX];
+  extern __shared__ __attribute__((aligned(16))) float Wl[];  // [2][D][DP]: lin_src, lin_dst
+  __shared__ __attribute__((aligned(16))) float z[3][TDMAX];
   __shared__ float part[4][3][TDMAX];
   __shared__ float dh[2][TDMAX];
+  __shared__ float vsb[TDMAX], vdb[TDMAX], vfw[TDMAX + 1];  // lin_src.bias, lin_dst.bias, lin_final (w | b)
+  __shared__ int scr[3];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // D % 8 == 4 (D = 100): unpadded rows are conflict-free both for b128 row reads with lanes over rows
+  // (start banks 4 D o mod 64 distinct over 16 lanes) and for b32 column reads, and the LDS image is the
+  // global one (b128 stores); other D: pitch D + 1, element stores
+  const int D = c.D;
+  const bool flat = D % 8 == 4;
+  const int DP = flat ? D : D + 1;
+  float* Wsrc = Wl;
+  float* Wdst = Wl + D * DP;
   const int B = (int)c.ctl[TGNX_CTL_B];
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    c.cnt[CNT_LIST] = 3 * (hi - lo);
-    if (c.adf.p) {  // fused Adam: this step's scalars for the gradient writers (tgn_adam computes them itself)
-      const int64_t t = c.ctl[TGNX_CTL_ADAM_T] + (c.adv ? 1 : 0);
-      float* sc = reinterpret_cast<float*>(c.ctl + TGNX_CTL_ADAM_SC);
-      sc[0] = (float)(c.lr / (1.0 - pow((double)c.b1, (double)t)));
-      sc[1] = (float)sqrt(1.0 - pow((double)c.b2, (double)t));
-    }
-  }
+  const int64_t err = c.ctl[TGNX_CTL_ERR];
   const int i = lo + blockIdx.x;
-  if (B == 0 || i >= hi || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int D = c.D;
-  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
-  const int64_t roots[3] = {c.ev_src[start + i], c.ev_dst[start + i], c.neg[start + i]};
-  int cr[3];
+  const bool live = !(B == 0 || i >= hi || err != 0);
+  if (wv == 0) {
+    int cr[3];  // the roots' centre rows (tgn_agg_emit) by rank-local event: issued with the ctl loads
 #pragma unroll
-  for (int r = 0; r < 3; ++r) cr[r] = root_row(c, roots[r]);
-  for (int x = tid; x < 3 * D; x += blockDim.x) z[x / D][x % D] = c.Zc[(int64_t)cr[x / D] * D + x % D];
-  __syncthreads();
-  const float* P = c.params;
-  const float* Wsrc = P + c.L.lsw;
-  const float* Wdst = P + c.L.ldw;
-  const int kc = (D + 3) / 4, k0 = wv * kc, nk = min(D - k0, kc);
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {  // lin_src(z_s), lin_dst(z_p), lin_dst(z_n): split contraction
-    const int o = lane + 64 * q;
-    if (o < D) {
-      float a = 0.f, b = 0.f, d2 = 0.f;
-      for (int k = 0; k < nk; ++k) {
-        const float ws = Wsrc[(int64_t)o * D + k0 + k], wd = Wdst[(int64_t)o * D + k0 + k];
-        a += ws * z[0][k0 + k];
-        b += wd * z[1][k0 + k];
-        d2 += wd * z[2][k0 + k];
+    for (int r = 0; r < 3; ++r) cr[r] = c.evr[3 * blockIdx.x + r];  // grid = max_batch: in bounds
+    if (!live) return;
+    for (int x = lane; x < 3 * D; x += 64) z[x / D][x % D] = c.Zc[(int64_t)cr[x / D] * D + x % D];
+    if (lane < 3) scr[lane] = cr[lane];
+  } else {
+    const int st = tid - 64;  // 192 staging threads
+    if (blockIdx.x == 0 && st == 0) {
+      c.cnt[CNT_LIST] = 3 * (hi - lo);
+      if (c.adf.p) {  // fused Adam: this step's scalars for the gradient writers (tgn_adam computes them itself)
+        const int64_t t = c.ctl[TGNX_CTL_ADAM_T] + (c.adv ? 1 : 0);
+        float* sc = reinterpret_cast<float*>(c.ctl + TGNX_CTL_ADAM_SC);
+        sc[0] = (float)(c.lr / (1.0 - pow((double)c.b1, (double)t)));
+        sc[1] = (float)sqrt(1.0 - pow((double)c.b2, (double)t));
       }
-      part[wv][0][o] = a;
-      part[wv][1][o] = b;
-      part[wv][2][o] = d2;
+    }
+    if (!live) return;
+    // D is even, so D * D % 4 == 0; the flat buffer's blocks are 16-B aligned (tgnx_tgn_param_layout)
+    const int n4 = D * D / 4;
+    const float invD = 1.0f / (float)D;
+    const float4* S4 = reinterpret_cast<const float4*>(c.params + c.L.lsw);
+    const float4* D4 = reinterpret_cast<const float4*>(c.params + c.L.ldw);
+    for (int b0 = 0; b0 < n4; b0 += 192 * PRED_SU) {
+      float4 ws4[PRED_SU], wd4[PRED_SU];
+#pragma unroll
+      for (int u = 0; u < PRED_SU; ++u) {
+        const int x = min(b0 + st + 192 * u, n4 - 1);
+        ws4[u] = S4[x];
+        wd4[u] = D4[x];
+      }
+      if (b0 == 0)
+        for (int x = st; x < 3 * D + 1; x += 192) {
+          const float v = x < D ? c.params[c.L.lsb + x] : x < 2 * D ? c.params[c.L.ldb + x - D]
+                        : x < 3 * D ? c.params[c.L.lfw + x - 2 * D] : c.params[c.L.lfb];
+          if (x < D) vsb[x] = v;
+          else if (x < 2 * D) vdb[x - D] = v;
+          else vfw[x - 2 * D] = v;
+        }
+      if (flat) {
+#pragma unroll
+        for (int u = 0; u < PRED_SU; ++u) {
+          const int x = b0 + st + 192 * u;
+          if (x < n4) {
+            reinterpret_cast<float4*>(Wsrc)[x] = ws4[u];
+            reinterpret_cast<float4*>(Wdst)[x] = wd4[u];
+          }
+        }
+        continue;
+      }
+#pragma unroll
+      for (int u = 0; u < PRED_SU; ++u) {
+        const int x = b0 + st + 192 * u;
+        if (x < n4) {
+          const float vs[4] = {ws4[u].x, ws4[u].y, ws4[u].z, ws4[u].w};
+          const float vd[4] = {wd4[u].x, wd4[u].y, wd4[u].z, wd4[u].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {  // row / column of element 4x + j (no integer division: it is a
+                                         // ~40-instruction software routine per element)
+            const int e = 4 * x + j, o = div_small(e, D, invD), k = e - o * D;
+            Wsrc[o * DP + k] = vs[j];
+            Wdst[o * DP + k] = vd[j];
+          }
+        }
+      }
     }
   }
   __syncthreads();
+  const int cr[3] = {scr[0], scr[1], scr[2]};
+  const int kc = (D + 3) / 4, k0 = wv * kc, nk = min(D - k0, kc);
+  if (flat) {  // lin_src(z_s), lin_dst(z_p), lin_dst(z_n): wave wv takes float4 columns [q0, q0 + nq)
+    const int c4 = D / 4, kq = (c4 + 3) / 4, q0 = wv * kq, nq = max(0, min(c4 - q0, kq));
+    const float4* z0 = reinterpret_cast<const float4*>(z[0]) + q0;
+    const float4* z1 = reinterpret_cast<const float4*>(z[1]) + q0;
+    const float4* z2 = reinterpret_cast<const float4*>(z[2]) + q0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int o = lane + 64 * q;
+      if (o < D) {
+        const float4* ws = reinterpret_cast<const float4*>(Wsrc + o * D) + q0;
+        const float4* wd = reinterpret_cast<const float4*>(Wdst + o * D) + q0;
+        float a = 0.f, b = 0.f, d2 = 0.f;
+#pragma unroll 4
+        for (int j = 0; j < nq; ++j) {
+          const float4 u = ws[j], v = wd[j], x0 = z0[j], x1 = z1[j], x2 = z2[j];
+          a += (u.x * x0.x + u.y * x0.y) + (u.z * x0.z + u.w * x0.w);
+          b += (v.x * x1.x + v.y * x1.y) + (v.z * x1.z + v.w * x1.w);
+          d2 += (v.x * x2.x + v.y * x2.y) + (v.z * x2.z + v.w * x2.w);
+        }
+        part[wv][0][o] = a;
+        part[wv][1][o] = b;
+        part[wv][2][o] = d2;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // lin_src(z_s), lin_dst(z_p), lin_dst(z_n): split contraction
+      const int o = lane + 64 * q;
+      if (o < D) {
+        float a = 0.f, b = 0.f, d2 = 0.f;
+        for (int k = 0; k < nk; ++k) {
+          const float ws = Wsrc[o * DP + k0 + k], wd = Wdst[o * DP + k0 + k];
+          a += ws * z[0][k0 + k];
+          b += wd * z[1][k0 + k];
+          d2 += wd * z[2][k0 + k];
+        }
+        part[wv][0][o] = a;
+        part[wv][1][o] = b;
+        part[wv][2][o] = d2;
+      }
+    }
+  }
+  __syncthreads();
+  TGNX_STAMP_AT(0);
   float* ev = c.evs + (int64_t)i * evs_stride(D);
   if (wv == 0) {
     float hp[2], hn[2], zp = 0.f, zn = 0.f;
@@ -1317,16 +1502,16 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c) {
       const int o = lane + 64 * q;
       hp[q] = hn[q] = 0.f;
       if (o < D) {
-        const float s = ((part[0][0][o] + part[1][0][o]) + (part[2][0][o] + part[3][0][o])) + P[c.L.lsb + o];
-        const float dp = ((part[0][1][o] + part[1][1][o]) + (part[2][1][o] + part[3][1][o])) + P[c.L.ldb + o];
-        const float dn = ((part[0][2][o] + part[1][2][o]) + (part[2][2][o] + part[3][2][o])) + P[c.L.ldb + o];
+        const float s = ((part[0][0][o] + part[1][0][o]) + (part[2][0][o] + part[3][0][o])) + vsb[o];
+        const float dp = ((part[0][1][o] + part[1][1][o]) + (part[2][1][o] + part[3][1][o])) + vdb[o];
+        const float dn = ((part[0][2][o] + part[1][2][o]) + (part[2][2][o] + part[3][2][o])) + vdb[o];
         hp[q] = fmaxf(s + dp, 0.f);
         hn[q] = fmaxf(s + dn, 0.f);
-        zp += P[c.L.lfw + o] * hp[q];
-        zn += P[c.L.lfw + o] * hn[q];
+        zp += vfw[o] * hp[q];
+        zn += vfw[o] * hn[q];
       }
     }
-    const float ap = wave_sum(zp) + P[c.L.lfb], an = wave_sum(zn) + P[c.L.lfb];
+    const float ap = wave_sum(zp) + vfw[D], an = wave_sum(zn) + vfw[D];
     const float sp = sigm(ap), sn = sigm(an);
     const float invB = 1.0f / (float)B;
     const float dap = (sigm(sp) - 1.0f) * sp * (1.0f - sp) * invB;
@@ -1335,7 +1520,7 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c) {
     for (int q = 0; q < 2; ++q) {
       const int o = lane + 64 * q;
       if (o < D) {
-        const float wf = P[c.L.lfw + o];
+        const float wf = vfw[o];
         const float dhp = hp[q] > 0.f ? dap * wf : 0.f;
         const float dhn = hn[q] > 0.f ? dan * wf : 0.f;
         dh[0][o] = dhp;
@@ -1357,18 +1542,22 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c) {
       c.out_neg[i] = sn;
     }
   }
-  __syncthreads();
-  // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn (split over k, coalesced over o)
+  // barrier for dh (LDS) only: the evs-row stores of wave 0 stay in flight (__syncthreads waits vmcnt(0))
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  TGNX_STAMP_AT(1);
+  // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn (split over k, lanes over o)
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int o = lane + 64 * q;
     if (o < D) {
       float a = 0.f, b = 0.f, d2 = 0.f;
+#pragma unroll 5
       for (int k = 0; k < nk; ++k) {
         const int kk = k0 + k;
-        a += Wsrc[(int64_t)kk * D + o] * (dh[0][kk] + dh[1][kk]);
-        b += Wdst[(int64_t)kk * D + o] * dh[0][kk];
-        d2 += Wdst[(int64_t)kk * D + o] * dh[1][kk];
+        a += Wsrc[kk * DP + o] * (dh[0][kk] + dh[1][kk]);
+        b += Wdst[kk * DP + o] * dh[0][kk];
+        d2 += Wdst[kk * DP + o] * dh[1][kk];
       }
       part[wv][0][o] = a;
       part[wv][1][o] = b;
@@ -1424,23 +1613,26 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
     lp_vec_body(c, ((int)blockIdx.x - ncb) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
     return;
   }
-  const int B = (int)c.ctl[TGNX_CTL_B];
-  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int R = c.cnt[c.rsel];
   const int lane = threadIdx.x & 63;
   const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (x >= R) return;
+  // first round: batch descriptor, centre count, the centre's row / edge range (clamped, as tgn_attn_fwd)
+  const int xc = min(x, max(c.ccap - 1, 0));
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int64_t err = c.ctl[TGNX_CTL_ERR];
+  const int R = c.cnt[c.rsel];
+  const int i = c.cent_loc[xc];
+  const int e0 = c.ceoff[xc], e1 = c.ceoff[xc + 1];
+  if (B == 0 || err != 0 || x >= R) return;
   const int C = c.C, HC = c.HC;
   const bool okl = lane < C;
   const float on = f01(okl);
   const int l0 = min(lane, C - 1);
-  const int i = c.cent_loc[x];
   const float* Pi = c.P + (int64_t)i * 4 * HC;
   float* dPi = c.dP + (int64_t)i * 4 * HC;
   const float q0 = Pi[l0], q1 = Pi[C + l0];
   const float g0 = c.dZc[(int64_t)x * HC + l0] * on, g1 = c.dZc[(int64_t)x * HC + C + l0] * on;
   const float sqc = sqrtf((float)C);
-  const int e0 = c.ceoff[x], ne = c.ceoff[x + 1] - e0;
+  const int ne = e1 - e0;
   const int le = e0 + min(lane, max(ne - 1, 0));
   const int jl = c.e_j[le];
   const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
@@ -1450,6 +1642,58 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
   if (lane < ne && c.drop) {
     k0v = att_keep(c, seed, x, e0 + lane, 0);
     k1v = att_keep(c, seed, x, e0 + lane, 1);
+  }
+  if (ne > 0 && ne <= ATT_EB) {  // every ring of K <= 16: v, k and edge rows of all edges in one round
+    float kk0[ATT_EB], kk1[ATT_EB], v0[ATT_EB], v1[ATT_EB];
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      const int e = min(u, ne - 1);
+      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
+      const float ea = Ee[l0], eb = Ee[C + l0];
+      kk0[u] = Pj[HC + l0] + ea;
+      kk1[u] = Pj[HC + C + l0] + eb;
+      v0[u] = Pj[2 * HC + l0] + ea;
+      v1[u] = Pj[2 * HC + C + l0] + eb;
+    }
+    float da0 = 0.f, da1 = 0.f;
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      if (u >= ne) break;
+      const float p0 = wave_sum(g0 * v0[u]), p1 = wave_sum(g1 * v1[u]);
+      if (lane == u) { da0 = p0 * k0v; da1 = p1 * k1v; }
+    }
+    const float s0 = wave_sum(a0 * da0), s1 = wave_sum(a1 * da1);
+    const float ds0 = a0 * (da0 - s0), ds1 = a1 * (da1 - s1);
+    const float t0 = a0 * k0v, t1 = a1 * k1v;
+    float dq0 = 0.f, dq1 = 0.f;
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      if (u >= ne) break;
+      const float d0 = __shfl(ds0, u, 64) / sqc, d1 = __shfl(ds1, u, 64) / sqc;
+      const float b0 = __shfl(t0, u, 64), b1 = __shfl(t1, u, 64);
+      float* dEe = c.dE + (int64_t)(e0 + u) * HC;
+      float* dKe = c.dKV + (int64_t)(e0 + u) * 2 * HC;  // [dk (HC) | dv (HC)]
+      dq0 += d0 * kk0[u];
+      dq1 += d1 * kk1[u];
+      if (okl) {
+        const float dk0 = d0 * q0, dk1 = d1 * q1;
+        const float dv0 = b0 * g0, dv1 = b1 * g1;
+        dEe[lane] = dk0 + dv0;
+        dEe[C + lane] = dk1 + dv1;
+        dKe[lane] = dk0;
+        dKe[C + lane] = dk1;
+        dKe[HC + lane] = dv0;
+        dKe[HC + C + lane] = dv1;
+      }
+    }
+    if (okl) {
+      dPi[lane] = dq0;
+      dPi[C + lane] = dq1;
+      dPi[3 * HC + lane] = g0;
+      dPi[3 * HC + C + lane] = g1;
+    }
+    return;
   }
   // d alpha~_eh = Σ_{ch in h} dout (v_j + e); d alpha = d alpha~ * keep
   float da0 = 0.f, da1 = 0.f;
@@ -1619,7 +1863,7 @@ struct EpiProjGrad {
       const int x = threadIdx.x + 256 * it;
       const int r = x / T::tn, cc = x % T::tn, row = t.m0 + r, n = t.n0 + cc;
       const bool ok = x < T::tm * T::tn && row < t.M && n < t.N;
-      const int gi = row / HC, q = row % HC;
+      const int gi = proj_g(row, HC), q = row - gi * HC;
       vx[it] = ok ? t(r, cc) : 0.f;
       ix[it] = !ok ? -1 : n < D ? wq + gi * pw + (int64_t)q * D + n : bq + gi * pb + q;
     }
@@ -1655,7 +1899,7 @@ struct LoadLpA {
   static constexpr bool k_fast = false;
   __device__ float operator()(int r, int k) const {
     const int lo = (int)ctl[TGNX_CTL_LO], nloc = max(1, (int)(ctl[TGNX_CTL_HI] - ctl[TGNX_CTL_LO]));
-    const int blk = k / nloc, i = lo + k % nloc;
+    const int blk = (k >= nloc) + (k >= 2 * nloc), i = lo + k - blk * nloc;  // k < 3 nloc: no division
     const float* ev = evs + (int64_t)i * S;
     const bool src = r < D;
     const int o = src ? r : r - D;
@@ -1670,7 +1914,7 @@ struct LoadLpB {
   static constexpr bool k_fast = false;
   __device__ float operator()(int n, int k) const {
     const int lo = (int)ctl[TGNX_CTL_LO], nloc = max(1, (int)(ctl[TGNX_CTL_HI] - ctl[TGNX_CTL_LO]));
-    const int blk = k / nloc, i = lo + k % nloc;
+    const int blk = (k >= nloc) + (k >= 2 * nloc), i = lo + k - blk * nloc;
     return evs[(int64_t)i * S + blk * D + n];
   }
 };
@@ -1788,7 +2032,7 @@ struct LoadProjWT {
   int HC, D;
   static constexpr bool k_fast = false;
   __device__ float operator()(int n, int k) const {
-    const int g = k / HC, r = k % HC;
+    const int g = proj_g(k, HC), r = k - g * HC;
     return w[g * pw + (int64_t)r * D + n];
   }
 };
@@ -2204,7 +2448,7 @@ static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_spl
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
-      Ep, alpha, Zc, evs, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
+      Ep, alpha, Zc, evs, evr, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
       rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF, total;
   int tgp_rows, tgp_e1;
 };
@@ -2244,6 +2488,7 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.alpha = carve(off, (size_t)k.Etr * TH * 4);
   W.Zc = carve(off, (size_t)k.Rcap * HC * 4);
   W.evs = carve(off, (size_t)k.B * evs_stride(D) * 4);
+  W.evr = carve(off, (size_t)k.B * 3 * 4);
   W.Hs = carve(off, (size_t)k.Rcap * D * 4);
   W.Hd = carve(off, (size_t)k.Rcap * D * 4);
   W.dZc = carve(off, (size_t)k.Rtr * HC * 4);
@@ -2393,6 +2638,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.alpha = reinterpret_cast<float*>(ws + W.alpha);
   c.Zc = reinterpret_cast<float*>(ws + W.Zc);
   c.evs = reinterpret_cast<float*>(ws + W.evs);
+  c.evr = reinterpret_cast<int*>(ws + W.evr);
   c.Hs = reinterpret_cast<float*>(ws + W.Hs);
   c.Hd = reinterpret_cast<float*>(ws + W.Hd);
   c.dZc = reinterpret_cast<float*>(ws + W.dZc);
@@ -2423,6 +2669,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.L = make_lay(c.D, c.d, k.layers);
   c.layers = k.layers;
   c.rsel = CNT_R;
+  c.ccap = k.Rcap;
   c.att_salt = 7;
   if (k.layers == 2) {
     c.rb = reinterpret_cast<uint32_t*>(ws + W.rb);
@@ -2468,10 +2715,20 @@ static Ctx root_view(const Ctx& c) {
   r.dP = c.dP2;
   r.dE = c.dE2;
   r.rsel = CNT_R1;
+  r.ccap = c.R1cap;
   r.att_salt = 9;
   return r;
 }
 
+// tgn_agg_emit's two grid-stride parts (sampled edges, wave per (centre, ring slot); sampled nodes):
+// grids sized from capacities launch mostly idle workgroups, which hold dispatch slots
+// (stamps timeline, wiki shape: caps 4096 / 2048 -> 1024 / 512 took agg_emit 16.5 -> 13.9 us)
+#ifndef TGNX_AGG_EDGE_CAP
+#define TGNX_AGG_EDGE_CAP 1024
+#endif
+#ifndef TGNX_AGG_NODE_CAP
+#define TGNX_AGG_NODE_CAP 512
+#endif
 static inline int gridn(int64_t n, int per, int cap = 4096) {
   int64_t g = (n + per - 1) / per;
   if (g < 1) g = 1;
@@ -2533,6 +2790,14 @@ int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf
   return TGNX_OK;
 }
 
+// tgn_pred_train stages the predictor weights in dynamic LDS (up to 2 x 128 x 129 floats)
+static bool pred_smem_ok(int D) {
+  static const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&tgn_pred_train),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)tgn_pred_smem(TDMAX)) == hipSuccess;
+  return ok && tgn_pred_smem(D) <= tgn_pred_smem(TDMAX);
+}
+
 struct AdvArgs {
   int64_t lo, hi, batch;
   int rank, world;
@@ -2547,8 +2812,13 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   if (rc) return rc;
   if (adv) {
     TGNX_CHECK_ARG(adv->batch > 0 && adv->batch <= cfg->max_batch && adv->world >= 1 && adv->rank >= 0 &&
-                       adv->rank < adv->world && adv->lo >= 0 && adv->hi >= adv->lo,
-                   "tgnx_tgn_train_step_resident: bad cursor arguments");
+                       adv->rank < adv->world && adv->lo >= 0 && adv->hi >= adv->lo && adv->hi <= c.nev,
+                   "tgnx_tgn_train_step_resident: bad cursor arguments (batch, rank / world, or split beyond the "
+                   "event table)");
+    // the fused step applies Adam to this rank's gradients in place: only a world-1 step has the whole sum
+    TGNX_CHECK_ARG(!fuse_adam || adv->world == 1,
+                   "tgnx_tgn_train_step_resident: world > 1 steps all-reduce before Adam "
+                   "(tgnx_tgn_train_fwd_bwd_resident + exchange + tgnx_tgn_train_update)");
     c.adv = 1;
     c.adv_lo = adv->lo;
     c.adv_hi = adv->hi;
@@ -2585,9 +2855,11 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   tgn_scan<true><<<1, 1024, 0, s>>>(c);  // plans: in tgn_mark
   probe_end(TGNX_K_ASSEMBLE, s);
   TGNX_LAUNCH_CHECK("tgn_scan");
-  const int nedge = gridn((int64_t)k.Rtr * c.K, 4, 4096);
+  const int nedge = gridn((int64_t)k.Rtr * c.K, 4, TGNX_AGG_EDGE_CAP);
   probe_begin(TGNX_K_EDGE_META, s);
-  tgn_agg_emit<<<nedge + gridn(k.Mtr, 4, 2048), 256, 0, s>>>(c, 0, nedge, nullptr, nullptr, 0, 0);
+  const int nevb = gridn(3 * k.B, 256);
+  tgn_agg_emit<<<nevb + nedge + gridn(k.Mtr, 4, TGNX_AGG_NODE_CAP), 256, 0, s>>>(c, 0, nedge, nullptr, nullptr, 0, 0,
+                                                                                   nevb);
   probe_end(TGNX_K_EDGE_META, s);
   TGNX_LAUNCH_CHECK("tgn_agg_emit");
   // GRU over every sampled node ‖ lin_edge over every sampled edge (‖ 2 hops: conv2's lin_edge over the
@@ -2626,7 +2898,8 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     TGNX_LAUNCH_CHECK("tgn_attn_fwd2");
   }
   probe_begin(TGNX_K_PRED, s);
-  tgn_pred_train<<<k.B, 256, 0, s>>>(cr);
+  TGNX_CHECK_ARG(pred_smem_ok(c.D), "tgn_pred_train: dynamic LDS attribute refused");
+  tgn_pred_train<<<k.B, 256, tgn_pred_smem(c.D), s>>>(cr);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
   probe_begin(TGNX_K_SEG_BWD, s);

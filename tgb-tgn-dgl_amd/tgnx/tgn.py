@@ -259,7 +259,10 @@ class TgnEngine:
         self.dst_nodes = None if dst_nodes is None else torch.as_tensor(dst_nodes).to(self.dev, torch.long).contiguous()
         self.seed, self.rank, self.world = int(seed), int(rank), int(world)
         self.fuse_adam = True
-        self.fold_cursor = True   # resident world-1 steps: tgnx_tgn_train_step_resident
+        # resident steps fold the batch cursor into the step's first launch: tgnx_tgn_train_step_resident
+        # (world 1, Adam fused) or tgnx_tgn_train_fwd_bwd_resident (world > 1; exchange + update follow).
+        # Both forms are tested against advance + step per rank (test_gpu_tgn.py, test_gpu_tgn_dp.py).
+        self.fold_cursor = True
         if optimizer is None:
             self.adam_m, self.adam_v = torch.zeros_like(model.flat), torch.zeros_like(model.flat)
         else:

@@ -109,7 +109,8 @@ def main():
     for x, L in launches_x.items():
         for l in L:
             for r in l:
-                allw.append((int(r["t0"]) - off[x], int(r["t1"]) - off[x], int(r["kid"]), int(r["blk"]), x))
+                allw.append((int(r["t0"]) - off[x], int(r["t1"]) - off[x], int(r["kid"]), int(r["blk"]), x,
+                             int(r["wave"])))
     allw.sort()
     glaunch, cur, tmax = [], [], 0
     for w in allw:
@@ -168,6 +169,13 @@ def main():
                     st_, du = np.array(ws, dtype=np.float64).T * 0.01
                     parts.append(f"[{a}-{b - 1}] {st_.mean():.1f}/{du.mean():.1f}/{du.max():.1f}")
             print(f"  {i:2d} {NAMES.get(ls[0][0][2], ls[0][0][2]):14s} " + "  ".join(parts))
+    for i in range(nl):  # intra-kernel checkpoints (TGNX_STAMP_AT), busy workgroups
+        ls = [s[i] for s in steps]
+        mids = [(w[5] & 0xFFFF, w[5] >> 16, w[1] - w[0]) for l in ls for w in l if w[5]]
+        if mids:
+            a = np.array(mids, dtype=np.float64) * 0.01
+            print(f"  checkpoints {NAMES.get(ls[0][0][2], ls[0][0][2])}: at0 {a[:, 0].mean():.2f} us, at1 "
+                  f"{a[:, 1].mean():.2f} us, end {a[:, 2].mean():.2f} us (mean over {len(mids)} workgroups)")
     step_span = np.mean([(max(w[1] for w in s[-1]) - min(w[0] for w in s[0])) * 0.01 for s in steps])
     print(f"sum of spans {tot_span:.1f}, sum of gaps {tot_gap:.1f}, first start -> last end {step_span:.1f} us; "
           f"replay {step_us:.1f} us/step")
