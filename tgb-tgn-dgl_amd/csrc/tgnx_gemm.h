@@ -24,32 +24,66 @@ namespace tgnx {
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-template <int TM_, int TN_, int KC_, int PF_ = 1>
+template <int TM_, int TN_, int KC_, int PF_ = 1, bool WS_ = false>
 struct GemmCfg {
   static constexpr int TM = TM_, TN = TN_, KC = KC_;
   static constexpr int PF = PF_;  // k-chunks whose global loads are in flight ahead of the MFMAs
-  static constexpr int FM = TM / 32, FN = TN / 32;  // 16x16 MFMA tiles per wave (2x2 waves)
+  // WS (wave split-K): every wave owns the whole TMxTN tile and every 4th 16-deep k-slab of a chunk;
+  // the four partial tiles are summed through LDS in wave order.  Otherwise the 4 waves tile the output
+  // 2x2, each a (TM/2)x(TN/2) quadrant over the whole chunk.
+  static constexpr bool WS = WS_;
+  static constexpr int FM = WS ? TM / 16 : TM / 32, FN = WS ? TN / 16 : TN / 32;  // 16x16 MFMA tiles per wave
   static constexpr int PK = KC + 4;                  // LDS row pitch of the k-contiguous operand rows
   static constexpr int PB = TN + 1;                  // LDS pitch of the C tile
   static constexpr int LA = TM * KC / 256, LB = TN * KC / 256;  // operand elements per thread per chunk
-  static constexpr int SMEM = (TM + TN) * PK;        // floats (operands; the C tile reuses them)
-  static_assert(TM % 32 == 0 && TN % 32 == 0 && KC % 16 == 0 && LA % 4 == 0 && LB % 4 == 0, "tile");
-  static_assert(TM * (TN + 1) + 512 <= SMEM, "C tile + epilogue scratch must fit the operand LDS");
+  static constexpr int SOP = (TM + TN) * PK, SRED = (WS ? 5 : 1) * TM * PB + 512;
+  static constexpr int SMEM = SOP > SRED ? SOP : SRED;  // floats (operands; the C tile reuses them)
+  static_assert(WS ? (TM % 16 == 0 && TN % 16 == 0 && KC % 64 == 0) : (TM % 32 == 0 && TN % 32 == 0 && KC % 16 == 0),
+                "tile");
+  static_assert(LA % 4 == 0 && LB % 4 == 0 && TM * TN % 256 == 0, "operand / C-tile split over 256 threads");
 };
+// The TGN step's GEMMs: 16x16 output tiles, wave split-K (GemmCfg::WS).  Each 16x16x4 fp32 MFMA issues
+// for 32 cycles per SIMD, so a tile's time is set by its MFMA count on one CU: 32x32 tiles with the 2x2
+// wave grid ran the GRU GEMM (M ~ 415, N = 400, K = 572) as 169 tiles of 4 x 143 chained MFMAs; 16x16 tiles
+// spread the same MFMAs over 4x the workgroups (650 on 256 CUs) and the wave split cuts each wave's
+// chain to K/64 slabs (tools/gemm_lab.hip: GRU 9.5 -> 8.2 us, dz0 7.9 -> 4.9 us per launch).
+#ifndef TGNX_G32_T
+#define TGNX_G32_T 16
+#endif
+#ifndef TGNX_G32_WS
+#define TGNX_G32_WS 1
+#endif
 #ifndef TGNX_G32_KC
 #define TGNX_G32_KC 64
 #endif
 #ifndef TGNX_G32_PF
 #define TGNX_G32_PF 1
 #endif
-using G32 = GemmCfg<32, 32, TGNX_G32_KC, TGNX_G32_PF>;  // the TGN step's GEMMs
+using G32 = GemmCfg<TGNX_G32_T, TGNX_G32_T, TGNX_G32_KC, TGNX_G32_PF, TGNX_G32_WS>;  // the TGN step's GEMMs
+#ifndef TGNX_G32L_T
+#define TGNX_G32L_T 16
+#endif
+#ifndef TGNX_G32L_WS
+#define TGNX_G32L_WS 1
+#endif
 #ifndef TGNX_G32L_KC
 #define TGNX_G32L_KC 64
 #endif
 #ifndef TGNX_G32L_PF
 #define TGNX_G32L_PF 1
 #endif
-using G32L = GemmCfg<32, 32, TGNX_G32L_KC, TGNX_G32L_PF>;  // long-K direct GEMMs (GRU, dz0, dX_enc): fewer chunks
+using G32L = GemmCfg<TGNX_G32L_T, TGNX_G32L_T, TGNX_G32L_KC, TGNX_G32L_PF, TGNX_G32L_WS>;  // long-K direct GEMMs (GRU, dz0, dX_enc)
+// deferred split-K weight gradients (K = edges / nodes, split S ways): already S x tiles workgroups
+#ifndef TGNX_GW_T
+#define TGNX_GW_T 32
+#endif
+#ifndef TGNX_GW_WS
+#define TGNX_GW_WS 0
+#endif
+#ifndef TGNX_GW_KC
+#define TGNX_GW_KC 64
+#endif
+using GW = GemmCfg<TGNX_GW_T, TGNX_GW_T, TGNX_GW_KC, 1, TGNX_GW_WS>;
 using G64 = GemmCfg<64, 64, 64>;   // large-M GEMMs (eval scoring)
 
 struct GemmShape {
@@ -237,13 +271,13 @@ __device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, 
   const int tile = wk.tile, s = wk.s;
   const int m0 = wk.tm * TM, n0 = wk.tn * TN;
   if (!wk.ok || m0 >= rt.Mr || n0 >= rt.Nr || s >= rt.Sr) return;  // the fixup skips such tiles / splits too
-  const int wr = (wv >> 1) * (TM / 2), wc = (wv & 1) * (TN / 2);
+  const int wr = CFG::WS ? 0 : (wv >> 1) * (TM / 2), wc = CFG::WS ? 0 : (wv & 1) * (TN / 2);
   const int li = lane & 15, lk = lane >> 4;
-  f32x4_t acc[FM][FN];
+  f32x4_t acc[FM][FN], acc2[FM][FN];  // acc2: second accumulator chain of the WS path (odd MFMA steps)
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = acc2[i][j] = {0.f, 0.f, 0.f, 0.f};
   constexpr int PF = CFG::PF;
   float ra[PF][LA], rb[PF][LB];
   // chunk ch -> register slot p (every load of the slot in flight at once)
@@ -328,6 +362,23 @@ __device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, 
     for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const f32x4_t*>(Bs + (wc + 16 * j + li) * PK + kk + 4 * lk);
   };
   auto mfma_chunk = [&]() {
+    if constexpr (CFG::WS) {  // this wave's slabs wv, wv + 4, ... of the chunk
+#pragma unroll
+      for (int u = 0; u < KC / 64; ++u) {
+        f32x4_t a[FM], b[FN];
+        slab(16 * (wv + 4 * u), a, b);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+              if (q & 1) acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][q], b[j][q], acc2[i][j], 0, 0, 0);
+              else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
+            }
+      }
+      return;
+    }
     f32x4_t a[2][FM], b[2][FN];
     slab(0, a[0], b[0]);
 #pragma unroll
@@ -361,6 +412,30 @@ __device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, 
         __syncthreads();
       }
     }
+  }
+  if constexpr (CFG::WS) {  // wave partials -> LDS, summed in wave order into the C tile
+    float* red = smem;  // [4][TM][PB], then Ct [TM][PB]
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          red[wv * TM * PB + (16 * i + lk * 4 + r) * PB + 16 * j + li] = acc[i][j][r] + acc2[i][j][r];
+    __syncthreads();
+    float* Ct = red + 4 * TM * PB;
+    constexpr int PER = TM * TN / 256;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int x = tid + 256 * e, o = (x / TN) * PB + x % TN;
+      const float v = ((red[o] + red[TM * PB + o]) + red[2 * TM * PB + o]) + red[3 * TM * PB + o];
+      if (g.deferred) part[((size_t)tile * g.S + s) * TM * TN + x] = v;  // row-major partial tile
+      else Ct[o] = v;
+    }
+    if (g.deferred) return;
+    __syncthreads();
+    epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, Ct + TM * PB});
+    return;
   }
   if (g.deferred) {  // partial tile in register layout, summed by gemm_fixup_kernel
     f32x4_t* mine = reinterpret_cast<f32x4_t*>(part + ((size_t)tile * g.S + s) * TM * TN);
@@ -496,6 +571,25 @@ __device__ void gemm_fix_tile(const GemmFix<CFG, EPI>& f, int tile, float* smem)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wr = (wv >> 1) * (TM / 2), wc = (wv & 1) * (TN / 2), li = lane & 15, lk = lane >> 4;
   float* Ct = smem;
+  if constexpr (CFG::WS) {  // row-major partials
+    constexpr int PER = TM * TN / 256, SU = 8;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int x = threadIdx.x + 256 * e;
+      float sum = 0.f;
+      for (int q0 = 0; q0 < rt.Sr; q0 += SU) {
+        float pv[SU];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) pv[u] = f.part[((size_t)tile * f.g.S + min(q0 + u, rt.Sr - 1)) * TM * TN + x];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) sum += pv[u] * f01(q0 + u < rt.Sr);
+      }
+      Ct[(x / TN) * PB + x % TN] = sum;
+    }
+    __syncthreads();
+    f.epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, smem + TM * PB});
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll

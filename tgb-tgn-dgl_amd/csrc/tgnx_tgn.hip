@@ -2439,13 +2439,13 @@ static Caps make_caps(const tgnx_tgn_config* cfg) {
 // 1-hop ones), at least 8
 static int ksplit(int K, int smin) { return std::max(smin, std::min(64, K / 2048)); }
 // the deferred (split-K) weight-gradient GEMMs of a train step
-static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(k.HC, k.D + k.d, k.Etr, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, ksplit(k.Etr, 8)); }
-static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.HC, k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
+static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.Etr, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, ksplit(k.Etr, 8)); }
+static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.HC, k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
 // 2 hops: conv2's projections (K = outer centres) and lin_edge (K = root edges)
-static GemmShape shp_dWp2(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.HC, k.D + 1, k.Rtr, nullptr, nullptr, cnt ? cnt + CNT_R : nullptr, ksplit(k.Rtr, 4)); }
-static GemmShape shp_dWe2(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(k.HC, k.D + k.d, k.E1tr, nullptr, nullptr, cnt ? cnt + CNT_E1 : nullptr, ksplit(k.E1tr, 8)); }
-static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, 5); }
-static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<G32>(4 * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
+static GemmShape shp_dWp2(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.HC, k.D + 1, k.Rtr, nullptr, nullptr, cnt ? cnt + CNT_R : nullptr, ksplit(k.Rtr, 4)); }
+static GemmShape shp_dWe2(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.E1tr, nullptr, nullptr, cnt ? cnt + CNT_E1 : nullptr, ksplit(k.E1tr, 8)); }
+static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, 5); }
+static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
       Ep, alpha, Zc, evs, evr, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
@@ -2911,7 +2911,7 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
     // conv2's (dk, dv) sums ‖ its dE2-only GEMMs (as in the 1-hop step below), then dh1 ‖ dW_proj2
     gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{cr}, gridn(k.E1tr, KVR_CH, 1 << 20)},
-                 gemm_job<G32>(shp_dWe2(k, c.cnt), LoadKRow{c.dE2, HC, k.E1tr, HC}, LoadEdgeAttrMapT{ea1},
+                 gemm_job<GW>(shp_dWe2(k, c.cnt), LoadKRow{c.dE2, HC, k.E1tr, HC}, LoadEdgeAttrMapT{ea1},
                                EpiDeferred{}, c.pF),
                  gemm_job<G32>(gemm_shape<G32>(k.E1tr, D, HC, c.cnt + CNT_E1), LoadRowK{c.dE2, k.E1tr, HC, HC},
                                LoadKRow{P + c.L.we2, D, HC, D + d},
@@ -2920,7 +2920,7 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     gemmN_launch(s,
                  gemm_job<G32L>(gemm_shape<G32L>(k.Rtr, HC, 4 * HC, c.cnt + CNT_R), LoadRowK{c.dP2, k.Rtr, 4 * HC, 4 * HC},
                                 LoadProjWT{P + c.L.wq2, c.L.pw, HC, HC}, EpiStore{c.dZc, nullptr, HC, 0}, (float*)nullptr),
-                 gemm_job<G32>(shp_dWp2(k, c.cnt), LoadKRow{c.dP2, 4 * HC, k.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
+                 gemm_job<GW>(shp_dWp2(k, c.cnt), LoadKRow{c.dP2, 4 * HC, k.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
                                EpiDeferred{}, c.pE));
     TGNX_LAUNCH_CHECK("tgn_dh1");
     tgn_attn_bwd<<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c, gridn(k.Rtr, 4, 1 << 20));
@@ -2937,7 +2937,7 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   const EpiGradStore e_dWe{G, c.L.we, D + d, c.adf};
   probe_begin(TGNX_K_KV, s);
   gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(k.Etr, KVR_CH, 1 << 20)},
-               gemm_job<G32>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, EpiDeferred{}, c.pA),
+               gemm_job<GW>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, EpiDeferred{}, c.pA),
                gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
                              LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
                              (float*)nullptr));
@@ -2951,15 +2951,15 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   // epilogue — all read only what attn_bwd / kv_reduce / pred_train produced
   const int rows_edge = (k.Etr + G32::TM - 1) / G32::TM, rows_msg = (k.Mtr + G32::TM - 1) / G32::TM;
   probe_begin(TGNX_K_EDGE_BWD, s);
-  gemmN_launch(s, gemm_job<G32>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB),
-               gemm_job<G32>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
+  gemmN_launch(s, gemm_job<GW>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB),
+               gemm_job<GW>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
                              LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, EpiDeferred{}, c.pC),
                gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
                              LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, EpiGruBwd{c.gates, c.mem, c.nid, c.dG, D},
                              (float*)nullptr));
   probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
-  gemm2_launch<G32, G32L>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{},
+  gemm2_launch<GW, G32L>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{},
                c.pD, gemm_shape<G32L>(k.Mtr, D, 4 * D, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
                LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, nullptr, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
@@ -2971,15 +2971,15 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   const TrainTail tail{TeReduceTail{c, rows_edge, rows_msg}, nte, nmem, nst, ninc};
   probe_begin(TGNX_K_FINISH, s);
   if (two)
-    gemm_fixup_launch(nte + nmem + nst + nring + (c.adv ? 1 : 0), tail, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
-                      gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
-                      gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg),
-                      gemm_fix<G32>(shp_dWp2(k, c.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC, c.adf}),
-                      gemm_fix<G32>(shp_dWe2(k, c.cnt), c.pF, EpiGradStore{G, c.L.we2, D + d, c.adf}));
+    gemm_fixup_launch(nte + nmem + nst + nring + (c.adv ? 1 : 0), tail, s, gemm_fix<GW>(shp_dWe(k, c.cnt), c.pA, e_dWe),
+                      gemm_fix<GW>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
+                      gemm_fix<GW>(shp_dWg(k, c.cnt), c.pD, e_dWg),
+                      gemm_fix<GW>(shp_dWp2(k, c.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC, c.adf}),
+                      gemm_fix<GW>(shp_dWe2(k, c.cnt), c.pF, EpiGradStore{G, c.L.we2, D + d, c.adf}));
   else
-    gemm_fixup_launch(nte + nmem + nst + nring + (c.adv ? 1 : 0), tail, s, gemm_fix<G32>(shp_dWe(k, c.cnt), c.pA, e_dWe),
-                      gemm_fix<G32>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<G32>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
-                      gemm_fix<G32>(shp_dWg(k, c.cnt), c.pD, e_dWg));
+    gemm_fixup_launch(nte + nmem + nst + nring + (c.adv ? 1 : 0), tail, s, gemm_fix<GW>(shp_dWe(k, c.cnt), c.pA, e_dWe),
+                      gemm_fix<GW>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
+                      gemm_fix<GW>(shp_dWg(k, c.cnt), c.pD, e_dWg));
   probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgn_fixup_update");
   return TGNX_OK;

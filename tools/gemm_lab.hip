@@ -288,6 +288,132 @@ __global__ void __launch_bounds__(256) gemm4_kernel(GemmShape g, AL al, BL bl, E
   }
 }
 
+
+// ------------------------------------------------------------------ candidate: small tile, wave-split-K
+// One TMxTN tile (TM, TN multiples of 16) per workgroup; the 256 threads load each KC-deep chunk (16-B
+// loads, LDS k-contiguous as gemm_tile); wave w multiplies the 16-deep slabs w, w + 4, ... of the chunk
+// into its own TMxTN accumulators; the four partial tiles are summed through LDS in wave order.
+template <int TM, int TN, int KC, int PF, class AL, class BL, class EPI>
+__global__ void __launch_bounds__(256) gemmk_kernel(GemmShape g, AL al, BL bl, EPI epi) {
+  constexpr int FM = TM / 16, FN = TN / 16, PK = KC + 4, PB = TN + 1;
+  constexpr int VA = TM * KC / 1024, VB = TN * KC / 1024, NSW = KC / 64;  // float4 per thread; slabs per wave
+  static_assert(VA >= 1 && VB >= 1 && KC % 64 == 0, "shape");
+  constexpr int SOP = (TM + TN) * PK, SRED = 5 * TM * PB + 512;
+  __shared__ __attribute__((aligned(16))) float smem[SOP > SRED ? SOP : SRED];
+  float* As = smem;
+  float* Bs = smem + TM * PK;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, li = lane & 15, lk = lane >> 4;
+  const int Mr = g.Mdev ? min(*g.Mdev, g.M) : g.M, Nr = g.N, Kr = g.K;
+  const int tmr = (Mr + TM - 1) / TM, tnr = (Nr + TN - 1) / TN, per = (tmr * tnr + 7) >> 3;
+  const int nchunk = (Kr + KC - 1) / KC;
+  for (int vb = blockIdx.x; vb < 8 * per; vb += gridDim.x) {
+    const GemmWork wk = gemm_work<TM, TN>(g, Mr, Nr, 1, vb);
+    const int m0 = wk.tm * TM, n0 = wk.tn * TN;
+    if (!wk.ok || m0 >= Mr || n0 >= Nr) continue;
+    using TA = LoaderTraits<AL>;
+    using TB = LoaderTraits<BL>;
+    typename TA::Idx ia[VA];
+    typename TB::Idx ib[VB];
+    const int mlast = Mr - 1, nlast = Nr - 1, k4last = (Kr - 1) & ~3;
+#pragma unroll
+    for (int i = 0; i < VA; ++i) ia[i] = TA::index(al, min(m0 + (tid + 256 * i) / (KC / 4), mlast), 0);
+#pragma unroll
+    for (int i = 0; i < VB; ++i) ib[i] = TB::index(bl, min(n0 + (tid + 256 * i) / (KC / 4), nlast), 0);
+    float4 ra[PF][VA], rb[PF][VB];
+    auto fetch = [&](float4* fa, float4* fb, int ch) {
+      const int k0 = ch * KC;
+#pragma unroll
+      for (int i = 0; i < VA; ++i) {
+        const int x = tid + 256 * i, r = x / (KC / 4), kk = 4 * (x % (KC / 4));
+        fa[i] = al.load4(ia[i], min(m0 + r, mlast), min(k0 + kk, k4last));
+      }
+#pragma unroll
+      for (int i = 0; i < VB; ++i) {
+        const int x = tid + 256 * i, r = x / (KC / 4), kk = 4 * (x % (KC / 4));
+        fb[i] = bl.load4(ib[i], min(n0 + r, nlast), min(k0 + kk, k4last));
+      }
+    };
+    auto stash = [&](const float4* fa, const float4* fb, int ch) {
+      const int kc = max(0, min(KC, Kr - ch * KC));
+#pragma unroll
+      for (int i = 0; i < VA; ++i) {
+        const int x = tid + 256 * i, r = x / (KC / 4), kk = 4 * (x % (KC / 4));
+        const bool rok = m0 + r <= mlast;
+        *reinterpret_cast<f32x4_t*>(As + r * PK + kk) =
+            f32x4_t{(rok && kk < kc) ? fa[i].x : 0.f, (rok && kk + 1 < kc) ? fa[i].y : 0.f,
+                    (rok && kk + 2 < kc) ? fa[i].z : 0.f, (rok && kk + 3 < kc) ? fa[i].w : 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < VB; ++i) {
+        const int x = tid + 256 * i, r = x / (KC / 4), kk = 4 * (x % (KC / 4));
+        const bool rok = n0 + r <= nlast;
+        *reinterpret_cast<f32x4_t*>(Bs + r * PK + kk) =
+            f32x4_t{(rok && kk < kc) ? fb[i].x : 0.f, (rok && kk + 1 < kc) ? fb[i].y : 0.f,
+                    (rok && kk + 2 < kc) ? fb[i].z : 0.f, (rok && kk + 3 < kc) ? fb[i].w : 0.f};
+      }
+    };
+    f32x4_t acc[2][FM][FN];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[h][i][j] = {0.f, 0.f, 0.f, 0.f};
+    auto mfma_chunk = [&]() {
+#pragma unroll
+      for (int u = 0; u < NSW; ++u) {
+        const int kk = 16 * (wv + 4 * u);
+        f32x4_t a[FM], b[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) a[i] = *reinterpret_cast<const f32x4_t*>(As + (16 * i + li) * PK + kk + 4 * lk);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) b[j] = *reinterpret_cast<const f32x4_t*>(Bs + (16 * j + li) * PK + kk + 4 * lk);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[q & 1][i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][q], b[j][q], acc[q & 1][i][j], 0, 0, 0);
+      }
+    };
+    const int last = max(nchunk, 1);
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+      if (p < last) fetch(ra[p], rb[p], p);
+    for (int c0 = 0; c0 < last; c0 += PF) {
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        const int ch = c0 + p;
+        if (ch < last) {
+          stash(ra[p], rb[p], ch);
+          __syncthreads();
+          if (ch + PF < last) fetch(ra[p], rb[p], ch + PF);
+          mfma_chunk();
+          __syncthreads();
+        }
+      }
+    }
+    float* red = smem;  // [4][TM][PB] wave partials, then Ct [TM][PB]
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          red[wv * TM * PB + (16 * i + 4 * lk + r) * PB + 16 * j + li] = acc[0][i][j][r] + acc[1][i][j][r];
+    __syncthreads();
+    float* Ct = red + 4 * TM * PB;
+    for (int x = tid; x < TM * TN; x += 256) {
+      const int r = x / TN, cc = x % TN, o = r * PB + cc;
+      Ct[o] = ((red[o] + red[TM * PB + o]) + red[2 * TM * PB + o]) + red[3 * TM * PB + o];
+    }
+    __syncthreads();
+    epi(GemmTile<TM, TN>{Ct, m0, n0, Mr, Nr, Ct + TM * PB});
+    __syncthreads();
+  }
+}
+
 // ---- per-workgroup timeline: {start, end} (s_memrealtime, 100 MHz), HW_ID, XCC_ID
 struct Stamp {
   unsigned long long t0, t1;
@@ -405,8 +531,11 @@ int main(int argc, char** argv) {
       check(name, us);
     };
     base(GemmCfg<32, 32, 64, 1>{}, "base 32x32 KC64 PF1");
-    base(GemmCfg<32, 32, 32, 2>{}, "base 32x32 KC32 PF2");
-    base(GemmCfg<32, 32, 128, 1>{}, "base 32x32 KC128 PF1");
+    base(GemmCfg<16, 16, 64, 1, true>{}, "lib WS 16x16 KC64 PF1 (scalar)");
+    base(GemmCfg<16, 16, 128, 1, true>{}, "lib WS 16x16 KC128 PF1 (scalar)");
+    base(GemmCfg<16, 32, 64, 1, true>{}, "lib WS 16x32 KC64 PF1 (scalar)");
+    base(GemmCfg<32, 16, 64, 1, true>{}, "lib WS 32x16 KC64 PF1 (scalar)");
+    base(GemmCfg<16, 16, 64, 2, true>{}, "lib WS 16x16 KC64 PF2 (scalar)");
     const LoadGather4 al4{{X, idx, K}};
     const LoadRowK4 bl4{{W, N, K, K}};
     auto v4 = [&](auto cfg, const char* name) {
@@ -414,22 +543,33 @@ int main(int argc, char** argv) {
       const GemmShape g = gemm_shape<CFG>(M, N, K);
       const float us = time_graph([&] { gemm4_kernel<CFG, false, false><<<gemm_blocks(g), 256, 0, st>>>(g, al4, bl4, epi); }, st);
       check(name, us);
-      const float u2 = time_graph([&] { gemm4_kernel<CFG, true, false><<<gemm_blocks(g), 256, 0, st>>>(g, al4, bl4, epi); }, st);
-      char nm[64];
-      snprintf(nm, sizeof nm, "%s unc", name);
-      check(nm, u2);
-      const float u3 = time_graph([&] { gemm4_kernel<CFG, true, true><<<gemm_blocks(g), 256, 0, st>>>(g, al4, bl4, epi); }, st);
-      snprintf(nm, sizeof nm, "%s unc+sb", name);
-      check(nm, u3);
     };
     if (K % 4 == 0) {
       v4(GemmCfg<32, 32, 64, 1>{}, "v4 32x32 KC64 PF1");
-      v4(GemmCfg<32, 32, 64, 2>{}, "v4 32x32 KC64 PF2");
       v4(GemmCfg<32, 32, 128, 1>{}, "v4 32x32 KC128 PF1");
       v4(GemmCfg<32, 32, 128, 2>{}, "v4 32x32 KC128 PF2");
-      v4(GemmCfg<32, 32, 32, 4>{}, "v4 32x32 KC32 PF4");
-      v4(GemmCfg<32, 32, 64, 3>{}, "v4 32x32 KC64 PF3");
-      v4(GemmCfg<32, 32, 32, 2>{}, "v4 32x32 KC32 PF2");
+      auto vk = [&](auto tm, auto tn, auto kc, auto pf, const char* name) {
+        constexpr int TM = decltype(tm)::value, TN = decltype(tn)::value, KC = decltype(kc)::value, PF = decltype(pf)::value;
+        const GemmShape g = gemm_shape<GemmCfg<32, 32, 64>>(M, N, K);
+        const int tiles = ((M + TM - 1) / TM) * ((N + TN - 1) / TN), nb = (tiles + 7) & ~7;
+        const float us = time_graph([&] { gemmk_kernel<TM, TN, KC, PF><<<nb, 256, 0, st>>>(g, al4, bl4, epi); }, st);
+        check(name, us);
+      };
+      using I16 = std::integral_constant<int, 16>;
+      using I32 = std::integral_constant<int, 32>;
+      using I64 = std::integral_constant<int, 64>;
+      using P1 = std::integral_constant<int, 1>;
+      using P2 = std::integral_constant<int, 2>;
+      vk(I16{}, I16{}, I64{}, P1{}, "wk 16x16 KC64 PF1");
+      vk(I16{}, I16{}, I64{}, P2{}, "wk 16x16 KC64 PF2");
+      vk(I16{}, I16{}, std::integral_constant<int, 128>{}, P1{}, "wk 16x16 KC128 PF1");
+      vk(I16{}, I16{}, std::integral_constant<int, 192>{}, P1{}, "wk 16x16 KC192 PF1");
+      vk(I16{}, I16{}, std::integral_constant<int, 128>{}, P2{}, "wk 16x16 KC128 PF2");
+      vk(I32{}, I16{}, I64{}, P1{}, "wk 32x16 KC64 PF1");
+      vk(I32{}, I16{}, std::integral_constant<int, 128>{}, P1{}, "wk 32x16 KC128 PF1");
+      vk(I16{}, I32{}, I64{}, P1{}, "wk 16x32 KC64 PF1");
+      vk(I32{}, I32{}, I64{}, P1{}, "wk 32x32 KC64 PF1");
+      vk(I32{}, I32{}, std::integral_constant<int, 128>{}, P1{}, "wk 32x32 KC128 PF1");
     }
     auto wsk = [&](auto tm, auto tn, auto pd, const char* name) {
       constexpr int TM = decltype(tm)::value, TN = decltype(tn)::value, PD = decltype(pd)::value;
@@ -441,7 +581,6 @@ int main(int argc, char** argv) {
     using I16 = std::integral_constant<int, 16>;
     using I32 = std::integral_constant<int, 32>;
     using I64 = std::integral_constant<int, 64>;
-    wsk(I32{}, I32{}, std::integral_constant<int, 2>{}, "wsplitK 32x32 PD2");
     CK(hipFree(X));
     CK(hipFree(W));
     CK(hipFree(C));
