@@ -171,6 +171,7 @@ struct LoaderTraits {  // plain loader
   static constexpr bool row_idx = true;
   __device__ static Idx index(const L&, int, int) { return 0; }
   __device__ static float load(const L& l, const Idx&, int r, int k) { return l(r, k); }
+  __device__ static float4 load4(const L& l, const Idx&, int r, int k) { return l.load4(r, k); }
 };
 template <class L>
 struct LoaderTraits<L, std::void_t<typename L::Idx>> {  // two-phase gather
@@ -178,7 +179,26 @@ struct LoaderTraits<L, std::void_t<typename L::Idx>> {  // two-phase gather
   static constexpr bool row_idx = L::row_idx;
   __device__ static Idx index(const L& l, int r, int k) { return l.index(r, k); }
   __device__ static float load(const L& l, const Idx& i, int r, int k) { return l.load(i, r, k); }
+  __device__ static float4 load4(const L& l, const Idx& i, int r, int k) { return l.load4(i, r, k); }
 };
+// 16-B operand loads.  A k_fast loader may also provide `bool vec4() const` (runtime: every k segment
+// of its rows starts at a multiple of 4 floats and every row is 16-B aligned) and `load4` (elements k..k+3
+// of row r, k % 4 == 0, one global_load_dwordx4).  When vec4() holds for both operands and K % 4 == 0,
+// the body fetches such operands 4 k per lane (a quarter of the load instructions; ~1 us per launch on
+// the TGN GEMMs, tools/gemm_lab.hip) and stashes them with one ds_write_b128.
+#ifndef TGNX_GEMM_VEC4
+#define TGNX_GEMM_VEC4 1
+#endif
+template <class L, class = void>
+struct HasVec4 : std::false_type {};
+template <class L>
+struct HasVec4<L, std::void_t<decltype(std::declval<const L&>().vec4())>> : std::integral_constant<bool, L::k_fast> {};
+template <class L>
+__device__ __forceinline__ bool vec_ok(const L& l) {
+  if constexpr (HasVec4<L>::value) return l.vec4();
+  else return true;
+}
+__device__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // Row-major operand: element (r, k) at p[r * ld + k]  (k_fast).  rows x ks bound the buffer (the body
 // clamps r, k to the GEMM's runtime bounds, which every call site keeps within it).
@@ -187,6 +207,10 @@ struct LoadRowK {
   int rows, ks, ld;
   static constexpr bool k_fast = true;
   __device__ float operator()(int r, int k) const { return p[(int64_t)min(r, rows - 1) * ld + min(k, ks - 1)]; }
+  __device__ bool vec4() const { return (ld & 3) == 0 && (ks & 3) == 0 && al16(p); }
+  __device__ float4 load4(int r, int k) const {
+    return *reinterpret_cast<const float4*>(p + (int64_t)min(r, rows - 1) * ld + min(k, ks - 4));
+  }
 };
 // Transposed operand: element (r, k) at p[k * ld + r]  (r fast)
 struct LoadKRow {
@@ -259,7 +283,7 @@ __device__ __forceinline__ GemmWork gemm_work(const GemmShape& g, int Mr, int Nr
 }
 
 // One work item (virtual block `bid` of the XCD-grouped order) of a GEMM; `smem` holds CFG::SMEM floats.
-template <class CFG, class AL, class BL, class EPI>
+template <class CFG, bool V, class AL, class BL, class EPI>
 __device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, const AL& al, const BL& bl,
                                           const EPI& epi, float* part, int bid, float* smem) {
   constexpr int TM = CFG::TM, TN = CFG::TN, KC = CFG::KC, FM = CFG::FM, FN = CFG::FN;
@@ -285,49 +309,91 @@ __device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, 
   using TB = LoaderTraits<BL>;
   typename TA::Idx ia[LA];
   typename TB::Idx ib[LB];
-  const int mlast = rt.Mr - 1, nlast = rt.Nr - 1, klast = max(rt.Kr - 1, 0);
+  const int mlast = rt.Mr - 1, nlast = rt.Nr - 1, klast = max(rt.Kr - 1, 0), k4last = max(rt.Kr - 4, 0);
+  // 16-B operands (V: vec_ok for both and K % 4 == 0): item i of the thread = float4 (row x / (KC/4),
+  // k 4 (x % (KC/4))), x = tid + 256 i
+  constexpr bool AV = V && HasVec4<AL>::value, BV = V && HasVec4<BL>::value;
+  static_assert(!AV || TA::row_idx, "16-B loads need a row index");
+  static_assert(!BV || TB::row_idx, "16-B loads need a row index");
   // index phase (every index load of the operand issued before any data load)
   auto index_a = [&](int k0) {
+    if constexpr (AV) {
 #pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      int r, kk;
-      gemm_map<AL::k_fast, TM, KC>(tid, i, r, kk);
-      ia[i] = TA::index(al, min(m0 + r, mlast), min(k0 + kk, klast));
+      for (int i = 0; i < LA / 4; ++i) ia[i] = TA::index(al, min(m0 + (tid + 256 * i) / (KC / 4), mlast), 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < LA; ++i) {
+        int r, kk;
+        gemm_map<AL::k_fast, TM, KC>(tid, i, r, kk);
+        ia[i] = TA::index(al, min(m0 + r, mlast), min(k0 + kk, klast));
+      }
     }
   };
   auto index_b = [&](int k0) {
+    if constexpr (BV) {
 #pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      int r, kk;
-      gemm_map<BL::k_fast, TN, KC>(tid, i, r, kk);
-      ib[i] = TB::index(bl, min(n0 + r, nlast), min(k0 + kk, klast));
+      for (int i = 0; i < LB / 4; ++i) ib[i] = TB::index(bl, min(n0 + (tid + 256 * i) / (KC / 4), nlast), 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < LB; ++i) {
+        int r, kk;
+        gemm_map<BL::k_fast, TN, KC>(tid, i, r, kk);
+        ib[i] = TB::index(bl, min(n0 + r, nlast), min(k0 + kk, klast));
+      }
     }
   };
   if (TA::row_idx) index_a(0);
   if (TB::row_idx) index_b(0);
   // chunk ch -> registers: clamped in-range loads (out-of-range elements are zeroed in stash)
   auto fetch = [&](float* fa, float* fb, int ch) {
-    const int k0 = ch * KC, kc = max(0, min(KC, rt.Kr - k0));
+    const int k0 = ch * KC;
     if (!TA::row_idx) index_a(k0);
     if (!TB::row_idx) index_b(k0);
+    if constexpr (AV) {
 #pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      int r, kk;
-      gemm_map<AL::k_fast, TM, KC>(tid, i, r, kk);
-      fa[i] = TA::load(al, ia[i], min(m0 + r, mlast), min(k0 + kk, klast));
+      for (int i = 0; i < LA / 4; ++i) {
+        const int x = tid + 256 * i;
+        const float4 v = TA::load4(al, ia[i], min(m0 + x / (KC / 4), mlast), min(k0 + 4 * (x % (KC / 4)), k4last));
+        fa[4 * i] = v.x; fa[4 * i + 1] = v.y; fa[4 * i + 2] = v.z; fa[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LA; ++i) {
+        int r, kk;
+        gemm_map<AL::k_fast, TM, KC>(tid, i, r, kk);
+        fa[i] = TA::load(al, ia[i], min(m0 + r, mlast), min(k0 + kk, klast));
+      }
     }
+    if constexpr (BV) {
 #pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      int r, kk;
-      gemm_map<BL::k_fast, TN, KC>(tid, i, r, kk);
-      fb[i] = TB::load(bl, ib[i], min(n0 + r, nlast), min(k0 + kk, klast));
+      for (int i = 0; i < LB / 4; ++i) {
+        const int x = tid + 256 * i;
+        const float4 v = TB::load4(bl, ib[i], min(n0 + x / (KC / 4), nlast), min(k0 + 4 * (x % (KC / 4)), k4last));
+        fb[4 * i] = v.x; fb[4 * i + 1] = v.y; fb[4 * i + 2] = v.z; fb[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < LB; ++i) {
+        int r, kk;
+        gemm_map<BL::k_fast, TN, KC>(tid, i, r, kk);
+        fb[i] = TB::load(bl, ib[i], min(n0 + r, nlast), min(k0 + kk, klast));
+      }
     }
   };
   // registers -> LDS, zeroing elements outside the runtime bounds (rlast: last valid row of the tile
   // origin r0; kc: valid k of the chunk)
-  auto stash1 = [&](float* S, const float* rv, auto kfast, auto rows, auto cnt, int r0, int rlast, int kc) {
-    constexpr int ROWS = decltype(rows)::value, CNT = decltype(cnt)::value;
-    if constexpr (decltype(kfast)::value) {
+  auto stash1 = [&](float* S, const float* rv, auto mode, auto rows, auto cnt, int r0, int rlast, int kc) {
+    constexpr int ROWS = decltype(rows)::value, CNT = decltype(cnt)::value, MODE = decltype(mode)::value;
+    if constexpr (MODE == 2) {  // 16-B items
+#pragma unroll
+      for (int i = 0; i < CNT / 4; ++i) {
+        const int x = tid + 256 * i, r = x / (KC / 4), kk = 4 * (x % (KC / 4));
+        const bool rok = r0 + r <= rlast;
+        *reinterpret_cast<f32x4_t*>(S + r * PK + kk) =
+            f32x4_t{(rok && kk < kc) ? rv[4 * i] : 0.f, (rok && kk + 1 < kc) ? rv[4 * i + 1] : 0.f,
+                    (rok && kk + 2 < kc) ? rv[4 * i + 2] : 0.f, (rok && kk + 3 < kc) ? rv[4 * i + 3] : 0.f};
+      }
+    } else if constexpr (MODE == 1) {  // k-fast scalars
 #pragma unroll
       for (int i = 0; i < CNT; ++i) {
         int r, kk;
@@ -348,9 +414,9 @@ __device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, 
   };
   auto stash = [&](const float* fa, const float* fb, int ch) {
     const int kc = max(0, min(KC, rt.Kr - ch * KC));
-    stash1(As, fa, std::integral_constant<bool, AL::k_fast>{}, std::integral_constant<int, TM>{},
+    stash1(As, fa, std::integral_constant<int, AV ? 2 : AL::k_fast ? 1 : 0>{}, std::integral_constant<int, TM>{},
            std::integral_constant<int, LA>{}, m0, mlast, kc);
-    stash1(Bs, fb, std::integral_constant<bool, BL::k_fast>{}, std::integral_constant<int, TN>{},
+    stash1(Bs, fb, std::integral_constant<int, BV ? 2 : BL::k_fast ? 1 : 0>{}, std::integral_constant<int, TN>{},
            std::integral_constant<int, LB>{}, n0, nlast, kc);
   };
   // k permutation inside a 16-deep slab: MFMA step q of lane (li, lk) takes k = 4 lk + q, so each
@@ -463,8 +529,17 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
   const GemmRt rt = gemm_runtime<CFG>(g);
   const int tmr = (rt.Mr + CFG::TM - 1) / CFG::TM, tnr = (rt.Nr + CFG::TN - 1) / CFG::TN;
   const int per = (tmr * tnr * rt.Sr + 7) >> 3, grid = gemm_blocks(g);
+  if constexpr (TGNX_GEMM_VEC4 && (HasVec4<AL>::value || HasVec4<BL>::value)) {
+    if ((rt.Kr & 3) == 0 && rt.Kr >= 4 && vec_ok(al) && vec_ok(bl)) {
+      for (int vb = bid; vb < 8 * per; vb += grid) {
+        gemm_tile<CFG, true>(g, rt, al, bl, epi, part, vb, smem);
+        __syncthreads();
+      }
+      return;
+    }
+  }
   for (int vb = bid; vb < 8 * per; vb += grid) {
-    gemm_tile<CFG>(g, rt, al, bl, epi, part, vb, smem);
+    gemm_tile<CFG, false>(g, rt, al, bl, epi, part, vb, smem);
     __syncthreads();
   }
 }

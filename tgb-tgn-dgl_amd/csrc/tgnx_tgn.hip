@@ -1045,6 +1045,11 @@ struct LoadGruA {
     const float* p = k < Qm ? X + (int64_t)m * Qm + k : mem + v * D + (k - Qm);
     return *p;
   }
+  __device__ bool vec4() const { return ((Qm | D) & 3) == 0 && al16(X) && al16(mem); }
+  __device__ float4 load4(Idx v, int m, int k) const {
+    const float* p = k < Qm ? X + (int64_t)m * Qm + k : mem + v * D + (k - Qm);
+    return *reinterpret_cast<const float4*>(p);
+  }
 };
 // GRU weights with gates interleaved by unit: row 4j+g = (r, z, n_input, n_hidden) of unit j over
 // the columns [message | memory] (GRUCell weight_ih [3D, Qm], weight_hh [3D, D]).
@@ -1059,6 +1064,16 @@ struct LoadGruW {
     const bool zero = ih ? g == 3 : g == 2;
     const float* p = ih ? wih + (int64_t)(gr * D + j) * Qm + k : whh + (int64_t)(gr * D + j) * D + (k - Qm);
     return *p * f01(!zero);
+  }
+  __device__ bool vec4() const { return ((Qm | D) & 3) == 0 && al16(wih) && al16(whh); }
+  __device__ float4 load4(int n, int k) const {
+    const int j = n >> 2, g = n & 3;
+    const bool ih = k < Qm;
+    const int gr = ih ? min(g, 2) : (g == 3 ? 2 : g);
+    const float z = f01(!(ih ? g == 3 : g == 2));
+    const float* p = ih ? wih + (int64_t)(gr * D + j) * Qm + k : whh + (int64_t)(gr * D + j) * D + (k - Qm);
+    const float4 w = *reinterpret_cast<const float4*>(p);
+    return make_float4(w.x * z, w.y * z, w.z * z, w.w * z);
   }
 };
 // GRUCell (torch gru_cell: r, z = σ(gi + gh), n = tanh(gi_n + r gh_n), h' = (h - n) z + n)
@@ -1104,6 +1119,11 @@ struct LoadEdgeAttr {
     const float* p = k < D ? enc + (int64_t)e * D + k : ev_msg + id * d + (k - D);
     return *p;
   }
+  __device__ bool vec4() const { return ((D | d) & 3) == 0 && al16(enc) && al16(ev_msg); }
+  __device__ float4 load4(Idx id, int e, int k) const {
+    const float* p = k < D ? enc + (int64_t)e * D + k : ev_msg + id * d + (k - D);
+    return *reinterpret_cast<const float4*>(p);
+  }
 };
 // same operand with rows / columns swapped (B operand of dW_edge = dEᵀ EA)
 struct LoadEdgeAttrT {
@@ -1134,6 +1154,11 @@ struct LoadEdgeAttrMap {
     const float* p = k < D ? enc + (int64_t)r.e2 * D + k : ev_msg + r.id * d + (k - D);
     return *p;
   }
+  __device__ bool vec4() const { return ((D | d) & 3) == 0 && al16(enc) && al16(ev_msg); }
+  __device__ float4 load4(const Idx& r, int, int k) const {
+    const float* p = k < D ? enc + (int64_t)r.e2 * D + k : ev_msg + r.id * d + (k - D);
+    return *reinterpret_cast<const float4*>(p);
+  }
 };
 struct LoadEdgeAttrMapT {
   LoadEdgeAttrMap a;
@@ -1160,6 +1185,11 @@ struct LoadZ {
     const float* p = eval ? mem + v * D + k : Z0 + (int64_t)m * D + k;
     return *p;
   }
+  __device__ bool vec4() const { return (D & 3) == 0 && al16(Z0) && al16(mem); }
+  __device__ float4 load4(Idx v, int m, int k) const {
+    const float* p = eval ? mem + v * D + k : Z0 + (int64_t)m * D + k;
+    return *reinterpret_cast<const float4*>(p);
+  }
 };
 // row n < 4 HC of the stacked projections [q; k; v; skip] -> (linear g, row r): compares, not an integer
 // division (a ~40-instruction routine per element inside the GEMM loaders' K loop)
@@ -1173,6 +1203,11 @@ struct LoadProjW {
   __device__ float operator()(int n, int k) const {
     const int g = proj_g(n, HC), r = n - g * HC;
     return w[g * pw + (int64_t)r * D + k];
+  }
+  __device__ bool vec4() const { return ((D | (int)pw) & 3) == 0 && al16(w); }
+  __device__ float4 load4(int n, int k) const {
+    const int g = proj_g(n, HC), r = n - g * HC;
+    return *reinterpret_cast<const float4*>(w + g * pw + (int64_t)r * D + k);
   }
 };
 struct EpiProj {
