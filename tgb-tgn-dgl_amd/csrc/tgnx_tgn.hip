@@ -226,6 +226,10 @@ __device__ __forceinline__ float softplusf(float x) { return fmaxf(x, 0.f) + log
 // found the word empty), so tgn_scan visits only the words that hold nodes: O(sampled + N / 1024)
 // instead of O(N / 32) per batch (a single-workgroup walk of a 1M-node bitmap took ~40 us per pass).
 // Plain read first: hub words are hit by many lanes, most find the bit set.
+// tgn_scan walks every bitmap word of a small graph directly (<= 2 words per thread of its 1024) and
+// the nonzero words of a large one from the summary bitmaps; mark sets summary bits only for the latter
+constexpr int TGN_SCAN_THREADS = 1024;
+__host__ __device__ __forceinline__ bool scan_direct(int64_t words) { return words <= 2 * (int64_t)TGN_SCAN_THREADS; }
 __device__ __forceinline__ void mark_node(uint32_t* bm, uint32_t* sum, int64_t v) {
   const int64_t w = v >> 5;
   const uint32_t bit = 1u << (v & 31);
@@ -304,17 +308,38 @@ __global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
       const int x = q - 2 * nl;
       v = c.neg[(start + x / Kn) * Kn + x % Kn];
     }
+    // every load of the entry before any atomic (vmcnt retires in issue order: a load issued after an
+    // atomic waits for it), atomics without return: a lane sets a bit its plain read found clear, and the
+    // word's summary bit only when that read found the whole word zero (a nonzero word was seen after an
+    // atomic of a lane that found it zero, which set the summary; the bitmaps start the batch cleared).
+    // The chain is entry -> ring slot -> neighbour word -> atomics.
+    const int64_t vw = v >> 5;
+    const uint32_t vbit = 1u << (v & 31);
+    const bool summ = !scan_direct(c.words);
+    uint32_t wcv = 0u, wnv = 0u, wrv = 0u;
+    if (sl == 0) {
+      wcv = c.cb[vw];
+      wnv = c.nb[vw];
+      if (c.layers == 2) wrv = c.rb[vw];
+    }
     int k = 0;
     for (int j0 = 0; j0 < c.K; j0 += 16) {
-      const int j = j0 + sl;
-      const bool ok = j < c.K && c.eid[v * c.K + j] >= 0;
-      if (ok) {  // plain read first: hub words are hit by many lanes, most find the bit set
-        const int64_t u = c.nbr[v * c.K + j];
-        mark_node(c.nb, c.nbs, u);
+      const int j = j0 + sl, jc = min(j, c.K - 1);
+      const int64_t ej = c.eid[v * c.K + jc], u = c.nbr[v * c.K + jc];
+      const bool ok = j < c.K && ej >= 0;
+      const int64_t uw = ok ? (u >> 5) : vw;
+      const uint32_t ubit = 1u << (u & 31);
+      const uint32_t wu = c.nb[uw];
+      uint32_t wcu = 0u;
+      if (c.layers == 2) wcu = c.cb[uw];
+      if (ok) {
+        if (!(wu & ubit)) atomicOr(&c.nb[uw], ubit);
+        if (summ && !wu) atomicOr(&c.nbs[uw >> 5], 1u << (uw & 31));
         if (c.layers == 2) {
+          if (!(wcu & ubit)) atomicOr(&c.cb[uw], ubit);
+          if (summ && !wcu) atomicOr(&c.cbs[uw >> 5], 1u << (uw & 31));
           // 2 hops: the neighbour is an outer centre; its own ring neighbours are sampled nodes
           // (the lane walks u's ring row, all K slot loads issued before the marking)
-          mark_node(c.cb, c.cbs, u);
           int ku = 0;
           for (int i0 = 0; i0 < c.K; i0 += 8) {
             int64_t ev[8], w[8];
@@ -328,8 +353,7 @@ __global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
             for (int i = 0; i < 8; ++i) {
               if (i0 + i >= c.K || ev[i] < 0) continue;
               ++ku;
-              const int64_t x = w[i];
-              mark_node(c.nb, c.nbs, x);
+              mark_node(c.nb, c.nbs, w[i]);
             }
           }
           c.kval[u] = ku;
@@ -340,9 +364,14 @@ __global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
     if (sl == 0) {
       if (q < 2 * nl) c.node_gen[v] = gen;
       c.kval[v] = k;
-      mark_node(c.cb, c.cbs, v);
-      mark_node(c.nb, c.nbs, v);
-      if (c.layers == 2) mark_node(c.rb, c.rbs, v);
+      if (!(wcv & vbit)) atomicOr(&c.cb[vw], vbit);
+      if (summ && !wcv) atomicOr(&c.cbs[vw >> 5], 1u << (vw & 31));
+      if (!(wnv & vbit)) atomicOr(&c.nb[vw], vbit);
+      if (summ && !wnv) atomicOr(&c.nbs[vw >> 5], 1u << (vw & 31));
+      if (c.layers == 2) {
+        if (!(wrv & vbit)) atomicOr(&c.rb[vw], vbit);
+        if (summ && !wrv) atomicOr(&c.rbs[vw >> 5], 1u << (vw & 31));
+      }
     }
   }
 }
@@ -452,7 +481,7 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
   const int gen = (int)c.ctl[TGNX_CTL_GEN] + (c.adv ? 1 : 0);  // cursor folded into mark: counters advance at the end
   // pass 0: the words each thread walks.  Small graphs (<= 2 words per thread): contiguous word ranges
   // (summaries just cleared); large graphs: the nonzero words in word order, from the summaries
-  const bool direct = c.words <= 2 * (int64_t)T;
+  const bool direct = scan_direct(c.words);
   int ncw, nnw, nrw = 0;
   if (direct) {
     ncw = nnw = (int)c.words;
@@ -2887,7 +2916,7 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   }
   TGNX_LAUNCH_CHECK("tgn_mark");
   probe_begin(TGNX_K_ASSEMBLE, s);
-  tgn_scan<true><<<1, 1024, 0, s>>>(c);  // plans: in tgn_mark
+  tgn_scan<true><<<1, TGN_SCAN_THREADS, 0, s>>>(c);  // plans: in tgn_mark
   probe_end(TGNX_K_ASSEMBLE, s);
   TGNX_LAUNCH_CHECK("tgn_scan");
   const int nedge = gridn((int64_t)k.Rtr * c.K, 4, TGNX_AGG_EDGE_CAP);
@@ -3092,7 +3121,7 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
     tgn_mark<false><<<nmark, 256, 0, s>>>(c, nmark);
   }
   TGNX_LAUNCH_CHECK("tgn_mark");
-  tgn_scan<false><<<3, 1024, tgn_scan_smem(k.B), s>>>(c);
+  tgn_scan<false><<<3, TGN_SCAN_THREADS, tgn_scan_smem(k.B), s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_scan");
   const int nedge = gridn((int64_t)Rq * c.K, 4, 4096);
   tgn_agg_emit<<<nedge + gridn(Mq, 256), 256, 0, s>>>(c, 1, nedge, nullptr, nullptr, 0, 0);
