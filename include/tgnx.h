@@ -329,14 +329,27 @@ int tgnx_tgn_train_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf,
  * same as tgnx_tgnn_advance(ctl, mode 1, ..., split_lo, split_hi, batch, rank, world, base_seed,
  * train 1) followed by tgnx_tgn_train_step(gen_neg 1), one launch fewer.  World 1 only (Adam is folded
  * in as well; world > 1 is refused), split_hi <= num_events.
- * ctl words, in stream order: the step's first launch writes the batch descriptor (BATCH_START, B,
- * CUR_EID, LO, HI, SEED) from the unchanged counters; the step's LAST launch advances NB, GEN and (when
- * B > 0) ADAM_T.  So once the call's work has completed, ctl equals what advance + step leave; between
+ * ctl words, in stream order: the step's second launch (the scan) writes the batch descriptor
+ * (BATCH_START, B, CUR_EID, LO, HI, SEED) from the unchanged counters; the step's LAST launch advances NB,
+ * GEN and (when B > 0) ADAM_T.  So once the call's work has completed, ctl equals what advance + step leave; between
  * the two (e.g. a kernel of the caller's own, enqueued in between) the counters still hold the previous
  * step's values, whereas tgnx_tgnn_advance has already advanced them. */
 int tgnx_tgn_train_step_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
                                  int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
                                  int32_t dropout, void* stream);
+/* tgnx_tgn_train_step_resident (world 1) pipelined across steps: the step marks the NEXT batch of the split
+ * inside its predictor launch (its ring insert now runs beside the GRU, before that) and scans it after its
+ * own last launch, so the next pipelined call starts at the message aggregation: two launches fewer per
+ * step on the critical path.  prefetched = 1: the previous call on these buffers was a pipelined step with
+ * the same split / batch / seed and nothing else ran on them since; prefetched = 0: mark + scan this batch
+ * first (the first step, or after any other call: eval, flush, reset, another train form, a new cursor).
+ * Results equal tgnx_tgn_train_step_resident's step for step (same batches, negatives, dropout streams).
+ * ctl after the call: NB / GEN / ADAM_T advanced as for the resident step; the batch descriptor words
+ * (BATCH_START .. SEED) and SUM_E / SUM_S already describe / include the NEXT batch, and neg[] holds the
+ * next batch's negatives.  Test: tests/test_gpu_tgn.py (pipelined vs resident). */
+int tgnx_tgn_train_step_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                                  int64_t split_hi, int64_t batch, uint64_t base_seed, int32_t dropout,
+                                  int32_t prefetched, void* stream);
 /* Data parallel form: tgnx_tgn_train_fwd_bwd with the folded cursor (the exchange, tgnx_tgn_apply_rows and
  * tgnx_tgn_train_update follow).  ctl words as for tgnx_tgn_train_step_resident: the descriptor is written
  * by the first launch, NB / GEN / ADAM_T advance in the last launch of THIS call, so they have advanced

@@ -232,6 +232,7 @@ def test_tgn_resident_folded_cursor_equals_advance_plus_step():
         s, ref, opt_ref, lref, model, opt, eng = _setup("last")
         model.cfg.dropout = 0.1
         eng.fold_cursor = fold
+        eng.pipeline = False
         eng.bind_resident(0, 7 * 50 + 20, 50, dropout=True)   # the last batch is partial (20 events)
         eng.begin_epoch()
         engines.append((model, opt, eng))
@@ -254,6 +255,56 @@ def test_tgn_resident_folded_cursor_equals_advance_plus_step():
             o, n, _ = m1._views[name]
             assert _rel(m1.flat[o:o + n], m2.flat[o:o + n]) < 1e-4, (st, name)
         assert torch.allclose(m1.memory.memory, m2.memory.memory, atol=1e-5), st
+        assert abs(e1.loss_sum() - e2.loss_sum()) <= 1e-5 * max(1.0, abs(e2.loss_sum())), st
+        with torch.no_grad():
+            m1.flat.copy_(m2.flat)
+            o1.exp_avg.copy_(o2.exp_avg)
+            o1.exp_avg_sq.copy_(o2.exp_avg_sq)
+            m1.memory.memory.copy_(m2.memory.memory)
+
+
+@pytest.mark.parametrize("layers", [1, 2])
+def test_tgn_pipelined_equals_resident(layers):
+    """tgnx_tgn_train_step_pipelined (each step marks the next batch inside its predictor launch and scans it
+    after its last launch; ring insert beside the GRU) against tgnx_tgn_train_step_resident on a twin
+    engine: graph replay (the first step eager with prefetched = 0), device negatives, attention dropout,
+    a partial last batch and a step past the split.  After every step: step counters and the ring exactly,
+    this batch's negatives exactly (the pipelined engine has drawn the next batch's too), outputs,
+    parameters and memory within the fused-Adam tolerances (resynchronised per step)."""
+    engines = []
+    for pipe in (True, False):
+        s, ref, opt_ref, lref, model, opt, eng = _setup("last", layers=layers)
+        model.cfg.dropout = 0.1
+        eng.pipeline = pipe
+        eng.bind_resident(0, 7 * 50 + 20, 50, dropout=True)   # the last batch is partial (20 events)
+        eng.begin_epoch()
+        if pipe:
+            eng.capture_resident()
+        engines.append((model, opt, eng))
+    (m1, o1, e1), (m2, o2, e2) = engines
+    for st in range(9):                                        # 8 batches, then one past the split (B = 0)
+        e1.replay_resident()
+        e2.resident_train_step()
+        torch.cuda.synchronize()
+        e1.check()
+        e2.check()
+        for w in (3, 4, 10):                                   # GEN, ADAM_T, NB
+            assert int(e1.ctl[w]) == int(e2.ctl[w]), (st, w, int(e1.ctl[w]), int(e2.ctl[w]))
+        B, start = int(e2.ctl[2]), int(e2.ctl[0])
+        assert torch.equal(e1.neg_train[:start + B], e2.neg_train[:start + B]), st
+        for a, b in ((e1.loader.neighbors, e2.loader.neighbors), (e1.loader.e_id, e2.loader.e_id),
+                     (e1.loader.t, e2.loader.t)):
+            assert torch.equal(a, b), st
+        if B:
+            assert torch.allclose(e1.out_pos[:B], e2.out_pos[:B], atol=1e-5), st
+            assert torch.allclose(e1.out_neg[:B], e2.out_neg[:B], atol=1e-5), st
+        for name in m1.param_order:
+            if name in SHIFT_INVARIANT:
+                continue
+            o, n, _ = m1._views[name]
+            assert _rel(m1.flat[o:o + n], m2.flat[o:o + n]) < 1e-4, (st, name)
+        assert torch.allclose(m1.memory.memory, m2.memory.memory, atol=1e-5), st
+        assert torch.equal(m1.memory.last_update, m2.memory.last_update), st
         assert abs(e1.loss_sum() - e2.loss_sum()) <= 1e-5 * max(1.0, abs(e2.loss_sum())), st
         with torch.no_grad():
             m1.flat.copy_(m2.flat)

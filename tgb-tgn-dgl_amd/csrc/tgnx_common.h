@@ -210,6 +210,7 @@ __device__ __forceinline__ uint64_t bitonic_lane_stage(uint64_t v, int i, int k)
 __device__ __forceinline__ void sort_u64_reg(uint64_t* key, uint64_t* tmp, int n) {
   const int i = threadIdx.x;
   uint64_t v = i < n ? key[i] : ~0ull;
+  const int wn = (n + WAVE - 1) & ~(WAVE - 1);  // whole waves holding keys
   int flip = 0;
   for (int k = 2; k <= n; k <<= 1) {
     for (int j = k >> 1; j >= WAVE; j >>= 1) {
@@ -221,23 +222,66 @@ __device__ __forceinline__ void sort_u64_reg(uint64_t* key, uint64_t* tmp, int n
       const bool take_min = ((i & j) == 0) == ((i & k) == 0);
       v = take_min ? (o < v ? o : v) : (o > v ? o : v);
     }
-    switch (k >= 64 ? 32 : k >> 1) {  // remaining distances 32..1 (wave-uniform)
-      case 32: v = bitonic_lane_stage<32>(v, i, k); [[fallthrough]];
-      case 16: v = bitonic_lane_stage<16>(v, i, k); [[fallthrough]];
-      case 8: v = bitonic_lane_stage<8>(v, i, k); [[fallthrough]];
-      case 4: v = bitonic_lane_stage<4>(v, i, k); [[fallthrough]];
-      case 2: v = bitonic_lane_stage<2>(v, i, k); [[fallthrough]];
-      default: v = bitonic_lane_stage<1>(v, i, k);
-    }
+    if (i < wn)  // waves past the keys skip the lane stages (a 1024-thread block sorting 512 keys)
+      switch (k >= 64 ? 32 : k >> 1) {  // remaining distances 32..1 (wave-uniform)
+        case 32: v = bitonic_lane_stage<32>(v, i, k); [[fallthrough]];
+        case 16: v = bitonic_lane_stage<16>(v, i, k); [[fallthrough]];
+        case 8: v = bitonic_lane_stage<8>(v, i, k); [[fallthrough]];
+        case 4: v = bitonic_lane_stage<4>(v, i, k); [[fallthrough]];
+        case 2: v = bitonic_lane_stage<2>(v, i, k); [[fallthrough]];
+        default: v = bitonic_lane_stage<1>(v, i, k);
+      }
   }
   __syncthreads();
   if (i < n) key[i] = v;
   __syncthreads();
 }
 
+// Rank sort of n DISTINCT uint64 keys (n <= blockDim.x): key i goes to position #{j : key[j] < key[i]}.
+// Two threads per key when the block has them (adjacent lanes, each counting half the keys from LDS
+// broadcast reads, 2 keys per ds_read_b128).  n^2 compares, but no dependent stages: 400 keys (a
+// B = 200 ring / store plan) take ~1 us against ~5.5 us for the 39 lane + 6 LDS stages of the bitonic
+// network (stamps timeline).  `tmp` holds n keys; the result is in key[0, n).
+__device__ __forceinline__ void sort_u64_rank(uint64_t* key, uint64_t* tmp, int n) {
+  const int P = 2 * n <= (int)blockDim.x ? 2 : 1;
+  const int i = threadIdx.x / P, h = threadIdx.x % P;
+  const int half = ((n + 3) >> 2) << 1;  // even split point (16-B aligned pairs)
+  if (i < n) {
+    const uint64_t v = key[i];
+    const int j0 = P == 2 ? h * half : 0, j1 = P == 2 ? (h ? n : min(half, n)) : n;
+    // 16 keys (8 ds_read_b128) in flight per round: a read-use chain per key pair waited the LDS latency
+    // (~6.5 us for 400 keys, stamps timeline)
+    int r = 0;
+    int j = j0;
+    for (; j + 15 < j1; j += 16) {
+      uint64_t a[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) a[u] = key[j + u];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) r += a[u] < v;
+    }
+    for (; j < j1; ++j) r += key[j] < v;
+    if (P == 2) r += __shfl_xor(r, 1, WAVE);
+    if (h == 0) tmp[r] = v;
+  }
+  __syncthreads();
+  for (int x = threadIdx.x; x < n; x += blockDim.x) key[x] = tmp[x];
+  __syncthreads();
+}
+
 // Sort n uint64 keys in LDS, ascending, by the whole block (key[n, n_pow2) padded with ~0 on
 // return): register bitonic when n_pow2 <= blockDim.x (`tmp` holds n_pow2 keys), LDS bitonic above.
-__device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, int n_pow2) {
+// `distinct`: the keys are pairwise distinct and n <= blockDim.x -> rank sort.
+__device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, int n_pow2, bool distinct = false) {
+#ifdef TGNX_DIAG_NOSORT  // timing experiment only: results wrong
+  if (distinct) return;
+#endif
+  if (distinct && n <= (int)blockDim.x) {
+    sort_u64_rank(key, tmp, n);
+    for (int i = n + threadIdx.x; i < n_pow2; i += blockDim.x) key[i] = ~0ull;
+    __syncthreads();
+    return;
+  }
   for (int i = n + threadIdx.x; i < n_pow2; i += blockDim.x) key[i] = ~0ull;
   __syncthreads();
   if (n_pow2 <= (int)blockDim.x) sort_u64_reg(key, tmp, n_pow2);

@@ -588,17 +588,18 @@ __device__ __forceinline__ bool gemm_job_dispatch(const J& j, int& bid, float* s
   bid -= nb;
   return false;
 }
-// a non-GEMM piece of work riding in a gemmN launch: nb 256-thread workgroups running f(bid, smem)
-template <class F>
+// a non-GEMM piece of work riding in a gemmN launch: nb 256-thread workgroups running f(bid, smem), smem
+// at least SM floats of LDS
+template <class F, int SM = 4>
 struct BlockJob {
   struct Cfg {
-    static constexpr int SMEM = 4;
+    static constexpr int SMEM = SM;
   };
   F f;
   int nb;
 };
-template <class F>
-__device__ __forceinline__ bool gemm_job_dispatch(const BlockJob<F>& j, int& bid, float* smem) {
+template <class F, int SM>
+__device__ __forceinline__ bool gemm_job_dispatch(const BlockJob<F, SM>& j, int& bid, float* smem) {
   if (bid < j.nb) {
     j.f(bid, smem);
     return true;
@@ -608,8 +609,8 @@ __device__ __forceinline__ bool gemm_job_dispatch(const BlockJob<F>& j, int& bid
 }
 template <class J>
 inline int job_blocks(const J& j) { return gemm_blocks(j.g); }
-template <class F>
-inline int job_blocks(const BlockJob<F>& j) { return j.nb; }
+template <class F, int SM>
+inline int job_blocks(const BlockJob<F, SM>& j) { return j.nb; }
 template <class... J>
 __global__ void __launch_bounds__(256) gemmN_kernel(J... j) {
   TGNX_STAMP(22);

@@ -17,8 +17,13 @@ constexpr int INSERT_MAX_B = 4096;
 // (node << 32 | (B-1-i) << 1 | dir; dir 0 = dst side holding src, 1 = src side holding dst) sorted
 // in LDS so each node's run lists its new entries newest first; run_start[r] = first entry of run r.
 // Returns the number of runs.  Needs the whole workgroup.
+struct NoCheckpoint {
+  __device__ void operator()(int) const {}
+};
+template <class AT = NoCheckpoint>
 __device__ __forceinline__ int ring_plan_block(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int B,
-                                               unsigned char* smem, int* sh, uint64_t** key_out, int** runs_out) {
+                                               unsigned char* smem, int* sh, uint64_t** key_out, int** runs_out,
+                                               AT at = AT{}) {
   const int n2 = 2 * B;
   const int n = next_pow2(n2);
   uint64_t* key = reinterpret_cast<uint64_t*>(smem);
@@ -34,7 +39,9 @@ __device__ __forceinline__ int ring_plan_block(const int64_t* __restrict__ src, 
     key[p] = k;
   }
   __syncthreads();
-  sort_u64(key, reinterpret_cast<uint64_t*>(run_start + n2 + (n2 & 1)), n2, n);
+  at(0);
+  sort_u64(key, reinterpret_cast<uint64_t*>(run_start + n2 + (n2 & 1)), n2, n, true);  // keys distinct: (node, i, dir)
+  at(1);
   const int T = blockDim.x;
   int pc = (n2 + T - 1) / T;
   int p0 = threadIdx.x * pc, p1 = min(n2, p0 + pc);

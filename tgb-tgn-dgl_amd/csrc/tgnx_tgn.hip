@@ -242,46 +242,72 @@ __device__ __forceinline__ void mark_node(uint32_t* bm, uint32_t* sum, int64_t v
 // train negatives are drawn here (NegLinkSamplerDest, counter-based stream as in tgnx_tgnn);
 // src / pos nodes are stamped for the update list (memory_module.py:129).  16 lanes per entry, one
 // ring slot each (all slot loads in flight at once); the entry's valid-slot count goes to kval[v].
-__device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh);
+template <class AT = NoCheckpoint>
+__device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh, AT at = AT{});
+// The resident step's batch descriptor, from the step counters (tgnn_advance mode 1 restated): the
+// batch `ahead` batches past the counters' one.  Every block derives it itself; the scan launch writes it
+// into ctl for the later launches (TGNX_CTL_BATCH_START .. SEED).  The pipelined step marks the next
+// batch (ahead = 1) before this step's last launch advances the counters.
+struct ResDesc {
+  int64_t start, seed;
+  int B, lo, hi, gen;
+};
+__device__ __forceinline__ ResDesc res_desc(const Ctx& c, int ahead) {
+  ResDesc d;
+  const int64_t nb = c.ctl[TGNX_CTL_NB] + ahead;
+  d.start = c.adv_lo + nb * c.adv_batch;
+  d.B = d.start >= c.adv_hi ? 0 : (int)min(c.adv_hi - d.start, c.adv_batch);
+  d.lo = (int)((int64_t)d.B * c.adv_rank / c.adv_world);
+  d.hi = (int)((int64_t)d.B * (c.adv_rank + 1) / c.adv_world);
+  d.seed = (int64_t)(mix64(c.adv_seed ^ mix64((uint64_t)(nb + 1))) >> 1);
+  d.gen = (int)c.ctl[TGNX_CTL_GEN] + 1 + ahead;
+  return d;
+}
+// K1 body over `nmark` 256-thread blocks (bid = this block's index among them).  Resident train steps
+// (c.adv) take the batch from the counters (ahead: see res_desc), every other step from ctl.
+// lbm (LDS, MARK_LDS_WORDS x 3, or null): for a graph the scan walks directly (<= 2 words per scan thread),
+// the block sets its bits in LDS bitmaps and ORs the nonzero words into the global ones at the end: a
+// wiki-shaped hub neighbour sits in ~40 % of the page rings, and ~240 global atomics on its word queued at
+// the memory side (~11-13 ns each, MI355X_MICROARCH.md 'fanin'); now each word takes one per block.
+constexpr int MARK_LDS_WORDS = 2 * TGN_SCAN_THREADS;
 template <bool TRAIN>
-__global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
-  TGNX_STAMP(1);
-  int B;
+__device__ void mark_body(const Ctx& c, int bid, int nmark, int ahead, uint32_t* lbm) {
+  int B, lo, nl, gen;
   int64_t start;
-  if (TRAIN && c.adv) {  // tgnn_advance (mode 1) restated: every block from the unchanged step counters
-    const int64_t nb = c.ctl[TGNX_CTL_NB];
-    start = c.adv_lo + nb * c.adv_batch;
-    B = start >= c.adv_hi ? 0 : (int)min(c.adv_hi - start, c.adv_batch);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the descriptor for the later launches (no block here reads it)
-      c.ctl[TGNX_CTL_BATCH_START] = start;
-      c.ctl[TGNX_CTL_B] = B;
-      c.ctl[TGNX_CTL_CUR_EID] = start;
-      c.ctl[TGNX_CTL_LO] = (int64_t)B * c.adv_rank / c.adv_world;
-      c.ctl[TGNX_CTL_HI] = (int64_t)B * (c.adv_rank + 1) / c.adv_world;
-      c.ctl[TGNX_CTL_SEED] = (int64_t)(mix64(c.adv_seed ^ mix64((uint64_t)(nb + 1))) >> 1);
-    }
+  uint64_t nseed, noff;
+  const bool adv = TRAIN && c.adv;
+  if (adv) {
+    const ResDesc d = res_desc(c, ahead);
+    B = d.B;
+    start = d.start;
+    lo = d.lo;
+    nl = d.hi - d.lo;
+    gen = d.gen;
+    nseed = (uint64_t)d.seed;
+    noff = (uint64_t)d.start;
   } else {
     B = (int)c.ctl[TGNX_CTL_B];
     start = c.ctl[TGNX_CTL_BATCH_START];
+    // train: this rank's event slice [lo, lo + nl) (data parallel; the whole batch at world 1)
+    lo = TRAIN ? (int)c.ctl[TGNX_CTL_LO] : 0;
+    nl = TRAIN ? (int)(c.ctl[TGNX_CTL_HI] - c.ctl[TGNX_CTL_LO]) : B;
+    gen = (int)c.ctl[TGNX_CTL_GEN];
+    nseed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+    noff = (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
   }
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  if ((int)blockIdx.x >= nmark) {  // train: ring-insert / message-store plans (1024 threads)
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ int sh[40];
-    plan_blocks(c, (int)blockIdx.x - nmark, B, start, smem, sh);
-    return;
+  const bool local = lbm && scan_direct(c.words);  // block-uniform
+  const int W = (int)c.words;
+  uint32_t *Lc = lbm, *Ln = lbm + MARK_LDS_WORDS, *Lr = lbm + 2 * MARK_LDS_WORDS;
+  if (local) {
+    for (int x = threadIdx.x; x < W; x += blockDim.x) Lc[x] = Ln[x] = Lr[x] = 0u;
+    __syncthreads();
   }
-  if (threadIdx.x >= 256) return;  // marking runs 256-thread groups
-  const bool adv = TRAIN && c.adv;
-  const int gen = (int)c.ctl[TGNX_CTL_GEN] + (adv ? 1 : 0);
   const int Kn = TRAIN ? 1 : c.Kn;
-  // train: this rank's event slice [lo, lo + nl) (data parallel; the whole batch at world 1)
-  const int lo = !TRAIN ? 0 : adv ? B * c.adv_rank / c.adv_world : (int)c.ctl[TGNX_CTL_LO];
-  const int nl = !TRAIN ? B : adv ? B * (c.adv_rank + 1) / c.adv_world - lo : (int)(c.ctl[TGNX_CTL_HI] - c.ctl[TGNX_CTL_LO]);
   const int nq = nl * (2 + Kn);
   const int sl = threadIdx.x & 15, grp = (threadIdx.x & 63) >> 4;
   const int gstride = (nmark * 256) >> 4;
-  for (int q = (blockIdx.x * 256 + threadIdx.x) >> 4; q < nq; q += gstride) {
+  for (int q = (bid * 256 + (int)threadIdx.x) >> 4; q < nq; q += gstride) {
     int64_t v;
     if (q < nl) {
       v = c.ev_src[start + lo + q];
@@ -290,9 +316,7 @@ __global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
     } else if (TRAIN) {
       const int i = lo + q - 2 * nl;
       if (c.gen_neg) {
-        const uint64_t seed = adv ? (mix64(c.adv_seed ^ mix64((uint64_t)(c.ctl[TGNX_CTL_NB] + 1))) >> 1)
-                                  : (uint64_t)c.ctl[TGNX_CTL_SEED];
-        const uint64_t off = adv ? (uint64_t)start : (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
+        const uint64_t seed = nseed, off = noff;
         const int64_t pd = c.ev_dst[start + i];
         v = c.dst_nodes[0];
         for (uint64_t attempt = 0; attempt < 64; ++attempt) {
@@ -317,7 +341,7 @@ __global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
     const uint32_t vbit = 1u << (v & 31);
     const bool summ = !scan_direct(c.words);
     uint32_t wcv = 0u, wnv = 0u, wrv = 0u;
-    if (sl == 0) {
+    if (sl == 0 && !local) {
       wcv = c.cb[vw];
       wnv = c.nb[vw];
       if (c.layers == 2) wrv = c.rb[vw];
@@ -329,57 +353,87 @@ __global__ void __launch_bounds__(1024) tgn_mark(Ctx c, int nmark) {
       const bool ok = j < c.K && ej >= 0;
       const int64_t uw = ok ? (u >> 5) : vw;
       const uint32_t ubit = 1u << (u & 31);
-      const uint32_t wu = c.nb[uw];
-      uint32_t wcu = 0u;
-      if (c.layers == 2) wcu = c.cb[uw];
-      if (ok) {
+      uint32_t wu = 0u, wcu = 0u;
+      if (!local) {
+        wu = c.nb[uw];
+        if (c.layers == 2) wcu = c.cb[uw];
+      }
+      if (ok && local) {
+        atomicOr(&Ln[uw], ubit);
+        if (c.layers == 2) atomicOr(&Lc[uw], ubit);
+      } else if (ok) {
         if (!(wu & ubit)) atomicOr(&c.nb[uw], ubit);
         if (summ && !wu) atomicOr(&c.nbs[uw >> 5], 1u << (uw & 31));
         if (c.layers == 2) {
           if (!(wcu & ubit)) atomicOr(&c.cb[uw], ubit);
           if (summ && !wcu) atomicOr(&c.cbs[uw >> 5], 1u << (uw & 31));
-          // 2 hops: the neighbour is an outer centre; its own ring neighbours are sampled nodes
-          // (the lane walks u's ring row, all K slot loads issued before the marking)
-          int ku = 0;
-          for (int i0 = 0; i0 < c.K; i0 += 8) {
-            int64_t ev[8], w[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              const int ii = min(i0 + i, c.K - 1);
-              ev[i] = c.eid[u * c.K + ii];
-              w[i] = c.nbr[u * c.K + ii];
-            }
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              if (i0 + i >= c.K || ev[i] < 0) continue;
-              ++ku;
-              mark_node(c.nb, c.nbs, w[i]);
-            }
-          }
-          c.kval[u] = ku;
         }
+      }
+      if (ok && c.layers == 2) {
+        // 2 hops: the neighbour is an outer centre; its own ring neighbours are sampled nodes
+        // (the lane walks u's ring row, all K slot loads issued before the marking)
+        int ku = 0;
+        for (int i0 = 0; i0 < c.K; i0 += 8) {
+          int64_t ev[8], w[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int ii = min(i0 + i, c.K - 1);
+            ev[i] = c.eid[u * c.K + ii];
+            w[i] = c.nbr[u * c.K + ii];
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if (i0 + i >= c.K || ev[i] < 0) continue;
+            ++ku;
+            if (local) atomicOr(&Ln[w[i] >> 5], 1u << (w[i] & 31));
+            else mark_node(c.nb, c.nbs, w[i]);
+          }
+        }
+        c.kval[u] = ku;
       }
       k += __popcll((__ballot(ok) >> (16 * grp)) & 0xFFFFull);
     }
     if (sl == 0) {
       if (q < 2 * nl) c.node_gen[v] = gen;
       c.kval[v] = k;
-      if (!(wcv & vbit)) atomicOr(&c.cb[vw], vbit);
-      if (summ && !wcv) atomicOr(&c.cbs[vw >> 5], 1u << (vw & 31));
-      if (!(wnv & vbit)) atomicOr(&c.nb[vw], vbit);
-      if (summ && !wnv) atomicOr(&c.nbs[vw >> 5], 1u << (vw & 31));
-      if (c.layers == 2) {
-        if (!(wrv & vbit)) atomicOr(&c.rb[vw], vbit);
-        if (summ && !wrv) atomicOr(&c.rbs[vw >> 5], 1u << (vw & 31));
+      if (local) {
+        atomicOr(&Lc[vw], vbit);
+        atomicOr(&Ln[vw], vbit);
+        if (c.layers == 2) atomicOr(&Lr[vw], vbit);
+      } else {
+        if (!(wcv & vbit)) atomicOr(&c.cb[vw], vbit);
+        if (summ && !wcv) atomicOr(&c.cbs[vw >> 5], 1u << (vw & 31));
+        if (!(wnv & vbit)) atomicOr(&c.nb[vw], vbit);
+        if (summ && !wnv) atomicOr(&c.nbs[vw >> 5], 1u << (vw & 31));
+        if (c.layers == 2) {
+          if (!(wrv & vbit)) atomicOr(&c.rb[vw], vbit);
+          if (summ && !wrv) atomicOr(&c.rbs[vw >> 5], 1u << (vw & 31));
+        }
       }
     }
   }
+  if (local) {  // direct-scan graph: no summaries
+    __syncthreads();
+    for (int x = threadIdx.x; x < W; x += blockDim.x) {
+      const uint32_t a = Lc[x], b = Ln[x], r = Lr[x];
+      if (a) atomicOr(&c.cb[x], a);
+      if (b) atomicOr(&c.nb[x], b);
+      if (r) atomicOr(&c.rb[x], r);
+    }
+  }
+}
+template <bool TRAIN>
+__global__ void __launch_bounds__(256) tgn_mark(Ctx c, int nmark) {
+  TGNX_STAMP(1);
+  __shared__ uint32_t lbm[3 * MARK_LDS_WORDS];
+  mark_body<TRAIN>(c, blockIdx.x, nmark, 0, lbm);
 }
 
 // message-store plan of a batch: (node << 33 | dir << 32 | i), dir 0 = as source (msg_s_store),
 // 1 = as destination (msg_d_store); sorted, each (node, dir) run lists its events in batch order
 // (memory_module.py:188-191 with a stable sort).
-__device__ void store_plan_block(const Ctx& c, int B, int64_t start, unsigned char* smem, int* sh) {
+template <class AT>
+__device__ void store_plan_block(const Ctx& c, int B, int64_t start, unsigned char* smem, int* sh, AT at) {
   const int n2 = 2 * B, n = next_pow2(n2);
   uint64_t* key = reinterpret_cast<uint64_t*>(smem);
   int* runs = reinterpret_cast<int*>(smem + (size_t)n * 8);
@@ -394,7 +448,9 @@ __device__ void store_plan_block(const Ctx& c, int B, int64_t start, unsigned ch
     key[p] = k;
   }
   __syncthreads();
-  sort_u64(key, tmp, n2, n);
+  at(0);
+  sort_u64(key, tmp, n2, n, true);  // keys distinct: (node, dir, i)
+  at(1);
   const int T = blockDim.x, pc = (n2 + T - 1) / T;
   const int p0 = threadIdx.x * pc, p1 = min(n2, p0 + pc);
   int cntr = 0;
@@ -440,21 +496,21 @@ __device__ void occupied_words2(uint32_t* sa, uint32_t* sb, int64_t words, int* 
   if (sb) emit(sb, lb, ob);
 }
 
-// K2 (3 workgroups): WG0 ordered bitmap walks -> centres (+ edge offsets, update list) and sampled
-// nodes (+ assoc, centre ranks); WG1 ring-insert plan; WG2 message-store plan.
+// dynamic LDS of the scan launch (the plan workgroups' keys, runs and sort buffer)
 __host__ __device__ inline size_t tgn_scan_smem(int Bmax) {
   const int n = next_pow2(2 * Bmax);
   return (size_t)n * 16 + (size_t)(2 * Bmax + 4) * 4 + 64;
 }
 
 // the batch's ring-insert plan (which = 0) and message-store plan (which = 1); they read only the batch's
-// events, so the train step runs them as two extra 1024-thread workgroups of tgn_mark
-__device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh) {
+// events and run as two extra 1024-thread workgroups of the scan launch
+template <class AT>
+__device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh, AT at) {
   const int tid = threadIdx.x, T = blockDim.x;
   if (which == 0) {
     uint64_t* key;
     int* runs;
-    const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs);
+    const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs, at);
     for (int p = tid; p < 2 * B; p += T) c.rkeys[p] = key[p];
     for (int r = tid; r < U; r += T) c.rruns[r] = runs[r];
     if (tid == 0) {
@@ -462,23 +518,44 @@ __device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsig
       c.cnt[CNT_RUNS] = U;
     }
   } else {
-    store_plan_block(c, B, start, smem, sh);
+    store_plan_block(c, B, start, smem, sh, at);
   }
 }
+// K2 (3 workgroups): WG0 ordered bitmap walks -> centres (+ edge offsets, update list) and sampled
+// nodes (+ assoc, centre ranks); WG1 / WG2 the batch's ring-insert / message-store plans (they read only
+// the batch's events).  Resident train steps: every workgroup takes the batch from the step counters
+// and WG0 writes the descriptor into ctl for the later launches (no workgroup of this launch reads it).
 template <bool TRAIN>
 __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
   TGNX_STAMP(2);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int sh[40];
-  const int B = (int)c.ctl[TGNX_CTL_B];
-  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   const int tid = threadIdx.x, T = blockDim.x;
-  if (blockIdx.x >= 1) {  // eval: the plans ride here (train: in tgn_mark)
-    plan_blocks(c, (int)blockIdx.x - 1, B, start, smem, sh);
+  int B, gen;
+  int64_t start;
+  if (TRAIN && c.adv) {
+    const ResDesc d = res_desc(c, 0);
+    B = d.B;
+    start = d.start;
+    gen = d.gen;
+    if (blockIdx.x == 0 && tid == 0) {
+      c.ctl[TGNX_CTL_BATCH_START] = d.start;
+      c.ctl[TGNX_CTL_B] = d.B;
+      c.ctl[TGNX_CTL_CUR_EID] = d.start;
+      c.ctl[TGNX_CTL_LO] = d.lo;
+      c.ctl[TGNX_CTL_HI] = d.hi;
+      c.ctl[TGNX_CTL_SEED] = d.seed;
+    }
+  } else {
+    B = (int)c.ctl[TGNX_CTL_B];
+    start = c.ctl[TGNX_CTL_BATCH_START];
+    gen = (int)c.ctl[TGNX_CTL_GEN];
+  }
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  if (blockIdx.x >= 1) {
+    plan_blocks(c, (int)blockIdx.x - 1, B, start, smem, sh, [&](int slot) { TGNX_STAMP_AT(slot); });
     return;
   }
-  const int gen = (int)c.ctl[TGNX_CTL_GEN] + (c.adv ? 1 : 0);  // cursor folded into mark: counters advance at the end
   // pass 0: the words each thread walks.  Small graphs (<= 2 words per thread): contiguous word ranges
   // (summaries just cleared); large graphs: the nonzero words in word order, from the summaries
   const bool direct = scan_direct(c.words);
@@ -1421,7 +1498,9 @@ __host__ __device__ inline int evs_stride(int D) { return 7 * D + 8; }
 // load instruction.)
 __host__ __device__ inline size_t tgn_pred_smem(int D) { return (size_t)2 * D * (D + 1) * sizeof(float); }
 constexpr int PRED_SU = 16;  // float4 per staging thread per matrix per round (D <= 110: one round)
-__global__ void __launch_bounds__(256) tgn_pred_train(Ctx c) {
+// nmk > 0 (pipelined resident step): the last nmk blocks mark the NEXT batch instead (mark_body, ahead 1):
+// the ring insert of this batch ran beside the GRU, and nothing of this step reads what marking writes.
+__global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
   TGNX_STAMP(5);
   extern __shared__ __attribute__((aligned(16))) float Wl[];  // [2][D][DP]: lin_src, lin_dst
   __shared__ __attribute__((aligned(16))) float z[3][TDMAX];
@@ -1429,6 +1508,10 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c) {
   __shared__ float dh[2][TDMAX];
   __shared__ float vsb[TDMAX], vdb[TDMAX], vfw[TDMAX + 1];  // lin_src.bias, lin_dst.bias, lin_final (w | b)
   __shared__ int scr[3];
+  if ((int)blockIdx.x >= (int)gridDim.x - nmk) {  // (the dynamic LDS holds >= 3 x MARK_LDS_WORDS words)
+    mark_body<true>(c, (int)blockIdx.x - ((int)gridDim.x - nmk), nmk, 1, reinterpret_cast<uint32_t*>(Wl));
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // D % 8 == 4 (D = 100): unpadded rows are conflict-free both for b128 row reads with lanes over rows
   // (start banks 4 D o mod 64 distinct over 16 lanes) and for b32 column reads, and the LDS image is the
@@ -2291,6 +2374,15 @@ __device__ __forceinline__ void xrow_header(float* h, int64_t v, int64_t luv) {
   h[2] = (float)(uint32_t)((b >> 24) & 0xFFFFFFull);
   h[3] = (float)(uint32_t)(b >> 48);
 }
+// ring insert of the batch (neighbor_loader.py:52-104): wave per node run of the ring plan (4 per block)
+__device__ __forceinline__ void ring_merge_block(const Ctx& c, int blk, int B, int64_t start) {
+  const int r = blk * 4 + (threadIdx.x >> 6);
+  if (r < c.cnt[CNT_RUNS]) {
+    const int a = c.rruns[r];
+    ring_merge_run(c.nbr, c.eid, c.rt, c.K, c.ev_src + start, c.ev_dst + start, c.ev_t + start, B,
+                   c.ctl[TGNX_CTL_CUR_EID], c.assoc, c.rkeys, a, c.rruns[r + 1] - a, r, threadIdx.x & 63);
+  }
+}
 // update_state pieces (memory_module.py:126-150, :180-191) and the ring insert, by block range:
 // [0, nmem): memory / last_update of the update list from the GRU rows (wave per node; train rows
 // are the sampled nodes' rows via assoc, eval / flush rows are list positions);
@@ -2344,13 +2436,32 @@ __device__ void update_body(const Ctx& c, int blk, int nmem, int nst, int mem_mo
     }
     return;
   }
-  const int r = (blk - nmem - nst) * 4 + (threadIdx.x >> 6);
-  if (r < c.cnt[CNT_RUNS]) {
-    const int a = c.rruns[r];
-    ring_merge_run(c.nbr, c.eid, c.rt, c.K, c.ev_src + start, c.ev_dst + start, c.ev_t + start, B,
-                   c.ctl[TGNX_CTL_CUR_EID], c.assoc, c.rkeys, a, c.rruns[r + 1] - a, r, lane);
-  }
+  ring_merge_block(c, blk - nmem - nst, B, start);
 }
+// the train step's ring insert, riding in the GRU ‖ lin_edge launch: nothing after tgn_agg_emit reads the
+// ring (the sampled edges are copied out), and the next batch's marking runs after it
+struct RingMergeJob {
+  Ctx c;
+  __device__ void operator()(int bid, float*) const {
+    const int B = (int)c.ctl[TGNX_CTL_B];
+    if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+    ring_merge_block(c, bid, B, c.ctl[TGNX_CTL_BATCH_START]);
+  }
+};
+// pipelined step: the next batch's marking riding in a launch after the ring insert (nb 256-thread blocks;
+// the launch's LDS holds the block's bitmaps)
+struct MarkNextJob {
+  Ctx c;
+  int nb;
+  __device__ void operator()(int bid, float* smem) const {
+    mark_body<true>(c, bid, nb, 1, reinterpret_cast<uint32_t*>(smem));
+  }
+};
+// launch of the pipelined step that carries the next batch's marking: 3 = q|k|v|skip GEMM, 5 =
+// tgn_pred_train, 7 = kv_reduce ‖ dE GEMMs, 8 = weight gradients ‖ dz0, 9 = dW_gru ‖ dX_enc
+#ifndef TGNX_PIPE_MARK_AT
+#define TGNX_PIPE_MARK_AT 7
+#endif
 
 __global__ void __launch_bounds__(256) tgn_update(Ctx c, int nmem, int nst, int mem_mode, const int64_t* list,
                                                   const int* list_cnt, int n_host, int64_t base) {
@@ -2867,8 +2978,11 @@ struct AdvArgs {
   int rank, world;
   uint64_t seed;
 };
+// pipe (resident world-1 fused steps only): 0 = plain step; 1 = pipelined, this batch already marked and
+// scanned by the previous pipelined step; 2 = pipelined, mark + scan this batch first.  A pipelined step
+// marks the next batch inside tgn_pred_train and scans it after its own last launch.
 static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
-                           void* stream, bool fuse_adam, const AdvArgs* adv = nullptr) {
+                           void* stream, bool fuse_adam, const AdvArgs* adv = nullptr, int pipe = 0) {
   Ctx c;
   Caps k;
   WsLay W;
@@ -2904,21 +3018,23 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     c.adf.eps = c.eps;
   }
   TGNX_CHECK_ARG(!gen_neg || (buf->dst_nodes && buf->n_dst > 0), "tgnx_tgn_train_fwd_bwd: no destination set");
+  TGNX_CHECK_ARG(pipe == 0 || (adv && fuse_adam && adv->world == 1),
+                 "tgnx_tgn_train_step_pipelined: resident world-1 steps only");
   c.gen_neg = gen_neg ? 1 : 0;
   c.drop = dropout && cfg->dropout > 0.f;
   hipStream_t s = as_stream(stream);
   const float* P = c.params;
   float* G = c.grads;
   const int D = c.D, HC = c.HC, Qm = c.Qm, d = c.d;
-  {
+  if (pipe != 1) {
     const int nmark = gridn(3 * k.B * 16, 256);
-    tgn_mark<true><<<nmark + 2, 1024, tgn_scan_smem(k.B), s>>>(c, nmark);
+    tgn_mark<true><<<nmark, 256, 0, s>>>(c, nmark);
+    TGNX_LAUNCH_CHECK("tgn_mark");
+    probe_begin(TGNX_K_ASSEMBLE, s);
+    tgn_scan<true><<<3, TGN_SCAN_THREADS, tgn_scan_smem(k.B), s>>>(c);
+    probe_end(TGNX_K_ASSEMBLE, s);
+    TGNX_LAUNCH_CHECK("tgn_scan");
   }
-  TGNX_LAUNCH_CHECK("tgn_mark");
-  probe_begin(TGNX_K_ASSEMBLE, s);
-  tgn_scan<true><<<1, TGN_SCAN_THREADS, 0, s>>>(c);  // plans: in tgn_mark
-  probe_end(TGNX_K_ASSEMBLE, s);
-  TGNX_LAUNCH_CHECK("tgn_scan");
   const int nedge = gridn((int64_t)k.Rtr * c.K, 4, TGNX_AGG_EDGE_CAP);
   probe_begin(TGNX_K_EDGE_META, s);
   const int nevb = gridn(3 * k.B, 256);
@@ -2936,18 +3052,23 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
                                     EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, (float*)nullptr);
   const auto j_edge = gemm_job<G32>(gemm_shape<G32>(k.Etr, HC, D + d, c.cnt + CNT_E), ea,
                                     LoadRowK{P + c.L.we, HC, D + d, D + d}, EpiStore{c.Ep, nullptr, HC, 0}, (float*)nullptr);
+  const BlockJob<RingMergeJob> j_ring{RingMergeJob{c}, gridn(2 * k.B, 4)};
   probe_begin(TGNX_K_EDGE_FWD, s);
   if (two)
-    gemmN_launch(s, j_gru, j_edge,
+    gemmN_launch(s, j_ring, j_gru, j_edge,
                  gemm_job<G32>(gemm_shape<G32>(k.E1tr, HC, D + d, c.cnt + CNT_E1), ea1,
                                LoadRowK{P + c.L.we2, HC, D + d, D + d}, EpiStore{c.Ep2, nullptr, HC, 0}, (float*)nullptr));
   else
-    gemmN_launch(s, j_gru, j_edge);
+    gemmN_launch(s, j_ring, j_gru, j_edge);
   probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgn_gru_edge");
-  gemm_launch<G32>(gemm_shape<G32>(k.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
-              LoadProjW{P + c.L.wq, c.L.pw, HC, D},
-              EpiProj{P + c.L.bq, c.L.pb, c.P, HC}, nullptr, s);
+  const int nmark = gridn(3 * k.B * 16, 256);
+  auto mk_at = [&](int at) {
+    return BlockJob<MarkNextJob, 3 * MARK_LDS_WORDS>{MarkNextJob{c, nmark}, pipe && at == TGNX_PIPE_MARK_AT ? nmark : 0};
+  };
+  gemmN_launch(s, mk_at(3),
+               gemm_job<G32>(gemm_shape<G32>(k.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
+                             LoadProjW{P + c.L.wq, c.L.pw, HC, D}, EpiProj{P + c.L.bq, c.L.pb, c.P, HC}, (float*)nullptr));
   TGNX_LAUNCH_CHECK("tgn_proj");
   probe_begin(TGNX_K_SEG_FWD, s);
   tgn_attn_fwd<true><<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c);
@@ -2963,7 +3084,9 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   }
   probe_begin(TGNX_K_PRED, s);
   TGNX_CHECK_ARG(pred_smem_ok(c.D), "tgn_pred_train: dynamic LDS attribute refused");
-  tgn_pred_train<<<k.B, 256, tgn_pred_smem(c.D), s>>>(cr);
+  const int nmk = pipe && TGNX_PIPE_MARK_AT == 5 ? nmark : 0;
+  const size_t psm = std::max(tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0);
+  tgn_pred_train<<<k.B + nmk, 256, psm, s>>>(cr, nmk);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
   probe_begin(TGNX_K_SEG_BWD, s);
@@ -3000,7 +3123,7 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   // idle: the dE-only GEMMs fill them here instead of lengthening the dP launch below.
   const EpiGradStore e_dWe{G, c.L.we, D + d, c.adf};
   probe_begin(TGNX_K_KV, s);
-  gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(k.Etr, KVR_CH, 1 << 20)},
+  gemmN_launch(s, mk_at(7), BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(k.Etr, KVR_CH, 1 << 20)},
                gemm_job<GW>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, EpiDeferred{}, c.pA),
                gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
                              LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
@@ -3015,7 +3138,7 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   // epilogue — all read only what attn_bwd / kv_reduce / pred_train produced
   const int rows_edge = (k.Etr + G32::TM - 1) / G32::TM, rows_msg = (k.Mtr + G32::TM - 1) / G32::TM;
   probe_begin(TGNX_K_EDGE_BWD, s);
-  gemmN_launch(s, gemm_job<GW>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB),
+  gemmN_launch(s, mk_at(8), gemm_job<GW>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB),
                gemm_job<GW>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
                              LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, EpiDeferred{}, c.pC),
                gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
@@ -3023,29 +3146,36 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
                              (float*)nullptr));
   probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
-  gemm2_launch<GW, G32L>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{},
-               c.pD, gemm_shape<G32L>(k.Mtr, D, 4 * D, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
-               LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, nullptr, s);
+  gemmN_launch(s, mk_at(9),
+               gemm_job<GW>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D},
+                            EpiDeferred{}, c.pD),
+               gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, 4 * D, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
+                              LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge},
+                              (float*)nullptr));
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
   // split-K sums + epilogues ‖ Δt reduction ‖ update_state (train order: memory of src ∪ dst from
-  // this step's GRU rows, then the stores) + ring insert, one launch
+  // this step's GRU rows, then the stores), one launch (the ring insert ran beside the GRU)
   const int nte = (2 * D + 63) / 64;
-  const int nmem = gridn(k.Ucap, 4, 1024), nst = gridn(2 * k.B, 256), nring = gridn(2 * k.B, 4);
-  const int ninc = c.adv ? nte + nmem + nst + nring : -1;
+  const int nmem = gridn(k.Ucap, 4, 1024), nst = gridn(2 * k.B, 256);
+  const int ninc = c.adv ? nte + nmem + nst : -1;
   const TrainTail tail{TeReduceTail{c, rows_edge, rows_msg}, nte, nmem, nst, ninc};
   probe_begin(TGNX_K_FINISH, s);
   if (two)
-    gemm_fixup_launch(nte + nmem + nst + nring + (c.adv ? 1 : 0), tail, s, gemm_fix<GW>(shp_dWe(k, c.cnt), c.pA, e_dWe),
+    gemm_fixup_launch(nte + nmem + nst + (c.adv ? 1 : 0), tail, s, gemm_fix<GW>(shp_dWe(k, c.cnt), c.pA, e_dWe),
                       gemm_fix<GW>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
                       gemm_fix<GW>(shp_dWg(k, c.cnt), c.pD, e_dWg),
                       gemm_fix<GW>(shp_dWp2(k, c.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC, c.adf}),
                       gemm_fix<GW>(shp_dWe2(k, c.cnt), c.pF, EpiGradStore{G, c.L.we2, D + d, c.adf}));
   else
-    gemm_fixup_launch(nte + nmem + nst + nring + (c.adv ? 1 : 0), tail, s, gemm_fix<GW>(shp_dWe(k, c.cnt), c.pA, e_dWe),
+    gemm_fixup_launch(nte + nmem + nst + (c.adv ? 1 : 0), tail, s, gemm_fix<GW>(shp_dWe(k, c.cnt), c.pA, e_dWe),
                       gemm_fix<GW>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
                       gemm_fix<GW>(shp_dWg(k, c.cnt), c.pD, e_dWg));
   probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgn_fixup_update");
+  if (pipe) {  // the next batch (counters advanced by the fixup): sorted node sets, plans, descriptor
+    tgn_scan<true><<<3, TGN_SCAN_THREADS, tgn_scan_smem(k.B), s>>>(c);
+    TGNX_LAUNCH_CHECK("tgn_scan_next");
+  }
   return TGNX_OK;
 }
 
@@ -3064,6 +3194,13 @@ int tgnx_tgn_train_step_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buff
                                  int32_t dropout, void* stream) {
   const AdvArgs a{split_lo, split_hi, batch, rank, world, base_seed};
   return train_step_impl(cfg, buf, 1, dropout, stream, true, &a);
+}
+
+int tgnx_tgn_train_step_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                                  int64_t split_hi, int64_t batch, uint64_t base_seed, int32_t dropout,
+                                  int32_t prefetched, void* stream) {
+  const AdvArgs a{split_lo, split_hi, batch, 0, 1, base_seed};
+  return train_step_impl(cfg, buf, 1, dropout, stream, true, &a, prefetched ? 1 : 2);
 }
 
 int tgnx_tgn_train_fwd_bwd_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,

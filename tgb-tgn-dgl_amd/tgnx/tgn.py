@@ -263,6 +263,11 @@ class TgnEngine:
         # (world 1, Adam fused) or tgnx_tgn_train_fwd_bwd_resident (world > 1; exchange + update follow).
         # Both forms are tested against advance + step per rank (test_gpu_tgn.py, test_gpu_tgn_dp.py).
         self.fold_cursor = True
+        # world-1 fused resident steps pipeline across steps (tgnx_tgn_train_step_pipelined): each step marks
+        # and scans the next batch, so the next step starts at the message aggregation.  `_prefetched` says
+        # whether the last call on these buffers was such a step (any other call clears it).
+        self.pipeline = True
+        self._prefetched = False
         if optimizer is None:
             self.adam_m, self.adam_v = torch.zeros_like(model.flat), torch.zeros_like(model.flat)
         else:
@@ -294,6 +299,7 @@ class TgnEngine:
             raise RuntimeError(f"tgnx_tgn_ws_bytes: {_lib.lib().tgnx_last_error().decode()}")
         self.ws = torch.zeros(nb, dtype=torch.uint8, device=self.dev)   # scratch only: zero = initial state
         self.out_neg = torch.zeros(self.cfg.max_batch * kn, dtype=torch.float32, device=self.dev)
+        self._prefetched = False
         if hasattr(self, "_res_buf"):
             self._res_buf = self._buffers(_p(self.neg_train))
             self._buf_ref = ctypes.byref(self._res_buf)
@@ -318,18 +324,21 @@ class TgnEngine:
         return _lib.stream(self.dev)
 
     def advance(self, batch_start: int, B: int, train: bool):
+        self._prefetched = False
         _lib.call("tgnx_tgnn_advance", _p(self.ctl), 0, batch_start, B, batch_start, 0, 0, 1, self.rank, self.world,
                   self.seed, 1 if train else 0, self._stream())
 
     # ------------------------------------------------------------------ state
     def reset_state(self):
         """memory_module.reset_state + neighbor_loader.reset_state (pyg_epoch_utils.py:15-16)."""
+        self._prefetched = False
         b = self._buffers(0)
         _lib.call("tgnx_tgn_reset_state", ctypes.byref(self.cfg), ctypes.byref(b), self._stream())
         self.loader.reset_state()
 
     def flush(self):
         """TGNMemory.train(False) (memory_module.py:209-215)."""
+        self._prefetched = False
         b = self._buffers(0)
         _lib.call("tgnx_tgn_flush", ctypes.byref(self.cfg), ctypes.byref(b), self._stream())
 
@@ -389,6 +398,7 @@ class TgnEngine:
         device; the batch cursor lives in the control block (no host arguments change per step)."""
         self._res = (int(split_lo), int(split_hi), int(batch))
         self._res_drop = 1 if dropout else 0
+        self._prefetched = False
         self._res_buf = self._buffers(_p(self.neg_train))
         L = _lib.lib()
         self._res_fused = self._fused()
@@ -401,12 +411,19 @@ class TgnEngine:
         """pyg_epoch_utils.py:11-16: memory reset_state + neighbor_loader reset_state; cursor to 0."""
         self.reset_state()
         self.ctl[10] = 0
+        self._prefetched = False
 
-    def _pre(self):
+    def _pipelined(self) -> bool:
+        return self.pipeline and self.fold_cursor and self._res_fused
+
+    def _pre(self, prefetched: bool = False):
         adv, fb = self._f[:2]
         lo, hi, batch = self._res
         st = self._stream()
-        if self.fold_cursor:   # the batch cursor folded into the step's first launch
+        if self._pipelined():
+            rc = _lib.lib().tgnx_tgn_train_step_pipelined(self._cfg_ref, self._buf_ref, lo, hi, batch, self.seed,
+                                                         self._res_drop, 1 if prefetched else 0, st)
+        elif self.fold_cursor:   # the batch cursor folded into the step's first launches
             f = _lib.lib().tgnx_tgn_train_step_resident if self._res_fused else _lib.lib().tgnx_tgn_train_fwd_bwd_resident
             rc = f(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank, self.world, self.seed, self._res_drop, st)
         else:
@@ -431,9 +448,10 @@ class TgnEngine:
             self._exchange()
 
     def resident_train_step(self):
-        self._pre()
+        self._pre(self._prefetched)
         self._allreduce()
         self._post()
+        self._prefetched = self._pipelined()
 
     def capture_resident(self):
         """One resident step as HIP graph(s) (world > 1: the collectives stay eager between them)."""
@@ -441,8 +459,8 @@ class TgnEngine:
         saved = self.ctl.clone()
         if self.world == 1:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._pre()
+            with torch.cuda.graph(g):   # pipelined: the steady-state step (the previous step prefetched)
+                self._pre(True)
                 self._post()
             self._graphs = (g, None)
         else:
@@ -457,10 +475,14 @@ class TgnEngine:
 
     def replay_resident(self):
         g1, g2 = self._graphs
+        if self._pipelined() and not self._prefetched:
+            self.resident_train_step()   # marks + scans this batch first (eager), prefetches the next
+            return
         g1.replay()
         if g2 is not None:
             self._allreduce()
             g2.replay()
+        self._prefetched = self._pipelined()
 
     def units(self):
         """(sum of sampled edges, sum of sampled nodes) since the last reset."""

@@ -96,8 +96,10 @@ def main():
         if cur:
             L.append(cur)
         launches_x[x] = L
-    # align XCD clocks on tgn_mark launches
-    starts = {x: [min(int(r["t0"]) for r in l) for l in L if int(l[0]["kid"]) == 1] for x, L in launches_x.items()}
+    # align XCD clocks on tgn_agg_emit launches (once per step in every step form; the pipelined step has no
+    # tgn_mark launch: it marks the next batch inside tgn_pred_train)
+    SK = 3
+    starts = {x: [min(int(r["t0"]) for r in l) for l in L if int(l[0]["kid"]) == SK] for x, L in launches_x.items()}
     ref = starts.get(0) or next(iter(starts.values()))
     off = {}
     for x, s in starts.items():
@@ -121,10 +123,11 @@ def main():
         tmax = max(tmax, w[1]) if len(cur) > 1 else w[1]
     if cur:
         glaunch.append(cur)
-    # fold into steps: the step starts at tgn_mark
+    # fold into steps: a step starts at tgn_agg_emit (the non-pipelined step's mark / scan then close the
+    # previous one)
     steps, st = [], None
     for l in glaunch:
-        if l[0][2] == 1:
+        if l[0][2] == SK:
             st = []
             steps.append(st)
         if st is not None:
