@@ -3173,7 +3173,9 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgn_fixup_update");
   if (pipe) {  // the next batch (counters advanced by the fixup): sorted node sets, plans, descriptor
+    probe_begin(TGNX_K_ASSEMBLE, s);
     tgn_scan<true><<<3, TGN_SCAN_THREADS, tgn_scan_smem(k.B), s>>>(c);
+    probe_end(TGNX_K_ASSEMBLE, s);
     TGNX_LAUNCH_CHECK("tgn_scan_next");
   }
   return TGNX_OK;
