@@ -337,7 +337,9 @@ def run_tgn(args, world, rank, dev):
         _lib.call("tgnx_probe_read", ctypes.byref(ms), ctypes.byref(n))
         _lib.call("tgnx_probe_enable", 0)
         pe1, pm1 = eng.units()
-        launches = max(int(n.value), 1)
+        if int(n.value) == 0:   # no such launch in this step (1 hop: the attention forward runs in tgn_pred_train)
+            continue
+        launches = int(n.value)
         avg_ms = ms.value / launches
         E = (pe1 - pe0) / launches
         M = (pm1 - pm0) / launches

@@ -173,6 +173,7 @@ struct Ctx {
   float* e_t;
   float *X, *trel, *lu;
   int* evr;  // [3 B] centre row of each root (src, dst, neg) of this rank's events (tgn_agg_emit)
+  int4* evq;  // [3 B] 1 hop: per root {centre row, P row, edge range} (tgn_pred_train<ATT>); nullptr at 2 hops
   int64_t* xw;
   float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
   float *dZc, *dP, *dE, *dG, *tgp;
@@ -1038,7 +1039,13 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
     for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < 3 * (hi - lo); x += nevb * blockDim.x) {
       const int i = lo + x / 3, r = x % 3;
       const int64_t* src = r == 0 ? c.ev_src : r == 1 ? c.ev_dst : c.neg;
-      c.evr[x] = root_row(c, src[start + i]);
+      if (c.evq) {  // 1 hop: the root's centre row, its P row and edge range (one round for the attention)
+        const int a = (int)c.assoc[src[start + i]], xr = c.crank[a];
+        c.evr[x] = xr;
+        c.evq[x] = make_int4(xr, a, c.ceoff[xr], c.ceoff[xr + 1]);
+      } else {
+        c.evr[x] = root_row(c, src[start + i]);
+      }
     }
     return;
   }
@@ -1349,85 +1356,67 @@ __device__ __forceinline__ float att_keep(const Ctx& c, uint64_t seed, int x, in
                 c.inv_keep);
 }
 constexpr int ATT_EB = 16;  // edges whose neighbour rows are loaded in one batch (ring K <= 32: <= 2 batches)
-// A centre with 1..ATT_EB edges: the k, v and edge rows of every edge and the centre's skip row are
-// issued as one round (each edge row loaded once for k + e and v + e); same arithmetic as the batched
-// loop of tgn_attn_fwd.
+// TransformerConv forward of centre x (row i of P, edges [e0, e0 + ne)), one wave: returns this lane's
+// output pair (channel lane of both heads, lane < C).  A centre with 1..ATT_EB edges issues the k, v and
+// edge rows of every edge and its skip row as one round (each edge row loaded once for k + e and v + e);
+// longer rings walk ATT_EB-edge load batches.  Train: the softmax weights go to alpha (tgn_attn_bwd).
 template <bool TRAIN>
-__device__ __forceinline__ void attn_fwd_one(const Ctx& c, int x, int lane, float on, int l0, const float* Pi,
-                                             float q0, float q1, float sqc, int e0, int ne, int jl) {
-  const int C = c.C, HC = c.HC;
-  float k0[ATT_EB], k1[ATT_EB], v0[ATT_EB], v1[ATT_EB];
-#pragma unroll
-  for (int u = 0; u < ATT_EB; ++u) {
-    const int e = min(u, ne - 1);
-    const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
-    const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
-    const float ea = Ee[l0], eb = Ee[C + l0];
-    k0[u] = Pj[HC + l0] + ea;
-    k1[u] = Pj[HC + C + l0] + eb;
-    v0[u] = Pj[2 * HC + l0] + ea;
-    v1[u] = Pj[2 * HC + C + l0] + eb;
-  }
-  const float sk0 = Pi[3 * HC + l0], sk1 = Pi[3 * HC + C + l0];
-  float my0 = -INFINITY, my1 = -INFINITY;
-#pragma unroll
-  for (int u = 0; u < ATT_EB; ++u) {
-    if (u >= ne) break;
-    const float p0 = wave_sum(q0 * k0[u] * on) / sqc, p1 = wave_sum(q1 * k1[u] * on) / sqc;
-    if (lane == u) { my0 = p0; my1 = p1; }
-  }
-  const float mx0 = wave_max(my0), mx1 = wave_max(my1);
-  const float ex0 = lane < ne ? expf(my0 - mx0) : 0.f, ex1 = lane < ne ? expf(my1 - mx1) : 0.f;
-  const float a0 = ex0 / (wave_sum(ex0) + 1e-16f), a1 = ex1 / (wave_sum(ex1) + 1e-16f);
-  float t0 = a0, t1 = a1;
-  if (TRAIN && lane < ne) {
-    c.alpha[(int64_t)(e0 + lane) * 2] = a0;
-    c.alpha[(int64_t)(e0 + lane) * 2 + 1] = a1;
-    if (c.drop) {
-      const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-      t0 *= att_keep(c, seed, x, e0 + lane, 0);
-      t1 *= att_keep(c, seed, x, e0 + lane, 1);
-    }
-  }
-  float o0 = 0.f, o1 = 0.f;
-#pragma unroll
-  for (int u = 0; u < ATT_EB; ++u) {
-    if (u >= ne) break;
-    o0 += v0[u] * __shfl(t0, u, 64);
-    o1 += v1[u] * __shfl(t1, u, 64);
-  }
-  if (lane < C) {
-    c.Zc[(int64_t)x * HC + lane] = o0 + sk0;
-    c.Zc[(int64_t)x * HC + C + lane] = o1 + sk1;
-  }
-}
-template <bool TRAIN>
-__global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
-  TGNX_STAMP(4);
-  const int lane = threadIdx.x & 63;
-  const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
-  // one round for the batch descriptor, the centre count and the centre's row / edge range: the centre
-  // arrays hold ccap rows (ceoff ccap + 1), so the read is clamped, and discarded past the runtime count
-  const int xc = min(x, max(c.ccap - 1, 0));
-  const int B = (int)c.ctl[TGNX_CTL_B];
-  const int64_t err = c.ctl[TGNX_CTL_ERR];
-  const int R = c.cnt[c.rsel];
-  const int i = c.cent_loc[xc];
-  const int e0 = c.ceoff[xc], e1 = c.ceoff[xc + 1];
-  if (B == 0 || err != 0 || x >= R) return;
+__device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0, int ne, int lane) {
   const int C = c.C, HC = c.HC;
   const float on = f01(lane < C);
   const int l0 = min(lane, C - 1);
   const float* Pi = c.P + (int64_t)i * 4 * HC;
   const float q0 = Pi[l0], q1 = Pi[C + l0];
   const float sqc = sqrtf((float)C);
-  const int ne = e1 - e0;
   const int jl = c.e_j[e0 + min(lane, max(ne - 1, 0))];   // lane e: the neighbour row of edge e
-  if (ne > 0 && ne <= ATT_EB) {  // every ring of K <= 16: k, v and edge rows of all edges in one round
-    attn_fwd_one<TRAIN>(c, x, lane, on, l0, Pi, q0, q1, sqc, e0, ne, jl);
-    return;
-  }
+  const float sk0 = Pi[3 * HC + l0], sk1 = Pi[3 * HC + C + l0];
   float my0 = -INFINITY, my1 = -INFINITY;
+  float o0 = 0.f, o1 = 0.f;
+  float t0, t1;
+  auto softmax = [&]() {
+    const float mx0 = wave_max(my0), mx1 = wave_max(my1);
+    const float ex0 = lane < ne ? expf(my0 - mx0) : 0.f, ex1 = lane < ne ? expf(my1 - mx1) : 0.f;
+    const float a0 = ex0 / (wave_sum(ex0) + 1e-16f), a1 = ex1 / (wave_sum(ex1) + 1e-16f);
+    t0 = a0;
+    t1 = a1;
+    if (TRAIN && lane < ne) {
+      c.alpha[(int64_t)(e0 + lane) * 2] = a0;
+      c.alpha[(int64_t)(e0 + lane) * 2 + 1] = a1;
+      if (c.drop) {
+        const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+        t0 *= att_keep(c, seed, x, e0 + lane, 0);
+        t1 *= att_keep(c, seed, x, e0 + lane, 1);
+      }
+    }
+  };
+  if (ne > 0 && ne <= ATT_EB) {  // every ring of K <= 16: one load round
+    float k0[ATT_EB], k1[ATT_EB], v0[ATT_EB], v1[ATT_EB];
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      const int e = min(u, ne - 1);
+      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
+      const float ea = Ee[l0], eb = Ee[C + l0];
+      k0[u] = Pj[HC + l0] + ea;
+      k1[u] = Pj[HC + C + l0] + eb;
+      v0[u] = Pj[2 * HC + l0] + ea;
+      v1[u] = Pj[2 * HC + C + l0] + eb;
+    }
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      if (u >= ne) break;
+      const float p0 = wave_sum(q0 * k0[u] * on) / sqc, p1 = wave_sum(q1 * k1[u] * on) / sqc;
+      if (lane == u) { my0 = p0; my1 = p1; }
+    }
+    softmax();
+#pragma unroll
+    for (int u = 0; u < ATT_EB; ++u) {
+      if (u >= ne) break;
+      o0 += v0[u] * __shfl(t0, u, 64);
+      o1 += v1[u] * __shfl(t1, u, 64);
+    }
+    return make_float2(o0 + sk0, o1 + sk1);
+  }
   for (int b = 0; b < ne; b += ATT_EB) {
     float k0[ATT_EB], k1[ATT_EB];
 #pragma unroll
@@ -1445,20 +1434,7 @@ __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
       if (lane == b + u) { my0 = p0; my1 = p1; }
     }
   }
-  const float mx0 = wave_max(my0), mx1 = wave_max(my1);
-  const float ex0 = lane < ne ? expf(my0 - mx0) : 0.f, ex1 = lane < ne ? expf(my1 - mx1) : 0.f;
-  const float a0 = ex0 / (wave_sum(ex0) + 1e-16f), a1 = ex1 / (wave_sum(ex1) + 1e-16f);
-  float t0 = a0, t1 = a1;
-  if (TRAIN && lane < ne) {
-    c.alpha[(int64_t)(e0 + lane) * 2] = a0;
-    c.alpha[(int64_t)(e0 + lane) * 2 + 1] = a1;
-    if (c.drop) {
-      const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-      t0 *= att_keep(c, seed, x, e0 + lane, 0);
-      t1 *= att_keep(c, seed, x, e0 + lane, 1);
-    }
-  }
-  float o0 = 0.f, o1 = 0.f;
+  softmax();
   for (int b = 0; b < ne; b += ATT_EB) {
     float v0[ATT_EB], v1[ATT_EB];
 #pragma unroll
@@ -1476,9 +1452,26 @@ __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
       o1 += v1[u] * __shfl(t1, b + u, 64);
     }
   }
-  if (lane < C) {
-    c.Zc[(int64_t)x * HC + lane] = o0 + Pi[3 * HC + lane];
-    c.Zc[(int64_t)x * HC + C + lane] = o1 + Pi[3 * HC + C + lane];
+  return make_float2(o0 + sk0, o1 + sk1);
+}
+template <bool TRAIN>
+__global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
+  TGNX_STAMP(4);
+  const int lane = threadIdx.x & 63;
+  const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // one round for the batch descriptor, the centre count and the centre's row / edge range: the centre
+  // arrays hold ccap rows (ceoff ccap + 1), so the read is clamped, and discarded past the runtime count
+  const int xc = min(x, max(c.ccap - 1, 0));
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  const int64_t err = c.ctl[TGNX_CTL_ERR];
+  const int R = c.cnt[c.rsel];
+  const int i = c.cent_loc[xc];
+  const int e0 = c.ceoff[xc], e1 = c.ceoff[xc + 1];
+  if (B == 0 || err != 0 || x >= R) return;
+  const float2 o = attn_centre<TRAIN>(c, x, i, e0, e1 - e0, lane);
+  if (lane < c.C) {
+    c.Zc[(int64_t)x * c.HC + lane] = o.x;
+    c.Zc[(int64_t)x * c.HC + c.C + lane] = o.y;
   }
 }
 
@@ -1500,6 +1493,12 @@ __host__ __device__ inline size_t tgn_pred_smem(int D) { return (size_t)2 * D * 
 constexpr int PRED_SU = 16;  // float4 per staging thread per matrix per round (D <= 110: one round)
 // nmk > 0 (pipelined resident step): the last nmk blocks mark the NEXT batch instead (mark_body, ahead 1):
 // the ring insert of this batch ran beside the GRU, and nothing of this step reads what marking writes.
+// ATT (1-hop train): the TransformerConv forward of the event's three roots runs here too — waves 1-3 one
+// root each (attn_centre, its row / edge range from the per-root record tgn_agg_emit wrote), writing the
+// embedding rows straight into LDS, while wave 0 stages the weights: no tgn_attn_fwd launch, and the
+// attention chain overlaps the weight staging.  A centre shared by several roots is computed by each of
+// them, identically (its alpha stores write equal values).
+template <bool ATT>
 __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
   TGNX_STAMP(5);
   extern __shared__ __attribute__((aligned(16))) float Wl[];  // [2][D][DP]: lin_src, lin_dst
@@ -1526,7 +1525,18 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
   const int64_t err = c.ctl[TGNX_CTL_ERR];
   const int i = lo + blockIdx.x;
   const bool live = !(B == 0 || i >= hi || err != 0);
-  if (wv == 0) {
+  constexpr int NST = ATT ? 64 : 192;  // staging threads (ATT: wave 0; 8 waves with 5 staging ones: ±0)
+  if (ATT && wv >= 1) {
+    const int r = wv - 1;
+    const int4 q = c.evq[3 * blockIdx.x + r];  // {centre row, P row, edge range}; grid = max_batch: in bounds
+    if (!live) return;
+    const float2 o = attn_centre<true>(c, q.x, q.y, q.z, q.w - q.z, lane);
+    if (lane < c.C) {
+      z[r][lane] = o.x;
+      z[r][c.C + lane] = o.y;
+    }
+    if (lane == 0) scr[r] = q.x;
+  } else if (!ATT && wv == 0) {
     int cr[3];  // the roots' centre rows (tgn_agg_emit) by rank-local event: issued with the ctl loads
 #pragma unroll
     for (int r = 0; r < 3; ++r) cr[r] = c.evr[3 * blockIdx.x + r];  // grid = max_batch: in bounds
@@ -1534,7 +1544,7 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
     for (int x = lane; x < 3 * D; x += 64) z[x / D][x % D] = c.Zc[(int64_t)cr[x / D] * D + x % D];
     if (lane < 3) scr[lane] = cr[lane];
   } else {
-    const int st = tid - 64;  // 192 staging threads
+    const int st = ATT ? tid : tid - 64;  // NST staging threads
     if (blockIdx.x == 0 && st == 0) {
       c.cnt[CNT_LIST] = 3 * (hi - lo);
       if (c.adf.p) {  // fused Adam: this step's scalars for the gradient writers (tgn_adam computes them itself)
@@ -1550,16 +1560,16 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
     const float invD = 1.0f / (float)D;
     const float4* S4 = reinterpret_cast<const float4*>(c.params + c.L.lsw);
     const float4* D4 = reinterpret_cast<const float4*>(c.params + c.L.ldw);
-    for (int b0 = 0; b0 < n4; b0 += 192 * PRED_SU) {
+    for (int b0 = 0; b0 < n4; b0 += NST * PRED_SU) {
       float4 ws4[PRED_SU], wd4[PRED_SU];
 #pragma unroll
       for (int u = 0; u < PRED_SU; ++u) {
-        const int x = min(b0 + st + 192 * u, n4 - 1);
+        const int x = min(b0 + st + NST * u, n4 - 1);
         ws4[u] = S4[x];
         wd4[u] = D4[x];
       }
       if (b0 == 0)
-        for (int x = st; x < 3 * D + 1; x += 192) {
+        for (int x = st; x < 3 * D + 1; x += NST) {
           const float v = x < D ? c.params[c.L.lsb + x] : x < 2 * D ? c.params[c.L.ldb + x - D]
                         : x < 3 * D ? c.params[c.L.lfw + x - 2 * D] : c.params[c.L.lfb];
           if (x < D) vsb[x] = v;
@@ -1569,7 +1579,7 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
       if (flat) {
 #pragma unroll
         for (int u = 0; u < PRED_SU; ++u) {
-          const int x = b0 + st + 192 * u;
+          const int x = b0 + st + NST * u;
           if (x < n4) {
             reinterpret_cast<float4*>(Wsrc)[x] = ws4[u];
             reinterpret_cast<float4*>(Wdst)[x] = wd4[u];
@@ -1579,7 +1589,7 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
       }
 #pragma unroll
       for (int u = 0; u < PRED_SU; ++u) {
-        const int x = b0 + st + 192 * u;
+        const int x = b0 + st + NST * u;
         if (x < n4) {
           const float vs[4] = {ws4[u].x, ws4[u].y, ws4[u].z, ws4[u].w};
           const float vd[4] = {wd4[u].x, wd4[u].y, wd4[u].z, wd4[u].w};
@@ -1594,6 +1604,9 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
       }
     }
   }
+#ifdef TGNX_STAMP_STAGE  // diagnostic: checkpoint 1 = wave 0 done with its part before the first barrier
+  TGNX_STAMP_AT(1);
+#endif
   __syncthreads();
   const int cr[3] = {scr[0], scr[1], scr[2]};
   const int kc = (D + 3) / 4, k0 = wv * kc, nk = min(D - k0, kc);
@@ -1692,7 +1705,9 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
   // barrier for dh (LDS) only: the evs-row stores of wave 0 stay in flight (__syncthreads waits vmcnt(0))
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+#ifndef TGNX_STAMP_STAGE
   TGNX_STAMP_AT(1);
+#endif
   // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn (split over k, lanes over o)
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
@@ -2459,6 +2474,12 @@ struct MarkNextJob {
 };
 // launch of the pipelined step that carries the next batch's marking: 3 = q|k|v|skip GEMM, 5 =
 // tgn_pred_train, 7 = kv_reduce ‖ dE GEMMs, 8 = weight gradients ‖ dz0, 9 = dW_gru ‖ dX_enc
+#ifndef TGNX_SCAN_T
+#define TGNX_SCAN_T TGN_SCAN_THREADS  // train-step scan workgroup size (experiments)
+#endif
+#ifndef TGNX_PRED_ATT
+#define TGNX_PRED_ATT 1  // 1 hop: attention forward inside tgn_pred_train (0: its own launch)
+#endif
 #ifndef TGNX_PIPE_MARK_AT
 #define TGNX_PIPE_MARK_AT 7
 #endif
@@ -2623,7 +2644,7 @@ static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_spl
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
-      Ep, alpha, Zc, evs, evr, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
+      Ep, alpha, Zc, evs, evr, evq, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
       rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF, total;
   int tgp_rows, tgp_e1;
 };
@@ -2664,6 +2685,7 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.Zc = carve(off, (size_t)k.Rcap * HC * 4);
   W.evs = carve(off, (size_t)k.B * evs_stride(D) * 4);
   W.evr = carve(off, (size_t)k.B * 3 * 4);
+  W.evq = carve(off, (size_t)k.B * 3 * 16);
   W.Hs = carve(off, (size_t)k.Rcap * D * 4);
   W.Hd = carve(off, (size_t)k.Rcap * D * 4);
   W.dZc = carve(off, (size_t)k.Rtr * HC * 4);
@@ -2814,6 +2836,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.Zc = reinterpret_cast<float*>(ws + W.Zc);
   c.evs = reinterpret_cast<float*>(ws + W.evs);
   c.evr = reinterpret_cast<int*>(ws + W.evr);
+  c.evq = k.layers == 2 ? nullptr : reinterpret_cast<int4*>(ws + W.evq);
   c.Hs = reinterpret_cast<float*>(ws + W.Hs);
   c.Hd = reinterpret_cast<float*>(ws + W.Hd);
   c.dZc = reinterpret_cast<float*>(ws + W.dZc);
@@ -2967,9 +2990,11 @@ int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf
 
 // tgn_pred_train stages the predictor weights in dynamic LDS (up to 2 x 128 x 129 floats)
 static bool pred_smem_ok(int D) {
-  static const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&tgn_pred_train),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)tgn_pred_smem(TDMAX)) == hipSuccess;
+  auto set = [](const void* f) {
+    return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tgn_pred_smem(TDMAX)) == hipSuccess;
+  };
+  static const bool ok = set(reinterpret_cast<const void*>(&tgn_pred_train<false>)) &&
+                         set(reinterpret_cast<const void*>(&tgn_pred_train<true>));
   return ok && tgn_pred_smem(D) <= tgn_pred_smem(TDMAX);
 }
 
@@ -3031,7 +3056,7 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     tgn_mark<true><<<nmark, 256, 0, s>>>(c, nmark);
     TGNX_LAUNCH_CHECK("tgn_mark");
     probe_begin(TGNX_K_ASSEMBLE, s);
-    tgn_scan<true><<<3, TGN_SCAN_THREADS, tgn_scan_smem(k.B), s>>>(c);
+    tgn_scan<true><<<3, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
     probe_end(TGNX_K_ASSEMBLE, s);
     TGNX_LAUNCH_CHECK("tgn_scan");
   }
@@ -3070,10 +3095,14 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
                gemm_job<G32>(gemm_shape<G32>(k.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
                              LoadProjW{P + c.L.wq, c.L.pw, HC, D}, EpiProj{P + c.L.bq, c.L.pb, c.P, HC}, (float*)nullptr));
   TGNX_LAUNCH_CHECK("tgn_proj");
-  probe_begin(TGNX_K_SEG_FWD, s);
-  tgn_attn_fwd<true><<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c);
-  probe_end(TGNX_K_SEG_FWD, s);
-  TGNX_LAUNCH_CHECK("tgn_attn_fwd");
+  // 1 hop: the attention forward runs inside tgn_pred_train (per root, beside its weight staging)
+  const bool att_in_pred = !two && TGNX_PRED_ATT;
+  if (!att_in_pred) {
+    probe_begin(TGNX_K_SEG_FWD, s);
+    tgn_attn_fwd<true><<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c);
+    probe_end(TGNX_K_SEG_FWD, s);
+    TGNX_LAUNCH_CHECK("tgn_attn_fwd");
+  }
   const Ctx cr = two ? root_view(c) : c;  // the level the predictor reads
   if (two) {  // conv2 over the roots: projections of h1 (rows = outer centres), attention per root
     gemm_launch<G32>(gemm_shape<G32>(k.Rtr, 4 * HC, HC, c.cnt + CNT_R), LoadRowK{c.Zc, k.Rtr, HC, HC},
@@ -3086,7 +3115,10 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   TGNX_CHECK_ARG(pred_smem_ok(c.D), "tgn_pred_train: dynamic LDS attribute refused");
   const int nmk = pipe && TGNX_PIPE_MARK_AT == 5 ? nmark : 0;
   const size_t psm = std::max(tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0);
-  tgn_pred_train<<<k.B + nmk, 256, psm, s>>>(cr, nmk);
+  if (att_in_pred)
+    tgn_pred_train<true><<<k.B + nmk, 256, psm, s>>>(cr, nmk);
+  else
+    tgn_pred_train<false><<<k.B + nmk, 256, psm, s>>>(cr, nmk);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
   probe_begin(TGNX_K_SEG_BWD, s);
@@ -3174,7 +3206,7 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   TGNX_LAUNCH_CHECK("tgn_fixup_update");
   if (pipe) {  // the next batch (counters advanced by the fixup): sorted node sets, plans, descriptor
     probe_begin(TGNX_K_ASSEMBLE, s);
-    tgn_scan<true><<<3, TGN_SCAN_THREADS, tgn_scan_smem(k.B), s>>>(c);
+    tgn_scan<true><<<3, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
     probe_end(TGNX_K_ASSEMBLE, s);
     TGNX_LAUNCH_CHECK("tgn_scan_next");
   }
