@@ -143,7 +143,11 @@ int64_t tgnx_stamps_count(void);
 #define TGNX_CTL_LOSS 12        /* (double) running sum of loss * B (epoch_utils.py:310) */
 #define TGNX_CTL_SUM_E 13       /* running sum of assembled edges (roofline units) */
 #define TGNX_CTL_SUM_S 14       /* running sum of assembled segments */
-#define TGNX_CTL_WORDS 16
+/* 15: internal (fused-Adam step scalars) */
+#define TGNX_CTL_STEP_B 16      /* B of the last trained step (tgnx_tgnn_advance / the resident step's last
+                                   launch): what tgnx_tgn_train_update checks, since a pipelined step's
+                                   descriptor already holds the NEXT batch when its update runs */
+#define TGNX_CTL_WORDS 24
 
 #define TGNX_TGNN_NPARAM 15     /* te_w te_b attn_l attn_r attn_e Wn bn We be Ws bs Wd bd Wo bo */
 
@@ -359,13 +363,26 @@ int tgnx_tgn_train_step_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buf
 int tgnx_tgn_train_fwd_bwd_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
                                     int64_t split_hi, int64_t batch, int32_t rank, int32_t world,
                                     uint64_t base_seed, int32_t dropout, void* stream);
+/* tgnx_tgn_train_fwd_bwd_resident pipelined across steps, as tgnx_tgn_train_step_pipelined (world >= 1;
+ * Adam is not folded in): the next batch (this rank's slice) is marked inside the k / v reduction launch and
+ * scanned after this call's last launch, so the next call starts at the message aggregation.  The exchange
+ * and tgnx_tgn_apply_rows_update follow each call (that update reads STEP_B, not B: the descriptor words
+ * already describe the next batch).  prefetched as for tgnx_tgn_train_step_pipelined.  Per rank, results
+ * equal tgnx_tgn_train_fwd_bwd_resident's step for step.  Test: tests/test_gpu_tgn_dp.py. */
+int tgnx_tgn_train_fwd_bwd_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                                     int64_t split_hi, int64_t batch, int32_t rank, int32_t world,
+                                     uint64_t base_seed, int32_t dropout, int32_t prefetched, void* stream);
+/* tgnx_tgn_apply_rows + tgnx_tgn_train_update in one launch (data parallel, after the exchange). */
+int tgnx_tgn_apply_rows_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, float* rows, int64_t nrows,
+                               void* stream);
 /* Data parallel: write the exchanged rows of every rank (rows [nrows, TGNX_TGN_ROW(mem_dim)], slots
  * with node -1 skipped) into memory / last_update, then zero `rows` (ready for the next summing
  * exchange).  Ranks that updated the same node computed the same row (same replicated inputs), so the
  * order does not matter. */
 int tgnx_tgn_apply_rows(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, float* rows, int64_t nrows,
                         void* stream);
-/* Train batch, part 2: Adam on the (possibly all-reduced) grads, loss sum. */
+/* Train batch, part 2: Adam on the (possibly all-reduced) grads, loss sum; nothing when the step's batch
+ * (ctl STEP_B) was empty. */
 int tgnx_tgn_train_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream);
 /* Eval batch (TGB tgbl link prediction): every event's [pos, Kn negatives] scored with the
  * batch-start memory and ring, per-event reciprocal rank in buf->mrr, then update_state in eval

@@ -113,6 +113,7 @@ def test_tgn_dp_resident_folded_cursor_per_rank():
             e = TgnEngine(model, LastNeighborLoader(N, 10, device=dev), ev, TgnAdam(model, 1e-3),
                           dst_nodes=s.dst_nodes, seed=77, rank=rank, world=2)
             e.fold_cursor = fold
+            e.pipeline = False   # the pipelined form has its own test below
             e.bind_resident(0, split_hi, B, dropout=True)
             e.begin_epoch()
             eng[fold, rank] = e
@@ -159,3 +160,86 @@ def test_tgn_dp_resident_folded_cursor_per_rank():
                 f.adam_m.copy_(u.adam_m)
                 f.adam_v.copy_(u.adam_v)
                 f.model.memory.memory.copy_(u.model.memory.memory)
+
+
+def test_tgn_dp_pipelined_per_rank():
+    """Data-parallel pipelined steps (tgnx_tgn_train_fwd_bwd_pipelined, world = 2, one device: each step
+    marks its rank's slice of the NEXT batch in the k / v reduction launch and scans it after its last
+    launch; tgnx_tgn_apply_rows_update writes the exchanged rows and runs Adam in one launch) against the
+    folded resident steps + apply_rows + train_update, per rank: counters, negatives, gradients and packed
+    rows after fwd_bwd; memory, last_update, parameters, moments and loss after the update.  The split ends
+    with a partial batch (20 events) and one step runs past it (B = 0: memory — node 0 included — and
+    parameters must not change).  The pipelined twin is re-synchronised from the folded one after each step."""
+    from oracle.tgn_ref import RefTGN
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.synth import make_stream
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    N, B, d, D = 400, 64, 16, 32
+    s = make_stream("tgbl-wiki", seed=9, num_events=B * 9, num_nodes=N, msg_dim=d)
+    torch.manual_seed(0)
+    sd = RefTGN(N, d, hidden=D, aggr="last", dropout=0.1).state_dict()
+    dev = torch.device("cuda")
+    ev = dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32), msg=s.msg)
+    split_hi = 7 * B + 20
+    eng = {}
+    for pipe in (True, False):
+        for rank in (0, 1):
+            model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=1, aggr="last", dropout=0.1)
+            model.load_reference_state(sd)
+            e = TgnEngine(model, LastNeighborLoader(N, 10, device=dev), ev, TgnAdam(model, 1e-3),
+                          dst_nodes=s.dst_nodes, seed=77, rank=rank, world=2)
+            e.pipeline = pipe
+            e.bind_resident(0, split_hi, B, dropout=True)
+            e.begin_epoch()
+            assert e._pipelined() == pipe
+            eng[pipe, rank] = e
+    for st in range(9):
+        mem0 = eng[False, 0].model.memory.memory.clone()
+        flat0 = eng[False, 0].model.flat.clone()
+        for e in eng.values():
+            e._pre(e._prefetched)
+        torch.cuda.synchronize()
+        for e in eng.values():
+            e.check()
+        end = min(split_hi, (st + 1) * B)
+        for rank in (0, 1):
+            p, u = eng[True, rank], eng[False, rank]
+            for w in (3, 4, 10, 16):   # GEN, ADAM_T, NB, STEP_B
+                assert int(p.ctl[w]) == int(u.ctl[w]), (st, rank, w, int(p.ctl[w]), int(u.ctl[w]))
+            Bst = int(u.ctl[16])
+            assert Bst == (B if st < 7 else 20 if st == 7 else 0), (st, Bst)
+            assert torch.equal(p.neg_train[:end], u.neg_train[:end]), (st, rank)
+            G = p.model.grad_flat.numel()
+            if Bst:
+                assert _rel(p.comm[:G - 1], u.comm[:G - 1]) < 1e-5, (st, rank)
+                assert abs(float(p.comm[G - 1]) - float(u.comm[G - 1])) < 1e-5, (st, rank)
+            assert torch.equal(p.xrows, u.xrows), (st, rank)
+        for pipe in (True, False):
+            tot = eng[pipe, 0].comm + eng[pipe, 1].comm
+            for rank in (0, 1):
+                eng[pipe, rank].comm.copy_(tot)
+        for e in eng.values():
+            e._post()
+            e._prefetched = e._pipelined()
+        torch.cuda.synchronize()
+        for rank in (0, 1):
+            p, u = eng[True, rank], eng[False, rank]
+            pm, um = p.model, u.model
+            assert torch.equal(pm.memory.last_update, um.memory.last_update), (st, rank)
+            assert torch.allclose(pm.memory.memory, um.memory.memory, atol=1e-6), (st, rank)
+            assert _rel(pm.flat, um.flat) < 1e-6, (st, rank)
+            assert _rel(p.adam_m, u.adam_m) < 1e-5 and _rel(p.adam_v, u.adam_v) < 1e-5, (st, rank)
+            assert abs(p.loss_sum() - u.loss_sum()) <= 1e-6 * max(1.0, abs(u.loss_sum())), (st, rank)
+            assert torch.equal(p.loader.e_id, u.loader.e_id) and torch.equal(p.model.store, u.model.store), (st, rank)
+        if st == 8:   # past the split: nothing changes (the exchange slots read as unused, Adam skips)
+            for e in eng.values():
+                assert torch.equal(e.model.memory.memory, mem0), st
+                assert torch.equal(e.model.flat, flat0), st
+        assert torch.equal(eng[True, 0].model.memory.memory, eng[True, 1].model.memory.memory), st
+        for rank in (0, 1):
+            p, u = eng[True, rank], eng[False, rank]
+            with torch.no_grad():
+                p.model.flat.copy_(u.model.flat)
+                p.adam_m.copy_(u.adam_m)
+                p.adam_v.copy_(u.adam_v)
+                p.model.memory.memory.copy_(u.model.memory.memory)

@@ -2348,10 +2348,18 @@ struct TeReduceTail {
 };
 
 // ------------------------------------------------------------------ optimizer + state update
-__global__ void __launch_bounds__(256) tgn_adam(Ctx c) {
+// Adam over the flat buffer; the last nrb blocks (data parallel, after the exchange) write the exchanged
+// memory rows instead (tgn_apply_rows' body).  Skipped when the step's batch was empty (STEP_B: a
+// pipelined step's descriptor already holds the next batch).
+__device__ void apply_rows_body(float* mem, int64_t* lu, float* rows, int64_t nrows, int D, int64_t N, int bid, int nb);
+__global__ void __launch_bounds__(256) tgn_adam(Ctx c, float* rows, int64_t nrows, int nrb) {
   TGNX_STAMP(7);
+  if ((int)blockIdx.x >= (int)gridDim.x - nrb) {
+    apply_rows_body(c.mem, c.lu_buf, rows, nrows, c.D, c.N, (int)blockIdx.x - ((int)gridDim.x - nrb), nrb);
+    return;
+  }
   __shared__ float sc[2];
-  const int64_t B = c.ctl[TGNX_CTL_B];
+  const int64_t B = c.ctl[TGNX_CTL_STEP_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   if (threadIdx.x == 0) {
     const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
@@ -2362,11 +2370,12 @@ __global__ void __launch_bounds__(256) tgn_adam(Ctx c) {
   __syncthreads();
   const float step = sc[0], bc2s = sc[1];
   const int64_t n4 = c.L.total / 4;
+  const int nab = (int)gridDim.x - nrb;
   float4* P4 = reinterpret_cast<float4*>(c.params);
   float4* M4 = reinterpret_cast<float4*>(c.am);
   float4* V4 = reinterpret_cast<float4*>(c.av);
   const float4* G4 = reinterpret_cast<const float4*>(c.grads);
-  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n4; x += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n4; x += (int64_t)nab * blockDim.x) {
     const float4 g = G4[x];
     float4 m = M4[x], v = V4[x], p = P4[x];
     adam1(g.x, m.x, v.x, p.x, c.b1, c.b2, c.eps, step, bc2s);
@@ -2406,9 +2415,15 @@ __device__ void update_body(const Ctx& c, int blk, int nmem, int nst, int mem_mo
                             const int* list_cnt, int n_host, int64_t base) {
   const int lane = threadIdx.x & 63;
   if (blk < nmem) {
-    if (mem_mode == 0 && (c.ctl[TGNX_CTL_B] == 0 || c.ctl[TGNX_CTL_ERR] != 0)) return;
-    const int n = list_cnt ? *list_cnt : n_host;
     const int RW = TGNX_TGN_ROW(c.D);
+    if (mem_mode == 0 && (c.ctl[TGNX_CTL_B] == 0 || c.ctl[TGNX_CTL_ERR] != 0)) {
+      // nothing updated: every exchange slot of this rank unused (the slots hold zeros since the last
+      // apply, which would otherwise read as node 0)
+      if (c.xrows)
+        for (int u = blk * blockDim.x + threadIdx.x; u < c.xcap; u += nmem * blockDim.x) c.xrows[(int64_t)u * RW] = -1.f;
+      return;
+    }
+    const int n = list_cnt ? *list_cnt : n_host;
     float* xr = mem_mode == 0 ? c.xrows : nullptr;
     if (xr && n > c.xcap) {
       if (blk == 0 && threadIdx.x == 0) c.ctl[TGNX_CTL_ERR] |= 8;
@@ -2500,6 +2515,7 @@ struct TrainTail {
         int64_t* ctl = te.c.ctl;
         ctl[TGNX_CTL_GEN] += 1;
         ctl[TGNX_CTL_NB] += 1;
+        ctl[TGNX_CTL_STEP_B] = ctl[TGNX_CTL_B];
         if (ctl[TGNX_CTL_B] > 0) ctl[TGNX_CTL_ADAM_T] += 1;
       }
       return;
@@ -2511,10 +2527,10 @@ struct TrainTail {
 
 // data parallel: the exchanged memory rows of every rank -> memory / last_update (wave per row); the
 // rows are zeroed after use (the next step's exchange sums every rank's slot into them)
-__global__ void __launch_bounds__(256) tgn_apply_rows(float* mem, int64_t* lu, float* rows, int64_t nrows, int D,
-                                                      int64_t N) {
+__device__ void apply_rows_body(float* mem, int64_t* lu, float* rows, int64_t nrows, int D, int64_t N, int bid,
+                                int nb) {
   const int lane = threadIdx.x & 63, RW = TGNX_TGN_ROW(D);
-  for (int64_t u = blockIdx.x * 4 + (threadIdx.x >> 6); u < nrows; u += (int64_t)gridDim.x * 4) {
+  for (int64_t u = bid * 4 + (threadIdx.x >> 6); u < nrows; u += (int64_t)nb * 4) {
     float* row = rows + u * RW;
     const float h0 = row[0], h1 = row[1], h2 = row[2], h3 = row[3];
     const int64_t v = (int64_t)h0;
@@ -2527,6 +2543,10 @@ __global__ void __launch_bounds__(256) tgn_apply_rows(float* mem, int64_t* lu, f
     if (ok && lane == 0)
       lu[v] = (int64_t)((uint64_t)(uint32_t)h1 | ((uint64_t)(uint32_t)h2 << 24) | ((uint64_t)(uint32_t)h3 << 48));
   }
+}
+__global__ void __launch_bounds__(256) tgn_apply_rows(float* mem, int64_t* lu, float* rows, int64_t nrows, int D,
+                                                      int64_t N) {
+  apply_rows_body(mem, lu, rows, nrows, D, N, blockIdx.x, gridDim.x);
 }
 }  // namespace tgn
 }  // namespace tgnx
@@ -3043,8 +3063,7 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     c.adf.eps = c.eps;
   }
   TGNX_CHECK_ARG(!gen_neg || (buf->dst_nodes && buf->n_dst > 0), "tgnx_tgn_train_fwd_bwd: no destination set");
-  TGNX_CHECK_ARG(pipe == 0 || (adv && fuse_adam && adv->world == 1),
-                 "tgnx_tgn_train_step_pipelined: resident world-1 steps only");
+  TGNX_CHECK_ARG(pipe == 0 || adv, "tgnx_tgn_train_step_pipelined: resident steps only");
   c.gen_neg = gen_neg ? 1 : 0;
   c.drop = dropout && cfg->dropout > 0.f;
   hipStream_t s = as_stream(stream);
@@ -3237,6 +3256,13 @@ int tgnx_tgn_train_step_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buf
   return train_step_impl(cfg, buf, 1, dropout, stream, true, &a, prefetched ? 1 : 2);
 }
 
+int tgnx_tgn_train_fwd_bwd_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                                     int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
+                                     int32_t dropout, int32_t prefetched, void* stream) {
+  const AdvArgs a{split_lo, split_hi, batch, rank, world, base_seed};
+  return train_step_impl(cfg, buf, 1, dropout, stream, false, &a, prefetched ? 1 : 2);
+}
+
 int tgnx_tgn_train_fwd_bwd_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
                                     int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
                                     int32_t dropout, void* stream) {
@@ -3265,9 +3291,25 @@ int tgnx_tgn_train_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* bu
   if (rc) return rc;
   TGNX_CHECK_ARG(buf->grads && buf->adam_m && buf->adam_v, "tgnx_tgn_train_update: null optimizer buffer");
   probe_begin(TGNX_K_ADAM, as_stream(stream));
-  tgn_adam<<<gridn(c.L.total / 4, 256), 256, 0, as_stream(stream)>>>(c);
+  tgn_adam<<<gridn(c.L.total / 4, 256), 256, 0, as_stream(stream)>>>(c, nullptr, 0, 0);
   probe_end(TGNX_K_ADAM, as_stream(stream));
   TGNX_LAUNCH_CHECK("tgn_adam");
+  return TGNX_OK;
+}
+int tgnx_tgn_apply_rows_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, float* rows, int64_t nrows,
+                               void* stream) {
+  Ctx c;
+  Caps k;
+  WsLay W;
+  int rc = make_ctx(cfg, buf, 1, c, k, W);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(buf->grads && buf->adam_m && buf->adam_v, "tgnx_tgn_apply_rows_update: null optimizer buffer");
+  TGNX_CHECK_ARG(nrows >= 0 && (nrows == 0 || rows), "tgnx_tgn_apply_rows_update: bad rows");
+  const int nrb = nrows ? gridn(nrows, 4, 1024) : 0;
+  probe_begin(TGNX_K_ADAM, as_stream(stream));
+  tgn_adam<<<gridn(c.L.total / 4, 256) + nrb, 256, 0, as_stream(stream)>>>(c, rows, nrows, nrb);
+  probe_end(TGNX_K_ADAM, as_stream(stream));
+  TGNX_LAUNCH_CHECK("tgn_adam_rows");
   return TGNX_OK;
 }
 

@@ -239,6 +239,7 @@ __global__ void tgnn_advance(int64_t* ctl, int mode, int64_t batch_start, int64_
   }
   ctl[TGNX_CTL_BATCH_START] = bs;
   ctl[TGNX_CTL_B] = Bv;
+  ctl[TGNX_CTL_STEP_B] = Bv;
   ctl[TGNX_CTL_CUR_EID] = ce;
   ctl[TGNX_CTL_GEN] += 1;
   ctl[TGNX_CTL_NB] += 1;

@@ -55,7 +55,7 @@ class TgnnEngine:
             raise RuntimeError(f"tgnx_tgnn_ws_bytes: invalid config: {_lib.lib().tgnx_last_error().decode()}")
         self.ws = torch.zeros(nb, dtype=torch.uint8, device=self.dev)
         self.node_map = torch.zeros(4 * cfg.num_nodes, dtype=torch.int32, device=self.dev)
-        self.ctl = torch.zeros(16, dtype=torch.int64, device=self.dev)
+        self.ctl = torch.zeros(24, dtype=torch.int64, device=self.dev)   # TGNX_CTL_WORDS
         cap = cfg.max_batch * max(cfg.max_neg, 1)
         self.out_pos = torch.zeros(cfg.max_batch, dtype=torch.float32, device=self.dev)
         self.out_neg = torch.zeros(cap, dtype=torch.float32, device=self.dev)

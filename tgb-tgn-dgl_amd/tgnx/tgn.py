@@ -251,7 +251,7 @@ class TgnEngine:
         if nb == 0:
             raise RuntimeError(f"tgnx_tgn_ws_bytes: {_lib.lib().tgnx_last_error().decode()}")
         self.ws = torch.zeros(nb, dtype=torch.uint8, device=self.dev)
-        self.ctl = torch.zeros(16, dtype=torch.int64, device=self.dev)
+        self.ctl = torch.zeros(24, dtype=torch.int64, device=self.dev)   # TGNX_CTL_WORDS
         self.neg_train = torch.zeros(cfg.num_events, dtype=torch.long, device=self.dev)
         self.out_pos = torch.zeros(cfg.max_batch, dtype=torch.float32, device=self.dev)
         self.out_neg = torch.zeros(cfg.max_batch * max(cfg.max_neg, 1), dtype=torch.float32, device=self.dev)
@@ -263,7 +263,8 @@ class TgnEngine:
         # (world 1, Adam fused) or tgnx_tgn_train_fwd_bwd_resident (world > 1; exchange + update follow).
         # Both forms are tested against advance + step per rank (test_gpu_tgn.py, test_gpu_tgn_dp.py).
         self.fold_cursor = True
-        # world-1 fused resident steps pipeline across steps (tgnx_tgn_train_step_pipelined): each step marks
+        # resident steps pipeline across steps (world 1: tgnx_tgn_train_step_pipelined; world > 1:
+        # tgnx_tgn_train_fwd_bwd_pipelined, then the exchange and tgnx_tgn_apply_rows_update): each step marks
         # and scans the next batch, so the next step starts at the message aggregation.  `_prefetched` says
         # whether the last call on these buffers was such a step (any other call clears it).
         self.pipeline = True
@@ -366,9 +367,11 @@ class TgnEngine:
     def apply_update(self, allreduce: bool = True):
         if allreduce and self.world > 1:
             self._exchange()
-        if self.world > 1:
-            self._apply_rows(self._pending)
-        _lib.call("tgnx_tgn_train_update", ctypes.byref(self.cfg), ctypes.byref(self._pending), self._stream())
+        if self.world > 1:   # the exchanged rows and Adam in one launch
+            _lib.call("tgnx_tgn_apply_rows_update", ctypes.byref(self.cfg), ctypes.byref(self._pending),
+                      _p(self.xgather), self.xgather.shape[0], self._stream())
+        else:
+            _lib.call("tgnx_tgn_train_update", ctypes.byref(self.cfg), ctypes.byref(self._pending), self._stream())
 
     def _exchange(self):
         """The step's one collective: gradient sum and the touched memory rows of every rank (an
@@ -403,7 +406,7 @@ class TgnEngine:
         L = _lib.lib()
         self._res_fused = self._fused()
         self._f = (L.tgnx_tgnn_advance, L.tgnx_tgn_train_step if self._res_fused else L.tgnx_tgn_train_fwd_bwd,
-                   L.tgnx_tgn_train_update, L.tgnx_tgn_apply_rows)
+                   L.tgnx_tgn_train_update, L.tgnx_tgn_apply_rows_update)
         self._cfg_ref, self._buf_ref = ctypes.byref(self.cfg), ctypes.byref(self._res_buf)
         self._ctl_p = ctypes.c_void_p(self.ctl.data_ptr())
 
@@ -414,15 +417,19 @@ class TgnEngine:
         self._prefetched = False
 
     def _pipelined(self) -> bool:
-        return self.pipeline and self.fold_cursor and self._res_fused
+        return self.pipeline and self.fold_cursor and (self._res_fused or self.world > 1)
 
     def _pre(self, prefetched: bool = False):
         adv, fb = self._f[:2]
         lo, hi, batch = self._res
         st = self._stream()
-        if self._pipelined():
+        if self._pipelined() and self._res_fused:
             rc = _lib.lib().tgnx_tgn_train_step_pipelined(self._cfg_ref, self._buf_ref, lo, hi, batch, self.seed,
                                                          self._res_drop, 1 if prefetched else 0, st)
+        elif self._pipelined():
+            rc = _lib.lib().tgnx_tgn_train_fwd_bwd_pipelined(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank,
+                                                            self.world, self.seed, self._res_drop,
+                                                            1 if prefetched else 0, st)
         elif self.fold_cursor:   # the batch cursor folded into the step's first launches
             f = _lib.lib().tgnx_tgn_train_step_resident if self._res_fused else _lib.lib().tgnx_tgn_train_fwd_bwd_resident
             rc = f(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank, self.world, self.seed, self._res_drop, st)
@@ -435,10 +442,10 @@ class TgnEngine:
     def _post(self):
         st = self._stream()
         rc = 0
-        if self.world > 1:
+        if self.world > 1:   # the exchanged rows and Adam, one launch
             rc |= self._f[3](self._cfg_ref, self._buf_ref, ctypes.c_void_p(self.xgather.data_ptr()),
                              ctypes.c_int64(self.xgather.shape[0]), st)
-        if not self._res_fused:   # fused step: Adam already applied
+        elif not self._res_fused:   # fused step: Adam already applied
             rc |= self._f[2](self._cfg_ref, self._buf_ref, st)
         if rc:
             raise RuntimeError(f"tgnx TGN resident update failed: {_lib.lib().tgnx_last_error().decode()}")
@@ -465,8 +472,8 @@ class TgnEngine:
             self._graphs = (g, None)
         else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
-                self._pre()
+            with torch.cuda.graph(g1):   # pipelined: the steady-state step (the previous step prefetched)
+                self._pre(self._pipelined())
             with torch.cuda.graph(g2):
                 self._post()
             self._graphs = (g1, g2)
