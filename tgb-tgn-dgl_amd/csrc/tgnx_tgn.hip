@@ -734,6 +734,9 @@ __device__ __forceinline__ void store_event(const Ctx& c, const StoreView& s, in
   other = *(src ? c.ev_dst + e : c.ev_src + e);
   t = c.ev_t[e];
 }
+// AG: the aggregation compiled in (0 last, 1 mean, -1 either by c.aggr): the last-only kernel does not carry
+// the mean path's registers (233 -> fewer VGPRs: more tgn_agg_emit workgroups resident at once)
+template <int AG>
 __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
   const int D = c.D, d = c.d, Qm = c.Qm, enc0 = 2 * D + d;
   const StoreView sv = store_view(c, n);
@@ -753,7 +756,7 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
   }
   const float lun = (float)c.lu_buf[n];
   const float* rowN = c.mem + n * D;
-  if (c.aggr == 0) {
+  if (AG == 0 || (AG < 0 && c.aggr == 0)) {
     // winner: max t, first index in [msg_s; msg_d] order
     float tb = -INFINITY;
     int kb = 0x7fffffff;
@@ -1024,6 +1027,7 @@ __device__ __forceinline__ int root_row(const Ctx& c, int64_t v) {
 // The rest: mode 0 aggregation over the sampled nodes (train) + zeroing of the backward
 // accumulators, mode 1 last_update of the sampled nodes from the buffer (eval scoring), mode 2
 // aggregation over a node list (eval update / flush; list == nullptr: nodes base + m).
+template <int AG>
 __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, const int64_t* list,
                                                     const int* list_cnt, int n_host, int64_t base, int nevb = 0) {
   TGNX_STAMP(3);
@@ -1126,14 +1130,14 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
     }
   }
   const int n = mode == 0 ? c.cnt[CNT_M] : (list_cnt ? *list_cnt : n_host);
-  if (c.aggr == 1 && (mode == 0 || list)) {  // MeanAggregator, train / eval update: a workgroup per node (hub
+  if (AG != 0 && c.aggr == 1 && (mode == 0 || list)) {  // MeanAggregator, train / eval update: a workgroup per node (hub
                                              // nodes store many messages); the all-node flush stays wave-per-node
     for (int m = bid; m < n; m += nb) agg_node_mean_wg(c, mode == 0 ? c.nid[m] : list[m], m, mode == 0);
     return;
   }
   for (int m = bid * 4 + (threadIdx.x >> 6); m < n; m += nb * 4) {
     const int64_t v = mode == 0 ? c.nid[m] : (list ? list[m] : base + m);
-    agg_node(c, v, m, lane, mode == 0);
+    agg_node<AG>(c, v, m, lane, mode == 0);
   }
 }
 
@@ -2941,6 +2945,9 @@ static Ctx root_view(const Ctx& c) {
 // tgn_agg_emit's two grid-stride parts (sampled edges, wave per (centre, ring slot); sampled nodes):
 // grids sized from capacities launch mostly idle workgroups, which hold dispatch slots
 // (stamps timeline, wiki shape: caps 4096 / 2048 -> 1024 / 512 took agg_emit 16.5 -> 13.9 us)
+#ifndef TGNX_AGG_SPECIALIZE
+#define TGNX_AGG_SPECIALIZE 1  // last-aggregation steps launch tgn_agg_emit<0> (97 VGPRs instead of 233)
+#endif
 #ifndef TGNX_AGG_EDGE_CAP
 #define TGNX_AGG_EDGE_CAP 1024
 #endif
@@ -2957,7 +2964,10 @@ static inline int gridn(int64_t n, int per, int cap = 4096) {
 static void gru_list(const Ctx& c, const Caps& k, const int64_t* list, const int* list_cnt, int n_host, int64_t base,
                      int mcap, hipStream_t s) {
   const float* P = c.params;
-  tgn_agg_emit<<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
+  if (c.aggr == 0)
+    tgn_agg_emit<0><<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
+  else
+    tgn_agg_emit<-1><<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
   const GemmShape g1 = gemm_shape<G32L>(mcap, 4 * c.D, c.Qm + c.D, list_cnt);
   gemm_launch<G32L>(g1, LoadGruA{c.X, c.mem, list ? list : c.nid, base, c.Qm, c.D, list ? 0 : 1},
                    LoadGruW{P + c.L.w_ih, P + c.L.w_hh, c.Qm, c.D},
@@ -3082,8 +3092,11 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   const int nedge = gridn((int64_t)k.Rtr * c.K, 4, TGNX_AGG_EDGE_CAP);
   probe_begin(TGNX_K_EDGE_META, s);
   const int nevb = gridn(3 * k.B, 256);
-  tgn_agg_emit<<<nevb + nedge + gridn(k.Mtr, 4, TGNX_AGG_NODE_CAP), 256, 0, s>>>(c, 0, nedge, nullptr, nullptr, 0, 0,
-                                                                                   nevb);
+  const int nagg = nevb + nedge + gridn(k.Mtr, 4, TGNX_AGG_NODE_CAP);
+  if (c.aggr == 0 && TGNX_AGG_SPECIALIZE)
+    tgn_agg_emit<0><<<nagg, 256, 0, s>>>(c, 0, nedge, nullptr, nullptr, 0, 0, nevb);
+  else
+    tgn_agg_emit<-1><<<nagg, 256, 0, s>>>(c, 0, nedge, nullptr, nullptr, 0, 0, nevb);
   probe_end(TGNX_K_EDGE_META, s);
   TGNX_LAUNCH_CHECK("tgn_agg_emit");
   // GRU over every sampled node ‖ lin_edge over every sampled edge (‖ 2 hops: conv2's lin_edge over the
@@ -3337,7 +3350,7 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   tgn_scan<false><<<3, TGN_SCAN_THREADS, tgn_scan_smem(k.B), s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_scan");
   const int nedge = gridn((int64_t)Rq * c.K, 4, 4096);
-  tgn_agg_emit<<<nedge + gridn(Mq, 256), 256, 0, s>>>(c, 1, nedge, nullptr, nullptr, 0, 0);
+  tgn_agg_emit<-1><<<nedge + gridn(Mq, 256), 256, 0, s>>>(c, 1, nedge, nullptr, nullptr, 0, 0);
   TGNX_LAUNCH_CHECK("tgn_emit");
   const LoadEdgeAttr ea{c.encE, c.e_id, c.ev_msg, D, d};
   const auto j_edge = gemm_job<G32>(gemm_shape<G32>(Eq, HC, D + d, c.cnt + CNT_E), ea,
