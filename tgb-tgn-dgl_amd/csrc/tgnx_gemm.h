@@ -612,7 +612,14 @@ inline int job_blocks(const J& j) { return gemm_blocks(j.g); }
 template <class F, int SM>
 inline int job_blocks(const BlockJob<F, SM>& j) { return j.nb; }
 template <class... J>
+#ifndef TGNX_GEMMN_WAVES
+#define TGNX_GEMMN_WAVES 0  // amdgpu_waves_per_eu floor for gemmN launches (0 = compiler's choice; 5 measured +5 %)
+#endif
+#if TGNX_GEMMN_WAVES > 0
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TGNX_GEMMN_WAVES))) gemmN_kernel(J... j) {
+#else
 __global__ void __launch_bounds__(256) gemmN_kernel(J... j) {
+#endif
   TGNX_STAMP(22);
   constexpr int SM = std::max({J::Cfg::SMEM...});
   __shared__ __attribute__((aligned(16))) float smem[SM];

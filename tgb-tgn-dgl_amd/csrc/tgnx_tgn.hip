@@ -1931,7 +1931,10 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
 // and sums runs of equal neighbours in registers: one global atomic per (wave, neighbour run, column),
 // so a hub row sees a few atomics per chunk instead of one per edge.  (Merging in LDS with ds_add_f32
 // instead ran at about one element per two clocks per CU: slower than the contention it removed.)
-constexpr int KVR_CH = 64;            // edges per workgroup
+#ifndef TGNX_KVR_CH
+#define TGNX_KVR_CH 32  // 64: 133 VGPRs in the kv_reduce job lowered the whole launch to 3 waves per SIMD (+0.9 us)
+#endif
+constexpr int KVR_CH = TGNX_KVR_CH;   // edges per workgroup
 constexpr int KVR_PW = KVR_CH / 4;    // sorted edges per wave
 __device__ void kv_reduce_body(const Ctx& c, int bid) {
   const int B = (int)c.ctl[TGNX_CTL_B];
