@@ -276,7 +276,8 @@ def run_tgn(args, world, rank, dev):
     g = torch.Generator().manual_seed(0)
     model = TGNModel(N, stream.num_events, d, D, dev, ring=K, max_batch=Bg, max_neg=1,
                      aggr="mean" if args.aggr == "mean" else "last", dropout=0.0 if args.no_dropout else 0.1,
-                     generator=g, layers=args.layers)
+                     generator=g, layers=args.layers, updater=args.updater,
+                     memory="dyrep" if args.updater == "rnn" else "tgn")
     opt = TgnAdam(model, 1e-4)
     loader = LastNeighborLoader(N, K, device=dev)
     eng = TgnEngine(model, loader, dict(src=stream.src, dst=stream.dst, t=stream.t.astype(np.float32), msg=stream.msg),
@@ -375,7 +376,8 @@ def run_tgn(args, world, rank, dev):
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     # the PMC passes (tools/pmc_traffic.sh) run the default workload: wiki-shaped, 1 hop, last aggregation
-    pmc_workload = args.dataset == "tgbl-wiki" and args.layers == 1 and args.aggr == "last" and args.batch == 200
+    pmc_workload = (args.dataset == "tgbl-wiki" and args.layers == 1 and args.aggr == "last" and args.batch == 200
+                    and args.updater == "gru")
     if os.path.exists(pmc) and pmc_workload:
         try:
             traffic = json.load(open(pmc)).get(dom, {}).get("bytes_per_launch")
@@ -418,7 +420,9 @@ def run_tgn(args, world, rank, dev):
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic {args.dataset}-shaped stream (SURVEY.md §8d), events resident in HBM",
-        "config": {"workload": f"{args.dataset} TGN memory path (TGNMemory + GRUCell, IdentityMessage + "
+        "config": {"workload": f"{args.dataset} TGN memory path "
+                               f"({'DyRepMemory + RNNCell' if args.updater == 'rnn' else 'TGNMemory + GRUCell'}, "
+                               f"IdentityMessage + "
                                f"{'Mean' if args.aggr == 'mean' else 'Last'}Aggregator, "
                                f"{'2-hop temporal attention (conv2(conv1)), ' if args.layers == 2 else ''}"
                                f"TransformerConv heads=2, "
@@ -455,6 +459,8 @@ def main():
     ap.add_argument("--aggr", choices=["last", "mean"], default="last")
     ap.add_argument("--layers", type=int, choices=[1, 2], default=1,
                     help="TGN attention hops (2: the comment config's 2-hop temporal attention)")
+    ap.add_argument("--updater", choices=["gru", "rnn"], default="gru",
+                    help="TGN memory updater (rnn: DyRepMemory memory_updater_type 'rnn')")
     ap.add_argument("--only", action="store_true", help="skip the secondary path")
     ap.add_argument("--no-dropout", action="store_true", help="train mode without dropout")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -278,6 +278,9 @@ typedef struct {
   int32_t aggr;        /* 0 = LastAggregator, 1 = MeanAggregator */
   float dropout, lr, beta1, beta2, eps;
   int32_t layers;      /* 1 (emb_module.py:55-73) or 2 (2-hop: conv2(conv1(x)) over the 2-hop sample) */
+  int32_t updater;     /* memory updater: 0 = GRUCell (TGNMemory memory_module.py:71-72; DyRepMemory 'gru'),
+                          1 = RNNCell (DyRepMemory memory_updater_type 'rnn', memory_module.py:256-259):
+                          weight_ih [D, Qm], weight_hh [D, D], bias_ih / bias_hh [D] in the same layout slots */
 } tgnx_tgn_config;
 
 typedef struct {

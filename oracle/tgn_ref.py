@@ -90,14 +90,22 @@ def mean_aggregate(msg, index, t, dim_size):
 
 
 class RefTGNMemory(nn.Module):
-    """modules/memory_module.py:25-215 with IdentityMessage and Last/Mean aggregation."""
+    """modules/memory_module.py:25-215 with IdentityMessage and Last/Mean aggregation; the updater cell
+    `memory_updater` is a GRUCell or RNNCell (memory_updater_cell, :57, :70-78).  DyRepMemory
+    (:218-421) with use_src_emb_in_msg = use_dst_emb_in_msg = False computes exactly this (same update
+    order :316-331 vs :126-138, messages :381-421 vs :193-207, last_update :365 vs :176, cell :259-264)."""
 
-    def __init__(self, num_nodes, raw_msg_dim, memory_dim, time_dim, aggr="last"):
+    def __init__(self, num_nodes, raw_msg_dim, memory_dim, time_dim, aggr="last", updater="gru"):
         super().__init__()
         self.num_nodes, self.raw_msg_dim, self.memory_dim, self.time_dim = num_nodes, raw_msg_dim, memory_dim, time_dim
         self.out_channels = raw_msg_dim + 2 * memory_dim + time_dim
         self.time_enc = RefTimeEncoder(time_dim)
-        self.gru = nn.GRUCell(self.out_channels, memory_dim)
+        if updater == "gru":
+            self.memory_updater = nn.GRUCell(self.out_channels, memory_dim)
+        elif updater == "rnn":
+            self.memory_updater = nn.RNNCell(self.out_channels, memory_dim)   # tanh
+        else:
+            raise ValueError("Memory updater can be either 'gru' or 'rnn'.")
         self.aggr = aggr
         self.register_buffer("memory", torch.zeros(num_nodes, memory_dim))
         self.register_buffer("last_update", torch.zeros(num_nodes, dtype=torch.long))
@@ -146,7 +154,7 @@ class RefTGNMemory(nn.Module):
         t = torch.cat([t_s, t_d], dim=0)
         agg = last_aggregate if self.aggr == "last" else mean_aggregate
         aggr = agg(msg, self._assoc[idx], t, n_id.size(0))
-        memory = self.gru(aggr, self.memory[n_id])
+        memory = self.memory_updater(aggr, self.memory[n_id])
         last_update, _ = scatter_max_first(t, idx, self.num_nodes)
         return memory, last_update[n_id]
 
@@ -245,9 +253,9 @@ class RefLinkPredictor(nn.Module):
 class RefTGN(nn.Module):
     """pyg_model_utils.py:10-36: memory + gnn (sharing memory.time_enc) + link_pred."""
 
-    def __init__(self, num_nodes, msg_dim, hidden=100, aggr="last", dropout=0.1, layers=1):
+    def __init__(self, num_nodes, msg_dim, hidden=100, aggr="last", dropout=0.1, layers=1, updater="gru"):
         super().__init__()
-        self.memory = RefTGNMemory(num_nodes, msg_dim, hidden, hidden, aggr)
+        self.memory = RefTGNMemory(num_nodes, msg_dim, hidden, hidden, aggr, updater)
         self.gnn = RefGraphAttentionEmbedding(hidden, hidden, msg_dim, self.memory.time_enc, dropout, layers)
         self.link_pred = RefLinkPredictor(hidden)
         self.layers = layers

@@ -24,7 +24,7 @@ def _rel(a, b):
     return float((a - b).norm() / (b.norm() + 1e-12))
 
 
-def _setup(aggr, N=300, B=50, d=16, D=32, nb=10, seed=3, max_neg=20, layers=1):
+def _setup(aggr, N=300, B=50, d=16, D=32, nb=10, seed=3, max_neg=20, layers=1, updater="gru", memory="tgn"):
     from oracle.sampler_ref import RefLastNeighborLoader
     from oracle.tgn_ref import RefTGN
     from tgnx.sampler import LastNeighborLoader
@@ -32,11 +32,11 @@ def _setup(aggr, N=300, B=50, d=16, D=32, nb=10, seed=3, max_neg=20, layers=1):
     from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
     s = make_stream("tgbl-wiki", seed=seed, num_events=B * nb, num_nodes=N, msg_dim=d)
     torch.manual_seed(0)
-    ref = RefTGN(N, d, hidden=D, aggr=aggr, dropout=0.0, layers=layers)
+    ref = RefTGN(N, d, hidden=D, aggr=aggr, dropout=0.0, layers=layers, updater=updater)
     opt_ref = torch.optim.Adam(ref.parameters(), lr=1e-3)
     dev = torch.device("cuda")
     model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=max_neg, aggr=aggr, dropout=0.0,
-                     layers=layers)
+                     layers=layers, updater=updater, memory=memory)
     model.load_reference_state(ref.state_dict())
     opt = TgnAdam(model, 1e-3)
     loader = LastNeighborLoader(N, 10, device=dev)
@@ -61,12 +61,17 @@ def _sync(ref, opt_ref, model, opt):
         model.memory.last_update.copy_(ref.memory.last_update)
 
 
-@pytest.mark.parametrize("aggr,layers", [("last", 1), ("mean", 1), ("last", 2), ("mean", 2)])
-def test_tgn_train_steps_and_eval_match_oracle(aggr, layers):
-    """layers = 2: the 2-hop extension (oracle RefTGN(layers=2); no reference parity possible)."""
+@pytest.mark.parametrize("aggr,layers,updater", [("last", 1, "gru"), ("mean", 1, "gru"), ("last", 2, "gru"),
+                                                  ("mean", 2, "gru"), ("last", 1, "rnn"), ("mean", 1, "rnn"),
+                                                  ("last", 2, "rnn")])
+def test_tgn_train_steps_and_eval_match_oracle(aggr, layers, updater):
+    """layers = 2: the 2-hop extension (oracle RefTGN(layers=2); no reference parity possible).
+    updater = 'rnn': the RNNCell memory updater (TGNMemory memory_updater_cell / DyRepMemory
+    memory_updater_type, memory_module.py:70-78, :259-264; the engine built as DyRepMemory)."""
     from oracle.tgn_ref import eval_step, mrr_per_event, train_step
     B = 50
-    s, ref, opt_ref, lref, model, opt, eng = _setup(aggr, layers=layers)
+    s, ref, opt_ref, lref, model, opt, eng = _setup(aggr, layers=layers, updater=updater,
+                                                    memory="dyrep" if updater == "rnn" else "tgn")
     PARAM_ORDER = model.param_order
     ev_t = torch.from_numpy(s.t.astype(np.float32))
     ev_msg = torch.from_numpy(s.msg)

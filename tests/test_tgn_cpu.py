@@ -46,28 +46,31 @@ def test_last_aggregator_ties_and_empty_rows():
                                               [(2 + 6 + 8) / 3, (3 + 7 + 9) / 3], [0, 0]], rtol=1e-6)
 
 
-def _cfg(N=9227, E=157474, D=100, d=172, B=200, kn=1, aggr=0, heads=2, layers=1):
+def _cfg(N=9227, E=157474, D=100, d=172, B=200, kn=1, aggr=0, heads=2, layers=1, updater=0):
     from tgnx.tgn import TgnConfig
     return TgnConfig(num_nodes=N, num_events=E, ring=10, mem_dim=D, msg_dim=d, heads=heads, max_batch=B, max_neg=kn,
-                     aggr=aggr, dropout=0.1, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8, layers=layers)
+                     aggr=aggr, dropout=0.1, lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8, layers=layers,
+                     updater=updater)
 
 
+@pytest.mark.parametrize("updater", ["gru", "rnn"])
 @pytest.mark.parametrize("layers", [1, 2])
 @pytest.mark.parametrize("D,d", [(100, 172), (100, 1), (32, 16), (6, 2)])
-def test_param_layout_matches_reference_shapes(D, d, layers):
+def test_param_layout_matches_reference_shapes(D, d, layers, updater):
     """tgnx_tgn_param_layout: one slot per reference parameter (pyg_model_utils.py:10-36 modules; layers = 2
-    adds the oracle's gnn.conv2), sized as the reference's shapes, 16-B aligned, disjoint; the projection
-    stride invariant (the same stride for conv2)."""
+    adds the oracle's gnn.conv2; the memory updater a GRUCell or an RNNCell, memory_module.py:70-78), sized
+    as the reference's shapes, 16-B aligned, disjoint; the projection stride invariant (the same stride
+    for conv2)."""
     from oracle.tgn_ref import RefTGN
     from tgnx import _lib
     from tgnx.tgn import PARAM_ORDER, PARAM_ORDER2, param_shapes
     order = PARAM_ORDER2 if layers == 2 else PARAM_ORDER
-    cfg = _cfg(D=D, d=d, layers=layers)
+    cfg = _cfg(D=D, d=d, layers=layers, updater=1 if updater == "rnn" else 0)
     off = (ctypes.c_int64 * (len(order) + 1))()
     _lib.call("tgnx_tgn_param_layout", ctypes.byref(cfg), off)
     off = list(off)
-    ref = {k: tuple(v.shape) for k, v in RefTGN(50, d, hidden=D, layers=layers).named_parameters()}
-    shapes = param_shapes(D, d, layers)
+    ref = {k: tuple(v.shape) for k, v in RefTGN(50, d, hidden=D, layers=layers, updater=updater).named_parameters()}
+    shapes = param_shapes(D, d, layers, updater)
     assert set(ref) == set(order) and all(ref[k] == shapes[k] for k in order)
     spans = sorted((off[i], off[i] + int(np.prod(shapes[k]))) for i, k in enumerate(order))
     for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
@@ -112,7 +115,7 @@ def test_workspace_and_store_sizing():
 
 @pytest.mark.parametrize("field,value,msg", [("heads", 8, b"heads"), ("mem_dim", 101, b"mem_dim"),
                                              ("max_batch", 5000, b"max_batch"), ("aggr", 3, b"aggr"),
-                                             ("ring", 0, b"ring")])
+                                             ("ring", 0, b"ring"), ("updater", 2, b"updater")])
 def test_config_rejections(field, value, msg):
     from tgnx import _lib
     L = _lib.lib()
@@ -166,3 +169,21 @@ def test_two_hop_oracle_reduces_to_one_hop():
     a = eval_step(m1, l1, t, msg, src[sl], dst[sl], negs, t[sl], msg[sl])
     c = eval_step(m2, l2, t, msg, src[sl], dst[sl], negs, t[sl], msg[sl])
     torch.testing.assert_close(a[1], c[1], rtol=1e-5, atol=1e-6)
+
+
+def test_dyrep_model_surface():
+    """DyRepMemory (modules/memory_module.py:218-421) behind getModel: memory_updater_type 'gru' | 'rnn' with
+    the reference's state-dict names (memory.memory_updater.*, shared with TGNMemory, :70-78); embeddings in
+    the messages refused; an unknown updater rejected as the reference does (:75-78)."""
+    from oracle.tgn_ref import RefTGN
+    from tgnx.tgn import PARAM_ORDER, param_shapes
+    ref = RefTGN(30, 4, hidden=8, updater="rnn")
+    assert isinstance(ref.memory.memory_updater, torch.nn.RNNCell)
+    shapes = param_shapes(8, 4, 1, "rnn")
+    assert {k: tuple(v.shape) for k, v in ref.named_parameters()} == {k: shapes[k] for k in PARAM_ORDER}
+    assert shapes["memory.memory_updater.weight_ih"] == (8, 3 * 8 + 4)
+    from tgnx.tgn import TGNModel
+    with pytest.raises(NotImplementedError):
+        TGNModel(30, 10, 4, 8, "cpu", memory="dyrep", updater="rnn", use_dst_emb_in_msg=True)
+    with pytest.raises(ValueError):
+        TGNModel(30, 10, 4, 8, "cpu", memory="dyrep", updater="lstm")

@@ -45,16 +45,17 @@ struct Lay {
   // layers = 2: gnn.conv2 (same shapes, same fixed-stride projection block), after lin_final.bias
   int64_t wk2, bk2, wq2, bq2, wv2, bv2, we2, wsk2, bsk2;
 };
-static Lay make_lay(int D, int d, int layers) {
-  const int64_t Qm = 3 * (int64_t)D + d, HC = D;
+// cell: the memory updater, 0 = GRUCell (weights [3D, .]), 1 = RNNCell (DyRepMemory 'rnn', weights [D, .])
+static Lay make_lay(int D, int d, int layers, int cell = 0) {
+  const int64_t Qm = 3 * (int64_t)D + d, HC = D, G3 = cell ? 1 : 3;
   Lay L;
   int64_t o = 0;
   L.te_w = o; o += al4(D);
   L.te_b = o; o += al4(D);
-  L.w_ih = o; o += al4(3 * D * Qm);
-  L.w_hh = o; o += al4(3 * (int64_t)D * D);
-  L.b_ih = o; o += al4(3 * D);
-  L.b_hh = o; o += al4(3 * D);
+  L.w_ih = o; o += al4(G3 * D * Qm);
+  L.w_hh = o; o += al4(G3 * (int64_t)D * D);
+  L.b_ih = o; o += al4(G3 * D);
+  L.b_hh = o; o += al4(G3 * D);
   L.pw = al4(HC * D);
   L.pb = al4(HC);
   auto proj = [&](int64_t& wq, int64_t& wk, int64_t& wv, int64_t& wsk, int64_t& bq, int64_t& bk, int64_t& bv,
@@ -2303,6 +2304,131 @@ struct LoadGruWencT {
     return wih[(int64_t)(min(gg, 2) * D + j) * Qm + off + n] * f01(gg != 3);
   }
 };
+// ---- RNNCell memory updater (DyRepMemory memory_updater_type = 'rnn', modules/memory_module.py:256-259):
+// h' = tanh(W_ih x + b_ih + W_hh h + b_hh), one GEMM column per unit over [message | memory].
+struct LoadRnnW {
+  const float *wih, *whh;
+  int Qm, D;
+  static constexpr bool k_fast = true;
+  __device__ float operator()(int n, int k) const {
+    const float* p = k < Qm ? wih + (int64_t)n * Qm + k : whh + (int64_t)n * D + (k - Qm);
+    return *p;
+  }
+  __device__ bool vec4() const { return ((Qm | D) & 3) == 0 && al16(wih) && al16(whh); }
+  __device__ float4 load4(int n, int k) const {
+    const float* p = k < Qm ? wih + (int64_t)n * Qm + k : whh + (int64_t)n * D + (k - Qm);
+    return *reinterpret_cast<const float4*>(p);
+  }
+};
+struct EpiRnn {
+  const float *bih, *bhh;
+  int D;
+  float* Z0;
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    float b[T::per];
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) {  // gathers first
+      const int j = min(t.n0 + T::col_of(i), D - 1);
+      b[i] = bih[j] + bhh[j];
+    }
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) {
+      const int r = T::row_of(i), cc = T::col_of(i), m = t.m0 + r, j = t.n0 + cc;
+      if (m >= t.M || j >= t.N) continue;
+      Z0[(int64_t)m * D + j] = tanhf(t(r, cc) + b[i]);
+    }
+  }
+};
+// dh' (the dz0 GEMM) -> d(pre-activation) = dh' (1 - h'^2)
+struct EpiRnnBwd {
+  const float* Z0;
+  float* dG;
+  int D;
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    float h[T::per];
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) {
+      const int m = min(t.m0 + T::row_of(i), t.M - 1), j = min(t.n0 + T::col_of(i), D - 1);
+      h[i] = Z0[(int64_t)m * D + j];
+    }
+#pragma unroll
+    for (int i = 0; i < T::per; ++i) {
+      const int r = T::row_of(i), cc = T::col_of(i), m = t.m0 + r, j = t.n0 + cc;
+      if (m >= t.M || j >= t.N) continue;
+      dG[(int64_t)m * D + j] = t(r, cc) * (1.0f - h[i] * h[i]);
+    }
+  }
+};
+// dW = dGᵀ [X | H | 1]: row j -> W_ih[j, :Qm], W_hh[j, :], and b_ih[j], b_hh[j] (both get the column sum)
+struct EpiRnnWGrad {
+  float* g;
+  int64_t wih, whh, bih, bhh;
+  int Qm, D;
+  AdamFuse af;
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    constexpr int NI = (T::tm * T::tn + 255) / 256;
+    int64_t ix[2 * NI];
+    float vx[2 * NI];
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int x = threadIdx.x + 256 * it;
+      const int r = x / T::tn, cc = x % T::tn, j = t.m0 + r, n = t.n0 + cc;
+      const bool ok = x < T::tm * T::tn && j < t.M && n < t.N;
+      int64_t a = -1, b = -1;
+      if (ok) {
+        if (n < Qm) a = wih + (int64_t)j * Qm + n;
+        else if (n < Qm + D) a = whh + (int64_t)j * D + (n - Qm);
+        else {
+          a = bih + j;
+          b = bhh + j;
+        }
+      }
+      ix[2 * it] = a;
+      ix[2 * it + 1] = b;
+      vx[2 * it] = vx[2 * it + 1] = ok ? t(r, cc) : 0.f;
+    }
+    af.put_n(g, ix, vx);
+  }
+};
+// encoding columns of W_ih as the B operand of dX_enc = dG W_ih[:, enc]: element (n, r = unit)
+struct LoadRnnWencT {
+  const float* wih;
+  int Qm, D, off;
+  static constexpr bool k_fast = false;
+  __device__ float operator()(int n, int r) const { return wih[(int64_t)r * Qm + off + n]; }
+};
+// the memory updater's functors by cell type (GEMM columns per unit G: GRU 4 interleaved gates, RNN 1)
+template <int CELL>
+struct CellOps;
+template <>
+struct CellOps<0> {
+  static constexpr int G = 4;
+  static __host__ LoadGruW w(const Ctx& c) { return LoadGruW{c.params + c.L.w_ih, c.params + c.L.w_hh, c.Qm, c.D}; }
+  static __host__ EpiGru epi(const Ctx& c, const int64_t* list, int64_t base) {
+    return EpiGru{c.params + c.L.b_ih, c.params + c.L.b_hh, c.mem, list, base, c.D, c.Z0, c.gates};
+  }
+  static __host__ EpiGruBwd bwd(const Ctx& c) { return EpiGruBwd{c.gates, c.mem, c.nid, c.dG, c.D}; }
+  static __host__ EpiGruWGrad wgrad(const Ctx& c) {
+    return EpiGruWGrad{c.grads, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, c.Qm, c.D, c.adf};
+  }
+  static __host__ LoadGruWencT wenc(const Ctx& c) { return LoadGruWencT{c.params + c.L.w_ih, c.Qm, c.D, 2 * c.D + c.d}; }
+};
+template <>
+struct CellOps<1> {
+  static constexpr int G = 1;
+  static __host__ LoadRnnW w(const Ctx& c) { return LoadRnnW{c.params + c.L.w_ih, c.params + c.L.w_hh, c.Qm, c.D}; }
+  static __host__ EpiRnn epi(const Ctx& c, const int64_t*, int64_t) {
+    return EpiRnn{c.params + c.L.b_ih, c.params + c.L.b_hh, c.D, c.Z0};
+  }
+  static __host__ EpiRnnBwd bwd(const Ctx& c) { return EpiRnnBwd{c.Z0, c.dG, c.D}; }
+  static __host__ EpiRnnWGrad wgrad(const Ctx& c) {
+    return EpiRnnWGrad{c.grads, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, c.Qm, c.D, c.adf};
+  }
+  static __host__ LoadRnnWencT wenc(const Ctx& c) { return LoadRnnWencT{c.params + c.L.w_ih, c.Qm, c.D, 2 * c.D + c.d}; }
+};
 // message-encoding -> Δt-encoding parameter grads (Last: the winner's Δt; Mean: each stored
 // message's Δt with weight 1 / count, folded into s0m / s1m by agg_node), per row-tile partials
 struct EpiTeMsg {
@@ -2626,6 +2752,7 @@ static size_t carve(size_t& off, size_t bytes) {
 }
 struct Caps {
   int B, Kn, Qtr, Qcap, Rtr, Rcap, Mtr, Mcap, Etr, Ecap, Ucap, Qm, D, d, HC;
+  int cell, G;  // memory updater (0 GRU, 1 RNN) and its GEMM columns per unit (4: r, z, n_in, n_hid; 1)
   int layers, R1tr, R1cap, E1tr, E1cap;  // 2 hops: root level (R*/E*/M* above: the outer sample)
   int64_t N;
 };
@@ -2645,6 +2772,8 @@ static Caps make_caps(const tgnx_tgn_config* cfg) {
   k.Qcap = k.B * (2 + k.Kn);
   if (k.Qcap < k.Qtr) k.Qcap = k.Qtr;
   k.layers = cfg_layers(cfg);
+  k.cell = cfg->updater;
+  k.G = k.cell ? 1 : 4;
   k.R1tr = cap(k.Qtr);
   k.R1cap = cap(k.Qcap);
   k.Rtr = k.layers == 2 ? cap((int64_t)k.R1tr * (K + 1)) : k.R1tr;
@@ -2668,7 +2797,7 @@ static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_spli
 static GemmShape shp_dWp2(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.HC, k.D + 1, k.Rtr, nullptr, nullptr, cnt ? cnt + CNT_R : nullptr, ksplit(k.Rtr, 4)); }
 static GemmShape shp_dWe2(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.E1tr, nullptr, nullptr, cnt ? cnt + CNT_E1 : nullptr, ksplit(k.E1tr, 8)); }
 static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, 5); }
-static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
+static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
       Ep, alpha, Zc, evs, evr, evq, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
@@ -2774,6 +2903,7 @@ static int check_cfg(const tgnx_tgn_config* cfg) {
   TGNX_CHECK_ARG(cfg->aggr == 0 || cfg->aggr == 1, "tgn: aggr must be 0 (last) or 1 (mean)");
   TGNX_CHECK_ARG(cfg->dropout >= 0.f && cfg->dropout < 1.f, "tgn: bad dropout");
   TGNX_CHECK_ARG(cfg->layers >= 0 && cfg->layers <= 2, "tgn: layers must be 1 or 2, got %d", cfg->layers);
+  TGNX_CHECK_ARG(cfg->updater == 0 || cfg->updater == 1, "tgn: updater must be 0 (GRUCell) or 1 (RNNCell)");
   return TGNX_OK;
 }
 
@@ -2891,7 +3021,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.Ecap = k.Ecap;
   c.Ucap = k.Ucap;
   c.tgp_rows = W.tgp_rows;
-  c.L = make_lay(c.D, c.d, k.layers);
+  c.L = make_lay(c.D, c.d, k.layers, k.cell);
   c.layers = k.layers;
   c.rsel = CNT_R;
   c.ccap = k.Rcap;
@@ -2964,17 +3094,23 @@ static inline int gridn(int64_t n, int per, int cap = 4096) {
 }
 
 // the GRU of a node list (eval update / flush): messages -> GRUCell (X, Z0 rows 0..n)
-static void gru_list(const Ctx& c, const Caps& k, const int64_t* list, const int* list_cnt, int n_host, int64_t base,
-                     int mcap, hipStream_t s) {
-  const float* P = c.params;
+template <int CELL>
+static void gru_list_c(const Ctx& c, const int64_t* list, const int* list_cnt, int n_host, int64_t base, int mcap,
+                       hipStream_t s) {
+  using Cl = CellOps<CELL>;
   if (c.aggr == 0)
     tgn_agg_emit<0><<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
   else
     tgn_agg_emit<-1><<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
-  const GemmShape g1 = gemm_shape<G32L>(mcap, 4 * c.D, c.Qm + c.D, list_cnt);
-  gemm_launch<G32L>(g1, LoadGruA{c.X, c.mem, list ? list : c.nid, base, c.Qm, c.D, list ? 0 : 1},
-                   LoadGruW{P + c.L.w_ih, P + c.L.w_hh, c.Qm, c.D},
-              EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, list, base, c.D, c.Z0, c.gates}, nullptr, s);
+  const GemmShape g1 = gemm_shape<G32L>(mcap, Cl::G * c.D, c.Qm + c.D, list_cnt);
+  gemm_launch<G32L>(g1, LoadGruA{c.X, c.mem, list ? list : c.nid, base, c.Qm, c.D, list ? 0 : 1}, Cl::w(c),
+                    Cl::epi(c, list, base), nullptr, s);
+}
+// the memory update of a node list (eval update, flush): aggregation + the memory updater
+static void gru_list(const Ctx& c, const Caps& k, const int64_t* list, const int* list_cnt, int n_host, int64_t base,
+                     int mcap, hipStream_t s) {
+  if (k.cell) gru_list_c<1>(c, list, list_cnt, n_host, base, mcap, s);
+  else gru_list_c<0>(c, list, list_cnt, n_host, base, mcap, s);
 }
 
 }  // namespace tgn
@@ -2990,7 +3126,7 @@ int tgnx_tgn_param_layout(const tgnx_tgn_config* cfg, int64_t* off) {
   if (rc) return rc;
   TGNX_CHECK_ARG(off, "tgnx_tgn_param_layout: null output");
   const int layers = cfg_layers(cfg);
-  const Lay L = make_lay(cfg->mem_dim, cfg->msg_dim, layers);
+  const Lay L = make_lay(cfg->mem_dim, cfg->msg_dim, layers, cfg->updater);
   const int64_t v[TGNX_TGN_NPARAM2] = {L.te_w, L.te_b, L.w_ih, L.w_hh, L.b_ih, L.b_hh, L.wk,  L.bk,  L.wq,  L.bq,
                                        L.wv,   L.bv,   L.we,   L.wsk,  L.bsk,  L.lsw,  L.lsb, L.ldw, L.ldb, L.lfw,
                                        L.lfb,  L.wk2,  L.bk2,  L.wq2,  L.bq2,  L.wv2,  L.bv2, L.we2, L.wsk2, L.bsk2};
@@ -3039,8 +3175,11 @@ struct AdvArgs {
 // pipe (resident world-1 fused steps only): 0 = plain step; 1 = pipelined, this batch already marked and
 // scanned by the previous pipelined step; 2 = pipelined, mark + scan this batch first.  A pipelined step
 // marks the next batch inside tgn_pred_train and scans it after its own last launch.
-static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
-                           void* stream, bool fuse_adam, const AdvArgs* adv = nullptr, int pipe = 0) {
+extern "C++" {  // (inside the extern "C" block: the cell-templated step)
+template <int CELL>
+static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
+                             void* stream, bool fuse_adam, const AdvArgs* adv, int pipe) {
+  using Cl = CellOps<CELL>;
   Ctx c;
   Caps k;
   WsLay W;
@@ -3107,9 +3246,9 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   const LoadEdgeAttr ea{c.encE, c.e_id, c.ev_msg, D, d};
   const bool two = k.layers == 2;
   const LoadEdgeAttrMap ea1{c.encE, c.e1_id, c.e1_e2, c.ev_msg, D, d};
-  const auto j_gru = gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, 4 * D, Qm + D, c.cnt + CNT_M), LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0},
-                                    LoadGruW{P + c.L.w_ih, P + c.L.w_hh, Qm, D},
-                                    EpiGru{P + c.L.b_ih, P + c.L.b_hh, c.mem, c.nid, 0, D, c.Z0, c.gates}, (float*)nullptr);
+  const auto j_gru = gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, Cl::G * D, Qm + D, c.cnt + CNT_M),
+                                    LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0}, Cl::w(c), Cl::epi(c, c.nid, 0),
+                                    (float*)nullptr);
   const auto j_edge = gemm_job<G32>(gemm_shape<G32>(k.Etr, HC, D + d, c.cnt + CNT_E), ea,
                                     LoadRowK{P + c.L.we, HC, D + d, D + d}, EpiStore{c.Ep, nullptr, HC, 0}, (float*)nullptr);
   const BlockJob<RingMergeJob> j_ring{RingMergeJob{c}, gridn(2 * k.B, 4)};
@@ -3200,7 +3339,7 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   // weight gradients (deferred split-K) ‖ ...
   const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D, c.adf};
   const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D, c.adf};
-  const EpiGruWGrad e_dWg{G, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, Qm, D, c.adf};
+  const auto e_dWg = Cl::wgrad(c);
   // one launch: dW_proj, dW_src/dst (deferred split-K) ‖ dz0 = dP W with the GRU backward in its
   // epilogue — all read only what attn_bwd / kv_reduce / pred_train produced
   const int rows_edge = (k.Etr + G32::TM - 1) / G32::TM, rows_msg = (k.Mtr + G32::TM - 1) / G32::TM;
@@ -3209,15 +3348,16 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
                gemm_job<GW>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
                              LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, EpiDeferred{}, c.pC),
                gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
-                             LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, EpiGruBwd{c.gates, c.mem, c.nid, c.dG, D},
+                             LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, Cl::bwd(c),
                              (float*)nullptr));
   probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
   gemmN_launch(s, mk_at(9),
-               gemm_job<GW>(shp_dWg(k, c.cnt), LoadKRow{c.dG, 4 * D, k.Mtr, 4 * D}, LoadGruAT1{c.X, c.mem, c.nid, Qm, D},
-                            EpiDeferred{}, c.pD),
-               gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, 4 * D, c.cnt + CNT_M), LoadRowK{c.dG, k.Mtr, 4 * D, 4 * D},
-                              LoadGruWencT{P + c.L.w_ih, Qm, D, 2 * D + d}, EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge},
+               gemm_job<GW>(shp_dWg(k, c.cnt), LoadKRow{c.dG, Cl::G * D, k.Mtr, Cl::G * D},
+                            LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{}, c.pD),
+               gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, Cl::G * D, c.cnt + CNT_M),
+                              LoadRowK{c.dG, k.Mtr, Cl::G * D, Cl::G * D}, Cl::wenc(c),
+                              EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge},
                               (float*)nullptr));
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
   // split-K sums + epilogues ‖ Δt reduction ‖ update_state (train order: memory of src ∪ dst from
@@ -3246,6 +3386,14 @@ static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
     TGNX_LAUNCH_CHECK("tgn_scan_next");
   }
   return TGNX_OK;
+}
+
+}  // extern "C++"
+
+static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
+                           void* stream, bool fuse_adam, const AdvArgs* adv = nullptr, int pipe = 0) {
+  if (cfg && cfg->updater == 1) return train_step_impl_c<1>(cfg, buf, gen_neg, dropout, stream, fuse_adam, adv, pipe);
+  return train_step_impl_c<0>(cfg, buf, gen_neg, dropout, stream, fuse_adam, adv, pipe);
 }
 
 int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,

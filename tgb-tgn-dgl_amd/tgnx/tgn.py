@@ -3,7 +3,7 @@
 `getModel` / `getOptimizer` mirror pyg_model_utils.py:10-43: the returned dict has 'memory' (TGNMemory:
 time_enc + GRUCell, memory / last_update buffers, message stores), 'gnn' (GraphAttentionEmbedding:
 TransformerConv, sharing memory.time_enc) and 'link_pred' (LinkPredictor); state_dict keys are the
-reference's (`memory.gru.weight_ih`, `gnn.conv.lin_key.weight`, `link_pred.lin_final.bias`, ...).  Every
+reference's (`memory.memory_updater.weight_ih`, `gnn.conv.lin_key.weight`, `link_pred.lin_final.bias`, ...).  Every
 trainable tensor is a view into one flat fp32 device buffer (`tgnx_tgn_param_layout`); the step runs in
 libtgnx (TgnEngine below), there is no torch-op path.
 
@@ -26,7 +26,8 @@ P = ctypes.c_void_p
 
 PARAM_ORDER = [  # flat-buffer order = tgnx_tgn_param_layout
     "memory.time_enc.lin.weight", "memory.time_enc.lin.bias",
-    "memory.gru.weight_ih", "memory.gru.weight_hh", "memory.gru.bias_ih", "memory.gru.bias_hh",
+    "memory.memory_updater.weight_ih", "memory.memory_updater.weight_hh", "memory.memory_updater.bias_ih",
+    "memory.memory_updater.bias_hh",
     "gnn.conv.lin_key.weight", "gnn.conv.lin_key.bias", "gnn.conv.lin_query.weight", "gnn.conv.lin_query.bias",
     "gnn.conv.lin_value.weight", "gnn.conv.lin_value.bias", "gnn.conv.lin_edge.weight",
     "gnn.conv.lin_skip.weight", "gnn.conv.lin_skip.bias",
@@ -46,7 +47,8 @@ class TgnConfig(ctypes.Structure):
                 ("mem_dim", ctypes.c_int32), ("msg_dim", ctypes.c_int32), ("heads", ctypes.c_int32),
                 ("max_batch", ctypes.c_int32), ("max_neg", ctypes.c_int32), ("aggr", ctypes.c_int32),
                 ("dropout", ctypes.c_float), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
-                ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("layers", ctypes.c_int32)]
+                ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("layers", ctypes.c_int32),
+                ("updater", ctypes.c_int32)]
 
 
 class TgnBuffers(ctypes.Structure):
@@ -57,11 +59,18 @@ class TgnBuffers(ctypes.Structure):
                 ("xcap", ctypes.c_int64)]
 
 
-def param_shapes(D: int, d: int, layers: int = 1) -> dict:
+# the memory modules' updater cell: TGNMemory.memory_updater (memory_module.py:70-78, memory_updater_cell
+# 'gru' | 'rnn') and DyRepMemory.memory_updater (:259-264, memory_updater_type) — the same state-dict names
+MEMORY_TYPES = ("tgn", "dyrep")
+
+
+def param_shapes(D: int, d: int, layers: int = 1, updater: str = "gru") -> dict:
     Q = 3 * D + d
+    G3 = 1 if updater == "rnn" else 3     # RNNCell: [D, .]; GRUCell: [3D, .] (r, z, n)
+    u = "memory.memory_updater"
     s = {"memory.time_enc.lin.weight": (D, 1), "memory.time_enc.lin.bias": (D,),
-         "memory.gru.weight_ih": (3 * D, Q), "memory.gru.weight_hh": (3 * D, D),
-         "memory.gru.bias_ih": (3 * D,), "memory.gru.bias_hh": (3 * D,),
+         f"{u}.weight_ih": (G3 * D, Q), f"{u}.weight_hh": (G3 * D, D),
+         f"{u}.bias_ih": (G3 * D,), f"{u}.bias_hh": (G3 * D,),
          "gnn.conv.lin_edge.weight": (D, D + d),
          "link_pred.lin_src.weight": (D, D), "link_pred.lin_src.bias": (D,),
          "link_pred.lin_dst.weight": (D, D), "link_pred.lin_dst.bias": (D,),
@@ -75,18 +84,18 @@ def param_shapes(D: int, d: int, layers: int = 1) -> dict:
     return s
 
 
-def reference_init(D: int, d: int, generator=None, layers: int = 1) -> dict:
+def reference_init(D: int, d: int, generator=None, layers: int = 1, updater: str = "gru") -> dict:
     g = generator
 
     def unif(shape, bound):
         return (torch.rand(shape, generator=g) * 2 - 1) * bound
 
     out = {}
-    for name, shape in param_shapes(D, d, layers).items():
+    for name, shape in param_shapes(D, d, layers, updater).items():
         if name.startswith("memory.time_enc"):
             bound = 1.0                                   # Linear(1, D): fan_in = 1
-        elif name.startswith("memory.gru"):
-            bound = 1.0 / math.sqrt(D)                    # GRUCell.reset_parameters
+        elif name.startswith("memory.memory_updater"):
+            bound = 1.0 / math.sqrt(D)                    # GRUCell / RNNCell.reset_parameters
         elif name.endswith("lin_edge.weight"):
             bound = 1.0 / math.sqrt(D + d)
         else:
@@ -100,18 +109,35 @@ class _Holder(nn.Module):
 
 
 class TGNModel(nn.Module):
-    """memory + gnn + link_pred of pyg_model_utils.py:10-36 over one flat parameter buffer."""
+    """memory + gnn + link_pred of pyg_model_utils.py:10-36 over one flat parameter buffer.
+
+    memory = "tgn": TGNMemory (modules/memory_module.py:25-215) with memory_updater_cell = updater,
+    "gru" (GRUCell, the default) or "rnn" (RNNCell, :70-78);
+    memory = "dyrep": DyRepMemory (modules/memory_module.py:218-421) with memory_updater_type = updater
+    and use_src_emb_in_msg = use_dst_emb_in_msg = False: its update order, messages and state-dict names
+    are then TGNMemory's.  Embeddings in the messages need the embedding module's output at update time
+    from a DyRep training loop the reference does not contain; they are refused (NotImplementedError)."""
 
     def __init__(self, num_nodes, num_events, msg_dim, hidden_dim, device, ring=10, max_batch=2048, max_neg=1,
-                 aggr="last", dropout=0.1, generator=None, layers=1):
+                 aggr="last", dropout=0.1, generator=None, layers=1, memory="tgn", updater="gru",
+                 use_src_emb_in_msg=False, use_dst_emb_in_msg=False):
         super().__init__()
+        if memory not in MEMORY_TYPES:
+            raise ValueError(f"memory must be 'tgn' or 'dyrep', got {memory!r}")
+        if updater not in ("gru", "rnn"):
+            raise ValueError(f"Memory updater can be either 'gru' or 'rnn' (memory_module.py:75-78), got {updater!r}")
+        if use_src_emb_in_msg or use_dst_emb_in_msg:
+            raise NotImplementedError("DyRepMemory use_src/dst_emb_in_msg: the embeddings at update time come from a "
+                                      "DyRep training loop the reference does not contain (DESIGN.md §8)")
+        self.memory_type, self.updater = memory, updater
         dev = _lib.require_device(device)
         D, d = int(hidden_dim), int(msg_dim)
         num_events = max(int(num_events or 0), 1)
         self.num_nodes, self.num_events, self.D, self.d = int(num_nodes), num_events, D, d
         self.cfg = TgnConfig(num_nodes=num_nodes, num_events=num_events, ring=ring, mem_dim=D, msg_dim=d, heads=2,
                              max_batch=max_batch, max_neg=max_neg, aggr=0 if aggr == "last" else 1, dropout=dropout,
-                             lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8, layers=int(layers))
+                             lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8, layers=int(layers),
+                             updater=1 if updater == "rnn" else 0)
         if layers not in (1, 2):
             raise ValueError(f"layers must be 1 or 2, got {layers}")
         self.layers = int(layers)
@@ -123,12 +149,12 @@ class TGNModel(nn.Module):
         total = self.offsets[-1]
         self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
         self.grad_flat = torch.zeros(total + 1, dtype=torch.float32, device=dev)    # + batch-loss slot
-        shapes = param_shapes(D, d, layers)
-        init = reference_init(D, d, generator, layers)
+        shapes = param_shapes(D, d, layers, updater)
+        init = reference_init(D, d, generator, layers, updater)
         self.memory = _Holder()
         self.memory.time_enc = _Holder()
         self.memory.time_enc.lin = _Holder()
-        self.memory.gru = _Holder()
+        self.memory.memory_updater = _Holder()
         self.gnn = _Holder()
         self.gnn.conv = _Holder()
         if layers == 2:
@@ -507,7 +533,8 @@ class TgnEngine:
 def getModel(feature_dim, hidden_dim, num_nodes, device, num_events=None, **kw):
     """pyg_model_utils.py:10-36.  num_events (optional) pre-sizes the message-store arena; otherwise the
     engine sizes it when it binds the event table.  Extra keywords: ring, max_batch, max_neg, aggr,
-    dropout (TGNModel)."""
+    dropout, layers, updater = 'gru' | 'rnn' (TGNMemory memory_updater_cell), memory = 'tgn' | 'dyrep'
+    (DyRepMemory as the memory module, modules/memory_module.py:218-421; TGNModel)."""
     m = TGNModel(num_nodes, num_events, feature_dim, hidden_dim, device, **kw)
     return {"memory": m.memory, "gnn": m.gnn, "link_pred": m.link_pred, "model": m}
 
