@@ -97,6 +97,49 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, WAVE));
   return v;
 }
+// Full-wave reductions on DPP / permlane swaps: no LDS round trip (__shfl_xor lowers to ds_bpermute).
+// Every lane of the wave must be active; every lane gets the same (bitwise) result.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float swap16_sum(float v) {  // v + v[lane ^ 16]
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(p[0]) + __int_as_float(p[1]);
+}
+__device__ __forceinline__ float swap32_sum(float v) {  // v + v[lane ^ 32]
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(p[0]) + __int_as_float(p[1]);
+}
+#ifdef TGNX_NO_DPP  // A/B: the ds_bpermute forms
+__device__ __forceinline__ float wave_sum_f(float v) { return wave_sum(v); }
+__device__ __forceinline__ float wave_max_f(float v) { return wave_max(v); }
+__device__ __forceinline__ float lane_f(float v, int l) { return __shfl(v, l, WAVE); }
+__device__ __forceinline__ int lane_i(int v, int l) { return __shfl(v, l, WAVE); }
+#else
+__device__ __forceinline__ float wave_sum_f(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+  v += dpp_f<0x141>(v);  // row_half_mirror: the other quad of the 8-lane half-row (quads are uniform)
+  v += dpp_f<0x140>(v);  // row_mirror: the other half of the 16-lane row
+  return swap32_sum(swap16_sum(v));
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  v = fmaxf(__int_as_float(p[0]), __int_as_float(p[1]));
+  p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return fmaxf(__int_as_float(p[0]), __int_as_float(p[1]));
+}
+// lane l (wave-uniform) of v, through a scalar register
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ int lane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+#endif
 __device__ __forceinline__ int wave_incl_scan(int v) {
   const int l = lane_id();
 #pragma unroll

@@ -32,6 +32,9 @@ namespace tgn {
 constexpr int TH = 2;        // TransformerConv heads (emb_module.py:66)
 constexpr int TDMAX = 128;   // memory / time / embedding dim capacity (C = D / 2 <= 64 lanes)
 constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touch keys)
+#ifndef TGNX_PRED_ATT_REC
+#define TGNX_PRED_ATT_REC 1  // per-root neighbour-row records for the attention in tgn_pred_train<ATT>
+#endif
 enum { CNT_R = 0, CNT_M = 1, CNT_E = 2, CNT_U = 3, CNT_RUNS = 4, CNT_SRUNS = 5, CNT_LIST = 6, CNT_WORDS = 16 };
 
 __host__ __device__ inline int64_t al4(int64_t x) { return (x + 3) & ~int64_t(3); }
@@ -175,6 +178,10 @@ struct Ctx {
   float *X, *trel, *lu;
   int* evr;  // [3 B] centre row of each root (src, dst, neg) of this rank's events (tgn_agg_emit)
   int4* evq;  // [3 B] 1 hop: per root {centre row, P row, edge range} (tgn_pred_train<ATT>); nullptr at 2 hops
+  int* evj;   // [3 B][16] 1 hop, ring K <= 16: per root the P rows of its edges' neighbours (e_j of its range)
+  int4* cevq;  // [Rcap] with evj: per centre {P row, edge range} (tgn_attn_bwd's first round)
+  int* cevj;   // [Rcap][16] with evj: per centre its edges' neighbour rows (every root of the centre writes
+               // the same values)
   int64_t* xw;
   float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
   float *dZc, *dP, *dE, *dG, *tgp;
@@ -1041,6 +1048,34 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
                                  // tgn_pred_train starts from one index load (root_row: assoc -> rank)
     const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
     const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+    if (c.evj) {  // 16 lanes per root: its record and its edges' neighbour rows (ring slot order, valid
+                  // slots compacted: the e_j of its edge range), so the attention in tgn_pred_train<ATT>
+                  // reads q, skip and every k / v / edge row in its second round
+      const int sl = threadIdx.x & 15, K = c.K;
+      for (int x = (blockIdx.x * blockDim.x + threadIdx.x) >> 4; x < 3 * (hi - lo); x += (nevb * blockDim.x) >> 4) {
+        const int i = lo + x / 3, r = x % 3;
+        const int64_t* src = r == 0 ? c.ev_src : r == 1 ? c.ev_dst : c.neg;
+        const int64_t v = src[start + i];
+        const int a = (int)c.assoc[v];
+        const int64_t e = c.eid[v * K + min(sl, K - 1)], u = c.nbr[v * K + min(sl, K - 1)];
+        const bool ok = sl < K && e >= 0;
+        const uint32_t m = (uint32_t)(__ballot(ok) >> (threadIdx.x & 48)) & 0xFFFFu;
+        const int xr = c.crank[a];
+        const int ju = (int)c.assoc[ok ? u : v];
+        if (ok) {
+          const int idx = __popc(m & ((1u << sl) - 1u));
+          c.evj[x * 16 + idx] = ju;
+          c.cevj[xr * 16 + idx] = ju;
+        }
+        if (sl == 0) {
+          const int e0 = c.ceoff[xr], e1 = c.ceoff[xr + 1];
+          c.evr[x] = xr;
+          c.evq[x] = make_int4(xr, a, e0, e1);
+          c.cevq[xr] = make_int4(a, e0, e1, 0);
+        }
+      }
+      return;
+    }
     for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < 3 * (hi - lo); x += nevb * blockDim.x) {
       const int i = lo + x / 3, r = x % 3;
       const int64_t* src = r == 0 ? c.ev_src : r == 1 ? c.ev_dst : c.neg;
@@ -1365,23 +1400,24 @@ constexpr int ATT_EB = 16;  // edges whose neighbour rows are loaded in one batc
 // output pair (channel lane of both heads, lane < C).  A centre with 1..ATT_EB edges issues the k, v and
 // edge rows of every edge and its skip row as one round (each edge row loaded once for k + e and v + e);
 // longer rings walk ATT_EB-edge load batches.  Train: the softmax weights go to alpha (tgn_attn_bwd).
+// jrec >= 0 (a per-root record, lanes 0..ne-1): lane e's neighbour row of edge e, instead of e_j
 template <bool TRAIN>
-__device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0, int ne, int lane) {
+__device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0, int ne, int lane, int jrec = -1) {
   const int C = c.C, HC = c.HC;
   const float on = f01(lane < C);
   const int l0 = min(lane, C - 1);
   const float* Pi = c.P + (int64_t)i * 4 * HC;
   const float q0 = Pi[l0], q1 = Pi[C + l0];
   const float sqc = sqrtf((float)C);
-  const int jl = c.e_j[e0 + min(lane, max(ne - 1, 0))];   // lane e: the neighbour row of edge e
+  const int jl = jrec >= 0 ? jrec : c.e_j[e0 + min(lane, max(ne - 1, 0))];   // lane e: the neighbour row of edge e
   const float sk0 = Pi[3 * HC + l0], sk1 = Pi[3 * HC + C + l0];
   float my0 = -INFINITY, my1 = -INFINITY;
   float o0 = 0.f, o1 = 0.f;
   float t0, t1;
   auto softmax = [&]() {
-    const float mx0 = wave_max(my0), mx1 = wave_max(my1);
+    const float mx0 = wave_max_f(my0), mx1 = wave_max_f(my1);
     const float ex0 = lane < ne ? expf(my0 - mx0) : 0.f, ex1 = lane < ne ? expf(my1 - mx1) : 0.f;
-    const float a0 = ex0 / (wave_sum(ex0) + 1e-16f), a1 = ex1 / (wave_sum(ex1) + 1e-16f);
+    const float a0 = ex0 / (wave_sum_f(ex0) + 1e-16f), a1 = ex1 / (wave_sum_f(ex1) + 1e-16f);
     t0 = a0;
     t1 = a1;
     if (TRAIN && lane < ne) {
@@ -1399,7 +1435,7 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       const int e = min(u, ne - 1);
-      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
       const float ea = Ee[l0], eb = Ee[C + l0];
       k0[u] = Pj[HC + l0] + ea;
@@ -1410,15 +1446,15 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       if (u >= ne) break;
-      const float p0 = wave_sum(q0 * k0[u] * on) / sqc, p1 = wave_sum(q1 * k1[u] * on) / sqc;
+      const float p0 = wave_sum_f(q0 * k0[u] * on) / sqc, p1 = wave_sum_f(q1 * k1[u] * on) / sqc;
       if (lane == u) { my0 = p0; my1 = p1; }
     }
     softmax();
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       if (u >= ne) break;
-      o0 += v0[u] * __shfl(t0, u, 64);
-      o1 += v1[u] * __shfl(t1, u, 64);
+      o0 += v0[u] * lane_f(t0, u);
+      o1 += v1[u] * lane_f(t1, u);
     }
     return make_float2(o0 + sk0, o1 + sk1);
   }
@@ -1427,7 +1463,7 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {  // all loads of the batch in flight
       const int e = min(b + u, ne - 1);
-      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
       k0[u] = Pj[HC + l0] + Ee[l0];
       k1[u] = Pj[HC + C + l0] + Ee[C + l0];
@@ -1435,7 +1471,7 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       if (b + u >= ne) break;
-      const float p0 = wave_sum(q0 * k0[u] * on) / sqc, p1 = wave_sum(q1 * k1[u] * on) / sqc;
+      const float p0 = wave_sum_f(q0 * k0[u] * on) / sqc, p1 = wave_sum_f(q1 * k1[u] * on) / sqc;
       if (lane == b + u) { my0 = p0; my1 = p1; }
     }
   }
@@ -1445,7 +1481,7 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       const int e = min(b + u, ne - 1);
-      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
       v0[u] = Pj[2 * HC + l0] + Ee[l0];
       v1[u] = Pj[2 * HC + C + l0] + Ee[C + l0];
@@ -1453,8 +1489,8 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       if (b + u >= ne) break;
-      o0 += v0[u] * __shfl(t0, b + u, 64);
-      o1 += v1[u] * __shfl(t1, b + u, 64);
+      o0 += v0[u] * lane_f(t0, b + u);
+      o1 += v1[u] * lane_f(t1, b + u);
     }
   }
   return make_float2(o0 + sk0, o1 + sk1);
@@ -1534,8 +1570,9 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
   if (ATT && wv >= 1) {
     const int r = wv - 1;
     const int4 q = c.evq[3 * blockIdx.x + r];  // {centre row, P row, edge range}; grid = max_batch: in bounds
+    const int jr = c.evj ? c.evj[(3 * blockIdx.x + r) * 16 + (lane & 15)] : -1;  // the edges' neighbour rows
     if (!live) return;
-    const float2 o = attn_centre<true>(c, q.x, q.y, q.z, q.w - q.z, lane);
+    const float2 o = attn_centre<true>(c, q.x, q.y, q.z, q.w - q.z, lane, c.evj && q.w - q.z <= 16 ? max(jr, 0) : -1);
     if (lane < c.C) {
       z[r][lane] = o.x;
       z[r][c.C + lane] = o.y;
@@ -1782,13 +1819,24 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
   }
   const int lane = threadIdx.x & 63;
   const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
-  // first round: batch descriptor, centre count, the centre's row / edge range (clamped, as tgn_attn_fwd)
+  // first round: batch descriptor, centre count, the centre's row / edge range (clamped, as tgn_attn_fwd);
+  // 1 hop with records (tgn_agg_emit): its edges' neighbour rows too, so every row load is in round two
   const int xc = min(x, max(c.ccap - 1, 0));
   const int B = (int)c.ctl[TGNX_CTL_B];
   const int64_t err = c.ctl[TGNX_CTL_ERR];
   const int R = c.cnt[c.rsel];
-  const int i = c.cent_loc[xc];
-  const int e0 = c.ceoff[xc], e1 = c.ceoff[xc + 1];
+  int i, e0, e1, jrec = 0;
+  if (c.cevj) {
+    const int4 q = c.cevq[xc];
+    jrec = c.cevj[xc * 16 + (lane & 15)];
+    i = q.x;
+    e0 = q.y;
+    e1 = q.z;
+  } else {
+    i = c.cent_loc[xc];
+    e0 = c.ceoff[xc];
+    e1 = c.ceoff[xc + 1];
+  }
   if (B == 0 || err != 0 || x >= R) return;
   const int C = c.C, HC = c.HC;
   const bool okl = lane < C;
@@ -1801,7 +1849,7 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
   const float sqc = sqrtf((float)C);
   const int ne = e1 - e0;
   const int le = e0 + min(lane, max(ne - 1, 0));
-  const int jl = c.e_j[le];
+  const int jl = c.cevj && ne <= 16 ? max(jrec, 0) : c.e_j[le];
   const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
   const float al0 = c.alpha[(int64_t)le * 2], al1 = c.alpha[(int64_t)le * 2 + 1];
   const float a0 = lane < ne ? al0 : 0.f, a1 = lane < ne ? al1 : 0.f;
@@ -1815,7 +1863,7 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       const int e = min(u, ne - 1);
-      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
       const float ea = Ee[l0], eb = Ee[C + l0];
       kk0[u] = Pj[HC + l0] + ea;
@@ -1827,18 +1875,18 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       if (u >= ne) break;
-      const float p0 = wave_sum(g0 * v0[u]), p1 = wave_sum(g1 * v1[u]);
+      const float p0 = wave_sum_f(g0 * v0[u]), p1 = wave_sum_f(g1 * v1[u]);
       if (lane == u) { da0 = p0 * k0v; da1 = p1 * k1v; }
     }
-    const float s0 = wave_sum(a0 * da0), s1 = wave_sum(a1 * da1);
+    const float s0 = wave_sum_f(a0 * da0), s1 = wave_sum_f(a1 * da1);
     const float ds0 = a0 * (da0 - s0), ds1 = a1 * (da1 - s1);
     const float t0 = a0 * k0v, t1 = a1 * k1v;
     float dq0 = 0.f, dq1 = 0.f;
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       if (u >= ne) break;
-      const float d0 = __shfl(ds0, u, 64) / sqc, d1 = __shfl(ds1, u, 64) / sqc;
-      const float b0 = __shfl(t0, u, 64), b1 = __shfl(t1, u, 64);
+      const float d0 = lane_f(ds0, u) / sqc, d1 = lane_f(ds1, u) / sqc;
+      const float b0 = lane_f(t0, u), b1 = lane_f(t1, u);
       float* dEe = c.dE + (int64_t)(e0 + u) * HC;
       float* dKe = c.dKV + (int64_t)(e0 + u) * 2 * HC;  // [dk (HC) | dv (HC)]
       dq0 += d0 * kk0[u];
@@ -1869,7 +1917,7 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       const int e = min(b + u, ne - 1);
-      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
       v0[u] = Pj[2 * HC + l0] + Ee[l0];
       v1[u] = Pj[2 * HC + C + l0] + Ee[C + l0];
@@ -1877,12 +1925,12 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       if (b + u >= ne) break;
-      const float p0 = wave_sum(g0 * v0[u]), p1 = wave_sum(g1 * v1[u]);
+      const float p0 = wave_sum_f(g0 * v0[u]), p1 = wave_sum_f(g1 * v1[u]);
       if (lane == b + u) { da0 = p0 * k0v; da1 = p1 * k1v; }
     }
   }
   // softmax backward: d score = alpha (d alpha - Σ alpha d alpha)
-  const float s0 = wave_sum(a0 * da0), s1 = wave_sum(a1 * da1);
+  const float s0 = wave_sum_f(a0 * da0), s1 = wave_sum_f(a1 * da1);
   const float ds0 = a0 * (da0 - s0), ds1 = a1 * (da1 - s1);
   const float t0 = a0 * k0v, t1 = a1 * k1v;
   float dq0 = 0.f, dq1 = 0.f;
@@ -1891,7 +1939,7 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
 #pragma unroll
     for (int u = 0; u < ATT_EB; ++u) {
       const int e = min(b + u, ne - 1);
-      const float* Pj = c.P + (int64_t)__shfl(jl, e, 64) * 4 * HC;
+      const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
       kk0[u] = Pj[HC + l0] + Ee[l0];
       kk1[u] = Pj[HC + C + l0] + Ee[C + l0];
@@ -1900,8 +1948,8 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
     for (int u = 0; u < ATT_EB; ++u) {
       const int e = b + u;
       if (e >= ne) break;
-      const float d0 = __shfl(ds0, e, 64) / sqc, d1 = __shfl(ds1, e, 64) / sqc;
-      const float b0 = __shfl(t0, e, 64), b1 = __shfl(t1, e, 64);
+      const float d0 = lane_f(ds0, e) / sqc, d1 = lane_f(ds1, e) / sqc;
+      const float b0 = lane_f(t0, e), b1 = lane_f(t1, e);
       float* dEe = c.dE + (int64_t)(e0 + e) * HC;
       float* dKe = c.dKV + (int64_t)(e0 + e) * 2 * HC;  // [dk (HC) | dv (HC)]
       dq0 += d0 * kk0[u];
@@ -2800,7 +2848,7 @@ static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_spl
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
-      Ep, alpha, Zc, evs, evr, evq, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
+      Ep, alpha, Zc, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
       rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF, total;
   int tgp_rows, tgp_e1;
 };
@@ -2842,6 +2890,9 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.evs = carve(off, (size_t)k.B * evs_stride(D) * 4);
   W.evr = carve(off, (size_t)k.B * 3 * 4);
   W.evq = carve(off, (size_t)k.B * 3 * 16);
+  W.evj = carve(off, (size_t)k.B * 3 * 16 * 4);
+  W.cevq = carve(off, (size_t)k.Rcap * 16);
+  W.cevj = carve(off, (size_t)k.Rcap * 16 * 4);
   W.Hs = carve(off, (size_t)k.Rcap * D * 4);
   W.Hd = carve(off, (size_t)k.Rcap * D * 4);
   W.dZc = carve(off, (size_t)k.Rtr * HC * 4);
@@ -2994,6 +3045,9 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.evs = reinterpret_cast<float*>(ws + W.evs);
   c.evr = reinterpret_cast<int*>(ws + W.evr);
   c.evq = k.layers == 2 ? nullptr : reinterpret_cast<int4*>(ws + W.evq);
+  c.evj = k.layers == 2 || cfg->ring > 16 || !TGNX_PRED_ATT_REC ? nullptr : reinterpret_cast<int*>(ws + W.evj);
+  c.cevq = c.evj ? reinterpret_cast<int4*>(ws + W.cevq) : nullptr;
+  c.cevj = c.evj ? reinterpret_cast<int*>(ws + W.cevj) : nullptr;
   c.Hs = reinterpret_cast<float*>(ws + W.Hs);
   c.Hd = reinterpret_cast<float*>(ws + W.Hd);
   c.dZc = reinterpret_cast<float*>(ws + W.dZc);
@@ -3233,7 +3287,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   }
   const int nedge = gridn((int64_t)k.Rtr * c.K, 4, TGNX_AGG_EDGE_CAP);
   probe_begin(TGNX_K_EDGE_META, s);
-  const int nevb = gridn(3 * k.B, 256);
+  const int nevb = gridn(3 * k.B * (c.evj ? 16 : 1), 256);
   const int nagg = nevb + nedge + gridn(k.Mtr, 4, TGNX_AGG_NODE_CAP);
   if (c.aggr == 0 && TGNX_AGG_SPECIALIZE)
     tgn_agg_emit<0><<<nagg, 256, 0, s>>>(c, 0, nedge, nullptr, nullptr, 0, 0, nevb);
