@@ -116,6 +116,13 @@ __device__ __forceinline__ float wave_sum_f(float v) { return wave_sum(v); }
 __device__ __forceinline__ float wave_max_f(float v) { return wave_max(v); }
 __device__ __forceinline__ float lane_f(float v, int l) { return __shfl(v, l, WAVE); }
 __device__ __forceinline__ int lane_i(int v, int l) { return __shfl(v, l, WAVE); }
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, WAVE));
+  return v;
+}
+__device__ __forceinline__ float xor32_f(float v) { return __shfl_xor(v, 32, WAVE); }
+__device__ __forceinline__ float xor16_f(float v) { return __shfl_xor(v, 16, WAVE); }
 #else
 __device__ __forceinline__ float wave_sum_f(float v) {
   v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
@@ -133,6 +140,25 @@ __device__ __forceinline__ float wave_max_f(float v) {
   v = fmaxf(__int_as_float(p[0]), __int_as_float(p[1]));
   p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
   return fmaxf(__int_as_float(p[0]), __int_as_float(p[1]));
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));
+  v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));
+  auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = min((int)p[0], (int)p[1]);
+  p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return min((int)p[0], (int)p[1]);
+}
+// v of lane ^ 32 / lane ^ 16 (exchanges through the permlane swaps; full wave)
+__device__ __forceinline__ float xor32_f(float v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float((threadIdx.x & 32) ? p[0] : p[1]);
+}
+__device__ __forceinline__ float xor16_f(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float((threadIdx.x & 16) ? p[0] : p[1]);
 }
 // lane l (wave-uniform) of v, through a scalar register
 __device__ __forceinline__ float lane_f(float v, int l) {

@@ -88,8 +88,9 @@ __device__ __forceinline__ void ring_merge_run(int64_t* __restrict__ nbr, int64_
   }
   int re = 0, rtk = 0;
   for (int j = 0; j < K + m; ++j) {
-    const int64_t oe = __shfl(ce, j);
-    const float ot = __shfl(ct, j);
+    const int64_t oe = (int64_t)(((uint64_t)(uint32_t)lane_i((int)(ce >> 32), j) << 32) |
+                                 (uint64_t)(uint32_t)lane_i((int)ce, j));   // j uniform: readlane
+    const float ot = lane_f(ct, j);
     re += (oe > ce) || (oe == ce && j < lane);
     rtk += (ot > ct) || (ot == ct && j < lane);
   }

@@ -718,9 +718,8 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
 // Loads are batched: each 64-event chunk of the store is fetched lane-parallel (event id, other
 // endpoint, t) and broadcast by shuffles; the X row is filled 8 columns per lane at a time from
 // selected addresses (unconditional loads, encoding columns blended arithmetically).
-__device__ __forceinline__ int64_t shfl_i64(int64_t v, int src) {
-  return (int64_t)(((uint64_t)(uint32_t)__shfl((int)(v >> 32), src, 64) << 32) |
-                   (uint64_t)(uint32_t)__shfl((int)v, src, 64));
+__device__ __forceinline__ int64_t shfl_i64(int64_t v, int src) {  // src wave-uniform (readlane)
+  return (int64_t)(((uint64_t)(uint32_t)lane_i((int)(v >> 32), src) << 32) | (uint64_t)(uint32_t)lane_i((int)v, src));
 }
 // stored event k of node n (k < sc: as source, else as destination): id, other endpoint, t
 struct StoreView {
@@ -780,10 +779,8 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
         ob = o;
       }
     }
-    const float tm = wave_max(tb);
-    int kk = tb == tm ? kb : 0x7fffffff;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) kk = min(kk, __shfl_xor(kk, o, 64));
+    const float tm = wave_max_f(tb);
+    const int kk = wave_min_i(tb == tm ? kb : 0x7fffffff);
     const int wl = __ffsll(__ballot(kb == kk)) - 1;
     const int64_t e = shfl_i64(eb, wl), other = shfl_i64(ob, wl);
     const float tr = tm - lun;
@@ -848,7 +845,7 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
           for (int u = 0; u < AGG_MB; ++u) {
             const int q = min(qb + u, nq - 1);
             const int64_t e = shfl_i64(e_l, q), o = shfl_i64(o_l, q);
-            dt[u] = __shfl(t_l, q, 64) - lun;
+            dt[u] = lane_f(t_l, q) - lun;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
               const int k = min(k0 + lane + 64 * i, Qm - 1);
@@ -884,7 +881,7 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
         }
       }
     }
-    tmax = wave_max(tmax);
+    tmax = wave_max_f(tmax);
     if (lane == 0) {
       c.xw[m] = 1;
       c.trel[m] = 0.f;
@@ -946,7 +943,7 @@ __device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m, bool grad) {
         for (int u = 0; u < AGG_MB; ++u) {
           const int q = min(qb + u, nq - 1);
           const int64_t e = shfl_i64(e_l, q), o = shfl_i64(o_l, q);
-          dt[u] = __shfl(t_l, q, 64) - lun;
+          dt[u] = lane_f(t_l, q) - lun;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const int k = min(k0 + lane + 64 * i, Qm - 1);
@@ -978,7 +975,7 @@ __device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m, bool grad) {
       red[w][2][i][lane] = s1[i];
     }
     if (k0 == 0) {
-      const float wm = wave_max(tmax);
+      const float wm = wave_max_f(tmax);
       if (lane == 0) rmax[w] = wm;
     }
     __syncthreads();
@@ -1017,7 +1014,7 @@ __device__ float store_tmax(const Ctx& c, int64_t u, int lane) {
     const int64_t e = *(kk < sv.sc ? c.arena + sv.so + kk : c.arena + sv.dof + (kk - sv.sc));
     tb = fmaxf(tb, c.ev_t[e]);   // clamped duplicates of the last event do not change the max
   }
-  return wave_max(tb);
+  return wave_max_f(tb);
 }
 
 // row of a root's embedding: its centre index (2 hops: its root index, via the outer centre)
@@ -1106,11 +1103,8 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
       const uint64_t valid = __ballot(lane < K && e_l >= 0);
       if (!((valid >> j) & 1ull)) continue;
       const int o = c.ceoff[x] + __popcll(valid & ((1ull << j) - 1ull));
-      const int64_t e = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(e_l >> 32), j, 64) << 32) |
-                                  (uint64_t)(uint32_t)__shfl((int)e_l, j, 64));
-      const int64_t u = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(u_l >> 32), j, 64) << 32) |
-                                  (uint64_t)(uint32_t)__shfl((int)u_l, j, 64));
-      const float te = __shfl(t_l, j, 64);
+      const int64_t e = shfl_i64(e_l, j), u = shfl_i64(u_l, j);
+      const float te = lane_f(t_l, j);
       const int ju = (int)c.assoc[u];
       const float lu = mode == 0 ? store_tmax(c, u, lane) : (float)c.lu_buf[u];
       if (lane == 0) {
@@ -1411,6 +1405,14 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
   const float sqc = sqrtf((float)C);
   const int jl = jrec >= 0 ? jrec : c.e_j[e0 + min(lane, max(ne - 1, 0))];   // lane e: the neighbour row of edge e
   const float sk0 = Pi[3 * HC + l0], sk1 = Pi[3 * HC + C + l0];
+  // the attention-dropout key (centre node, lane's edge e_id) and seed, loaded with the first rows instead
+  // of after the softmax
+  uint64_t dseed = 0, dnode = 0, deid = 0;
+  if (TRAIN) {
+    dseed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+    dnode = (uint64_t)c.cent[x];
+    deid = (uint64_t)c.e_id[e0 + min(lane, max(ne - 1, 0))];
+  }
   float my0 = -INFINITY, my1 = -INFINITY;
   float o0 = 0.f, o1 = 0.f;
   float t0, t1;
@@ -1424,9 +1426,9 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
       c.alpha[(int64_t)(e0 + lane) * 2] = a0;
       c.alpha[(int64_t)(e0 + lane) * 2 + 1] = a1;
       if (c.drop) {
-        const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-        t0 *= att_keep(c, seed, x, e0 + lane, 0);
-        t1 *= att_keep(c, seed, x, e0 + lane, 1);
+        const uint32_t base = drop_base(dseed, (uint64_t)c.att_salt, dnode, deid);
+        t0 *= keep32(base, 0u, c.p, c.inv_keep);
+        t1 *= keep32(base, 1u, c.p, c.inv_keep);
       }
     }
   };
@@ -1713,7 +1715,7 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
         zn += vfw[o] * hn[q];
       }
     }
-    const float ap = wave_sum(zp) + vfw[D], an = wave_sum(zn) + vfw[D];
+    const float ap = wave_sum_f(zp) + vfw[D], an = wave_sum_f(zn) + vfw[D];
     const float sp = sigm(ap), sn = sigm(an);
     const float invB = 1.0f / (float)B;
     const float dap = (sigm(sp) - 1.0f) * sp * (1.0f - sp) * invB;
@@ -1791,7 +1793,7 @@ __device__ void lp_vec_body(const Ctx& c, int y, int lane) {
     else if (y == 3 * D) s += ev[7 * D + 4] + ev[7 * D + 5];
     else s += ev[7 * D + 6];
   }
-  s = wave_sum(s);
+  s = wave_sum_f(s);
   if (lane == 0) {
     float* g = c.grads;
     if (y < D) c.adf.put(g, c.L.lsb + y, s);

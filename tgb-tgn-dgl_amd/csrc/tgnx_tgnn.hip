@@ -703,25 +703,33 @@ __device__ __forceinline__ void edge_gather(const Ctx& c, int e, const EdgeCols<
   S.nb = m.nb;
 }
 
-// Sum of v[0..7] over the wave by recursive halving (10 shuffles): on return lane l holds the
-// total of head l / 8 (lanes with l % 8 == 0 write).
+// Sum of v[0..7] over the wave by recursive halving (10 exchanges: permlane swaps for lane ^ 32 / ^ 16,
+// DPP for the rest — no LDS round trip): on return lane l holds the total of head l / 8 (lanes with
+// l % 8 == 0 write).  Full wave.
 __device__ __forceinline__ float wave_sum8(const float (&v)[H], int lane) {
   const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
   float k4[4], k2[2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const float keep = b5 ? v[4 + i] : v[i], send = b5 ? v[i] : v[4 + i];
-    k4[i] = keep + __shfl_xor(send, 32, 64);
+    k4[i] = keep + xor32_f(send);
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const float keep = b4 ? k4[2 + i] : k4[i], send = b4 ? k4[i] : k4[2 + i];
-    k2[i] = keep + __shfl_xor(send, 16, 64);
+    k2[i] = keep + xor16_f(send);
   }
+#ifdef TGNX_NO_DPP
   float s = (b3 ? k2[1] : k2[0]) + __shfl_xor(b3 ? k2[0] : k2[1], 8, 64);
   s += __shfl_xor(s, 4, 64);
   s += __shfl_xor(s, 2, 64);
   s += __shfl_xor(s, 1, 64);
+#else
+  float s = (b3 ? k2[1] : k2[0]) + dpp_f<0x128>(b3 ? k2[0] : k2[1]);  // row_ror:8 = lane ^ 8 in the row
+  s += dpp_f<0xB1>(s);   // lane ^ 1
+  s += dpp_f<0x4E>(s);   // lane ^ 2
+  s += dpp_f<0x141>(s);  // half-row mirror: the other quad (quads uniform by now)
+#endif
   return s;
 }
 
