@@ -1651,7 +1651,10 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
 #ifdef TGNX_STAMP_STAGE  // diagnostic: checkpoint 1 = wave 0 done with its part before the first barrier
   TGNX_STAMP_AT(1);
 #endif
-  __syncthreads();
+  // LDS-only barriers in this kernel (the weights, embedding rows and partial sums are LDS; the attention's
+  // alpha stores and the evs rows need not have landed): __syncthreads would wait for vmcnt(0)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   const int cr[3] = {scr[0], scr[1], scr[2]};
   const int kc = (D + 3) / 4, k0 = wv * kc, nk = min(D - k0, kc);
   if (flat) {  // lin_src(z_s), lin_dst(z_p), lin_dst(z_n): wave wv takes float4 columns [q0, q0 + nq)
@@ -1696,7 +1699,8 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
       }
     }
   }
-  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   TGNX_STAMP_AT(0);
   float* ev = c.evs + (int64_t)i * evs_stride(D);
   if (wv == 0) {
@@ -1770,12 +1774,15 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
       part[wv][2][o] = d2;
     }
   }
-  __syncthreads();
-  for (int x = tid; x < 3 * D; x += blockDim.x) {
-    const int r = x / D, o = x % D;
-    const float g = (part[0][r][o] + part[1][r][o]) + (part[2][r][o] + part[3][r][o]);
-    atomicAdd(&c.dZc[(int64_t)cr[r] * D + o], g);
-  }
+  // LDS-only barrier again: the evs-row and alpha stores stay in flight
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+    for (int o = tid; o < D; o += blockDim.x) {
+      const float g = (part[0][r][o] + part[1][r][o]) + (part[2][r][o] + part[3][r][o]);
+      atomicAdd(&c.dZc[(int64_t)cr[r] * D + o], g);
+    }
 }
 
 // predictor bias / output-layer / loss reductions over this rank's events (wave per output)
