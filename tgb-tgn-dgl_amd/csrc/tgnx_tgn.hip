@@ -588,37 +588,89 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
   }
   auto word = [&](const int* list, int i) -> int64_t { return direct ? (int64_t)i : (int64_t)list[i]; };
   // pass 1: centres (sorted) and sampled nodes (sorted, + assoc): thread t takes a contiguous run of each
-  // word list; block scans give the ranks; words are cleared
+  // word list; block scans give the ranks; words are cleared.  Direct (small) graphs: a thread's <= 2 words
+  // of both bitmaps stay in registers, and in 1-hop train steps the centres and their node ranks (a
+  // centre is a sampled node too: its rank is the word's first node rank + the node bits below it) are
+  // staged in LDS for pass 2 — no global round trip for cent[] / assoc[] there.
   const int cq = (ncw + T - 1) / T, c0 = min(ncw, tid * cq), c1 = min(ncw, c0 + cq);
   const int nq = (nnw + T - 1) / T, n0 = min(nnw, tid * nq), n1 = min(nnw, n0 + nq);
   int nc = 0, np = 0;
-  for (int i = c0; i < c1; ++i) nc += __popc(c.cb[word(c.cl, i)]);
-  for (int i = n0; i < n1; ++i) np += __popc(c.nb[word(c.nl, i)]);
+  uint32_t dcw[2] = {0u, 0u}, dnw[2] = {0u, 0u};
+  if (direct) {  // c0..c1 == n0..n1, <= 2 words
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (c0 + j < c1) {
+        dcw[j] = c.cb[c0 + j];
+        dnw[j] = c.nb[c0 + j];
+      }
+      nc += __popc(dcw[j]);
+      np += __popc(dnw[j]);
+    }
+  } else {
+    for (int i = c0; i < c1; ++i) nc += __popc(c.cb[word(c.cl, i)]);
+    for (int i = n0; i < n1; ++i) np += __popc(c.nb[word(c.nl, i)]);
+  }
   int R, M, rc, rank;
   block_excl_scan2(nc, np, sh, &rc, &rank, &R, &M);
   const bool fits = R <= c.Rcap && M <= c.Mcap;
-  for (int i = c0; i < c1; ++i) {
-    const int64_t w = word(c.cl, i);
-    uint32_t m = c.cb[w];
-    if (m) c.cb[w] = 0u;
-    while (m) {
-      const int b = __ffs(m) - 1;
-      m &= m - 1;
-      if (fits) c.cent[rc] = (w << 5) + b;
-      ++rc;
+  const bool lds_c = direct && TRAIN && c.layers == 1 && R <= 3 * c.Bmax;  // (block-uniform)
+  int64_t* lv = reinterpret_cast<int64_t*>(smem);                          // [3 Bmax] centre node
+  int* lloc = reinterpret_cast<int*>(smem + (size_t)3 * c.Bmax * 8);       // [3 Bmax] its node rank
+  if (direct) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (c0 + j >= c1) break;
+      const int64_t w = c0 + j;
+      const int rw = rank;
+      uint32_t m = dnw[j];
+      if (m) c.nb[w] = 0u;
+      while (m) {
+        const int b = __ffs(m) - 1;
+        m &= m - 1;
+        const int64_t v = (w << 5) + b;
+        if (fits) c.nid[rank] = v;
+        c.assoc[v] = rank;
+        ++rank;
+      }
+      m = dcw[j];
+      if (m) c.cb[w] = 0u;
+      while (m) {
+        const int b = __ffs(m) - 1;
+        m &= m - 1;
+        if (fits) {
+          c.cent[rc] = (w << 5) + b;
+          if (lds_c) {
+            lv[rc] = (w << 5) + b;
+            lloc[rc] = rw + __popc(dnw[j] & ((1u << b) - 1u));
+          }
+        }
+        ++rc;
+      }
     }
-  }
-  for (int i = n0; i < n1; ++i) {
-    const int64_t w = word(c.nl, i);
-    uint32_t m = c.nb[w];
-    if (m) c.nb[w] = 0u;
-    while (m) {
-      const int b = __ffs(m) - 1;
-      m &= m - 1;
-      const int64_t v = (w << 5) + b;
-      if (fits) c.nid[rank] = v;
-      c.assoc[v] = rank;
-      ++rank;
+  } else {
+    for (int i = c0; i < c1; ++i) {
+      const int64_t w = word(c.cl, i);
+      uint32_t m = c.cb[w];
+      if (m) c.cb[w] = 0u;
+      while (m) {
+        const int b = __ffs(m) - 1;
+        m &= m - 1;
+        if (fits) c.cent[rc] = (w << 5) + b;
+        ++rc;
+      }
+    }
+    for (int i = n0; i < n1; ++i) {
+      const int64_t w = word(c.nl, i);
+      uint32_t m = c.nb[w];
+      if (m) c.nb[w] = 0u;
+      while (m) {
+        const int b = __ffs(m) - 1;
+        m &= m - 1;
+        const int64_t v = (w << 5) + b;
+        if (fits) c.nid[rank] = v;
+        c.assoc[v] = rank;
+        ++rank;
+      }
     }
   }
   if (!fits) {
@@ -633,6 +685,51 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
   // offsets and the update list (memory_module.py:129 src ∪ dst, sorted)
   const int xc = (R + T - 1) / T, x0 = min(R, tid * xc), x1 = min(R, x0 + xc);
   int ne = 0, nu = 0;
+  if (lds_c && xc <= 2) {  // the chunk's (<= 2) centres in registers across the block scan
+    int64_t v[2] = {0, 0};
+    int loc[2] = {0, 0}, kv[2] = {0, 0};
+    bool up[2] = {false, false};
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (x0 + j < x1) {
+        v[j] = lv[x0 + j];
+        loc[j] = lloc[x0 + j];
+      }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (x0 + j < x1) {
+        kv[j] = c.kval[v[j]];
+        up[j] = c.node_gen[v[j]] == gen;
+        ne += kv[j];
+        nu += up[j];
+      }
+    int E, U, re, ru;
+    block_excl_scan2(ne, nu, sh, &re, &ru, &E, &U);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (x0 + j < x1) {
+        const int x = x0 + j;
+        c.ceoff[x] = re;
+        re += kv[j];
+        c.cent_loc[x] = loc[j];
+        c.crank[loc[j]] = x;
+        if (up[j]) {
+          c.upd[ru] = v[j];
+          c.upd_loc[ru] = loc[j];
+          ++ru;
+        }
+      }
+    if (tid == 0) {
+      c.ceoff[R] = E;
+      c.cnt[CNT_R] = R;
+      c.cnt[CNT_M] = M;
+      c.cnt[CNT_E] = E;
+      c.cnt[CNT_U] = U;
+      c.ctl[TGNX_CTL_SUM_E] += E;
+      c.ctl[TGNX_CTL_SUM_S] += M;
+    }
+    return;  // (1 hop: no root pass)
+  }
   for (int x = x0; x < x1; ++x) {
     const int64_t v = c.cent[x];
     ne += c.kval[v];
