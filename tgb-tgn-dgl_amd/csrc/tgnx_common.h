@@ -341,7 +341,76 @@ __device__ __forceinline__ void sort_u64_rank(uint64_t* key, uint64_t* tmp, int 
 // Sort n uint64 keys in LDS, ascending, by the whole block (key[n, n_pow2) padded with ~0 on
 // return): register bitonic when n_pow2 <= blockDim.x (`tmp` holds n_pow2 keys), LDS bitonic above.
 // `distinct`: the keys are pairwise distinct and n <= blockDim.x -> rank sort.
-__device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, int n_pow2, bool distinct = false) {
+// Bitonic sort of n (power of two, T < n <= 4 T with T = blockDim.x, a multiple of 64) uint64 keys with
+// four keys per thread in registers (positions t, t + T, t + 2T, t + 3T): partner distances >= T are
+// compare-exchanges inside the thread, 64 <= j < T one LDS round (ping-pong `key` / `tmp`, one barrier
+// for all four registers), j < 64 cross-lane.  n = 4096 at T = 1024: 18 barriers instead of the 78 of
+// bitonic_sort_u64 (3,200 keys: a data-parallel step's global-batch insert plan at world 8).  tmp: n keys.
+#ifndef TGNX_SORT_REG4
+#define TGNX_SORT_REG4 1
+#endif
+__device__ __forceinline__ void cmpx_u64(uint64_t& a, uint64_t& b, bool up) {
+  const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+  a = up ? lo : hi;
+  b = up ? hi : lo;
+}
+__device__ __forceinline__ void sort_u64_reg4(uint64_t* key, uint64_t* tmp, int n) {
+  const int T = blockDim.x, t = threadIdx.x;
+  const int nm = n / T;  // 2 or 4 registers in use
+  uint64_t v[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) v[m] = m < nm ? key[t + m * T] : ~0ull;
+  int flip = 0;
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j >= WAVE; j >>= 1) {
+      if (j >= T) {  // same thread: register m pairs with m ^ (j / T)
+        if (j == T) {
+          cmpx_u64(v[0], v[1], (t & k) == 0);
+          if (nm == 4) cmpx_u64(v[2], v[3], ((t + 2 * T) & k) == 0);
+        } else {  // j == 2T
+          cmpx_u64(v[0], v[2], (t & k) == 0);
+          cmpx_u64(v[1], v[3], ((t + T) & k) == 0);
+        }
+        continue;
+      }
+      uint64_t* buf = flip ? tmp : key;
+      flip ^= 1;
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (m < nm) buf[t + m * T] = v[m];
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        if (m < nm) {
+          const int p = t + m * T;
+          const uint64_t o = buf[p ^ j];
+          const bool take_min = ((p & j) == 0) == ((p & k) == 0);
+          v[m] = take_min ? (o < v[m] ? o : v[m]) : (o > v[m] ? o : v[m]);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      if (m >= nm) continue;
+      const int p = t + m * T;
+      switch (k >= 64 ? 32 : k >> 1) {  // remaining distances 32..1
+        case 32: v[m] = bitonic_lane_stage<32>(v[m], p, k); [[fallthrough]];
+        case 16: v[m] = bitonic_lane_stage<16>(v[m], p, k); [[fallthrough]];
+        case 8: v[m] = bitonic_lane_stage<8>(v[m], p, k); [[fallthrough]];
+        case 4: v[m] = bitonic_lane_stage<4>(v[m], p, k); [[fallthrough]];
+        case 2: v[m] = bitonic_lane_stage<2>(v[m], p, k); [[fallthrough]];
+        default: v[m] = bitonic_lane_stage<1>(v[m], p, k);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+    if (m < nm) key[t + m * T] = v[m];
+  __syncthreads();
+}
+// tmp_full: tmp holds n_pow2 keys (enables the four-keys-per-thread sort for T < n_pow2 <= 4 T)
+__device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, int n_pow2, bool distinct = false,
+                                         bool tmp_full = false) {
 #ifdef TGNX_DIAG_NOSORT  // timing experiment only: results wrong
   if (distinct) return;
 #endif
@@ -354,6 +423,7 @@ __device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, in
   for (int i = n + threadIdx.x; i < n_pow2; i += blockDim.x) key[i] = ~0ull;
   __syncthreads();
   if (n_pow2 <= (int)blockDim.x) sort_u64_reg(key, tmp, n_pow2);
+  else if (tmp_full && n_pow2 <= 4 * (int)blockDim.x && TGNX_SORT_REG4) sort_u64_reg4(key, tmp, n_pow2);
   else bitonic_sort_u64(key, n_pow2);
 }
 

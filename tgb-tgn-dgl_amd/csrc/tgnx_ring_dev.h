@@ -20,10 +20,12 @@ constexpr int INSERT_MAX_B = 4096;
 struct NoCheckpoint {
   __device__ void operator()(int) const {}
 };
+// big_tmp: the LDS past the run starts holds next_pow2(2B) more keys (the scan launch, the standalone
+// insert): the register sort then also serves 1024 < 2B <= 4096
 template <class AT = NoCheckpoint>
 __device__ __forceinline__ int ring_plan_block(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int B,
                                                unsigned char* smem, int* sh, uint64_t** key_out, int** runs_out,
-                                               AT at = AT{}) {
+                                               AT at = AT{}, bool big_tmp = false) {
   const int n2 = 2 * B;
   const int n = next_pow2(n2);
   uint64_t* key = reinterpret_cast<uint64_t*>(smem);
@@ -40,7 +42,7 @@ __device__ __forceinline__ int ring_plan_block(const int64_t* __restrict__ src, 
   }
   __syncthreads();
   at(0);
-  sort_u64(key, reinterpret_cast<uint64_t*>(run_start + n2 + (n2 & 1)), n2, n, true);  // keys distinct: (node, i, dir)
+  sort_u64(key, reinterpret_cast<uint64_t*>(run_start + n2 + (n2 & 1)), n2, n, true, big_tmp);  // keys distinct: (node, i, dir)
   at(1);
   const int T = blockDim.x;
   int pc = (n2 + T - 1) / T;
@@ -109,7 +111,7 @@ __device__ __forceinline__ void ring_insert_block(int64_t* __restrict__ nbr, int
                                                   unsigned char* smem, int* sh) {
   uint64_t* key;
   int* run_start;
-  const int U = ring_plan_block(src, dst, B, smem, sh, &key, &run_start);
+  const int U = ring_plan_block(src, dst, B, smem, sh, &key, &run_start, NoCheckpoint{}, true);
   const int n2 = 2 * B;
   const int lane = threadIdx.x & 63, nwv = blockDim.x >> 6;
   for (int r = threadIdx.x >> 6; r < U; r += nwv) {
@@ -121,9 +123,9 @@ __device__ __forceinline__ void ring_insert_block(int64_t* __restrict__ nbr, int
 }
 
 __host__ __device__ __forceinline__ size_t ring_insert_smem_bytes(int B) {
-  // keys + run starts (+ register-sort ping-pong buffer for next_pow2(2B) <= 1024)
+  // keys + run starts (+ register-sort ping-pong buffer for next_pow2(2B) <= 4096)
   const int n = next_pow2(2 * B);
-  return (size_t)n * 8 + (size_t)(2 * B + 2) * 4 + (n <= 1024 ? (size_t)n * 8 : 0);
+  return (size_t)n * 8 + (size_t)(2 * B + 2) * 4 + (n <= 4096 ? (size_t)n * 8 : 0);
 }
 
 }  // namespace tgnx

@@ -458,7 +458,7 @@ __device__ void store_plan_block(const Ctx& c, int B, int64_t start, unsigned ch
   }
   __syncthreads();
   at(0);
-  sort_u64(key, tmp, n2, n, true);  // keys distinct: (node, dir, i)
+  sort_u64(key, tmp, n2, n, true, true);  // keys distinct: (node, dir, i); tmp holds n keys (tgn_scan_smem)
   at(1);
   const int T = blockDim.x, pc = (n2 + T - 1) / T;
   const int p0 = threadIdx.x * pc, p1 = min(n2, p0 + pc);
@@ -519,7 +519,7 @@ __device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsig
   if (which == 0) {
     uint64_t* key;
     int* runs;
-    const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs, at);
+    const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs, at, true);
     for (int p = tid; p < 2 * B; p += T) c.rkeys[p] = key[p];
     for (int r = tid; r < U; r += T) c.rruns[r] = runs[r];
     if (tid == 0) {
