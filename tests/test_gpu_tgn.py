@@ -316,3 +316,41 @@ def test_tgn_pipelined_equals_resident(layers):
             o1.exp_avg.copy_(o2.exp_avg)
             o1.exp_avg_sq.copy_(o2.exp_avg_sq)
             m1.memory.memory.copy_(m2.memory.memory)
+
+
+def test_tgn_large_batch_partitioned_plans_match_oracle():
+    """A batch of 1,100 events (2,200 plan keys): the insert and store plans split by node range over
+    several workgroups each (plan_part, tgn_scan; P = ceil(2B / 512) = 5), as a data-parallel step plans
+    its global batch.  Train steps against the oracle: outputs, memory, last_update, the ring (neighbours,
+    e_id, t) and the loader's assoc of the inserted nodes (neighbor_loader.py:72-73: their rank among the
+    batch's nodes), then a flush."""
+    from oracle.tgn_ref import train_step
+    B, nb = 1100, 3
+    s, ref, opt_ref, lref, model, opt, eng = _setup("last", N=3000, B=B, nb=nb, max_neg=1)
+    ev_t = torch.from_numpy(s.t.astype(np.float32))
+    ev_msg = torch.from_numpy(s.msg)
+    rng = np.random.default_rng(5)
+    for st in range(nb):
+        a = st * B
+        sl = slice(a, a + B)
+        src, pos = torch.from_numpy(s.src[sl]), torch.from_numpy(s.dst[sl])
+        neg = torch.from_numpy(rng.choice(s.dst_nodes, size=B))
+        _, po, no = train_step(ref, opt_ref, lref, ev_t, ev_msg, src, pos, neg, ev_t[sl], ev_msg[sl])
+        pg, ng = eng.train_batch(a, B, neg=neg)
+        torch.cuda.synchronize()
+        eng.check()
+        assert torch.allclose(pg.cpu(), po, atol=2e-5) and torch.allclose(ng.cpu(), no, atol=2e-5), st
+        assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5), st
+        assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update), st
+        assert np.array_equal(eng.loader.e_id.cpu().numpy(), lref.e_id), st
+        live = lref.e_id >= 0
+        assert np.array_equal(eng.loader.neighbors.cpu().numpy()[live], lref.neighbors[live]), st
+        assert np.array_equal(eng.loader.t.cpu().numpy(), lref.t), st
+        ins = np.unique(np.concatenate([s.src[sl], s.dst[sl]]))
+        assert np.array_equal(eng.loader._assoc.cpu().numpy()[ins], np.arange(ins.size)), st
+        _sync(ref, opt_ref, model, opt)
+    ref.memory.train(False)
+    eng.flush()
+    torch.cuda.synchronize()
+    assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5)
+    assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update)

@@ -35,7 +35,7 @@ constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touc
 #ifndef TGNX_PRED_ATT_REC
 #define TGNX_PRED_ATT_REC 1  // per-root neighbour-row records for the attention in tgn_pred_train<ATT>
 #endif
-enum { CNT_R = 0, CNT_M = 1, CNT_E = 2, CNT_U = 3, CNT_RUNS = 4, CNT_SRUNS = 5, CNT_LIST = 6, CNT_WORDS = 16 };
+enum { CNT_R = 0, CNT_M = 1, CNT_E = 2, CNT_U = 3, CNT_LIST = 6, CNT_WORDS = 16 };  // (4, 5: unused)
 
 __host__ __device__ inline int64_t al4(int64_t x) { return (x + 3) & ~int64_t(3); }
 
@@ -198,6 +198,11 @@ struct Ctx {
   float *pA, *pB, *pC, *pD;  // split-K partials of the deferred weight-gradient GEMMs
   uint64_t *rkeys, *skeys;
   int *rruns, *sruns;
+  // plans split by node range over pplan workgroups each (tgn_scan): partition q's keys at [poff[q], +n_q) of
+  // the key array (node order across partitions), its runs at runs[poff[q] + q ...] (+ terminator); pcnt[q]
+  // = its run count.  pplan = 1: one workgroup per plan, runs at [0, U].
+  int pplan;
+  int *rpc, *rpo, *spc, *spo;
   int Bmax, Qcap, Rcap, Mcap, Ecap, Ucap, tgp_rows;
   Lay L;
   // ---- 2-hop (layers = 2).  The arrays above then describe the OUTER sample: centres = the 1-hop node
@@ -238,6 +243,15 @@ __device__ __forceinline__ float softplusf(float x) { return fmaxf(x, 0.f) + log
 // tgn_scan walks every bitmap word of a small graph directly (<= 2 words per thread of its 1024) and
 // the nonzero words of a large one from the summary bitmaps; mark sets summary bits only for the latter
 constexpr int TGN_SCAN_THREADS = 1024;
+// plan partitions per plan (tgn_scan): one per TGNX_PLAN_KEYS keys of the (global) batch, up to TGNX_PLAN_PMAX
+#ifndef TGNX_PLAN_KEYS
+#define TGNX_PLAN_KEYS 512
+#endif
+#define TGNX_PLAN_PMAX 16
+__host__ __device__ inline int plan_parts(int B) {
+  const int p = (2 * B + TGNX_PLAN_KEYS - 1) / TGNX_PLAN_KEYS;
+  return p < 1 ? 1 : (p > TGNX_PLAN_PMAX ? TGNX_PLAN_PMAX : p);
+}
 __host__ __device__ __forceinline__ bool scan_direct(int64_t words) { return words <= 2 * (int64_t)TGN_SCAN_THREADS; }
 __device__ __forceinline__ void mark_node(uint32_t* bm, uint32_t* sum, int64_t v) {
   const int64_t w = v >> 5;
@@ -440,7 +454,8 @@ __global__ void __launch_bounds__(256) tgn_mark(Ctx c, int nmark) {
 
 // message-store plan of a batch: (node << 33 | dir << 32 | i), dir 0 = as source (msg_s_store),
 // 1 = as destination (msg_d_store); sorted, each (node, dir) run lists its events in batch order
-// (memory_module.py:188-191 with a stable sort).
+// (memory_module.py:188-191 with a stable sort): plan_part(which = 1) below.
+
 template <class AT>
 __device__ void store_plan_block(const Ctx& c, int B, int64_t start, unsigned char* smem, int* sh, AT at) {
   const int n2 = 2 * B, n = next_pow2(n2);
@@ -473,7 +488,8 @@ __device__ void store_plan_block(const Ctx& c, int B, int64_t start, unsigned ch
   for (int r = threadIdx.x; r < U; r += T) c.sruns[r] = runs[r];
   if (threadIdx.x == 0) {
     c.sruns[U] = n2;
-    c.cnt[CNT_SRUNS] = U;
+    c.spc[0] = U;
+    c.spo[0] = 0;
   }
 }
 
@@ -513,10 +529,133 @@ __host__ __device__ inline size_t tgn_scan_smem(int Bmax) {
 
 // the batch's ring-insert plan (which = 0) and message-store plan (which = 1); they read only the batch's
 // events and run as two extra 1024-thread workgroups of the scan launch
+// One partition (node range) of a batch's plan: which = 0 ring-insert plan (keys node << 32 | (B-1-i) << 1 | dir,
+// runs per node), 1 message-store plan (node << 33 | dir << 32 | i, runs per (node, dir)).  With P > 1 the
+// P workgroups of a plan derive the same node splitters from a 64-entry sample (sorted by wave 0), count
+// every partition's entries (so each knows its key offset), compact their own entries in entry order and
+// sort only those: P sorts of ~2B / P keys in parallel instead of one of 2B (a data-parallel step plans
+// the whole global batch; sorting 3,200 keys took one workgroup 49 us).
+template <class AT>
+__device__ void plan_part(const Ctx& c, int which, int part, int P, int B, int64_t start, unsigned char* smem, int* sh,
+                          AT at) {
+  const int tid = threadIdx.x, T = blockDim.x, n2 = 2 * B;
+  const int64_t* src = c.ev_src + start;
+  const int64_t* dst = c.ev_dst + start;
+  __shared__ int64_t split[17];
+  __shared__ int pn[17];
+  auto node_of = [&](int p) -> int64_t {
+    const int i = p < B ? p : p - B;
+    return which == 0 ? (p < B ? dst[i] : src[i]) : (p < B ? src[i] : dst[i]);
+  };
+  auto key_of = [&](int p, int64_t v) -> uint64_t {
+    const int i = p < B ? p : p - B, dir = p < B ? 0 : 1;
+    const uint64_t node = (uint64_t)v;
+    return which == 0 ? (node << 32) | ((uint64_t)(B - 1 - i) << 1) | (uint64_t)dir
+                      : (node << 33) | ((uint64_t)dir << 32) | (uint64_t)i;
+  };
+  auto part_of = [&](int64_t v) {
+    int q = 0;
+    for (int x = 1; x < P; ++x) q += v >= split[x];
+    return q;
+  };
+  uint64_t* key = reinterpret_cast<uint64_t*>(smem);
+  int* runs = reinterpret_cast<int*>(smem + (size_t)next_pow2(n2) * 8);
+  uint64_t* tmp = reinterpret_cast<uint64_t*>(smem + (size_t)next_pow2(n2) * 8 + (size_t)(n2 + 2) * 4 + 8);
+  // entries p = tid + j T (all loads of a thread in flight at once); a partition's keys are compacted in
+  // any order (wave-aggregated LDS slots): the keys are distinct, so the sort fixes their order
+  constexpr int MAXE = 8;  // 2B <= 8192 at T = 1024
+  int64_t v[MAXE];
+#pragma unroll
+  for (int j = 0; j < MAXE; ++j) v[j] = node_of(min(tid + j * T, n2 - 1));  // unconditional (clamped) loads
+  __shared__ int lpos;
+  int off = 0;
+  if (P > 1) {
+    if (tid < WAVE) {  // 64 sampled nodes, sorted in registers; splitters at the P-quantiles
+      uint64_t sv = (uint64_t)node_of((int)(((int64_t)tid * n2) >> 6));
+      for (int k = 2; k <= WAVE; k <<= 1) switch (k >> 1) {
+          case 32: sv = bitonic_lane_stage<32>(sv, tid, k); [[fallthrough]];
+          case 16: sv = bitonic_lane_stage<16>(sv, tid, k); [[fallthrough]];
+          case 8: sv = bitonic_lane_stage<8>(sv, tid, k); [[fallthrough]];
+          case 4: sv = bitonic_lane_stage<4>(sv, tid, k); [[fallthrough]];
+          case 2: sv = bitonic_lane_stage<2>(sv, tid, k); [[fallthrough]];
+          default: sv = bitonic_lane_stage<1>(sv, tid, k);
+        }
+      for (int x = 1; x < P; ++x)
+        if (tid == (x * WAVE) / P) split[x] = (int64_t)sv;
+    }
+    if (tid <= P) pn[tid] = 0;
+    if (tid == 0) lpos = 0;
+    __syncthreads();
+    int q[MAXE];
+    int cnt[17];
+#pragma unroll
+    for (int x = 0; x < 17; ++x) cnt[x] = 0;
+#pragma unroll
+    for (int j = 0; j < MAXE; ++j) {
+      q[j] = tid + j * T < n2 ? part_of(v[j]) : -1;
+#pragma unroll
+      for (int x = 0; x < 17; ++x) cnt[x] += x == q[j];
+    }
+#pragma unroll
+    for (int x = 0; x < 17; ++x)  // (partition counts: one LDS atomic per wave and partition)
+      if (x < P) {
+        const int w = (int)wave_sum_f((float)cnt[x]);  // exact: < 2^24
+        if ((tid & (WAVE - 1)) == 0 && w) atomicAdd(&pn[x], w);
+      }
+    // this partition's keys into LDS slots (wave-aggregated)
+#pragma unroll
+    for (int j = 0; j < MAXE; ++j) {
+      const bool me = q[j] == part;
+      const uint64_t m = __ballot(me);
+      int base = 0;
+      if ((tid & (WAVE - 1)) == 0 && m) base = atomicAdd(&lpos, __popcll(m));
+      base = lane_i(base, 0);
+      if (me) key[base + __popcll(m & ((1ull << (tid & (WAVE - 1))) - 1ull))] = key_of(tid + j * T, v[j]);
+    }
+    __syncthreads();
+    for (int x = 0; x < part; ++x) off += pn[x];
+  } else {
+#pragma unroll
+    for (int j = 0; j < MAXE; ++j) {
+      const int p = tid + j * T;
+      if (p < n2) key[p] = key_of(p, v[j]);
+    }
+  }
+  const int nk = P > 1 ? pn[part] : n2;
+  const int n = next_pow2(max(nk, 1));
+  for (int p = nk + tid; p < n; p += T) key[p] = ~0ull;
+  __syncthreads();
+  at(0);
+  sort_u64(key, tmp, nk, n, true, true);  // keys distinct
+  at(1);
+  constexpr int sh_run = 32;  // runs: node (ring plan: key >> 32) / (node, dir) (store plan: key >> 32)
+  const int pc = (nk + T - 1) / T, p0 = min(nk, tid * pc), p1 = min(nk, p0 + pc);
+  int cr = 0;
+  for (int p = p0; p < p1; ++p) cr += (p == 0 || (key[p] >> sh_run) != (key[p - 1] >> sh_run));
+  int U;
+  int rid = block_excl_scan(cr, sh, &U);
+  for (int p = p0; p < p1; ++p)
+    if (p == 0 || (key[p] >> sh_run) != (key[p - 1] >> sh_run)) runs[rid++] = p;
+  __syncthreads();
+  uint64_t* gk = which == 0 ? c.rkeys : c.skeys;
+  int* gr = (which == 0 ? c.rruns : c.sruns) + off + part;
+  for (int p = tid; p < nk; p += T) gk[off + p] = key[p];
+  for (int r = tid; r < U; r += T) gr[r] = off + runs[r];
+  if (tid == 0) {
+    gr[U] = off + nk;
+    (which == 0 ? c.rpc : c.spc)[part] = U;
+    (which == 0 ? c.rpo : c.spo)[part] = off;
+  }
+}
 template <class AT>
 __device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh, AT at) {
-  const int tid = threadIdx.x, T = blockDim.x;
-  if (which == 0) {
+  // blocks [0, pplan): ring-plan partitions; [pplan, 2 pplan): store-plan partitions.  One partition (a
+  // world-1 batch): the single-workgroup plans (their keys come straight from the events, no compaction)
+  const int P = c.pplan;
+  if (P > 1) {
+    plan_part(c, which < P ? 0 : 1, which % P, P, B, start, smem, sh, at);
+  } else if (which == 0) {
+    const int tid = threadIdx.x, T = blockDim.x;
     uint64_t* key;
     int* runs;
     const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs, at, true);
@@ -524,12 +663,34 @@ __device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsig
     for (int r = tid; r < U; r += T) c.rruns[r] = runs[r];
     if (tid == 0) {
       c.rruns[U] = 2 * B;
-      c.cnt[CNT_RUNS] = U;
+      c.rpc[0] = U;
+      c.rpo[0] = 0;
     }
   } else {
     store_plan_block(c, B, start, smem, sh, at);
   }
 }
+// run r of a partitioned plan -> its key range [a, a + len) (r: the global run index, partitions in node order)
+__device__ __forceinline__ bool plan_run(const int* runs, const int* pc, const int* po, int P, int r, int& a, int& len) {
+  int base = 0;
+  for (int q = 0; q < P; ++q) {
+    const int u = pc[q];
+    if (r < base + u) {
+      const int* g = runs + po[q] + q + (r - base);
+      a = g[0];
+      len = g[1] - a;
+      return true;
+    }
+    base += u;
+  }
+  return false;
+}
+__device__ __forceinline__ int plan_runs(const int* pc, int P) {
+  int u = 0;
+  for (int q = 0; q < P; ++q) u += pc[q];
+  return u;
+}
+
 // K2 (3 workgroups): WG0 ordered bitmap walks -> centres (+ edge offsets, update list) and sampled
 // nodes (+ assoc, centre ranks); WG1 / WG2 the batch's ring-insert / message-store plans (they read only
 // the batch's events).  Resident train steps: every workgroup takes the batch from the step counters
@@ -2688,11 +2849,10 @@ __device__ __forceinline__ void xrow_header(float* h, int64_t v, int64_t luv) {
 // ring insert of the batch (neighbor_loader.py:52-104): wave per node run of the ring plan (4 per block)
 __device__ __forceinline__ void ring_merge_block(const Ctx& c, int blk, int B, int64_t start) {
   const int r = blk * 4 + (threadIdx.x >> 6);
-  if (r < c.cnt[CNT_RUNS]) {
-    const int a = c.rruns[r];
+  int a, len;
+  if (plan_run(c.rruns, c.rpc, c.rpo, c.pplan, r, a, len))  // r = the node's rank among the batch's nodes
     ring_merge_run(c.nbr, c.eid, c.rt, c.K, c.ev_src + start, c.ev_dst + start, c.ev_t + start, B,
-                   c.ctl[TGNX_CTL_CUR_EID], c.assoc, c.rkeys, a, c.rruns[r + 1] - a, r, threadIdx.x & 63);
-  }
+                   c.ctl[TGNX_CTL_CUR_EID], c.assoc, c.rkeys, a, len, r, threadIdx.x & 63);
 }
 // update_state pieces (memory_module.py:126-150, :180-191) and the ring insert, by block range:
 // [0, nmem): memory / last_update of the update list from the GRU rows (wave per node; train rows
@@ -2739,12 +2899,13 @@ __device__ void update_body(const Ctx& c, int blk, int nmem, int nst, int mem_mo
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   if (blk < nmem + nst) {
     const int bid = blk - nmem;
-    const int n2 = 2 * B, U = c.cnt[CNT_SRUNS];
+    const int n2 = 2 * B, U = plan_runs(c.spc, c.pplan);
     const int64_t ab = 2 * start;  // arena slot of this batch
     for (int p = bid * blockDim.x + threadIdx.x; p < n2; p += nst * blockDim.x)
       c.arena[ab + p] = start + (int64_t)(c.skeys[p] & 0xFFFFFFFFull);
     for (int r = bid * blockDim.x + threadIdx.x; r < U; r += nst * blockDim.x) {
-      const int a = c.sruns[r], len = c.sruns[r + 1] - a;
+      int a, len;
+      plan_run(c.sruns, c.spc, c.spo, c.pplan, r, a, len);
       const uint64_t k = c.skeys[a];
       const int64_t v = (int64_t)(k >> 33);
       const int dir = (int)((k >> 32) & 1u);
@@ -2954,7 +3115,7 @@ static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_spl
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
-      Ep, alpha, Zc, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns,
+      Ep, alpha, Zc, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
       rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF, total;
   int tgp_rows, tgp_e1;
 };
@@ -3019,9 +3180,10 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.pD = carve(off, gemm_partial_floats(shp_dWg(k, nullptr)) * 4);
   const int n2 = 2 * k.B;
   W.rkeys = carve(off, (size_t)n2 * 8);
-  W.rruns = carve(off, (size_t)(n2 + 2) * 4);
+  W.rruns = carve(off, (size_t)(n2 + 2 + TGNX_PLAN_PMAX) * 4);
   W.skeys = carve(off, (size_t)n2 * 8);
-  W.sruns = carve(off, (size_t)(n2 + 2) * 4);
+  W.sruns = carve(off, (size_t)(n2 + 2 + TGNX_PLAN_PMAX) * 4);
+  W.pcnt = carve(off, (size_t)4 * TGNX_PLAN_PMAX * 4);
   const bool two = k.layers == 2;
   const size_t R1 = two ? k.R1cap : 0, E1 = k.E1cap, R2 = two ? k.Rcap : 0;
   W.rb = carve(off, two ? words * 4 : 0);
@@ -3174,6 +3336,11 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.rruns = reinterpret_cast<int*>(ws + W.rruns);
   c.skeys = reinterpret_cast<uint64_t*>(ws + W.skeys);
   c.sruns = reinterpret_cast<int*>(ws + W.sruns);
+  c.rpc = reinterpret_cast<int*>(ws + W.pcnt);
+  c.rpo = c.rpc + TGNX_PLAN_PMAX;
+  c.spc = c.rpo + TGNX_PLAN_PMAX;
+  c.spo = c.spc + TGNX_PLAN_PMAX;
+  c.pplan = plan_parts(k.B);
   c.Bmax = k.B;
   c.Qcap = k.Qcap;
   c.Rcap = k.Rcap;
@@ -3387,7 +3554,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     tgn_mark<true><<<nmark, 256, 0, s>>>(c, nmark);
     TGNX_LAUNCH_CHECK("tgn_mark");
     probe_begin(TGNX_K_ASSEMBLE, s);
-    tgn_scan<true><<<3, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
+    tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
     probe_end(TGNX_K_ASSEMBLE, s);
     TGNX_LAUNCH_CHECK("tgn_scan");
   }
@@ -3541,7 +3708,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   TGNX_LAUNCH_CHECK("tgn_fixup_update");
   if (pipe) {  // the next batch (counters advanced by the fixup): sorted node sets, plans, descriptor
     probe_begin(TGNX_K_ASSEMBLE, s);
-    tgn_scan<true><<<3, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
+    tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
     probe_end(TGNX_K_ASSEMBLE, s);
     TGNX_LAUNCH_CHECK("tgn_scan_next");
   }
@@ -3658,7 +3825,7 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
     tgn_mark<false><<<nmark, 256, 0, s>>>(c, nmark);
   }
   TGNX_LAUNCH_CHECK("tgn_mark");
-  tgn_scan<false><<<3, TGN_SCAN_THREADS, tgn_scan_smem(k.B), s>>>(c);
+  tgn_scan<false><<<1 + 2 * c.pplan, TGN_SCAN_THREADS, tgn_scan_smem(k.B), s>>>(c);
   TGNX_LAUNCH_CHECK("tgn_scan");
   const int nedge = gridn((int64_t)Rq * c.K, 4, 4096);
   tgn_agg_emit<-1><<<nedge + gridn(Mq, 256), 256, 0, s>>>(c, 1, nedge, nullptr, nullptr, 0, 0);
