@@ -375,6 +375,15 @@ int tgnx_tgn_train_fwd_bwd_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_b
 int tgnx_tgn_train_fwd_bwd_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
                                      int64_t split_hi, int64_t batch, int32_t rank, int32_t world,
                                      uint64_t base_seed, int32_t dropout, int32_t prefetched, void* stream);
+/* tgnx_tgn_train_fwd_bwd_pipelined without its last launch (the next batch's scan), and that scan alone:
+ * fwd_bwd_split, then the exchange started asynchronously, tgnx_tgn_scan_next on the compute stream while
+ * the collective runs (the scan touches neither the exchange buffer nor what the update writes), then
+ * tgnx_tgn_apply_rows_update after the exchange — the same results as the pipelined call. */
+int tgnx_tgn_train_fwd_bwd_split(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                                 int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
+                                 int32_t dropout, int32_t prefetched, void* stream);
+int tgnx_tgn_scan_next(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo, int64_t split_hi,
+                       int64_t batch, int32_t rank, int32_t world, uint64_t base_seed, void* stream);
 /* tgnx_tgn_apply_rows + tgnx_tgn_train_update in one launch (data parallel, after the exchange). */
 int tgnx_tgn_apply_rows_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, float* rows, int64_t nrows,
                                void* stream);

@@ -162,7 +162,8 @@ def test_tgn_dp_resident_folded_cursor_per_rank():
                 f.model.memory.memory.copy_(u.model.memory.memory)
 
 
-def test_tgn_dp_pipelined_per_rank():
+@pytest.mark.parametrize("split", [True, False])
+def test_tgn_dp_pipelined_per_rank(split):
     """Data-parallel pipelined steps (tgnx_tgn_train_fwd_bwd_pipelined, world = 2, one device: each step
     marks its rank's slice of the NEXT batch in the k / v reduction launch and scans it after its last
     launch; tgnx_tgn_apply_rows_update writes the exchanged rows and runs Adam in one launch) against the
@@ -189,9 +190,10 @@ def test_tgn_dp_pipelined_per_rank():
             e = TgnEngine(model, LastNeighborLoader(N, 10, device=dev), ev, TgnAdam(model, 1e-3),
                           dst_nodes=s.dst_nodes, seed=77, rank=rank, world=2)
             e.pipeline = pipe
+            e.split_scan = split   # the next batch's scan beside the exchange (tgnx_tgn_scan_next) or in fwd_bwd
             e.bind_resident(0, split_hi, B, dropout=True)
             e.begin_epoch()
-            assert e._pipelined() == pipe
+            assert e._pipelined() == pipe and e._split() == (pipe and split)
             eng[pipe, rank] = e
     for st in range(9):
         mem0 = eng[False, 0].model.memory.memory.clone()
@@ -219,6 +221,7 @@ def test_tgn_dp_pipelined_per_rank():
             for rank in (0, 1):
                 eng[pipe, rank].comm.copy_(tot)
         for e in eng.values():
+            e._scan_next()   # (split: the next batch's scan, which rides beside the exchange)
             e._post()
             e._prefetched = e._pipelined()
         torch.cuda.synchronize()

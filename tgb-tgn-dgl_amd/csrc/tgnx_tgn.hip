@@ -3507,6 +3507,8 @@ template <int CELL>
 static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
                              void* stream, bool fuse_adam, const AdvArgs* adv, int pipe) {
   using Cl = CellOps<CELL>;
+  const bool no_tail = (pipe & 4) != 0;  // pipelined, but the next batch's scan is the caller's (tgnx_tgn_scan_next)
+  pipe &= 3;
   Ctx c;
   Caps k;
   WsLay W;
@@ -3706,7 +3708,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                       gemm_fix<GW>(shp_dWg(k, c.cnt), c.pD, e_dWg));
   probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgn_fixup_update");
-  if (pipe) {  // the next batch (counters advanced by the fixup): sorted node sets, plans, descriptor
+  if (pipe && !no_tail) {  // the next batch (counters advanced by the fixup): sorted node sets, plans, descriptor
     probe_begin(TGNX_K_ASSEMBLE, s);
     tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
     probe_end(TGNX_K_ASSEMBLE, s);
@@ -3745,6 +3747,38 @@ int tgnx_tgn_train_step_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buf
                                   int32_t prefetched, void* stream) {
   const AdvArgs a{split_lo, split_hi, batch, 0, 1, base_seed};
   return train_step_impl(cfg, buf, 1, dropout, stream, true, &a, prefetched ? 1 : 2);
+}
+
+int tgnx_tgn_train_fwd_bwd_split(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                                 int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
+                                 int32_t dropout, int32_t prefetched, void* stream) {
+  const AdvArgs a{split_lo, split_hi, batch, rank, world, base_seed};
+  return train_step_impl(cfg, buf, 1, dropout, stream, false, &a, (prefetched ? 1 : 2) | 4);
+}
+
+int tgnx_tgn_scan_next(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo, int64_t split_hi,
+                       int64_t batch, int32_t rank, int32_t world, uint64_t base_seed, void* stream) {
+  Ctx c;
+  Caps k;
+  WsLay W;
+  int rc = make_ctx(cfg, buf, 1, c, k, W);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(batch > 0 && batch <= cfg->max_batch && world >= 1 && rank >= 0 && rank < world && split_lo >= 0 &&
+                     split_hi >= split_lo && split_hi <= c.nev,
+                 "tgnx_tgn_scan_next: bad cursor arguments");
+  c.adv = 1;
+  c.adv_lo = split_lo;
+  c.adv_hi = split_hi;
+  c.adv_batch = batch;
+  c.adv_rank = rank;
+  c.adv_world = world;
+  c.adv_seed = base_seed;
+  hipStream_t s = as_stream(stream);
+  probe_begin(TGNX_K_ASSEMBLE, s);
+  tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
+  probe_end(TGNX_K_ASSEMBLE, s);
+  TGNX_LAUNCH_CHECK("tgn_scan_next");
+  return TGNX_OK;
 }
 
 int tgnx_tgn_train_fwd_bwd_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,

@@ -294,6 +294,9 @@ class TgnEngine:
         # and scans the next batch, so the next step starts at the message aggregation.  `_prefetched` says
         # whether the last call on these buffers was such a step (any other call clears it).
         self.pipeline = True
+        # world > 1 pipelined steps leave the next batch's scan out of fwd_bwd and run it while the exchange
+        # is in flight (tgnx_tgn_train_fwd_bwd_split + tgnx_tgn_scan_next)
+        self.split_scan = True
         self._prefetched = False
         if optimizer is None:
             self.adam_m, self.adam_v = torch.zeros_like(model.flat), torch.zeros_like(model.flat)
@@ -453,9 +456,9 @@ class TgnEngine:
             rc = _lib.lib().tgnx_tgn_train_step_pipelined(self._cfg_ref, self._buf_ref, lo, hi, batch, self.seed,
                                                          self._res_drop, 1 if prefetched else 0, st)
         elif self._pipelined():
-            rc = _lib.lib().tgnx_tgn_train_fwd_bwd_pipelined(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank,
-                                                            self.world, self.seed, self._res_drop,
-                                                            1 if prefetched else 0, st)
+            f = _lib.lib().tgnx_tgn_train_fwd_bwd_split if self._split() else _lib.lib().tgnx_tgn_train_fwd_bwd_pipelined
+            rc = f(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank, self.world, self.seed, self._res_drop,
+                   1 if prefetched else 0, st)
         elif self.fold_cursor:   # the batch cursor folded into the step's first launches
             f = _lib.lib().tgnx_tgn_train_step_resident if self._res_fused else _lib.lib().tgnx_tgn_train_fwd_bwd_resident
             rc = f(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank, self.world, self.seed, self._res_drop, st)
@@ -476,13 +479,32 @@ class TgnEngine:
         if rc:
             raise RuntimeError(f"tgnx TGN resident update failed: {_lib.lib().tgnx_last_error().decode()}")
 
-    def _allreduce(self):
+    def _split(self) -> bool:
+        return self.split_scan and self.world > 1 and self._pipelined() and not self._res_fused
+
+    def _scan_next(self):
+        """The next batch's scan (split pipelined steps): rides beside the exchange."""
+        if self._split():
+            lo, hi, batch = self._res
+            rc = _lib.lib().tgnx_tgn_scan_next(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank, self.world,
+                                               self.seed, self._stream())
+            if rc:
+                raise RuntimeError(f"tgnx_tgn_scan_next failed: {_lib.lib().tgnx_last_error().decode()}")
+
+    def _allreduce(self, between=None):
+        """The exchange; `between` (the next batch's scan) runs on the compute stream while it is in flight."""
         if self.world > 1:
-            self._exchange()
+            import torch.distributed as dist
+            work = dist.all_reduce(self.comm, async_op=True)
+            if between is not None:
+                between()
+            work.wait()
+        elif between is not None:
+            between()
 
     def resident_train_step(self):
         self._pre(self._prefetched)
-        self._allreduce()
+        self._allreduce(self._scan_next)
         self._post()
         self._prefetched = self._pipelined()
 
@@ -495,25 +517,30 @@ class TgnEngine:
             with torch.cuda.graph(g):   # pipelined: the steady-state step (the previous step prefetched)
                 self._pre(True)
                 self._post()
-            self._graphs = (g, None)
+            self._graphs = (g, None, None)
         else:
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g1):   # pipelined: the steady-state step (the previous step prefetched)
                 self._pre(self._pipelined())
+            gs = None
+            if self._split():
+                gs = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gs):
+                    self._scan_next()
             with torch.cuda.graph(g2):
                 self._post()
-            self._graphs = (g1, g2)
+            self._graphs = (g1, g2, gs)
         torch.cuda.synchronize(self.dev)
         self.ctl.copy_(saved)
 
     def replay_resident(self):
-        g1, g2 = self._graphs
+        g1, g2, gs = self._graphs
         if self._pipelined() and not self._prefetched:
             self.resident_train_step()   # marks + scans this batch first (eager), prefetches the next
             return
         g1.replay()
         if g2 is not None:
-            self._allreduce()
+            self._allreduce(gs.replay if gs is not None else None)
             g2.replay()
         self._prefetched = self._pipelined()
 
