@@ -268,8 +268,8 @@ def test_tgn_resident_folded_cursor_equals_advance_plus_step():
             m1.memory.memory.copy_(m2.memory.memory)
 
 
-@pytest.mark.parametrize("layers", [1, 2])
-def test_tgn_pipelined_equals_resident(layers):
+@pytest.mark.parametrize("layers,updater", [(1, "gru"), (2, "gru"), (1, "rnn")])
+def test_tgn_pipelined_equals_resident(layers, updater):
     """tgnx_tgn_train_step_pipelined (each step marks the next batch inside its predictor launch and scans it
     after its last launch; ring insert beside the GRU) against tgnx_tgn_train_step_resident on a twin
     engine: graph replay (the first step eager with prefetched = 0), device negatives, attention dropout,
@@ -278,7 +278,7 @@ def test_tgn_pipelined_equals_resident(layers):
     parameters and memory within the fused-Adam tolerances (resynchronised per step)."""
     engines = []
     for pipe in (True, False):
-        s, ref, opt_ref, lref, model, opt, eng = _setup("last", layers=layers)
+        s, ref, opt_ref, lref, model, opt, eng = _setup("last", layers=layers, updater=updater)
         model.cfg.dropout = 0.1
         eng.pipeline = pipe
         eng.bind_resident(0, 7 * 50 + 20, 50, dropout=True)   # the last batch is partial (20 events)
@@ -323,10 +323,10 @@ def test_tgn_large_batch_partitioned_plans_match_oracle():
     several workgroups each (plan_part, tgn_scan; P = ceil(2B / 512) = 5), as a data-parallel step plans
     its global batch.  Train steps against the oracle: outputs, memory, last_update, the ring (neighbours,
     e_id, t) and the loader's assoc of the inserted nodes (neighbor_loader.py:72-73: their rank among the
-    batch's nodes), then a flush."""
+    batch's nodes), then a flush and an eval batch of the same size."""
     from oracle.tgn_ref import train_step
     B, nb = 1100, 3
-    s, ref, opt_ref, lref, model, opt, eng = _setup("last", N=3000, B=B, nb=nb, max_neg=1)
+    s, ref, opt_ref, lref, model, opt, eng = _setup("last", N=3000, B=B, nb=nb + 1, max_neg=1)
     ev_t = torch.from_numpy(s.t.astype(np.float32))
     ev_msg = torch.from_numpy(s.msg)
     rng = np.random.default_rng(5)
@@ -354,3 +354,16 @@ def test_tgn_large_batch_partitioned_plans_match_oracle():
     torch.cuda.synchronize()
     assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5)
     assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update)
+    # an eval batch of the same size (its update and insert use the partitioned plans too)
+    from oracle.tgn_ref import eval_step
+    a = nb * B   # the next batch (e_ids continue the stream)
+    sl = slice(a, a + B)
+    src, pos = torch.from_numpy(s.src[sl]), torch.from_numpy(s.dst[sl])
+    negs = torch.from_numpy(rng.choice(s.dst_nodes, size=(B, 1)))
+    po, no = eval_step(ref, lref, ev_t, ev_msg, src, pos, negs, ev_t[sl], ev_msg[sl])
+    pg, ngm, rr = eng.eval_batch(a, B, negs)
+    torch.cuda.synchronize()
+    eng.check()
+    assert torch.allclose(pg.cpu(), po, atol=2e-5) and torch.allclose(ngm.cpu(), no, atol=2e-5)
+    assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5)
+    assert np.array_equal(eng.loader.e_id.cpu().numpy(), lref.e_id)
