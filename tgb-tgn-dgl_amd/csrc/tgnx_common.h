@@ -255,12 +255,22 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
 }
 
 // lane i <- lane i ^ J, picking the cheapest cross-lane path for each distance: DPP quad_perm
-// (1, 2), DPP row_ror:8 (8), ds_swizzle xor mode within 32 lanes (4, 16), bpermute (32).
+// (1, 2), DPP row_ror:8 (8), ds_swizzle xor mode within 32 lanes (4), v_permlane16_swap (16) and
+// v_permlane32_swap (32) (full waves; -DTGNX_NO_DPP: swizzle / bpermute).
 template <int J>
 __device__ __forceinline__ unsigned xlane_xor(unsigned v) {
   if constexpr (J == 1) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
   else if constexpr (J == 2) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
   else if constexpr (J == 8) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
+#ifndef TGNX_NO_DPP
+  else if constexpr (J == 16) {  // v_permlane16_swap: rows 0 <-> 1, 2 <-> 3
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? (unsigned)p[0] : (unsigned)p[1];
+  } else if constexpr (J == 32) {  // v_permlane32_swap: halves
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? (unsigned)p[0] : (unsigned)p[1];
+  }
+#endif
   else if constexpr (J < 32) return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (J << 10));
   else return __shfl_xor(v, J, WAVE);
 }
