@@ -348,6 +348,48 @@ __device__ __forceinline__ void sort_u64_rank(uint64_t* key, uint64_t* tmp, int 
   __syncthreads();
 }
 
+// Sort of 64 < n <= 1024 DISTINCT keys in O(n log n) LDS work: each wave sorts 64-key chunks in
+// registers (bitonic lane stages, no barriers), then each key's final position = its place in its chunk
+// + a 7-step binary search (count of smaller keys) in every other chunk — independent searches, so
+// their LDS latencies overlap.  The n^2 rank sort's compares made a 400-key plan VALU-bound (~5 us
+// at 1024 threads, ~6.4 us at 256; stamps timeline).  tmp: roundup(n, 64) keys; result in key[0, n).
+__device__ __forceinline__ uint64_t wave_sort64(uint64_t v, int lane) {
+  for (int k = 2; k <= WAVE; k <<= 1) switch (k >> 1) {
+      case 32: v = bitonic_lane_stage<32>(v, lane, k); [[fallthrough]];
+      case 16: v = bitonic_lane_stage<16>(v, lane, k); [[fallthrough]];
+      case 8: v = bitonic_lane_stage<8>(v, lane, k); [[fallthrough]];
+      case 4: v = bitonic_lane_stage<4>(v, lane, k); [[fallthrough]];
+      case 2: v = bitonic_lane_stage<2>(v, lane, k); [[fallthrough]];
+      default: v = bitonic_lane_stage<1>(v, lane, k);
+    }
+  return v;
+}
+__device__ __forceinline__ void sort_u64_chunks(uint64_t* key, uint64_t* tmp, int n) {
+  const int T = blockDim.x, t = threadIdx.x, lane = t & (WAVE - 1);
+  const int C = (n + WAVE - 1) / WAVE;  // <= 16
+  for (int ch = t / WAVE; ch < C; ch += T / WAVE) {
+    const int p = ch * WAVE + lane;
+    tmp[p] = wave_sort64(p < n ? key[p] : ~0ull, lane);
+  }
+  __syncthreads();
+  for (int p = t; p < n; p += T) {
+    const uint64_t v = tmp[p];
+    const int own = p / WAVE;
+    int r = p & (WAVE - 1);
+#pragma unroll
+    for (int ch = 0; ch < 16; ++ch) {
+      if (ch >= C || ch == own) continue;
+      const uint64_t* b = tmp + ch * WAVE;
+      int pos = 0;
+#pragma unroll
+      for (int st = 32; st >= 1; st >>= 1) pos += b[pos + st - 1] < v ? st : 0;
+      r += pos + (b[pos] < v ? 1 : 0);
+    }
+    key[r] = v;
+  }
+  __syncthreads();
+}
+
 // Sort n uint64 keys in LDS, ascending, by the whole block (key[n, n_pow2) padded with ~0 on
 // return): register bitonic when n_pow2 <= blockDim.x (`tmp` holds n_pow2 keys), LDS bitonic above.
 // `distinct`: the keys are pairwise distinct and n <= blockDim.x -> rank sort.
@@ -356,6 +398,9 @@ __device__ __forceinline__ void sort_u64_rank(uint64_t* key, uint64_t* tmp, int 
 // compare-exchanges inside the thread, 64 <= j < T one LDS round (ping-pong `key` / `tmp`, one barrier
 // for all four registers), j < 64 cross-lane.  n = 4096 at T = 1024: 18 barriers instead of the 78 of
 // bitonic_sort_u64 (3,200 keys: a data-parallel step's global-batch insert plan at world 8).  tmp: n keys.
+#ifndef TGNX_SORT_CHUNKS_MIN
+#define TGNX_SORT_CHUNKS_MIN 64  // distinct keys: chunked sort above this many (rank sort below)
+#endif
 #ifndef TGNX_SORT_REG4
 #define TGNX_SORT_REG4 1
 #endif
@@ -424,8 +469,9 @@ __device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, in
 #ifdef TGNX_DIAG_NOSORT  // timing experiment only: results wrong
   if (distinct) return;
 #endif
-  if (distinct && n <= (int)blockDim.x) {
-    sort_u64_rank(key, tmp, n);
+  if (distinct && (n <= (int)blockDim.x || n <= 1024)) {
+    if (n > TGNX_SORT_CHUNKS_MIN && n <= 1024) sort_u64_chunks(key, tmp, n);
+    else sort_u64_rank(key, tmp, n);
     for (int i = n + threadIdx.x; i < n_pow2; i += blockDim.x) key[i] = ~0ull;
     __syncthreads();
     return;

@@ -712,17 +712,23 @@ inline int gemm_fix_blocks(const GemmFix<CFG, EPI>& f) { return f.g.tiles_m * f.
 
 constexpr int GEMM_FIX_SMEM = 64 * 65 + 512;  // floats: the largest C tile (G64) + epilogue scratch
 
-// Sum the partials of several deferred GEMMs (block ranges in argument order); blocks past them
-// call `tail(bid)` (extra reductions that ride in the same launch).
+// Sum the partials of several deferred GEMMs (block ranges in argument order); the first `head` blocks
+// and the blocks past the GEMMs call `tail(bid, smem)` (bid: 0 .. head - 1, then head, head + 1, ...):
+// extra work that rides in the same launch, the head blocks dispatched first.
 template <class TAIL, class... F>
-__global__ void __launch_bounds__(256) gemm_fixup_kernel(TAIL tail, F... f) {
+__global__ void __launch_bounds__(256) gemm_fixup_kernel(TAIL tail, int head, F... f) {
   TGNX_STAMP(23);
   __shared__ __attribute__((aligned(16))) float smem[GEMM_FIX_SMEM];
   int bid = blockIdx.x;
-  if (!(gemm_fix_dispatch(f, bid, smem) || ...)) tail(bid);
+  if (bid < head) {
+    tail(bid, smem);
+    return;
+  }
+  bid -= head;
+  if (!(gemm_fix_dispatch(f, bid, smem) || ...)) tail(head + bid, smem);
 }
 struct NoTail {
-  __device__ void operator()(int) const {}
+  __device__ void operator()(int, float*) const {}
 };
 
 // Epilogue: C[m, n] = v (+ bias[n]) (+= C if accumulate), row-major ldc.
@@ -770,7 +776,13 @@ static inline void gemm2_launch(const GemmShape& g1, const AL1& a1, const BL1& b
 template <class TAIL, class... F>
 static inline void gemm_fixup_launch(int tail_blocks, const TAIL& tail, hipStream_t s, const F&... f) {
   const int nb = (gemm_fix_blocks(f) + ... + 0) + tail_blocks;
-  if (nb > 0) gemm_fixup_kernel<TAIL, F...><<<nb, 256, 0, s>>>(tail, f...);
+  if (nb > 0) gemm_fixup_kernel<TAIL, F...><<<nb, 256, 0, s>>>(tail, 0, f...);
+}
+// the same with `head` of the tail blocks first in the grid
+template <class TAIL, class... F>
+static inline void gemm_fixup_launch_h(int head, int tail_blocks, const TAIL& tail, hipStream_t s, const F&... f) {
+  const int nb = (gemm_fix_blocks(f) + ... + 0) + tail_blocks;
+  if (nb > 0) gemm_fixup_kernel<TAIL, F...><<<nb, 256, 0, s>>>(tail, head, f...);
 }
 
 }  // namespace tgnx

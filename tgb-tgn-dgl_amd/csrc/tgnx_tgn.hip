@@ -203,6 +203,13 @@ struct Ctx {
   // = its run count.  pplan = 1: one workgroup per plan, runs at [0, U].
   int pplan;
   int *rpc, *rpo, *spc, *spo;
+  // the fixup's copy of what the next batch's scan rewrites (it runs beside the fixup, SnapJob below):
+  // ctl words, counts, update list; errw = the live error word (the fixup's view reads ctl from the copy)
+  int64_t* snap_ctl;
+  int* snap_cnt;
+  int64_t* snap_upd;
+  int* snap_upd_loc;
+  int64_t* errw;
   int Bmax, Qcap, Rcap, Mcap, Ecap, Ucap, tgp_rows;
   Lay L;
   // ---- 2-hop (layers = 2).  The arrays above then describe the OUTER sample: centres = the 1-hop node
@@ -266,7 +273,7 @@ __device__ __forceinline__ void mark_node(uint32_t* bm, uint32_t* sum, int64_t v
 // src / pos nodes are stamped for the update list (memory_module.py:129).  16 lanes per entry, one
 // ring slot each (all slot loads in flight at once); the entry's valid-slot count goes to kval[v].
 template <class AT = NoCheckpoint>
-__device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh, AT at = AT{});
+__device__ __forceinline__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh, AT at = AT{});
 // The resident step's batch descriptor, from the step counters (tgnn_advance mode 1 restated): the
 // batch `ahead` batches past the counters' one.  Every block derives it itself; the scan launch writes it
 // into ctl for the later launches (TGNX_CTL_BATCH_START .. SEED).  The pipelined step marks the next
@@ -457,7 +464,7 @@ __global__ void __launch_bounds__(256) tgn_mark(Ctx c, int nmark) {
 // (memory_module.py:188-191 with a stable sort): plan_part(which = 1) below.
 
 template <class AT>
-__device__ void store_plan_block(const Ctx& c, int B, int64_t start, unsigned char* smem, int* sh, AT at) {
+__device__ __forceinline__ void store_plan_block(const Ctx& c, int B, int64_t start, unsigned char* smem, int* sh, AT at) {
   const int n2 = 2 * B, n = next_pow2(n2);
   uint64_t* key = reinterpret_cast<uint64_t*>(smem);
   int* runs = reinterpret_cast<int*>(smem + (size_t)n * 8);
@@ -536,7 +543,7 @@ __host__ __device__ inline size_t tgn_scan_smem(int Bmax) {
 // sort only those: P sorts of ~2B / P keys in parallel instead of one of 2B (a data-parallel step plans
 // the whole global batch; sorting 3,200 keys took one workgroup 49 us).
 template <class AT>
-__device__ void plan_part(const Ctx& c, int which, int part, int P, int B, int64_t start, unsigned char* smem, int* sh,
+__device__ __forceinline__ void plan_part(const Ctx& c, int which, int part, int P, int B, int64_t start, unsigned char* smem, int* sh,
                           AT at) {
   const int tid = threadIdx.x, T = blockDim.x, n2 = 2 * B;
   const int64_t* src = c.ev_src + start;
@@ -648,7 +655,7 @@ __device__ void plan_part(const Ctx& c, int which, int part, int P, int B, int64
   }
 }
 template <class AT>
-__device__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh, AT at) {
+__device__ __forceinline__ void plan_blocks(const Ctx& c, int which, int B, int64_t start, unsigned char* smem, int* sh, AT at) {
   // blocks [0, pplan): ring-plan partitions; [pplan, 2 pplan): store-plan partitions.  One partition (a
   // world-1 batch): the single-workgroup plans (their keys come straight from the events, no compaction)
   const int P = c.pplan;
@@ -695,10 +702,10 @@ __device__ __forceinline__ int plan_runs(const int* pc, int P) {
 // nodes (+ assoc, centre ranks); WG1 / WG2 the batch's ring-insert / message-store plans (they read only
 // the batch's events).  Resident train steps: every workgroup takes the batch from the step counters
 // and WG0 writes the descriptor into ctl for the later launches (no workgroup of this launch reads it).
-template <bool TRAIN>
-__global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
-  TGNX_STAMP(2);
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// scan_body: workgroup `role` of it (0: walks, 1 .. 2 pplan: plans), any workgroup size T with the
+// graph's bitmap words <= 2 T when scan_direct (scan_folds), LDS at smem (tgn_scan_smem)
+template <bool TRAIN, class AT>
+__device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char* smem, AT at) {
   __shared__ int sh[40];
   const int tid = threadIdx.x, T = blockDim.x;
   int B, gen;
@@ -708,7 +715,7 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
     B = d.B;
     start = d.start;
     gen = d.gen;
-    if (blockIdx.x == 0 && tid == 0) {
+    if (role == 0 && tid == 0) {
       c.ctl[TGNX_CTL_BATCH_START] = d.start;
       c.ctl[TGNX_CTL_B] = d.B;
       c.ctl[TGNX_CTL_CUR_EID] = d.start;
@@ -722,8 +729,8 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
     gen = (int)c.ctl[TGNX_CTL_GEN];
   }
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  if (blockIdx.x >= 1) {
-    plan_blocks(c, (int)blockIdx.x - 1, B, start, smem, sh, [&](int slot) { TGNX_STAMP_AT(slot); });
+  if (role >= 1) {
+    plan_blocks(c, role - 1, B, start, smem, sh, at);
     return;
   }
   // pass 0: the words each thread walks.  Small graphs (<= 2 words per thread): contiguous word ranges
@@ -846,18 +853,19 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
   // offsets and the update list (memory_module.py:129 src ∪ dst, sorted)
   const int xc = (R + T - 1) / T, x0 = min(R, tid * xc), x1 = min(R, x0 + xc);
   int ne = 0, nu = 0;
-  if (lds_c && xc <= 2) {  // the chunk's (<= 2) centres in registers across the block scan
-    int64_t v[2] = {0, 0};
-    int loc[2] = {0, 0}, kv[2] = {0, 0};
-    bool up[2] = {false, false};
+  constexpr int XR = 4;
+  if (lds_c && xc <= XR) {  // the chunk's (<= 4) centres in registers across the block scan
+    int64_t v[XR] = {};
+    int loc[XR] = {}, kv[XR] = {};
+    bool up[XR] = {};
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < XR; ++j)
       if (x0 + j < x1) {
         v[j] = lv[x0 + j];
         loc[j] = lloc[x0 + j];
       }
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < XR; ++j)
       if (x0 + j < x1) {
         kv[j] = c.kval[v[j]];
         up[j] = c.node_gen[v[j]] == gen;
@@ -867,7 +875,7 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
     int E, U, re, ru;
     block_excl_scan2(ne, nu, sh, &re, &ru, &E, &U);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < XR; ++j)
       if (x0 + j < x1) {
         const int x = x0 + j;
         c.ceoff[x] = re;
@@ -967,6 +975,12 @@ __global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
     c.cnt[CNT_R1] = R1;
     c.cnt[CNT_E1] = E1;
   }
+}
+template <bool TRAIN>
+__global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
+  TGNX_STAMP(2);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  scan_body<TRAIN>(c, (int)blockIdx.x, smem, [&](int slot) { TGNX_STAMP_AT(slot); });
 }
 
 // ------------------------------------------------------------------ messages (memory_module.py:152-207)
@@ -2761,7 +2775,7 @@ struct TeReduceTail {
   int rows_edge, rows_msg;
   // tail block b: columns [64 b, 64 b + 64) of the 2D (w, b) gradients; wave w sums the rows
   // [w R / 4, (w + 1) R / 4) with 8 loads in flight, the 4 wave sums combine in fixed order
-  __device__ void operator()(int bid) const {
+  __device__ __forceinline__ void operator()(int bid) const {
     __shared__ float red[4][64];
     const int D = c.D, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int x = bid * 64 + lane;
@@ -2858,7 +2872,7 @@ __device__ __forceinline__ void ring_merge_block(const Ctx& c, int blk, int B, i
 // [0, nmem): memory / last_update of the update list from the GRU rows (wave per node; train rows
 // are the sampled nodes' rows via assoc, eval / flush rows are list positions);
 // [nmem, nmem + nst): message stores of the batch; the rest: ring merge, wave per node run.
-__device__ void update_body(const Ctx& c, int blk, int nmem, int nst, int mem_mode, const int64_t* list,
+__device__ __forceinline__ void update_body(const Ctx& c, int blk, int nmem, int nst, int mem_mode, const int64_t* list,
                             const int* list_cnt, int n_host, int64_t base) {
   const int lane = threadIdx.x & 63;
   if (blk < nmem) {
@@ -2873,7 +2887,7 @@ __device__ void update_body(const Ctx& c, int blk, int nmem, int nst, int mem_mo
     const int n = list_cnt ? *list_cnt : n_host;
     float* xr = mem_mode == 0 ? c.xrows : nullptr;
     if (xr && n > c.xcap) {
-      if (blk == 0 && threadIdx.x == 0) c.ctl[TGNX_CTL_ERR] |= 8;
+      if (blk == 0 && threadIdx.x == 0) *c.errw |= 8;
       return;
     }
     for (int u = blk * 4 + (threadIdx.x >> 6); u < n; u += nmem * 4) {
@@ -2952,24 +2966,63 @@ __global__ void __launch_bounds__(256) tgn_update(Ctx c, int nmem, int nst, int 
   update_body(c, blockIdx.x, nmem, nst, mem_mode, list, list_cnt, n_host, base);
 }
 
-// tail blocks of the train step's fixup launch: the Δt-encoding reduction (nte blocks), then
-// update_state + ring insert (update_body: nothing in the fixup reads memory, stores or the ring)
+// the message-store half of update_state, riding in the launch before the fixup (dW_gru ‖ dX_enc):
+// nothing after tgn_agg_emit reads the stores
+struct StoreJob {
+  Ctx c;
+  int nst;
+  __device__ void operator()(int bid, float*) const { update_body(c, bid, 0, nst, 0, nullptr, nullptr, 0, 0); }
+};
+// One block in the same launch: copies what the fixup reads of the step descriptor (ctl words, counts,
+// update list) for fixup_view — the pipelined step's next-batch scan runs inside the fixup launch and
+// rewrites them — then advances the resident step counters (what tgnn_advance did at the start of the
+// step; after this launch only the next batch's scan reads them).
+struct SnapJob {
+  Ctx c;
+  __device__ void operator()(int, float*) const {
+    const int tid = threadIdx.x, U = min(c.cnt[CNT_U], c.Ucap);
+    for (int i = tid; i < TGNX_CTL_WORDS; i += blockDim.x) c.snap_ctl[i] = c.ctl[i];
+    for (int i = tid; i < CNT_WORDS; i += blockDim.x) c.snap_cnt[i] = c.cnt[i];
+    for (int i = tid; i < U; i += blockDim.x) {
+      c.snap_upd[i] = c.upd[i];
+      c.snap_upd_loc[i] = c.upd_loc[i];
+    }
+    if (!c.adv) return;  // (block-uniform)
+    __syncthreads();
+    if (tid == 0) {
+      int64_t* ctl = c.ctl;
+      ctl[TGNX_CTL_GEN] += 1;
+      ctl[TGNX_CTL_NB] += 1;
+      ctl[TGNX_CTL_STEP_B] = ctl[TGNX_CTL_B];
+      if (ctl[TGNX_CTL_B] > 0) ctl[TGNX_CTL_ADAM_T] += 1;
+    }
+  }
+};
+static_assert(TGNX_PIPE_MARK_AT != 9, "the next batch's marking reads the step counters SnapJob advances");
+// the fixup launch's Ctx: SnapJob's copies in place of the live descriptor
+static inline Ctx fixup_view(const Ctx& c) {
+  Ctx f = c;
+  f.ctl = c.snap_ctl;
+  f.cnt = c.snap_cnt;
+  f.upd = c.snap_upd;
+  f.upd_loc = c.snap_upd_loc;
+  if (f.adf.p) f.adf.ctl = c.snap_ctl;
+  return f;
+}
+template <bool TRAIN, class AT>
+__device__ void scan_body(const Ctx& c, int role, unsigned char* smem, AT at);
+// tail blocks of the train step's fixup launch: [0, nscan) the next batch's scan (pipelined steps whose
+// scan fits the launch's LDS and 256-thread workgroups, scan_folds; `nxt` = the live Ctx), then the
+// Δt-encoding reduction (nte blocks), then the memory / last_update half of update_state (nmem blocks;
+// nothing in the fixup reads memory).  te.c is the fixup's view (fixup_view).
 struct TrainTail {
   TeReduceTail te;
-  int nte, nmem, nst, ninc;  // ninc: index of the step-counter block (folded cursor), -1 without
-  __device__ void operator()(int bid) const {
-    if (bid == ninc) {  // what tgnn_advance did at the start of the step (no other block reads these)
-      if (threadIdx.x == 0) {
-        int64_t* ctl = te.c.ctl;
-        ctl[TGNX_CTL_GEN] += 1;
-        ctl[TGNX_CTL_NB] += 1;
-        ctl[TGNX_CTL_STEP_B] = ctl[TGNX_CTL_B];
-        if (ctl[TGNX_CTL_B] > 0) ctl[TGNX_CTL_ADAM_T] += 1;
-      }
-      return;
-    }
-    if (bid < nte) te(bid);
-    else update_body(te.c, bid - nte, nmem, nst, 0, te.c.upd, te.c.cnt + CNT_U, 0, 0);
+  Ctx nxt;
+  int nscan, nte, nmem;
+  __device__ __forceinline__ void operator()(int bid, float* smem) const {
+    if (bid < nscan) scan_body<true>(nxt, bid, reinterpret_cast<unsigned char*>(smem), NoCheckpoint{});
+    else if ((bid -= nscan) < nte) te(bid);
+    else update_body(te.c, bid - nte, nmem, 0, 0, te.c.upd, te.c.cnt + CNT_U, 0, 0);
   }
 };
 
@@ -3116,7 +3169,7 @@ static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_spli
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
       Ep, alpha, Zc, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
-      rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF, total;
+      snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF, total;
   int tgp_rows, tgp_e1;
 };
 static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
@@ -3184,6 +3237,7 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.skeys = carve(off, (size_t)n2 * 8);
   W.sruns = carve(off, (size_t)(n2 + 2 + TGNX_PLAN_PMAX) * 4);
   W.pcnt = carve(off, (size_t)4 * TGNX_PLAN_PMAX * 4);
+  W.snap = carve(off, (size_t)TGNX_CTL_WORDS * 8 + CNT_WORDS * 4 + (size_t)k.Ucap * 12);
   const bool two = k.layers == 2;
   const size_t R1 = two ? k.R1cap : 0, E1 = k.E1cap, R2 = two ? k.Rcap : 0;
   W.rb = carve(off, two ? words * 4 : 0);
@@ -3340,6 +3394,11 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.rpo = c.rpc + TGNX_PLAN_PMAX;
   c.spc = c.rpo + TGNX_PLAN_PMAX;
   c.spo = c.spc + TGNX_PLAN_PMAX;
+  c.snap_ctl = reinterpret_cast<int64_t*>(ws + W.snap);
+  c.snap_upd = c.snap_ctl + TGNX_CTL_WORDS;
+  c.snap_cnt = reinterpret_cast<int*>(c.snap_upd + k.Ucap);
+  c.snap_upd_loc = c.snap_cnt + CNT_WORDS;
+  c.errw = b->ctl + TGNX_CTL_ERR;
   c.pplan = plan_parts(k.B);
   c.Bmax = k.B;
   c.Qcap = k.Qcap;
@@ -3503,6 +3562,15 @@ struct AdvArgs {
 // scanned by the previous pipelined step; 2 = pipelined, mark + scan this batch first.  A pipelined step
 // marks the next batch inside tgn_pred_train and scans it after its own last launch.
 extern "C++" {  // (inside the extern "C" block: the cell-templated step)
+#ifndef TGNX_SCAN_FOLD
+#define TGNX_SCAN_FOLD 1  // pipelined step: the next batch's scan inside the fixup launch when it fits (0: own launch)
+#endif
+// the next batch's scan as 256-thread head workgroups of the fixup launch: its LDS within the launch's,
+// and (small graphs, walked directly) <= 2 bitmap words per thread
+static inline bool scan_folds(const Ctx& c, const Caps& k) {
+  return TGNX_SCAN_FOLD && tgn_scan_smem(k.B) <= (size_t)GEMM_FIX_SMEM * 4 && (size_t)3 * k.B * 12 <= (size_t)GEMM_FIX_SMEM * 4 &&
+         (!scan_direct(c.words) || c.words <= 2 * 256);
+}
 template <int CELL>
 static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
                              void* stream, bool fuse_adam, const AdvArgs* adv, int pipe) {
@@ -3656,7 +3724,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // partials of the sampled edges).  Jobs of one gemmN launch add up rather than overlap (measured:
   // the five backward jobs in one launch took 28 us, dz0 alone 16), while kv_reduce leaves most CUs
   // idle: the dE-only GEMMs fill them here instead of lengthening the dP launch below.
-  const EpiGradStore e_dWe{G, c.L.we, D + d, c.adf};
+  const Ctx cf = fixup_view(c);
+  const EpiGradStore e_dWe{G, c.L.we, D + d, cf.adf};
   probe_begin(TGNX_K_KV, s);
   gemmN_launch(s, mk_at(7), BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(k.Etr, KVR_CH, 1 << 20)},
                gemm_job<GW>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, EpiDeferred{}, c.pA),
@@ -3666,9 +3735,9 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   probe_end(TGNX_K_KV, s);
   TGNX_LAUNCH_CHECK("tgn_kv_reduce_dE");
   // weight gradients (deferred split-K) ‖ ...
-  const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D, c.adf};
-  const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D, c.adf};
-  const auto e_dWg = Cl::wgrad(c);
+  const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D, cf.adf};
+  const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D, cf.adf};
+  const auto e_dWg = Cl::wgrad(cf);
   // one launch: dW_proj, dW_src/dst (deferred split-K) ‖ dz0 = dP W with the GRU backward in its
   // epilogue — all read only what attn_bwd / kv_reduce / pred_train produced
   const int rows_edge = (k.Etr + G32::TM - 1) / G32::TM, rows_msg = (k.Mtr + G32::TM - 1) / G32::TM;
@@ -3681,7 +3750,9 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                              (float*)nullptr));
   probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
-  gemmN_launch(s, mk_at(9),
+  // ‖ the message stores ‖ the fixup's descriptor copy + the counter advance (SnapJob)
+  const int nst = gridn(2 * k.B, 256);
+  gemmN_launch(s, mk_at(9), BlockJob<SnapJob>{SnapJob{c}, 1}, BlockJob<StoreJob>{StoreJob{c, nst}, nst},
                gemm_job<GW>(shp_dWg(k, c.cnt), LoadKRow{c.dG, Cl::G * D, k.Mtr, Cl::G * D},
                             LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{}, c.pD),
                gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, Cl::G * D, c.cnt + CNT_M),
@@ -3689,26 +3760,30 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                               EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge},
                               (float*)nullptr));
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
-  // split-K sums + epilogues ‖ Δt reduction ‖ update_state (train order: memory of src ∪ dst from
-  // this step's GRU rows, then the stores), one launch (the ring insert ran beside the GRU)
+  // split-K sums + epilogues ‖ Δt reduction ‖ update_state's memory half (train order: memory of src ∪
+  // dst from this step's GRU rows; the stores and the ring insert ran in earlier launches), reading the
+  // step descriptor from SnapJob's copy (cf) — so that the pipelined step's next-batch scan (counters
+  // advanced by SnapJob) rides in the same launch as its first workgroups when it fits (scan_folds)
   const int nte = (2 * D + 63) / 64;
-  const int nmem = gridn(k.Ucap, 4, 1024), nst = gridn(2 * k.B, 256);
-  const int ninc = c.adv ? nte + nmem + nst : -1;
-  const TrainTail tail{TeReduceTail{c, rows_edge, rows_msg}, nte, nmem, nst, ninc};
+  const int nmem = gridn(k.Ucap, 4, 1024);
+  const bool scan_next = pipe && !no_tail;
+  const bool fold = scan_next && scan_folds(c, k);
+  const int nscan = fold ? 1 + 2 * c.pplan : 0;
+  const TrainTail tail{TeReduceTail{cf, rows_edge, rows_msg}, c, nscan, nte, nmem};
   probe_begin(TGNX_K_FINISH, s);
   if (two)
-    gemm_fixup_launch(nte + nmem + nst + (c.adv ? 1 : 0), tail, s, gemm_fix<GW>(shp_dWe(k, c.cnt), c.pA, e_dWe),
-                      gemm_fix<GW>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
-                      gemm_fix<GW>(shp_dWg(k, c.cnt), c.pD, e_dWg),
-                      gemm_fix<GW>(shp_dWp2(k, c.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC, c.adf}),
-                      gemm_fix<GW>(shp_dWe2(k, c.cnt), c.pF, EpiGradStore{G, c.L.we2, D + d, c.adf}));
+    gemm_fixup_launch_h(nscan, nscan + nte + nmem, tail, s, gemm_fix<GW>(shp_dWe(k, cf.cnt), c.pA, e_dWe),
+                        gemm_fix<GW>(shp_dWp(k, cf.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(k, cf.cnt), c.pC, e_dWlp),
+                        gemm_fix<GW>(shp_dWg(k, cf.cnt), c.pD, e_dWg),
+                        gemm_fix<GW>(shp_dWp2(k, cf.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC, cf.adf}),
+                        gemm_fix<GW>(shp_dWe2(k, cf.cnt), c.pF, EpiGradStore{G, c.L.we2, D + d, cf.adf}));
   else
-    gemm_fixup_launch(nte + nmem + nst + (c.adv ? 1 : 0), tail, s, gemm_fix<GW>(shp_dWe(k, c.cnt), c.pA, e_dWe),
-                      gemm_fix<GW>(shp_dWp(k, c.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(k, c.cnt), c.pC, e_dWlp),
-                      gemm_fix<GW>(shp_dWg(k, c.cnt), c.pD, e_dWg));
+    gemm_fixup_launch_h(nscan, nscan + nte + nmem, tail, s, gemm_fix<GW>(shp_dWe(k, cf.cnt), c.pA, e_dWe),
+                        gemm_fix<GW>(shp_dWp(k, cf.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(k, cf.cnt), c.pC, e_dWlp),
+                        gemm_fix<GW>(shp_dWg(k, cf.cnt), c.pD, e_dWg));
   probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgn_fixup_update");
-  if (pipe && !no_tail) {  // the next batch (counters advanced by the fixup): sorted node sets, plans, descriptor
+  if (scan_next && !fold) {  // the next batch (counters advanced by SnapJob): sorted node sets, plans, descriptor
     probe_begin(TGNX_K_ASSEMBLE, s);
     tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
     probe_end(TGNX_K_ASSEMBLE, s);
