@@ -123,7 +123,7 @@ int64_t tgnx_stamps_count(void);
  * U_e = attn_e·W_e, U_{l,r} = attn_{l,r}·W_n reach the output (ft is [N,H,1],
  * :560-563), so the embedding is drop(mem) + (1/H)·Σ_h ft_h.
  *
- * ctl is a device int64[16] control block (see TGNX_CTL_*); every kernel of a
+ * ctl is a device int64[TGNX_CTL_WORDS] (24) control block (see TGNX_CTL_*); every kernel of a
  * step reads the batch geometry from it, so a step can be replayed from a
  * HIP graph.  The model's parameters live in one flat fp32 buffer laid out by
  * tgnx_tgnn_param_layout (names = the reference's state_dict keys).
@@ -401,8 +401,13 @@ int tgnx_tgn_train_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* bu
  * order (store, then GRU update) and the ring insert. */
 int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t Kn, void* stream);
 /* train(False): update the memory of every node from its stored messages, clear the stores
- * (memory_module.py:209-215). */
-int tgnx_tgn_flush(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream);
+ * (memory_module.py:209-215).  Every row is computed from the pre-flush state (:212 updates arange(N) at
+ * once).  Graphs with more nodes than the workspace's GRU row capacity run in chunks that read a snapshot
+ * of memory / last_update: pass a 16-B aligned device scratch of tgnx_tgn_flush_scratch_bytes(cfg) bytes
+ * (0 when one chunk holds every node; scratch may then be NULL). */
+size_t tgnx_tgn_flush_scratch_bytes(const tgnx_tgn_config* cfg);
+int tgnx_tgn_flush(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* scratch, size_t scratch_bytes,
+                   void* stream);
 
 #ifdef __cplusplus
 }

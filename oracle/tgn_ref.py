@@ -118,10 +118,13 @@ class RefTGNMemory(nn.Module):
         self._reset_message_store()
 
     def _reset_message_store(self):                                    # :140-145
+        # every node starts with an empty store (:144-145); kept sparse here, an absent key reads as
+        # the empty tuple (so graphs of ~1M nodes reset in O(1))
         i = torch.empty((0,), dtype=torch.long)
         m = torch.empty((0, self.raw_msg_dim))
-        self.msg_s_store = {j: (i, i, i, m) for j in range(self.num_nodes)}
-        self.msg_d_store = {j: (i, i, i, m) for j in range(self.num_nodes)}
+        self._empty = (i, i, i, m)
+        self.msg_s_store = {}
+        self.msg_d_store = {}
 
     def forward(self, n_id):                                           # :116-124
         if self.training:
@@ -165,7 +168,7 @@ class RefTGNMemory(nn.Module):
             store[i] = (src[idx], dst[idx], t[idx], raw_msg[idx])
 
     def _compute_msg(self, n_id, store):                               # :193-207
-        data = [store[i] for i in n_id.tolist()]
+        data = [store[i] for i in n_id.tolist() if i in store] or [self._empty]
         src, dst, t, raw = (torch.cat(x, dim=0) for x in zip(*data))
         t_rel = t - self.last_update[src]
         t_enc = self.time_enc(t_rel.to(raw.dtype))

@@ -1,0 +1,266 @@
+"""GPU parity of the TGN memory path at the BASELINE.json config shapes (configs #3–#5) against the oracle
+restatement oracle/tgn_ref.py (parity unpinned for its torch_geometric / torch_scatter parts, see its
+header).  The small-graph tests (test_gpu_tgn.py) run N <= 9,227 and d in {8, 16, 172}; these run the
+code paths the larger configs select:
+
+  * graphs above 131,072 nodes: the summary-bitmap marking / scan (tgnx_tgn.hip scan_direct() false);
+  * d = 1 / d = 2: Q = 3D + d and D + d not multiples of 4, so the element-wise (non-vec4) GEMM loaders;
+  * unix-scale timestamps (~1e9, fp32 spacing 64 s): last_update int64 -> fp32 promotion in Δt
+    (memory_module.py:203 `t - self.last_update[src]`, emb_module.py:70 `last_update[src] - t`);
+  * review: MeanAggregator (config/TGN.yml mail_combine 'mean') with a hub source;
+  * comment: 2-hop attention at batch 600 (S = K + K² per root, partitioned plans);
+  * coin: data parallel, world 2 on one device, against world 1.
+
+Per step, as test_gpu_tgn.py: outputs 2e-5 abs, every gradient 2e-3 relative (L2), memory 1e-5 abs,
+last_update exact, parameters after Adam; then train(False) flush and a TGB-style eval batch (scores,
+per-event reciprocal ranks, eval-order update).  Parameters / moments / memory are resynchronised from
+the oracle after each compared step."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHIFT_INVARIANT = {"gnn.conv.lin_key.bias": "gnn.conv.lin_key.weight", "gnn.conv2.lin_key.bias": "gnn.conv2.lin_key.weight"}
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def _sync(ref, opt_ref, model, opt):
+    named = dict(ref.named_parameters())
+    with torch.no_grad():
+        for name in model.param_order:
+            o, n, _ = model._views[name]
+            p = named[name]
+            model.flat[o:o + n].copy_(p.detach().reshape(-1))
+            st = opt_ref.state.get(p, {})
+            if st:
+                opt.exp_avg[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                opt.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+        model.memory.memory.copy_(ref.memory.memory)
+        model.memory.last_update.copy_(ref.memory.last_update)
+
+
+def _oracle_parity(shape, N, B, d, aggr, layers, nb, kn, seed, D=100):
+    from oracle.sampler_ref import RefLastNeighborLoader
+    from oracle.tgn_ref import RefTGN, eval_step, mrr_per_event, train_step
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.synth import make_stream
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    s = make_stream(shape, seed=seed, num_events=B * (nb + 1), num_nodes=N, msg_dim=d)
+    assert float(s.t[0]) > 2 ** 24 or shape == "tgbl-wiki"   # unix-scale times for the TGB configs
+    torch.manual_seed(0)
+    ref = RefTGN(N, d, hidden=D, aggr=aggr, dropout=0.0, layers=layers)
+    opt_ref = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    dev = torch.device("cuda")
+    model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=kn, aggr=aggr, dropout=0.0,
+                     layers=layers)
+    model.load_reference_state(ref.state_dict())
+    opt = TgnAdam(model, 1e-3)
+    eng = TgnEngine(model, LastNeighborLoader(N, 10, device=dev), dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32),
+                    msg=s.msg), opt, dst_nodes=s.dst_nodes)
+    eng.reset_state()
+    lref = RefLastNeighborLoader(N, 10)
+    ev_t, ev_msg = torch.from_numpy(s.t.astype(np.float32)), torch.from_numpy(s.msg)
+    rng = np.random.default_rng(seed + 1)
+    named = dict(ref.named_parameters())
+    for st in range(nb):
+        sl = slice(st * B, (st + 1) * B)
+        src, pos = torch.from_numpy(s.src[sl]), torch.from_numpy(s.dst[sl])
+        neg = torch.from_numpy(rng.choice(s.dst_nodes, size=B))
+        loss, po, no = train_step(ref, opt_ref, lref, ev_t, ev_msg, src, pos, neg, ev_t[sl], ev_msg[sl])
+        pg, ng = eng.train_batch(st * B, B, neg=neg)
+        torch.cuda.synchronize()
+        eng.check()
+        assert torch.allclose(pg.cpu(), po, atol=2e-5), (st, float((pg.cpu() - po).abs().max()))
+        assert torch.allclose(ng.cpu(), no, atol=2e-5), (st, float((ng.cpu() - no).abs().max()))
+        assert abs(float(model.grad_flat[-1]) - loss) < 1e-5 * max(1.0, abs(loss))
+        g = model.grads_by_name()
+        for name in model.param_order:
+            if name in SHIFT_INVARIANT:
+                scale = float(named[SHIFT_INVARIANT[name]].grad.norm()) + 1e-12
+                assert float(g[name].norm()) < 1e-4 * scale and float(named[name].grad.norm()) < 1e-4 * scale
+                continue
+            r = _rel(g[name], named[name].grad)
+            assert r < 2e-3, (st, name, r)
+        assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5), \
+            (st, float((model.memory.memory.cpu() - ref.memory.memory).abs().max()))
+        assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update), st
+        live = lref.e_id >= 0
+        assert np.array_equal(eng.loader.e_id.cpu().numpy(), lref.e_id), st
+        assert np.array_equal(eng.loader.neighbors.cpu().numpy()[live], lref.neighbors[live]), st
+        _sync(ref, opt_ref, model, opt)
+    ref.memory.train(False)
+    eng.flush()
+    torch.cuda.synchronize()
+    assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5)
+    assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update)
+    sl = slice(nb * B, (nb + 1) * B)
+    src, pos = torch.from_numpy(s.src[sl]), torch.from_numpy(s.dst[sl])
+    negs = torch.from_numpy(rng.choice(s.dst_nodes, size=(B, kn)))
+    po, no = eval_step(ref, lref, ev_t, ev_msg, src, pos, negs, ev_t[sl], ev_msg[sl])
+    pg, ngm, rr = eng.eval_batch(nb * B, B, negs)
+    torch.cuda.synchronize()
+    eng.check()
+    assert torch.allclose(pg.cpu(), po, atol=2e-5), float((pg.cpu() - po).abs().max())
+    assert torch.allclose(ngm.cpu(), no, atol=2e-5), float((ngm.cpu() - no).abs().max())
+    # reciprocal ranks: exact unless a negative ties the positive within the score tolerance
+    ref_rr = mrr_per_event(po, no)
+    close = ((no - po.view(-1, 1)).abs() <= 4e-5).any(1).numpy()
+    assert np.allclose(rr.cpu().numpy()[~close], ref_rr[~close], atol=1e-6)
+    assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5)
+    assert torch.equal(model.memory.last_update.cpu(), ref.memory.last_update)
+
+
+def test_tgn_review_shape_mean_matches_oracle():
+    """BASELINE config #3: tgbl-review shape (N = 352,637, d = 1, bipartite with 1,000 destinations,
+    unix-scale t), D = 100, B = 200, MeanAggregator, 100 eval negatives."""
+    _oracle_parity("tgbl-review", N=352_637, B=200, d=1, aggr="mean", layers=1, nb=5, kn=100, seed=11)
+
+
+def test_tgn_coin_shape_matches_oracle():
+    """BASELINE config #4's per-GPU shape: tgbl-coin (N = 638,486, non-bipartite, d = 1), B = 200."""
+    _oracle_parity("tgbl-coin", N=638_486, B=200, d=1, aggr="last", layers=1, nb=4, kn=50, seed=12)
+
+
+def test_tgn_comment_shape_2hop_b600_matches_oracle():
+    """BASELINE config #5's per-step shape: tgbl-comment-like (non-bipartite, d = 2, unix-scale t) on
+    300,000 nodes (summary-bitmap path), 2-hop attention (layers = 2), batch 600."""
+    _oracle_parity("tgbl-comment", N=300_000, B=600, d=2, aggr="last", layers=2, nb=3, kn=10, seed=13)
+
+
+@pytest.mark.parametrize("shape,N,d,aggr,layers,B", [("tgbl-coin", 638_486, 1, "last", 1, 200),
+                                                    ("tgbl-review", 352_637, 1, "mean", 1, 200),
+                                                    ("tgbl-comment", 300_000, 2, "last", 2, 600)])
+def test_tgn_dp_world2_large_graph_matches_single(shape, N, d, aggr, layers, B):
+    """Data parallel at the large configs (BASELINE #4 coin DP; #5's 2-hop batch 600): two world = 2 rank
+    engines on one device run their event slices of the same global batches; the host sums their
+    exchange buffers (the all-reduce: gradients + the rank-owned memory-row slots); both apply them.
+    Against a world = 1 engine on the same batches with device negatives and attention dropout on, lr = 0
+    (parameters fixed, so memory / outputs / gradients compare step after step): outputs 1e-5, gradient
+    sum 1e-4 relative, last_update / stores / ring exact, memory 1e-5 abs, the two ranks' memory tables
+    bit-identical."""
+    from oracle.tgn_ref import RefTGN
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.synth import make_stream
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    D, nb = 100, 4
+    s = make_stream(shape, seed=21, num_events=B * nb, num_nodes=N, msg_dim=d)
+    torch.manual_seed(0)
+    sd = RefTGN(N, d, hidden=D, aggr=aggr, dropout=0.1, layers=layers).state_dict()
+    dev = torch.device("cuda")
+    ev = dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32), msg=s.msg)
+    engines = []
+    for rank, world in ((0, 1), (0, 2), (1, 2)):
+        model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=1, aggr=aggr, dropout=0.1,
+                         layers=layers)
+        model.load_reference_state(sd)
+        eng = TgnEngine(model, LastNeighborLoader(N, 10, device=dev), ev, TgnAdam(model, 0.0), dst_nodes=s.dst_nodes,
+                        seed=1234, rank=rank, world=world)
+        eng.reset_state()
+        engines.append(eng)
+    e1, r0, r1 = engines
+    for st in range(nb):
+        a = st * B
+        e1.train_batch(a, B, neg=None, dropout=True, update=True)
+        for r in (r0, r1):
+            r.train_batch(a, B, neg=None, dropout=True, update=False)
+        torch.cuda.synchronize()
+        for e in engines:
+            e.check()
+        for rk, r in enumerate((r0, r1)):
+            lo, hi = B * rk // 2, B * (rk + 1) // 2
+            assert torch.equal(r.neg_train[a + lo:a + hi], e1.neg_train[a + lo:a + hi]), (st, rk)
+            assert torch.allclose(r.out_pos[lo:hi], e1.out_pos[lo:hi], atol=1e-5), (st, rk)
+            assert torch.allclose(r.out_neg[lo:hi], e1.out_neg[lo:hi], atol=1e-5), (st, rk)
+        gsum = r0.model.grad_flat + r1.model.grad_flat
+        g1 = e1.model.grad_flat
+        for name in e1.model.param_order:
+            if name.endswith("lin_key.bias"):
+                continue
+            o, n, _ = e1.model._views[name]
+            rel = float((gsum[o:o + n] - g1[o:o + n]).norm() / (g1[o:o + n].norm() + 1e-12))
+            assert rel < 1e-4, (st, name, rel)
+        assert abs(float(gsum[-1]) - float(g1[-1])) < 1e-5
+        tot = r0.comm + r1.comm                       # the all-reduce
+        for r in (r0, r1):
+            r.comm.copy_(tot)
+            r.apply_update(allreduce=False)
+        torch.cuda.synchronize()
+        assert torch.equal(r0.model.memory.memory, r1.model.memory.memory), st
+        assert torch.equal(r0.model.memory.last_update, e1.model.memory.last_update), st
+        assert torch.allclose(r0.model.memory.memory, e1.model.memory.memory, atol=1e-5), \
+            (st, float((r0.model.memory.memory - e1.model.memory.memory).abs().max()))
+        assert torch.equal(r0.model.store, e1.model.store), st
+        assert torch.equal(r0.loader.neighbors, e1.loader.neighbors) and torch.equal(r0.loader.e_id, e1.loader.e_id)
+
+
+@pytest.mark.parametrize("shape,N,d,aggr,layers,B", [("tgbl-review", 352_637, 1, "mean", 1, 200),
+                                                    ("tgbl-wiki", 9_227, 172, "mean", 1, 300),
+                                                    ("tgbl-comment", 300_000, 2, "last", 2, 600)])
+def test_tgn_pipelined_equals_resident_large(shape, N, d, aggr, layers, B):
+    """The bench's step (tgnx_tgn_train_step_pipelined: the next batch marked inside the k / v launch and
+    scanned in the fixup launch) against tgnx_tgn_train_step_resident on a twin engine, at the shapes the
+    published numbers use: MeanAggregator (tgn_agg_emit<-1> + the next batch's marking), graphs above
+    131,072 nodes (summary bitmaps), batches of > 512 plan keys (partitioned plans) and 2-hop at B = 600.
+    Graph replay, device negatives, attention dropout, a partial last batch and a step past the split.
+    After every step: counters, ring and this batch's negatives exactly; outputs / parameters / memory
+    within the fused-Adam tolerances (resynchronised per step)."""
+    from oracle.tgn_ref import RefTGN
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.synth import make_stream
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    D, nb = 100, 5
+    s = make_stream(shape, seed=31, num_events=B * nb, num_nodes=N, msg_dim=d)
+    torch.manual_seed(0)
+    sd = RefTGN(N, d, hidden=D, aggr=aggr, dropout=0.1, layers=layers).state_dict()
+    dev = torch.device("cuda")
+    ev = dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32), msg=s.msg)
+    split_hi = (nb - 2) * B + B // 3
+    engines = []
+    for pipe in (True, False):
+        model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=1, aggr=aggr, dropout=0.1,
+                         layers=layers)
+        model.load_reference_state(sd)
+        opt = TgnAdam(model, 1e-3)
+        eng = TgnEngine(model, LastNeighborLoader(N, 10, device=dev), ev, opt, dst_nodes=s.dst_nodes, seed=5)
+        eng.pipeline = pipe
+        eng.bind_resident(0, split_hi, B, dropout=True)
+        eng.begin_epoch()
+        if pipe:
+            eng.capture_resident()
+        engines.append((model, opt, eng))
+    (m1, o1, e1), (m2, o2, e2) = engines
+    for st in range(nb):                     # nb - 2 full batches, a partial one, one past the split
+        e1.replay_resident()
+        e2.resident_train_step()
+        torch.cuda.synchronize()
+        e1.check()
+        e2.check()
+        for w in (3, 4, 10):
+            assert int(e1.ctl[w]) == int(e2.ctl[w]), (st, w, int(e1.ctl[w]), int(e2.ctl[w]))
+        Bst, start = int(e2.ctl[2]), int(e2.ctl[0])
+        assert torch.equal(e1.neg_train[:start + Bst], e2.neg_train[:start + Bst]), st
+        for a, b in ((e1.loader.neighbors, e2.loader.neighbors), (e1.loader.e_id, e2.loader.e_id),
+                     (e1.loader.t, e2.loader.t)):
+            assert torch.equal(a, b), st
+        if Bst:
+            assert torch.allclose(e1.out_pos[:Bst], e2.out_pos[:Bst], atol=1e-5), st
+            assert torch.allclose(e1.out_neg[:Bst], e2.out_neg[:Bst], atol=1e-5), st
+        for name in m1.param_order:
+            if name in SHIFT_INVARIANT:
+                continue
+            o, n, _ = m1._views[name]
+            assert _rel(m1.flat[o:o + n], m2.flat[o:o + n]) < 1e-4, (st, name)
+        assert torch.allclose(m1.memory.memory, m2.memory.memory, atol=1e-5), st
+        assert torch.equal(m1.memory.last_update, m2.memory.last_update), st
+        assert torch.equal(m1.store, m2.store), st
+        assert abs(e1.loss_sum() - e2.loss_sum()) <= 1e-5 * max(1.0, abs(e2.loss_sum())), st
+        with torch.no_grad():
+            m1.flat.copy_(m2.flat)
+            o1.exp_avg.copy_(o2.exp_avg)
+            o1.exp_avg_sq.copy_(o2.exp_avg_sq)
+            m1.memory.memory.copy_(m2.memory.memory)

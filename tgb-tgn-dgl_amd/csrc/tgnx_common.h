@@ -31,6 +31,15 @@ void set_error(const char* fmt, ...);
     }                                                                            \
   } while (0)
 
+#define TGNX_HIP_CHECK(call)                                                     \
+  do {                                                                           \
+    hipError_t _e = (call);                                                      \
+    if (_e != hipSuccess) {                                                      \
+      ::tgnx::set_error("%s: %s", #call, hipGetErrorString(_e));                 \
+      return TGNX_EHIP;                                                          \
+    }                                                                            \
+  } while (0)
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---------------------------------------------------------------- wave timeline stamps (diagnostic build)

@@ -3981,7 +3981,15 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   return TGNX_OK;
 }
 
-int tgnx_tgn_flush(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream) {
+size_t tgnx_tgn_flush_scratch_bytes(const tgnx_tgn_config* cfg) {
+  if (check_cfg(cfg)) return 0;
+  const Caps k = make_caps(cfg);
+  if (cfg->num_nodes <= k.Mcap) return 0;  // one chunk: every row is computed before any is written
+  return (size_t)(al4(cfg->num_nodes * (int64_t)cfg->mem_dim) * 4 + cfg->num_nodes * 8);
+}
+
+int tgnx_tgn_flush(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* scratch, size_t scratch_bytes,
+                   void* stream) {
   Ctx c;
   Caps k;
   WsLay W;
@@ -3989,9 +3997,27 @@ int tgnx_tgn_flush(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void
   if (rc) return rc;
   hipStream_t s = as_stream(stream);
   const int chunk = k.Mcap;
+  // The reference updates every node from the state before the flush (memory_module.py:212,
+  // _update_memory(arange(N)): all rows computed, then written).  The workspace holds Mcap GRU rows, so
+  // graphs larger than that run in chunks; a later chunk's messages read the memory / last_update of
+  // their other endpoint, which an earlier chunk has already rewritten.  So the chunks read a snapshot
+  // of memory / last_update taken before the first write.
+  Ctx cr = c;
+  if (c.N > chunk) {
+    const size_t need = tgnx_tgn_flush_scratch_bytes(cfg);
+    TGNX_CHECK_ARG(scratch && scratch_bytes >= need && ((uintptr_t)scratch & 15) == 0,
+                   "tgnx_tgn_flush: num_nodes > the workspace's row capacity needs a 16-B aligned scratch of "
+                   "tgnx_tgn_flush_scratch_bytes(cfg) bytes");
+    float* snap_mem = reinterpret_cast<float*>(scratch);
+    int64_t* snap_lu = reinterpret_cast<int64_t*>(snap_mem + al4(c.N * (int64_t)c.D));
+    TGNX_HIP_CHECK(hipMemcpyAsync(snap_mem, c.mem, (size_t)c.N * c.D * 4, hipMemcpyDeviceToDevice, s));
+    TGNX_HIP_CHECK(hipMemcpyAsync(snap_lu, c.lu_buf, (size_t)c.N * 8, hipMemcpyDeviceToDevice, s));
+    cr.mem = snap_mem;
+    cr.lu_buf = snap_lu;
+  }
   for (int64_t base = 0; base < c.N; base += chunk) {
     const int n = (int)std::min<int64_t>(chunk, c.N - base);
-    gru_list(c, k, nullptr, nullptr, n, base, n, s);
+    gru_list(cr, k, nullptr, nullptr, n, base, n, s);
     TGNX_LAUNCH_CHECK("tgn_flush_gru");
     tgn_update<<<gridn(n, 4, 1024), 256, 0, s>>>(c, gridn(n, 4, 1024), 0, 1, nullptr, nullptr, n, base);
     TGNX_LAUNCH_CHECK("tgn_flush_write");

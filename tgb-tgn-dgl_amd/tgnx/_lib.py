@@ -51,7 +51,8 @@ SIGNATURES = {
     "tgnx_tgn_train_fwd_bwd_split": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64, c_i32, c_i32, c_vp]),
     "tgnx_tgn_scan_next": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64, c_vp]),
     "tgnx_tgn_eval_step": (ctypes.c_int, [P, P, c_i32, c_vp]),
-    "tgnx_tgn_flush": (ctypes.c_int, [P, P, c_vp]),
+    "tgnx_tgn_flush": (ctypes.c_int, [P, P, P, ctypes.c_size_t, c_vp]),
+    "tgnx_tgn_flush_scratch_bytes": (ctypes.c_size_t, [P]),
     "tgnx_tgn_apply_rows": (ctypes.c_int, [P, P, P, c_i64, c_vp]),
     "tgnx_tcsr_build_ws_bytes": (c_sz, [c_i64, c_i32]),
     "tgnx_tcsr_build": (ctypes.c_int, [P, P, P, c_i64, c_i64, c_i32, P, P, P, P, P, P, c_sz, c_vp]),

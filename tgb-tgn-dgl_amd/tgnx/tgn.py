@@ -370,7 +370,12 @@ class TgnEngine:
         """TGNMemory.train(False) (memory_module.py:209-215)."""
         self._prefetched = False
         b = self._buffers(0)
-        _lib.call("tgnx_tgn_flush", ctypes.byref(self.cfg), ctypes.byref(b), self._stream())
+        nb = int(_lib.lib().tgnx_tgn_flush_scratch_bytes(ctypes.byref(self.cfg)))
+        # graphs beyond one workspace chunk: a snapshot of memory / last_update, freed after the call
+        scratch = torch.empty(max(nb, 16), dtype=torch.uint8, device=self.dev) if nb else None
+        _lib.call("tgnx_tgn_flush", ctypes.byref(self.cfg), ctypes.byref(b), _p(scratch), nb, self._stream())
+        if scratch is not None:
+            self._flush_scratch = scratch   # alive until the stream has consumed it (next flush replaces it)
 
     # ------------------------------------------------------------------ steps
     def train_batch(self, start: int, B: int, neg=None, dropout: bool = True, update: bool = True):
