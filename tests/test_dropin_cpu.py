@@ -94,3 +94,32 @@ def test_product_fails_loudly_without_gpu():
     from tgnx.sampler import LastNeighborLoader
     with pytest.raises(RuntimeError, match="HIP device"):
         LastNeighborLoader(10, 3, device="cpu")
+
+
+def test_config_sections_select_the_tgn_model(tmp_path):
+    """pyg-mem-tgn.py:36,49 passes only gnn_param to getModel; tgnx's parse_config records the file so that
+    pyg_model_utils.getModel honours the memory section (config/TGN.yml:10-18: mail_combine, memory_update),
+    sampling.neighbor[0] and train.batch_size.  Host logic only (no model is built)."""
+    import yaml
+
+    from tgnx.data import config_of, parse_config
+    from tgnx.tgn import model_options
+    src = os.path.join(PKG, "config", "TGN.yml")
+    s, mem, g, tr = parse_config(src)
+    assert config_of(g)[1] is mem
+    assert model_options(g) == {"layers": 1, "aggr": "last", "updater": "gru", "ring": 10, "max_batch": 2000}
+    conf = yaml.safe_load(open(src))
+    conf["memory"][0].update(mail_combine="mean", memory_update="rnn")
+    conf["gnn"][0]["layer"] = 2
+    conf["sampling"][0]["neighbor"] = [20]
+    p = tmp_path / "c.yml"
+    yaml.safe_dump(conf, open(p, "w"))
+    s2, mem2, g2, tr2 = parse_config(str(p))
+    assert model_options(g2) == {"layers": 2, "aggr": "mean", "updater": "rnn", "ring": 20, "max_batch": 2000}
+    # a gnn dict that did not come from parse_config: only its own keys
+    assert model_options(dict(g2)) == {"layers": 2}
+    assert model_options(dict(g2), memory_param=dict(mem2)) == {"layers": 2, "aggr": "mean", "updater": "rnn"}
+    with pytest.raises(ValueError):
+        model_options(g2, memory_param=dict(mem2, mail_combine="max"))
+    with pytest.raises(NotImplementedError):
+        model_options(g2, memory_param=dict(mem2, type="none"))

@@ -63,3 +63,88 @@ def test_pyg_dropin_epoch(monkeypatch):
     # a second test() call does not flush again and scores the next split with the same state rules
     mrr2 = pe.test(model, data.msg, te, nl, ns, None, "cuda", opt, crit, ev, metric, "test")
     assert 0.0 < mrr2 <= 1.0
+
+
+def _write_cfg(path, mail_combine, batch):
+    import yaml
+    src = open(__import__("os").path.join(__import__("os").path.dirname(__file__), "..", "tgb-tgn-dgl_amd", "config",
+                                           "TGN.yml")).read()
+    conf = yaml.safe_load(src)
+    conf["memory"][0]["mail_combine"] = mail_combine
+    conf["train"][0]["epoch"] = 1
+    conf["train"][0]["batch_size"] = batch
+    with open(path, "w") as f:
+        yaml.safe_dump(conf, f)
+    return str(path)
+
+
+def test_reference_script_with_one_line_swap(tmp_path, monkeypatch):
+    """The reference's entry script (/root/reference/pyg-mem-tgn.py:16-63) with only its model import swapped
+    (:24 -> :25), run call for call through the shims: parse_config, getDataWithDependecyBlock,
+    NegLinkSamplerDest(unique destinations) without a device, LastNeighborLoader, getModel(d, dim_out, N,
+    device, gnn_param=gnn_param), getOptimizer, and epoch_utils.train / test (NOT pyg_epoch_utils: :19
+    keeps the DGL loop's import, which dispatches on the model dict).  The config says mail_combine 'mean';
+    the model must be the MeanAggregator TGN: a fresh getModel from the same gnn_param, on two batches
+    with injected negatives and dropout off, matches oracle RefTGN(aggr='mean') and not aggr='last'."""
+    monkeypatch.setenv("TGNX_SYNTH_EVENTS", "3000")
+    monkeypatch.setenv("TGNX_EVAL_NEGS", "20")
+    from dependencyGraph import dependecyAwareBatch as dab  # noqa: F401  (imported by the script, :17)
+    from epoch_utils import test, train
+    from neg_sampler import NegLinkSamplerDest
+    from neighbor_loader import LastNeighborLoader
+    from pyg_model_utils import getModel, getOptimizer
+    from utils import getDataWithDependecyBlock, parse_config
+    cfg = _write_cfg(tmp_path / "TGN_mean.yml", "mean", 200)
+    device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    sample_param, memory_param, gnn_param, train_param = parse_config(cfg)
+    data, train_dataloader, val_dataloader, test_dataloader, neg_sampler, evaluator, metric = \
+        getDataWithDependecyBlock("tgbl-wiki", train_param)
+    unique_destination_nodes = torch.unique(data.dst)
+    neg_dest_sampler = NegLinkSamplerDest(unique_destination_nodes)
+    assoc = torch.empty(data.num_nodes, dtype=torch.long, device=device)
+    neighbor_loader = LastNeighborLoader(data.num_nodes, size=sample_param["neighbor"][0], device=device)
+    model = getModel(data.msg.shape[1], gnn_param["dim_out"], data.num_nodes, device, gnn_param=gnn_param)
+    optimizer = getOptimizer(model, train_param["lr"])
+    criterion = torch.nn.BCEWithLogitsLoss()
+    m = model["model"]
+    assert set(model) >= {"memory", "gnn", "link_pred"}
+    assert m.cfg.aggr == 1 and m.layers == 1 and m.updater == "gru" and m.cfg.max_batch == 200 and m.cfg.ring == 10
+    for e in range(train_param["epoch"]):
+        loss = train(model, data.msg, train_dataloader, neighbor_loader, neg_dest_sampler, assoc, device, optimizer,
+                     criterion)
+        assert np.isfinite(loss) and loss > 0
+        mrr = test(model, data.msg, val_dataloader, neighbor_loader, neg_sampler, assoc, device, optimizer, criterion,
+                   evaluator, metric, "val")
+        assert 0.0 < mrr <= 1.0
+    assert m._tgnx_engine.loss_sum() > 0
+
+    # the selection is the MeanAggregator: oracle parity with aggr='mean' (and a mismatch with 'last')
+    from oracle.sampler_ref import RefLastNeighborLoader
+    from oracle.tgn_ref import RefTGN, train_step
+    from tgnx.tgn import TgnEngine
+    N, d, D, B = data.num_nodes, data.msg.shape[1], gnn_param["dim_out"], 200
+    torch.manual_seed(0)
+    refs = {a: RefTGN(N, d, hidden=D, aggr=a, dropout=0.0) for a in ("mean", "last")}
+    refs["last"].load_state_dict(refs["mean"].state_dict())
+    m2 = getModel(d, D, N, device, gnn_param=gnn_param, dropout=0.0)
+    m2["model"].load_reference_state(refs["mean"].state_dict())
+    e2 = TgnEngine(m2["model"], LastNeighborLoader(N, 10, device=device),
+                   dict(src=data.src, dst=data.dst, t=data.t.float(), msg=data.msg.float()), getOptimizer(m2, 1e-4),
+                   dst_nodes=unique_destination_nodes)
+    e2.reset_state()
+    opts = {a: torch.optim.Adam(r.parameters(), lr=1e-4) for a, r in refs.items()}
+    lrefs = {a: RefLastNeighborLoader(N, 10) for a in refs}
+    ev_t, ev_msg = data.t.float(), data.msg.float()
+    rng = np.random.default_rng(3)
+    diff_last = 0.0
+    for st in range(3):
+        sl = slice(st * B, (st + 1) * B)
+        neg = torch.from_numpy(rng.choice(unique_destination_nodes.numpy(), size=B))
+        pg, ng = e2.train_batch(st * B, B, neg=neg)
+        torch.cuda.synchronize()
+        outs = {a: train_step(refs[a], opts[a], lrefs[a], ev_t, ev_msg, data.src[sl], data.dst[sl], neg, ev_t[sl],
+                              ev_msg[sl]) for a in refs}
+        _, po, no = outs["mean"]
+        assert torch.allclose(pg.cpu(), po, atol=2e-5) and torch.allclose(ng.cpu(), no, atol=2e-5), st
+        diff_last = max(diff_last, float((pg.cpu() - outs["last"][1]).abs().max()))
+    assert diff_last > 1e-3   # the two aggregations differ on this stream: the match above selects 'mean'

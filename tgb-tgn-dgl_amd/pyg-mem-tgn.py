@@ -29,11 +29,12 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--path", choices=["dgl", "pyg"], default="dgl", help="#change based on dgl/pyg")
     args = ap.parse_args()
+    # the reference's imports (pyg-mem-tgn.py:16-25): epoch_utils for both paths (it hands a TGN model to the
+    # PyG loop), the model module per the "#change based on dgl/pyg" swap
+    from epoch_utils import test, train
     if args.path == "dgl":
-        from epoch_utils import test, train
         from model_utils import getModel, getOptimizer
     else:
-        from pyg_epoch_utils import test, train
         from pyg_model_utils import getModel, getOptimizer
 
     device = torch.device("cuda")
@@ -45,12 +46,9 @@ def main():
     neg_dest_sampler = NegLinkSamplerDest(torch.unique(data.dst), device=device)
     neighbor_loader = LastNeighborLoader(data.num_nodes, size=sample_param["neighbor"][0], device=device)
     assoc = torch.empty(data.num_nodes, dtype=torch.long, device=device)
-    if args.path == "dgl":
-        model = getModel(data.msg.shape[1], gnn_param["dim_out"], data.num_nodes, device, gnn_param=gnn_param,
-                         ring=sample_param["neighbor"][0], max_batch=train_param["batch_size"])
-    else:
-        model = getModel(data.msg.shape[1], gnn_param["dim_out"], data.num_nodes, device,
-                         ring=sample_param["neighbor"][0], max_batch=train_param["batch_size"])
+    # pyg-mem-tgn.py:49: the config's other sections (memory.mail_combine / memory_update, neighbor,
+    # batch_size) reach the model through gnn_param (tgnx parse_config records the file)
+    model = getModel(data.msg.shape[1], gnn_param["dim_out"], data.num_nodes, device, gnn_param=gnn_param)
     optimizer = getOptimizer(model, train_param["lr"])
     criterion = torch.nn.BCEWithLogitsLoss()
     t_start = time.time()

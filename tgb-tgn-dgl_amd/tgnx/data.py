@@ -30,10 +30,25 @@ from .synth import SHAPES, eval_negatives, make_stream
 from .tgb_io import load_tgb, uniform_negatives
 
 
+# sections of the configs parse_config returned, by the identity of their gnn section: the reference's
+# script passes only gnn_param to getModel (pyg-mem-tgn.py:36,49), so pyg_model_utils.getModel finds the
+# memory / sampling / train sections of the same file through it (memory.mail_combine, memory_update)
+_PARSED = {}
+
+
 def parse_config(f):
     """utils.py:17-23."""
-    conf = yaml.safe_load(open(f, "r"))
-    return conf["sampling"][0], conf["memory"][0], conf["gnn"][0], conf["train"][0]
+    with open(f, "r") as fh:
+        conf = yaml.safe_load(fh)
+    out = conf["sampling"][0], conf["memory"][0], conf["gnn"][0], conf["train"][0]
+    _PARSED[id(out[2])] = out
+    return out
+
+
+def config_of(gnn_param):
+    """(sampling, memory, gnn, train) of the parse_config call that returned this gnn section, or None."""
+    got = _PARSED.get(id(gnn_param))
+    return got if got is not None and got[2] is gnn_param else None
 
 
 def block_ids(src: np.ndarray, dst: np.ndarray, batch: int) -> np.ndarray:

@@ -11,6 +11,9 @@ dropout (0.6) is active in the first epoch only (:20, :170-172); negatives are t
 to the batch's shortest list (:48-56); the eval predictor pairs negative row r with source
 r mod B (model_utils.py:192).
 
+A {'memory', 'gnn', 'link_pred'} model (pyg_model_utils.getModel, the import swap at pyg-mem-tgn.py:23-25)
+is handed to the PyG TGN loop (tgnx/tgn_epoch.py), so the reference script keeps its epoch_utils import.
+
 With a tgnx SplitLoader the whole split is resident in HBM and each batch is a few C-ABI
 calls with no host synchronisation; any other iterable of batch dicts is copied per batch.
 """
@@ -52,7 +55,17 @@ def _ap_auc(pos: np.ndarray, neg: np.ndarray):
     return average_precision_score(y, p), roc_auc_score(y, p)
 
 
+def _is_tgn(model) -> bool:
+    """A {'memory', 'gnn', 'link_pred'} dict: pyg_model_utils.getModel (the import swap at
+    pyg-mem-tgn.py:23-25), trained by the PyG TGN loop (tgnx/tgn_epoch.py)."""
+    return isinstance(model, dict) and "memory" in model and "link_pred" in model
+
+
 def train(model, feats, train_loader, neighbor_loader, neg_dest_sampler, assoc, device, optimizer, criterion):
+    if _is_tgn(model):
+        from . import tgn_epoch
+        return tgn_epoch.train(model, feats, train_loader, neighbor_loader, neg_dest_sampler, assoc, device,
+                               optimizer, criterion)
     gnn, eng = _engine(model, feats, neighbor_loader, optimizer, neg_dest_sampler)
     neighbor_loader.reset_state()                       # epoch_utils.py:175
     eng.reset_loss()
@@ -94,6 +107,10 @@ def train(model, feats, train_loader, neighbor_loader, neg_dest_sampler, assoc, 
 @torch.no_grad()
 def test(model, feats, loader, neighbor_loader, neg_sampler, assoc, device, optimizer, criterion, evaluator,
          metric, split_mode):
+    if _is_tgn(model):
+        from . import tgn_epoch
+        return tgn_epoch.test(model, feats, loader, neighbor_loader, neg_sampler, assoc, device, optimizer, criterion,
+                              evaluator, metric, split_mode)
     gnn = model["gnn"] if isinstance(model, dict) else model
     gnn.eval()                                           # epoch_utils.py:20 (never undone: reference quirk)
     perf = []

@@ -201,6 +201,15 @@ class FusedAdam(torch.optim.Optimizer):
 
 
 def getModel(feature_dim, hidden_dim, num_nodes, device, gnn_param=None, **kw):
+    """model_utils.py:700-707.  When gnn_param came from tgnx's parse_config, the sampler width and the
+    batch capacity default to the same file's sampling.neighbor[0] and train.batch_size."""
+    from .data import config_of
+    got = config_of(gnn_param) if gnn_param is not None else None
+    if got is not None:
+        if got[0].get("neighbor"):
+            kw.setdefault("ring", int(got[0]["neighbor"][0]))
+        if "batch_size" in got[3]:
+            kw.setdefault("max_batch", int(got[3]["batch_size"]))
     if gnn_param is not None:
         gnn = TGNN(feature_dim, gnn_param["dim_out"], num_nodes, device, num_heads=gnn_param["att_head"],
                    layers=gnn_param["layer"], **kw)

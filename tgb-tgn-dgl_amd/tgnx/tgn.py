@@ -562,12 +562,56 @@ class TgnEngine:
             raise RuntimeError(f"tgnx TGN step error flags {err:#x} (batch or sampled set beyond capacity)")
 
 
-def getModel(feature_dim, hidden_dim, num_nodes, device, num_events=None, **kw):
-    """pyg_model_utils.py:10-36.  num_events (optional) pre-sizes the message-store arena; otherwise the
-    engine sizes it when it binds the event table.  Extra keywords: ring, max_batch, max_neg, aggr,
-    dropout, layers, updater = 'gru' | 'rnn' (TGNMemory memory_updater_cell), memory = 'tgn' | 'dyrep'
+# config/TGN.yml memory section -> the PyG TGN's modules (TGL key names; TGN.yml:10-18)
+MAIL_COMBINE = {"last": "last", "mean": "mean"}          # msg_agg.py LastAggregator / MeanAggregator
+MEMORY_UPDATE = {"gru": "gru", "rnn": "rnn"}             # memory_module.py:70-78 memory_updater_cell
+
+
+def model_options(gnn_param=None, memory_param=None, sample_param=None, train_param=None) -> dict:
+    """TGNModel keywords from config/TGN.yml sections (utils.parse_config order).  gnn: `layer` -> layers
+    (attention hops, 1 or 2); memory: `mail_combine` -> aggr, `memory_update` -> updater, `type` must be
+    'node' (TGL's 'none' is a memory-less model, not the TGN path); sampling: `neighbor[0]` -> ring;
+    train: `batch_size` -> max_batch.  When only gnn_param is given and it came from tgnx's parse_config
+    (as in pyg-mem-tgn.py:36,49), the other sections of the same file are used."""
+    from .data import config_of
+    if gnn_param is not None and memory_param is None:
+        got = config_of(gnn_param)
+        if got is not None:
+            sample_param = sample_param if sample_param is not None else got[0]
+            memory_param = got[1]
+            train_param = train_param if train_param is not None else got[3]
+    out = {}
+    if gnn_param is not None and "layer" in gnn_param:
+        out["layers"] = int(gnn_param["layer"])
+    if memory_param is not None:
+        typ = memory_param.get("type", "node")
+        if typ != "node":
+            raise NotImplementedError(f"memory.type {typ!r}: only 'node' memory (TGNMemory) is the TGN path")
+        mc = memory_param.get("mail_combine", "last")
+        if mc not in MAIL_COMBINE:
+            raise ValueError(f"memory.mail_combine must be 'last' or 'mean' (msg_agg.py), got {mc!r}")
+        mu = memory_param.get("memory_update", "gru")
+        if mu not in MEMORY_UPDATE:
+            raise ValueError(f"memory.memory_update must be 'gru' or 'rnn' (memory_module.py:70-78), got {mu!r}")
+        out["aggr"], out["updater"] = MAIL_COMBINE[mc], MEMORY_UPDATE[mu]
+    if sample_param is not None and sample_param.get("neighbor"):
+        out["ring"] = int(sample_param["neighbor"][0])
+    if train_param is not None and "batch_size" in train_param:
+        out["max_batch"] = int(train_param["batch_size"])
+    return out
+
+
+def getModel(feature_dim, hidden_dim, num_nodes, device, gnn_param=None, memory_param=None, num_events=None, **kw):
+    """pyg_model_utils.py:10-36 with the call of pyg-mem-tgn.py:49 (`gnn_param=`; the reference's own
+    getModel lacks it): hidden_dim is the memory / time / embedding width (gnn dim_out), and the config
+    sections select the model (model_options: layer, mail_combine, memory_update, neighbor, batch_size).
+    num_events (optional) pre-sizes the message-store arena; otherwise the engine sizes it when it binds
+    the event table.  Explicit keywords win over the config: ring, max_batch, max_neg, aggr, dropout,
+    layers, updater = 'gru' | 'rnn' (TGNMemory memory_updater_cell), memory = 'tgn' | 'dyrep'
     (DyRepMemory as the memory module, modules/memory_module.py:218-421; TGNModel)."""
-    m = TGNModel(num_nodes, num_events, feature_dim, hidden_dim, device, **kw)
+    opts = model_options(gnn_param, memory_param)
+    opts.update(kw)
+    m = TGNModel(num_nodes, num_events, feature_dim, hidden_dim, device, **opts)
     return {"memory": m.memory, "gnn": m.gnn, "link_pred": m.link_pred, "model": m}
 
 
