@@ -43,18 +43,74 @@ def block_ids(src, dst, batch):
     return out
 
 
+def _log(msg: str) -> None:
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def _cgroup_cpus():
+    """CPU quota of this process's cgroup (v2 cpu.max or v1 cfs quota / period), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                return max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def _cores() -> int:
+    """Host cores this process may use (the CPU baseline uses all of them): the affinity mask,
+    bounded by the cgroup's CPU quota (a GPU box's mask lists the whole machine while its quota is a share;
+    threads beyond the quota only time-slice)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    q = _cgroup_cpus()
+    return min(n, q) if q else n
+
+
+def _cpu_info() -> dict:
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    return {"cpu_model": _cpu_model(), "affinity_cpus": aff, "cgroup_cpu_quota": _cgroup_cpus()}
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _metric(dataset: str, model: str) -> str:
+    return (f"temporal edges/sec on {dataset} TGN (train step)" if model == "tgn" else
+            f"temporal edges/sec on {dataset} TGNN, running DGL block-loop path (train step)")
+
+
 def cpu_baseline(stream, B, budget_s=15.0, max_batches=40):
-    """Oracle (faithful per-block CPU restatement, the 'port') on the same stream, bounded sample."""
+    """Oracle (faithful per-block CPU restatement, the 'port') on the same stream, bounded sample; the
+    train epoch's time is extrapolated from it (stated in the sample)."""
     sys.path.insert(0, ROOT)
     from oracle import blocks_ref
     from oracle.epoch_ref import train_batch
     from oracle.sampler_ref import RefLastNeighborLoader
     from oracle.tgnn_ref import RefTGNN
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+    cores = _cores()
     torch.set_num_threads(cores)
     N, d = stream.shape.num_nodes, stream.shape.msg_dim
     torch.manual_seed(0)
@@ -77,14 +133,19 @@ def cpu_baseline(stream, B, budget_s=15.0, max_batches=40):
         if n > 0:                         # first batch (empty ring, allocator warm-up) excluded
             t_total += dt
         n += 1
+        _log(f"cpu_baseline (TGNN oracle) B={B}: batch {n} {dt:.2f} s")
     timed = max(n - 1, 1)
-    return {"value": round(timed * B / max(t_total, 1e-9), 2), "unit": "events/s", "cores": cores, "kind": "port",
+    rate = timed * B / max(t_total, 1e-9)
+    return {"value": round(rate, 2), "unit": "events/s", "cores": cores, "kind": "port", **_cpu_info(),
+            "epoch_s_extrapolated": round(stream.train_end / rate, 1),
             "sample": f"oracle per-block restatement (oracle/epoch_ref.py), train batches 2..{n} of the same "
-                      f"wiki-shaped stream, B={B}, K=10, dropout 0.6 (reference epoch 1), torch CPU threads={cores}"}
+                      f"{stream.shape.name}-shaped stream, B={B}, K=10, dropout 0.6 (reference epoch 1), torch CPU "
+                      f"threads={cores}; the train epoch ({stream.train_end} events) extrapolated at this rate"}
 
 
 def run_tgnn(args, world, rank, dev):
     """The running reference path (model_utils.TGNN, DGL EdgeGATConv block loop)."""
+    _log(f"tgnn: {args.dataset} B={args.batch * world}")
 
     from tgnx import _lib
     from tgnx.engine import TgnnEngine
@@ -191,7 +252,7 @@ def run_tgnn(args, world, rank, dev):
 
     if True:
         out = {
-            "metric": "temporal edges/sec on tgbl-wiki TGN (train step)",
+            "metric": _metric(args.dataset, "tgnn"),
             "value": round(args.steps * Bg / elapsed, 1),
             "unit": "events/s",
             "n_gpus": world,
@@ -225,41 +286,118 @@ def run_tgnn(args, world, rank, dev):
 
 
 
-def cpu_baseline_tgn(stream, B, budget_s=15.0, max_batches=40):
-    """Oracle restatement of the TGN memory path (oracle/tgn_ref.py) on the same stream, bounded sample."""
+def cpu_baseline_tgn(stream, B, budget_s=45.0, aggr="last", layers=1):
+    """Oracle restatement of the TGN memory path (oracle/tgn_ref.py) over ONE full train epoch of the same
+    stream at batch B (BASELINE config #1: one epoch on the CPU), all affinity cores; batch 1 (empty state,
+    allocator warm-up) is run but not timed.  If the epoch would exceed budget_s, the rate of the batches
+    run so far is reported and the epoch time extrapolated from it (stated in the sample)."""
     sys.path.insert(0, ROOT)
     from oracle.sampler_ref import RefLastNeighborLoader
     from oracle.tgn_ref import RefTGN, train_step
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+    cores = _cores()
     torch.set_num_threads(cores)
     N, d = stream.shape.num_nodes, stream.shape.msg_dim
     torch.manual_seed(0)
-    model = RefTGN(N, d, hidden=100, aggr="last", dropout=0.1)
+    model = RefTGN(N, d, hidden=100, aggr=aggr, dropout=0.1, layers=layers)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     loader = RefLastNeighborLoader(N, 10)
     ev_t = torch.from_numpy(stream.t.astype(np.float32))
     ev_msg = torch.from_numpy(stream.msg)
     rng = np.random.default_rng(0)
-    n, t_total = 0, 0.0
-    while n < max_batches and t_total < budget_s:
-        sl = slice(n * B, (n + 1) * B)
-        src, dst = torch.from_numpy(stream.src[sl]), torch.from_numpy(stream.dst[sl])
-        neg = torch.from_numpy(rng.choice(stream.dst_nodes, size=src.shape[0]))
+    E = stream.train_end
+    nb = math.ceil(E / B)
+    t_total, t_first, timed_ev, n = 0.0, 0.0, 0, 0
+    for n in range(nb):
+        a, b = n * B, min((n + 1) * B, E)
+        src, dst = torch.from_numpy(stream.src[a:b]), torch.from_numpy(stream.dst[a:b])
+        neg = torch.from_numpy(rng.choice(stream.dst_nodes, size=b - a))
         t0 = time.perf_counter()
-        train_step(model, opt, loader, ev_t, ev_msg, src, dst, neg, ev_t[sl], ev_msg[sl])
+        train_step(model, opt, loader, ev_t, ev_msg, src, dst, neg, ev_t[a:b], ev_msg[a:b])
         dt = time.perf_counter() - t0
-        if n > 0:
+        if n == 0:
+            t_first = dt
+            _log(f"cpu_baseline_tgn B={B}: batch 1 {dt:.2f} s, {cores} threads")
+        else:
             t_total += dt
-        n += 1
-    timed = max(n - 1, 1)
-    return {"value": round(timed * B / max(t_total, 1e-9), 2), "unit": "events/s", "cores": cores, "kind": "port",
-            "sample": f"oracle TGN restatement (oracle/tgn_ref.py: TGNMemory + GRU + TransformerConv + LinkPredictor), "
-                      f"train batches 2..{n} of the same wiki-shaped stream, B={B}, K=10, last aggregation, "
-                      f"torch CPU threads={cores}"}
+            timed_ev += b - a
+        if n % 50 == 49:
+            _log(f"cpu_baseline_tgn B={B}: {n + 1}/{nb} batches, {t_total:.1f} s")
+        if t_total > budget_s:
+            break
+    done = n + 1
+    rate = timed_ev / max(t_total, 1e-9)
+    full = done == nb
+    out = {"value": round(rate, 2), "unit": "events/s", "cores": cores, "kind": "port", **_cpu_info(),
+           "batch": B, "epoch_events": E, "batches_run": done, "full_epoch": full}
+    if full:
+        out["epoch_s"] = round(t_first + t_total, 2)
+    else:
+        out["epoch_s_extrapolated"] = round(t_first + (E - min(B, E)) / max(rate, 1e-9), 1)
+    out["sample"] = (f"oracle TGN restatement (oracle/tgn_ref.py: TGNMemory + {'Mean' if aggr == 'mean' else 'Last'}"
+                     f"Aggregator + GRU + TransformerConv + LinkPredictor, attention dropout 0.1), "
+                     f"{'one full' if full else 'part of one'} {stream.shape.name}-shaped train epoch "
+                     f"({E} events, {done}/{nb} batches of {B}); rate over batches 2..{done} (batch 1 untimed), "
+                     f"torch CPU threads = {cores} (all affinity cores)"
+                     + ("" if full else f"; epoch time extrapolated at this rate (budget {budget_s:.0f} s)"))
+    return out
+
+
+def tgn_step_bytes(d, D, K, layers):
+    """SURVEY §8(d) algorithmic bytes per event of the TGN train step: forward
+    B_ev = R [S (20 + 4d + 4D + 4) + 4D + 4] + 4 K 20 + (20 + 4d), R = 3 roots, S = K (1 hop) or K + K^2
+    (2 hops), plus the GRU memory path 2 (56 + 8d + 12D); training counts x 2 (backward re-gathers)."""
+    S = K if layers == 1 else K + K * K
+    fwd = 3 * (S * (20 + 4 * d + 4 * D + 4) + 4 * D + 4) + 4 * K * 20 + (20 + 4 * d)
+    gru = 2 * (56 + 8 * d + 12 * D)
+    return 2 * (fwd + gru)
+
+
+def tgn_launch_bytes(name, E, M, Bw, Bg, D, d, K, P, N):
+    """Algorithmic bytes of one launch of the TGN step: E sampled edges, M sampled nodes,
+    Bw this rank's events, Bg the global batch, P trainable parameters, N nodes."""
+    Qm = 3 * D + d
+    per_edge = 20 + 4 * d + 4 * D + 4                 # SURVEY §8(d): ring entry, msg row, neighbour row, Δt
+    if name == "tgn_agg_emit":                        # edge records + Δt enc ‖ message gather + aggregate
+        return M * (8 * D + 4 * d + 40 + 4 * Qm) + E * (per_edge + 4)
+    if name == "tgn_gru_edge":                        # ring insert ‖ GRU ([X | memory] in, z + gates out) ‖ lin_edge
+        return Bg * 4 * K * 20 + M * (4 * Qm + 4 * D + 4 * D + 16 * D) + E * (4 * d + 12 + 4 * D)
+    if name == "tgn_proj":                            # z0 in, q / k / v / skip out
+        return M * (4 * D + 16 * D)
+    if name in ("tgn_attn_fwd", "tgn_attn_bwd"):      # per edge: k, v, edge rows (+ softmax terms)
+        return E * (12 * D + 8)
+    if name == "tgn_pred_train":                      # per event 3 embedding rows ‖ the attention of its roots
+        return Bw * 12 * D + E * (12 * D + 8) + 4 * (2 * D * D + 3 * D + 1)   # (each centre's edges once)
+    if name == "tgn_kv_dE":                           # (dk, dv) sums ‖ dW_edge ‖ dEnc W_e
+        return E * (8 * D + 8 * D) + E * (4 * D + 4 * (D + d) + 12 + 4 * D)
+    if name == "tgn_wgrad_dz0":                       # dW_proj, dW_src/dst ‖ dz0 + GRU backward
+        return M * 76 * D
+    if name == "tgn_wgrad3":                          # dW_gru (dG, [X | memory]) ‖ dX_enc ‖ stores
+        return M * (16 * D + 4 * Qm + 4 * D + 16 * D) + Bg * 2 * (8 + 4 * d)
+    if name == "tgn_fixup_update":                    # Adam over every parameter (p, m, v, g in; p, m, v out)
+        return 28 * P
+    if name == "tgn_adam":
+        return 28 * P
+    if name == "tgn_scan":                            # two node bitmaps, sorted node / centre lists
+        return N // 4 + 8 * (M + E)
+    return 0
+
+
+def _probe_floor_us(n=200):
+    from tgnx import _lib
+    ms = ctypes.c_double()
+    _lib.call("tgnx_probe_floor", n, _lib.stream(), ctypes.byref(ms))
+    return ms.value * 1e3
+
+
+def _pmc(workload_ok):
+    """profiles/pmc_traffic.json (tools/pmc_traffic.sh on the default workload): bytes per launch."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not (workload_ok and os.path.exists(pmc)):
+        return {}
+    try:
+        return {k: v for k, v in json.load(open(pmc)).items() if isinstance(v, dict)}
+    except Exception:
+        return {}
 
 
 def run_tgn(args, world, rank, dev):
@@ -272,7 +410,8 @@ def run_tgn(args, world, rank, dev):
     shape = SHAPES[args.dataset]
     stream = make_stream(shape, seed=0)
     N, d, D, K = shape.num_nodes, shape.msg_dim, 100, 10
-    Bg = args.batch * world
+    # weak scaling: --batch events per GPU (global B x world); --global-batch: B events split over the ranks
+    Bg = args.global_batch if args.global_batch else args.batch * world
     g = torch.Generator().manual_seed(0)
     model = TGNModel(N, stream.num_events, d, D, dev, ring=K, max_batch=Bg, max_neg=1,
                      aggr="mean" if args.aggr == "mean" else "last", dropout=0.0 if args.no_dropout else 0.1,
@@ -305,6 +444,7 @@ def run_tgn(args, world, rank, dev):
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
+    _log(f"tgn: {args.dataset} B={Bg} warmup {args.warmup}")
     for _ in range(args.warmup):
         step()
     barrier()
@@ -320,14 +460,19 @@ def run_tgn(args, world, rank, dev):
     eng.check()
     loss = eng.loss_sum()
     assert math.isfinite(loss), "non-finite loss"
+    _log(f"tgn: {args.steps} steps {elapsed * 1e3 / args.steps:.4f} ms/step; probes")
+    ms_step = elapsed / args.steps * 1e3
+    value = args.steps * Bg / elapsed
 
-    # live per-launch timing (HIP events on the launch stream), units from the device counters
-    Qm = 3 * D + d
+    # live per-launch timing: HIP events around eager launches on the launch stream, units from the device
+    # counters.  The pipelined step prefetches: after step j the counters include batch j + 1, so a window
+    # of n probe steps counts batches k + 1 .. k + n (stationary stream: the per-launch averages hold).
+    Bw = Bg / world
+    P = model.trainable_count()
     probes = {}
-    spec = (("tgn_gru_edge", 1), ("tgn_attn_fwd", 6), ("tgn_attn_bwd", 8), ("tgn_kv_dE", 10), ("tgn_wgrad_dz0", 2),
-            ("tgn_agg_emit", 9), ("tgn_scan", 3), ("tgn_pred_train", 4), ("tgn_fixup_update", 5), ("tgn_adam", 7))
-    if getattr(eng, "_res_fused", False):   # world 1: Adam rides in the gradient writers (no tgn_adam launch)
-        spec = tuple(x for x in spec if x[0] != "tgn_adam")
+    spec = (("tgn_agg_emit", 9), ("tgn_gru_edge", 1), ("tgn_proj", 11), ("tgn_attn_fwd", 6), ("tgn_pred_train", 4),
+            ("tgn_attn_bwd", 8), ("tgn_kv_dE", 10), ("tgn_wgrad_dz0", 2), ("tgn_wgrad3", 12), ("tgn_fixup_update", 5),
+            ("tgn_scan", 3), ("tgn_adam", 7))
     for name, kid in spec:
         _lib.call("tgnx_probe_enable", kid)
         pe0, pm0 = eng.units()
@@ -338,85 +483,91 @@ def run_tgn(args, world, rank, dev):
         _lib.call("tgnx_probe_read", ctypes.byref(ms), ctypes.byref(n))
         _lib.call("tgnx_probe_enable", 0)
         pe1, pm1 = eng.units()
-        if int(n.value) == 0:   # no such launch in this step (1 hop: the attention forward runs in tgn_pred_train)
+        if int(n.value) == 0:   # no such launch in this step (1 hop: attention forward inside tgn_pred_train; scan folded)
             continue
         launches = int(n.value)
         avg_ms = ms.value / launches
-        E = (pe1 - pe0) / launches
-        M = (pm1 - pm0) / launches
-        # algorithmic bytes per launch: edges carry the §8(d) per-sampled-edge record
-        # (ring entry 20 + msg row 4d + neighbour memory / projections 4D + Δt 4); nodes carry their
-        # message gather (2 memory rows + msg row + Δt) and GRU rows (X 4Qm, memory 4D, z 4D, gates 16D)
-        per_edge = 20 + 4 * d + 4 * D + 4
-        if name == "tgn_gru_edge":
-            algo = M * (4 * Qm + 4 * D + 4 * D + 16 * D) + E * (4 * d + 12 + 4 * D)
-        elif name == "tgn_attn_fwd":
-            algo = E * (12 * D + 8)
-        elif name == "tgn_attn_bwd":
-            algo = E * (12 * D + 8)
-        elif name == "tgn_kv_dE":
-            # the (dk, dv) sums (dKV rows in, dP k/v columns out) beside dW_edge (dE + edge attrs) and
-            # dEnc W_e (dE again)
-            algo = E * (8 * D + 8 * D) + E * (4 * D + 4 * (D + d) + 12 + 4 * D)
-        elif name == "tgn_wgrad_dz0":
-            # dW_proj (dP + z0), dz0 (dP, gates, memory, dG out)
-            algo = M * (16 * D + 4 * D + 16 * D + 16 * D + 8 * D + 16 * D)
-        elif name == "tgn_agg_emit":
-            algo = M * (8 * D + 4 * d + 40 + 4 * Qm) + E * (per_edge + 4)
-        else:
-            algo = 0.0
-        probes[name] = dict(avg_us=avg_ms * 1e3, edges=E, nodes=M, bytes=algo,
+        steps_n = max(args.probe_steps, 1)
+        E = (pe1 - pe0) / steps_n
+        M = (pm1 - pm0) / steps_n
+        algo = tgn_launch_bytes(name, E, M, Bw, Bg, D, d, K, P, N) * (steps_n / launches if name != "tgn_scan" else 1)
+        probes[name] = dict(avg_us=avg_ms * 1e3, launches=launches, edges=E, nodes=M, bytes=algo,
                             gbs=(algo / (avg_ms * 1e-3) / 1e9) if algo else None)
-    dom = max((k for k in probes if probes[k]["bytes"]), key=lambda k: probes[k]["avg_us"])
+    floor_us = _probe_floor_us()
+    dom = max(probes, key=lambda k: probes[k]["avg_us"])        # the longest launch of the step
     pd = probes[dom]
+    k_us = max(pd["avg_us"] - floor_us, 1e-3)
+    Qm = 3 * D + d
     flops_gru_edge = None
     if "tgn_gru_edge" in probes:
         q = probes["tgn_gru_edge"]
         flops_gru_edge = 2 * q["nodes"] * (Qm + D) * 4 * D + 2 * q["edges"] * (D + d) * D
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    # the PMC passes (tools/pmc_traffic.sh) run the default workload: wiki-shaped, 1 hop, last aggregation
     pmc_workload = (args.dataset == "tgbl-wiki" and args.layers == 1 and args.aggr == "last" and args.batch == 200
-                    and args.updater == "gru")
-    if os.path.exists(pmc) and pmc_workload:
-        try:
-            traffic = json.load(open(pmc)).get(dom, {}).get("bytes_per_launch")
-        except Exception:
-            traffic = None
+                    and args.updater == "gru" and not args.global_batch)
+    pmc = _pmc(pmc_workload)
+    step_algo = tgn_step_bytes(d, D, K, args.layers) * Bw          # per GPU per step
+    pmc_step = sum(v.get("bytes_per_launch", 0) for k, v in pmc.items() if k.startswith("tgn_")) if pmc else None
+    roofline = {
+        "bound": "hbm", "kernel": dom, "achieved": round(pd["gbs"], 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(pd["gbs"] / HBM_PEAK_GBS, 5),
+        "traffic": pmc.get(dom, {}).get("bytes_per_launch"),
+        "avg_launch_us": round(pd["avg_us"], 3), "algo_bytes_per_launch": round(pd["bytes"]),
+        "probe_floor_us": round(floor_us, 3),
+        "kernel_us_est": round(k_us, 3),
+        "achieved_kernel_est": round(pd["bytes"] / (k_us * 1e-6) / 1e9, 2),
+        "frac_kernel_est": round(pd["bytes"] / (k_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
+        "step_algo_bytes": round(step_algo),
+        "step_frac": round(step_algo / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+        "pmc_step_bytes": pmc_step,
+        "pmc_over_algo_step": round(pmc_step / step_algo, 3) if pmc_step else None,
+        "bytes_model": "per launch: DESIGN.md §5b (bench.tgn_launch_bytes; per sampled edge 20 + 4d + 4D + 4, "
+                       "SURVEY §8d, plus per-node message / GRU rows, 28 B per parameter for Adam); step: SURVEY "
+                       "§8(d) B_ev(train) x events per GPU (bench.tgn_step_bytes)",
+        "timing": "avg_launch_us: HIP-event pair around the eager launch (includes dispatch); kernel_us_est: minus "
+                  "the event-pair time of an empty launch (probe_floor_us); rocprofv3 durations: profiles/",
+        "units_window": "probe windows count batches k+1..k+n (pipelined prefetch), stationary stream",
+    }
+    if flops_gru_edge:
+        roofline["tgn_gru_edge_tflops"] = round(flops_gru_edge / (probes["tgn_gru_edge"]["avg_us"] * 1e-6) / 1e12, 3)
     # validation pass on the device (TGNMemory.train(False) flush, then TGB-style scoring of the first
     # val batches against the dataset's negative count): exercises the eval path at full size; MRR
-    # parity against the oracle is tests/test_gpu_tgn.py (bench may not run the oracle outside its
+    # parity against the oracle is tests/test_gpu_tgn*.py (bench may not run the oracle outside its
     # cpu_baseline leg)
     from tgnx.synth import eval_negatives
-    nval = min(10, max(1, (stream.val_end - stream.train_end) // args.batch))
-    negs = eval_negatives(stream, "val", shape.num_neg_eval, limit=nval * args.batch)
+    Be = Bg // world
+    nval = min(10, max(1, (stream.val_end - stream.train_end) // Be))
+    negs = eval_negatives(stream, "val", shape.num_neg_eval, limit=nval * Be)
     eng.flush()
     torch.cuda.synchronize()
     tv = time.perf_counter()
     rrs = []
     for i in range(nval):
-        a = stream.train_end + i * args.batch
-        _, _, rr = eng.eval_batch(a, args.batch, torch.from_numpy(negs[i * args.batch:(i + 1) * args.batch]))
+        a = stream.train_end + i * Be
+        _, _, rr = eng.eval_batch(a, Be, torch.from_numpy(negs[i * Be:(i + 1) * Be]))
         rrs.append(rr.clone())
     torch.cuda.synchronize()
     tv = time.perf_counter() - tv
     eng.check()
     val = {"mrr": round(float(torch.stack(rrs).mean()), 5), "batches": nval, "negatives": int(shape.num_neg_eval),
-           "events_per_s": round(nval * args.batch / tv, 1), "note": "synthetic stream, mid-epoch state; "
-           "eval-path smoke at full size (MRR parity vs the oracle: tests/test_gpu_tgn.py)"}
-    cpu = None
+           "events_per_s": round(nval * Be / tv, 1), "note": "synthetic stream, mid-epoch state; "
+           "eval-path smoke at full size (MRR parity vs the oracle: tests/test_gpu_tgn*.py)"}
+    cpu = cpu1 = None
+    _log("tgn: eval pass done")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_tgn(stream, args.batch)
+        cpu = cpu_baseline_tgn(stream, Bg, aggr=args.aggr, layers=args.layers)
+        if args.dataset == "tgbl-wiki" and args.layers == 1 and args.aggr == "last" and Bg != 2000:
+            cpu1 = cpu_baseline_tgn(stream, 2000)      # BASELINE config #1: config/TGN.yml batch_size 2000
+            cpu1["config"] = "BASELINE #1: tgbl-wiki TGN.yml (batch 2000) on the CPU, one epoch"
     return {
-        "metric": "temporal edges/sec on tgbl-wiki TGN (train step)",
-        "value": round(args.steps * Bg / elapsed, 1),
+        "metric": _metric(args.dataset, "tgn"),
+        "value": round(value, 1),
         "unit": "events/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_batch else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic {args.dataset}-shaped stream (SURVEY.md §8d), events resident in HBM",
@@ -426,22 +577,18 @@ def run_tgn(args, world, rank, dev):
                                f"{'Mean' if args.aggr == 'mean' else 'Last'}Aggregator, "
                                f"{'2-hop temporal attention (conv2(conv1)), ' if args.layers == 2 else ''}"
                                f"TransformerConv heads=2, "
-                               f"LinkPredictor), batch {args.batch}/GPU, {K} temporal neighbours, D=100, d={d}, "
-                               f"attention dropout {'off' if args.no_dropout else '0.1'}",
+                               f"LinkPredictor), batch {Bg} global ({Bg // world}/GPU), {K} temporal neighbours, "
+                               f"D=100, d={d}, attention dropout {'off' if args.no_dropout else '0.1'}",
                    "global_batch": Bg, "parallelism": f"dp{world}",
                    "launch": "hip-graph replay per step" if use_graph else "eager",
                    "layers": args.layers,
-                   "sampled_edges_per_step": round(probes[dom]["edges"], 1),
-                   "sampled_nodes_per_step": round(probes[dom]["nodes"], 1)},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(pd["gbs"], 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(pd["gbs"] / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "avg_launch_us": round(pd["avg_us"], 3), "algo_bytes_per_launch": round(pd["bytes"]),
-                     "bytes_model": "DESIGN.md §TGN: per sampled edge 20 + 4d + 4D + 4 (SURVEY §8d) plus per-node "
-                                    "message / GRU rows; tgn_gru_edge also " +
-                                    (f"{flops_gru_edge / (probes['tgn_gru_edge']['avg_us'] * 1e-6) / 1e12:.3f} "
-                                     f"TFLOP/s fp32 MFMA" if flops_gru_edge else "")},
+                   "sampled_edges_per_step": round(pd["edges"], 1),
+                   "sampled_nodes_per_step": round(pd["nodes"], 1)},
+        "roofline": roofline,
         "kernels_us": {k: round(v["avg_us"], 3) for k, v in probes.items()},
+        "kernels_gbs": {k: round(v["gbs"], 1) for k, v in probes.items() if v["gbs"]},
         "cpu_baseline": cpu,
+        "cpu_baseline_config1": cpu1,
         "val_eval_gpu": val,
         "loss_sum": round(loss, 4),
     }
@@ -452,7 +599,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--batch", type=int, default=200, help="events per GPU per step")
+    ap.add_argument("--batch", type=int, default=200, help="events per GPU per step (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="events per step over all GPUs (strong scaling; BASELINE #5: 'batch 600' on 8 GPUs)")
     ap.add_argument("--dataset", default="tgbl-wiki")
     ap.add_argument("--model", choices=["tgn", "tgnn"], default="tgn",
                     help="tgn: the TGN memory path (north star, headline); tgnn: the running DGL block-loop path")

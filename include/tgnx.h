@@ -98,8 +98,13 @@ int tgnx_block_ids_host(const int64_t* src, const int64_t* dst, int64_t num_even
 #define TGNX_K_SEG_BWD 8        /* tgnn_seg_bwd */
 #define TGNX_K_EDGE_META 9      /* tgnn_edge_meta */
 #define TGNX_K_KV 10             /* TGN: kv_reduce ‖ dW_edge ‖ dEnc·W_e launch */
+#define TGNX_K_PROJ 11           /* TGN: q / k / v / skip projections launch */
+#define TGNX_K_WGRAD3 12         /* TGN: dW_gru ‖ dX_enc ‖ message stores ‖ descriptor snapshot launch */
 int tgnx_probe_enable(int32_t kernel_id);
 int tgnx_probe_read(double* total_ms, int64_t* launches);
+/* The probe floor: average event-pair time around n launches of an empty kernel on `stream` (dispatch +
+ * completion of a launch without work), so that probe averages minus it estimate kernel durations. */
+int tgnx_probe_floor(int32_t n, void* stream, double* avg_ms);
 /* Workgroup timeline stamps (diagnostic; measurement only): a library built with -DTGNX_STAMPS records, for
  * wave 0 of every workgroup of the TGN step's kernels, {start, end} (s_memrealtime ticks, 100 MHz), kernel
  * id, block and XCC as 32-byte records into `buf`: 64 shards (by block) of cap / 64 records, shard s at

@@ -3662,9 +3662,11 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   auto mk_at = [&](int at) {
     return BlockJob<MarkNextJob, 3 * MARK_LDS_WORDS>{MarkNextJob{c, nmark}, pipe && at == TGNX_PIPE_MARK_AT ? nmark : 0};
   };
+  probe_begin(TGNX_K_PROJ, s);
   gemmN_launch(s, mk_at(3),
                gemm_job<G32>(gemm_shape<G32>(k.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
                              LoadProjW{P + c.L.wq, c.L.pw, HC, D}, EpiProj{P + c.L.bq, c.L.pb, c.P, HC}, (float*)nullptr));
+  probe_end(TGNX_K_PROJ, s);
   TGNX_LAUNCH_CHECK("tgn_proj");
   // 1 hop: the attention forward runs inside tgn_pred_train (per root, beside its weight staging)
   const bool att_in_pred = !two && TGNX_PRED_ATT;
@@ -3752,6 +3754,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
   // ‖ the message stores ‖ the fixup's descriptor copy + the counter advance (SnapJob)
   const int nst = gridn(2 * k.B, 256);
+  probe_begin(TGNX_K_WGRAD3, s);
   gemmN_launch(s, mk_at(9), BlockJob<SnapJob>{SnapJob{c}, 1}, BlockJob<StoreJob>{StoreJob{c, nst}, nst},
                gemm_job<GW>(shp_dWg(k, c.cnt), LoadKRow{c.dG, Cl::G * D, k.Mtr, Cl::G * D},
                             LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{}, c.pD),
@@ -3759,6 +3762,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                               LoadRowK{c.dG, k.Mtr, Cl::G * D, Cl::G * D}, Cl::wenc(c),
                               EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge},
                               (float*)nullptr));
+  probe_end(TGNX_K_WGRAD3, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
   // split-K sums + epilogues ‖ Δt reduction ‖ update_state's memory half (train order: memory of src ∪
   // dst from this step's GRU rows; the stores and the ring insert ran in earlier launches), reading the

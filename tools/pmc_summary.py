@@ -15,6 +15,8 @@ KERNELS = {
     "tgn_attn_fwd": ("tgn_attn_fwd<true>",),
     "tgn_attn_bwd": ("tgn_attn_bwd",),
     "tgn_kv_dE": ("gemmN_kernel", "KvReduceJob"),
+    "tgn_proj": ("gemmN_kernel", "LoadProjW,"),
+    "tgn_wgrad3": ("gemmN_kernel", "SnapJob"),
     "tgn_agg_emit": ("tgn_agg_emit",),
     "tgn_scan": ("tgn_scan<true>",),
     "tgn_mark": ("tgn_mark<true>",),
