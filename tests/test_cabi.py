@@ -44,3 +44,21 @@ def test_block_ids_host_rejects_bad_input():
     rc = _lib.lib().tgnx_block_ids_host(src.ctypes.data, src.ctypes.data, 2, 2, out.ctypes.data)
     assert rc != 0
     assert b"negative" in _lib.lib().tgnx_last_error()
+
+
+def test_torch_ops_library_registers_every_op():
+    """torch.ops.tgnx (csrc/tgnx_torch.cpp, TORCH_LIBRARY over the C ABI) loads without a GPU and
+    registers its schemas; the host op (block_ids) runs and matches the oracle (dependencyGraph.py:8-49)."""
+    import numpy as np
+    import torch
+
+    from oracle import blocks_ref
+    from tgnx import ops
+    ns = ops.load()
+    for name in ops.OPS:
+        assert hasattr(ns, name), name
+    assert "Tensor(a!) assoc" in str(ns.ring_sample.default._schema)
+    rng = np.random.default_rng(0)
+    src, dst = rng.integers(0, 50, 600), rng.integers(0, 50, 600)
+    got = ns.block_ids(torch.from_numpy(src), torch.from_numpy(dst), 200).numpy()
+    assert np.array_equal(got, blocks_ref.block_ids(src, dst, 200))
