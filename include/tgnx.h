@@ -286,6 +286,10 @@ typedef struct {
   int32_t updater;     /* memory updater: 0 = GRUCell (TGNMemory memory_module.py:71-72; DyRepMemory 'gru'),
                           1 = RNNCell (DyRepMemory memory_updater_type 'rnn', memory_module.py:256-259):
                           weight_ih [D, Qm], weight_hh [D, D], bias_ih / bias_hh [D] in the same layout slots */
+  int32_t emb_in_msg;  /* DyRepMemory (memory_module.py:218-421): bit 0 use_src_emb_in_msg, bit 1
+                          use_dst_emb_in_msg (:387-408) — update_state of src ∪ dst builds its messages with the
+                          batch's embeddings in place of the memory rows of endpoints in src ∪ dst (train: the
+                          train forward's, eval: the eval forward's).  0 = TGNMemory messages.  layers = 1, world 1. */
 } tgnx_tgn_config;
 
 typedef struct {

@@ -95,8 +95,11 @@ class RefTGNMemory(nn.Module):
     (:218-421) with use_src_emb_in_msg = use_dst_emb_in_msg = False computes exactly this (same update
     order :316-331 vs :126-138, messages :381-421 vs :193-207, last_update :365 vs :176, cell :259-264)."""
 
-    def __init__(self, num_nodes, raw_msg_dim, memory_dim, time_dim, aggr="last", updater="gru"):
+    def __init__(self, num_nodes, raw_msg_dim, memory_dim, time_dim, aggr="last", updater="gru",
+                 use_src_emb_in_msg=False, use_dst_emb_in_msg=False):
         super().__init__()
+        # DyRepMemory (memory_module.py:242-267): embeddings in the messages of update_state (:387-408)
+        self.use_src_emb_in_msg, self.use_dst_emb_in_msg = bool(use_src_emb_in_msg), bool(use_dst_emb_in_msg)
         self.num_nodes, self.raw_msg_dim, self.memory_dim, self.time_dim = num_nodes, raw_msg_dim, memory_dim, time_dim
         self.out_channels = raw_msg_dim + 2 * memory_dim + time_dim
         self.time_enc = RefTimeEncoder(time_dim)
@@ -131,27 +134,27 @@ class RefTGNMemory(nn.Module):
             return self._get_updated_memory(n_id)
         return self.memory[n_id], self.last_update[n_id]
 
-    def update_state(self, src, dst, t, raw_msg):                      # :126-138
+    def update_state(self, src, dst, t, raw_msg, embeddings=None, assoc=None):   # :126-138 (DyRep :316-329)
         n_id = torch.cat([src, dst]).unique()
         if self.training:
-            self._update_memory(n_id)
+            self._update_memory(n_id, embeddings, assoc)
             self._update_msg_store(src, dst, t, raw_msg, self.msg_s_store)
             self._update_msg_store(dst, src, t, raw_msg, self.msg_d_store)
         else:
             self._update_msg_store(src, dst, t, raw_msg, self.msg_s_store)
             self._update_msg_store(dst, src, t, raw_msg, self.msg_d_store)
-            self._update_memory(n_id)
+            self._update_memory(n_id, embeddings, assoc)
 
-    def _update_memory(self, n_id):                                    # :147-150
-        memory, last_update = self._get_updated_memory(n_id)
+    def _update_memory(self, n_id, embeddings=None, assoc=None):      # :147-150 (DyRep :338-341)
+        memory, last_update = self._get_updated_memory(n_id, embeddings, assoc)
         with torch.no_grad():
             self.memory[n_id] = memory.detach()
             self.last_update[n_id] = last_update.detach().long()
 
-    def _get_updated_memory(self, n_id):                               # :152-178
+    def _get_updated_memory(self, n_id, embeddings=None, assoc=None):  # :152-178 (DyRep :343-367)
         self._assoc[n_id] = torch.arange(n_id.size(0))
-        msg_s, t_s, src_s, _ = self._compute_msg(n_id, self.msg_s_store)
-        msg_d, t_d, src_d, _ = self._compute_msg(n_id, self.msg_d_store)
+        msg_s, t_s, src_s, _ = self._compute_msg(n_id, self.msg_s_store, embeddings, assoc)
+        msg_d, t_d, src_d, _ = self._compute_msg(n_id, self.msg_d_store, embeddings, assoc)
         idx = torch.cat([src_s, src_d], dim=0)
         msg = torch.cat([msg_s, msg_d], dim=0)
         t = torch.cat([t_s, t_d], dim=0)
@@ -167,12 +170,20 @@ class RefTGNMemory(nn.Module):
         for i, idx in zip(n_id.tolist(), perm.split(count.tolist())):
             store[i] = (src[idx], dst[idx], t[idx], raw_msg[idx])
 
-    def _compute_msg(self, n_id, store):                               # :193-207
+    def _compute_msg(self, n_id, store, embeddings=None, assoc=None):  # :193-207 (DyRep :376-412)
         data = [store[i] for i in n_id.tolist() if i in store] or [self._empty]
         src, dst, t, raw = (torch.cat(x, dim=0) for x in zip(*data))
         t_rel = t - self.last_update[src]
         t_enc = self.time_enc(t_rel.to(raw.dtype))
-        msg = identity_message(self.memory[src], self.memory[dst], raw, t_enc)
+        src_mem, dst_mem = self.memory[src], self.memory[dst]
+        # DyRep (:387-408): an endpoint in n_id takes its embedding row (embeddings[assoc[node]])
+        if self.use_src_emb_in_msg and embeddings is not None and src.numel():
+            m = torch.isin(src, n_id)
+            src_mem[m] = embeddings[assoc[src[m]]]
+        if self.use_dst_emb_in_msg and embeddings is not None and dst.numel():
+            m = torch.isin(dst, n_id)
+            dst_mem[m] = embeddings[assoc[dst[m]]]
+        msg = identity_message(src_mem, dst_mem, raw, t_enc)
         return msg, t, src, dst
 
     def train(self, mode: bool = True):                                # :209-215
@@ -256,9 +267,11 @@ class RefLinkPredictor(nn.Module):
 class RefTGN(nn.Module):
     """pyg_model_utils.py:10-36: memory + gnn (sharing memory.time_enc) + link_pred."""
 
-    def __init__(self, num_nodes, msg_dim, hidden=100, aggr="last", dropout=0.1, layers=1, updater="gru"):
+    def __init__(self, num_nodes, msg_dim, hidden=100, aggr="last", dropout=0.1, layers=1, updater="gru",
+                 use_src_emb_in_msg=False, use_dst_emb_in_msg=False):
         super().__init__()
-        self.memory = RefTGNMemory(num_nodes, msg_dim, hidden, hidden, aggr, updater)
+        self.memory = RefTGNMemory(num_nodes, msg_dim, hidden, hidden, aggr, updater, use_src_emb_in_msg,
+                                   use_dst_emb_in_msg)
         self.gnn = RefGraphAttentionEmbedding(hidden, hidden, msg_dim, self.memory.time_enc, dropout, layers)
         self.link_pred = RefLinkPredictor(hidden)
         self.layers = layers
@@ -271,6 +284,18 @@ def sample_hops(model: RefTGN, loader, n_id):
     if model.layers == 2:
         n_id, ei, e_id, _ = loader(n_id)
     return torch.from_numpy(n_id), torch.from_numpy(ei), torch.from_numpy(e_id)
+
+
+def _emb_args(model: RefTGN, z, assoc):
+    """DyRepMemory.update_state's (embeddings, assoc) (memory_module.py:316-317): the batch's embeddings over
+    its sampled node set and the loop's node -> row map, when the memory uses them in messages.  Which
+    embeddings a DyRep loop passes is that loop's choice (the reference contains none; TGB's DyRep example
+    [ext] passes the batch's GNN output): here the same forward's, detached (the update does not reach the
+    batch's loss)."""
+    mem = model.memory
+    if mem.use_src_emb_in_msg or mem.use_dst_emb_in_msg:
+        return z.detach(), assoc
+    return ()
 
 
 def train_step(model: RefTGN, opt, loader, ev_t, ev_msg, src, pos, neg, t, msg):
@@ -287,7 +312,7 @@ def train_step(model: RefTGN, opt, loader, ev_t, ev_msg, src, pos, neg, t, msg):
     neg_out = model.link_pred(z[assoc[src]], z[assoc[neg]])
     crit = nn.BCEWithLogitsLoss()
     loss = crit(pos_out, torch.ones_like(pos_out)) + crit(neg_out, torch.zeros_like(neg_out))
-    model.memory.update_state(src, pos, t, msg)
+    model.memory.update_state(src, pos, t, msg, *_emb_args(model, z, assoc))
     loader.insert(src.numpy(), pos.numpy(), t.numpy())
     loss.backward()
     opt.step()
@@ -367,7 +392,7 @@ def eval_step(model: RefTGN, loader, ev_t, ev_msg, src, pos, negs, t, msg):
     z = model.gnn(z, last_update, ei, ev_t[e_id], ev_msg[e_id])
     zs = z[assoc[src]].unsqueeze(1).expand(-1, cand.shape[1], -1)
     y = model.link_pred(zs.reshape(-1, z.shape[1]), z[assoc[cand.reshape(-1)]]).view(cand.shape)
-    model.memory.update_state(src, pos, t, msg)
+    model.memory.update_state(src, pos, t, msg, *_emb_args(model, z, assoc))
     loader.insert(src.numpy(), pos.numpy(), t.numpy())
     return y[:, 0].clone(), y[:, 1:].clone()
 

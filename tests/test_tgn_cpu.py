@@ -174,7 +174,7 @@ def test_two_hop_oracle_reduces_to_one_hop():
 def test_dyrep_model_surface():
     """DyRepMemory (modules/memory_module.py:218-421) behind getModel: memory_updater_type 'gru' | 'rnn' with
     the reference's state-dict names (memory.memory_updater.*, shared with TGNMemory, :70-78); embeddings in
-    the messages refused; an unknown updater rejected as the reference does (:75-78)."""
+    an unknown updater rejected as the reference does (:75-78); embedding messages only on DyRepMemory, 1 hop."""
     from oracle.tgn_ref import RefTGN
     from tgnx.tgn import PARAM_ORDER, param_shapes
     ref = RefTGN(30, 4, hidden=8, updater="rnn")
@@ -183,7 +183,44 @@ def test_dyrep_model_surface():
     assert {k: tuple(v.shape) for k, v in ref.named_parameters()} == {k: shapes[k] for k in PARAM_ORDER}
     assert shapes["memory.memory_updater.weight_ih"] == (8, 3 * 8 + 4)
     from tgnx.tgn import TGNModel
+    with pytest.raises(ValueError):
+        TGNModel(30, 10, 4, 8, "cpu", memory="tgn", updater="rnn", use_dst_emb_in_msg=True)
     with pytest.raises(NotImplementedError):
-        TGNModel(30, 10, 4, 8, "cpu", memory="dyrep", updater="rnn", use_dst_emb_in_msg=True)
+        TGNModel(30, 10, 4, 8, "cpu", memory="dyrep", updater="rnn", layers=2, use_dst_emb_in_msg=True)
     with pytest.raises(ValueError):
         TGNModel(30, 10, 4, 8, "cpu", memory="dyrep", updater="lstm")
+
+
+def test_dyrep_embedding_messages_follow_the_reference_loop():
+    """oracle RefTGNMemory._compute_msg with embeddings (vectorised isin) against the reference's own per-entry
+    loop (memory_module.py:387-408, restated literally here: `if s in n_id` per stored message), on stores
+    filled by two batches: the source / destination memory rows replaced by embeddings[assoc[node]] exactly
+    for the endpoints in n_id."""
+    from oracle.tgn_ref import RefTGNMemory
+    torch.manual_seed(0)
+    N, d, D = 40, 3, 6
+    for flags in ((1, 0), (0, 1), (1, 1)):
+        mem = RefTGNMemory(N, d, D, D, "last", "rnn", *flags)
+        mem.memory.copy_(torch.randn(N, D))
+        g = torch.Generator().manual_seed(1)
+        for b in range(2):
+            src, dst = torch.randint(0, N, (12,), generator=g), torch.randint(0, N, (12,), generator=g)
+            t = torch.arange(12, dtype=torch.float32) + 20 * b
+            mem._update_msg_store(src, dst, t, torch.randn(12, d), mem.msg_s_store)
+            mem._update_msg_store(dst, src, t, torch.randn(12, d), mem.msg_d_store)
+        n_id = torch.cat([src, dst]).unique()
+        emb = torch.randn(N, D)
+        assoc = torch.randperm(N)
+        inv = torch.empty(N, dtype=torch.long)
+        inv[assoc] = torch.arange(N)
+        embeddings = emb[inv]                       # embeddings[assoc[v]] == emb[v]
+        for store in (mem.msg_s_store, mem.msg_d_store):
+            msg, _, s_, d_ = mem._compute_msg(n_id, store, embeddings, assoc)
+            src_mem, dst_mem = mem.memory[s_].clone(), mem.memory[d_].clone()
+            for i, v in enumerate(s_):              # memory_module.py:389-397
+                if flags[0] and v in n_id:
+                    src_mem[i] = embeddings[assoc[v]]
+            for i, v in enumerate(d_):              # :400-408
+                if flags[1] and v in n_id:
+                    dst_mem[i] = embeddings[assoc[v]]
+            assert torch.equal(msg[:, :D], src_mem) and torch.equal(msg[:, D:2 * D], dst_mem)

@@ -229,6 +229,13 @@ struct Ctx {
   int64_t* e1_id;                    // root edge -> event id
   float *P2, *Ep2, *alpha1, *Zr, *dZr, *dP2, *dE2, *pE, *pF;
   int R1cap, E1cap, tgp_e1;          // tgp rows of the root edges start at tgp_e1
+  // DyRepMemory use_src_emb_in_msg (bit 0) / use_dst_emb_in_msg (bit 1) (memory_module.py:387-408; 0 =
+  // TGNMemory messages): the memory update of src ∪ dst builds its messages with the embedding rows zemb
+  // (per centre) in place of memory rows; Zupd: the memory updater's output rows of the update list
+  // (train: computed beside the step's own GRU rows, read by the fixup's memory write)
+  int emb;
+  const float* zemb;
+  float* Zupd;
 };
 constexpr int CNT_R1 = 7, CNT_E1 = 8;
 
@@ -1013,9 +1020,33 @@ __device__ __forceinline__ void store_event(const Ctx& c, const StoreView& s, in
   other = *(src ? c.ev_dst + e : c.ev_src + e);
   t = c.ev_t[e];
 }
+// EMB (DyRepMemory use_{src,dst}_emb_in_msg, memory_module.py:387-408; aggregation over the update list
+// c.upd only): the memory row of a message endpoint is replaced by the endpoint's embedding when it is in
+// the update set n_id = src ∪ dst of the batch — c.upd, sorted; its entry's sampled row (upd_loc) gives its
+// centre row (crank), which holds the embedding.  (assoc cannot be used: the batch's ring insert, earlier in
+// the step, rewrote it.)  self: the store's own node, list entry m — the `src` of every message it stores.
+template <bool EMB>
+__device__ __forceinline__ const float* msg_row(const Ctx& c, int64_t v, bool self, int m) {
+  if (EMB) {
+    int u = -1;
+    if (self) {
+      if (c.emb & 1) u = m;
+    } else if (c.emb & 2) {
+      int lo = 0, hi = min(c.cnt[CNT_U], c.Ucap);  // first entry >= v
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (c.upd[mid] < v) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < min(c.cnt[CNT_U], c.Ucap) && c.upd[lo] == v) u = lo;
+    }
+    if (u >= 0) return c.zemb + (int64_t)c.crank[c.upd_loc[u]] * c.HC;
+  }
+  return c.mem + v * c.D;
+}
 // AG: the aggregation compiled in (0 last, 1 mean, -1 either by c.aggr): the last-only kernel does not carry
 // the mean path's registers (233 -> fewer VGPRs: more tgn_agg_emit workgroups resident at once)
-template <int AG>
+template <int AG, bool EMB = false>
 __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
   const int D = c.D, d = c.d, Qm = c.Qm, enc0 = 2 * D + d;
   const StoreView sv = store_view(c, n);
@@ -1034,7 +1065,7 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
     return;
   }
   const float lun = (float)c.lu_buf[n];
-  const float* rowN = c.mem + n * D;
+  const float* rowN = msg_row<EMB>(c, n, true, m);
   if (AG == 0 || (AG < 0 && c.aggr == 0)) {
     // winner: max t, first index in [msg_s; msg_d] order
     float tb = -INFINITY;
@@ -1056,7 +1087,7 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
     const int wl = __ffsll(__ballot(kb == kk)) - 1;
     const int64_t e = shfl_i64(eb, wl), other = shfl_i64(ob, wl);
     const float tr = tm - lun;
-    const float* rowO = c.mem + other * D;
+    const float* rowO = msg_row<EMB>(c, other, false, m);
     const float* raw = c.ev_msg + e * d;
     for (int k0 = lane; k0 < Qm; k0 += 64 * 8) {
       float v[8];
@@ -1118,10 +1149,11 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
             const int q = min(qb + u, nq - 1);
             const int64_t e = shfl_i64(e_l, q), o = shfl_i64(o_l, q);
             dt[u] = lane_f(t_l, q) - lun;
+            const float* rowO = msg_row<EMB>(c, o, false, m);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
               const int k = min(k0 + lane + 64 * i, Qm - 1);
-              const float* p = k < D ? rowN + k : k < 2 * D ? c.mem + o * D + (k - D)
+              const float* p = k < D ? rowN + k : k < 2 * D ? rowO + (k - D)
                                                     : k < enc0 ? c.ev_msg + e * d + (k - 2 * D) : rowN;
               v[u][i] = *p;
             }
@@ -1166,6 +1198,7 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
 // into 4 contiguous ranges, one per wave, and the partial sums combine in LDS in wave order.  A hub node
 // of the review-shaped stream stores ~100-200 messages of its last batch; one wave evaluating D
 // time-encoding sin/cos pairs per message ran 84 us (agg_emit), all other waves done long before.
+template <bool EMB = false>
 __device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m, bool grad) {
   __shared__ float red[4][3][8][64];
   __shared__ float rmax[4];
@@ -1188,7 +1221,7 @@ __device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m, bool grad) {
     return;
   }
   const float lun = (float)c.lu_buf[n];
-  const float* rowN = c.mem + n * D;
+  const float* rowN = msg_row<EMB>(c, n, true, m);
   const float* P = c.params;
   const int qa = w * tot / 4, qe = (w + 1) * tot / 4;  // this wave's messages (event order)
   constexpr int AGG_MB = 4;
@@ -1216,10 +1249,11 @@ __device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m, bool grad) {
           const int q = min(qb + u, nq - 1);
           const int64_t e = shfl_i64(e_l, q), o = shfl_i64(o_l, q);
           dt[u] = lane_f(t_l, q) - lun;
+          const float* rowO = msg_row<EMB>(c, o, false, m);
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const int k = min(k0 + lane + 64 * i, Qm - 1);
-            const float* p = k < D ? rowN + k : k < 2 * D ? c.mem + o * D + (k - D)
+            const float* p = k < D ? rowN + k : k < 2 * D ? rowO + (k - D)
                                                   : k < enc0 ? c.ev_msg + e * d + (k - 2 * D) : rowN;
             v[u][i] = *p;
           }
@@ -1304,7 +1338,7 @@ __device__ __forceinline__ int root_row(const Ctx& c, int64_t v) {
 // The rest: mode 0 aggregation over the sampled nodes (train) + zeroing of the backward
 // accumulators, mode 1 last_update of the sampled nodes from the buffer (eval scoring), mode 2
 // aggregation over a node list (eval update / flush; list == nullptr: nodes base + m).
-template <int AG>
+template <int AG, bool EMB = false>
 __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, const int64_t* list,
                                                     const int* list_cnt, int n_host, int64_t base, int nevb = 0) {
   TGNX_STAMP(3);
@@ -1434,12 +1468,12 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
   const int n = mode == 0 ? c.cnt[CNT_M] : (list_cnt ? *list_cnt : n_host);
   if (AG != 0 && c.aggr == 1 && (mode == 0 || list)) {  // MeanAggregator, train / eval update: a workgroup per node (hub
                                              // nodes store many messages); the all-node flush stays wave-per-node
-    for (int m = bid; m < n; m += nb) agg_node_mean_wg(c, mode == 0 ? c.nid[m] : list[m], m, mode == 0);
+    for (int m = bid; m < n; m += nb) agg_node_mean_wg<EMB>(c, mode == 0 ? c.nid[m] : list[m], m, mode == 0);
     return;
   }
   for (int m = bid * 4 + (threadIdx.x >> 6); m < n; m += nb * 4) {
     const int64_t v = mode == 0 ? c.nid[m] : (list ? list[m] : base + m);
-    agg_node<AG>(c, v, m, lane, mode == 0);
+    agg_node<AG, EMB>(c, v, m, lane, mode == 0);
   }
 }
 
@@ -1850,6 +1884,10 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
     if (lane < c.C) {
       z[r][lane] = o.x;
       z[r][c.C + lane] = o.y;
+      if (c.emb) {  // DyRep embedding messages read the centre's embedding (every root of it writes equal values)
+        c.Zc[(int64_t)q.x * c.HC + lane] = o.x;
+        c.Zc[(int64_t)q.x * c.HC + c.C + lane] = o.y;
+      }
     }
     if (lane == 0) scr[r] = q.x;
   } else if (!ATT && wv == 0) {
@@ -2894,8 +2932,9 @@ __device__ __forceinline__ void update_body(const Ctx& c, int blk, int nmem, int
       const int64_t v = list ? list[u] : base + u;
       const int m = mem_mode == 0 ? c.upd_loc[u] : u;
       const int64_t luv = (int64_t)c.lu[m];
+      const float* zrow = c.Zupd && mem_mode == 0 ? c.Zupd + (int64_t)u * c.D : c.Z0 + (int64_t)m * c.D;
       for (int k = lane; k < c.D; k += 64) {
-        const float z = c.Z0[(int64_t)m * c.D + k];
+        const float z = zrow[k];
         c.mem[v * c.D + k] = z;
         if (xr) xr[(int64_t)u * RW + 4 + k] = z;
       }
@@ -3169,7 +3208,8 @@ static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_spli
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
       Ep, alpha, Zc, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
-      snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF, total;
+      snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF,
+      uX, uZ, uG, ulu, uxw, utrel, total;
   int tgp_rows, tgp_e1;
 };
 static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
@@ -3259,6 +3299,14 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.dE2 = carve(off, (size_t)k.E1tr * HC * 4);
   W.pE = carve(off, two ? gemm_partial_floats(shp_dWp2(k, nullptr)) * 4 : 0);
   W.pF = carve(off, two ? gemm_partial_floats(shp_dWe2(k, nullptr)) * 4 : 0);
+  // DyRep embedding messages: the update list's own aggregation / updater rows (train)
+  const size_t U = cfg->emb_in_msg ? (size_t)k.Ucap : 0;
+  W.uX = carve(off, U * k.Qm * 4);
+  W.uZ = carve(off, U * D * 4);
+  W.uG = carve(off, U * 4 * D * 4);
+  W.ulu = carve(off, U * 4);
+  W.uxw = carve(off, U * 8);
+  W.utrel = carve(off, U * 4);
   W.total = off;
   return W;
 }
@@ -3277,6 +3325,10 @@ static int check_cfg(const tgnx_tgn_config* cfg) {
   TGNX_CHECK_ARG(cfg->dropout >= 0.f && cfg->dropout < 1.f, "tgn: bad dropout");
   TGNX_CHECK_ARG(cfg->layers >= 0 && cfg->layers <= 2, "tgn: layers must be 1 or 2, got %d", cfg->layers);
   TGNX_CHECK_ARG(cfg->updater == 0 || cfg->updater == 1, "tgn: updater must be 0 (GRUCell) or 1 (RNNCell)");
+  TGNX_CHECK_ARG(cfg->emb_in_msg >= 0 && cfg->emb_in_msg <= 3,
+                 "tgn: emb_in_msg is bit 0 use_src_emb_in_msg | bit 1 use_dst_emb_in_msg");
+  TGNX_CHECK_ARG(cfg->emb_in_msg == 0 || cfg->layers <= 1,
+                 "tgn: DyRep embedding messages (emb_in_msg) are built for the 1-hop embedding (layers = 1)");
   return TGNX_OK;
 }
 
@@ -3412,6 +3464,8 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.rsel = CNT_R;
   c.ccap = k.Rcap;
   c.att_salt = 7;
+  c.emb = cfg->emb_in_msg;
+  c.zemb = c.Zc;
   if (k.layers == 2) {
     c.rb = reinterpret_cast<uint32_t*>(ws + W.rb);
     c.rbs = reinterpret_cast<uint32_t*>(ws + W.rbs);
@@ -3441,6 +3495,18 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
 
 // 2 hops: the root level as a Ctx for the attention / prediction kernels — centres = roots, node rows =
 // outer centres (P2 = conv2's projections of h1), edges = the roots' ring rows, output Zr
+// the DyRep embedding-message update of a train step: aggregation / updater rows of the update list in their
+// own buffers (the step's GRU rows, gates and aggregated messages are still needed by its backward)
+static Ctx emb_view(const Ctx& c, const WsLay& W, char* ws) {
+  Ctx e = c;
+  e.X = reinterpret_cast<float*>(ws + W.uX);
+  e.Z0 = reinterpret_cast<float*>(ws + W.uZ);
+  e.gates = reinterpret_cast<float*>(ws + W.uG);
+  e.lu = reinterpret_cast<float*>(ws + W.ulu);
+  e.xw = reinterpret_cast<int64_t*>(ws + W.uxw);
+  e.trel = reinterpret_cast<float*>(ws + W.utrel);
+  return e;
+}
 static Ctx root_view(const Ctx& c) {
   Ctx r = c;
   r.cent = c.cent1;
@@ -3482,9 +3548,11 @@ static inline int gridn(int64_t n, int per, int cap = 4096) {
 // the GRU of a node list (eval update / flush): messages -> GRUCell (X, Z0 rows 0..n)
 template <int CELL>
 static void gru_list_c(const Ctx& c, const int64_t* list, const int* list_cnt, int n_host, int64_t base, int mcap,
-                       hipStream_t s) {
+                       hipStream_t s, bool emb = false) {
   using Cl = CellOps<CELL>;
-  if (c.aggr == 0)
+  if (emb)   // DyRep embedding messages (update of src ∪ dst only)
+    tgn_agg_emit<-1, true><<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
+  else if (c.aggr == 0)
     tgn_agg_emit<0><<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
   else
     tgn_agg_emit<-1><<<gridn(mcap, 4, 2048), 256, 0, s>>>(c, 2, 0, list, list_cnt, n_host, base);
@@ -3494,9 +3562,9 @@ static void gru_list_c(const Ctx& c, const int64_t* list, const int* list_cnt, i
 }
 // the memory update of a node list (eval update, flush): aggregation + the memory updater
 static void gru_list(const Ctx& c, const Caps& k, const int64_t* list, const int* list_cnt, int n_host, int64_t base,
-                     int mcap, hipStream_t s) {
-  if (k.cell) gru_list_c<1>(c, list, list_cnt, n_host, base, mcap, s);
-  else gru_list_c<0>(c, list, list_cnt, n_host, base, mcap, s);
+                     int mcap, hipStream_t s, bool emb = false) {
+  if (k.cell) gru_list_c<1>(c, list, list_cnt, n_host, base, mcap, s, emb);
+  else gru_list_c<0>(c, list, list_cnt, n_host, base, mcap, s, emb);
 }
 
 }  // namespace tgn
@@ -3600,6 +3668,9 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     c.adv_seed = adv->seed;
   }
   TGNX_CHECK_ARG(buf->neg && buf->grads && buf->out_pos && buf->out_neg, "tgnx_tgn_train_fwd_bwd: null buffer");
+  // DyRep embedding messages need every embedding of src ∪ dst on this rank: world 1 only
+  TGNX_CHECK_ARG(!c.emb || !buf->xrows, "tgn: DyRep embedding messages (emb_in_msg) are a world-1 step");
+  if (c.emb) c.Zupd = reinterpret_cast<float*>(reinterpret_cast<char*>(buf->ws) + W.uZ);
   if (fuse_adam) {
     TGNX_CHECK_ARG(buf->adam_m && buf->adam_v, "tgnx_tgn_train_step: null optimizer buffer");
     TGNX_CHECK_ARG(!buf->xrows, "tgnx_tgn_train_step: data parallel steps all-reduce before Adam (fwd_bwd + update)");
@@ -3694,6 +3765,14 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     tgn_pred_train<false><<<k.B + nmk, 256, psm, s>>>(cr, nmk);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
+  if (c.emb) {
+    // DyRepMemory.update_state in train order (memory_module.py:322-325): the memory of src ∪ dst from their
+    // stored messages with the embeddings of this batch's forward in place of memory rows (:387-408) — the
+    // stores are still the previous batch's (StoreJob runs later); the fixup writes these rows (Zupd)
+    const Ctx ce = emb_view(c, W, reinterpret_cast<char*>(buf->ws));
+    gru_list_c<CELL>(ce, c.upd, c.cnt + CNT_U, 0, 0, k.Ucap, s, true);
+    TGNX_LAUNCH_CHECK("tgn_emb_update");
+  }
   probe_begin(TGNX_K_SEG_BWD, s);
   if (two) {
     // conv2 backward (‖ predictor reductions) -> dP2, dE2; then dh1 = dP2 [Wq2; Wk2; Wv2; Wsk2] ‖ dW_proj2,
@@ -3978,7 +4057,8 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   const int nst = gridn(2 * k.B, 256), nring = gridn(2 * k.B, 4);
   tgn_update<<<nst + nring, 256, 0, s>>>(c, 0, nst, 1, nullptr, nullptr, 0, 0);
   TGNX_LAUNCH_CHECK("tgn_store_insert");
-  gru_list(c, k, c.upd, c.cnt + CNT_U, 0, 0, k.Ucap, s);
+  // (DyRep embedding messages: the eval forward's embeddings of src ∪ dst, memory_module.py:327-329)
+  gru_list(c, k, c.upd, c.cnt + CNT_U, 0, 0, k.Ucap, s, c.emb != 0);
   TGNX_LAUNCH_CHECK("tgn_gru_update");
   tgn_update<<<gridn(k.Ucap, 4, 1024), 256, 0, s>>>(c, gridn(k.Ucap, 4, 1024), 0, 1, c.upd, c.cnt + CNT_U, 0, 0);
   TGNX_LAUNCH_CHECK("tgn_memory_write");

@@ -48,7 +48,7 @@ class TgnConfig(ctypes.Structure):
                 ("max_batch", ctypes.c_int32), ("max_neg", ctypes.c_int32), ("aggr", ctypes.c_int32),
                 ("dropout", ctypes.c_float), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
                 ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("layers", ctypes.c_int32),
-                ("updater", ctypes.c_int32)]
+                ("updater", ctypes.c_int32), ("emb_in_msg", ctypes.c_int32)]
 
 
 class TgnBuffers(ctypes.Structure):
@@ -113,10 +113,11 @@ class TGNModel(nn.Module):
 
     memory = "tgn": TGNMemory (modules/memory_module.py:25-215) with memory_updater_cell = updater,
     "gru" (GRUCell, the default) or "rnn" (RNNCell, :70-78);
-    memory = "dyrep": DyRepMemory (modules/memory_module.py:218-421) with memory_updater_type = updater
-    and use_src_emb_in_msg = use_dst_emb_in_msg = False: its update order, messages and state-dict names
-    are then TGNMemory's.  Embeddings in the messages need the embedding module's output at update time
-    from a DyRep training loop the reference does not contain; they are refused (NotImplementedError)."""
+    memory = "dyrep": DyRepMemory (modules/memory_module.py:218-421) with memory_updater_type = updater; its
+    use_src_emb_in_msg / use_dst_emb_in_msg (:387-408) build update_state's messages with the batch's
+    embeddings (the TransformerConv output of the same forward: train / eval) in place of the memory rows of
+    endpoints in src ∪ dst (1-hop embedding, world 1).  Without them its update order, messages and
+    state-dict names are TGNMemory's."""
 
     def __init__(self, num_nodes, num_events, msg_dim, hidden_dim, device, ring=10, max_batch=2048, max_neg=1,
                  aggr="last", dropout=0.1, generator=None, layers=1, memory="tgn", updater="gru",
@@ -126,9 +127,11 @@ class TGNModel(nn.Module):
             raise ValueError(f"memory must be 'tgn' or 'dyrep', got {memory!r}")
         if updater not in ("gru", "rnn"):
             raise ValueError(f"Memory updater can be either 'gru' or 'rnn' (memory_module.py:75-78), got {updater!r}")
-        if use_src_emb_in_msg or use_dst_emb_in_msg:
-            raise NotImplementedError("DyRepMemory use_src/dst_emb_in_msg: the embeddings at update time come from a "
-                                      "DyRep training loop the reference does not contain (DESIGN.md §8)")
+        emb = (1 if use_src_emb_in_msg else 0) | (2 if use_dst_emb_in_msg else 0)
+        if emb and memory != "dyrep":
+            raise ValueError("use_src/dst_emb_in_msg are DyRepMemory options (memory='dyrep'; memory_module.py:242-245)")
+        if emb and int(layers) != 1:
+            raise NotImplementedError("DyRep embedding messages are built for the 1-hop embedding (layers = 1)")
         self.memory_type, self.updater = memory, updater
         dev = _lib.require_device(device)
         D, d = int(hidden_dim), int(msg_dim)
@@ -137,7 +140,7 @@ class TGNModel(nn.Module):
         self.cfg = TgnConfig(num_nodes=num_nodes, num_events=num_events, ring=ring, mem_dim=D, msg_dim=d, heads=2,
                              max_batch=max_batch, max_neg=max_neg, aggr=0 if aggr == "last" else 1, dropout=dropout,
                              lr=1e-4, beta1=0.9, beta2=0.999, eps=1e-8, layers=int(layers),
-                             updater=1 if updater == "rnn" else 0)
+                             updater=1 if updater == "rnn" else 0, emb_in_msg=emb)
         if layers not in (1, 2):
             raise ValueError(f"layers must be 1 or 2, got {layers}")
         self.layers = int(layers)
