@@ -378,3 +378,39 @@ def test_tgn_large_batch_partitioned_plans_match_oracle():
     assert torch.allclose(pg.cpu(), po, atol=2e-5) and torch.allclose(ngm.cpu(), no, atol=2e-5)
     assert torch.allclose(model.memory.memory.cpu(), ref.memory.memory, atol=1e-5)
     assert np.array_equal(eng.loader.e_id.cpu().numpy(), lref.e_id)
+
+
+def test_tgn_pipelined_reprepares_after_loader_reset():
+    """A pipelined step prepares the next batch from the ring (marking + scan); a host-side ring change through
+    the loader between steps (here LastNeighborLoader.reset_state, neighbor_loader.py:106-109, called
+    directly on the loader) bumps its version, so the next pipelined step prepares the batch again instead of
+    using the stale scan.  Against a resident twin given the same reset: ring, outputs and memory."""
+    engines = []
+    for pipe in (True, False):
+        s, ref, opt_ref, lref, model, opt, eng = _setup("last")
+        model.cfg.dropout = 0.0
+        eng.pipeline = pipe
+        eng.bind_resident(0, 7 * 50, 50, dropout=False)
+        eng.begin_epoch()
+        if pipe:
+            eng.capture_resident()
+        engines.append((model, opt, eng))
+    (m1, o1, e1), (m2, o2, e2) = engines
+    for st in range(5):
+        if st == 3:
+            for e in (e1, e2):
+                e.loader.reset_state()          # the ring is empty again; the prefetched scan saw it full
+        e1.replay_resident()
+        e2.resident_train_step()
+        torch.cuda.synchronize()
+        e1.check()
+        e2.check()
+        B = int(e2.ctl[2])
+        assert torch.equal(e1.loader.e_id, e2.loader.e_id) and torch.equal(e1.loader.neighbors, e2.loader.neighbors), st
+        assert torch.allclose(e1.out_pos[:B], e2.out_pos[:B], atol=1e-5), st
+        assert torch.allclose(m1.memory.memory, m2.memory.memory, atol=1e-5), st
+        with torch.no_grad():
+            m1.flat.copy_(m2.flat)
+            o1.exp_avg.copy_(o2.exp_avg)
+            o1.exp_avg_sq.copy_(o2.exp_avg_sq)
+            m1.memory.memory.copy_(m2.memory.memory)

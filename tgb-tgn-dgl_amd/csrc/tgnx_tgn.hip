@@ -2,22 +2,26 @@
 // wired as pyg_model_utils.py:10-36, trained by the canonical loop pyg_epoch_utils.py:106-137 carries
 // commented out.  Reference semantics restated in oracle/tgn_ref.py (the checker).
 //
-// One train step (B events, ~13 launches, no host sync):
-//   tgn_mark        negatives, bitmaps of centres (src/pos/neg) and of every sampled node
-//   tgn_scan (3 WG) sorted unique centres + edge offsets + update list, sorted unique nodes + assoc
-//                   ‖ ring-insert plan ‖ message-store sort of the batch
-//   tgn_agg_emit    sampled edges (neighbor_loader.py:26-50 order) ‖ per node: stored messages ->
-//                   IdentityMessage -> Last/Mean aggregate, updated last_update (memory_module.py:152-207)
-//   GEMM G1 ‖ G3    GRUCell over [msg | memory] with the gate math in the epilogue ‖ lin_edge over
-//                   [cos(w Δt + b) | msg] gathered on the fly (the per-neighbour QKV contraction)
-//   GEMM G2         lin_query/key/value/skip of every sampled node
-//   tgn_attn_fwd    TransformerConv softmax + aggregation per centre (wave per centre)
-//   tgn_pred_train  LinkPredictor + BCE + backward rows per event
-//   tgn_attn_bwd    attention backward ‖ predictor bias / output-layer / loss reductions
-//   tgn_kv_reduce   per-edge dk / dv summed into the neighbours' dP rows (sorted runs, no hub contention)
-//                   ‖ dW_edge, dEnc·W_e (the GEMMs that need only dE)
-//   GEMMs           dW_proj, dW_src/dst ‖ dZ0 (+ GRU backward epilogue); dW_gru ‖ message-encoding grads
-//   tgn_adam, tgn_update (memory / last_update of src ∪ dst, message stores, ring merge)
+// One pipelined train step at world 1 (tgnx_tgn_train_step_pipelined, the bench's step): 9 launches, no
+// host sync, graph-replayed.  The previous step already marked and scanned this batch.
+//   1 tgn_agg_emit   sampled edges (neighbor_loader.py:26-50 order) + Δt cos/sin ‖ per sampled node its
+//                    stored messages -> IdentityMessage -> Last/Mean aggregate (memory_module.py:152-207)
+//                    ‖ per-root / per-centre records for the predictor's attention
+//   2 gemmN          ring insert of the batch ‖ GRUCell / RNNCell over [msg | memory] (gate math in the
+//                    epilogue) ‖ lin_edge over [cos(w Δt + b) | msg] (the per-neighbour contraction)
+//   3 gemmN          lin_query / key / value / skip of every sampled node
+//   4 tgn_pred_train per event: TransformerConv forward of its 3 roots (waves 1-3) ‖ predictor weight
+//                    staging (wave 0); LinkPredictor + BCE + backward rows
+//                    (DyRep embedding messages: + one update-list aggregation / updater launch here)
+//   5 tgn_attn_bwd   attention backward ‖ predictor bias / output-layer / loss reductions (+ fused Adam)
+//   6 gemmN          the NEXT batch's marking ‖ per-edge (dk, dv) summed into the neighbours' k / v rows
+//                    ‖ dW_edge (split-K) ‖ dEnc·W_e
+//   7 gemmN          dW_proj, dW_src/dst (split-K) ‖ dz0 = dP W with the cell backward in the epilogue
+//   8 gemmN          dW_cell (split-K) ‖ dX_enc ‖ message stores ‖ step-descriptor snapshot + counters
+//   9 gemm_fixup     the NEXT batch's scan (sorted node sets, insert / store plans) ‖ split-K sums with
+//                    fused Adam ‖ Δt reduction ‖ memory / last_update of src ∪ dst
+// Data parallel (world > 1): the same launches without fused Adam; the exchange (one all-reduce of
+// [gradients | memory-row slots]) and tgnx_tgn_apply_rows_update follow.
 #include "tgnx_gemm.h"
 #include "tgnx_math.h"
 #include "tgnx_ring_dev.h"

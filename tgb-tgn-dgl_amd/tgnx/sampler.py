@@ -25,11 +25,15 @@ class LastNeighborLoader:
         self._ws = torch.empty(0, dtype=torch.uint8, device=dev)
         self._ws_q = -1
         self._counts = torch.zeros(2, dtype=torch.long, device=dev)
+        # bumped by every host-side change of the ring (reset_state / insert): an engine that prepared the
+        # next batch from the ring (pipelined TGN step) re-prepares it when the version moved
+        self.version = 0
         self.reset_state()
 
     # neighbor_loader.py:106-109
     def reset_state(self):
         self.cur_e_id = 0
+        self.version += 1
         _lib.call("tgnx_ring_reset", _lib.ptr(self.e_id), _lib.ptr(self.t), self.num_nodes, self.size,
                   _lib.stream(self.device))
 
@@ -73,3 +77,4 @@ class LastNeighborLoader:
                   self.num_nodes, self.size, _lib.ptr(src), _lib.ptr(dst), _lib.ptr(t), B, self.cur_e_id,
                   _lib.ptr(self._assoc), _lib.stream(self.device))
         self.cur_e_id += B
+        self.version += 1

@@ -301,6 +301,7 @@ class TgnEngine:
         # is in flight (tgnx_tgn_train_fwd_bwd_split + tgnx_tgn_scan_next)
         self.split_scan = True
         self._prefetched = False
+        self._prefetch_version = None
         if optimizer is None:
             self.adam_m, self.adam_v = torch.zeros_like(model.flat), torch.zeros_like(model.flat)
         else:
@@ -510,11 +511,20 @@ class TgnEngine:
         elif between is not None:
             between()
 
+    def _prefetch_valid(self) -> bool:
+        """The previous pipelined step's preparation of this batch still holds: no other engine call since
+        (tracked by _prefetched) and no host-side change of the ring through the loader (its version)."""
+        return self._prefetched and getattr(self.loader, "version", None) == self._prefetch_version
+
+    def _mark_prefetched(self):
+        self._prefetched = self._pipelined()
+        self._prefetch_version = getattr(self.loader, "version", None)
+
     def resident_train_step(self):
-        self._pre(self._prefetched)
+        self._pre(self._prefetch_valid())
         self._allreduce(self._scan_next)
         self._post()
-        self._prefetched = self._pipelined()
+        self._mark_prefetched()
 
     def capture_resident(self):
         """One resident step as HIP graph(s) (world > 1: the collectives stay eager between them)."""
@@ -543,14 +553,14 @@ class TgnEngine:
 
     def replay_resident(self):
         g1, g2, gs = self._graphs
-        if self._pipelined() and not self._prefetched:
+        if self._pipelined() and not self._prefetch_valid():
             self.resident_train_step()   # marks + scans this batch first (eager), prefetches the next
             return
         g1.replay()
         if g2 is not None:
             self._allreduce(gs.replay if gs is not None else None)
             g2.replay()
-        self._prefetched = self._pipelined()
+        self._mark_prefetched()
 
     def units(self):
         """(sum of sampled edges, sum of sampled nodes) since the last reset."""
