@@ -382,13 +382,6 @@ def tgn_launch_bytes(name, E, M, Bw, Bg, D, d, K, P, N):
     return 0
 
 
-def _probe_floor_us(n=200):
-    from tgnx import _lib
-    ms = ctypes.c_double()
-    _lib.call("tgnx_probe_floor", n, _lib.stream(), ctypes.byref(ms))
-    return ms.value * 1e3
-
-
 def _pmc(workload_ok):
     """profiles/pmc_traffic.json (tools/pmc_traffic.sh on the default workload): bytes per launch."""
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -493,10 +486,8 @@ def run_tgn(args, world, rank, dev):
         algo = tgn_launch_bytes(name, E, M, Bw, Bg, D, d, K, P, N) * (steps_n / launches if name != "tgn_scan" else 1)
         probes[name] = dict(avg_us=avg_ms * 1e3, launches=launches, edges=E, nodes=M, bytes=algo,
                             gbs=(algo / (avg_ms * 1e-3) / 1e9) if algo else None)
-    floor_us = _probe_floor_us()
     dom = max(probes, key=lambda k: probes[k]["avg_us"])        # the longest launch of the step
     pd = probes[dom]
-    k_us = max(pd["avg_us"] - floor_us, 1e-3)
     Qm = 3 * D + d
     flops_gru_edge = None
     if "tgn_gru_edge" in probes:
@@ -512,10 +503,6 @@ def run_tgn(args, world, rank, dev):
         "frac": round(pd["gbs"] / HBM_PEAK_GBS, 5),
         "traffic": pmc.get(dom, {}).get("bytes_per_launch"),
         "avg_launch_us": round(pd["avg_us"], 3), "algo_bytes_per_launch": round(pd["bytes"]),
-        "probe_floor_us": round(floor_us, 3),
-        "kernel_us_est": round(k_us, 3),
-        "achieved_kernel_est": round(pd["bytes"] / (k_us * 1e-6) / 1e9, 2),
-        "frac_kernel_est": round(pd["bytes"] / (k_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
         "step_algo_bytes": round(step_algo),
         "step_frac": round(step_algo / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
         "pmc_step_bytes": pmc_step,
@@ -523,8 +510,9 @@ def run_tgn(args, world, rank, dev):
         "bytes_model": "per launch: DESIGN.md §5b (bench.tgn_launch_bytes; per sampled edge 20 + 4d + 4D + 4, "
                        "SURVEY §8d, plus per-node message / GRU rows, 28 B per parameter for Adam); step: SURVEY "
                        "§8(d) B_ev(train) x events per GPU (bench.tgn_step_bytes)",
-        "timing": "avg_launch_us: HIP-event pair around the eager launch (includes dispatch); kernel_us_est: minus "
-                  "the event-pair time of an empty launch (probe_floor_us); rocprofv3 durations: profiles/",
+        "timing": "avg_launch_us: the kernel's own begin / end timestamps (hipExtLaunchKernelGGL start / stop "
+                  "events bound to the dispatch, on its launch stream: what rocprofv3 --kernel-trace reports), "
+                  "eager launches of the same step; rocprofv3 summary of the same command: profiles/r3/",
         "units_window": "probe windows count batches k+1..k+n (pipelined prefetch), stationary stream",
     }
     if flops_gru_edge:

@@ -84,9 +84,12 @@ int tgnx_block_ids_host(const int64_t* src, const int64_t* dst, int64_t num_even
 
 /* ------------------------------------------------------------------------
  * Kernel probe (measurement only): while enabled, every launch of kernel
- * `kernel_id` (TGNX_K_*) is bracketed by a pair of hipEvents recorded on the
- * launch stream; tgnx_probe_read waits for them and returns the summed
- * duration (ms) and the launch count, then clears.  Off by default.
+ * `kernel_id` (TGNX_K_*) is timed on its launch stream — TGN launches by a pair
+ * of hipEvents bound to the dispatch itself (hipExtLaunchKernelGGL start / stop:
+ * the kernel's begin / end timestamps, as rocprofv3 --kernel-trace reports),
+ * other launches by marker events around them (dispatch included);
+ * tgnx_probe_read waits for them and returns the summed duration (ms) and the
+ * launch count, then clears.  Off by default.
  * ------------------------------------------------------------------------ */
 #define TGNX_K_EDGE_FWD 1       /* tgnn_edge_fwd  */
 #define TGNX_K_EDGE_BWD 2       /* tgnn_edge_bwd  */
@@ -102,9 +105,6 @@ int tgnx_block_ids_host(const int64_t* src, const int64_t* dst, int64_t num_even
 #define TGNX_K_WGRAD3 12         /* TGN: dW_gru ‖ dX_enc ‖ message stores ‖ descriptor snapshot launch */
 int tgnx_probe_enable(int32_t kernel_id);
 int tgnx_probe_read(double* total_ms, int64_t* launches);
-/* The probe floor: average event-pair time around n launches of an empty kernel on `stream` (dispatch +
- * completion of a launch without work), so that probe averages minus it estimate kernel durations. */
-int tgnx_probe_floor(int32_t n, void* stream, double* avg_ms);
 /* Workgroup timeline stamps (diagnostic; measurement only): a library built with -DTGNX_STAMPS records, for
  * wave 0 of every workgroup of the TGN step's kernels, {start, end} (s_memrealtime ticks, 100 MHz), kernel
  * id, block and XCC as 32-byte records into `buf`: 64 shards (by block) of cap / 64 records, shard s at

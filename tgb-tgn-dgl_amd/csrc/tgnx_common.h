@@ -1,6 +1,7 @@
 // Shared device/host helpers for libtgnx (gfx950 / CDNA4, wave64).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -39,6 +40,19 @@ void set_error(const char* fmt, ...);
       return TGNX_EHIP;                                                          \
     }                                                                            \
   } while (0)
+
+// kernel probe (tgnx_host.cpp): inside an open probe region, the first launch through launch_k binds the
+// probe's kernel event pair to itself (hipExtLaunchKernelGGL start / stop events = the dispatch's own begin /
+// end timestamps); every other launch is a plain one.
+bool probe_take(hipEvent_t* k0, hipEvent_t* k1);
+template <typename... KArgs, typename... Args>
+inline void launch_k(void (*kern)(KArgs...), dim3 grid, dim3 block, uint32_t smem, hipStream_t s, Args... args) {
+  hipEvent_t k0, k1;
+  if (probe_take(&k0, &k1))
+    hipExtLaunchKernelGGL(kern, grid, block, smem, s, k0, k1, 0, args...);
+  else
+    hipLaunchKernelGGL(kern, grid, block, smem, s, args...);
+}
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -629,7 +629,7 @@ __global__ void __launch_bounds__(256) gemmN_kernel(J... j) {
 template <class... J>
 static inline void gemmN_launch(hipStream_t s, const J&... j) {
   const int nb = (job_blocks(j) + ... + 0);
-  if (nb > 0) gemmN_kernel<J...><<<nb, 256, 0, s>>>(j...);
+  if (nb > 0) launch_k(gemmN_kernel<J...>, dim3(nb), dim3(256), 0, s, j...);
 }
 
 // ---------------------------------------------------------------- split-K fixup
@@ -764,7 +764,7 @@ template <class CFG, class AL, class BL, class EPI>
 static inline void gemm_launch(const GemmShape& g, const AL& al, const BL& bl, const EPI& epi, float* part,
                                hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0) return;
-  gemm_kernel<CFG, AL, BL, EPI><<<gemm_blocks(g), 256, 0, s>>>(g, al, bl, epi, part);
+  launch_k(gemm_kernel<CFG, AL, BL, EPI>, dim3(gemm_blocks(g)), dim3(256), 0, s, g, al, bl, epi, part);
 }
 template <class C1, class C2, class AL1, class BL1, class EP1, class AL2, class BL2, class EP2>
 static inline void gemm2_launch(const GemmShape& g1, const AL1& a1, const BL1& b1, const EP1& e1, float* p1,
@@ -776,13 +776,13 @@ static inline void gemm2_launch(const GemmShape& g1, const AL1& a1, const BL1& b
 template <class TAIL, class... F>
 static inline void gemm_fixup_launch(int tail_blocks, const TAIL& tail, hipStream_t s, const F&... f) {
   const int nb = (gemm_fix_blocks(f) + ... + 0) + tail_blocks;
-  if (nb > 0) gemm_fixup_kernel<TAIL, F...><<<nb, 256, 0, s>>>(tail, 0, f...);
+  if (nb > 0) launch_k(gemm_fixup_kernel<TAIL, F...>, dim3(nb), dim3(256), 0, s, tail, 0, f...);
 }
 // the same with `head` of the tail blocks first in the grid
 template <class TAIL, class... F>
 static inline void gemm_fixup_launch_h(int head, int tail_blocks, const TAIL& tail, hipStream_t s, const F&... f) {
   const int nb = (gemm_fix_blocks(f) + ... + 0) + tail_blocks;
-  if (nb > 0) gemm_fixup_kernel<TAIL, F...><<<nb, 256, 0, s>>>(tail, head, f...);
+  if (nb > 0) launch_k(gemm_fixup_kernel<TAIL, F...>, dim3(nb), dim3(256), 0, s, tail, head, f...);
 }
 
 }  // namespace tgnx

@@ -1,8 +1,6 @@
 // C ABI of the MFMA GEMM (tgnx_gemm.h): C = op(A) op(B) (+ bias) (+ C).
 #include "tgnx_gemm.h"
 
-#include <vector>
-
 using namespace tgnx;
 
 // Tile config: 64x64 once that already fills the chip, else 32x32.  K up to 4 chunks: one workgroup
@@ -55,36 +53,6 @@ int tgnx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, 
   else
     run(LoadKRow{A, (int)M, Kc, (int)lda}, LoadKRow{B, (int)N, Kc, (int)ldb});
   TGNX_LAUNCH_CHECK("tgnx_gemm_f32");
-  return TGNX_OK;
-}
-
-// the floor of a kernel probe: an event pair around a launch of an empty kernel (1 workgroup) costs
-// the dispatch and completion of a launch with no work; bench.py subtracts it from probe averages
-// to estimate the kernel's own duration (what rocprofv3 --kernel-trace reports)
-__global__ void tgnx_empty_kernel() {}
-
-int tgnx_probe_floor(int32_t n, void* stream, double* avg_ms) {
-  TGNX_CHECK_ARG(n > 0 && n <= 4096 && avg_ms, "tgnx_probe_floor: bad arguments");
-  hipStream_t s = as_stream(stream);
-  // back to back, as the probed launches of a step run (a sync per launch would add the idle GPU's wake-up)
-  std::vector<hipEvent_t> ev(2 * (size_t)n);
-  for (auto& e : ev) TGNX_HIP_CHECK(hipEventCreate(&e));
-  for (int i = 0; i < n; ++i) {
-    (void)hipEventRecord(ev[2 * i], s);
-    tgnx_empty_kernel<<<1, 64, 0, s>>>();
-    (void)hipEventRecord(ev[2 * i + 1], s);
-  }
-  const hipError_t le = hipGetLastError();
-  TGNX_HIP_CHECK(hipEventSynchronize(ev[2 * (size_t)n - 1]));
-  double ms = 0.0;
-  for (int i = 0; i < n; ++i) {
-    float f = 0.f;
-    (void)hipEventElapsedTime(&f, ev[2 * i], ev[2 * i + 1]);
-    ms += f;
-  }
-  for (auto& e : ev) (void)hipEventDestroy(e);
-  TGNX_HIP_CHECK(le);
-  *avg_ms = ms / n;
   return TGNX_OK;
 }
 

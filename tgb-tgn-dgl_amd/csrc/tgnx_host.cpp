@@ -25,29 +25,50 @@ void set_error(const char* fmt, ...) {
 
 namespace tgnx {
 // ------------------------------------------------------------------ kernel probe
+// Each probed region records a marker-event pair around it (probe_begin / probe_end: includes the launch's
+// dispatch); the region's first launch through launch_k (tgnx_common.h) also binds a second pair to the
+// kernel itself (hipExtLaunchKernelGGL start / stop events: the dispatch packet's begin / end timestamps,
+// the duration rocprofv3 --kernel-trace reports).  tgnx_probe_read prefers the kernel-bound pair.
 struct Probe {
   int id = 0;
-  std::vector<hipEvent_t> ev;  // start/stop pairs
-  size_t used = 0;
+  std::vector<hipEvent_t> ev;  // per record: marker start, marker stop, kernel start, kernel stop
+  std::vector<char> bound;     // per record: the kernel pair was bound
+  size_t used = 0;             // records
+  bool open = false;           // a region is open (between probe_begin and probe_end)
+  bool armed = false;          // ... and its kernel pair is still unbound
 };
 static Probe g_probe;
 
-void probe_begin(int id, hipStream_t s) {
-  if (g_probe.id != id) return;
-  if (g_probe.used + 2 > g_probe.ev.size()) {
-    size_t n = g_probe.ev.size() ? g_probe.ev.size() * 2 : 512;
-    while (g_probe.ev.size() < n) {
-      hipEvent_t e;
-      if (hipEventCreate(&e) != hipSuccess) return;
-      g_probe.ev.push_back(e);
-    }
+static bool probe_grow() {
+  if ((g_probe.used + 1) * 4 <= g_probe.ev.size()) return true;
+  const size_t n = std::max<size_t>(2048, g_probe.ev.size() * 2);
+  while (g_probe.ev.size() < n) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return false;
+    g_probe.ev.push_back(e);
   }
-  (void)hipEventRecord(g_probe.ev[g_probe.used], s);
+  g_probe.bound.resize(n / 4, 0);
+  return true;
+}
+void probe_begin(int id, hipStream_t s) {
+  if (g_probe.id != id || !probe_grow()) return;
+  g_probe.open = g_probe.armed = true;
+  g_probe.bound[g_probe.used] = 0;
+  (void)hipEventRecord(g_probe.ev[4 * g_probe.used], s);
+}
+bool probe_take(hipEvent_t* k0, hipEvent_t* k1) {
+  if (!g_probe.armed) return false;
+  g_probe.armed = false;
+  g_probe.bound[g_probe.used] = 1;
+  *k0 = g_probe.ev[4 * g_probe.used + 2];
+  *k1 = g_probe.ev[4 * g_probe.used + 3];
+  return true;
 }
 void probe_end(int id, hipStream_t s) {
-  if (g_probe.id != id || g_probe.used + 2 > g_probe.ev.size()) return;
-  (void)hipEventRecord(g_probe.ev[g_probe.used + 1], s);
-  g_probe.used += 2;
+  if (g_probe.id != id || !g_probe.open) return;
+  (void)hipEventRecord(g_probe.ev[4 * g_probe.used + 1], s);
+  g_probe.open = g_probe.armed = false;
+  g_probe.used += 1;
 }
 }  // namespace tgnx
 
@@ -56,22 +77,25 @@ extern "C" {
 int tgnx_probe_enable(int32_t kernel_id) {
   tgnx::g_probe.id = kernel_id;
   tgnx::g_probe.used = 0;
+  tgnx::g_probe.open = tgnx::g_probe.armed = false;
   return TGNX_OK;
 }
 
 int tgnx_probe_read(double* total_ms, int64_t* launches) {
   double ms = 0.0;
-  for (size_t i = 0; i + 1 < tgnx::g_probe.used; i += 2) {
-    if (hipEventSynchronize(tgnx::g_probe.ev[i + 1]) != hipSuccess) {
+  for (size_t i = 0; i < tgnx::g_probe.used; ++i) {
+    const bool k = tgnx::g_probe.bound[i] != 0;
+    hipEvent_t a = tgnx::g_probe.ev[4 * i + (k ? 2 : 0)], b = tgnx::g_probe.ev[4 * i + (k ? 3 : 1)];
+    if (hipEventSynchronize(tgnx::g_probe.ev[4 * i + 1]) != hipSuccess) {
       tgnx::set_error("tgnx_probe_read: event sync failed");
       return TGNX_EHIP;
     }
     float f = 0.f;
-    (void)hipEventElapsedTime(&f, tgnx::g_probe.ev[i], tgnx::g_probe.ev[i + 1]);
+    (void)hipEventElapsedTime(&f, a, b);
     ms += f;
   }
   if (total_ms) *total_ms = ms;
-  if (launches) *launches = (int64_t)(tgnx::g_probe.used / 2);
+  if (launches) *launches = (int64_t)tgnx::g_probe.used;
   tgnx::g_probe.used = 0;
   return TGNX_OK;
 }

@@ -3707,10 +3707,12 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   probe_begin(TGNX_K_EDGE_META, s);
   const int nevb = gridn(3 * k.B * (c.evj ? 16 : 1), 256);
   const int nagg = nevb + nedge + gridn(k.Mtr, 4, TGNX_AGG_NODE_CAP);
+  const int64_t* nol = nullptr;
+  const int* noc = nullptr;
   if (c.aggr == 0 && TGNX_AGG_SPECIALIZE)
-    tgn_agg_emit<0><<<nagg, 256, 0, s>>>(c, 0, nedge, nullptr, nullptr, 0, 0, nevb);
+    launch_k(tgn_agg_emit<0>, dim3(nagg), dim3(256), 0, s, c, 0, nedge, nol, noc, 0, (int64_t)0, nevb);
   else
-    tgn_agg_emit<-1><<<nagg, 256, 0, s>>>(c, 0, nedge, nullptr, nullptr, 0, 0, nevb);
+    launch_k(tgn_agg_emit<-1>, dim3(nagg), dim3(256), 0, s, c, 0, nedge, nol, noc, 0, (int64_t)0, nevb);
   probe_end(TGNX_K_EDGE_META, s);
   TGNX_LAUNCH_CHECK("tgn_agg_emit");
   // GRU over every sampled node ‖ lin_edge over every sampled edge (‖ 2 hops: conv2's lin_edge over the
@@ -3747,7 +3749,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const bool att_in_pred = !two && TGNX_PRED_ATT;
   if (!att_in_pred) {
     probe_begin(TGNX_K_SEG_FWD, s);
-    tgn_attn_fwd<true><<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c);
+    launch_k(tgn_attn_fwd<true>, dim3(gridn(k.Rtr, 4, 1 << 20)), dim3(256), 0, s, c);
     probe_end(TGNX_K_SEG_FWD, s);
     TGNX_LAUNCH_CHECK("tgn_attn_fwd");
   }
@@ -3764,9 +3766,9 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const int nmk = pipe && TGNX_PIPE_MARK_AT == 5 ? nmark : 0;
   const size_t psm = std::max(tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0);
   if (att_in_pred)
-    tgn_pred_train<true><<<k.B + nmk, 256, psm, s>>>(cr, nmk);
+    launch_k(tgn_pred_train<true>, dim3(k.B + nmk), dim3(256), (uint32_t)psm, s, cr, nmk);
   else
-    tgn_pred_train<false><<<k.B + nmk, 256, psm, s>>>(cr, nmk);
+    launch_k(tgn_pred_train<false>, dim3(k.B + nmk), dim3(256), (uint32_t)psm, s, cr, nmk);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
   if (c.emb) {
@@ -3801,7 +3803,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     tgn_attn_bwd<<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c, gridn(k.Rtr, 4, 1 << 20));
   } else {
     const int ncb = gridn(k.Rtr, 4, 1 << 20);
-    tgn_attn_bwd<<<ncb + gridn(3 * D + 2, 4), 256, 0, s>>>(c, ncb);
+    launch_k(tgn_attn_bwd, dim3(ncb + gridn(3 * D + 2, 4)), dim3(256), 0, s, c, ncb);
   }
   probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_attn_bwd");

@@ -30,7 +30,6 @@ SIGNATURES = {
     "tgnx_block_ids_host": (ctypes.c_int, [P, P, c_i64, c_i64, P]),
     "tgnx_probe_enable": (ctypes.c_int, [c_i32]),
     "tgnx_probe_read": (ctypes.c_int, [P, P]),
-    "tgnx_probe_floor": (ctypes.c_int, [c_i32, c_vp, P]),
     "tgnx_stamps_set": (ctypes.c_int, [P, ctypes.c_uint32]),
     "tgnx_stamps_count": (c_i64, []),
     "tgnx_tgnn_param_layout": (ctypes.c_int, [P, P]),

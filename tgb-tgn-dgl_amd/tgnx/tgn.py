@@ -312,6 +312,9 @@ class TgnEngine:
         # other slots zero), so the sum of the row part is the all-gather.  tgnx_tgn_apply_rows writes
         # them into memory / last_update on every rank and zeroes the slots for the next step.
         self.xrows = self.xgather = self.comm = None
+        # the exchange collective: torch.distributed.all_reduce over the default group, unless a callable
+        # (comm, async_op) -> work | None is set here (tools/dp_compute.py: a stand-in without a collective)
+        self.exchange = None
         if self.world > 1:
             self.xcap = min(cfg.num_nodes, 2 * (-(-cfg.max_batch // self.world)))
             rw = cfg.mem_dim + 4
@@ -414,6 +417,9 @@ class TgnEngine:
     def _exchange(self):
         """The step's one collective: gradient sum and the touched memory rows of every rank (an
         all-gather carried by the same all-reduce, see __init__)."""
+        if self.exchange is not None:
+            self.exchange(self.comm, False)
+            return
         import torch.distributed as dist
         dist.all_reduce(self.comm)
 
@@ -503,11 +509,15 @@ class TgnEngine:
     def _allreduce(self, between=None):
         """The exchange; `between` (the next batch's scan) runs on the compute stream while it is in flight."""
         if self.world > 1:
-            import torch.distributed as dist
-            work = dist.all_reduce(self.comm, async_op=True)
+            if self.exchange is not None:
+                work = self.exchange(self.comm, True)
+            else:
+                import torch.distributed as dist
+                work = dist.all_reduce(self.comm, async_op=True)
             if between is not None:
                 between()
-            work.wait()
+            if work is not None:
+                work.wait()
         elif between is not None:
             between()
 
