@@ -1313,6 +1313,124 @@ __device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m, bool grad) {
   }
 }
 
+// The same MeanAggregator (train step, d <= 192) with lanes over the message's COLUMN CLASSES instead of
+// 8 generic X columns: per message a lane loads only what varies — its 2 columns of the other endpoint's
+// memory row and its <= 3 raw-message columns (the node's own row is loaded once, the D encoding columns
+// are computed) — so 16 messages' rows are in flight per round instead of 4: a hub node of the
+// review-shaped stream (~50 messages per wave) walks 4 dependent load rounds instead of 13.  Sums run in
+// the same order as agg_node_mean_wg (per wave in event order, waves combined 0..3): bit-identical X rows.
+constexpr int AGG_MC = 16;  // messages whose rows are loaded in one round
+template <bool EMB = false>
+__device__ void agg_node_mean_cols(const Ctx& c, int64_t n, int m, bool grad) {
+  __shared__ float red[4][3 * TDMAX + 192 + 2 * TDMAX];  // per wave: X columns (Qm) | sin sums | sin·Δt sums
+  __shared__ float rmax[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int D = c.D, d = c.d, Qm = c.Qm, enc0 = 2 * D + d;
+  const StoreView sv = store_view(c, n);
+  const int tot = (int)sv.tot;
+  float* X = c.X + (int64_t)m * Qm;
+  if (tot == 0) {  // workgroup-uniform
+    if (w == 0) {
+      for (int k = lane; k < Qm; k += 64) X[k] = 0.f;
+      if (grad)
+        for (int q = lane; q < D; q += 64) c.s0m[(int64_t)m * D + q] = c.s1m[(int64_t)m * D + q] = 0.f;
+      if (lane == 0) {
+        c.xw[m] = -1;
+        c.trel[m] = 0.f;
+        c.lu[m] = 0.f;
+      }
+    }
+    return;
+  }
+  const float lun = (float)c.lu_buf[n];
+  const float* rowN = msg_row<EMB>(c, n, true, m);
+  const float* P = c.params;
+  // this lane's columns: memory / encoding j = lane + 64 a (j < D), raw r = lane + 64 b (r < d)
+  float nv[2], tw[2], tb[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int j = min(lane + 64 * a, D - 1);
+    nv[a] = rowN[j];
+    tw[a] = P[c.L.te_w + j];
+    tb[a] = P[c.L.te_b + j];
+  }
+  float sN[2] = {0.f, 0.f}, sO[2] = {0.f, 0.f}, sC[2] = {0.f, 0.f}, s0[2] = {0.f, 0.f}, s1[2] = {0.f, 0.f};
+  float sR[3] = {0.f, 0.f, 0.f};
+  const int qa = w * tot / 4, qe = (w + 1) * tot / 4;  // this wave's messages (event order)
+  float tmax = -INFINITY;
+  for (int q0 = qa; q0 < qe; q0 += 64) {
+    int64_t e_l, o_l;
+    float t_l;
+    store_event(c, sv, q0 + lane, e_l, o_l, t_l);
+    if (q0 + lane < qe) tmax = fmaxf(tmax, t_l);
+    const int nq = min(64, qe - q0);
+    for (int qb = 0; qb < nq; qb += AGG_MC) {
+      float vo[AGG_MC][2], vr[AGG_MC][3];
+#pragma unroll
+      for (int u = 0; u < AGG_MC; ++u) {
+        const int q = min(qb + u, nq - 1);
+        const int64_t e = shfl_i64(e_l, q), o = shfl_i64(o_l, q);
+        const float* rowO = msg_row<EMB>(c, o, false, m);
+        const float* raw = c.ev_msg + e * d;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) vo[u][a] = rowO[min(lane + 64 * a, D - 1)];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) vr[u][b] = raw[min(lane + 64 * b, d - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < AGG_MC; ++u) {
+        if (qb + u >= nq) break;
+        const float dt = lane_f(t_l, qb + u) - lun;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          float sn, cs;
+          te_sincos(fmaf(tw[a], dt, tb[a]), sn, cs);
+          sN[a] += nv[a];
+          sO[a] += vo[u][a];
+          sC[a] += cs;
+          s0[a] += sn;
+          s1[a] += sn * dt;
+        }
+#pragma unroll
+        for (int b = 0; b < 3; ++b) sR[b] += vr[u][b];
+      }
+    }
+  }
+  float* rw = red[w];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int j = lane + 64 * a;
+    if (j < D) {
+      rw[j] = sN[a];
+      rw[D + j] = sO[a];
+      rw[enc0 + j] = sC[a];
+      rw[Qm + j] = s0[a];
+      rw[Qm + D + j] = s1[a];
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+    if (lane + 64 * b < d) rw[2 * D + lane + 64 * b] = sR[b];
+  const float wm = wave_max_f(tmax);
+  if (lane == 0) rmax[w] = wm;
+  __syncthreads();
+  const float inv = 1.0f / (float)tot;
+  for (int k = threadIdx.x; k < Qm; k += blockDim.x)
+    X[k] = (((red[0][k] + red[1][k]) + red[2][k]) + red[3][k]) / (float)tot;
+  if (grad)
+    for (int j = threadIdx.x; j < D; j += blockDim.x) {
+      const int k0 = Qm + j, k1 = Qm + D + j;
+      c.s0m[(int64_t)m * D + j] = (((red[0][k0] + red[1][k0]) + red[2][k0]) + red[3][k0]) * inv;
+      c.s1m[(int64_t)m * D + j] = (((red[0][k1] + red[1][k1]) + red[2][k1]) + red[3][k1]) * inv;
+    }
+  if (threadIdx.x == 0) {
+    c.xw[m] = 1;
+    c.trel[m] = 0.f;
+    c.lu[m] = fmaxf(fmaxf(rmax[0], rmax[1]), fmaxf(rmax[2], rmax[3]));
+  }
+  __syncthreads();
+}
+
 // last_update the GRU step gives node u (memory_module.py:175-176): max t over its stored messages, 0
 // without messages (PyG scatter 'max' fill); wave-uniform
 __device__ float store_tmax(const Ctx& c, int64_t u, int lane) {
@@ -1472,9 +1590,14 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
   const int n = mode == 0 ? c.cnt[CNT_M] : (list_cnt ? *list_cnt : n_host);
   if (AG != 0 && c.aggr == 1 && (mode == 0 || list)) {  // MeanAggregator, train / eval update: a workgroup per node (hub
                                              // nodes store many messages); the all-node flush stays wave-per-node
-    for (int m = bid; m < n; m += nb) agg_node_mean_wg<EMB>(c, mode == 0 ? c.nid[m] : list[m], m, mode == 0);
+    if (AG == 1 || c.d <= 192) {  // (AG == 1 is launched for d <= 192 only)
+      for (int m = bid; m < n; m += nb) agg_node_mean_cols<EMB>(c, mode == 0 ? c.nid[m] : list[m], m, mode == 0);
+    } else {
+      for (int m = bid; m < n; m += nb) agg_node_mean_wg<EMB>(c, mode == 0 ? c.nid[m] : list[m], m, mode == 0);
+    }
     return;
   }
+  if constexpr (AG == 1) return;  // (launched for train steps only: the mean path above)
   for (int m = bid * 4 + (threadIdx.x >> 6); m < n; m += nb * 4) {
     const int64_t v = mode == 0 ? c.nid[m] : (list ? list[m] : base + m);
     agg_node<AG, EMB>(c, v, m, lane, mode == 0);
@@ -3711,6 +3834,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const int* noc = nullptr;
   if (c.aggr == 0 && TGNX_AGG_SPECIALIZE)
     launch_k(tgn_agg_emit<0>, dim3(nagg), dim3(256), 0, s, c, 0, nedge, nol, noc, 0, (int64_t)0, nevb);
+  else if (c.aggr == 1 && c.d <= 192 && TGNX_AGG_SPECIALIZE)
+    launch_k(tgn_agg_emit<1>, dim3(nagg), dim3(256), 0, s, c, 0, nedge, nol, noc, 0, (int64_t)0, nevb);
   else
     launch_k(tgn_agg_emit<-1>, dim3(nagg), dim3(256), 0, s, c, 0, nedge, nol, noc, 0, (int64_t)0, nevb);
   probe_end(TGNX_K_EDGE_META, s);
