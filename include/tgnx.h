@@ -366,6 +366,18 @@ int tgnx_tgn_train_step_resident(const tgnx_tgn_config* cfg, const tgnx_tgn_buff
 int tgnx_tgn_train_step_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
                                   int64_t split_hi, int64_t batch, uint64_t base_seed, int32_t dropout,
                                   int32_t prefetched, void* stream);
+/* tgnx_tgn_train_step_pipelined with two parities of the scan's per-batch outputs (sorted node / centre sets,
+ * edge offsets, update list, insert / store plans, counts) in the workspace: a step reads set `parity`
+ * while the next batch is marked in its predictor launch and scanned into set 1 - parity inside its k / v
+ * reduction launch, so its last launch (split-K sums, Adam, memory update) no longer waits for the scan.
+ * Alternate parity 0, 1, 0, ... across consecutive calls (two HIP graphs); prefetched as for
+ * tgnx_tgn_train_step_pipelined (prefetched = 0 marks + scans this batch into set `parity` first).  A step
+ * whose set holds another batch (wrong parity) sets ctl[ERR] bit 16 and computes nothing after its first
+ * launch.  World 1, 1 hop (layers = 1); other calls use set 0 and scan for themselves.  Results equal
+ * tgnx_tgn_train_step_pipelined's step for step.  Test: tests/test_gpu_tgn.py (pp vs resident). */
+int tgnx_tgn_train_step_pp(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                           int64_t split_hi, int64_t batch, uint64_t base_seed, int32_t dropout, int32_t prefetched,
+                           int32_t parity, void* stream);
 /* Data parallel form: tgnx_tgn_train_fwd_bwd with the folded cursor (the exchange, tgnx_tgn_apply_rows and
  * tgnx_tgn_train_update follow).  ctl words as for tgnx_tgn_train_step_resident: the descriptor is written
  * by the first launch, NB / GEN / ADAM_T advance in the last launch of THIS call, so they have advanced

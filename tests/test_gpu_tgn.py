@@ -277,21 +277,27 @@ def test_tgn_resident_folded_cursor_equals_advance_plus_step():
             m1.memory.memory.copy_(m2.memory.memory)
 
 
+@pytest.mark.parametrize("pp", [True, False])
 @pytest.mark.parametrize("layers,updater,emb", [(1, "gru", (0, 0)), (2, "gru", (0, 0)), (1, "rnn", (0, 0)),
                                                 (1, "rnn", (1, 1))])
-def test_tgn_pipelined_equals_resident(layers, updater, emb):
+def test_tgn_pipelined_equals_resident(layers, updater, emb, pp):
     """tgnx_tgn_train_step_pipelined (each step marks the next batch inside its predictor launch and scans it
-    after its last launch; ring insert beside the GRU) against tgnx_tgn_train_step_resident on a twin
-    engine: graph replay (the first step eager with prefetched = 0), device negatives, attention dropout,
-    a partial last batch and a step past the split.  After every step: step counters and the ring exactly,
-    this batch's negatives exactly (the pipelined engine has drawn the next batch's too), outputs,
-    parameters and memory within the fused-Adam tolerances (resynchronised per step)."""
+    after its last launch; ring insert beside the GRU) — or, pp (1 hop), tgnx_tgn_train_step_pp (the next batch
+    scanned into the other parity's set inside the k / v reduction launch, two graphs replayed alternately) —
+    against tgnx_tgn_train_step_resident on a twin engine: graph replay (the first step eager with
+    prefetched = 0), device negatives, attention dropout, a partial last batch and a step past the split.
+    After every step: step counters and the ring exactly, this batch's negatives exactly (the pipelined
+    engine has drawn the next batch's too), outputs, parameters and memory within the fused-Adam tolerances
+    (resynchronised per step)."""
+    if pp and layers == 2:
+        pytest.skip("parity sets are a 1-hop step (2 hops: the pipelined step)")
     engines = []
     for pipe in (True, False):
         s, ref, opt_ref, lref, model, opt, eng = _setup("last", layers=layers, updater=updater,
                                                         memory="dyrep" if any(emb) else "tgn", emb=emb)
         model.cfg.dropout = 0.1
         eng.pipeline = pipe
+        eng.parity_sets = pp
         eng.bind_resident(0, 7 * 50 + 20, 50, dropout=True)   # the last batch is partial (20 events)
         eng.begin_epoch()
         if pipe:
@@ -414,3 +420,23 @@ def test_tgn_pipelined_reprepares_after_loader_reset():
             o1.exp_avg.copy_(o2.exp_avg)
             o1.exp_avg_sq.copy_(o2.exp_avg_sq)
             m1.memory.memory.copy_(m2.memory.memory)
+
+
+def test_tgn_pp_wrong_parity_sets_error():
+    """tgnx_tgn_train_step_pp with prefetched = 1 but the parity whose set holds the PREVIOUS batch: the
+    step's first launch finds the set's batch tag stale, sets ctl[ERR] bit 16 and the step computes nothing
+    (memory and parameters unchanged); check() raises."""
+    s, ref, opt_ref, lref, model, opt, eng = _setup("last")
+    eng.bind_resident(0, 7 * 50, 50, dropout=False)
+    eng.begin_epoch()
+    eng.resident_train_step()            # eager, parity 0; scans batch 1 into set 1
+    torch.cuda.synchronize()
+    eng.check()
+    assert eng._parity == 1
+    mem, flat = model.memory.memory.clone(), model.flat.clone()
+    eng._pre(True, 0)                   # set 0 still holds batch 0
+    torch.cuda.synchronize()
+    assert int(eng.ctl[11]) & 16
+    assert torch.equal(model.memory.memory, mem) and torch.equal(model.flat, flat)
+    with pytest.raises(RuntimeError):
+        eng.check()

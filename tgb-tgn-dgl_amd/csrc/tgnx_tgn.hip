@@ -39,7 +39,9 @@ constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touc
 #ifndef TGNX_PRED_ATT_REC
 #define TGNX_PRED_ATT_REC 1  // per-root neighbour-row records for the attention in tgn_pred_train<ATT>
 #endif
-enum { CNT_R = 0, CNT_M = 1, CNT_E = 2, CNT_U = 3, CNT_LIST = 6, CNT_WORDS = 16 };  // (4, 5: unused)
+enum { CNT_R = 0, CNT_M = 1, CNT_E = 2, CNT_U = 3, CNT_LIST = 6, CNT_NB = 9, CNT_WORDS = 16 };  // (4, 5: unused)
+// ctl[ERR] bit of a step that found its scan-output set holding another batch (tgnx_tgn_train_step_pp)
+constexpr int64_t ERR_STALE_SET = 16;
 
 __host__ __device__ inline int64_t al4(int64_t x) { return (x + 3) & ~int64_t(3); }
 
@@ -240,6 +242,8 @@ struct Ctx {
   int emb;
   const float* zemb;
   float* Zupd;
+  // tgnx_tgn_train_step_pp: tgn_agg_emit checks that the scan-output set holds this step's batch (cnt[CNT_NB])
+  int tagchk;
 };
 constexpr int CNT_R1 = 7, CNT_E1 = 8;
 
@@ -261,6 +265,8 @@ __device__ __forceinline__ float softplusf(float x) { return fmaxf(x, 0.f) + log
 // tgn_scan walks every bitmap word of a small graph directly (<= 2 words per thread of its 1024) and
 // the nonzero words of a large one from the summary bitmaps; mark sets summary bits only for the latter
 constexpr int TGN_SCAN_THREADS = 1024;
+constexpr int SCAN_LW = 2 * TGN_SCAN_THREADS;  // LDS word list of the listed walk (tgn_scan)
+constexpr int SCAN_SWR = 4;                     // node-summary words per thread held in registers there
 // plan partitions per plan (tgn_scan): one per TGNX_PLAN_KEYS keys of the (global) batch, up to TGNX_PLAN_PMAX
 #ifndef TGNX_PLAN_KEYS
 #define TGNX_PLAN_KEYS 512
@@ -303,6 +309,15 @@ __device__ __forceinline__ ResDesc res_desc(const Ctx& c, int ahead) {
   d.seed = (int64_t)(mix64(c.adv_seed ^ mix64((uint64_t)(nb + 1))) >> 1);
   d.gen = (int)c.ctl[TGNX_CTL_GEN] + 1 + ahead;
   return d;
+}
+// the descriptor words of batch d into ctl, for the launches after this one
+__device__ __forceinline__ void write_desc(const Ctx& c, const ResDesc& d) {
+  c.ctl[TGNX_CTL_BATCH_START] = d.start;
+  c.ctl[TGNX_CTL_B] = d.B;
+  c.ctl[TGNX_CTL_CUR_EID] = d.start;
+  c.ctl[TGNX_CTL_LO] = d.lo;
+  c.ctl[TGNX_CTL_HI] = d.hi;
+  c.ctl[TGNX_CTL_SEED] = d.seed;
 }
 // K1 body over `nmark` 256-thread blocks (bid = this block's index among them).  Resident train steps
 // (c.adv) take the batch from the counters (ahead: see res_desc), every other step from ctl.
@@ -715,25 +730,22 @@ __device__ __forceinline__ int plan_runs(const int* pc, int P) {
 // and WG0 writes the descriptor into ctl for the later launches (no workgroup of this launch reads it).
 // scan_body: workgroup `role` of it (0: walks, 1 .. 2 pplan: plans), any workgroup size T with the
 // graph's bitmap words <= 2 T when scan_direct (scan_folds), LDS at smem (tgn_scan_smem)
-template <bool TRAIN, class AT>
-__device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char* smem, AT at) {
+// ahead: the batch `ahead` past the step counters' (1: the early scan of tgnx_tgn_train_step_pp, before this
+// step's counter advance); wdesc: write the batch descriptor into ctl (not while this step's launches still
+// read it); LW: capacity of the listed walk's LDS word list (>= 2 x the workgroup size)
+template <bool TRAIN, class AT, int LW = SCAN_LW>
+__device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char* smem, AT at, int ahead, bool wdesc) {
   __shared__ int sh[40];
   const int tid = threadIdx.x, T = blockDim.x;
   int B, gen;
   int64_t start;
   if (TRAIN && c.adv) {
-    const ResDesc d = res_desc(c, 0);
+    const ResDesc d = res_desc(c, ahead);
     B = d.B;
     start = d.start;
     gen = d.gen;
-    if (role == 0 && tid == 0) {
-      c.ctl[TGNX_CTL_BATCH_START] = d.start;
-      c.ctl[TGNX_CTL_B] = d.B;
-      c.ctl[TGNX_CTL_CUR_EID] = d.start;
-      c.ctl[TGNX_CTL_LO] = d.lo;
-      c.ctl[TGNX_CTL_HI] = d.hi;
-      c.ctl[TGNX_CTL_SEED] = d.seed;
-    }
+    if (role == 0 && tid == 0) c.cnt[CNT_NB] = (int)(c.ctl[TGNX_CTL_NB] + ahead);  // the batch this set holds
+    if (role == 0 && tid == 0 && wdesc) write_desc(c, d);
   } else {
     B = (int)c.ctl[TGNX_CTL_B];
     start = c.ctl[TGNX_CTL_BATCH_START];
@@ -747,7 +759,44 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
   // pass 0: the words each thread walks.  Small graphs (<= 2 words per thread): contiguous word ranges
   // (summaries just cleared); large graphs: the nonzero words in word order, from the summaries
   const bool direct = scan_direct(c.words);
+  // listed (large graphs, 1 hop): the nonzero node words (a centre is a sampled node, so its word is one
+  // of them) from the node summary into an LDS list in word order, then walked as the direct path walks
+  // its words (<= 2 per thread, in registers, centres staged for pass 2): 2 dependent global rounds to
+  // the sorted sets instead of 4 (summaries -> global word lists -> words -> cent[] -> assoc[])
+  __shared__ int lwl[LW];
+  bool listed = false;
   int ncw, nnw, nrw = 0;
+  if (!direct && c.layers == 1) {
+    const int64_t SW = (c.words + 31) >> 5, sq = (SW + T - 1) / T, s0 = min(SW, tid * sq), s1 = min(SW, s0 + sq);
+    uint32_t sv[SCAN_SWR];
+    int nz = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_SWR; ++j) {
+      sv[j] = s0 + j < s1 ? c.nbs[s0 + j] : 0u;
+      nz += __popc(sv[j]);
+    }
+    for (int64_t i = s0 + SCAN_SWR; i < s1; ++i) nz += __popc(c.nbs[i]);
+    int tw;
+    int o = block_excl_scan(nz, sh, &tw);
+    listed = tw <= min(2 * T, LW);  // (block-uniform)
+    if (listed) {
+      auto emit = [&](int64_t i, uint32_t m) {
+        if (!m) return;
+        c.nbs[i] = 0u;
+        c.cbs[i] = 0u;
+        while (m) {
+          const int b = __ffs(m) - 1;
+          m &= m - 1;
+          lwl[o++] = (int)((i << 5) + b);
+        }
+      };
+#pragma unroll
+      for (int j = 0; j < SCAN_SWR; ++j) emit(s0 + j, sv[j]);  // (zero past s1)
+      for (int64_t i = s0 + SCAN_SWR; i < s1; ++i) emit(i, c.nbs[i]);
+      ncw = nnw = tw;
+      __syncthreads();
+    }
+  }
   if (direct) {
     ncw = nnw = (int)c.words;
     if (c.layers == 2) nrw = (int)c.words;
@@ -756,7 +805,7 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
       c.cbs[i] = c.nbs[i] = 0u;
       if (c.layers == 2) c.rbs[i] = 0u;
     }
-  } else {
+  } else if (!listed) {
     occupied_words2(c.cbs, c.nbs, c.words, c.cl, c.nl, sh, &ncw, &nnw);
     if (c.layers == 2) {
       int unused;
@@ -775,12 +824,16 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
   const int nq = (nnw + T - 1) / T, n0 = min(nnw, tid * nq), n1 = min(nnw, n0 + nq);
   int nc = 0, np = 0;
   uint32_t dcw[2] = {0u, 0u}, dnw[2] = {0u, 0u};
-  if (direct) {  // c0..c1 == n0..n1, <= 2 words
+  int64_t dwi[2] = {0, 0};  // the words (direct: c0 + j; listed: from the LDS list)
+  const bool walk = direct || listed;
+  if (walk) {  // c0..c1 == n0..n1, <= 2 words
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dwi[j] = direct ? (int64_t)(c0 + j) : (int64_t)lwl[min(c0 + j, max(ncw - 1, 0))];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (c0 + j < c1) {
-        dcw[j] = c.cb[c0 + j];
-        dnw[j] = c.nb[c0 + j];
+        dcw[j] = c.cb[dwi[j]];
+        dnw[j] = c.nb[dwi[j]];
       }
       nc += __popc(dcw[j]);
       np += __popc(dnw[j]);
@@ -792,14 +845,14 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
   int R, M, rc, rank;
   block_excl_scan2(nc, np, sh, &rc, &rank, &R, &M);
   const bool fits = R <= c.Rcap && M <= c.Mcap;
-  const bool lds_c = direct && TRAIN && c.layers == 1 && R <= 3 * c.Bmax;  // (block-uniform)
+  const bool lds_c = walk && TRAIN && c.layers == 1 && R <= 3 * c.Bmax;  // (block-uniform)
   int64_t* lv = reinterpret_cast<int64_t*>(smem);                          // [3 Bmax] centre node
   int* lloc = reinterpret_cast<int*>(smem + (size_t)3 * c.Bmax * 8);       // [3 Bmax] its node rank
-  if (direct) {
+  if (walk) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (c0 + j >= c1) break;
-      const int64_t w = c0 + j;
+      const int64_t w = dwi[j];
       const int rw = rank;
       uint32_t m = dnw[j];
       if (m) c.nb[w] = 0u;
@@ -988,10 +1041,10 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
   }
 }
 template <bool TRAIN>
-__global__ void __launch_bounds__(1024) tgn_scan(Ctx c) {
+__global__ void __launch_bounds__(1024) tgn_scan(Ctx c, int ahead, int wdesc) {
   TGNX_STAMP(2);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  scan_body<TRAIN>(c, (int)blockIdx.x, smem, [&](int slot) { TGNX_STAMP_AT(slot); });
+  scan_body<TRAIN>(c, (int)blockIdx.x, smem, [&](int slot) { TGNX_STAMP_AT(slot); }, ahead, wdesc != 0);
 }
 
 // ------------------------------------------------------------------ messages (memory_module.py:152-207)
@@ -1466,6 +1519,8 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
   TGNX_STAMP(3);
   if (mode != 2) {
     const int B = (int)c.ctl[TGNX_CTL_B];
+    if (c.tagchk && blockIdx.x == 0 && threadIdx.x == 0 && B > 0 && c.cnt[CNT_NB] != (int)c.ctl[TGNX_CTL_NB])
+      c.ctl[TGNX_CTL_ERR] |= ERR_STALE_SET;  // (this launch's other blocks may compute garbage; later launches skip)
     if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   }
   const int lane = threadIdx.x & 63;
@@ -3143,8 +3198,17 @@ struct StoreJob {
 // update list) for fixup_view — the pipelined step's next-batch scan runs inside the fixup launch and
 // rewrites them — then advances the resident step counters (what tgnn_advance did at the start of the
 // step; after this launch only the next batch's scan reads them).
+// noadv (tgnx_tgn_train_step_pp): the counters advance in the fixup launch instead (the next batch's scan
+// rides in this launch and reads them)
+__device__ __forceinline__ void advance_counters(int64_t* ctl) {
+  ctl[TGNX_CTL_GEN] += 1;
+  ctl[TGNX_CTL_NB] += 1;
+  ctl[TGNX_CTL_STEP_B] = ctl[TGNX_CTL_B];
+  if (ctl[TGNX_CTL_B] > 0) ctl[TGNX_CTL_ADAM_T] += 1;
+}
 struct SnapJob {
   Ctx c;
+  int noadv;
   __device__ void operator()(int, float*) const {
     const int tid = threadIdx.x, U = min(c.cnt[CNT_U], c.Ucap);
     for (int i = tid; i < TGNX_CTL_WORDS; i += blockDim.x) c.snap_ctl[i] = c.ctl[i];
@@ -3153,15 +3217,9 @@ struct SnapJob {
       c.snap_upd[i] = c.upd[i];
       c.snap_upd_loc[i] = c.upd_loc[i];
     }
-    if (!c.adv) return;  // (block-uniform)
+    if (!c.adv || noadv) return;  // (block-uniform)
     __syncthreads();
-    if (tid == 0) {
-      int64_t* ctl = c.ctl;
-      ctl[TGNX_CTL_GEN] += 1;
-      ctl[TGNX_CTL_NB] += 1;
-      ctl[TGNX_CTL_STEP_B] = ctl[TGNX_CTL_B];
-      if (ctl[TGNX_CTL_B] > 0) ctl[TGNX_CTL_ADAM_T] += 1;
-    }
+    if (tid == 0) advance_counters(c.ctl);
   }
 };
 static_assert(TGNX_PIPE_MARK_AT != 9, "the next batch's marking reads the step counters SnapJob advances");
@@ -3175,19 +3233,37 @@ static inline Ctx fixup_view(const Ctx& c) {
   if (f.adf.p) f.adf.ctl = c.snap_ctl;
   return f;
 }
-template <bool TRAIN, class AT>
-__device__ void scan_body(const Ctx& c, int role, unsigned char* smem, AT at);
+template <bool TRAIN, class AT, int LW>
+__device__ void scan_body(const Ctx& c, int role, unsigned char* smem, AT at, int ahead, bool wdesc);
+// the next batch's scan as extra workgroups of the dW_cell / dX_enc launch (tgnx_tgn_train_step_pp): into the
+// other parity's set (c), batch one past the counters (they advance in the fixup launch), no descriptor
+// write (the fixup launch writes it)
+struct ScanJob {
+  Ctx c;
+  __device__ void operator()(int bid, float* smem) const {
+    scan_body<true, NoCheckpoint, 512>(c, bid, reinterpret_cast<unsigned char*>(smem), NoCheckpoint{}, 1, false);
+  }
+};
 // tail blocks of the train step's fixup launch: [0, nscan) the next batch's scan (pipelined steps whose
 // scan fits the launch's LDS and 256-thread workgroups, scan_folds; `nxt` = the live Ctx), then the
 // Δt-encoding reduction (nte blocks), then the memory / last_update half of update_state (nmem blocks;
 // nothing in the fixup reads memory).  te.c is the fixup's view (fixup_view).
+// wdesc (tgnx_tgn_train_step_pp, whose next batch was scanned earlier in the step): the first Δt block also
+// advances the step counters and writes the next batch's descriptor into the live ctl (nothing in this
+// launch reads them: te.c is the snapshot)
 struct TrainTail {
   TeReduceTail te;
   Ctx nxt;
-  int nscan, nte, nmem;
+  int nscan, nte, nmem, wdesc;
   __device__ __forceinline__ void operator()(int bid, float* smem) const {
-    if (bid < nscan) scan_body<true>(nxt, bid, reinterpret_cast<unsigned char*>(smem), NoCheckpoint{});
-    else if ((bid -= nscan) < nte) te(bid);
+    if (bid < nscan) scan_body<true, NoCheckpoint, 512>(nxt, bid, reinterpret_cast<unsigned char*>(smem), NoCheckpoint{}, 0, true);
+    else if ((bid -= nscan) < nte) {
+      if (wdesc && bid == 0 && threadIdx.x == 0) {  // (te.c reads the snapshot: nothing here reads these words)
+        advance_counters(nxt.ctl);
+        write_desc(nxt, res_desc(nxt, 0));
+      }
+      te(bid);
+    }
     else update_body(te.c, bid - nte, nmem, 0, 0, te.c.upd, te.c.cnt + CNT_U, 0, 0);
   }
 };
@@ -3338,6 +3414,9 @@ struct WsLay {
       snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF,
       uX, uZ, uG, ulu, uxw, utrel, total;
   int tgp_rows, tgp_e1;
+  // the scan's per-batch outputs of the second parity (tgnx_tgn_train_step_pp: a step reads its parity's
+  // set while the next batch's scan writes the other)
+  size_t cnt2, cent2, cent_loc2, ceoff2, crank2, upd_loc2, nid2, upd2, rkeys2, rruns2, skeys2, sruns2, pcnt2;
 };
 static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   WsLay W;
@@ -3434,6 +3513,19 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.ulu = carve(off, U * 4);
   W.uxw = carve(off, U * 8);
   W.utrel = carve(off, U * 4);
+  W.cnt2 = carve(off, CNT_WORDS * 4);
+  W.cent2 = carve(off, (size_t)k.Rcap * 8);
+  W.cent_loc2 = carve(off, (size_t)k.Rcap * 4);
+  W.ceoff2 = carve(off, (size_t)(k.Rcap + 1) * 4);
+  W.crank2 = carve(off, (size_t)k.Mcap * 4);
+  W.upd_loc2 = carve(off, (size_t)k.Ucap * 4);
+  W.nid2 = carve(off, (size_t)k.Mcap * 8);
+  W.upd2 = carve(off, (size_t)k.Ucap * 8);
+  W.rkeys2 = carve(off, (size_t)n2 * 8);
+  W.rruns2 = carve(off, (size_t)(n2 + 2 + TGNX_PLAN_PMAX) * 4);
+  W.skeys2 = carve(off, (size_t)n2 * 8);
+  W.sruns2 = carve(off, (size_t)(n2 + 2 + TGNX_PLAN_PMAX) * 4);
+  W.pcnt2 = carve(off, (size_t)4 * TGNX_PLAN_PMAX * 4);
   W.total = off;
   return W;
 }
@@ -3620,6 +3712,29 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   return TGNX_OK;
 }
 
+// the Ctx of scan-output set p (0: the set every other entry point uses, 1: the second parity)
+static Ctx set_view(const Ctx& c, const WsLay& W, char* ws, int p) {
+  Ctx v = c;
+  auto at = [&](size_t a, size_t b) { return ws + (p ? b : a); };
+  v.cnt = reinterpret_cast<int*>(at(W.cnt, W.cnt2));
+  v.cent = reinterpret_cast<int64_t*>(at(W.cent, W.cent2));
+  v.cent_loc = reinterpret_cast<int*>(at(W.cent_loc, W.cent_loc2));
+  v.ceoff = reinterpret_cast<int*>(at(W.ceoff, W.ceoff2));
+  v.crank = reinterpret_cast<int*>(at(W.crank, W.crank2));
+  v.upd_loc = reinterpret_cast<int*>(at(W.upd_loc, W.upd_loc2));
+  v.nid = reinterpret_cast<int64_t*>(at(W.nid, W.nid2));
+  v.upd = reinterpret_cast<int64_t*>(at(W.upd, W.upd2));
+  v.rkeys = reinterpret_cast<uint64_t*>(at(W.rkeys, W.rkeys2));
+  v.rruns = reinterpret_cast<int*>(at(W.rruns, W.rruns2));
+  v.skeys = reinterpret_cast<uint64_t*>(at(W.skeys, W.skeys2));
+  v.sruns = reinterpret_cast<int*>(at(W.sruns, W.sruns2));
+  v.rpc = reinterpret_cast<int*>(at(W.pcnt, W.pcnt2));
+  v.rpo = v.rpc + TGNX_PLAN_PMAX;
+  v.spc = v.rpo + TGNX_PLAN_PMAX;
+  v.spo = v.spc + TGNX_PLAN_PMAX;
+  return v;
+}
+
 // 2 hops: the root level as a Ctx for the attention / prediction kernels — centres = roots, node rows =
 // outer centres (P2 = conv2's projections of h1), edges = the roots' ring rows, output Zr
 // the DyRep embedding-message update of a train step: aggregation / updater rows of the update list in their
@@ -3762,13 +3877,18 @@ extern "C++" {  // (inside the extern "C" block: the cell-templated step)
 #endif
 // the next batch's scan as 256-thread head workgroups of the fixup launch: its LDS within the launch's,
 // and (small graphs, walked directly) <= 2 bitmap words per thread
-static inline bool scan_folds(const Ctx& c, const Caps& k) {
-  return TGNX_SCAN_FOLD && tgn_scan_smem(k.B) <= (size_t)GEMM_FIX_SMEM * 4 && (size_t)3 * k.B * 12 <= (size_t)GEMM_FIX_SMEM * 4 &&
-         (!scan_direct(c.words) || c.words <= 2 * 256);
+static inline bool scan_rides(const Ctx& c, const Caps& k, size_t lds) {
+  return tgn_scan_smem(k.B) <= lds && (size_t)3 * k.B * 12 <= lds && (!scan_direct(c.words) || c.words <= 2 * 256);
 }
+static inline bool scan_folds(const Ctx& c, const Caps& k) {
+  return TGNX_SCAN_FOLD && scan_rides(c, k, (size_t)GEMM_FIX_SMEM * 4);
+}
+// pp >= 0 (tgnx_tgn_train_step_pp, world 1, 1 hop): the step reads scan-output set pp; the next batch is marked
+// in the predictor launch and scanned into set 1 - pp inside the k / v reduction launch (its outputs are then
+// written while this step's later launches still read set pp's), the fixup launch only writes its descriptor
 template <int CELL>
 static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
-                             void* stream, bool fuse_adam, const AdvArgs* adv, int pipe) {
+                             void* stream, bool fuse_adam, const AdvArgs* adv, int pipe, int pp) {
   using Cl = CellOps<CELL>;
   const bool no_tail = (pipe & 4) != 0;  // pipelined, but the next batch's scan is the caller's (tgnx_tgn_scan_next)
   pipe &= 3;
@@ -3813,6 +3933,16 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   TGNX_CHECK_ARG(pipe == 0 || adv, "tgnx_tgn_train_step_pipelined: resident steps only");
   c.gen_neg = gen_neg ? 1 : 0;
   c.drop = dropout && cfg->dropout > 0.f;
+  const bool ppm = pp >= 0;
+  Ctx cn;  // ppm: the other parity's set (the next batch's scan writes it)
+  if (ppm) {
+    TGNX_CHECK_ARG(pp <= 1 && pipe != 0 && !no_tail && fuse_adam && k.layers == 1 && adv && adv->world == 1,
+                   "tgnx_tgn_train_step_pp: a fused world-1 1-hop resident step, parity 0 or 1");
+    char* ws = reinterpret_cast<char*>(buf->ws);
+    cn = set_view(c, W, ws, 1 - pp);
+    c = set_view(c, W, ws, pp);
+    c.tagchk = 1;
+  }
   hipStream_t s = as_stream(stream);
   const float* P = c.params;
   float* G = c.grads;
@@ -3822,7 +3952,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     tgn_mark<true><<<nmark, 256, 0, s>>>(c, nmark);
     TGNX_LAUNCH_CHECK("tgn_mark");
     probe_begin(TGNX_K_ASSEMBLE, s);
-    tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
+    tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c, 0, 1);
     probe_end(TGNX_K_ASSEMBLE, s);
     TGNX_LAUNCH_CHECK("tgn_scan");
   }
@@ -3862,7 +3992,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   TGNX_LAUNCH_CHECK("tgn_gru_edge");
   const int nmark = gridn(3 * k.B * 16, 256);
   auto mk_at = [&](int at) {
-    return BlockJob<MarkNextJob, 3 * MARK_LDS_WORDS>{MarkNextJob{c, nmark}, pipe && at == TGNX_PIPE_MARK_AT ? nmark : 0};
+    return BlockJob<MarkNextJob, 3 * MARK_LDS_WORDS>{MarkNextJob{c, nmark}, pipe && !ppm && at == TGNX_PIPE_MARK_AT ? nmark : 0};
   };
   probe_begin(TGNX_K_PROJ, s);
   gemmN_launch(s, mk_at(3),
@@ -3888,7 +4018,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   }
   probe_begin(TGNX_K_PRED, s);
   TGNX_CHECK_ARG(pred_smem_ok(c.D), "tgn_pred_train: dynamic LDS attribute refused");
-  const int nmk = pipe && TGNX_PIPE_MARK_AT == 5 ? nmark : 0;
+  const int nmk = (ppm || (pipe && TGNX_PIPE_MARK_AT == 5)) ? nmark : 0;
   const size_t psm = std::max(tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0);
   if (att_in_pred)
     launch_k(tgn_pred_train<true>, dim3(k.B + nmk), dim3(256), (uint32_t)psm, s, cr, nmk);
@@ -3939,11 +4069,12 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const Ctx cf = fixup_view(c);
   const EpiGradStore e_dWe{G, c.L.we, D + d, cf.adf};
   probe_begin(TGNX_K_KV, s);
-  gemmN_launch(s, mk_at(7), BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(k.Etr, KVR_CH, 1 << 20)},
-               gemm_job<GW>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, EpiDeferred{}, c.pA),
-               gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
-                             LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
-                             (float*)nullptr));
+  const auto j_kvr = BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(k.Etr, KVR_CH, 1 << 20)};
+  const auto j_dwe = gemm_job<GW>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, EpiDeferred{}, c.pA);
+  const auto j_denc = gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
+                                    LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
+                                    (float*)nullptr);
+  gemmN_launch(s, mk_at(7), j_kvr, j_dwe, j_denc);
   probe_end(TGNX_K_KV, s);
   TGNX_LAUNCH_CHECK("tgn_kv_reduce_dE");
   // weight gradients (deferred split-K) ‖ ...
@@ -3965,25 +4096,36 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // ‖ the message stores ‖ the fixup's descriptor copy + the counter advance (SnapJob)
   const int nst = gridn(2 * k.B, 256);
   probe_begin(TGNX_K_WGRAD3, s);
-  gemmN_launch(s, mk_at(9), BlockJob<SnapJob>{SnapJob{c}, 1}, BlockJob<StoreJob>{StoreJob{c, nst}, nst},
-               gemm_job<GW>(shp_dWg(k, c.cnt), LoadKRow{c.dG, Cl::G * D, k.Mtr, Cl::G * D},
-                            LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{}, c.pD),
-               gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, Cl::G * D, c.cnt + CNT_M),
-                              LoadRowK{c.dG, k.Mtr, Cl::G * D, Cl::G * D}, Cl::wenc(c),
-                              EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge},
-                              (float*)nullptr));
+  const auto j_dwg = gemm_job<GW>(shp_dWg(k, c.cnt), LoadKRow{c.dG, Cl::G * D, k.Mtr, Cl::G * D},
+                                  LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{}, c.pD);
+  const auto j_dxe = gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, Cl::G * D, c.cnt + CNT_M),
+                                    LoadRowK{c.dG, k.Mtr, Cl::G * D, Cl::G * D}, Cl::wenc(c),
+                                    EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, (float*)nullptr);
+  // ppm: the next batch's scan (into set 1 - pp; the counters advance in the fixup launch) as this launch's
+  // first workgroups when it fits their LDS, else its own launch after it
+  const bool scan_w3 = ppm && scan_rides(c, k, (size_t)3 * MARK_LDS_WORDS * 4);
+  if (scan_w3)
+    gemmN_launch(s, BlockJob<ScanJob, 3 * MARK_LDS_WORDS>{ScanJob{cn}, 1 + 2 * c.pplan}, BlockJob<SnapJob>{SnapJob{c, 1}, 1},
+                 BlockJob<StoreJob>{StoreJob{c, nst}, nst}, j_dwg, j_dxe);
+  else
+    gemmN_launch(s, mk_at(9), BlockJob<SnapJob>{SnapJob{c, ppm ? 1 : 0}, 1}, BlockJob<StoreJob>{StoreJob{c, nst}, nst}, j_dwg,
+                 j_dxe);
   probe_end(TGNX_K_WGRAD3, s);
   TGNX_LAUNCH_CHECK("tgn_wgrad3");
+  if (ppm && !scan_w3) {
+    tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(cn, 1, 0);
+    TGNX_LAUNCH_CHECK("tgn_scan_early");
+  }
   // split-K sums + epilogues ‖ Δt reduction ‖ update_state's memory half (train order: memory of src ∪
   // dst from this step's GRU rows; the stores and the ring insert ran in earlier launches), reading the
   // step descriptor from SnapJob's copy (cf) — so that the pipelined step's next-batch scan (counters
   // advanced by SnapJob) rides in the same launch as its first workgroups when it fits (scan_folds)
   const int nte = (2 * D + 63) / 64;
   const int nmem = gridn(k.Ucap, 4, 1024);
-  const bool scan_next = pipe && !no_tail;
+  const bool scan_next = pipe && !no_tail && !ppm;
   const bool fold = scan_next && scan_folds(c, k);
   const int nscan = fold ? 1 + 2 * c.pplan : 0;
-  const TrainTail tail{TeReduceTail{cf, rows_edge, rows_msg}, c, nscan, nte, nmem};
+  const TrainTail tail{TeReduceTail{cf, rows_edge, rows_msg}, c, nscan, nte, nmem, ppm ? 1 : 0};
   probe_begin(TGNX_K_FINISH, s);
   if (two)
     gemm_fixup_launch_h(nscan, nscan + nte + nmem, tail, s, gemm_fix<GW>(shp_dWe(k, cf.cnt), c.pA, e_dWe),
@@ -3999,7 +4141,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   TGNX_LAUNCH_CHECK("tgn_fixup_update");
   if (scan_next && !fold) {  // the next batch (counters advanced by SnapJob): sorted node sets, plans, descriptor
     probe_begin(TGNX_K_ASSEMBLE, s);
-    tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
+    tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c, 0, 1);
     probe_end(TGNX_K_ASSEMBLE, s);
     TGNX_LAUNCH_CHECK("tgn_scan_next");
   }
@@ -4009,9 +4151,9 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
 }  // extern "C++"
 
 static int train_step_impl(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
-                           void* stream, bool fuse_adam, const AdvArgs* adv = nullptr, int pipe = 0) {
-  if (cfg && cfg->updater == 1) return train_step_impl_c<1>(cfg, buf, gen_neg, dropout, stream, fuse_adam, adv, pipe);
-  return train_step_impl_c<0>(cfg, buf, gen_neg, dropout, stream, fuse_adam, adv, pipe);
+                           void* stream, bool fuse_adam, const AdvArgs* adv = nullptr, int pipe = 0, int pp = -1) {
+  if (cfg && cfg->updater == 1) return train_step_impl_c<1>(cfg, buf, gen_neg, dropout, stream, fuse_adam, adv, pipe, pp);
+  return train_step_impl_c<0>(cfg, buf, gen_neg, dropout, stream, fuse_adam, adv, pipe, pp);
 }
 
 int tgnx_tgn_train_fwd_bwd(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int32_t gen_neg, int32_t dropout,
@@ -4036,6 +4178,14 @@ int tgnx_tgn_train_step_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buf
                                   int32_t prefetched, void* stream) {
   const AdvArgs a{split_lo, split_hi, batch, 0, 1, base_seed};
   return train_step_impl(cfg, buf, 1, dropout, stream, true, &a, prefetched ? 1 : 2);
+}
+
+int tgnx_tgn_train_step_pp(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo, int64_t split_hi,
+                           int64_t batch, uint64_t base_seed, int32_t dropout, int32_t prefetched, int32_t parity,
+                           void* stream) {
+  const AdvArgs a{split_lo, split_hi, batch, 0, 1, base_seed};
+  TGNX_CHECK_ARG(parity == 0 || parity == 1, "tgnx_tgn_train_step_pp: parity must be 0 or 1");
+  return train_step_impl(cfg, buf, 1, dropout, stream, true, &a, prefetched ? 1 : 2, parity);
 }
 
 int tgnx_tgn_train_fwd_bwd_split(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
@@ -4064,7 +4214,7 @@ int tgnx_tgn_scan_next(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
   c.adv_seed = base_seed;
   hipStream_t s = as_stream(stream);
   probe_begin(TGNX_K_ASSEMBLE, s);
-  tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c);
+  tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(c, 0, 1);
   probe_end(TGNX_K_ASSEMBLE, s);
   TGNX_LAUNCH_CHECK("tgn_scan_next");
   return TGNX_OK;
@@ -4148,7 +4298,7 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
     tgn_mark<false><<<nmark, 256, 0, s>>>(c, nmark);
   }
   TGNX_LAUNCH_CHECK("tgn_mark");
-  tgn_scan<false><<<1 + 2 * c.pplan, TGN_SCAN_THREADS, tgn_scan_smem(k.B), s>>>(c);
+  tgn_scan<false><<<1 + 2 * c.pplan, TGN_SCAN_THREADS, tgn_scan_smem(k.B), s>>>(c, 0, 1);
   TGNX_LAUNCH_CHECK("tgn_scan");
   const int nedge = gridn((int64_t)Rq * c.K, 4, 4096);
   tgn_agg_emit<-1><<<nedge + gridn(Mq, 256), 256, 0, s>>>(c, 1, nedge, nullptr, nullptr, 0, 0);

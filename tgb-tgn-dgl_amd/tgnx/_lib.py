@@ -44,6 +44,7 @@ SIGNATURES = {
     "tgnx_tgn_train_step": (ctypes.c_int, [P, P, c_i32, c_i32, c_vp]),
     "tgnx_tgn_train_step_resident": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64, c_i32, c_vp]),
     "tgnx_tgn_train_step_pipelined": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_u64, c_i32, c_i32, c_vp]),
+    "tgnx_tgn_train_step_pp": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_u64, c_i32, c_i32, c_i32, c_vp]),
     "tgnx_tgn_train_fwd_bwd_resident": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64, c_i32, c_vp]),
     "tgnx_tgn_train_fwd_bwd_pipelined": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64, c_i32, c_i32,
                                                          c_vp]),

@@ -14,6 +14,7 @@ same bound), LinkPredictor torch Linear defaults; memory / last_update zero (mem
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 
 import numpy as np
@@ -300,6 +301,11 @@ class TgnEngine:
         # world > 1 pipelined steps leave the next batch's scan out of fwd_bwd and run it while the exchange
         # is in flight (tgnx_tgn_train_fwd_bwd_split + tgnx_tgn_scan_next)
         self.split_scan = True
+        # world-1 1-hop pipelined steps alternate two parities of the scan's per-batch outputs
+        # (tgnx_tgn_train_step_pp): the next batch is scanned into the other set mid-step instead of in the
+        # step's last launch; `_parity` = the set the next step reads (two captured graphs)
+        self.parity_sets = os.environ.get("TGNX_PP", "1") != "0"   # (TGNX_PP=0: same-box A/B against the fold)
+        self._parity = 0
         self._prefetched = False
         self._prefetch_version = None
         if optimizer is None:
@@ -463,11 +469,17 @@ class TgnEngine:
     def _pipelined(self) -> bool:
         return self.pipeline and self.fold_cursor and (self._res_fused or self.world > 1)
 
-    def _pre(self, prefetched: bool = False):
+    def _pp(self) -> bool:
+        return self.parity_sets and self.world == 1 and self._res_fused and self.model.layers == 1 and self._pipelined()
+
+    def _pre(self, prefetched: bool = False, parity=None):
         adv, fb = self._f[:2]
         lo, hi, batch = self._res
         st = self._stream()
-        if self._pipelined() and self._res_fused:
+        if self._pp():
+            rc = _lib.lib().tgnx_tgn_train_step_pp(self._cfg_ref, self._buf_ref, lo, hi, batch, self.seed, self._res_drop,
+                                                  1 if prefetched else 0, self._parity if parity is None else parity, st)
+        elif self._pipelined() and self._res_fused:
             rc = _lib.lib().tgnx_tgn_train_step_pipelined(self._cfg_ref, self._buf_ref, lo, hi, batch, self.seed,
                                                          self._res_drop, 1 if prefetched else 0, st)
         elif self._pipelined():
@@ -535,12 +547,19 @@ class TgnEngine:
         self._allreduce(self._scan_next)
         self._post()
         self._mark_prefetched()
+        self._parity ^= 1 if self._pp() else 0
 
     def capture_resident(self):
         """One resident step as HIP graph(s) (world > 1: the collectives stay eager between them)."""
         torch.cuda.synchronize(self.dev)
         saved = self.ctl.clone()
-        if self.world == 1:
+        if self.world == 1 and self._pp():   # one graph per parity, replayed alternately
+            gp = (torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph())
+            for par in (0, 1):
+                with torch.cuda.graph(gp[par]):
+                    self._pre(True, par)
+            self._graphs = (gp, None, None)
+        elif self.world == 1:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):   # pipelined: the steady-state step (the previous step prefetched)
                 self._pre(True)
@@ -565,6 +584,11 @@ class TgnEngine:
         g1, g2, gs = self._graphs
         if self._pipelined() and not self._prefetch_valid():
             self.resident_train_step()   # marks + scans this batch first (eager), prefetches the next
+            return
+        if isinstance(g1, tuple):   # parity graphs
+            g1[self._parity].replay()
+            self._parity ^= 1
+            self._mark_prefetched()
             return
         g1.replay()
         if g2 is not None:
