@@ -24,10 +24,14 @@ namespace tgnx {
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-template <int TM_, int TN_, int KC_, int PF_ = 1, bool WS_ = false>
+template <int TM_, int TN_, int KC_, int PF_ = 1, bool WS_ = false, int DR_ = 0>
 struct GemmCfg {
   static constexpr int TM = TM_, TN = TN_, KC = KC_;
   static constexpr int PF = PF_;  // k-chunks whose global loads are in flight ahead of the MFMAs
+  // DR > 0 (with WS, 16x16 tiles): direct operands — each wave loads its k-slabs' MFMA operands straight into
+  // registers, DR slabs (16 k each) per wave per round, every load of a round issued before the first MFMA;
+  // no LDS staging, no barriers in the K loop (gemm_tile_direct)
+  static constexpr int DR = DR_;
   // WS (wave split-K): every wave owns the whole TMxTN tile and every 4th 16-deep k-slab of a chunk;
   // the four partial tiles are summed through LDS in wave order.  Otherwise the 4 waves tile the output
   // 2x2, each a (TM/2)x(TN/2) quadrant over the whole chunk.
@@ -41,6 +45,7 @@ struct GemmCfg {
   static_assert(WS ? (TM % 16 == 0 && TN % 16 == 0 && KC % 64 == 0) : (TM % 32 == 0 && TN % 32 == 0 && KC % 16 == 0),
                 "tile");
   static_assert(LA % 4 == 0 && LB % 4 == 0 && TM * TN % 256 == 0, "operand / C-tile split over 256 threads");
+  static_assert(DR == 0 || (WS && TM == 16 && TN == 16), "direct operands: 16x16 wave-split tiles");
 };
 // The TGN step's GEMMs: 16x16 output tiles, wave split-K (GemmCfg::WS).  Each 16x16x4 fp32 MFMA issues
 // for 32 cycles per SIMD, so a tile's time is set by its MFMA count on one CU: 32x32 tiles with the 2x2
@@ -59,7 +64,10 @@ struct GemmCfg {
 #ifndef TGNX_G32_PF
 #define TGNX_G32_PF 1
 #endif
-using G32 = GemmCfg<TGNX_G32_T, TGNX_G32_T, TGNX_G32_KC, TGNX_G32_PF, TGNX_G32_WS>;  // the TGN step's GEMMs
+#ifndef TGNX_G32_DR
+#define TGNX_G32_DR 0
+#endif
+using G32 = GemmCfg<TGNX_G32_T, TGNX_G32_T, TGNX_G32_KC, TGNX_G32_PF, TGNX_G32_WS, TGNX_G32_DR>;  // the TGN step's GEMMs
 #ifndef TGNX_G32L_T
 #define TGNX_G32L_T 16
 #endif
@@ -72,7 +80,10 @@ using G32 = GemmCfg<TGNX_G32_T, TGNX_G32_T, TGNX_G32_KC, TGNX_G32_PF, TGNX_G32_W
 #ifndef TGNX_G32L_PF
 #define TGNX_G32L_PF 1
 #endif
-using G32L = GemmCfg<TGNX_G32L_T, TGNX_G32L_T, TGNX_G32L_KC, TGNX_G32L_PF, TGNX_G32L_WS>;  // long-K direct GEMMs (GRU, dz0, dX_enc)
+#ifndef TGNX_G32L_DR
+#define TGNX_G32L_DR 3  // slabs per wave per load round (same-box A/B, wiki step: 9 (one round for K <= 576: 160 VGPRs, 3 waves per SIMD) 0.1073, 7 0.1060, 5 0.1045, 4 0.1045, 3 0.1041, staged path 0.1053 ms)
+#endif
+using G32L = GemmCfg<TGNX_G32L_T, TGNX_G32L_T, TGNX_G32L_KC, TGNX_G32L_PF, TGNX_G32L_WS, TGNX_G32L_DR>;  // long-K direct GEMMs (GRU, dz0, dX_enc)
 // deferred split-K weight gradients (K = edges / nodes, split S ways): already S x tiles workgroups
 #ifndef TGNX_GW_T
 #define TGNX_GW_T 32
@@ -282,10 +293,93 @@ __device__ __forceinline__ GemmWork gemm_work(const GemmShape& g, int Mr, int Nr
   return w;
 }
 
+// Direct-operand 16x16 tile (CFG::DR > 0, wave split-K): wave w owns k-slabs w, w + 4, ... (16 k each), and
+// lane (li, lk) of an MFMA step q takes k = 16 slab + 4 lk + q — the same slabs, k order, accumulator chains
+// and wave-order combine as the LDS-staged WS path, so the results are bit-identical to it.  Each lane loads
+// its 4 consecutive k of row m0 + li (A) and column n0 + li (B) per slab straight into registers: a float4
+// for 16-B operands (V), else 4 scalars; DR slabs per round, all of a round's loads issued before its first
+// MFMA (k past K: both entries selected to zero at use).  The chunked loop waited a whole load latency per
+// 64-deep chunk (stash, barrier, MFMAs, barrier): the GRU GEMM's K = 572 paid 9 of them per tile.
+template <class CFG, bool V, class AL, class BL, class EPI>
+__device__ __forceinline__ void gemm_tile_direct(const GemmShape& g, const GemmRt& rt, const AL& al, const BL& bl,
+                                                 const EPI& epi, float* part, int bid, float* smem) {
+  constexpr int TM = 16, TN = 16, PB = CFG::PB, DR = CFG::DR;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const GemmWork wk = gemm_work<TM, TN>(g, rt.Mr, rt.Nr, rt.Sr, bid);
+  const int tile = wk.tile, s = wk.s;
+  const int m0 = wk.tm * TM, n0 = wk.tn * TN;
+  if (!wk.ok || m0 >= rt.Mr || n0 >= rt.Nr || s >= rt.Sr) return;
+  const int li = lane & 15, lk = lane >> 4;
+  using TA = LoaderTraits<AL>;
+  using TB = LoaderTraits<BL>;
+  static_assert(TA::row_idx && TB::row_idx, "direct operands: row-indexed loaders");
+  constexpr bool AV = V && HasVec4<AL>::value, BV = V && HasVec4<BL>::value;
+  const int ra = min(m0 + li, rt.Mr - 1), rb = min(n0 + li, rt.Nr - 1);
+  const typename TA::Idx ia = TA::index(al, ra, 0);
+  const typename TB::Idx ib = TB::index(bl, rb, 0);
+  const int klast = max(rt.Kr - 1, 0), k4last = max(rt.Kr - 4, 0);
+  const int nslab = (rt.Kr + 15) >> 4;
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+  for (int j0 = wv; j0 < nslab; j0 += 4 * DR) {  // rounds of DR slabs of this wave
+    float a[DR][4], b[DR][4];
+#pragma unroll
+    for (int u = 0; u < DR; ++u) {
+      const int k = 16 * (j0 + 4 * u) + 4 * lk;
+      if constexpr (AV) {
+        const float4 v = TA::load4(al, ia, ra, min(k, k4last));
+        a[u][0] = v.x; a[u][1] = v.y; a[u][2] = v.z; a[u][3] = v.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[u][q] = TA::load(al, ia, ra, min(k + q, klast));
+      }
+      if constexpr (BV) {
+        const float4 v = TB::load4(bl, ib, rb, min(k, k4last));
+        b[u][0] = v.x; b[u][1] = v.y; b[u][2] = v.z; b[u][3] = v.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b[u][q] = TB::load(bl, ib, rb, min(k + q, klast));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < DR; ++u) {
+      const int j = j0 + 4 * u;
+      if (j < nslab) {  // (wave-uniform)
+        const int k = 16 * j + 4 * lk;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool kin = k + q < rt.Kr;  // (the staged path's zero padding, on both operands)
+          const float aq = kin ? a[u][q] : 0.f, bq = kin ? b[u][q] : 0.f;
+          if (q & 1) acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, bq, acc2, 0, 0, 0);
+          else acc = __builtin_amdgcn_mfma_f32_16x16x4f32(aq, bq, acc, 0, 0, 0);
+        }
+      }
+    }
+  }
+  // wave partials -> LDS, summed in wave order (as the WS path)
+  float* red = smem;  // [4][TM][PB], then Ct [TM][PB]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wv * TM * PB + (lk * 4 + r) * PB + li] = acc[r] + acc2[r];
+  __syncthreads();
+  float* Ct = red + 4 * TM * PB;
+  {
+    const int x = tid, o = (x / TN) * PB + x % TN;  // TM * TN == 256: one element per thread
+    const float v = ((red[o] + red[TM * PB + o]) + red[2 * TM * PB + o]) + red[3 * TM * PB + o];
+    if (g.deferred) part[((size_t)tile * g.S + s) * TM * TN + x] = v;
+    else Ct[o] = v;
+  }
+  if (g.deferred) return;
+  __syncthreads();
+  epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, Ct + TM * PB});
+}
+
 // One work item (virtual block `bid` of the XCD-grouped order) of a GEMM; `smem` holds CFG::SMEM floats.
 template <class CFG, bool V, class AL, class BL, class EPI>
 __device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, const AL& al, const BL& bl,
                                           const EPI& epi, float* part, int bid, float* smem) {
+  if constexpr (CFG::DR > 0) {
+    gemm_tile_direct<CFG, V>(g, rt, al, bl, epi, part, bid, smem);
+    return;
+  }
   constexpr int TM = CFG::TM, TN = CFG::TN, KC = CFG::KC, FM = CFG::FM, FN = CFG::FN;
   constexpr int PK = CFG::PK, PB = CFG::PB, LA = CFG::LA, LB = CFG::LB;
   float* As = smem;            // [TM][PK]: row m, k contiguous

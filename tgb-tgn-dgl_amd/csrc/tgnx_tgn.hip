@@ -1660,6 +1660,12 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
 }
 
 // ------------------------------------------------------------------ GEMM operands / epilogues
+// Constant operand entries come from these (a pointer select before the load), never from arithmetic on a
+// loaded value: `v * 0/1 + c` in a loader made the compiler wait for the load right where fetch() issued it
+// (s_waitcnt vmcnt after every chunk's load), so the next chunk's operands were never in flight during the
+// current chunk's MFMAs — every K chunk of the GRU GEMM paid a whole load latency.
+__device__ __attribute__((aligned(16))) float kZero4[4] = {0.f, 0.f, 0.f, 0.f};
+__device__ __attribute__((aligned(16))) float kOne4[4] = {1.f, 1.f, 1.f, 1.f};
 // GRU input row m: [aggregated message (Qm) | memory of the node (D)]
 struct LoadGruA {
   const float* X;
@@ -1692,24 +1698,17 @@ struct LoadGruW {
   const float *wih, *whh;
   int Qm, D;
   static constexpr bool k_fast = true;
-  __device__ float operator()(int n, int k) const {  // branch-free
+  __device__ const float* at(int n, int k) const {  // branch-free; the zero blocks read kZero4
     const int j = n >> 2, g = n & 3;
     const bool ih = k < Qm;
     const int gr = ih ? min(g, 2) : (g == 3 ? 2 : g);  // weight row block (clamped: always a valid row)
     const bool zero = ih ? g == 3 : g == 2;
     const float* p = ih ? wih + (int64_t)(gr * D + j) * Qm + k : whh + (int64_t)(gr * D + j) * D + (k - Qm);
-    return *p * f01(!zero);
+    return zero ? kZero4 : p;
   }
+  __device__ float operator()(int n, int k) const { return *at(n, k); }
   __device__ bool vec4() const { return ((Qm | D) & 3) == 0 && al16(wih) && al16(whh); }
-  __device__ float4 load4(int n, int k) const {
-    const int j = n >> 2, g = n & 3;
-    const bool ih = k < Qm;
-    const int gr = ih ? min(g, 2) : (g == 3 ? 2 : g);
-    const float z = f01(!(ih ? g == 3 : g == 2));
-    const float* p = ih ? wih + (int64_t)(gr * D + j) * Qm + k : whh + (int64_t)(gr * D + j) * D + (k - Qm);
-    const float4 w = *reinterpret_cast<const float4*>(p);
-    return make_float4(w.x * z, w.y * z, w.z * z, w.w * z);
-  }
+  __device__ float4 load4(int n, int k) const { return *reinterpret_cast<const float4*>(at(n, k)); }
 };
 // GRUCell (torch gru_cell: r, z = σ(gi + gh), n = tanh(gi_n + r gh_n), h' = (h - n) z + n)
 struct EpiGru {
@@ -2564,7 +2563,7 @@ struct LoadZ1T {
   int D;
   static constexpr bool k_fast = false;
   __device__ float operator()(int n, int m) const {
-    return Z0[(int64_t)m * D + min(n, D - 1)] * f01(n < D) + f01(n >= D);
+    return *(n < D ? Z0 + (int64_t)m * D + n : kOne4);
   }
 };
 struct EpiProjGrad {
@@ -2802,8 +2801,7 @@ struct LoadGruAT1 {
   __device__ Idx index(int, int m) const { return nid[m]; }
   __device__ float load(Idx v, int n, int m) const {
     const bool x = n < Qm, one = n >= Qm + D;
-    const float* p = x ? X + (int64_t)m * Qm + n : mem + v * D + min(n - Qm, D - 1);
-    return *p * f01(!one) + f01(one);
+    return *(x ? X + (int64_t)m * Qm + n : one ? kOne4 : mem + v * D + (n - Qm));
   }
 };
 struct EpiGruWGrad {
@@ -2850,7 +2848,7 @@ struct LoadGruWencT {
   static constexpr bool k_fast = false;
   __device__ float operator()(int n, int r) const {
     const int j = r >> 2, gg = r & 3;
-    return wih[(int64_t)(min(gg, 2) * D + j) * Qm + off + n] * f01(gg != 3);
+    return *(gg == 3 ? kZero4 : wih + (int64_t)(gg * D + j) * Qm + off + n);
   }
 };
 // ---- RNNCell memory updater (DyRepMemory memory_updater_type = 'rnn', modules/memory_module.py:256-259):
