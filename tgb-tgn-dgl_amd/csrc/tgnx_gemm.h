@@ -175,6 +175,13 @@ struct GemmTile {
 // load into a branch whose join waits on it): the body zeroes out-of-range elements when it stashes
 // them, and loaders express constant entries arithmetically (v * 0/1 + c).
 __device__ __forceinline__ float f01(bool b) { return b ? 1.0f : 0.0f; }
+// lane l's value of a per-lane index (any lane l of the wave)
+__device__ __forceinline__ int shfl_idx(int v, int l) { return __shfl(v, l, 64); }
+__device__ __forceinline__ int64_t shfl_idx(int64_t v, int l) {
+  return (int64_t)(((uint64_t)(uint32_t)__shfl((int)(v >> 32), l, 64) << 32) | (uint64_t)(uint32_t)__shfl((int)v, l, 64));
+}
+template <class T>
+__device__ __forceinline__ T shfl_idx(const T& v, int) { return v; }  // (index types without a lane value)
 
 template <class L, class = void>
 struct LoaderTraits {  // plain loader
@@ -300,6 +307,25 @@ __device__ __forceinline__ GemmWork gemm_work(const GemmShape& g, int Mr, int Nr
 // for 16-B operands (V), else 4 scalars; DR slabs per round, all of a round's loads issued before its first
 // MFMA (k past K: both entries selected to zero at use).  The chunked loop waited a whole load latency per
 // 64-deep chunk (stash, barrier, MFMAs, barrier): the GRU GEMM's K = 572 paid 9 of them per tile.
+// Epilogue prefetch (direct tiles): an epilogue with `struct Pre` and
+//   `template <class RI> Pre pre(int m0, int n0, int M, int N, RI rowidx) const`
+// gets its loads issued with the tile's first operand round (rowidx(r): the A loader's index of tile row r,
+// e.g. the node of a gathered row) and is then called as epi(tile, pre): its gathers ride in the operand
+// rounds instead of adding their own dependent rounds after the MFMAs.
+template <class E, class = void>
+struct HasPre : std::false_type {};
+template <class E>
+struct HasPre<E, std::void_t<typename E::Pre>> : std::true_type {};
+struct NoPre {};
+template <class E, class = void>
+struct PreOf {
+  using type = NoPre;
+};
+template <class E>
+struct PreOf<E, std::void_t<typename E::Pre>> {
+  using type = typename E::Pre;
+};
+
 template <class CFG, bool V, class AL, class BL, class EPI>
 __device__ __forceinline__ void gemm_tile_direct(const GemmShape& g, const GemmRt& rt, const AL& al, const BL& bl,
                                                  const EPI& epi, float* part, int bid, float* smem) {
@@ -320,11 +346,11 @@ __device__ __forceinline__ void gemm_tile_direct(const GemmShape& g, const GemmR
   const int klast = max(rt.Kr - 1, 0), k4last = max(rt.Kr - 4, 0);
   const int nslab = (rt.Kr + 15) >> 4;
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
-  for (int j0 = wv; j0 < nslab; j0 += 4 * DR) {  // rounds of DR slabs of this wave
-    float a[DR][4], b[DR][4];
+  float a[DR][4], b[DR][4];
+  auto issue = [&](int j0) {  // one round: DR slabs of this wave, every load issued
 #pragma unroll
     for (int u = 0; u < DR; ++u) {
-      const int k = 16 * (j0 + 4 * u) + 4 * lk;
+      const int k = 16 * (j0 + 4 * rt.Sr * u) + 4 * lk;
       if constexpr (AV) {
         const float4 v = TA::load4(al, ia, ra, min(k, k4last));
         a[u][0] = v.x; a[u][1] = v.y; a[u][2] = v.z; a[u][3] = v.w;
@@ -340,9 +366,18 @@ __device__ __forceinline__ void gemm_tile_direct(const GemmShape& g, const GemmR
         for (int q = 0; q < 4; ++q) b[u][q] = TB::load(bl, ib, rb, min(k + q, klast));
       }
     }
+  };
+  // the epilogue's gathers with the first round (they need only the row indices the operands wait for too)
+  using PreT = typename PreOf<EPI>::type;
+  PreT pre{};
+  if constexpr (HasPre<EPI>::value) pre = epi.pre(m0, n0, rt.Mr, rt.Nr, [&](int r) { return shfl_idx(ia, r); });
+  // split s of S takes the 64-deep chunks s, s + S, ...: this wave's slabs 4 s + wv, 4 (s + S) + wv, ...
+  const int SS = 4 * rt.Sr;
+  for (int j0 = 4 * s + wv; j0 < nslab; j0 += SS * DR) {  // rounds of DR slabs of this wave
+    issue(j0);
 #pragma unroll
     for (int u = 0; u < DR; ++u) {
-      const int j = j0 + 4 * u;
+      const int j = j0 + SS * u;
       if (j < nslab) {  // (wave-uniform)
         const int k = 16 * j + 4 * lk;
 #pragma unroll
@@ -369,14 +404,16 @@ __device__ __forceinline__ void gemm_tile_direct(const GemmShape& g, const GemmR
   }
   if (g.deferred) return;
   __syncthreads();
-  epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, Ct + TM * PB});
+  if constexpr (HasPre<EPI>::value) epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, Ct + TM * PB}, pre);
+  else epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, Ct + TM * PB});
 }
 
 // One work item (virtual block `bid` of the XCD-grouped order) of a GEMM; `smem` holds CFG::SMEM floats.
 template <class CFG, bool V, class AL, class BL, class EPI>
 __device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, const AL& al, const BL& bl,
                                           const EPI& epi, float* part, int bid, float* smem) {
-  if constexpr (CFG::DR > 0) {
+  if constexpr (CFG::DR > 0 && V) {  // (element-wise operands: the staged path — measured faster there, the
+                                      // comment-shaped 2-hop GRU at Qm = 302: 26 vs 41 us per launch)
     gemm_tile_direct<CFG, V>(g, rt, al, bl, epi, part, bid, smem);
     return;
   }

@@ -3,9 +3,11 @@
 
 using namespace tgnx;
 
-// Tile config: 64x64 once that already fills the chip, else 32x32.  K up to 4 chunks: one workgroup
-// per tile loops over K; larger K: split-K partials + a fixup launch.
+// Tile config: 64x64 once that already fills the chip, else 16x16 wave-split tiles with direct operands (the
+// TGN step's long-K config, GemmCfg::DR: this entry point is also its unit test against torch).  K up to 4
+// chunks: one workgroup per tile loops over K; larger K: split-K partials + a fixup launch.
 static bool api_big(int64_t M, int64_t N) { return ((M + 63) / 64) * ((N + 63) / 64) >= 512; }
+using GD = GemmCfg<16, 16, 64, 1, true, 3>;
 template <class CFG>
 static GemmShape gemm_api_shape(int64_t M, int64_t N, int64_t K) {
   if (K <= 4 * CFG::KC) return gemm_shape<CFG>((int)M, (int)N, (int)K);
@@ -16,7 +18,7 @@ extern "C" {
 
 size_t tgnx_gemm_f32_ws_bytes(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0) return 256;
-  const GemmShape g = api_big(M, N) ? gemm_api_shape<G64>(M, N, K) : gemm_api_shape<G32>(M, N, K);
+  const GemmShape g = api_big(M, N) ? gemm_api_shape<G64>(M, N, K) : gemm_api_shape<GD>(M, N, K);
   return gemm_partial_floats(g) * 4 + 256;
 }
 
@@ -42,7 +44,7 @@ int tgnx_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, 
   };
   auto run = [&](const auto& al, const auto& bl) {
     if (api_big(M, N)) run2(G64{}, al, bl);
-    else run2(G32{}, al, bl);
+    else run2(GD{}, al, bl);
   };
   if (!trans_a && trans_b)
     run(LoadRowK{A, (int)M, Kc, (int)lda}, LoadRowK{B, (int)N, Kc, (int)ldb});

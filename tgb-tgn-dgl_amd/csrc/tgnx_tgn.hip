@@ -766,7 +766,7 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
   __shared__ int lwl[LW];
   bool listed = false;
   int ncw, nnw, nrw = 0;
-  if (!direct && c.layers == 1) {
+  if (!direct) {
     const int64_t SW = (c.words + 31) >> 5, sq = (SW + T - 1) / T, s0 = min(SW, tid * sq), s1 = min(SW, s0 + sq);
     uint32_t sv[SCAN_SWR];
     int nz = 0;
@@ -794,6 +794,11 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
       for (int j = 0; j < SCAN_SWR; ++j) emit(s0 + j, sv[j]);  // (zero past s1)
       for (int64_t i = s0 + SCAN_SWR; i < s1; ++i) emit(i, c.nbs[i]);
       ncw = nnw = tw;
+      if (c.layers == 2) {  // the roots' words for pass 3 (global list, as before)
+        int unused;
+        occupied_words2(c.rbs, nullptr, c.words, c.rl, nullptr, sh, &nrw, &unused);
+        __threadfence_block();
+      }
       __syncthreads();
     }
   }
@@ -845,7 +850,7 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
   int R, M, rc, rank;
   block_excl_scan2(nc, np, sh, &rc, &rank, &R, &M);
   const bool fits = R <= c.Rcap && M <= c.Mcap;
-  const bool lds_c = walk && TRAIN && c.layers == 1 && R <= 3 * c.Bmax;  // (block-uniform)
+  const bool lds_c = walk && TRAIN && R <= 3 * c.Bmax;  // (block-uniform)
   int64_t* lv = reinterpret_cast<int64_t*>(smem);                          // [3 Bmax] centre node
   int* lloc = reinterpret_cast<int*>(smem + (size_t)3 * c.Bmax * 8);       // [3 Bmax] its node rank
   if (walk) {
@@ -946,6 +951,7 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
         re += kv[j];
         c.cent_loc[x] = loc[j];
         c.crank[loc[j]] = x;
+        if (c.x2r) c.x2r[x] = -1;
         if (up[j]) {
           c.upd[ru] = v[j];
           c.upd_loc[ru] = loc[j];
@@ -961,37 +967,37 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
       c.ctl[TGNX_CTL_SUM_E] += E;
       c.ctl[TGNX_CTL_SUM_S] += M;
     }
-    return;  // (1 hop: no root pass)
-  }
-  for (int x = x0; x < x1; ++x) {
-    const int64_t v = c.cent[x];
-    ne += c.kval[v];
-    nu += c.node_gen[v] == gen;
-  }
-  int E, U, re, ru;
-  block_excl_scan2(ne, nu, sh, &re, &ru, &E, &U);
-  for (int x = x0; x < x1; ++x) {
-    const int64_t v = c.cent[x];
-    const int loc = (int)c.assoc[v];
-    c.ceoff[x] = re;
-    re += c.kval[v];
-    c.cent_loc[x] = loc;
-    c.crank[loc] = x;
-    if (c.x2r) c.x2r[x] = -1;
-    if (c.node_gen[v] == gen) {
-      c.upd[ru] = v;
-      c.upd_loc[ru] = loc;
-      ++ru;
+  } else {
+    for (int x = x0; x < x1; ++x) {
+      const int64_t v = c.cent[x];
+      ne += c.kval[v];
+      nu += c.node_gen[v] == gen;
     }
-  }
-  if (tid == 0) {
-    c.ceoff[R] = E;
-    c.cnt[CNT_R] = R;
-    c.cnt[CNT_M] = M;
-    c.cnt[CNT_E] = E;
-    c.cnt[CNT_U] = U;
-    c.ctl[TGNX_CTL_SUM_E] += E;
-    c.ctl[TGNX_CTL_SUM_S] += M;
+    int E, U, re, ru;
+    block_excl_scan2(ne, nu, sh, &re, &ru, &E, &U);
+    for (int x = x0; x < x1; ++x) {
+      const int64_t v = c.cent[x];
+      const int loc = (int)c.assoc[v];
+      c.ceoff[x] = re;
+      re += c.kval[v];
+      c.cent_loc[x] = loc;
+      c.crank[loc] = x;
+      if (c.x2r) c.x2r[x] = -1;
+      if (c.node_gen[v] == gen) {
+        c.upd[ru] = v;
+        c.upd_loc[ru] = loc;
+        ++ru;
+      }
+    }
+    if (tid == 0) {
+      c.ceoff[R] = E;
+      c.cnt[CNT_R] = R;
+      c.cnt[CNT_M] = M;
+      c.cnt[CNT_E] = E;
+      c.cnt[CNT_U] = U;
+      c.ctl[TGNX_CTL_SUM_E] += E;
+      c.ctl[TGNX_CTL_SUM_S] += M;
+    }
   }
   if (c.layers != 2) return;
   // pass 3 (2 hops): the roots (sorted) from their bitmap -> root index, outer-centre index (crank is
@@ -1717,7 +1723,42 @@ struct EpiGru {
   int64_t base;
   int D;
   float *Z0, *gates;
+  // thread x < 64 of a 16 x 16 tile: row x / 4, unit n0 / 4 + x % 4 — its biases and memory entry, loaded
+  // with the tile's first operand round (gemm_tile_direct); rowidx(r) = row r's node (LoadGruA's index)
+  struct Pre {
+    float bs[6], h;
+  };
+  template <class RI>
+  __device__ Pre pre(int m0, int n0, int M, int N, RI rowidx) const {
+    Pre p;
+    const int x = threadIdx.x & 63, r = x >> 2, u = x & 3;
+    const int64_t v = rowidx(r);  // (every lane takes part in the shuffle)
+    const int j = min(n0 / 4 + u, max(N / 4 - 1, 0));
+    p.bs[0] = bih[j]; p.bs[1] = bhh[j];
+    p.bs[2] = bih[D + j]; p.bs[3] = bhh[D + j];
+    p.bs[4] = bih[2 * D + j]; p.bs[5] = bhh[2 * D + j];
+    p.h = mem[v * D + j];
+    return p;
+  }
   template <class T>
+  __device__ void operator()(const T& t, const Pre& p) const {
+    static_assert(T::tm * T::tn / 4 <= 64, "one wave of (row, unit) items");
+    const int q4 = t.tn / 4, x = threadIdx.x;
+    if (x >= t.tm * q4) return;
+    const int r = x / q4, u = x % q4, m = t.m0 + r, j = t.n0 / 4 + u;
+    if (m >= t.M || 4 * j >= t.N) return;
+    const float* row = t.c + r * t.pitch + 4 * u;
+    const float pr = row[0] + (p.bs[0] + p.bs[1]);
+    const float pz = row[1] + (p.bs[2] + p.bs[3]);
+    const float gin = row[2] + p.bs[4];
+    const float ghn = row[3] + p.bs[5];
+    const float rr = sigm(pr), zz = sigm(pz);
+    const float nn = tanhf(gin + rr * ghn);
+    Z0[(int64_t)m * D + j] = (p.h - nn) * zz + nn;
+    float4* gp = reinterpret_cast<float4*>(gates + ((int64_t)m * D + j) * 4);
+    *gp = make_float4(rr, zz, nn, ghn);
+  }
+  template <class T>  // (staged tiles of any shape: the loads after the MFMAs)
   __device__ void operator()(const T& t) const {
     const int q4 = t.tn / 4;
     for (int x = threadIdx.x; x < t.tm * q4; x += blockDim.x) {
@@ -2761,7 +2802,32 @@ struct EpiGruBwd {
   const int64_t* nid;
   float* dG;
   int D;
+  // a 16 x 16 tile's element of this thread (GemmTile<16, 16>::row_of / col_of (0)): its node and saved gates,
+  // loaded with the tile's first operand round (gemm_tile_direct)
+  struct Pre {
+    int64_t node;
+    float4 gt;
+  };
+  template <class RI>
+  __device__ Pre pre(int m0, int n0, int M, int N, RI) const {
+    const int m = min(m0 + GemmTile<16, 16>::row_of(0), M - 1), j = min(n0 + GemmTile<16, 16>::col_of(0), N - 1);
+    return Pre{nid[m], *reinterpret_cast<const float4*>(gates + ((int64_t)m * D + j) * 4)};
+  }
   template <class T>
+  __device__ void operator()(const T& t, const Pre& p) const {
+    static_assert(T::per == 1, "16 x 16 tiles");
+    const int r = T::row_of(0), cc = T::col_of(0), m = t.m0 + r, j = t.n0 + cc;
+    const float h = mem[p.node * D + min(j, t.N - 1)];
+    if (m >= t.M || j >= t.N) return;
+    const float dhp = t(r, cc);
+    const float rr = p.gt.x, zz = p.gt.y, nn = p.gt.z, ghn = p.gt.w;
+    const float dn = dhp * (1.0f - zz), dz = dhp * (h - nn);
+    const float dpn = dn * (1.0f - nn * nn);
+    const float dr = dpn * ghn;
+    float4* o = reinterpret_cast<float4*>(dG + ((int64_t)m * D + j) * 4);
+    *o = make_float4(dr * rr * (1.0f - rr), dz * zz * (1.0f - zz), dpn, dpn * rr);
+  }
+  template <class T>  // (staged tiles of any shape)
   __device__ void operator()(const T& t) const {
     int64_t node[T::per];
     float4 gt[T::per];
