@@ -65,7 +65,7 @@ struct GemmCfg {
 #define TGNX_G32_PF 1
 #endif
 #ifndef TGNX_G32_DR
-#define TGNX_G32_DR 0
+#define TGNX_G32_DR 2  // (same-box A/B, wiki step: staged 0.1030, 2 slabs per round 0.1024, 5 0.1037 ms)
 #endif
 using G32 = GemmCfg<TGNX_G32_T, TGNX_G32_T, TGNX_G32_KC, TGNX_G32_PF, TGNX_G32_WS, TGNX_G32_DR>;  // the TGN step's GEMMs
 #ifndef TGNX_G32L_T

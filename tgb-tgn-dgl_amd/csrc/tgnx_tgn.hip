@@ -1612,16 +1612,26 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
         }
       }
       const float dt = lu - te;
-      for (int q = lane; q < D; q += 64) {
-        const float a = fmaf(tw[q], dt, tb[q]);
-        if (mode == 0) {
+      if (mode == 0) {  // train: the edge's whole lin_edge operand row [cos enc | msg] (stride D + d), so the
+                        // lin_edge / dW_edge GEMMs read dense rows (no event-id gather round per K chunk)
+        const int d = c.d, DA = D + d;
+        float* row = c.encE + (int64_t)o * DA;
+        const float* msg = c.ev_msg + e * d;
+        float mv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mv[i] = msg[min(lane + 64 * i, max(d - 1, 0))];  // (loads before the sincos)
+        for (int q = lane; q < D; q += 64) {
           float sn, cs;
-          te_sincos(a, sn, cs);
-          c.encE[(int64_t)o * D + q] = cs;
+          te_sincos(fmaf(tw[q], dt, tb[q]), sn, cs);
+          row[q] = cs;
           c.sinE[(int64_t)o * D + q] = sn;
-        } else {
-          c.encE[(int64_t)o * D + q] = te_cos(a);
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (lane + 64 * i < d) row[D + lane + 64 * i] = mv[i];
+        for (int q = lane + 256; q < d; q += 64) row[D + q] = msg[q];
+      } else {
+        for (int q = lane; q < D; q += 64) c.encE[(int64_t)o * D + q] = te_cos(fmaf(tw[q], dt, tb[q]));
       }
     }
     return;
@@ -1844,6 +1854,27 @@ struct LoadEdgeAttrMapT {
   __device__ float load(const Idx& r, int n, int e) const { return a.load(r, e, n); }
 };
 // node-embedding input row m: train z0 (GRU output), eval memory[nid[m]] (memory_module.py:121-122)
+// train: row e of a root-level edge operand = row map[e] of the outer edges' [cos enc | msg] rows (2 hops)
+struct LoadAttrMap {
+  const float* rows;
+  const int* map;
+  int ld;
+  static constexpr bool k_fast = true;
+  using Idx = int;
+  static constexpr bool row_idx = true;
+  __device__ Idx index(int e, int) const { return map[e]; }
+  __device__ float load(Idx r, int, int k) const { return rows[(int64_t)r * ld + k]; }
+  __device__ bool vec4() const { return (ld & 3) == 0 && al16(rows); }
+  __device__ float4 load4(Idx r, int, int k) const { return *reinterpret_cast<const float4*>(rows + (int64_t)r * ld + k); }
+};
+struct LoadAttrMapT {
+  LoadAttrMap a;
+  static constexpr bool k_fast = false;
+  using Idx = int;  // k = root edge: the index changes per chunk
+  static constexpr bool row_idx = false;
+  __device__ Idx index(int, int e) const { return a.map[e]; }
+  __device__ float load(Idx r, int n, int) const { return a.rows[(int64_t)r * a.ld + n]; }
+};
 struct LoadZ {
   const float* Z0;
   const float* mem;
@@ -3533,7 +3564,7 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.tgp_e1 = (k.Etr + G32::TM - 1) / G32::TM + (k.Mtr + G32::TM - 1) / G32::TM;
   W.tgp_rows = W.tgp_e1 + (k.E1tr + G32::TM - 1) / G32::TM;
   W.tgp = carve(off, (size_t)W.tgp_rows * 2 * D * 4);
-  W.encE = carve(off, (size_t)k.Ecap * D * 4);
+  W.encE = carve(off, (size_t)k.Ecap * (D + k.d) * 4);  // train: [cos enc | msg] rows; eval: cos rows (stride D)
   W.sinE = carve(off, (size_t)k.Etr * D * 4);
   W.s0m = carve(off, (size_t)k.Mtr * D * 4);
   W.s1m = carve(off, (size_t)k.Mtr * D * 4);
@@ -4036,9 +4067,9 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   TGNX_LAUNCH_CHECK("tgn_agg_emit");
   // GRU over every sampled node ‖ lin_edge over every sampled edge (‖ 2 hops: conv2's lin_edge over the
   // root edges)
-  const LoadEdgeAttr ea{c.encE, c.e_id, c.ev_msg, D, d};
+  const LoadRowK ea{c.encE, k.Etr, D + d, D + d};  // the edges' [cos enc | msg] rows (tgn_agg_emit, train)
   const bool two = k.layers == 2;
-  const LoadEdgeAttrMap ea1{c.encE, c.e1_id, c.e1_e2, c.ev_msg, D, d};
+  const LoadAttrMap ea1{c.encE, c.e1_e2, D + d};  // root edge -> its outer edge's row
   const auto j_gru = gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, Cl::G * D, Qm + D, c.cnt + CNT_M),
                                     LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0}, Cl::w(c), Cl::epi(c, c.nid, 0),
                                     (float*)nullptr);
@@ -4107,7 +4138,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
     // conv2's (dk, dv) sums ‖ its dE2-only GEMMs (as in the 1-hop step below), then dh1 ‖ dW_proj2
     gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{cr}, gridn(k.E1tr, KVR_CH, 1 << 20)},
-                 gemm_job<GW>(shp_dWe2(k, c.cnt), LoadKRow{c.dE2, HC, k.E1tr, HC}, LoadEdgeAttrMapT{ea1},
+                 gemm_job<GW>(shp_dWe2(k, c.cnt), LoadKRow{c.dE2, HC, k.E1tr, HC}, LoadAttrMapT{ea1},
                                EpiDeferred{}, c.pF),
                  gemm_job<G32>(gemm_shape<G32>(k.E1tr, D, HC, c.cnt + CNT_E1), LoadRowK{c.dE2, k.E1tr, HC, HC},
                                LoadKRow{P + c.L.we2, D, HC, D + d},
@@ -4134,7 +4165,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const EpiGradStore e_dWe{G, c.L.we, D + d, cf.adf};
   probe_begin(TGNX_K_KV, s);
   const auto j_kvr = BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(k.Etr, KVR_CH, 1 << 20)};
-  const auto j_dwe = gemm_job<GW>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadEdgeAttrT{ea}, EpiDeferred{}, c.pA);
+  const auto j_dwe = gemm_job<GW>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadKRow{c.encE, D + d, k.Etr, D + d},
+                                  EpiDeferred{}, c.pA);
   const auto j_denc = gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
                                     LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
                                     (float*)nullptr);
