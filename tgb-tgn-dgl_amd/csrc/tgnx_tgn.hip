@@ -3495,14 +3495,28 @@ static Caps make_caps(const tgnx_tgn_config* cfg) {
 // split count of a long-K weight-gradient GEMM: ~2k rows of K per split (2-hop edge sets are ~10x the
 // 1-hop ones), at least 8
 static int ksplit(int K, int smin) { return std::max(smin, std::min(64, K / 2048)); }
+// minimum split counts of the deferred weight-gradient GEMMs (their partials make an HBM round trip through
+// the fixup launch: fewer splits, less traffic, longer K chains per workgroup)
+#ifndef TGNX_S_WE
+#define TGNX_S_WE 8
+#endif
+#ifndef TGNX_S_WP
+#define TGNX_S_WP 4
+#endif
+#ifndef TGNX_S_WG
+#define TGNX_S_WG 2  // (runtime-capped: 3 at the wiki shape; A/B 0.1022 vs 0.1027 ms with 4, and 25 % fewer partials)
+#endif
+#ifndef TGNX_S_LP
+#define TGNX_S_LP 10  // (one 64-deep chunk per split at B = 200: A/B 0.1010 vs 0.1022 ms with 5; dW_edge 16 and dW_proj 8 splits: ±0)
+#endif
 // the deferred (split-K) weight-gradient GEMMs of a train step
-static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.Etr, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, ksplit(k.Etr, 8)); }
-static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.HC, k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
+static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.Etr, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, ksplit(k.Etr, TGNX_S_WE)); }
+static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.HC, k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, TGNX_S_WP)); }
 // 2 hops: conv2's projections (K = outer centres) and lin_edge (K = root edges)
 static GemmShape shp_dWp2(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.HC, k.D + 1, k.Rtr, nullptr, nullptr, cnt ? cnt + CNT_R : nullptr, ksplit(k.Rtr, 4)); }
 static GemmShape shp_dWe2(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.E1tr, nullptr, nullptr, cnt ? cnt + CNT_E1 : nullptr, ksplit(k.E1tr, 8)); }
-static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, 5); }
-static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, 4)); }
+static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, TGNX_S_LP); }
+static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, TGNX_S_WG)); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
       Ep, alpha, Zc, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
