@@ -3515,7 +3515,7 @@ static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_spli
 // 2 hops: conv2's projections (K = outer centres) and lin_edge (K = root edges)
 static GemmShape shp_dWp2(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.HC, k.D + 1, k.Rtr, nullptr, nullptr, cnt ? cnt + CNT_R : nullptr, ksplit(k.Rtr, 4)); }
 static GemmShape shp_dWe2(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.E1tr, nullptr, nullptr, cnt ? cnt + CNT_E1 : nullptr, ksplit(k.E1tr, 8)); }
-static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, TGNX_S_LP); }
+static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, std::max(TGNX_S_LP, std::min(64, (3 * k.B + 63) / 64))); }
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, TGNX_S_WG)); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
