@@ -352,9 +352,10 @@ def tgn_step_bytes(d, D, K, layers):
     return 2 * (fwd + gru)
 
 
-def tgn_launch_bytes(name, E, M, Bw, Bg, D, d, K, P, N):
+def tgn_launch_bytes(name, E, M, Bw, Bg, D, d, K, P, N, kvf=False):
     """Algorithmic bytes of one launch of the TGN step: E sampled edges, M sampled nodes,
-    Bw this rank's events, Bg the global batch, P trainable parameters, N nodes."""
+    Bw this rank's events, Bg the global batch, P trainable parameters, N nodes.  kvf: the 1-hop step whose
+    attention backward also sums each edge's (dk, dv) (no tgn_kv_dE launch; its dE-only GEMMs in tgn_wgrad3)."""
     Qm = 3 * D + d
     per_edge = 20 + 4 * d + 4 * D + 4                 # SURVEY §8(d): ring entry, msg row, neighbour row, Δt
     if name == "tgn_agg_emit":                        # edge records + Δt enc ‖ message gather + aggregate
@@ -363,6 +364,8 @@ def tgn_launch_bytes(name, E, M, Bw, Bg, D, d, K, P, N):
         return Bg * 4 * K * 20 + M * (4 * Qm + 4 * D + 4 * D + 16 * D) + E * (4 * d + 12 + 4 * D)
     if name == "tgn_proj":                            # z0 in, q / k / v / skip out
         return M * (4 * D + 16 * D)
+    if name == "tgn_attn_bwd" and kvf:                # + per edge: (dk, dv) summed into dP, dE written
+        return E * (12 * D + 8) + E * (8 * D + 4 * D)
     if name in ("tgn_attn_fwd", "tgn_attn_bwd"):      # per edge: k, v, edge rows (+ softmax terms)
         return E * (12 * D + 8)
     if name == "tgn_pred_train":                      # per event 3 embedding rows ‖ the attention of its roots
@@ -371,8 +374,9 @@ def tgn_launch_bytes(name, E, M, Bw, Bg, D, d, K, P, N):
         return E * (8 * D + 8 * D) + E * (4 * D + 4 * (D + d) + 12 + 4 * D)
     if name == "tgn_wgrad_dz0":                       # dW_proj, dW_src/dst ‖ dz0 + GRU backward
         return M * 76 * D
-    if name == "tgn_wgrad3":                          # dW_gru (dG, [X | memory]) ‖ dX_enc ‖ stores
-        return M * (16 * D + 4 * Qm + 4 * D + 16 * D) + Bg * 2 * (8 + 4 * d)
+    if name == "tgn_wgrad3":                          # dW_gru (dG, [X | memory]) ‖ dX_enc ‖ stores (‖ dW_edge ‖ dEnc W_e)
+        return (M * (16 * D + 4 * Qm + 4 * D + 16 * D) + Bg * 2 * (8 + 4 * d)
+                + (E * (4 * D + 4 * (D + d) + 12 + 4 * D) if kvf else 0))
     if name == "tgn_fixup_update":                    # Adam over every parameter (p, m, v, g in; p, m, v out)
         return 28 * P
     if name == "tgn_adam":
@@ -483,9 +487,12 @@ def run_tgn(args, world, rank, dev):
         steps_n = max(args.probe_steps, 1)
         E = (pe1 - pe0) / steps_n
         M = (pm1 - pm0) / steps_n
-        algo = tgn_launch_bytes(name, E, M, Bw, Bg, D, d, K, P, N) * (steps_n / launches if name != "tgn_scan" else 1)
-        probes[name] = dict(avg_us=avg_ms * 1e3, launches=launches, edges=E, nodes=M, bytes=algo,
-                            gbs=(algo / (avg_ms * 1e-3) / 1e9) if algo else None)
+        probes[name] = dict(avg_us=avg_ms * 1e3, launches=launches, edges=E, nodes=M, steps_n=steps_n)
+    kvf = args.layers == 1 and "tgn_kv_dE" not in probes
+    for name, q in probes.items():
+        algo = tgn_launch_bytes(name, q["edges"], q["nodes"], Bw, Bg, D, d, K, P, N, kvf) * (
+            q.pop("steps_n") / q["launches"] if name != "tgn_scan" else 1)
+        q.update(bytes=algo, gbs=(algo / (q["avg_us"] * 1e-6) / 1e9) if algo else None)
     dom = max(probes, key=lambda k: probes[k]["avg_us"])        # the longest launch of the step
     pd = probes[dom]
     Qm = 3 * D + d

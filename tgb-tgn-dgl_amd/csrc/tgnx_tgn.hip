@@ -199,6 +199,10 @@ struct Ctx {
   uint64_t adv_seed = 0;
   AdamFuse adf;  // fused optimizer (tgnx_tgn_train_step) or plain gradient stores
   float* dKV;  // per edge [dk | dv] of the attention backward [E][2 HC] (tgn_kv_reduce sums them into dP)
+  // kvf (1-hop train step, attention backward fused with the k / v sums, tgn_attn_bwd's edge blocks): the
+  // forward also writes alk = alpha * keep per edge [E][2] and Qo = [q | Σ alpha~ v] per centre [R][2 HC]
+  float *alk, *Qo;
+  int kvf = 0;
   float *encE, *sinE;  // per sampled edge: cos / sin of the Δt encoding argument [E][D]
   float *s0m, *s1m;    // per GRU row: (mean over its messages of) sin(arg), sin(arg) Δt  [M][D]
   float *pA, *pB, *pC, *pD;  // split-K partials of the deferred weight-gradient GEMMs
@@ -1989,6 +1993,20 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
         t0 *= keep32(base, 0u, c.p, c.inv_keep);
         t1 *= keep32(base, 1u, c.p, c.inv_keep);
       }
+      if (c.kvf) {
+        c.alk[(int64_t)(e0 + lane) * 2] = t0;
+        c.alk[(int64_t)(e0 + lane) * 2 + 1] = t1;
+      }
+    }
+  };
+  // kvf: the centre's q and aggregated message output (every root of the centre writes equal values)
+  auto put_qo = [&]() {
+    if (TRAIN && c.kvf && lane < C) {
+      float* qo = c.Qo + (int64_t)x * 2 * HC;
+      qo[lane] = q0;
+      qo[C + lane] = q1;
+      qo[HC + lane] = o0;
+      qo[HC + C + lane] = o1;
     }
   };
   if (ne > 0 && ne <= ATT_EB) {  // every ring of K <= 16: one load round
@@ -2017,6 +2035,7 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
       o0 += v0[u] * lane_f(t0, u);
       o1 += v1[u] * lane_f(t1, u);
     }
+    put_qo();
     return make_float2(o0 + sk0, o1 + sk1);
   }
   for (int b = 0; b < ne; b += ATT_EB) {
@@ -2054,6 +2073,7 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
       o1 += v1[u] * lane_f(t1, b + u);
     }
   }
+  put_qo();
   return make_float2(o0 + sk0, o1 + sk1);
 }
 template <bool TRAIN>
@@ -2378,17 +2398,135 @@ __device__ void lp_vec_body(const Ctx& c, int y, int lane) {
   }
 }
 
-// Backward of tgn_attn_fwd (wave per centre) ‖ trailing blocks: lp_vec_body.
+// Attention backward, edge half (kvf: 1-hop train step, the middle blocks of tgn_attn_bwd).  The centre's
+// output gradient g = dZc[x] enters linearly: with t = alpha * keep (alk) and the centre's aggregated message
+// output o = Σ_e t_e v_e (Qo, written by the forward), Σ_e alpha_e dalpha_e = g · o per head, so
+//   ds_e = t_e (g · v_e) - alpha_e (g · o),  dk_e = ds_e q / sqrt(C),  dv_e = t_e g,  dE_e = dk_e + dv_e
+// need no other edge of the centre: each edge's (dk, dv) is computed where it is summed into its neighbour's
+// dP row (no per-edge dKV round trip, no separate k / v reduction launch), while the centre blocks compute dq.
+// Workgroup per chunk of KVE_CH consecutive edges sorted by neighbour in LDS (as kv_reduce_body); a wave takes
+// KVE_PW sorted edges, lanes over the channels of both heads, and sums runs of equal neighbours in registers.
+#ifndef TGNX_KVE_CH
+#define TGNX_KVE_CH 32
+#endif
+constexpr int KVE_CH = TGNX_KVE_CH, KVE_PW = KVE_CH / 4;
+__device__ void kv_edge_body(const Ctx& c, int bid) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int E = c.ceoff[c.cnt[c.rsel]];
+  const int eb = bid * KVE_CH;
+  if (eb >= E) return;  // whole workgroup
+  const int ne = min(KVE_CH, E - eb);
+  __shared__ int sj[KVE_CH], sorder[KVE_CH];
+  const int t = threadIdx.x;
+  if (t < KVE_CH) sj[t] = t < ne ? c.e_j[eb + t] : INT_MAX;
+  __syncthreads();
+  if (t < ne) {  // stable rank of (neighbour, edge)
+    const int key = sj[t];
+    int r = 0;
+#pragma unroll 16
+    for (int u = 0; u < KVE_CH; ++u) {
+      const int ju = sj[u];
+      r += (ju < key) || (ju == key && u < t);
+    }
+    sorder[r] = t;
+  }
+  __syncthreads();
+  const int w = t >> 6, lane = t & 63;
+  const int i0 = w * KVE_PW;
+  if (i0 >= ne) return;
+  const int n = min(KVE_PW, ne - i0);
+  const int C = c.C, HC = c.HC;
+  const bool okl = lane < C;
+  const float on = f01(okl);
+  const int l0 = min(lane, C - 1);
+  const float isq = 1.0f / sqrtf((float)C);
+  int jj[KVE_PW], er[KVE_PW], xx[KVE_PW];
+  float a0[KVE_PW], a1[KVE_PW], t0[KVE_PW], t1[KVE_PW];
+#pragma unroll
+  for (int u = 0; u < KVE_PW; ++u) {
+    const int e = sorder[i0 + min(u, n - 1)];
+    jj[u] = sj[e];
+    er[u] = eb + e;
+  }
+#pragma unroll
+  for (int u = 0; u < KVE_PW; ++u) {  // first round: the edges' centres and softmax weights
+    xx[u] = c.e_c[er[u]];
+    a0[u] = c.alpha[(int64_t)er[u] * 2];
+    a1[u] = c.alpha[(int64_t)er[u] * 2 + 1];
+    t0[u] = c.alk[(int64_t)er[u] * 2];
+    t1[u] = c.alk[(int64_t)er[u] * 2 + 1];
+  }
+  float g0[KVE_PW], g1[KVE_PW], q0[KVE_PW], q1[KVE_PW], o0[KVE_PW], o1[KVE_PW], v0[KVE_PW], v1[KVE_PW];
+#pragma unroll
+  for (int u = 0; u < KVE_PW; ++u) {  // second round: centre rows (g, q, o), the neighbour's v row + edge row
+    const float* G = c.dZc + (int64_t)xx[u] * HC;
+    const float* Q = c.Qo + (int64_t)xx[u] * 2 * HC;
+    const float* Pj = c.P + (int64_t)jj[u] * 4 * HC + 2 * HC;
+    const float* Ee = c.Ep + (int64_t)er[u] * HC;
+    g0[u] = G[l0];
+    g1[u] = G[C + l0];
+    q0[u] = Q[l0];
+    q1[u] = Q[C + l0];
+    o0[u] = Q[HC + l0];
+    o1[u] = Q[HC + C + l0];
+    v0[u] = Pj[l0] + Ee[l0];
+    v1[u] = Pj[C + l0] + Ee[C + l0];
+  }
+  float s[4] = {0.f, 0.f, 0.f, 0.f};  // run sums: dk (head 0, 1), dv (head 0, 1)
+  int jc = jj[0];
+  auto flush = [&]() {
+    if (okl) {
+      float* dst = c.dP + (int64_t)jc * 4 * HC + HC;
+      atomicAdd(dst + lane, s[0]);
+      atomicAdd(dst + C + lane, s[1]);
+      atomicAdd(dst + HC + lane, s[2]);
+      atomicAdd(dst + HC + C + lane, s[3]);
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < KVE_PW; ++u) {
+    if (u >= n) break;
+    if (jj[u] != jc) {  // wave-uniform run boundary
+      flush();
+      s[0] = s[1] = s[2] = s[3] = 0.f;
+      jc = jj[u];
+    }
+    const float gv0 = wave_sum_f(g0[u] * v0[u] * on), gv1 = wave_sum_f(g1[u] * v1[u] * on);
+    const float go0 = wave_sum_f(g0[u] * o0[u] * on), go1 = wave_sum_f(g1[u] * o1[u] * on);
+    const float ds0 = (t0[u] * gv0 - a0[u] * go0) * isq, ds1 = (t1[u] * gv1 - a1[u] * go1) * isq;
+    const float dk0 = ds0 * q0[u], dk1 = ds1 * q1[u];
+    const float dv0 = t0[u] * g0[u], dv1 = t1[u] * g1[u];
+    if (okl) {
+      float* dEe = c.dE + (int64_t)er[u] * HC;
+      dEe[lane] = dk0 + dv0;
+      dEe[C + lane] = dk1 + dv1;
+    }
+    s[0] += dk0;
+    s[1] += dk1;
+    s[2] += dv0;
+    s[3] += dv1;
+  }
+  flush();
+}
+
+// Backward of tgn_attn_fwd (wave per centre) ‖ [nkv > 0: kv_edge_body blocks; the centre waves then write
+// dq and the skip gradient only] ‖ trailing blocks: lp_vec_body.
 // dk / dv of an edge belong to its neighbour's row of dP.  They are stored per edge (dKV, plain
 // coalesced stores) and summed into dP by tgn_kv_reduce: a hub neighbour is shared by most centres (a
 // wiki-shaped hub user sits in ~40 % of the page rings), and per-edge global atomics on its row
 // serialised at the L2 (attn_bwd 36 us, 15 us without them).
-__global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
+__global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv) {
   TGNX_STAMP(6);
-  if ((int)blockIdx.x >= ncb) {
-    lp_vec_body(c, ((int)blockIdx.x - ncb) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+  if ((int)blockIdx.x >= ncb + nkv) {
+    lp_vec_body(c, ((int)blockIdx.x - ncb - nkv) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
     return;
   }
+  if ((int)blockIdx.x >= ncb) {
+    kv_edge_body(c, (int)blockIdx.x - ncb);
+    return;
+  }
+  const bool wkv = nkv == 0;  // per-edge dk / dv / dE written here (else by the edge blocks)
   const int lane = threadIdx.x & 63;
   const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
   // first round: batch descriptor, centre count, the centre's row / edge range (clamped, as tgn_attn_fwd);
@@ -2463,7 +2601,7 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
       float* dKe = c.dKV + (int64_t)(e0 + u) * 2 * HC;  // [dk (HC) | dv (HC)]
       dq0 += d0 * kk0[u];
       dq1 += d1 * kk1[u];
-      if (okl) {
+      if (okl && wkv) {
         const float dk0 = d0 * q0, dk1 = d1 * q1;
         const float dv0 = b0 * g0, dv1 = b1 * g1;
         dEe[lane] = dk0 + dv0;
@@ -2526,7 +2664,7 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb) {
       float* dKe = c.dKV + (int64_t)(e0 + e) * 2 * HC;  // [dk (HC) | dv (HC)]
       dq0 += d0 * kk0[u];
       dq1 += d1 * kk1[u];
-      if (okl) {
+      if (okl && wkv) {
         const float dk0 = d0 * q0, dk1 = d1 * q1;
         const float dv0 = b0 * g0, dv1 = b1 * g1;
         dEe[lane] = dk0 + dv0;
@@ -3273,6 +3411,19 @@ struct MarkNextJob {
 #ifndef TGNX_PRED_ATT
 #define TGNX_PRED_ATT 1  // 1 hop: attention forward inside tgn_pred_train (0: its own launch)
 #endif
+#ifndef TGNX_KV_FUSE
+#define TGNX_KV_FUSE 1  // 1-hop train: (dk, dv) per edge computed and summed in tgn_attn_bwd (no k / v reduction launch)
+#endif
+#ifndef TGNX_KVF_LAYOUT
+// with TGNX_KV_FUSE, where the dE-only GEMMs (dW_edge, dEnc·W_e) ride: 0 = the dz0 launch, 1 = the dW_gru
+// launch (A/B: 0.0987 vs 0.1013 ms with 0, 0.1018 unfused); 2..4 = dW_proj / dW_lp moved there too (0.1013 -
+// 0.1035: slower); 5 = as 1 with dz0 the dz0 launch's first job (0.0985 vs 0.0991)
+#define TGNX_KVF_LAYOUT 5
+#endif
+#ifndef TGNX_L8_ORDER
+#define TGNX_L8_ORDER 3  // job order of the dW_gru launch (block ranges in order: the first dispatch first);
+                         // 3 (GEMMs before the snapshot / store blocks): 0.0970 vs 0.0986 ms with 0
+#endif
 #ifndef TGNX_PIPE_MARK_AT
 #define TGNX_PIPE_MARK_AT 7
 #endif
@@ -3519,7 +3670,7 @@ static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_spl
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, TGNX_S_WG)); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
-      Ep, alpha, Zc, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
+      Ep, alpha, alk, Qo, Zc, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
       snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF,
       uX, uZ, uG, ulu, uxw, utrel, total;
   int tgp_rows, tgp_e1;
@@ -3561,6 +3712,8 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.P = carve(off, (size_t)k.Mcap * 4 * HC * 4);
   W.Ep = carve(off, (size_t)k.Ecap * HC * 4);
   W.alpha = carve(off, (size_t)k.Etr * TH * 4);
+  W.alk = carve(off, (size_t)k.Etr * TH * 4);
+  W.Qo = carve(off, (size_t)k.Rtr * 2 * HC * 4);
   W.Zc = carve(off, (size_t)k.Rcap * HC * 4);
   W.evs = carve(off, (size_t)k.B * evs_stride(D) * 4);
   W.evr = carve(off, (size_t)k.B * 3 * 4);
@@ -3743,6 +3896,8 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.P = reinterpret_cast<float*>(ws + W.P);
   c.Ep = reinterpret_cast<float*>(ws + W.Ep);
   c.alpha = reinterpret_cast<float*>(ws + W.alpha);
+  c.alk = reinterpret_cast<float*>(ws + W.alk);
+  c.Qo = reinterpret_cast<float*>(ws + W.Qo);
   c.Zc = reinterpret_cast<float*>(ws + W.Zc);
   c.evs = reinterpret_cast<float*>(ws + W.evs);
   c.evr = reinterpret_cast<int*>(ws + W.evr);
@@ -4100,8 +4255,14 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgn_gru_edge");
   const int nmark = gridn(3 * k.B * 16, 256);
+  // 1 hop with the attention forward in the predictor: the attention backward computes each edge's (dk, dv)
+  // where it sums them (kv_edge_body), so the k / v reduction launch is gone and the GEMMs that need only dE
+  // ride in a later launch
+  const bool kvf = !two && TGNX_PRED_ATT && TGNX_KV_FUSE;
+  c.kvf = kvf ? 1 : 0;
+  const int mark_at = kvf && TGNX_PIPE_MARK_AT == 7 ? 8 : TGNX_PIPE_MARK_AT;
   auto mk_at = [&](int at) {
-    return BlockJob<MarkNextJob, 3 * MARK_LDS_WORDS>{MarkNextJob{c, nmark}, pipe && !ppm && at == TGNX_PIPE_MARK_AT ? nmark : 0};
+    return BlockJob<MarkNextJob, 3 * MARK_LDS_WORDS>{MarkNextJob{c, nmark}, pipe && !ppm && at == mark_at ? nmark : 0};
   };
   probe_begin(TGNX_K_PROJ, s);
   gemmN_launch(s, mk_at(3),
@@ -4148,7 +4309,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     // conv2 backward (‖ predictor reductions) -> dP2, dE2; then dh1 = dP2 [Wq2; Wk2; Wv2; Wsk2] ‖ dW_proj2,
     // dW_edge2 (deferred) ‖ conv2's lin_edge -> Δt-encoding partials; then conv backward from dh1
     const int ncb1 = gridn(k.R1tr, 4, 1 << 20);
-    tgn_attn_bwd<<<ncb1 + gridn(3 * D + 2, 4), 256, 0, s>>>(cr, ncb1);
+    tgn_attn_bwd<<<ncb1 + gridn(3 * D + 2, 4), 256, 0, s>>>(cr, ncb1, 0);
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
     // conv2's (dk, dv) sums ‖ its dE2-only GEMMs (as in the 1-hop step below), then dh1 ‖ dW_proj2
     gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{cr}, gridn(k.E1tr, KVR_CH, 1 << 20)},
@@ -4164,10 +4325,11 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                  gemm_job<GW>(shp_dWp2(k, c.cnt), LoadKRow{c.dP2, 4 * HC, k.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
                                EpiDeferred{}, c.pE));
     TGNX_LAUNCH_CHECK("tgn_dh1");
-    tgn_attn_bwd<<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c, gridn(k.Rtr, 4, 1 << 20));
+    tgn_attn_bwd<<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c, gridn(k.Rtr, 4, 1 << 20), 0);
   } else {
     const int ncb = gridn(k.Rtr, 4, 1 << 20);
-    launch_k(tgn_attn_bwd, dim3(ncb + gridn(3 * D + 2, 4)), dim3(256), 0, s, c, ncb);
+    const int nkv = kvf ? gridn(k.Etr, KVE_CH, 1 << 20) : 0;
+    launch_k(tgn_attn_bwd, dim3(ncb + nkv + gridn(3 * D + 2, 4)), dim3(256), 0, s, c, ncb, nkv);
   }
   probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_attn_bwd");
@@ -4177,16 +4339,18 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // idle: the dE-only GEMMs fill them here instead of lengthening the dP launch below.
   const Ctx cf = fixup_view(c);
   const EpiGradStore e_dWe{G, c.L.we, D + d, cf.adf};
-  probe_begin(TGNX_K_KV, s);
   const auto j_kvr = BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(k.Etr, KVR_CH, 1 << 20)};
   const auto j_dwe = gemm_job<GW>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadKRow{c.encE, D + d, k.Etr, D + d},
                                   EpiDeferred{}, c.pA);
   const auto j_denc = gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
                                     LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
                                     (float*)nullptr);
-  gemmN_launch(s, mk_at(7), j_kvr, j_dwe, j_denc);
-  probe_end(TGNX_K_KV, s);
-  TGNX_LAUNCH_CHECK("tgn_kv_reduce_dE");
+  if (!kvf) {
+    probe_begin(TGNX_K_KV, s);
+    gemmN_launch(s, mk_at(7), j_kvr, j_dwe, j_denc);
+    probe_end(TGNX_K_KV, s);
+    TGNX_LAUNCH_CHECK("tgn_kv_reduce_dE");
+  }
   // weight gradients (deferred split-K) ‖ ...
   const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D, cf.adf};
   const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D, cf.adf};
@@ -4195,17 +4359,18 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // epilogue — all read only what attn_bwd / kv_reduce / pred_train produced
   const int rows_edge = (k.Etr + G32::TM - 1) / G32::TM, rows_msg = (k.Mtr + G32::TM - 1) / G32::TM;
   probe_begin(TGNX_K_EDGE_BWD, s);
-  gemmN_launch(s, mk_at(8), gemm_job<GW>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB),
-               gemm_job<GW>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
-                             LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, EpiDeferred{}, c.pC),
-               gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
-                             LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, Cl::bwd(c),
-                             (float*)nullptr));
-  probe_end(TGNX_K_EDGE_BWD, s);
-  TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
+  const auto j_dwp = gemm_job<GW>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB);
+  const auto j_dwlp = gemm_job<GW>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
+                                   LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, EpiDeferred{}, c.pC);
+  const auto j_dz0 = gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
+                                    LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, Cl::bwd(c), (float*)nullptr);
+  auto l7 = [&](auto... jobs) {
+    gemmN_launch(s, mk_at(8), jobs...);
+    probe_end(TGNX_K_EDGE_BWD, s);
+    TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
+  };
   // ‖ the message stores ‖ the fixup's descriptor copy + the counter advance (SnapJob)
   const int nst = gridn(2 * k.B, 256);
-  probe_begin(TGNX_K_WGRAD3, s);
   const auto j_dwg = gemm_job<GW>(shp_dWg(k, c.cnt), LoadKRow{c.dG, Cl::G * D, k.Mtr, Cl::G * D},
                                   LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{}, c.pD);
   const auto j_dxe = gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, Cl::G * D, c.cnt + CNT_M),
@@ -4214,14 +4379,75 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // ppm: the next batch's scan (into set 1 - pp; the counters advance in the fixup launch) as this launch's
   // first workgroups when it fits their LDS, else its own launch after it
   const bool scan_w3 = ppm && scan_rides(c, k, (size_t)3 * MARK_LDS_WORDS * 4);
-  if (scan_w3)
-    gemmN_launch(s, BlockJob<ScanJob, 3 * MARK_LDS_WORDS>{ScanJob{cn}, 1 + 2 * c.pplan}, BlockJob<SnapJob>{SnapJob{c, 1}, 1},
-                 BlockJob<StoreJob>{StoreJob{c, nst}, nst}, j_dwg, j_dxe);
-  else
-    gemmN_launch(s, mk_at(9), BlockJob<SnapJob>{SnapJob{c, ppm ? 1 : 0}, 1}, BlockJob<StoreJob>{StoreJob{c, nst}, nst}, j_dwg,
-                 j_dxe);
-  probe_end(TGNX_K_WGRAD3, s);
-  TGNX_LAUNCH_CHECK("tgn_wgrad3");
+  const auto j_scan = BlockJob<ScanJob, 3 * MARK_LDS_WORDS>{ScanJob{cn}, 1 + 2 * c.pplan};
+  const auto j_snap = BlockJob<SnapJob>{SnapJob{c, ppm ? 1 : 0}, 1};
+  const auto j_store = BlockJob<StoreJob>{StoreJob{c, nst}, nst};
+  auto l8 = [&](auto... jobs) {
+    probe_begin(TGNX_K_WGRAD3, s);
+#if TGNX_L8_ORDER == 1
+    if (scan_w3)
+      gemmN_launch(s, j_scan, j_snap, j_store, j_dxe, j_dwg, jobs...);
+    else
+      gemmN_launch(s, mk_at(9), j_snap, j_store, j_dxe, j_dwg, jobs...);
+#elif TGNX_L8_ORDER == 2
+    if (scan_w3)
+      gemmN_launch(s, j_scan, j_snap, j_store, jobs..., j_dxe, j_dwg);
+    else
+      gemmN_launch(s, mk_at(9), j_snap, j_store, jobs..., j_dxe, j_dwg);
+#elif TGNX_L8_ORDER == 3
+    if (scan_w3)
+      gemmN_launch(s, j_scan, j_dxe, j_dwg, jobs..., j_snap, j_store);
+    else
+      gemmN_launch(s, mk_at(9), j_dxe, j_dwg, jobs..., j_snap, j_store);
+#elif TGNX_L8_ORDER == 4
+    if (scan_w3)
+      gemmN_launch(s, j_scan, j_dxe, jobs..., j_dwg, j_snap, j_store);
+    else
+      gemmN_launch(s, mk_at(9), j_dxe, jobs..., j_dwg, j_snap, j_store);
+#elif TGNX_L8_ORDER == 5
+    if (scan_w3)
+      gemmN_launch(s, j_scan, j_dwg, j_dxe, jobs..., j_snap, j_store);
+    else
+      gemmN_launch(s, mk_at(9), j_dwg, j_dxe, jobs..., j_snap, j_store);
+#elif TGNX_L8_ORDER == 6
+    if (scan_w3)
+      gemmN_launch(s, j_dxe, j_dwg, jobs..., j_scan, j_snap, j_store);
+    else
+      gemmN_launch(s, mk_at(9), j_dxe, j_dwg, jobs..., j_snap, j_store);
+#else
+    if (scan_w3)
+      gemmN_launch(s, j_scan, j_snap, j_store, j_dwg, j_dxe, jobs...);
+    else
+      gemmN_launch(s, mk_at(9), j_snap, j_store, j_dwg, j_dxe, jobs...);
+#endif
+    probe_end(TGNX_K_WGRAD3, s);
+    TGNX_LAUNCH_CHECK("tgn_wgrad3");
+  };
+  // which of the two weight-gradient launches the dE-only GEMMs (and the other deferred ones) ride in
+  if (!kvf) {
+    l7(j_dwp, j_dwlp, j_dz0);
+    l8();
+  } else {
+#if TGNX_KVF_LAYOUT == 0
+    l7(j_dwp, j_dwlp, j_dz0, j_dwe, j_denc);
+    l8();
+#elif TGNX_KVF_LAYOUT == 1
+    l7(j_dwp, j_dwlp, j_dz0);
+    l8(j_dwe, j_denc);
+#elif TGNX_KVF_LAYOUT == 2
+    l7(j_dz0);
+    l8(j_dwe, j_denc, j_dwp, j_dwlp);
+#elif TGNX_KVF_LAYOUT == 3
+    l7(j_dwp, j_dz0);
+    l8(j_dwe, j_denc, j_dwlp);
+#elif TGNX_KVF_LAYOUT == 4
+    l7(j_dwlp, j_dz0);
+    l8(j_dwe, j_denc, j_dwp);
+#else
+    l7(j_dz0, j_dwp, j_dwlp);
+    l8(j_dwe, j_denc);
+#endif
+  }
   if (ppm && !scan_w3) {
     tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(cn, 1, 0);
     TGNX_LAUNCH_CHECK("tgn_scan_early");
