@@ -694,8 +694,8 @@ __global__ void __launch_bounds__(256) gemm2_kernel(GemmShape g1, AL1 a1, BL1 b1
   else gemm_body<C2>(g2, a2, b2, e2, p2, blockIdx.x - n1, smem);
 }
 
-// Any number of independent GEMMs in one launch (block ranges in argument order; every range is a
-// multiple of 8 blocks, so each GEMM keeps its XCD grouping).
+// Any number of independent GEMMs in one launch (block ranges in argument order; every GEMM range is a
+// multiple of 8 blocks, so each GEMM keeps its XCD grouping when only GEMMs precede it).
 template <class CFG, class AL, class BL, class EPI>
 struct GemmJob {
   using Cfg = CFG;
@@ -720,7 +720,12 @@ __device__ __forceinline__ bool gemm_job_dispatch(const J& j, int& bid, float* s
   return false;
 }
 // a non-GEMM piece of work riding in a gemmN launch: nb 256-thread workgroups running f(bid, smem), smem
-// at least SM floats of LDS
+// at least SM floats of LDS.  Its block range is padded to a multiple of the 8 XCDs (the pad blocks exit), so
+// the GEMM ranges after it keep their XCD grouping (TGNX_BLOCKJOB_PAD 0: unpadded)
+#ifndef TGNX_BLOCKJOB_PAD
+#define TGNX_BLOCKJOB_PAD 0  // (A/B: 0.0965 vs 0.0962 ms unpadded; the step's launches are not fabric-bound)
+#endif
+__host__ __device__ constexpr int blockjob_span(int nb) { return TGNX_BLOCKJOB_PAD ? (nb + 7) & ~7 : nb; }
 template <class F, int SM = 4>
 struct BlockJob {
   struct Cfg {
@@ -731,17 +736,18 @@ struct BlockJob {
 };
 template <class F, int SM>
 __device__ __forceinline__ bool gemm_job_dispatch(const BlockJob<F, SM>& j, int& bid, float* smem) {
-  if (bid < j.nb) {
-    j.f(bid, smem);
+  const int span = blockjob_span(j.nb);
+  if (bid < span) {
+    if (bid < j.nb) j.f(bid, smem);
     return true;
   }
-  bid -= j.nb;
+  bid -= span;
   return false;
 }
 template <class J>
 inline int job_blocks(const J& j) { return gemm_blocks(j.g); }
 template <class F, int SM>
-inline int job_blocks(const BlockJob<F, SM>& j) { return j.nb; }
+inline int job_blocks(const BlockJob<F, SM>& j) { return blockjob_span(j.nb); }
 template <class... J>
 #ifndef TGNX_GEMMN_WAVES
 #define TGNX_GEMMN_WAVES 0  // amdgpu_waves_per_eu floor for gemmN launches (0 = compiler's choice; 5 measured +5 %)

@@ -42,6 +42,7 @@ constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touc
 enum { CNT_R = 0, CNT_M = 1, CNT_E = 2, CNT_U = 3, CNT_LIST = 6, CNT_NB = 9, CNT_WORDS = 16 };  // (4, 5: unused)
 // ctl[ERR] bit of a step that found its scan-output set holding another batch (tgnx_tgn_train_step_pp)
 constexpr int64_t ERR_STALE_SET = 16;
+constexpr int64_t ERR_SORT_CAP = 32;  // edge_sort_body: more sampled rows than its LDS counters (host-checked; never expected)
 
 __host__ __device__ inline int64_t al4(int64_t x) { return (x + 3) & ~int64_t(3); }
 
@@ -203,6 +204,7 @@ struct Ctx {
   // forward also writes alk = alpha * keep per edge [E][2] and Qo = [q | Σ alpha~ v] per centre [R][2 HC]
   float *alk, *Qo;
   int kvf = 0;
+  int *kj, *kx, *ke;  // kvf: the sampled edges sorted by neighbour row (tgn_pred_train's sort block): row, centre, edge
   float *encE, *sinE;  // per sampled edge: cos / sin of the Δt encoding argument [E][D]
   float *s0m, *s1m;    // per GRU row: (mean over its messages of) sin(arg), sin(arg) Δt  [M][D]
   float *pA, *pB, *pC, *pD;  // split-K partials of the deferred weight-gradient GEMMs
@@ -2120,8 +2122,53 @@ constexpr int PRED_SU = 16;  // float4 per staging thread per matrix per round (
 // embedding rows straight into LDS, while wave 0 stages the weights: no tgn_attn_fwd launch, and the
 // attention chain overlaps the weight staging.  A centre shared by several roots is computed by each of
 // them, identically (its alpha stores write equal values).
+// kvf: the sampled edges sorted by neighbour row (counting sort in LDS, one workgroup riding in the predictor
+// launch, off the step's critical path), so that the attention backward's edge blocks see long runs of equal
+// neighbours and sum each run before one atomic (order within a row: LDS-atomic order).  Rows past the LDS
+// (cap counters) cannot occur: the host takes this path only when every row fits (else ERR_SORT_CAP).
+__device__ void edge_sort_body(const Ctx& c, int* cntr, int cap) {
+  __shared__ int wsum[256];
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int E = c.ceoff[c.cnt[c.rsel]], M = c.cnt[CNT_M];
+  const int t = threadIdx.x;
+  if (M + 1 > cap) {  // (the host enables the sort for Mtr + 1 <= cap only)
+    if (t == 0) c.ctl[TGNX_CTL_ERR] |= ERR_SORT_CAP;
+    return;
+  }
+  for (int m = t; m < M; m += 256) cntr[m] = 0;
+  __syncthreads();
+  for (int e = t; e < E; e += 256) atomicAdd(&cntr[c.e_j[e]], 1);
+  __syncthreads();
+  const int per = (M + 255) / 256, m0 = min(t * per, M), m1 = min(m0 + per, M);
+  int sum = 0;
+  for (int m = m0; m < m1; ++m) sum += cntr[m];
+  wsum[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // inclusive scan of the per-thread sums
+    const int v = t >= o ? wsum[t - o] : 0;
+    __syncthreads();
+    wsum[t] += v;
+    __syncthreads();
+  }
+  int run = wsum[t] - sum;
+  for (int m = m0; m < m1; ++m) {
+    const int n = cntr[m];
+    cntr[m] = run;
+    run += n;
+  }
+  __syncthreads();
+  for (int e = t; e < E; e += 256) {
+    const int j = c.e_j[e], x = c.e_c[e];
+    const int pos = atomicAdd(&cntr[j], 1);
+    c.kj[pos] = j;
+    c.kx[pos] = x;
+    c.ke[pos] = e;
+  }
+}
+
 template <bool ATT>
-__global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
+__global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt) {
   TGNX_STAMP(5);
   extern __shared__ __attribute__((aligned(16))) float Wl[];  // [2][D][DP]: lin_src, lin_dst
   __shared__ __attribute__((aligned(16))) float z[3][TDMAX];
@@ -2131,6 +2178,10 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk) {
   __shared__ int scr[3];
   if ((int)blockIdx.x >= (int)gridDim.x - nmk) {  // (the dynamic LDS holds >= 3 x MARK_LDS_WORDS words)
     mark_body<true>(c, (int)blockIdx.x - ((int)gridDim.x - nmk), nmk, 1, reinterpret_cast<uint32_t*>(Wl));
+    return;
+  }
+  if ((int)blockIdx.x >= (int)gridDim.x - nmk - nsrt) {
+    edge_sort_body(c, reinterpret_cast<int*>(Wl), (int)(tgn_pred_smem(c.D) / 4));
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2410,6 +2461,16 @@ __device__ void lp_vec_body(const Ctx& c, int y, int lane) {
 #define TGNX_KVE_CH 32
 #endif
 constexpr int KVE_CH = TGNX_KVE_CH, KVE_PW = KVE_CH / 4;
+#ifndef TGNX_KVE_GSORT
+#define TGNX_KVE_GSORT 1  // edges globally sorted by neighbour (edge_sort_body in the predictor launch)
+#endif
+#ifndef TGNX_KVE_MERGE
+#define TGNX_KVE_MERGE 1  // runs crossing the workgroup's waves merged in LDS before their atomics
+#endif
+#ifndef TGNX_KVE_B
+#define TGNX_KVE_B 8
+#endif
+constexpr int KVE_B = TGNX_KVE_B < KVE_PW ? TGNX_KVE_B : KVE_PW;  // edges per load batch of a wave
 __device__ void kv_edge_body(const Ctx& c, int bid) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
@@ -2417,9 +2478,25 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
   const int eb = bid * KVE_CH;
   if (eb >= E) return;  // whole workgroup
   const int ne = min(KVE_CH, E - eb);
-  __shared__ int sj[KVE_CH], sorder[KVE_CH];
+  __shared__ int sj[KVE_CH], sx[KVE_CH], se[KVE_CH], sorder[KVE_CH], sb[2];
   const int t = threadIdx.x;
-  if (t < KVE_CH) sj[t] = t < ne ? c.e_j[eb + t] : INT_MAX;
+#if TGNX_KVE_GSORT
+  // globally sorted: a run whose row has no edge in the neighbouring chunks is the row's whole sum (a plain
+  // store); the chunk's first / last runs may continue there (the keys just outside the chunk tell)
+  if (t == KVE_CH) sb[0] = eb > 0 ? c.kj[eb - 1] : -1;
+  if (t == KVE_CH + 1) sb[1] = eb + ne < E ? c.kj[eb + ne] : -1;
+#endif
+  if (t < KVE_CH) {  // the edge's neighbour (sort key), centre and id, one round
+    const int ec = min(eb + t, E - 1);
+#if TGNX_KVE_GSORT
+    const int j = c.kj[ec], x = c.kx[ec], eo = c.ke[ec];
+#else
+    const int j = c.e_j[ec], x = c.e_c[ec], eo = ec;
+#endif
+    sj[t] = t < ne ? j : INT_MAX;
+    sx[t] = x;
+    se[t] = eo;
+  }
   __syncthreads();
   if (t < ne) {  // stable rank of (neighbour, edge)
     const int key = sj[t];
@@ -2434,49 +2511,33 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
   __syncthreads();
   const int w = t >> 6, lane = t & 63;
   const int i0 = w * KVE_PW;
+#if TGNX_KVE_MERGE
+  // a wave's first and last runs may continue in the neighbouring waves: they go to LDS pieces (slots 2w, 2w + 1,
+  // key -1 = none), merged in wave order by wave 0 before their atomics
+  __shared__ float ps[8][4][64];
+  __shared__ int pk[8];
+  if (i0 >= ne) {
+    if (lane == 0) pk[2 * w] = pk[2 * w + 1] = -1;
+  }
+  const int n = max(0, min(KVE_PW, ne - i0));
+#else
   if (i0 >= ne) return;
   const int n = min(KVE_PW, ne - i0);
+#endif
   const int C = c.C, HC = c.HC;
   const bool okl = lane < C;
   const float on = f01(okl);
   const int l0 = min(lane, C - 1);
   const float isq = 1.0f / sqrtf((float)C);
-  int jj[KVE_PW], er[KVE_PW], xx[KVE_PW];
-  float a0[KVE_PW], a1[KVE_PW], t0[KVE_PW], t1[KVE_PW];
-#pragma unroll
-  for (int u = 0; u < KVE_PW; ++u) {
-    const int e = sorder[i0 + min(u, n - 1)];
-    jj[u] = sj[e];
-    er[u] = eb + e;
-  }
-#pragma unroll
-  for (int u = 0; u < KVE_PW; ++u) {  // first round: the edges' centres and softmax weights
-    xx[u] = c.e_c[er[u]];
-    a0[u] = c.alpha[(int64_t)er[u] * 2];
-    a1[u] = c.alpha[(int64_t)er[u] * 2 + 1];
-    t0[u] = c.alk[(int64_t)er[u] * 2];
-    t1[u] = c.alk[(int64_t)er[u] * 2 + 1];
-  }
-  float g0[KVE_PW], g1[KVE_PW], q0[KVE_PW], q1[KVE_PW], o0[KVE_PW], o1[KVE_PW], v0[KVE_PW], v1[KVE_PW];
-#pragma unroll
-  for (int u = 0; u < KVE_PW; ++u) {  // second round: centre rows (g, q, o), the neighbour's v row + edge row
-    const float* G = c.dZc + (int64_t)xx[u] * HC;
-    const float* Q = c.Qo + (int64_t)xx[u] * 2 * HC;
-    const float* Pj = c.P + (int64_t)jj[u] * 4 * HC + 2 * HC;
-    const float* Ee = c.Ep + (int64_t)er[u] * HC;
-    g0[u] = G[l0];
-    g1[u] = G[C + l0];
-    q0[u] = Q[l0];
-    q1[u] = Q[C + l0];
-    o0[u] = Q[HC + l0];
-    o1[u] = Q[HC + C + l0];
-    v0[u] = Pj[l0] + Ee[l0];
-    v1[u] = Pj[C + l0] + Ee[C + l0];
-  }
   float s[4] = {0.f, 0.f, 0.f, 0.f};  // run sums: dk (head 0, 1), dv (head 0, 1)
-  int jc = jj[0];
+  int jc = n > 0 ? sj[sorder[i0]] : -1;
+  bool first = true;  // the open run is the wave's first
   auto flush = [&]() {
+#ifdef TGNX_KVE_NOATOM  // (timing probe only: wrong dP)
+    if (okl && s[0] == 12345.f) {
+#else
     if (okl) {
+#endif
       float* dst = c.dP + (int64_t)jc * 4 * HC + HC;
       atomicAdd(dst + lane, s[0]);
       atomicAdd(dst + C + lane, s[1]);
@@ -2484,30 +2545,117 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
       atomicAdd(dst + HC + C + lane, s[3]);
     }
   };
-#pragma unroll
-  for (int u = 0; u < KVE_PW; ++u) {
-    if (u >= n) break;
-    if (jj[u] != jc) {  // wave-uniform run boundary
-      flush();
-      s[0] = s[1] = s[2] = s[3] = 0.f;
-      jc = jj[u];
-    }
-    const float gv0 = wave_sum_f(g0[u] * v0[u] * on), gv1 = wave_sum_f(g1[u] * v1[u] * on);
-    const float go0 = wave_sum_f(g0[u] * o0[u] * on), go1 = wave_sum_f(g1[u] * o1[u] * on);
-    const float ds0 = (t0[u] * gv0 - a0[u] * go0) * isq, ds1 = (t1[u] * gv1 - a1[u] * go1) * isq;
-    const float dk0 = ds0 * q0[u], dk1 = ds1 * q1[u];
-    const float dv0 = t0[u] * g0[u], dv1 = t1[u] * g1[u];
+  auto store = [&]() {  // the row's complete (dk, dv) sums (globally sorted edges)
     if (okl) {
-      float* dEe = c.dE + (int64_t)er[u] * HC;
-      dEe[lane] = dk0 + dv0;
-      dEe[C + lane] = dk1 + dv1;
+      float* dst = c.dP + (int64_t)jc * 4 * HC + HC;
+      dst[lane] = s[0];
+      dst[C + lane] = s[1];
+      dst[HC + lane] = s[2];
+      dst[HC + C + lane] = s[3];
     }
-    s[0] += dk0;
-    s[1] += dk1;
-    s[2] += dv0;
-    s[3] += dv1;
+  };
+  // the wave's sorted edges in batches of KVE_B (all of a batch's loads in flight), runs continuing across
+  for (int b0 = 0; b0 < n; b0 += KVE_B) {
+    const int nb = min(KVE_B, n - b0);
+    int jj[KVE_B], er[KVE_B], xx[KVE_B];
+#pragma unroll
+    for (int u = 0; u < KVE_B; ++u) {
+      const int e = sorder[i0 + b0 + min(u, nb - 1)];
+      jj[u] = sj[e];
+      xx[u] = sx[e];
+      er[u] = se[e];
+    }
+    float a0[KVE_B], a1[KVE_B], t0[KVE_B], t1[KVE_B];
+    float g0[KVE_B], g1[KVE_B], q0[KVE_B], q1[KVE_B], o0[KVE_B], o1[KVE_B], v0[KVE_B], v1[KVE_B];
+#pragma unroll
+    for (int u = 0; u < KVE_B; ++u) {  // softmax weights, centre rows (g, q, o), the neighbour's v row + edge row
+      a0[u] = c.alpha[(int64_t)er[u] * 2];
+      a1[u] = c.alpha[(int64_t)er[u] * 2 + 1];
+      t0[u] = c.alk[(int64_t)er[u] * 2];
+      t1[u] = c.alk[(int64_t)er[u] * 2 + 1];
+      const float* G = c.dZc + (int64_t)xx[u] * HC;
+      const float* Q = c.Qo + (int64_t)xx[u] * 2 * HC;
+      const float* Pj = c.P + (int64_t)jj[u] * 4 * HC + 2 * HC;
+      const float* Ee = c.Ep + (int64_t)er[u] * HC;
+      g0[u] = G[l0];
+      g1[u] = G[C + l0];
+      q0[u] = Q[l0];
+      q1[u] = Q[C + l0];
+      o0[u] = Q[HC + l0];
+      o1[u] = Q[HC + C + l0];
+      v0[u] = Pj[l0] + Ee[l0];
+      v1[u] = Pj[C + l0] + Ee[C + l0];
+    }
+#pragma unroll
+    for (int u = 0; u < KVE_B; ++u) {
+      if (u >= nb) break;
+      if (jj[u] != jc) {  // wave-uniform run boundary
+#if TGNX_KVE_MERGE
+        if (first) {
+          for (int q = 0; q < 4; ++q) ps[2 * w][q][lane] = s[q];
+          if (lane == 0) pk[2 * w] = jc;
+          first = false;
+        } else {
+          if (TGNX_KVE_GSORT) store();
+          else flush();
+        }
+#else
+        flush();
+#endif
+        s[0] = s[1] = s[2] = s[3] = 0.f;
+        jc = jj[u];
+      }
+      const float gv0 = wave_sum_f(g0[u] * v0[u] * on), gv1 = wave_sum_f(g1[u] * v1[u] * on);
+      const float go0 = wave_sum_f(g0[u] * o0[u] * on), go1 = wave_sum_f(g1[u] * o1[u] * on);
+      const float ds0 = (t0[u] * gv0 - a0[u] * go0) * isq, ds1 = (t1[u] * gv1 - a1[u] * go1) * isq;
+      const float dk0 = ds0 * q0[u], dk1 = ds1 * q1[u];
+      const float dv0 = t0[u] * g0[u], dv1 = t1[u] * g1[u];
+      if (okl) {
+        float* dEe = c.dE + (int64_t)er[u] * HC;
+        dEe[lane] = dk0 + dv0;
+        dEe[C + lane] = dk1 + dv1;
+      }
+      s[0] += dk0;
+      s[1] += dk1;
+      s[2] += dv0;
+      s[3] += dv1;
+    }
   }
+#if TGNX_KVE_MERGE
+  if (n > 0) {  // the open run: the wave's only (slot 2w) or its last (slot 2w + 1)
+    const int sl = first ? 2 * w : 2 * w + 1;
+    for (int q = 0; q < 4; ++q) ps[sl][q][lane] = s[q];
+    if (lane == 0) {
+      pk[sl] = jc;
+      if (first) pk[2 * w + 1] = -1;
+    }
+  }
+  __syncthreads();
+  if (w != 0) return;
+  jc = -1;
+  bool firstg = true;  // the open group holds the chunk's first edge
+  const int kprev = TGNX_KVE_GSORT ? sb[0] : -2, knext = TGNX_KVE_GSORT ? sb[1] : -2;
+  for (int sl = 0; sl < 8; ++sl) {
+    const int key = pk[sl];
+    if (key < 0) continue;
+    if (key != jc) {
+      if (jc >= 0) {
+        if (TGNX_KVE_GSORT && !(firstg && jc == kprev)) store();
+        else flush();
+        firstg = false;
+      }
+      jc = key;
+      s[0] = s[1] = s[2] = s[3] = 0.f;
+    }
+    for (int q = 0; q < 4; ++q) s[q] += ps[sl][q][lane];
+  }
+  if (jc >= 0) {
+    if (TGNX_KVE_GSORT && !(firstg && jc == kprev) && jc != knext) store();
+    else flush();
+  }
+#else
   flush();
+#endif
 }
 
 // Backward of tgn_attn_fwd (wave per centre) ‖ [nkv > 0: kv_edge_body blocks; the centre waves then write
@@ -3669,7 +3817,7 @@ static GemmShape shp_dWe2(const Caps& k, const int* cnt) { return gemm_shape_spl
 static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, std::max(TGNX_S_LP, std::min(64, (3 * k.B + 63) / 64))); }
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, TGNX_S_WG)); }
 struct WsLay {
-  size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
+  size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, kj, kx, ke, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
       Ep, alpha, alk, Qo, Zc, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
       snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF,
       uX, uZ, uG, ulu, uxw, utrel, total;
@@ -3701,6 +3849,9 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.upd = carve(off, (size_t)k.Ucap * 8);
   W.e_j = carve(off, (size_t)k.Ecap * 4);
   W.e_c = carve(off, (size_t)k.Ecap * 4);
+  W.kj = carve(off, (size_t)k.Etr * 4);
+  W.kx = carve(off, (size_t)k.Etr * 4);
+  W.ke = carve(off, (size_t)k.Etr * 4);
   W.e_id = carve(off, (size_t)k.Ecap * 8);
   W.e_t = carve(off, (size_t)k.Ecap * 4);
   W.X = carve(off, (size_t)k.Mcap * k.Qm * 4);
@@ -3885,6 +4036,9 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.upd = reinterpret_cast<int64_t*>(ws + W.upd);
   c.e_j = reinterpret_cast<int*>(ws + W.e_j);
   c.e_c = reinterpret_cast<int*>(ws + W.e_c);
+  c.kj = reinterpret_cast<int*>(ws + W.kj);
+  c.kx = reinterpret_cast<int*>(ws + W.kx);
+  c.ke = reinterpret_cast<int*>(ws + W.ke);
   c.e_id = reinterpret_cast<int64_t*>(ws + W.e_id);
   c.e_t = reinterpret_cast<float*>(ws + W.e_t);
   c.X = reinterpret_cast<float*>(ws + W.X);
@@ -4258,7 +4412,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // 1 hop with the attention forward in the predictor: the attention backward computes each edge's (dk, dv)
   // where it sums them (kv_edge_body), so the k / v reduction launch is gone and the GEMMs that need only dE
   // ride in a later launch
-  const bool kvf = !two && TGNX_PRED_ATT && TGNX_KV_FUSE;
+  const bool kvf = !two && TGNX_PRED_ATT && TGNX_KV_FUSE && (!TGNX_KVE_GSORT || (size_t)k.Mtr + 1 <= tgn_pred_smem(c.D) / 4);
   c.kvf = kvf ? 1 : 0;
   const int mark_at = kvf && TGNX_PIPE_MARK_AT == 7 ? 8 : TGNX_PIPE_MARK_AT;
   auto mk_at = [&](int at) {
@@ -4290,10 +4444,11 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   TGNX_CHECK_ARG(pred_smem_ok(c.D), "tgn_pred_train: dynamic LDS attribute refused");
   const int nmk = (ppm || (pipe && TGNX_PIPE_MARK_AT == 5)) ? nmark : 0;
   const size_t psm = std::max(tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0);
+  const int nsrt = kvf && TGNX_KVE_GSORT ? 1 : 0;  // (kvf implies the rows fit the sort's LDS counters)
   if (att_in_pred)
-    launch_k(tgn_pred_train<true>, dim3(k.B + nmk), dim3(256), (uint32_t)psm, s, cr, nmk);
+    launch_k(tgn_pred_train<true>, dim3(k.B + nsrt + nmk), dim3(256), (uint32_t)psm, s, cr, nmk, nsrt);
   else
-    launch_k(tgn_pred_train<false>, dim3(k.B + nmk), dim3(256), (uint32_t)psm, s, cr, nmk);
+    launch_k(tgn_pred_train<false>, dim3(k.B + nsrt + nmk), dim3(256), (uint32_t)psm, s, cr, nmk, nsrt);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
   if (c.emb) {
