@@ -2533,11 +2533,7 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
   int jc = n > 0 ? sj[sorder[i0]] : -1;
   bool first = true;  // the open run is the wave's first
   auto flush = [&]() {
-#ifdef TGNX_KVE_NOATOM  // (timing probe only: wrong dP)
-    if (okl && s[0] == 12345.f) {
-#else
     if (okl) {
-#endif
       float* dst = c.dP + (int64_t)jc * 4 * HC + HC;
       atomicAdd(dst + lane, s[0]);
       atomicAdd(dst + C + lane, s[1]);
