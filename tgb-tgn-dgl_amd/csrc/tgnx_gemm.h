@@ -97,11 +97,15 @@ using G32L = GemmCfg<TGNX_G32L_T, TGNX_G32L_T, TGNX_G32L_KC, TGNX_G32L_PF, TGNX_
 using GW = GemmCfg<TGNX_GW_T, TGNX_GW_T, TGNX_GW_KC, 1, TGNX_GW_WS>;
 using G64 = GemmCfg<64, 64, 64>;   // large-M GEMMs (eval scoring)
 
+#ifndef TGNX_GEMM_GRID_CAP
+#define TGNX_GEMM_GRID_CAP 1024
+#endif
 struct GemmShape {
   int M, N, K, S, tiles_m, tiles_n;  // capacities: the grid is sized from these
   int tm, tn, kc;                    // the GemmCfg it was shaped for
   int deferred;                      // 1: write partials for gemm_fixup_kernel
   const int *Mdev, *Ndev, *Kdev;     // optional runtime sizes on the device (<= capacities)
+  int cap;                           // grid cap (a multiple of 8; gemm_blocks)
 };
 // direct GEMM: S = 1, the workgroup loops over all of K
 template <class CFG>
@@ -115,6 +119,12 @@ inline GemmShape gemm_shape(int M, int N, int K, const int* Mdev = nullptr, cons
   g.deferred = 0;
   g.tiles_m = (M + CFG::TM - 1) / CFG::TM;
   g.tiles_n = (N + CFG::TN - 1) / CFG::TN;
+  g.cap = TGNX_GEMM_GRID_CAP;
+  return g;
+}
+// the same GEMM with a smaller grid cap (its workgroups loop over the runtime tiles past it)
+inline GemmShape with_cap(GemmShape g, int cap) {
+  g.cap = (cap + 7) & ~7;
   return g;
 }
 // deferred split-K GEMM: S <= smax splits, split s handles k-chunks s, s + S, ...
@@ -133,12 +143,9 @@ inline GemmShape gemm_shape_split(int M, int N, int K, const int* Mdev, const in
 // runtime work in strides of the grid instead (gemm_body).
 // (idle workgroups past the runtime tiles hold dispatch slots: 2048 -> 1024 shortened the step ~7 us on
 // the wiki shape, stamps timeline; 512 lengthened the dW_gru launch, whose ~940 split blocks are all busy)
-#ifndef TGNX_GEMM_GRID_CAP
-#define TGNX_GEMM_GRID_CAP 1024
-#endif
 __host__ __device__ inline int gemm_blocks(const GemmShape& g) {
   const int full = (g.tiles_m * g.tiles_n * g.S + 7) & ~7;
-  return full < TGNX_GEMM_GRID_CAP ? full : TGNX_GEMM_GRID_CAP;
+  return full < g.cap ? full : g.cap;
 }
 inline size_t gemm_partial_floats(const GemmShape& g) {
   return g.deferred ? (size_t)g.tiles_m * g.tiles_n * g.S * g.tm * g.tn : 0;

@@ -3564,6 +3564,9 @@ struct MarkNextJob {
 // 0.1035: slower); 5 = as 1 with dz0 the dz0 launch's first job (0.0985 vs 0.0991)
 #define TGNX_KVF_LAYOUT 5
 #endif
+#ifndef TGNX_MD_CAP
+#define TGNX_MD_CAP 512  // grid cap of the step's M x D GEMMs (dz0, dX_enc): 7 column tiles at D = 100, ~30 row tiles at B = 200 (A/B 0.0966 vs 0.0971 ms with 1024)
+#endif
 #ifndef TGNX_L8_ORDER
 #define TGNX_L8_ORDER 3  // job order of the dW_gru launch (block ranges in order: the first dispatch first);
                          // 3 (GEMMs before the snapshot / store blocks): 0.0970 vs 0.0986 ms with 0
@@ -4513,7 +4516,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const auto j_dwp = gemm_job<GW>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB);
   const auto j_dwlp = gemm_job<GW>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
                                    LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, EpiDeferred{}, c.pC);
-  const auto j_dz0 = gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
+  const auto j_dz0 = gemm_job<G32L>(with_cap(gemm_shape<G32L>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), TGNX_MD_CAP), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
                                     LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, Cl::bwd(c), (float*)nullptr);
   auto l7 = [&](auto... jobs) {
     gemmN_launch(s, mk_at(8), jobs...);
@@ -4524,7 +4527,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const int nst = gridn(2 * k.B, 256);
   const auto j_dwg = gemm_job<GW>(shp_dWg(k, c.cnt), LoadKRow{c.dG, Cl::G * D, k.Mtr, Cl::G * D},
                                   LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{}, c.pD);
-  const auto j_dxe = gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, D, Cl::G * D, c.cnt + CNT_M),
+  const auto j_dxe = gemm_job<G32L>(with_cap(gemm_shape<G32L>(k.Mtr, D, Cl::G * D, c.cnt + CNT_M), TGNX_MD_CAP),
                                     LoadRowK{c.dG, k.Mtr, Cl::G * D, Cl::G * D}, Cl::wenc(c),
                                     EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, (float*)nullptr);
   // ppm: the next batch's scan (into set 1 - pp; the counters advance in the fixup launch) as this launch's
