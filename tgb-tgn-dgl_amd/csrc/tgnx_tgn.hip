@@ -3564,6 +3564,9 @@ struct MarkNextJob {
 // 0.1035: slower); 5 = as 1 with dz0 the dz0 launch's first job (0.0985 vs 0.0991)
 #define TGNX_KVF_LAYOUT 5
 #endif
+#ifndef TGNX_KVF_MARK_AT
+#define TGNX_KVF_MARK_AT 5  // with TGNX_KV_FUSE: the launch of a non-parity pipelined step's next-batch marking (5 or 8)
+#endif
 #ifndef TGNX_MD_CAP
 #define TGNX_MD_CAP 512  // grid cap of the step's M x D GEMMs (dz0, dX_enc): 7 column tiles at D = 100, ~30 row tiles at B = 200 (A/B 0.0966 vs 0.0971 ms with 1024)
 #endif
@@ -4413,7 +4416,9 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // ride in a later launch
   const bool kvf = !two && TGNX_PRED_ATT && TGNX_KV_FUSE && (!TGNX_KVE_GSORT || (size_t)k.Mtr + 1 <= tgn_pred_smem(c.D) / 4);
   c.kvf = kvf ? 1 : 0;
-  const int mark_at = kvf && TGNX_PIPE_MARK_AT == 7 ? 8 : TGNX_PIPE_MARK_AT;
+  // (kvf: no k / v launch; the next batch's marking of a non-parity pipelined step rides in the predictor launch
+  // beside its sort block, as the parity step's does)
+  const int mark_at = kvf ? TGNX_KVF_MARK_AT : TGNX_PIPE_MARK_AT;
   auto mk_at = [&](int at) {
     return BlockJob<MarkNextJob, 3 * MARK_LDS_WORDS>{MarkNextJob{c, nmark}, pipe && !ppm && at == mark_at ? nmark : 0};
   };
@@ -4441,7 +4446,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   }
   probe_begin(TGNX_K_PRED, s);
   TGNX_CHECK_ARG(pred_smem_ok(c.D), "tgn_pred_train: dynamic LDS attribute refused");
-  const int nmk = (ppm || (pipe && TGNX_PIPE_MARK_AT == 5)) ? nmark : 0;
+  const int nmk = (ppm || (pipe && mark_at == 5)) ? nmark : 0;
   const size_t psm = std::max(tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0);
   const int nsrt = kvf && TGNX_KVE_GSORT ? 1 : 0;  // (kvf implies the rows fit the sort's LDS counters)
   if (att_in_pred)
