@@ -23,6 +23,28 @@
 namespace tgnx {
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+// Write-through (sc1) stores for what a launch hands to the next one: a kernel boundary writes back the dirty
+// L2 lines its predecessor left (MI355X_MICROARCH.md price list: + B / 6 TB/s), write-through stores leave none.
+// (Vector stores: a relaxed agent-scope atomic store is global_store_dword sc1; 16 B: a buffer store, aux 16.)
+#ifndef TGNX_WT
+#define TGNX_WT 0  // (split-K partials + fused-Adam stores write-through: 0.0969 vs 0.0967 ms plain, same box)
+#endif
+__device__ __forceinline__ void st_wt(float* p, float v) {
+#if TGNX_WT
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
+// 16 B at byte offset off (per lane) of the wave-uniform base, whose extent is bytes
+__device__ __forceinline__ void st_wt4(float* base, int off, int bytes, f32x4_t v) {
+#if TGNX_WT
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r, off, 0, 16);
+#else
+  *reinterpret_cast<f32x4_t*>(reinterpret_cast<char*>(base) + off) = v;
+#endif
+}
 
 template <int TM_, int TN_, int KC_, int PF_ = 1, bool WS_ = false, int DR_ = 0>
 struct GemmCfg {
@@ -406,7 +428,7 @@ __device__ __forceinline__ void gemm_tile_direct(const GemmShape& g, const GemmR
   {
     const int x = tid, o = (x / TN) * PB + x % TN;  // TM * TN == 256: one element per thread
     const float v = ((red[o] + red[TM * PB + o]) + red[2 * TM * PB + o]) + red[3 * TM * PB + o];
-    if (g.deferred) part[((size_t)tile * g.S + s) * TM * TN + x] = v;
+    if (g.deferred) st_wt(part + ((size_t)tile * g.S + s) * TM * TN + x, v);
     else Ct[o] = v;
   }
   if (g.deferred) return;
@@ -633,7 +655,7 @@ __device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, 
     for (int e = 0; e < PER; ++e) {
       const int x = tid + 256 * e, o = (x / TN) * PB + x % TN;
       const float v = ((red[o] + red[TM * PB + o]) + red[2 * TM * PB + o]) + red[3 * TM * PB + o];
-      if (g.deferred) part[((size_t)tile * g.S + s) * TM * TN + x] = v;  // row-major partial tile
+      if (g.deferred) st_wt(part + ((size_t)tile * g.S + s) * TM * TN + x, v);  // row-major partial tile
       else Ct[o] = v;
     }
     if (g.deferred) return;
@@ -642,11 +664,11 @@ __device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, 
     return;
   }
   if (g.deferred) {  // partial tile in register layout, summed by gemm_fixup_kernel
-    f32x4_t* mine = reinterpret_cast<f32x4_t*>(part + ((size_t)tile * g.S + s) * TM * TN);
+    float* mine = part + ((size_t)tile * g.S + s) * TM * TN;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) mine[((wv * FM + i) * FN + j) * 64 + lane] = acc[i][j];
+      for (int j = 0; j < FN; ++j) st_wt4(mine, (((wv * FM + i) * FN + j) * 64 + lane) * 16, TM * TN * 4, acc[i][j]);
     return;
   }
   float* Ct = smem;  // [TM][PB]

@@ -136,10 +136,10 @@ struct AdamFuse {
     for (int i = 0; i < N; ++i) {
       if (idx[i] < 0) continue;
       adam1(val[i], mm[i], vv[i], pp[i], b1, b2, eps, s0, s1);
-      g[idx[i]] = val[i];
-      m[idx[i]] = mm[i];
-      v[idx[i]] = vv[i];
-      p[idx[i]] = pp[i];
+      st_wt(g + idx[i], val[i]);
+      st_wt(m + idx[i], mm[i]);
+      st_wt(v + idx[i], vv[i]);
+      st_wt(p + idx[i], pp[i]);
     }
   }
   __device__ __forceinline__ void put(float* g, int64_t i, float val) const {
