@@ -2,24 +2,26 @@
 // wired as pyg_model_utils.py:10-36, trained by the canonical loop pyg_epoch_utils.py:106-137 carries
 // commented out.  Reference semantics restated in oracle/tgn_ref.py (the checker).
 //
-// One pipelined train step at world 1 (tgnx_tgn_train_step_pipelined, the bench's step): 9 launches, no
-// host sync, graph-replayed.  The previous step already marked and scanned this batch.
-//   1 tgn_agg_emit   sampled edges (neighbor_loader.py:26-50 order) + Δt cos/sin ‖ per sampled node its
-//                    stored messages -> IdentityMessage -> Last/Mean aggregate (memory_module.py:152-207)
-//                    ‖ per-root / per-centre records for the predictor's attention
+// One train step at world 1 (tgnx_tgn_train_step_pp, the bench's step): 8 launches, no host sync, graph-replayed
+// (one graph per scan-output parity).  The previous step already marked and scanned this batch into its set.
+//   1 tgn_agg_emit   sampled edges (neighbor_loader.py:26-50 order) + Δt cos/sin into dense [enc | msg] rows ‖
+//                    per sampled node its stored messages -> IdentityMessage -> Last/Mean aggregate
+//                    (memory_module.py:152-207) ‖ per-root / per-centre records for the predictor's attention
 //   2 gemmN          ring insert of the batch ‖ GRUCell / RNNCell over [msg | memory] (gate math in the
 //                    epilogue) ‖ lin_edge over [cos(w Δt + b) | msg] (the per-neighbour contraction)
 //   3 gemmN          lin_query / key / value / skip of every sampled node
 //   4 tgn_pred_train per event: TransformerConv forward of its 3 roots (waves 1-3) ‖ predictor weight
-//                    staging (wave 0); LinkPredictor + BCE + backward rows
+//                    staging (wave 0); LinkPredictor + BCE + backward rows ‖ the sampled edges sorted by
+//                    neighbour (one block) ‖ the NEXT batch's marking into the other set
 //                    (DyRep embedding messages: + one update-list aggregation / updater launch here)
-//   5 tgn_attn_bwd   attention backward ‖ predictor bias / output-layer / loss reductions (+ fused Adam)
-//   6 gemmN          the NEXT batch's marking ‖ per-edge (dk, dv) summed into the neighbours' k / v rows
-//                    ‖ dW_edge (split-K) ‖ dEnc·W_e
-//   7 gemmN          dW_proj, dW_src/dst (split-K) ‖ dz0 = dP W with the cell backward in the epilogue
-//   8 gemmN          dW_cell (split-K) ‖ dX_enc ‖ message stores ‖ step-descriptor snapshot + counters
-//   9 gemm_fixup     the NEXT batch's scan (sorted node sets, insert / store plans) ‖ split-K sums with
-//                    fused Adam ‖ Δt reduction ‖ memory / last_update of src ∪ dst
+//   5 tgn_attn_bwd   attention backward: dq per centre ‖ per edge (dk, dv, dE) summed into the neighbours' k / v
+//                    rows ‖ predictor bias / output-layer / loss reductions (+ fused Adam)
+//   6 gemmN          dz0 = dP W with the cell backward in the epilogue ‖ dW_proj, dW_src/dst (split-K)
+//   7 gemmN          the NEXT batch's scan into the other set (sorted node sets, insert / store plans) ‖ dX_enc ‖
+//                    dW_cell, dW_edge (split-K) ‖ dEnc·W_e ‖ step-descriptor snapshot ‖ message stores
+//   8 gemm_fixup     split-K sums with fused Adam ‖ Δt reduction ‖ memory / last_update of src ∪ dst ‖ counters
+//                    advance + the next batch's descriptor
+// 2 hops keep the separate k / v reduction launch (tgn_kv_reduce beside the dE-only GEMMs).
 // Data parallel (world > 1): the same launches without fused Adam; the exchange (one all-reduce of
 // [gradients | memory-row slots]) and tgnx_tgn_apply_rows_update follow.
 #include "tgnx_gemm.h"
