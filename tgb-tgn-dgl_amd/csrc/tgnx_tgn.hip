@@ -3560,21 +3560,14 @@ struct MarkNextJob {
 #ifndef TGNX_KV_FUSE
 #define TGNX_KV_FUSE 1  // 1-hop train: (dk, dv) per edge computed and summed in tgn_attn_bwd (no k / v reduction launch)
 #endif
-#ifndef TGNX_KVF_LAYOUT
-// with TGNX_KV_FUSE, where the dE-only GEMMs (dW_edge, dEnc·W_e) ride: 0 = the dz0 launch, 1 = the dW_gru
-// launch (A/B: 0.0987 vs 0.1013 ms with 0, 0.1018 unfused); 2..4 = dW_proj / dW_lp moved there too (0.1013 -
-// 0.1035: slower); 5 = as 1 with dz0 the dz0 launch's first job (0.0985 vs 0.0991)
-#define TGNX_KVF_LAYOUT 5
-#endif
 #ifndef TGNX_KVF_MARK_AT
 #define TGNX_KVF_MARK_AT 5  // with TGNX_KV_FUSE: the launch of a non-parity pipelined step's next-batch marking (5 or 8)
 #endif
 #ifndef TGNX_MD_CAP
 #define TGNX_MD_CAP 512  // grid cap of the step's M x D GEMMs (dz0, dX_enc): 7 column tiles at D = 100, ~30 row tiles at B = 200 (A/B 0.0966 vs 0.0971 ms with 1024)
 #endif
-#ifndef TGNX_L8_ORDER
-#define TGNX_L8_ORDER 3  // job order of the dW_gru launch (block ranges in order: the first dispatch first);
-                         // 3 (GEMMs before the snapshot / store blocks): 0.0970 vs 0.0986 ms with 0
+#ifndef TGNX_SCAN_AT
+#define TGNX_SCAN_AT 7  // parity step: the launch the next batch's scan rides in (7: dW_gru; 6: dz0, 0.1005 vs 0.0965 ms)
 #endif
 #ifndef TGNX_PIPE_MARK_AT
 #define TGNX_PIPE_MARK_AT 7
@@ -4543,71 +4536,29 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const auto j_scan = BlockJob<ScanJob, 3 * MARK_LDS_WORDS>{ScanJob{cn}, 1 + 2 * c.pplan};
   const auto j_snap = BlockJob<SnapJob>{SnapJob{c, ppm ? 1 : 0}, 1};
   const auto j_store = BlockJob<StoreJob>{StoreJob{c, nst}, nst};
+  // (the scan may ride in the dz0 launch instead: TGNX_SCAN_AT 6)
+  const bool scan6 = scan_w3 && kvf && TGNX_SCAN_AT == 6;
   auto l8 = [&](auto... jobs) {
     probe_begin(TGNX_K_WGRAD3, s);
-#if TGNX_L8_ORDER == 1
-    if (scan_w3)
-      gemmN_launch(s, j_scan, j_snap, j_store, j_dxe, j_dwg, jobs...);
-    else
-      gemmN_launch(s, mk_at(9), j_snap, j_store, j_dxe, j_dwg, jobs...);
-#elif TGNX_L8_ORDER == 2
-    if (scan_w3)
-      gemmN_launch(s, j_scan, j_snap, j_store, jobs..., j_dxe, j_dwg);
-    else
-      gemmN_launch(s, mk_at(9), j_snap, j_store, jobs..., j_dxe, j_dwg);
-#elif TGNX_L8_ORDER == 3
-    if (scan_w3)
+    // the GEMM jobs before the snapshot / store blocks (0.0970 vs 0.0986 ms with those first)
+    if (scan_w3 && !scan6)
       gemmN_launch(s, j_scan, j_dxe, j_dwg, jobs..., j_snap, j_store);
     else
-      gemmN_launch(s, mk_at(9), j_dxe, j_dwg, jobs..., j_snap, j_store);
-#elif TGNX_L8_ORDER == 4
-    if (scan_w3)
-      gemmN_launch(s, j_scan, j_dxe, jobs..., j_dwg, j_snap, j_store);
-    else
-      gemmN_launch(s, mk_at(9), j_dxe, jobs..., j_dwg, j_snap, j_store);
-#elif TGNX_L8_ORDER == 5
-    if (scan_w3)
-      gemmN_launch(s, j_scan, j_dwg, j_dxe, jobs..., j_snap, j_store);
-    else
-      gemmN_launch(s, mk_at(9), j_dwg, j_dxe, jobs..., j_snap, j_store);
-#elif TGNX_L8_ORDER == 6
-    if (scan_w3)
-      gemmN_launch(s, j_dxe, j_dwg, jobs..., j_scan, j_snap, j_store);
-    else
-      gemmN_launch(s, mk_at(9), j_dxe, j_dwg, jobs..., j_snap, j_store);
-#else
-    if (scan_w3)
-      gemmN_launch(s, j_scan, j_snap, j_store, j_dwg, j_dxe, jobs...);
-    else
-      gemmN_launch(s, mk_at(9), j_snap, j_store, j_dwg, j_dxe, jobs...);
-#endif
+      gemmN_launch(s, j_dxe, j_dwg, jobs..., j_snap, j_store);
     probe_end(TGNX_K_WGRAD3, s);
     TGNX_LAUNCH_CHECK("tgn_wgrad3");
   };
-  // which of the two weight-gradient launches the dE-only GEMMs (and the other deferred ones) ride in
+  // kvf: the dE-only GEMMs ride in the dW_gru launch (in the dz0 launch: 0.1013 vs 0.0987 ms; dW_proj / dW_lp
+  // moved to the dW_gru launch too: 0.1013 - 0.1035), dz0 first in its launch (0.0985 vs 0.0991)
   if (!kvf) {
     l7(j_dwp, j_dwlp, j_dz0);
     l8();
-  } else {
-#if TGNX_KVF_LAYOUT == 0
-    l7(j_dwp, j_dwlp, j_dz0, j_dwe, j_denc);
-    l8();
-#elif TGNX_KVF_LAYOUT == 1
-    l7(j_dwp, j_dwlp, j_dz0);
+  } else if (scan6) {
+    l7(j_scan, j_dz0, j_dwp, j_dwlp);
     l8(j_dwe, j_denc);
-#elif TGNX_KVF_LAYOUT == 2
-    l7(j_dz0);
-    l8(j_dwe, j_denc, j_dwp, j_dwlp);
-#elif TGNX_KVF_LAYOUT == 3
-    l7(j_dwp, j_dz0);
-    l8(j_dwe, j_denc, j_dwlp);
-#elif TGNX_KVF_LAYOUT == 4
-    l7(j_dwlp, j_dz0);
-    l8(j_dwe, j_denc, j_dwp);
-#else
+  } else {
     l7(j_dz0, j_dwp, j_dwlp);
     l8(j_dwe, j_denc);
-#endif
   }
   if (ppm && !scan_w3) {
     tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(cn, 1, 0);
