@@ -1386,8 +1386,12 @@ __device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m, bool grad) {
 // are computed) — so 16 messages' rows are in flight per round instead of 4: a hub node of the
 // review-shaped stream (~50 messages per wave) walks 4 dependent load rounds instead of 13.  Sums run in
 // the same order as agg_node_mean_wg (per wave in event order, waves combined 0..3): bit-identical X rows.
-constexpr int AGG_MC = 16;  // messages whose rows are loaded in one round
-template <bool EMB = false>
+#ifndef TGNX_AGG_MC1
+#define TGNX_AGG_MC1 12  // messages per load round of the mean path at d <= 64 (review-shaped A/Bs: 12 0.1025 ms, 8 0.1027, 16 0.1025-0.1037, 24 0.1045, 32 0.1052)
+#endif
+// RB raw-message columns per lane (3: d <= 192; 1: d <= 64), MC messages whose rows are loaded in one round
+// (the same load registers: 16 x (2 + 3) or 24 x (2 + 1))
+template <bool EMB = false, int RB = 3, int MC = 16>
 __device__ void agg_node_mean_cols(const Ctx& c, int64_t n, int m, bool grad) {
   __shared__ float red[4][3 * TDMAX + 192 + 2 * TDMAX];  // per wave: X columns (Qm) | sin sums | sin·Δt sums
   __shared__ float rmax[4];
@@ -1422,7 +1426,9 @@ __device__ void agg_node_mean_cols(const Ctx& c, int64_t n, int m, bool grad) {
     tb[a] = P[c.L.te_b + j];
   }
   float sN[2] = {0.f, 0.f}, sO[2] = {0.f, 0.f}, sC[2] = {0.f, 0.f}, s0[2] = {0.f, 0.f}, s1[2] = {0.f, 0.f};
-  float sR[3] = {0.f, 0.f, 0.f};
+  float sR[RB];
+#pragma unroll
+  for (int b = 0; b < RB; ++b) sR[b] = 0.f;
   const int qa = w * tot / 4, qe = (w + 1) * tot / 4;  // this wave's messages (event order)
   float tmax = -INFINITY;
   for (int q0 = qa; q0 < qe; q0 += 64) {
@@ -1431,10 +1437,10 @@ __device__ void agg_node_mean_cols(const Ctx& c, int64_t n, int m, bool grad) {
     store_event(c, sv, q0 + lane, e_l, o_l, t_l);
     if (q0 + lane < qe) tmax = fmaxf(tmax, t_l);
     const int nq = min(64, qe - q0);
-    for (int qb = 0; qb < nq; qb += AGG_MC) {
-      float vo[AGG_MC][2], vr[AGG_MC][3];
+    for (int qb = 0; qb < nq; qb += MC) {
+      float vo[MC][2], vr[MC][RB];
 #pragma unroll
-      for (int u = 0; u < AGG_MC; ++u) {
+      for (int u = 0; u < MC; ++u) {
         const int q = min(qb + u, nq - 1);
         const int64_t e = shfl_i64(e_l, q), o = shfl_i64(o_l, q);
         const float* rowO = msg_row<EMB>(c, o, false, m);
@@ -1442,10 +1448,10 @@ __device__ void agg_node_mean_cols(const Ctx& c, int64_t n, int m, bool grad) {
 #pragma unroll
         for (int a = 0; a < 2; ++a) vo[u][a] = rowO[min(lane + 64 * a, D - 1)];
 #pragma unroll
-        for (int b = 0; b < 3; ++b) vr[u][b] = raw[min(lane + 64 * b, d - 1)];
+        for (int b = 0; b < RB; ++b) vr[u][b] = raw[min(lane + 64 * b, d - 1)];
       }
 #pragma unroll
-      for (int u = 0; u < AGG_MC; ++u) {
+      for (int u = 0; u < MC; ++u) {
         if (qb + u >= nq) break;
         const float dt = lane_f(t_l, qb + u) - lun;
 #pragma unroll
@@ -1459,7 +1465,7 @@ __device__ void agg_node_mean_cols(const Ctx& c, int64_t n, int m, bool grad) {
           s1[a] += sn * dt;
         }
 #pragma unroll
-        for (int b = 0; b < 3; ++b) sR[b] += vr[u][b];
+        for (int b = 0; b < RB; ++b) sR[b] += vr[u][b];
       }
     }
   }
@@ -1476,7 +1482,7 @@ __device__ void agg_node_mean_cols(const Ctx& c, int64_t n, int m, bool grad) {
     }
   }
 #pragma unroll
-  for (int b = 0; b < 3; ++b)
+  for (int b = 0; b < RB; ++b)
     if (lane + 64 * b < d) rw[2 * D + lane + 64 * b] = sR[b];
   const float wm = wave_max_f(tmax);
   if (lane == 0) rmax[w] = wm;
@@ -1670,7 +1676,10 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
   if (AG != 0 && c.aggr == 1 && (mode == 0 || list)) {  // MeanAggregator, train / eval update: a workgroup per node (hub
                                              // nodes store many messages); the all-node flush stays wave-per-node
     if (AG == 1 || c.d <= 192) {  // (AG == 1 is launched for d <= 192 only)
-      for (int m = bid; m < n; m += nb) agg_node_mean_cols<EMB>(c, mode == 0 ? c.nid[m] : list[m], m, mode == 0);
+      if (c.d <= 64)
+        for (int m = bid; m < n; m += nb) agg_node_mean_cols<EMB, 1, TGNX_AGG_MC1>(c, mode == 0 ? c.nid[m] : list[m], m, mode == 0);
+      else
+        for (int m = bid; m < n; m += nb) agg_node_mean_cols<EMB>(c, mode == 0 ? c.nid[m] : list[m], m, mode == 0);
     } else {
       for (int m = bid; m < n; m += nb) agg_node_mean_wg<EMB>(c, mode == 0 ? c.nid[m] : list[m], m, mode == 0);
     }
@@ -3560,6 +3569,9 @@ struct MarkNextJob {
 #ifndef TGNX_KV_FUSE
 #define TGNX_KV_FUSE 1  // 1-hop train: (dk, dv) per edge computed and summed in tgn_attn_bwd (no k / v reduction launch)
 #endif
+#ifndef TGNX_PP_MARK_AT_LARGE
+#define TGNX_PP_MARK_AT_LARGE 5  // (8: review-shaped 0.1040 vs 0.1037 ms, not kept)
+#endif
 #ifndef TGNX_KVF_MARK_AT
 #define TGNX_KVF_MARK_AT 5  // with TGNX_KV_FUSE: the launch of a non-parity pipelined step's next-batch marking (5 or 8)
 #endif
@@ -4414,8 +4426,10 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // (kvf: no k / v launch; the next batch's marking of a non-parity pipelined step rides in the predictor launch
   // beside its sort block, as the parity step's does)
   const int mark_at = kvf ? TGNX_KVF_MARK_AT : TGNX_PIPE_MARK_AT;
+  // parity step: the predictor launch (5) or, for graphs marked through summary bitmaps, the dz0 launch (8)
+  const int pp_mark_at = TGNX_PP_MARK_AT_LARGE == 8 && kvf && !scan_direct(c.words) ? 8 : 5;
   auto mk_at = [&](int at) {
-    return BlockJob<MarkNextJob, 3 * MARK_LDS_WORDS>{MarkNextJob{c, nmark}, pipe && !ppm && at == mark_at ? nmark : 0};
+    return BlockJob<MarkNextJob, 3 * MARK_LDS_WORDS>{MarkNextJob{c, nmark}, pipe && at == (ppm ? pp_mark_at : mark_at) ? nmark : 0};
   };
   probe_begin(TGNX_K_PROJ, s);
   gemmN_launch(s, mk_at(3),
@@ -4441,7 +4455,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   }
   probe_begin(TGNX_K_PRED, s);
   TGNX_CHECK_ARG(pred_smem_ok(c.D), "tgn_pred_train: dynamic LDS attribute refused");
-  const int nmk = (ppm || (pipe && mark_at == 5)) ? nmark : 0;
+  const int nmk = (ppm ? pp_mark_at == 5 : pipe && mark_at == 5) ? nmark : 0;
   const size_t psm = std::max(tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0);
   const int nsrt = kvf && TGNX_KVE_GSORT ? 1 : 0;  // (kvf implies the rows fit the sort's LDS counters)
   if (att_in_pred)
