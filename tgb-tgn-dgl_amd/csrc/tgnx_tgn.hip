@@ -207,6 +207,7 @@ struct Ctx {
   float *alk, *Qo;
   int kvf = 0;
   int *kj, *kx, *ke;  // kvf: the sampled edges sorted by neighbour row (tgn_pred_train's sort block): row, centre, edge
+  int kvs = 0;        // kvf: those arrays are this step's (else the edge blocks read the edges in sampling order)
   float *encE, *sinE;  // per sampled edge: cos / sin of the Δt encoding argument [E][D]
   float *s0m, *s1m;    // per GRU row: (mean over its messages of) sin(arg), sin(arg) Δt  [M][D]
   float *pA, *pB, *pC, *pD;  // split-K partials of the deferred weight-gradient GEMMs
@@ -2472,6 +2473,9 @@ __device__ void lp_vec_body(const Ctx& c, int y, int lane) {
 #define TGNX_KVE_CH 32
 #endif
 constexpr int KVE_CH = TGNX_KVE_CH, KVE_PW = KVE_CH / 4;
+#ifndef TGNX_KVF_2HOP
+#define TGNX_KVF_2HOP 1  // 2 hops: the outer level's attention backward sums its edges' (dk, dv) too
+#endif
 #ifndef TGNX_KVE_GSORT
 #define TGNX_KVE_GSORT 1  // edges globally sorted by neighbour (edge_sort_body in the predictor launch)
 #endif
@@ -2491,19 +2495,14 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
   const int ne = min(KVE_CH, E - eb);
   __shared__ int sj[KVE_CH], sx[KVE_CH], se[KVE_CH], sorder[KVE_CH], sb[2];
   const int t = threadIdx.x;
-#if TGNX_KVE_GSORT
+  const bool gs = c.kvs;  // workgroup-uniform
   // globally sorted: a run whose row has no edge in the neighbouring chunks is the row's whole sum (a plain
   // store); the chunk's first / last runs may continue there (the keys just outside the chunk tell)
-  if (t == KVE_CH) sb[0] = eb > 0 ? c.kj[eb - 1] : -1;
-  if (t == KVE_CH + 1) sb[1] = eb + ne < E ? c.kj[eb + ne] : -1;
-#endif
+  if (gs && t == KVE_CH) sb[0] = eb > 0 ? c.kj[eb - 1] : -1;
+  if (gs && t == KVE_CH + 1) sb[1] = eb + ne < E ? c.kj[eb + ne] : -1;
   if (t < KVE_CH) {  // the edge's neighbour (sort key), centre and id, one round
     const int ec = min(eb + t, E - 1);
-#if TGNX_KVE_GSORT
-    const int j = c.kj[ec], x = c.kx[ec], eo = c.ke[ec];
-#else
-    const int j = c.e_j[ec], x = c.e_c[ec], eo = ec;
-#endif
+    const int j = gs ? c.kj[ec] : c.e_j[ec], x = gs ? c.kx[ec] : c.e_c[ec], eo = gs ? c.ke[ec] : ec;
     sj[t] = t < ne ? j : INT_MAX;
     sx[t] = x;
     se[t] = eo;
@@ -2603,7 +2602,7 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
           if (lane == 0) pk[2 * w] = jc;
           first = false;
         } else {
-          if (TGNX_KVE_GSORT) store();
+          if (gs) store();
           else flush();
         }
 #else
@@ -2641,13 +2640,13 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
   if (w != 0) return;
   jc = -1;
   bool firstg = true;  // the open group holds the chunk's first edge
-  const int kprev = TGNX_KVE_GSORT ? sb[0] : -2, knext = TGNX_KVE_GSORT ? sb[1] : -2;
+  const int kprev = gs ? sb[0] : -2, knext = gs ? sb[1] : -2;
   for (int sl = 0; sl < 8; ++sl) {
     const int key = pk[sl];
     if (key < 0) continue;
     if (key != jc) {
       if (jc >= 0) {
-        if (TGNX_KVE_GSORT && !(firstg && jc == kprev)) store();
+        if (gs && !(firstg && jc == kprev)) store();
         else flush();
         firstg = false;
       }
@@ -2657,7 +2656,7 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
     for (int q = 0; q < 4; ++q) s[q] += ps[sl][q][lane];
   }
   if (jc >= 0) {
-    if (TGNX_KVE_GSORT && !(firstg && jc == kprev) && jc != knext) store();
+    if (gs && !(firstg && jc == kprev) && jc != knext) store();
     else flush();
   }
 #else
@@ -4421,8 +4420,11 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // 1 hop with the attention forward in the predictor: the attention backward computes each edge's (dk, dv)
   // where it sums them (kv_edge_body), so the k / v reduction launch is gone and the GEMMs that need only dE
   // ride in a later launch
-  const bool kvf = !two && TGNX_PRED_ATT && TGNX_KV_FUSE && (!TGNX_KVE_GSORT || (size_t)k.Mtr + 1 <= tgn_pred_smem(c.D) / 4);
+  // (2 hops: the outer level, whose attention forward is tgn_attn_fwd; its edges keep the sampling order)
+  const bool kvf = TGNX_KV_FUSE && (two ? TGNX_KVF_2HOP : TGNX_PRED_ATT);
+  const bool kvs = kvf && !two && TGNX_KVE_GSORT && (size_t)k.Mtr + 1 <= tgn_pred_smem(c.D) / 4;
   c.kvf = kvf ? 1 : 0;
+  c.kvs = kvs ? 1 : 0;
   // (kvf: no k / v launch; the next batch's marking of a non-parity pipelined step rides in the predictor launch
   // beside its sort block, as the parity step's does)
   const int mark_at = kvf ? TGNX_KVF_MARK_AT : TGNX_PIPE_MARK_AT;
@@ -4445,7 +4447,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     probe_end(TGNX_K_SEG_FWD, s);
     TGNX_LAUNCH_CHECK("tgn_attn_fwd");
   }
-  const Ctx cr = two ? root_view(c) : c;  // the level the predictor reads
+  Ctx cr = two ? root_view(c) : c;  // the level the predictor reads
+  if (two) cr.kvf = cr.kvs = 0;    // (conv2 keeps its k / v reduction launch)
   if (two) {  // conv2 over the roots: projections of h1 (rows = outer centres), attention per root
     gemm_launch<G32>(gemm_shape<G32>(k.Rtr, 4 * HC, HC, c.cnt + CNT_R), LoadRowK{c.Zc, k.Rtr, HC, HC},
                      LoadProjW{P + c.L.wq2, c.L.pw, HC, HC}, EpiProj{P + c.L.bq2, c.L.pb, c.P2, HC}, nullptr, s);
@@ -4457,7 +4460,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   TGNX_CHECK_ARG(pred_smem_ok(c.D), "tgn_pred_train: dynamic LDS attribute refused");
   const int nmk = (ppm ? pp_mark_at == 5 : pipe && mark_at == 5) ? nmark : 0;
   const size_t psm = std::max(tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0);
-  const int nsrt = kvf && TGNX_KVE_GSORT ? 1 : 0;  // (kvf implies the rows fit the sort's LDS counters)
+  const int nsrt = kvs ? 1 : 0;  // (kvs: the rows fit the sort's LDS counters)
   if (att_in_pred)
     launch_k(tgn_pred_train<true>, dim3(k.B + nsrt + nmk), dim3(256), (uint32_t)psm, s, cr, nmk, nsrt);
   else
@@ -4493,7 +4496,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                  gemm_job<GW>(shp_dWp2(k, c.cnt), LoadKRow{c.dP2, 4 * HC, k.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
                                EpiDeferred{}, c.pE));
     TGNX_LAUNCH_CHECK("tgn_dh1");
-    tgn_attn_bwd<<<gridn(k.Rtr, 4, 1 << 20), 256, 0, s>>>(c, gridn(k.Rtr, 4, 1 << 20), 0);
+    const int ncb = gridn(k.Rtr, 4, 1 << 20), nkv = kvf ? gridn(k.Etr, KVE_CH, 1 << 20) : 0;
+    tgn_attn_bwd<<<ncb + nkv, 256, 0, s>>>(c, ncb, nkv);
   } else {
     const int ncb = gridn(k.Rtr, 4, 1 << 20);
     const int nkv = kvf ? gridn(k.Etr, KVE_CH, 1 << 20) : 0;
