@@ -21,7 +21,8 @@
 //                    dW_cell, dW_edge (split-K) ‖ dEnc·W_e ‖ step-descriptor snapshot ‖ message stores
 //   8 gemm_fixup     split-K sums with fused Adam ‖ Δt reduction ‖ memory / last_update of src ∪ dst ‖ counters
 //                    advance + the next batch's descriptor
-// 2 hops keep the separate k / v reduction launch (tgn_kv_reduce beside the dE-only GEMMs).
+// 2 hops: the outer level's attention backward sums its edges' (dk, dv, dE) as launch 5 does; the inner
+// (conv2) level keeps its k / v reduction launch (tgn_kv_reduce2 beside its dE2-only GEMMs).
 // Data parallel (world > 1): the same launches without fused Adam; the exchange (one all-reduce of
 // [gradients | memory-row slots]) and tgnx_tgn_apply_rows_update follow.
 #include "tgnx_gemm.h"
