@@ -196,6 +196,9 @@ typedef struct {
   double* mrr;             /* eval: per-batch MRR, indexed by ctl[NB]-1 */
   void* ws;                /* tgnx_tgnn_ws_bytes(cfg) bytes, zero-filled once */
   void* node_map;          /* int32[4*N], zero-filled once (persistent across steps) */
+  float* out_ev;           /* optional (NULL: unused): [num_events, 2] train logits by event row (pos at
+                              [2e], neg at [2e + 1]): the epoch's outputs for the AP / AUC display
+                              (epoch_utils.py:310-317) without a copy per step */
 } tgnx_tgnn_buffers;
 
 int tgnx_tgnn_param_layout(const tgnx_tgnn_config* cfg, int64_t* offsets /* [TGNX_TGNN_NPARAM+1] */);
@@ -314,6 +317,10 @@ typedef struct {
                                      rank's step updated, exchanged after the step; NULL at
                                      world 1 */
   int64_t xcap;                   /* >= 2 * ceil(max_batch / world) */
+  float* out_ev;                  /* optional (NULL: unused): [num_events, 2] train outputs by event row —
+                                     sigmoid(pos), sigmoid(neg) of event e at [2e], [2e + 1] — so that an
+                                     epoch of replayed steps leaves every batch's outputs for the AP / AUC
+                                     display (pyg_epoch_utils.py:139-147) without a copy per step */
 } tgnx_tgn_buffers;
 /* exchanged memory row, all fields floats holding exact integers so that the row survives a SUM exchange
  * (one all-reduce over [gradients | every rank's row slots, zero but the sender's] is the all-gather):
@@ -405,6 +412,19 @@ int tgnx_tgn_train_fwd_bwd_split(const tgnx_tgn_config* cfg, const tgnx_tgn_buff
                                  int32_t dropout, int32_t prefetched, void* stream);
 int tgnx_tgn_scan_next(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo, int64_t split_hi,
                        int64_t batch, int32_t rank, int32_t world, uint64_t base_seed, void* stream);
+/* The data-parallel step on the parity-set design of tgnx_tgn_train_step_pp (world >= 1, 1 hop, Adam not
+ * folded in): the next batch (this rank's slice) is marked in the predictor launch and scanned into set
+ * 1 - parity inside the dW_cell launch; the last launch writes the gradients, packs this rank's updated
+ * memory rows into buf->xrows, advances the counters and writes the next descriptor.  One step is this
+ * call, then the exchange (the all-reduce of [gradients | row slots]), then tgnx_tgn_apply_rows_update —
+ * which this call runs FIRST when apply_prev = 1 (rows / nrows: the whole exchanged row block), so that a
+ * step is one graph [apply(k-1) ‖ step k] plus one collective.  apply_prev must be 1 exactly when the
+ * previous call's exchange has not yet been applied.  prefetched / parity as tgnx_tgn_train_step_pp.
+ * Test: tests/test_gpu_tgn_dp.py (per rank against the split pipelined step) and tests/test_gpu_tgn_dp_worlds.py. */
+int tgnx_tgn_train_fwd_bwd_pp(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                              int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
+                              int32_t dropout, int32_t prefetched, int32_t parity, int32_t apply_prev, float* rows,
+                              int64_t nrows, void* stream);
 /* tgnx_tgn_apply_rows + tgnx_tgn_train_update in one launch (data parallel, after the exchange). */
 int tgnx_tgn_apply_rows_update(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, float* rows, int64_t nrows,
                                void* stream);

@@ -123,3 +123,36 @@ def test_config_sections_select_the_tgn_model(tmp_path):
         model_options(g2, memory_param=dict(mem2, mail_combine="max"))
     with pytest.raises(NotImplementedError):
         model_options(g2, memory_param=dict(mem2, type="none"))
+
+
+def test_batched_ap_auc_matches_sklearn():
+    """tgnx.tgn_epoch.ap_auc_rows / epoch_ap_auc (the drop-in train()'s AP / AUC display, computed for every
+    batch of the epoch at once from the per-event output log) against sklearn's average_precision_score /
+    roc_auc_score per batch (pyg_epoch_utils.py:139-145), with tied scores, a partial last batch and the
+    reference's extra sigmoid."""
+    import numpy as np
+    import torch
+    from sklearn.metrics import average_precision_score, roc_auc_score
+
+    from tgnx.tgn_epoch import ap_auc_rows, epoch_ap_auc
+    rng = np.random.default_rng(0)
+    for R, P, N, levels in ((7, 50, 50, 12), (3, 200, 200, 1000), (5, 9, 13, 3)):
+        pos = torch.from_numpy(rng.integers(0, levels, (R, P)).astype(np.float32) / levels)
+        neg = torch.from_numpy(rng.integers(0, levels, (R, N)).astype(np.float32) / levels)
+        ap, auc = ap_auc_rows(pos, neg, chunk_elems=1000)
+        for r in range(R):
+            y = np.r_[np.ones(P), np.zeros(N)]
+            sc = np.r_[pos[r].numpy(), neg[r].numpy()]
+            assert abs(float(ap[r]) - average_precision_score(y, sc)) < 1e-12, (R, r)
+            assert abs(float(auc[r]) - roc_auc_score(y, sc)) < 1e-12, (R, r)
+    out_ev = torch.from_numpy(rng.random((1030, 2), dtype=np.float32))
+    lo, hi, B = 10, 1030, 200
+    aps, aucs = [], []
+    for a in range(lo, hi, B):
+        b = min(a + B, hi)
+        y_pred = torch.cat([out_ev[a:b, 0], out_ev[a:b, 1]]).sigmoid()
+        y_true = torch.cat([torch.ones(b - a), torch.zeros(b - a)])
+        aps.append(average_precision_score(y_true, y_pred))
+        aucs.append(roc_auc_score(y_true, y_pred))
+    ap, auc = epoch_ap_auc(out_ev, lo, hi, B)
+    assert abs(ap - float(np.mean(aps))) < 1e-12 and abs(auc - float(np.mean(aucs))) < 1e-12

@@ -65,14 +65,15 @@ def test_pyg_dropin_epoch(monkeypatch):
     assert 0.0 < mrr2 <= 1.0
 
 
-def _write_cfg(path, mail_combine, batch):
+def _write_cfg(path, mail_combine, batch=None):
     import yaml
     src = open(__import__("os").path.join(__import__("os").path.dirname(__file__), "..", "tgb-tgn-dgl_amd", "config",
                                            "TGN.yml")).read()
     conf = yaml.safe_load(src)
     conf["memory"][0]["mail_combine"] = mail_combine
     conf["train"][0]["epoch"] = 1
-    conf["train"][0]["batch_size"] = batch
+    if batch is not None:
+        conf["train"][0]["batch_size"] = batch
     with open(path, "w") as f:
         yaml.safe_dump(conf, f)
     return str(path)
@@ -85,8 +86,9 @@ def test_reference_script_with_one_line_swap(tmp_path, monkeypatch):
     device, gnn_param=gnn_param), getOptimizer, and epoch_utils.train / test (NOT pyg_epoch_utils: :19
     keeps the DGL loop's import, which dispatches on the model dict).  The config says mail_combine 'mean';
     the model must be the MeanAggregator TGN: a fresh getModel from the same gnn_param, on two batches
-    with injected negatives and dropout off, matches oracle RefTGN(aggr='mean') and not aggr='last'."""
-    monkeypatch.setenv("TGNX_SYNTH_EVENTS", "3000")
+    with injected negatives and dropout off, matches oracle RefTGN(aggr='mean') and not aggr='last'.  The batch
+    size is TGN.yml's own (config/TGN.yml:27, batch_size 2000): two full batches and a partial one per epoch."""
+    monkeypatch.setenv("TGNX_SYNTH_EVENTS", "8000")
     monkeypatch.setenv("TGNX_EVAL_NEGS", "20")
     from dependencyGraph import dependecyAwareBatch as dab  # noqa: F401  (imported by the script, :17)
     from epoch_utils import test, train
@@ -94,7 +96,7 @@ def test_reference_script_with_one_line_swap(tmp_path, monkeypatch):
     from neighbor_loader import LastNeighborLoader
     from pyg_model_utils import getModel, getOptimizer
     from utils import getDataWithDependecyBlock, parse_config
-    cfg = _write_cfg(tmp_path / "TGN_mean.yml", "mean", 200)
+    cfg = _write_cfg(tmp_path / "TGN_mean.yml", "mean")
     device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
     sample_param, memory_param, gnn_param, train_param = parse_config(cfg)
     data, train_dataloader, val_dataloader, test_dataloader, neg_sampler, evaluator, metric = \
@@ -108,7 +110,8 @@ def test_reference_script_with_one_line_swap(tmp_path, monkeypatch):
     criterion = torch.nn.BCEWithLogitsLoss()
     m = model["model"]
     assert set(model) >= {"memory", "gnn", "link_pred"}
-    assert m.cfg.aggr == 1 and m.layers == 1 and m.updater == "gru" and m.cfg.max_batch == 200 and m.cfg.ring == 10
+    assert m.cfg.aggr == 1 and m.layers == 1 and m.updater == "gru" and m.cfg.max_batch == 2000 and m.cfg.ring == 10
+    assert train_param["batch_size"] == 2000
     for e in range(train_param["epoch"]):
         loss = train(model, data.msg, train_dataloader, neighbor_loader, neg_dest_sampler, assoc, device, optimizer,
                      criterion)
@@ -122,7 +125,7 @@ def test_reference_script_with_one_line_swap(tmp_path, monkeypatch):
     from oracle.sampler_ref import RefLastNeighborLoader
     from oracle.tgn_ref import RefTGN, train_step
     from tgnx.tgn import TgnEngine
-    N, d, D, B = data.num_nodes, data.msg.shape[1], gnn_param["dim_out"], 200
+    N, d, D, B = data.num_nodes, data.msg.shape[1], gnn_param["dim_out"], train_param["batch_size"]
     torch.manual_seed(0)
     refs = {a: RefTGN(N, d, hidden=D, aggr=a, dropout=0.0) for a in ("mean", "last")}
     refs["last"].load_state_dict(refs["mean"].state_dict())
@@ -137,7 +140,7 @@ def test_reference_script_with_one_line_swap(tmp_path, monkeypatch):
     ev_t, ev_msg = data.t.float(), data.msg.float()
     rng = np.random.default_rng(3)
     diff_last = 0.0
-    for st in range(3):
+    for st in range(2):
         sl = slice(st * B, (st + 1) * B)
         neg = torch.from_numpy(rng.choice(unique_destination_nodes.numpy(), size=B))
         pg, ng = e2.train_batch(st * B, B, neg=neg)

@@ -132,17 +132,30 @@ def test_tgn_comment_shape_2hop_b600_matches_oracle():
     _oracle_parity("tgbl-comment", N=300_000, B=600, d=2, aggr="last", layers=2, nb=3, kn=10, seed=13)
 
 
-@pytest.mark.parametrize("shape,N,d,aggr,layers,B", [("tgbl-coin", 638_486, 1, "last", 1, 200),
-                                                    ("tgbl-review", 352_637, 1, "mean", 1, 200),
-                                                    ("tgbl-comment", 300_000, 2, "last", 2, 600)])
-def test_tgn_dp_world2_large_graph_matches_single(shape, N, d, aggr, layers, B):
-    """Data parallel at the large configs (BASELINE #4 coin DP; #5's 2-hop batch 600): two world = 2 rank
-    engines on one device run their event slices of the same global batches; the host sums their
-    exchange buffers (the all-reduce: gradients + the rank-owned memory-row slots); both apply them.
-    Against a world = 1 engine on the same batches with device negatives and attention dropout on, lr = 0
-    (parameters fixed, so memory / outputs / gradients compare step after step): outputs 1e-5, gradient
-    sum 1e-4 relative, last_update / stores / ring exact, memory 1e-5 abs, the two ranks' memory tables
-    bit-identical."""
+def test_tgn_tgnyml_batch2000_matches_oracle():
+    """BASELINE config #1's batch: config/TGN.yml:27 batch_size 2000 on the wiki shape (N = 9,227, d = 172),
+    1 hop, LastAggregator, 20 eval negatives — the largest batch the reference's own configuration runs, just
+    under the max_batch 2048 cap (6,000 roots; the predictor launch's neighbour sort falls back to sampling
+    order when the sampled rows exceed its LDS counters)."""
+    _oracle_parity("tgbl-wiki", N=9_227, B=2000, d=172, aggr="last", layers=1, nb=3, kn=20, seed=14)
+
+
+@pytest.mark.parametrize("shape,N,d,aggr,layers,B,W", [("tgbl-coin", 638_486, 1, "last", 1, 200, 2),
+                                                      ("tgbl-review", 352_637, 1, "mean", 1, 200, 2),
+                                                      ("tgbl-comment", 300_000, 2, "last", 2, 600, 2),
+                                                      ("tgbl-coin", 638_486, 1, "last", 1, 800, 4),
+                                                      ("tgbl-comment", 994_790, 2, "last", 2, 600, 8),
+                                                      ("tgbl-wiki", 9_227, 172, "last", 1, 1600, 8)])
+def test_tgn_dp_large_graph_matches_single(shape, N, d, aggr, layers, B, W):
+    """Data parallel at the large configs: W world-W rank engines on one device run their event slices of the
+    same global batches of B events; the host sums their exchange buffers (the all-reduce: gradients + the
+    rank-owned memory-row slots); every rank applies them.  World 2 at the coin / review / comment shapes, and
+    the BASELINE world sizes: #4 coin at world 4 (global 800 = 4 x 200: 1,600 plan keys, partitioned plans,
+    4 row slots), #5 comment 2-hop at world 8 with the strong-scaling reading (global 600 -> 75 per rank) on
+    the full N = 994,790, and the wiki headline at world 8 (weak: global 1,600 = 8 x 200).  Against a
+    world = 1 engine on the same batches with device negatives and attention dropout on, lr = 0 (parameters
+    fixed, so memory / outputs / gradients compare step after step): outputs 1e-5, gradient sum 1e-4
+    relative, last_update / stores / ring exact, memory 1e-5 abs, every rank's memory table bit-identical."""
     from oracle.tgn_ref import RefTGN
     from tgnx.sampler import LastNeighborLoader
     from tgnx.synth import make_stream
@@ -154,7 +167,7 @@ def test_tgn_dp_world2_large_graph_matches_single(shape, N, d, aggr, layers, B):
     dev = torch.device("cuda")
     ev = dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32), msg=s.msg)
     engines = []
-    for rank, world in ((0, 1), (0, 2), (1, 2)):
+    for rank, world in [(0, 1)] + [(r, W) for r in range(W)]:
         model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=1, aggr=aggr, dropout=0.1,
                          layers=layers)
         model.load_reference_state(sd)
@@ -162,21 +175,21 @@ def test_tgn_dp_world2_large_graph_matches_single(shape, N, d, aggr, layers, B):
                         seed=1234, rank=rank, world=world)
         eng.reset_state()
         engines.append(eng)
-    e1, r0, r1 = engines
+    e1, ranks = engines[0], engines[1:]
     for st in range(nb):
         a = st * B
         e1.train_batch(a, B, neg=None, dropout=True, update=True)
-        for r in (r0, r1):
+        for r in ranks:
             r.train_batch(a, B, neg=None, dropout=True, update=False)
         torch.cuda.synchronize()
         for e in engines:
             e.check()
-        for rk, r in enumerate((r0, r1)):
-            lo, hi = B * rk // 2, B * (rk + 1) // 2
+        for rk, r in enumerate(ranks):
+            lo, hi = B * rk // W, B * (rk + 1) // W
             assert torch.equal(r.neg_train[a + lo:a + hi], e1.neg_train[a + lo:a + hi]), (st, rk)
             assert torch.allclose(r.out_pos[lo:hi], e1.out_pos[lo:hi], atol=1e-5), (st, rk)
             assert torch.allclose(r.out_neg[lo:hi], e1.out_neg[lo:hi], atol=1e-5), (st, rk)
-        gsum = r0.model.grad_flat + r1.model.grad_flat
+        gsum = sum(r.model.grad_flat for r in ranks)
         g1 = e1.model.grad_flat
         for name in e1.model.param_order:
             if name.endswith("lin_key.bias"):
@@ -185,12 +198,14 @@ def test_tgn_dp_world2_large_graph_matches_single(shape, N, d, aggr, layers, B):
             rel = float((gsum[o:o + n] - g1[o:o + n]).norm() / (g1[o:o + n].norm() + 1e-12))
             assert rel < 1e-4, (st, name, rel)
         assert abs(float(gsum[-1]) - float(g1[-1])) < 1e-5
-        tot = r0.comm + r1.comm                       # the all-reduce
-        for r in (r0, r1):
+        tot = sum(r.comm for r in ranks)              # the all-reduce
+        for r in ranks:
             r.comm.copy_(tot)
             r.apply_update(allreduce=False)
         torch.cuda.synchronize()
-        assert torch.equal(r0.model.memory.memory, r1.model.memory.memory), st
+        r0 = ranks[0]
+        for r in ranks[1:]:
+            assert torch.equal(r.model.memory.memory, r0.model.memory.memory), st
         assert torch.equal(r0.model.memory.last_update, e1.model.memory.last_update), st
         assert torch.allclose(r0.model.memory.memory, e1.model.memory.memory, atol=1e-5), \
             (st, float((r0.model.memory.memory - e1.model.memory.memory).abs().max()))

@@ -113,7 +113,7 @@ def test_tgn_dp_resident_folded_cursor_per_rank():
             e = TgnEngine(model, LastNeighborLoader(N, 10, device=dev), ev, TgnAdam(model, 1e-3),
                           dst_nodes=s.dst_nodes, seed=77, rank=rank, world=2)
             e.fold_cursor = fold
-            e.pipeline = False   # the pipelined form has its own test below
+            e.pipeline = False   # the pipelined forms have their own tests below
             e.bind_resident(0, split_hi, B, dropout=True)
             e.begin_epoch()
             eng[fold, rank] = e
@@ -190,6 +190,7 @@ def test_tgn_dp_pipelined_per_rank(split):
             e = TgnEngine(model, LastNeighborLoader(N, 10, device=dev), ev, TgnAdam(model, 1e-3),
                           dst_nodes=s.dst_nodes, seed=77, rank=rank, world=2)
             e.pipeline = pipe
+            e.parity_sets = False  # (the parity-set step: test_tgn_dp_parity_sets_per_rank)
             e.split_scan = split   # the next batch's scan beside the exchange (tgnx_tgn_scan_next) or in fwd_bwd
             e.bind_resident(0, split_hi, B, dropout=True)
             e.begin_epoch()
@@ -240,6 +241,104 @@ def test_tgn_dp_pipelined_per_rank(split):
                 assert torch.equal(e.model.flat, flat0), st
         assert torch.equal(eng[True, 0].model.memory.memory, eng[True, 1].model.memory.memory), st
         for rank in (0, 1):
+            p, u = eng[True, rank], eng[False, rank]
+            with torch.no_grad():
+                p.model.flat.copy_(u.model.flat)
+                p.adam_m.copy_(u.adam_m)
+                p.adam_v.copy_(u.adam_v)
+                p.model.memory.memory.copy_(u.model.memory.memory)
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_tgn_dp_parity_sets_per_rank(graphs):
+    """The data-parallel parity-set step (tgnx_tgn_train_fwd_bwd_pp, world = 2, one device: the next batch's
+    slice marked in the predictor launch and scanned into the other parity set inside the dW_cell launch; the
+    exchanged rows + Adam of step k at the head of step k + 1) against the split pipelined step
+    (tgnx_tgn_train_fwd_bwd_split + tgnx_tgn_scan_next + tgnx_tgn_apply_rows_update), per rank, lr 1e-3.
+    The parity-set engines run through the engine's own step (graph replays or eager steps) with the
+    collective replaced by a no-op; the test sums the exchange buffers of both ranks between steps, then
+    finish() applies them (so the next replay takes the graph without the apply at its head).  Per step:
+    counters, negatives, gradients + loss slot and packed rows before the apply; memory, last_update,
+    parameters, moments, loss sum, ring and stores after it.  A partial batch and one step past the split."""
+    from oracle.tgn_ref import RefTGN
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.synth import make_stream
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    N, B, d, D = 400, 64, 16, 32
+    s = make_stream("tgbl-wiki", seed=9, num_events=B * 9, num_nodes=N, msg_dim=d)
+    torch.manual_seed(0)
+    sd = RefTGN(N, d, hidden=D, aggr="last", dropout=0.1).state_dict()
+    dev = torch.device("cuda")
+    ev = dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32), msg=s.msg)
+    split_hi = 7 * B + 20
+    eng = {}
+    for pp in (True, False):
+        for rank in (0, 1):
+            model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=1, aggr="last", dropout=0.1)
+            model.load_reference_state(sd)
+            e = TgnEngine(model, LastNeighborLoader(N, 10, device=dev), ev, TgnAdam(model, 1e-3),
+                          dst_nodes=s.dst_nodes, seed=77, rank=rank, world=2)
+            e.parity_sets = pp
+            e.exchange = lambda comm, async_op: None
+            e.bind_resident(0, split_hi, B, dropout=True)
+            e.begin_epoch()
+            assert e._dp_pp() == pp and e._split() == (not pp)
+            if pp and graphs:
+                e.capture_resident()
+            eng[pp, rank] = e
+    for st in range(9):
+        for rank in (0, 1):
+            p = eng[True, rank]
+            if graphs:
+                p.replay_resident()
+            else:
+                p.resident_train_step()
+            u = eng[False, rank]
+            u._pre(u._prefetched)
+        torch.cuda.synchronize()
+        for e in eng.values():
+            e.check()
+        end = min(split_hi, (st + 1) * B)
+        for rank in (0, 1):
+            p, u = eng[True, rank], eng[False, rank]
+            for w in (3, 4, 10, 16):   # GEN, ADAM_T, NB, STEP_B
+                assert int(p.ctl[w]) == int(u.ctl[w]), (st, rank, w, int(p.ctl[w]), int(u.ctl[w]))
+            Bst = int(u.ctl[16])
+            assert Bst == (B if st < 7 else 20 if st == 7 else 0), (st, Bst)
+            assert torch.equal(p.neg_train[:end], u.neg_train[:end]), (st, rank)
+            G = p.model.grad_flat.numel()
+            if Bst:
+                assert _rel(p.comm[:G - 1], u.comm[:G - 1]) < 1e-5, (st, rank)
+                assert abs(float(p.comm[G - 1]) - float(u.comm[G - 1])) < 1e-5, (st, rank)
+                lo, hi = Bst * rank // 2, Bst * (rank + 1) // 2
+                assert torch.allclose(p.out_pos[lo:hi], u.out_pos[lo:hi], atol=1e-6), (st, rank)
+            assert torch.equal(p.xrows, u.xrows), (st, rank)
+        for pp in (True, False):
+            tot = eng[pp, 0].comm + eng[pp, 1].comm
+            for rank in (0, 1):
+                eng[pp, rank].comm.copy_(tot)
+        for rank in (0, 1):
+            p, u = eng[True, rank], eng[False, rank]
+            assert p._apply_pending
+            p.finish()
+            u._scan_next()
+            u._post()
+            u._prefetched = True
+        torch.cuda.synchronize()
+        for rank in (0, 1):
+            p, u = eng[True, rank], eng[False, rank]
+            pm, um = p.model, u.model
+            for w in (0, 1, 2, 7, 8, 9, 11):   # the next batch's descriptor (both prefetched it), no error
+                assert int(p.ctl[w]) == int(u.ctl[w]), (st, rank, w)
+            assert torch.equal(pm.memory.last_update, um.memory.last_update), (st, rank)
+            assert torch.allclose(pm.memory.memory, um.memory.memory, atol=1e-6), (st, rank)
+            assert _rel(pm.flat, um.flat) < 1e-6, (st, rank)
+            assert _rel(p.adam_m, u.adam_m) < 1e-5 and _rel(p.adam_v, u.adam_v) < 1e-5, (st, rank)
+            assert abs(p.loss_sum() - u.loss_sum()) <= 1e-6 * max(1.0, abs(u.loss_sum())), (st, rank)
+            assert torch.equal(p.loader.e_id, u.loader.e_id) and torch.equal(p.model.store, u.model.store), (st, rank)
+            assert torch.equal(p.xgather, torch.zeros_like(p.xgather)), (st, rank)   # slots zeroed by the apply
+        assert torch.equal(eng[True, 0].model.memory.memory, eng[True, 1].model.memory.memory), st
+        for rank in (0, 1):   # re-synchronise the parity-set twin
             p, u = eng[True, rank], eng[False, rank]
             with torch.no_grad():
                 p.model.flat.copy_(u.model.flat)

@@ -1,19 +1,29 @@
-"""The TGN data-parallel step through a real process group: two processes on one device, gloo
-(RCCL refuses two ranks on one GPU), each driving TgnEngine exactly as bench.py does at world 2 —
+"""The TGN data-parallel step through a real process group: W processes on one device, gloo
+(RCCL refuses several ranks on one GPU), each driving TgnEngine exactly as bench.py does at world W —
 bind_resident, begin_epoch, capture_resident, replay_resident — so the exchange is the engine's own
-asynchronous dist.all_reduce over [gradients | memory-row slots], with the next batch's scan
-(tgnx_tgn_scan_next, split_scan) replayed on the compute stream while the collective is in flight, then
-the apply-rows + Adam graph (tgnx/tgn.py TgnEngine._allreduce / replay_resident).
+dist.all_reduce over [gradients | memory-row slots].  Step forms (tgnx/tgn.py TgnEngine):
+  * pp    — the parity-set step (tgnx_tgn_train_fwd_bwd_pp): one graph [apply(k-1) ‖ step k] + the collective
+            (1 hop; the default);
+  * split — the split pipelined step: fwd_bwd graph, the collective with the next batch's scan replayed
+            beside it, the apply + Adam graph (the 2-hop form);
+  * fold  — fwd_bwd with the scan folded in, the collective, the apply + Adam graph.
+BASELINE's configs at their world sizes: #4 tgbl-coin-shaped at world 4 (global batch 800: 1,600 plan keys,
+partitioned plans, 4 row slots), #5 tgbl-comment-shaped 2-hop at world 8 with the strong-scaling reading
+(global 600 -> 75 events per rank, N = 994,790), and the headline tgbl-wiki shape at world 8 (weak scaling,
+global 1,600: 3,200 plan keys).
 
-Checks, per step:
-  * lr = 0 (parameters fixed, so states compare step after step): each rank's memory, last_update, ring
-    and message stores against a world-1 engine on the same global batches (memory 1e-5 abs, the rest
-    exact), and the two ranks bit-identical;
-  * lr = 1e-3: the two ranks' parameters, Adam moments and memory bit-identical after every step (the
-    replicas never drift), parameters moved.
-The step includes a partial last batch and one step past the split (B = 0)."""
+Checks (inside the rank processes; rank 0 also runs a world-1 engine over the same global batches):
+  * lr = 0 (parameters fixed, so states compare step after step): every rank bit-identical (digests of
+    memory, last_update, ring, stores, all-gathered), and rank 0 against the world-1 engine — memory 1e-5
+    abs, last_update / ring / stores exact, parameters unchanged;
+  * lr = 1e-3: every rank's parameters, Adam moments and memory bit-identical after every compared step.
+In the pp form the exchange of step k is applied at the head of step k + 1's graph; states are compared after
+odd steps (finish() applies it there), so the even steps run the graph with the apply inside.  The epoch
+includes a partial last batch and a step past the split (B = 0)."""
+import json
 import os
 import socket
+import traceback
 
 import numpy as np
 import pytest
@@ -21,42 +31,63 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-N, d, D, B, NB = 2000, 16, 32, 128, 6
+NB = 6
+CASES = {   # name: (shape, N, d, D, global batch, world, layers)
+    "wiki-small": ("tgbl-wiki", 2000, 16, 32, 128, 2, 1),
+    "coin-w4": ("tgbl-coin", 638_486, 1, 100, 800, 4, 1),
+    "comment2hop-w8": ("tgbl-comment", 994_790, 2, 100, 600, 8, 2),
+    "wiki-w8": ("tgbl-wiki", 9_227, 172, 100, 1600, 8, 1),
+}
 
 
-def _stream():
+def _stream(case):
     from tgnx.synth import make_stream
-    return make_stream("tgbl-wiki", seed=41, num_events=B * NB, num_nodes=N, msg_dim=d)
+    shape, N, d, D, Bg, W, layers = CASES[case]
+    return make_stream(shape, seed=41, num_events=Bg * NB, num_nodes=N, msg_dim=d)
 
 
-def _engine(s, rank, world, lr):
+def _engine(case, s, rank, world, lr):
     from oracle.tgn_ref import RefTGN
     from tgnx.sampler import LastNeighborLoader
     from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    shape, N, d, D, Bg, W, layers = CASES[case]
     torch.manual_seed(0)
-    sd = RefTGN(N, d, hidden=D, aggr="last", dropout=0.1).state_dict()
+    sd = RefTGN(N, d, hidden=D, aggr="last", dropout=0.1, layers=layers).state_dict()
     dev = torch.device("cuda", 0)
-    model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=B, max_neg=1, aggr="last", dropout=0.1)
+    model = TGNModel(N, s.num_events, d, D, dev, ring=10, max_batch=Bg, max_neg=1, aggr="last", dropout=0.1,
+                     layers=layers)
     model.load_reference_state(sd)
-    eng = TgnEngine(model, LastNeighborLoader(N, 10, device=dev),
-                    dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32), msg=s.msg), TgnAdam(model, lr),
-                    dst_nodes=s.dst_nodes, seed=99, rank=rank, world=world)
-    return eng
+    return TgnEngine(model, LastNeighborLoader(N, 10, device=dev),
+                     dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32), msg=s.msg), TgnAdam(model, lr),
+                     dst_nodes=s.dst_nodes, seed=99, rank=rank, world=world)
 
 
-def _split_hi():
-    return (NB - 3) * B + 40     # NB - 3 full batches, a partial one, then steps past the split
+def _split_hi(case):
+    Bg = CASES[case][4]
+    return (NB - 3) * Bg + 40     # NB - 3 full batches, a partial one, then steps past the split
 
 
-def _snapshot(eng):
+def _digest(t):
+    """Order-sensitive integer digest of a tensor's bits (bit-identity across ranks)."""
+    x = t.contiguous().view(-1)
+    x = x.view(torch.int32) if x.element_size() == 4 else x.view(torch.int64)
+    x = x.to(torch.int64)
+    w = torch.arange(1, x.numel() + 1, device=x.device, dtype=torch.int64) % 1_000_003
+    return torch.stack([x.sum(), (x * w).sum(), (x ^ (w * 2654435761)).sum()])
+
+
+def _state(eng):
     m = eng.model
-    return dict(memory=m.memory.memory.cpu().numpy(), last_update=m.memory.last_update.cpu().numpy(),
-                flat=m.flat.cpu().numpy(), adam_m=eng.adam_m.cpu().numpy(), adam_v=eng.adam_v.cpu().numpy(),
-                eid=eng.loader.e_id.cpu().numpy(), nbr=eng.loader.neighbors.cpu().numpy(),
-                store=m.store.cpu().numpy())
+    return dict(memory=m.memory.memory, last_update=m.memory.last_update, flat=m.flat, adam_m=eng.adam_m,
+                adam_v=eng.adam_v, eid=eng.loader.e_id, nbr=eng.loader.neighbors, store=m.store)
 
 
-def _worker(rank, world, port, lr, split, out_dir):
+def _configure(eng, mode):
+    eng.parity_sets = mode == "pp"
+    eng.split_scan = mode == "split"
+
+
+def _worker(case, rank, world, port, lr, mode, out_dir):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for p in (root, os.path.join(root, "tgb-tgn-dgl_amd")):
@@ -65,20 +96,59 @@ def _worker(rank, world, port, lr, split, out_dir):
     import torch.distributed as dist
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    res = {"rank": rank, "ok": False, "compared": []}
     try:
-        s = _stream()
-        eng = _engine(s, rank, world, lr)
-        eng.split_scan = split
-        eng.bind_resident(0, _split_hi(), B, dropout=True)
+        Bg = CASES[case][4]
+        s = _stream(case)
+        eng = _engine(case, s, rank, world, lr)
+        _configure(eng, mode)
+        eng.bind_resident(0, _split_hi(case), Bg, dropout=True)
         eng.begin_epoch()
         eng.capture_resident()
+        assert eng._dp_pp() == (mode == "pp"), (mode, eng._dp_pp())
+        e1 = None
+        if rank == 0 and lr == 0.0:
+            e1 = _engine(case, s, 0, 1, 0.0)    # world 1 over the same GLOBAL batches
+            e1.bind_resident(0, _split_hi(case), Bg, dropout=True)
+            e1.begin_epoch()
+        flat0 = eng.model.flat.clone()
         for st in range(NB - 1):
             eng.replay_resident()
+            if e1 is not None:
+                e1.resident_train_step()
+            compare = mode != "pp" or st % 2 == 1 or st == NB - 2
+            if not compare:
+                continue
+            eng.finish()
             torch.cuda.synchronize()
             eng.check()
-            np.savez(os.path.join(out_dir, f"r{rank}_s{st}.npz"), **_snapshot(eng))
+            mine = _state(eng)
+            keys = ("memory", "last_update", "eid", "nbr", "store") + (("flat", "adam_m", "adam_v") if lr else ())
+            dg = torch.stack([_digest(mine[k]) for k in keys]).cpu()
+            got = [torch.zeros_like(dg) for _ in range(world)]
+            dist.all_gather(got, dg)
+            for r in range(1, world):
+                assert torch.equal(got[r], got[0]), (st, "rank", r, "differs from rank 0")
+            if e1 is not None:
+                e1.check()
+                ref = _state(e1)
+                assert torch.equal(mine["last_update"], ref["last_update"]), st
+                assert torch.equal(mine["eid"], ref["eid"]) and torch.equal(mine["store"], ref["store"]), st
+                live = ref["eid"] >= 0
+                assert torch.equal(mine["nbr"][live], ref["nbr"][live]), st
+                err = float((mine["memory"] - ref["memory"]).abs().max())
+                assert err < 1e-5, (st, err)
+                assert torch.equal(mine["flat"], ref["flat"]) and torch.equal(mine["flat"], flat0), st  # lr = 0
+            res["compared"].append(st)
+        if lr:
+            assert not torch.equal(eng.model.flat, flat0)    # Adam moved the parameters on every rank alike
         dist.barrier()
+        res["ok"] = True
+    except Exception:
+        res["error"] = traceback.format_exc()
     finally:
+        with open(os.path.join(out_dir, f"r{rank}.json"), "w") as f:
+            json.dump(res, f)
         dist.destroy_process_group()
 
 
@@ -88,56 +158,45 @@ def _free_port():
         return so.getsockname()[1]
 
 
-def _run_ranks(lr, split, out_dir):
+def _run_ranks(case, lr, mode, out_dir):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
+    os.makedirs(str(out_dir), exist_ok=True)
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, lr, split, str(out_dir))) for r in range(2)]
+    world = CASES[case][5]
+    procs = [ctx.Process(target=_worker, args=(case, r, world, port, lr, mode, str(out_dir))) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(timeout=240)
+        p.join(timeout=300)
     for p in procs:
         if p.is_alive():
             p.kill()
             p.join()
+    for r in range(world):
+        path = os.path.join(str(out_dir), f"r{r}.json")
+        assert os.path.exists(path), f"rank {r} left no result (exit code {procs[r].exitcode})"
+        res = json.load(open(path))
+        assert res["ok"], f"rank {r}:\n{res.get('error')}"
+        assert res["compared"], r
+    for p in procs:
         assert p.exitcode == 0, f"rank process exit code {p.exitcode}"
 
 
-@pytest.mark.parametrize("split", [True, False])
-def test_tgn_dp_process_group_lr0_matches_world1(tmp_path, split):
-    _run_ranks(0.0, split, tmp_path)
-    s = _stream()
-    e1 = _engine(s, 0, 1, 0.0)
-    # world 1 over the same GLOBAL batches (the ranks' batch B is the global batch, sliced per rank)
-    e1.bind_resident(0, _split_hi(), B, dropout=True)
-    e1.begin_epoch()
-    for st in range(NB - 1):
-        e1.resident_train_step()
-        torch.cuda.synchronize()
-        e1.check()
-        ref = _snapshot(e1)
-        r0, r1 = (np.load(tmp_path / f"r{r}_s{st}.npz") for r in (0, 1))
-        for k in ("memory", "last_update", "eid", "nbr", "store"):
-            assert np.array_equal(r0[k], r1[k]), (st, k)
-        assert np.array_equal(r0["last_update"], ref["last_update"]), st
-        assert np.array_equal(r0["eid"], ref["eid"]) and np.array_equal(r0["store"], ref["store"]), st
-        live = ref["eid"] >= 0
-        assert np.array_equal(r0["nbr"][live], ref["nbr"][live]), st
-        err = float(np.abs(r0["memory"] - ref["memory"]).max())
-        assert err < 1e-5, (st, err)
-        assert np.array_equal(r0["flat"], ref["flat"]), st   # lr = 0: parameters never move
+@pytest.mark.parametrize("mode", ["pp", "split", "fold"])
+def test_tgn_dp_process_group_lr0_matches_world1(tmp_path, mode):
+    _run_ranks("wiki-small", 0.0, mode, tmp_path)
 
 
-def test_tgn_dp_process_group_replicas_stay_identical(tmp_path):
-    _run_ranks(1e-3, True, tmp_path)
-    first = None
-    for st in range(NB - 1):
-        r0, r1 = (np.load(tmp_path / f"r{r}_s{st}.npz") for r in (0, 1))
-        for k in ("flat", "adam_m", "adam_v", "memory", "last_update", "store", "eid"):
-            assert np.array_equal(r0[k], r1[k]), (st, k)
-        if first is None:
-            first = r0["flat"]
-    s = _stream()
-    init = _engine(s, 0, 1, 0.0).model.flat.cpu().numpy()
-    assert not np.array_equal(first, init)       # Adam moved the parameters on both ranks alike
+@pytest.mark.parametrize("mode", ["pp", "split"])
+def test_tgn_dp_process_group_replicas_stay_identical(tmp_path, mode):
+    _run_ranks("wiki-small", 1e-3, mode, tmp_path)
+
+
+@pytest.mark.parametrize("case", ["coin-w4", "comment2hop-w8", "wiki-w8"])
+def test_tgn_dp_process_group_baseline_worlds(tmp_path, case):
+    """BASELINE configs #4 / #5 and the wiki headline at their world sizes, lr = 0 against world 1 and
+    lr = 1e-3 replicas (the 2-hop comment case takes the split form; the others the parity-set step)."""
+    mode = "split" if CASES[case][6] == 2 else "pp"
+    _run_ranks(case, 0.0, mode, tmp_path / "lr0")
+    _run_ranks(case, 1e-3, mode, tmp_path / "lr1")

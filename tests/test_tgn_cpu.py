@@ -224,3 +224,33 @@ def test_dyrep_embedding_messages_follow_the_reference_loop():
                 if flags[1] and v in n_id:
                     dst_mem[i] = embeddings[assoc[v]]
             assert torch.equal(msg[:, :D], src_mem) and torch.equal(msg[:, D:2 * D], dst_mem)
+
+
+def test_oracle_epoch_noise_floor_by_time_scale():
+    """The premise of tests/test_gpu_tgn_epochs.py (oracle on one thread: torch's multi-threaded CPU scatter
+    reductions are not run-to-run deterministic): on a wiki-shaped stream whose timestamps span 2,000 s the
+    oracle's 2-epoch trajectory is insensitive to a 1-ulp change of the time-encoder weight (loss sums to 1e-6,
+    val MRR exactly), while at the wiki time scale (2,678,373 s) the same change moves the loss sums by 1e-4 or
+    more and the epoch-2 val MRR by a visible amount — multi-epoch parity there can only be statistical
+    (DESIGN §7)."""
+    from epoch_parity import initial_state, oracle_epochs, scaled_stream
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        s = scaled_stream(0, t_max=2000)
+        sd = initial_state(s, 0)
+        a = oracle_epochs(s, sd, 0)
+        assert oracle_epochs(s, sd, 0) == a                      # deterministic on one thread
+        b = oracle_epochs(s, sd, 0, perturb="memory.time_enc.lin.weight")
+        for e in range(2):
+            assert abs(a["loss"][e] - b["loss"][e]) <= 1e-6 * a["loss"][e]
+            assert a["mrr"][e] == b["mrr"][e]
+        s = scaled_stream(0)
+        sd = initial_state(s, 0)
+        a = oracle_epochs(s, sd, 0)
+        b = oracle_epochs(s, sd, 0, perturb="memory.time_enc.lin.weight")
+        for e in range(2):
+            assert abs(a["loss"][e] - b["loss"][e]) > 1e-4 * a["loss"][e]
+        assert abs(a["mrr"][1] - b["mrr"][1]) > 1e-3
+    finally:
+        torch.set_num_threads(nt)

@@ -171,6 +171,7 @@ struct Ctx {
   float *params, *grads, *am, *av;
   int64_t* ctl;
   float *out_pos, *out_neg;
+  float* out_ev;   // optional: train outputs by event row [nev, 2] (sigmoid pos, neg), the epoch's log
   double* mrr;
   float* xrows;  // data parallel: this rank's updated memory rows (TGNX_TGN_ROW layout), or nullptr
   int xcap;
@@ -2395,6 +2396,11 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt) 
       s[6] = (softplusf(-sp) + softplusf(sn)) * invB;
       c.out_pos[i] = sp;
       c.out_neg[i] = sn;
+      if (c.out_ev) {
+        const int64_t e = c.ctl[TGNX_CTL_BATCH_START] + i;
+        c.out_ev[2 * e] = sp;
+        c.out_ev[2 * e + 1] = sn;
+      }
     }
   }
   // barrier for dh (LDS) only: the evs-row stores of wave 0 stay in flight (__syncthreads waits vmcnt(0))
@@ -4023,6 +4029,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.out_pos = b->out_pos;
   c.out_neg = b->out_neg;
   c.mrr = b->mrr;
+  c.out_ev = b->out_ev;
   c.xrows = b->xrows;
   c.xcap = b->xrows ? (int)std::min<int64_t>(b->xcap, 1 << 30) : 0;
   TGNX_CHECK_ARG(!b->xrows || b->xcap > 0, "tgn: xrows without xcap");
@@ -4363,8 +4370,9 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const bool ppm = pp >= 0;
   Ctx cn;  // ppm: the other parity's set (the next batch's scan writes it)
   if (ppm) {
-    TGNX_CHECK_ARG(pp <= 1 && pipe != 0 && !no_tail && fuse_adam && k.layers == 1 && adv && adv->world == 1,
-                   "tgnx_tgn_train_step_pp: a fused world-1 1-hop resident step, parity 0 or 1");
+    TGNX_CHECK_ARG(pp <= 1 && pipe != 0 && !no_tail && k.layers == 1 && adv && (!fuse_adam || adv->world == 1),
+                   "tgnx_tgn_train_step_pp / tgnx_tgn_train_fwd_bwd_pp: a 1-hop resident step, parity 0 or 1 "
+                   "(Adam fused at world 1 only)");
     char* ws = reinterpret_cast<char*>(buf->ws);
     cn = set_view(c, W, ws, 1 - pp);
     c = set_view(c, W, ws, pp);
@@ -4541,6 +4549,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     gemmN_launch(s, mk_at(8), jobs...);
     probe_end(TGNX_K_EDGE_BWD, s);
     TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
+    return TGNX_OK;
   };
   // ‖ the message stores ‖ the fixup's descriptor copy + the counter advance (SnapJob)
   const int nst = gridn(2 * k.B, 256);
@@ -4566,18 +4575,17 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
       gemmN_launch(s, j_dxe, j_dwg, jobs..., j_snap, j_store);
     probe_end(TGNX_K_WGRAD3, s);
     TGNX_LAUNCH_CHECK("tgn_wgrad3");
+    return TGNX_OK;
   };
   // kvf: the dE-only GEMMs ride in the dW_gru launch (in the dz0 launch: 0.1013 vs 0.0987 ms; dW_proj / dW_lp
   // moved to the dW_gru launch too: 0.1013 - 0.1035), dz0 first in its launch (0.0985 vs 0.0991)
+  // (the lambdas return the launch checks' status)
   if (!kvf) {
-    l7(j_dwp, j_dwlp, j_dz0);
-    l8();
+    if ((rc = l7(j_dwp, j_dwlp, j_dz0)) || (rc = l8())) return rc;
   } else if (scan6) {
-    l7(j_scan, j_dz0, j_dwp, j_dwlp);
-    l8(j_dwe, j_denc);
+    if ((rc = l7(j_scan, j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) return rc;
   } else {
-    l7(j_dz0, j_dwp, j_dwlp);
-    l8(j_dwe, j_denc);
+    if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) return rc;
   }
   if (ppm && !scan_w3) {
     tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(cn, 1, 0);
@@ -4653,6 +4661,20 @@ int tgnx_tgn_train_step_pp(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b
   const AdvArgs a{split_lo, split_hi, batch, 0, 1, base_seed};
   TGNX_CHECK_ARG(parity == 0 || parity == 1, "tgnx_tgn_train_step_pp: parity must be 0 or 1");
   return train_step_impl(cfg, buf, 1, dropout, stream, true, &a, prefetched ? 1 : 2, parity);
+}
+
+int tgnx_tgn_train_fwd_bwd_pp(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
+                              int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
+                              int32_t dropout, int32_t prefetched, int32_t parity, int32_t apply_prev, float* rows,
+                              int64_t nrows, void* stream) {
+  TGNX_CHECK_ARG(parity == 0 || parity == 1, "tgnx_tgn_train_fwd_bwd_pp: parity must be 0 or 1");
+  TGNX_CHECK_ARG(!apply_prev || (nrows >= 0 && (nrows == 0 || rows)), "tgnx_tgn_train_fwd_bwd_pp: bad rows");
+  if (apply_prev) {  // the previous step's exchanged rows + Adam (tgnx_tgn_apply_rows_update) at the head of this step
+    const int rc = tgnx_tgn_apply_rows_update(cfg, buf, rows, nrows, stream);
+    if (rc) return rc;
+  }
+  const AdvArgs a{split_lo, split_hi, batch, rank, world, base_seed};
+  return train_step_impl(cfg, buf, 1, dropout, stream, false, &a, prefetched ? 1 : 2, parity);
 }
 
 int tgnx_tgn_train_fwd_bwd_split(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,

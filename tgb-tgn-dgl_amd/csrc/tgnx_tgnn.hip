@@ -148,6 +148,7 @@ struct Ctx {
   float *params, *grads, *am, *av;
   int64_t* ctl;
   float *out_pos, *out_neg;
+  float* out_ev;  // optional: train logits by event row [nev, 2] (pos, neg), the epoch's log
   double* mrr;
   int4* nodemap;
   // workspace
@@ -1366,6 +1367,11 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
     c.seg_g[2 * nloc + i - lo] = gn;
     c.out_pos[i] = zp;
     c.out_neg[i] = zn;
+    if (c.out_ev) {
+      const int64_t e = c.ctl[TGNX_CTL_BATCH_START] + i;
+      c.out_ev[2 * e] = zp;
+      c.out_ev[2 * e + 1] = zn;
+    }
     ev[8 * D + 0] = dzp;
     ev[8 * D + 1] = dzn;
     ev[8 * D + 2] = li;
@@ -1828,6 +1834,7 @@ static int make_ctx(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* b, int
   c.av = b->adam_v;
   c.ctl = b->ctl;
   c.out_pos = b->out_pos;
+  c.out_ev = b->out_ev;
   c.out_neg = b->out_neg;
   c.mrr = b->mrr;
   c.nodemap = reinterpret_cast<int4*>(b->node_map);

@@ -12,16 +12,27 @@
 //   tcsr_build / tcsr_sample                 TGL's ext_full.npz + recent sampler (utils.py:73, README.md:2-5)
 //   gemm_f32                                 the modules' Linear contractions on the MFMA GEMM
 #include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <initializer_list>
 #include <tuple>
 
 #include "../../include/tgnx.h"
 
 namespace {
 
+// the current stream OF THE CURRENT DEVICE: every op first makes its tensors' device current (a device guard,
+// restored on return), so the launch goes to that device's stream with that device's pointers
 void* cur_stream() { return reinterpret_cast<void*>(c10::hip::getCurrentHIPStream().stream()); }
+
+// every device tensor of an op on one device (the one its guard selects)
+void same_device(const at::Tensor& ref, std::initializer_list<const at::Tensor*> xs) {
+  for (const at::Tensor* x : xs)
+    TORCH_CHECK(x->device() == ref.device(), "tgnx: all tensors of an op must be on one device: ", ref.device(),
+                " and ", x->device());
+}
 
 void check_rc(int rc, const char* what) {
   TORCH_CHECK(rc == TGNX_OK, what, " failed (", rc, "): ", tgnx_last_error());
@@ -45,6 +56,8 @@ void ring_reset(at::Tensor eid, at::Tensor t) {
   dev_tensor(eid, at::kLong, "e_id");
   dev_tensor(t, at::kFloat, "t");
   TORCH_CHECK(eid.dim() == 2 && t.sizes() == eid.sizes(), "ring tensors must be [num_nodes, size]");
+  same_device(eid, {&t});
+  const c10::OptionalDeviceGuard guard(eid.device());
   check_rc(tgnx_ring_reset(eid.data_ptr<int64_t>(), t.data_ptr<float>(), eid.size(0), (int32_t)eid.size(1),
                            cur_stream()),
            "tgnx_ring_reset");
@@ -56,6 +69,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> ring_sample(const at:
   ring_state(nbr, eid, t);
   dev_tensor(assoc, at::kLong, "assoc");
   dev_tensor(n_id, at::kLong, "n_id");
+  same_device(nbr, {&eid, &t, &assoc, &n_id});
+  const c10::OptionalDeviceGuard guard(nbr.device());
   const int64_t N = nbr.size(0), K = nbr.size(1), q = n_id.numel();
   TORCH_CHECK(assoc.numel() == N, "assoc must have num_nodes entries");
   const int64_t cap_n = std::max<int64_t>(q * (1 + K), 1), cap_e = std::max<int64_t>(q * K, 1);
@@ -83,6 +98,8 @@ void ring_insert(at::Tensor nbr, at::Tensor eid, at::Tensor t, const at::Tensor&
   dev_tensor(dst, at::kLong, "dst");
   dev_tensor(ev_t, at::kFloat, "ev_t");
   dev_tensor(assoc, at::kLong, "assoc");
+  same_device(nbr, {&eid, &t, &src, &dst, &ev_t, &assoc});
+  const c10::OptionalDeviceGuard guard(nbr.device());
   const int64_t B = src.numel();
   TORCH_CHECK(dst.numel() == B && ev_t.numel() == B, "src, dst, ev_t must have the same length");
   TORCH_CHECK(B <= tgnx_ring_insert_max_batch(), "batch ", B, " > ", tgnx_ring_insert_max_batch());
@@ -96,6 +113,8 @@ at::Tensor neg_sample(const at::Tensor& dst_nodes, const at::Tensor& pos, int64_
   dev_tensor(dst_nodes, at::kLong, "dst_nodes");
   dev_tensor(pos, at::kLong, "pos");
   TORCH_CHECK(dst_nodes.numel() > 0, "empty destination set");
+  same_device(dst_nodes, {&pos});
+  const c10::OptionalDeviceGuard guard(dst_nodes.device());
   at::Tensor out = at::empty_like(pos);
   check_rc(tgnx_neg_sample(dst_nodes.data_ptr<int64_t>(), dst_nodes.numel(), pos.data_ptr<int64_t>(), pos.numel(),
                            (uint64_t)seed, (uint64_t)offset, out.data_ptr<int64_t>(), cur_stream()),
@@ -121,6 +140,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, bool> tcsr_build(cons
   dev_tensor(src, at::kLong, "src");
   dev_tensor(dst, at::kLong, "dst");
   dev_tensor(t, at::kFloat, "t");
+  same_device(src, {&dst, &t});
+  const c10::OptionalDeviceGuard guard(src.device());
   const int64_t E = src.numel(), nnz = add_reverse ? 2 * E : E;
   auto lopt = src.options();
   at::Tensor indptr = at::empty({num_nodes + 1}, lopt), indices = at::empty({std::max<int64_t>(nnz, 1)}, lopt);
@@ -149,6 +170,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> tcsr_sample(const at:
   dev_tensor(roots, at::kLong, "roots");
   TORCH_CHECK(mode == 0 || mode == 1, "mode 0 (event-id cutoff) or 1 (time cutoff)");
   dev_tensor(cut, mode == 0 ? at::kLong : at::kFloat, "cut");
+  same_device(indptr, {&indices, &eid, &ts, &roots, &cut});
+  const c10::OptionalDeviceGuard guard(indptr.device());
   const int64_t Q = roots.numel();
   TORCH_CHECK(cut.numel() == Q, "one cutoff per root");
   auto lopt = roots.options();
@@ -168,6 +191,8 @@ at::Tensor gemm_f32(const at::Tensor& A, const at::Tensor& B, const c10::optiona
   dev_tensor(A, at::kFloat, "A");
   dev_tensor(B, at::kFloat, "B");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "A and B must be 2-D");
+  same_device(A, {&B});
+  const c10::OptionalDeviceGuard guard(A.device());
   const int64_t M = trans_a ? A.size(1) : A.size(0), K = trans_a ? A.size(0) : A.size(1);
   const int64_t KB = trans_b ? B.size(1) : B.size(0), N = trans_b ? B.size(0) : B.size(1);
   TORCH_CHECK(K == KB, "inner dimensions differ: ", K, " vs ", KB);
@@ -175,6 +200,7 @@ at::Tensor gemm_f32(const at::Tensor& A, const at::Tensor& B, const c10::optiona
   if (bias.has_value()) {
     dev_tensor(*bias, at::kFloat, "bias");
     TORCH_CHECK(bias->numel() == N, "bias must have N entries");
+    same_device(A, {&*bias});
     bp = bias->data_ptr<float>();
   }
   at::Tensor C = at::empty({M, N}, A.options());

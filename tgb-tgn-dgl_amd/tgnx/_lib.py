@@ -50,6 +50,8 @@ SIGNATURES = {
                                                          c_vp]),
     "tgnx_tgn_apply_rows_update": (ctypes.c_int, [P, P, P, c_i64, c_vp]),
     "tgnx_tgn_train_fwd_bwd_split": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64, c_i32, c_i32, c_vp]),
+    "tgnx_tgn_train_fwd_bwd_pp": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64, c_i32, c_i32, c_i32,
+                                                  c_i32, P, c_i64, c_vp]),
     "tgnx_tgn_scan_next": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64, c_vp]),
     "tgnx_tgn_eval_step": (ctypes.c_int, [P, P, c_i32, c_vp]),
     "tgnx_tgn_flush": (ctypes.c_int, [P, P, P, ctypes.c_size_t, c_vp]),

@@ -33,21 +33,29 @@ from .tgb_io import load_tgb, uniform_negatives
 # sections of the configs parse_config returned, by the identity of their gnn section: the reference's
 # script passes only gnn_param to getModel (pyg-mem-tgn.py:36,49), so pyg_model_utils.getModel finds the
 # memory / sampling / train sections of the same file through it (memory.mail_combine, memory_update)
-_PARSED = {}
+
+
+class GnnSection(dict):
+    """The `gnn` section parse_config returns: a plain dict that also carries its file's sibling sections
+    (sampling, memory, train), so that getModel(..., gnn_param=gnn) as pyg-mem-tgn.py:49 calls it can honour
+    mail_combine / memory_update / neighbor / batch_size.  Explicit getModel keywords override them; a copy
+    made with dict(gnn) carries only the gnn keys."""
+    __slots__ = ("sections",)
 
 
 def parse_config(f):
     """utils.py:17-23."""
     with open(f, "r") as fh:
         conf = yaml.safe_load(fh)
-    out = conf["sampling"][0], conf["memory"][0], conf["gnn"][0], conf["train"][0]
-    _PARSED[id(out[2])] = out
+    gnn = GnnSection(conf["gnn"][0])
+    out = conf["sampling"][0], conf["memory"][0], gnn, conf["train"][0]
+    gnn.sections = out
     return out
 
 
 def config_of(gnn_param):
     """(sampling, memory, gnn, train) of the parse_config call that returned this gnn section, or None."""
-    got = _PARSED.get(id(gnn_param))
+    got = getattr(gnn_param, "sections", None)
     return got if got is not None and got[2] is gnn_param else None
 
 

@@ -26,7 +26,8 @@ class TgnnBuffers(ctypes.Structure):
     _fields_ = [("ev_src", P), ("ev_dst", P), ("ev_t", P), ("ev_blk", P), ("ev_msg", P), ("neg", P),
                 ("dst_nodes", P), ("n_dst", ctypes.c_int64), ("feat", P), ("nbr", P), ("eid", P), ("rt", P),
                 ("assoc", P), ("time_assoc", P), ("memory", P), ("params", P), ("grads", P), ("adam_m", P),
-                ("adam_v", P), ("ctl", P), ("out_pos", P), ("out_neg", P), ("mrr", P), ("ws", P), ("node_map", P)]
+                ("adam_v", P), ("ctl", P), ("out_pos", P), ("out_neg", P), ("mrr", P), ("ws", P), ("node_map", P),
+                ("out_ev", P)]
 
 
 
@@ -68,6 +69,7 @@ class TgnnEngine:
         else:
             self.adam_m, self.adam_v = optimizer.exp_avg, optimizer.exp_avg_sq
         self._neg_scratch = None
+        self.out_ev = None    # optional per-event train-logit log (tgnx_tgnn_buffers.out_ev)
 
     # ------------------------------------------------------------------ plumbing
     def _buffers(self, src, dst, t, blk, msg, neg) -> TgnnBuffers:
@@ -83,6 +85,7 @@ class TgnnEngine:
         b.params, b.grads, b.adam_m, b.adam_v = _p(m.flat), _p(m.grad_flat), _p(self.adam_m), _p(self.adam_v)
         b.ctl, b.out_pos, b.out_neg, b.mrr = _p(self.ctl), _p(self.out_pos), _p(self.out_neg), _p(self.mrr)
         b.ws, b.node_map = _p(self.ws), _p(self.node_map)
+        b.out_ev = _p(self.out_ev)
         return b
 
     def _stream(self):

@@ -57,7 +57,7 @@ class TgnBuffers(ctypes.Structure):
                 ("n_dst", ctypes.c_int64), ("nbr", P), ("eid", P), ("rt", P), ("assoc", P), ("memory", P),
                 ("last_update", P), ("store", P), ("node_gen", P), ("params", P), ("grads", P), ("adam_m", P),
                 ("adam_v", P), ("ctl", P), ("out_pos", P), ("out_neg", P), ("mrr", P), ("ws", P), ("xrows", P),
-                ("xcap", ctypes.c_int64)]
+                ("xcap", ctypes.c_int64), ("out_ev", P)]
 
 
 # the memory modules' updater cell: TGNMemory.memory_updater (memory_module.py:70-78, memory_updater_cell
@@ -286,6 +286,7 @@ class TgnEngine:
         self.out_pos = torch.zeros(cfg.max_batch, dtype=torch.float32, device=self.dev)
         self.out_neg = torch.zeros(cfg.max_batch * max(cfg.max_neg, 1), dtype=torch.float32, device=self.dev)
         self.mrr = torch.zeros(cfg.max_batch, dtype=torch.float64, device=self.dev)
+        self.out_ev = None    # optional per-event train-output log (log_outputs)
         self.dst_nodes = None if dst_nodes is None else torch.as_tensor(dst_nodes).to(self.dev, torch.long).contiguous()
         self.seed, self.rank, self.world = int(seed), int(rank), int(world)
         self.fuse_adam = True
@@ -308,6 +309,10 @@ class TgnEngine:
         self._parity = 0
         self._prefetched = False
         self._prefetch_version = None
+        # data-parallel parity-set steps (tgnx_tgn_train_fwd_bwd_pp): the exchanged rows + Adam of step k run at
+        # the head of step k + 1's graph; `_apply_pending` = the last step's exchange is not applied yet
+        # (finish() applies it eagerly: before reading memory / parameters / the loss, and before any other call)
+        self._apply_pending = False
         if optimizer is None:
             self.adam_m, self.adam_v = torch.zeros_like(model.flat), torch.zeros_like(model.flat)
         else:
@@ -361,12 +366,14 @@ class TgnEngine:
         b.params, b.grads, b.adam_m, b.adam_v = _p(m.flat), _p(m.grad_flat), _p(self.adam_m), _p(self.adam_v)
         b.ctl, b.out_pos, b.out_neg, b.mrr, b.ws = _p(self.ctl), _p(self.out_pos), _p(self.out_neg), _p(self.mrr), _p(self.ws)
         b.xrows, b.xcap = _p(self.xrows), (0 if self.xrows is None else self.xcap)
+        b.out_ev = _p(self.out_ev)
         return b
 
     def _stream(self):
         return _lib.stream(self.dev)
 
     def advance(self, batch_start: int, B: int, train: bool):
+        self.finish()
         self._prefetched = False
         _lib.call("tgnx_tgnn_advance", _p(self.ctl), 0, batch_start, B, batch_start, 0, 0, 1, self.rank, self.world,
                   self.seed, 1 if train else 0, self._stream())
@@ -374,6 +381,7 @@ class TgnEngine:
     # ------------------------------------------------------------------ state
     def reset_state(self):
         """memory_module.reset_state + neighbor_loader.reset_state (pyg_epoch_utils.py:15-16)."""
+        self.finish()
         self._prefetched = False
         b = self._buffers(0)
         _lib.call("tgnx_tgn_reset_state", ctypes.byref(self.cfg), ctypes.byref(b), self._stream())
@@ -381,14 +389,15 @@ class TgnEngine:
 
     def flush(self):
         """TGNMemory.train(False) (memory_module.py:209-215)."""
+        self.finish()
         self._prefetched = False
         b = self._buffers(0)
         nb = int(_lib.lib().tgnx_tgn_flush_scratch_bytes(ctypes.byref(self.cfg)))
-        # graphs beyond one workspace chunk: a snapshot of memory / last_update, freed after the call
+        # graphs beyond one workspace chunk: a snapshot of memory / last_update.  It is allocated on, and
+        # the flush runs on, the current stream, so the caching allocator reuses the block only for work
+        # queued after the flush: it may go out of scope when this call returns
         scratch = torch.empty(max(nb, 16), dtype=torch.uint8, device=self.dev) if nb else None
         _lib.call("tgnx_tgn_flush", ctypes.byref(self.cfg), ctypes.byref(b), _p(scratch), nb, self._stream())
-        if scratch is not None:
-            self._flush_scratch = scratch   # alive until the stream has consumed it (next flush replaces it)
 
     # ------------------------------------------------------------------ steps
     def train_batch(self, start: int, B: int, neg=None, dropout: bool = True, update: bool = True):
@@ -449,6 +458,7 @@ class TgnEngine:
     def bind_resident(self, split_lo: int, split_hi: int, batch: int, dropout: bool = True):
         """Consecutive batches of `batch` events over [split_lo, split_hi), negatives drawn on the
         device; the batch cursor lives in the control block (no host arguments change per step)."""
+        self.finish()
         self._res = (int(split_lo), int(split_hi), int(batch))
         self._res_drop = 1 if dropout else 0
         self._prefetched = False
@@ -470,15 +480,29 @@ class TgnEngine:
         return self.pipeline and self.fold_cursor and (self._res_fused or self.world > 1)
 
     def _pp(self) -> bool:
-        return self.parity_sets and self.world == 1 and self._res_fused and self.model.layers == 1 and self._pipelined()
+        """Parity-set steps: world 1 with Adam fused (tgnx_tgn_train_step_pp), or data parallel
+        (tgnx_tgn_train_fwd_bwd_pp: the previous step's exchanged rows + Adam at the head of the step); 1 hop."""
+        if not (self.parity_sets and self.model.layers == 1 and self._pipelined()):
+            return False
+        return self._res_fused if self.world == 1 else True
 
-    def _pre(self, prefetched: bool = False, parity=None):
+    def _dp_pp(self) -> bool:
+        return self.world > 1 and self._pp()
+
+    def _pre(self, prefetched: bool = False, parity=None, apply=None):
         adv, fb = self._f[:2]
         lo, hi, batch = self._res
         st = self._stream()
-        if self._pp():
+        par = self._parity if parity is None else parity
+        if self._dp_pp():
+            ap = self._apply_pending if apply is None else apply
+            rc = _lib.lib().tgnx_tgn_train_fwd_bwd_pp(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank, self.world,
+                                                     self.seed, self._res_drop, 1 if prefetched else 0, par,
+                                                     1 if ap else 0, ctypes.c_void_p(self.xgather.data_ptr()),
+                                                     ctypes.c_int64(self.xgather.shape[0]), st)
+        elif self._pp():
             rc = _lib.lib().tgnx_tgn_train_step_pp(self._cfg_ref, self._buf_ref, lo, hi, batch, self.seed, self._res_drop,
-                                                  1 if prefetched else 0, self._parity if parity is None else parity, st)
+                                                  1 if prefetched else 0, par, st)
         elif self._pipelined() and self._res_fused:
             rc = _lib.lib().tgnx_tgn_train_step_pipelined(self._cfg_ref, self._buf_ref, lo, hi, batch, self.seed,
                                                          self._res_drop, 1 if prefetched else 0, st)
@@ -507,7 +531,7 @@ class TgnEngine:
             raise RuntimeError(f"tgnx TGN resident update failed: {_lib.lib().tgnx_last_error().decode()}")
 
     def _split(self) -> bool:
-        return self.split_scan and self.world > 1 and self._pipelined() and not self._res_fused
+        return self.split_scan and self.world > 1 and self._pipelined() and not self._res_fused and not self._pp()
 
     def _scan_next(self):
         """The next batch's scan (split pipelined steps): rides beside the exchange."""
@@ -543,17 +567,45 @@ class TgnEngine:
         self._prefetch_version = getattr(self.loader, "version", None)
 
     def resident_train_step(self):
+        if self._dp_pp():   # [apply(k - 1) ‖ step k], then the exchange; its apply heads the next step
+            self._pre(self._prefetch_valid(), apply=self._apply_pending)
+            self._apply_pending = False
+            self._allreduce()
+            self._apply_pending = True
+            self._mark_prefetched()
+            self._parity ^= 1
+            return
         self._pre(self._prefetch_valid())
         self._allreduce(self._scan_next)
         self._post()
         self._mark_prefetched()
         self._parity ^= 1 if self._pp() else 0
 
+    def finish(self):
+        """Apply a data-parallel parity-set step's exchange now (tgnx_tgn_apply_rows_update: the gathered
+        memory rows and Adam) instead of at the head of the next step.  Every call that reads or rewrites the
+        state runs this first; replays then take the graph without the apply."""
+        if not self._apply_pending:
+            return
+        rc = _lib.lib().tgnx_tgn_apply_rows_update(self._cfg_ref, self._buf_ref, ctypes.c_void_p(self.xgather.data_ptr()),
+                                                  ctypes.c_int64(self.xgather.shape[0]), self._stream())
+        self._apply_pending = False
+        if rc:
+            raise RuntimeError(f"tgnx_tgn_apply_rows_update failed: {_lib.lib().tgnx_last_error().decode()}")
+
     def capture_resident(self):
         """One resident step as HIP graph(s) (world > 1: the collectives stay eager between them)."""
         torch.cuda.synchronize(self.dev)
         saved = self.ctl.clone()
-        if self.world == 1 and self._pp():   # one graph per parity, replayed alternately
+        if self._dp_pp():   # per parity, with and without the previous step's apply at its head; the collective stays eager
+            gd = {}
+            for par in (0, 1):
+                for ap in (0, 1):
+                    gd[par, ap] = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gd[par, ap]):
+                        self._pre(True, par, bool(ap))
+            self._graphs = (gd, None, None)
+        elif self.world == 1 and self._pp():   # one graph per parity, replayed alternately
             gp = (torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph())
             for par in (0, 1):
                 with torch.cuda.graph(gp[par]):
@@ -585,6 +637,14 @@ class TgnEngine:
         if self._pipelined() and not self._prefetch_valid():
             self.resident_train_step()   # marks + scans this batch first (eager), prefetches the next
             return
+        if isinstance(g1, dict):   # data-parallel parity graphs
+            g1[self._parity, 1 if self._apply_pending else 0].replay()
+            self._apply_pending = False
+            self._allreduce()
+            self._apply_pending = True
+            self._parity ^= 1
+            self._mark_prefetched()
+            return
         if isinstance(g1, tuple):   # parity graphs
             g1[self._parity].replay()
             self._parity ^= 1
@@ -601,12 +661,20 @@ class TgnEngine:
         return int(self.ctl[13]), int(self.ctl[14])
 
     def loss_sum(self) -> float:
+        self.finish()   # (the loss sum is accumulated by the Adam launch)
         return float(self.ctl[12:13].view(torch.float64).item())
+
+    ERR_BITS = {4: "batch or sampled node / edge set beyond the workspace capacity",
+                8: "more updated memory rows than the exchange slots hold (xcap)",
+                16: "stale scan-output set: tgnx_tgn_train_step_pp / _fwd_bwd_pp called with the wrong parity, "
+                    "or a prefetch that no longer holds",
+                32: "edge sort beyond its LDS counters"}
 
     def check(self):
         err = int(self.ctl[11].item())
         if err:
-            raise RuntimeError(f"tgnx TGN step error flags {err:#x} (batch or sampled set beyond capacity)")
+            why = "; ".join(m for b, m in self.ERR_BITS.items() if err & b) or "unknown"
+            raise RuntimeError(f"tgnx TGN step error flags {err:#x}: {why}")
 
 
 # config/TGN.yml memory section -> the PyG TGN's modules (TGL key names; TGN.yml:10-18)

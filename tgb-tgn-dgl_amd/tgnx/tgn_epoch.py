@@ -6,7 +6,8 @@ pyg_epoch_utils.py:9-147 carries commented out, :106-137) on the fused HIP step 
   test(model, feats, loader, neighbor_loader, neg_sampler, assoc, device, optimizer, criterion,
        evaluator, metric, split_mode) -> mean over batches of the batch MRR (epoch_utils.py:163)
 
-Per train epoch: memory.reset_state + neighbor_loader.reset_state (pyg_epoch_utils.py:15-16); per
+Per train epoch: memory.reset_state + neighbor_loader.reset_state (pyg_epoch_utils.py:15-16), then the
+bench's step (the parity-set step replayed from captured HIP graphs, TgnEngine.replay_resident); per
 batch: negatives from the destination set (NegLinkSamplerDest distribution, drawn on the device),
 memory(n_id) with the GRU update of every sampled node, TransformerConv embedding, LinkPredictor,
 BCE-with-logits on its sigmoid outputs (as the reference feeds it), update_state, ring insert,
@@ -23,7 +24,6 @@ The loaders must be tgnx SplitLoaders (tgnx.data; what utils.getDataWithDependec
 the event table is bound resident in HBM once and batches address it by global row (e_id)."""
 from __future__ import annotations
 
-import numpy as np
 import torch
 
 from .data import SplitLoader
@@ -47,41 +47,84 @@ def _engine(model, train_loader, neighbor_loader, optimizer, neg_dest_sampler=No
             dst_nodes = torch.unique(torch.as_tensor(d.dst))
         eng = TgnEngine(m, neighbor_loader, dict(src=d.src, dst=d.dst, t=d.t.float(), msg=d.msg.float()),
                         optimizer, dst_nodes=torch.as_tensor(dst_nodes), seed=getattr(neg_dest_sampler, "seed", 0))
+        # the per-event train-output log (tgnx_tgn_buffers.out_ev): every replayed step writes its batch's
+        # outputs at their event rows, so the epoch's AP / AUC need no copy per step
+        eng.out_ev = torch.zeros(eng.cfg.num_events, 2, dtype=torch.float32, device=eng.dev)
         eng._mode_train = None
+        eng._bound = None
         m._tgnx_engine = eng
     return eng
 
 
-def _ap_auc(pos: np.ndarray, neg: np.ndarray):
-    from sklearn.metrics import average_precision_score, roc_auc_score
-    y = np.concatenate([np.ones_like(pos), np.zeros_like(neg)])
-    p = np.concatenate([pos, neg])     # the sigmoid outputs (pyg_epoch_utils.py:141 applies one more)
-    return average_precision_score(y, p), roc_auc_score(y, p)
+def ap_auc_rows(pos: torch.Tensor, neg: torch.Tensor, chunk_elems: int = 1 << 26):
+    """sklearn's average_precision_score / roc_auc_score of each row's labels [1]*P + [0]*N on the scores
+    [pos | neg] (pyg_epoch_utils.py:139-143), for a [R, P] / [R, N] pair of score tensors, on their device.
+    AUC = the Mann-Whitney statistic with ties counted 1/2 (roc_auc_score's trapezoids); AP = Σ over distinct
+    thresholds of Δrecall x precision, i.e. the mean over positives of the precision at the end of their
+    tie group (average_precision_score).  Returns float64 [R] tensors (ap, auc)."""
+    R, Pn = pos.shape
+    Nn = neg.shape[1]
+    if R == 0:
+        z = torch.zeros(0, dtype=torch.float64, device=pos.device)
+        return z, z
+    step = max(1, chunk_elems // max(1, Pn * Nn))
+    aucs, aps = [], []
+    for a in range(0, R, step):
+        p, n = pos[a:a + step], neg[a:a + step]
+        gt = (p[:, :, None] > n[:, None, :]).sum((1, 2)).double()
+        eq = (p[:, :, None] == n[:, None, :]).sum((1, 2)).double()
+        aucs.append((gt + 0.5 * eq) / (Pn * Nn))
+        sc = torch.cat([p, n], 1)
+        y = torch.cat([torch.ones_like(p), torch.zeros_like(n)], 1).double()
+        order = torch.argsort(sc, dim=1, descending=True, stable=True)
+        ss, yy = sc.gather(1, order), y.gather(1, order)
+        tp = yy.cumsum(1)
+        asc = (-ss).contiguous()                                   # ascending rows
+        end = torch.searchsorted(asc, asc, right=True) - 1         # last position of each tie group
+        prec = tp.gather(1, end) / (end + 1).double()
+        aps.append((yy * prec).sum(1) / Pn)
+    return torch.cat(aps), torch.cat(aucs)
+
+
+def epoch_ap_auc(out_ev: torch.Tensor, lo: int, hi: int, B: int):
+    """Mean over the epoch's batches of the batch AP and AUC (pyg_epoch_utils.py:139-145) from the per-event
+    output log: y_pred = sigmoid of the model's sigmoid outputs, as the reference computes it."""
+    sc = torch.sigmoid(out_ev[lo:hi])
+    n = hi - lo
+    full = n // B
+    ap, auc = ap_auc_rows(sc[:full * B, 0].view(full, B), sc[:full * B, 1].view(full, B))
+    if n > full * B:
+        a2, u2 = ap_auc_rows(sc[full * B:, 0].view(1, -1), sc[full * B:, 1].view(1, -1))
+        ap, auc = torch.cat([ap, a2]), torch.cat([auc, u2])
+    return float(ap.mean()), float(auc.mean())
 
 
 def train(model, feats, train_loader, neighbor_loader, neg_dest_sampler, assoc, device, optimizer, criterion):
+    """One train epoch as the benchmark runs it: the split bound resident, then the parity-set step replayed
+    from its captured graphs batch after batch (TgnEngine.replay_resident; the first step of the epoch runs
+    eagerly and prefetches the next), negatives drawn on the device, outputs logged per event."""
     eng = _engine(model, train_loader, neighbor_loader, optimizer, neg_dest_sampler)
-    eng.reset_state()                                     # pyg_epoch_utils.py:15-16
+    B = train_loader.batch_size
+    key = (train_loader.lo, train_loader.hi, B)
+    if eng._bound != key:
+        eng.bind_resident(train_loader.lo, train_loader.hi, B, dropout=True)
+        eng._bound = key
+        eng._graphs = None
+    eng.begin_epoch()                                     # pyg_epoch_utils.py:15-16 (+ the batch cursor)
     eng._mode_train = True
     loss0 = eng.loss_sum()
-    B = train_loader.batch_size
-    outs = []
-    for s in range(train_loader.lo, train_loader.hi, B):
-        n = min(train_loader.hi, s + B) - s
-        pos, neg = eng.train_batch(s, n)
-        outs.append(torch.stack([pos.clone(), neg.clone()]))
+    if getattr(eng, "_graphs", None) is None:
+        eng.capture_resident()
+    for _ in range(len(train_loader)):
+        eng.replay_resident()
+    eng.finish()
     neighbor_loader.cur_e_id = train_loader.hi
-    torch.cuda.synchronize(eng.dev)
+    loss = eng.loss_sum() - loss0                         # (synchronises)
     eng.check()
-    aps, aucs = [], []
-    for o in outs:
-        o = o.cpu().numpy()
-        ap, auc = _ap_auc(o[0], o[1])
-        aps.append(ap)
-        aucs.append(auc)
-    if aps:
-        print("ap and auc: ", float(np.mean(aps)), float(np.mean(aucs)))
-    return eng.loss_sum() - loss0
+    if train_loader.hi > train_loader.lo:
+        ap, auc = epoch_ap_auc(eng.out_ev, train_loader.lo, train_loader.hi, B)
+        print("ap and auc: ", ap, auc)
+    return loss
 
 
 @torch.no_grad()
