@@ -448,6 +448,7 @@ def run_tgn(args, world, rank, dev):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    eng.finish()          # data-parallel parity-set steps: the last step's exchanged rows + Adam (else a no-op)
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -475,6 +476,7 @@ def run_tgn(args, world, rank, dev):
         pe0, pm0 = eng.units()
         for _ in range(args.probe_steps):
             step(eager=True)
+        eng.finish()
         barrier()
         ms, n = ctypes.c_double(), ctypes.c_int64()
         _lib.call("tgnx_probe_read", ctypes.byref(ms), ctypes.byref(n))
@@ -546,13 +548,25 @@ def run_tgn(args, world, rank, dev):
     val = {"mrr": round(float(torch.stack(rrs).mean()), 5), "batches": nval, "negatives": int(shape.num_neg_eval),
            "events_per_s": round(nval * Be / tv, 1), "note": "synthetic stream, mid-epoch state; "
            "eval-path smoke at full size (MRR parity vs the oracle: tests/test_gpu_tgn*.py)"}
-    cpu = cpu1 = None
+    cpu = cpu1 = cpu_tgn2000 = loop = tcsr = None
     _log("tgn: eval pass done")
+    headline = args.dataset == "tgbl-wiki" and args.layers == 1 and args.aggr == "last" and args.updater == "gru"
+    if rank == 0 and world == 1 and headline and not args.no_train_loop:
+        loop = train_loop_rate(args, dev, value)
+    if rank == 0 and world == 1 and not args.no_tcsr:
+        tcsr = tcsr_sampler_bench(args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_tgn(stream, Bg, aggr=args.aggr, layers=args.layers)
-        if args.dataset == "tgbl-wiki" and args.layers == 1 and args.aggr == "last" and Bg != 2000:
-            cpu1 = cpu_baseline_tgn(stream, 2000)      # BASELINE config #1: config/TGN.yml batch_size 2000
-            cpu1["config"] = "BASELINE #1: tgbl-wiki TGN.yml (batch 2000) on the CPU, one epoch"
+        if headline and Bg != 2000:
+            # BASELINE #1 as written: config/TGN.yml (batch_size 2000) through pyg-mem-tgn.py, whose import block
+            # (:19, :24) runs the DGL TGNN dependency-block loop (model_utils.py:61-159) — its oracle restatement
+            cpu1 = cpu_baseline(stream, 2000, budget_s=25.0, max_batches=12)
+            cpu1["config"] = ("BASELINE #1: tgbl-wiki, config/TGN.yml batch_size 2000, the path pyg-mem-tgn.py runs "
+                              "(TGNN block loop, epoch_utils.train), CPU; sampled batches, epoch extrapolated")
+            # the TGN memory-path oracle at TGN.yml's batch (the headline model on the CPU; NOT config #1's model)
+            cpu_tgn2000 = cpu_baseline_tgn(stream, 2000)
+            cpu_tgn2000["config"] = ("TGN memory-path oracle (the headline model) at config/TGN.yml's batch_size "
+                                     "2000, one epoch on the CPU — not BASELINE #1's model (that is the TGNN loop)")
     return {
         "metric": _metric(args.dataset, "tgn"),
         "value": round(value, 1),
@@ -584,9 +598,95 @@ def run_tgn(args, world, rank, dev):
         "kernels_gbs": {k: round(v["gbs"], 1) for k, v in probes.items() if v["gbs"]},
         "cpu_baseline": cpu,
         "cpu_baseline_config1": cpu1,
+        "cpu_baseline_tgn_b2000": cpu_tgn2000,
+        "train_loop": loop,
+        "tcsr_sampler": tcsr,
         "val_eval_gpu": val,
         "loss_sum": round(loss, 4),
     }
+
+
+def train_loop_rate(args, dev, engine_value, epochs=3):
+    """SURVEY §8(d)'s metric as defined: train-split events per second of the `train` loop that the reference
+    script calls (pyg-mem-tgn.py:57 -> pyg_epoch_utils.train, here tgnx/tgn_epoch.train after the one-line
+    model-import swap), on the full synthetic tgbl-wiki-shaped stream, batch --batch, one GPU.  Each epoch
+    is timed whole (reset, the graph replays, the loss read-back and the AP / AUC display); epoch 1 also
+    captures the step graphs.  The reported value is the best later epoch."""
+    import pyg_epoch_utils as pe
+    import pyg_model_utils as pm
+    from tgnx.data import getDataWithDependecyBlock
+    from tgnx.neg import NegLinkSamplerDest
+    from tgnx.sampler import LastNeighborLoader
+    os.environ.setdefault("TGNX_EVAL_NEGS", "10")     # (no eval here; keeps the unused negative lists small)
+    B = args.batch
+    data, tr, va, te, ns, ev, metric = getDataWithDependecyBlock(args.dataset, {"batch_size": B})
+    d, N = data.msg.shape[1], data.num_nodes
+    torch.manual_seed(0)
+    model = pm.getModel(d, 100, N, dev, ring=10, max_batch=B, dropout=0.0 if args.no_dropout else 0.1)
+    opt = pm.getOptimizer(model, 1e-4)
+    nl = LastNeighborLoader(N, 10, device=dev)
+    nds = NegLinkSamplerDest(torch.unique(data.dst), device=dev)
+    crit = torch.nn.BCEWithLogitsLoss()
+    times, losses = [], []
+    import contextlib
+    import io
+    for ep in range(epochs):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()) as out:   # (its "ap and auc:" line; kept below)
+            losses.append(pe.train(model, data.msg, tr, nl, nds, None, dev, opt, crit))
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+        _log(f"train loop epoch {ep + 1}: {times[-1] * 1e3:.1f} ms, loss {losses[-1]:.2f}")
+    n = tr.hi - tr.lo
+    best = n / min(times[1:])
+    return {"value": round(best, 1), "unit": "events/s", "events_per_epoch": n, "batch": B,
+            "epoch_s": [round(t, 5) for t in times], "loss_sum": [round(x, 3) for x in losses],
+            "ap_auc_line": out.getvalue().strip(), "ratio_to_engine_value": round(best / engine_value, 4),
+            "note": "pyg_epoch_utils.train (tgnx/tgn_epoch.train) timed whole per epoch, best of epochs 2..; "
+                    "epoch 1 includes the graph capture"}
+
+
+def tcsr_sampler_bench(args, K=10, reps=20):
+    """The north star's t-CSR temporal sampler (csrc/tgnx_tcsr.hip tgnx_tcsr_sample): for every event of the
+    train split, its two endpoints' K most recent neighbours before the event (event-id cutoff = the
+    LastNeighborLoader ring row at that event), over the whole t-CSR of the stream — TGL's per-edge sampling
+    pass over an epoch.  Timed with HIP events around `reps` launches.  Algorithmic bytes per root: root id 8 +
+    cutoff 8 + indptr pair 16 + the binary search's ceil(log2(deg + 1)) eids (8 B each) + the window's c <= K
+    entries read (indices 8 + eid 8 + ts 4) + K outputs written (20 B each) + count 4."""
+    from tgnx.synth import SHAPES, make_stream
+    from tgnx.tcsr import TCSR
+    out = {}
+    for name, nev in (("tgbl-wiki", None), ("tgbl-comment", 8_000_000)):
+        s = make_stream(SHAPES[name], seed=0, num_events=nev)
+        dev = torch.device("cuda")
+        g = TCSR.build(s.src, s.dst, s.t, s.num_nodes, device=dev)
+        E = s.train_end
+        roots = torch.from_numpy(np.concatenate([s.src[:E], s.dst[:E]])).to(dev)
+        cut = torch.arange(E, dtype=torch.long, device=dev).repeat(2)
+        nbr, eid, ts, cnt = g.sample_recent(roots, K, cut_eid=cut)
+        torch.cuda.synchronize()
+        deg = (g.indptr[roots + 1] - g.indptr[roots]).double()
+        search = torch.ceil(torch.log2(deg + 1)).sum().item() * 8
+        algo = roots.numel() * (8 + 8 + 16 + 4 + 20 * K) + search + 20 * float(cnt.sum())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            g.sample_recent(roots, K, cut_eid=cut)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        out[name] = {"roots": int(roots.numel()), "nnz": int(g.indices.numel()), "num_nodes": s.num_nodes,
+                     "events": s.num_events, "us_per_launch": round(us, 2),
+                     "roots_per_s": round(roots.numel() / (us * 1e-6), 1),
+                     "algo_bytes_per_launch": round(algo), "gbs": round(algo / (us * 1e-6) / 1e9, 1),
+                     "hbm_frac": round(algo / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+        _log(f"tcsr {name}: {us:.1f} us per launch of {roots.numel()} roots, {out[name]['gbs']} GB/s")
+        del g, roots, cut, nbr, eid, ts, cnt
+    out["note"] = ("per launch: every train event's two endpoints (Q = 2 E_train roots), K = 10, event-id cutoff; "
+                   "timed with HIP events over 20 launches (includes the allocation-free launch overhead); "
+                   "tgbl-comment-shaped at N = 994,790 with 8M events (16M t-CSR entries)")
+    return out
 
 
 def main():
@@ -608,6 +708,8 @@ def main():
     ap.add_argument("--only", action="store_true", help="skip the secondary path")
     ap.add_argument("--no-dropout", action="store_true", help="train mode without dropout")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-train-loop", action="store_true", help="skip timing the drop-in pyg_epoch_utils.train loop")
+    ap.add_argument("--no-tcsr", action="store_true", help="skip the t-CSR sampler leg")
     ap.add_argument("--probe-steps", type=int, default=100)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
     ap.add_argument("--dist-backend", default="nccl", help="rehearsal only: 'gloo' to run N>1 on one device")

@@ -18,6 +18,16 @@ Modules exercised (file:line of the code that produced each fixture):
                  can be instantiated — no DGL op is ever called)
   msg.npz        modules/msg_func.py:12-18   IdentityMessage
   link_pred.npz  modules/decoder.py:108-123  LinkPredictor (sigmoid output)
+  tgn_memory_*.npz  modules/memory_module.py:25-215 + msg_agg.py:15-26 + msg_func.py:12-18
+                 TGNMemory itself (IdentityMessage, Last / MeanAggregator, GRUCell / RNNCell): train-mode
+                 memory(n_id) and update_state over several batches, train(False) (the flush), eval-mode
+                 memory(n_id) and update_state — every returned tensor and the memory / last_update
+                 buffers after each call.  Its missing third-party imports get placeholder modules
+                 (torch_geometric.nn.inits.zeros, torch_geometric.utils.scatter, torch_scatter.scatter_max,
+                 modules.time_enc.TimeEncoder) that restate those functions' published behaviour; so the
+                 fixture pins the module's own control flow — store layout and ordering, update-vs-store
+                 order in train / eval, _compute_msg's t_rel, the flush — while the placeholder arithmetic
+                 (scatter, the time encoder) stays parity-unpinned
 """
 from __future__ import annotations
 
@@ -232,13 +242,135 @@ def capture_link_pred(seed):
                         **{"p_" + k.replace(".", "__"): v for k, v in sd.items()})
 
 
+def _install_tgn_placeholders(ref):
+    """Placeholder modules for the imports memory_module.py / msg_agg.py need beyond torch (the published
+    behaviour of: PyG zeros (fill 0), PyG scatter (sum / mean / max with 0 in empty rows), torch_scatter
+    scatter_max (argmax = src.size(0) in empty rows, the first index of the max otherwise, its CPU kernel),
+    PyG TimeEncoder (cos(Linear(1, D)(t)))).  Returns the imported reference modules."""
+    tg = types.ModuleType("torch_geometric")
+    tg_nn = types.ModuleType("torch_geometric.nn")
+    tg_inits = types.ModuleType("torch_geometric.nn.inits")
+    tg_utils = types.ModuleType("torch_geometric.utils")
+
+    def zeros(value):
+        if value is not None:
+            value.data.fill_(0)
+
+    def scatter(src, index, dim=0, dim_size=None, reduce="sum"):
+        assert dim == 0
+        n = int(index.max()) + 1 if dim_size is None else dim_size
+        shape = (n,) + tuple(src.shape[1:])
+        idx = index.view(-1, *([1] * (src.dim() - 1))).expand_as(src)
+        if reduce in ("sum", "add"):
+            return src.new_zeros(shape).scatter_add(0, idx, src)
+        if reduce == "mean":
+            tot = src.new_zeros(shape).scatter_add(0, idx, src)
+            cnt = torch.zeros(n, dtype=src.dtype).scatter_add(0, index, torch.ones(index.shape[0], dtype=src.dtype))
+            return tot / cnt.clamp(min=1).view(-1, *([1] * (src.dim() - 1)))
+        if reduce == "max":
+            return src.new_zeros(shape).scatter_reduce(0, idx, src, reduce="amax", include_self=False)
+        raise ValueError(reduce)
+
+    tg_inits.zeros = zeros
+    tg_utils.scatter = scatter
+    tg.nn, tg_nn.inits, tg.utils = tg_nn, tg_inits, tg_utils
+    ts = types.ModuleType("torch_scatter")
+
+    def scatter_max(src, index, dim=0, dim_size=None):
+        assert dim == 0 and src.dim() == 1
+        n = int(index.max()) + 1 if dim_size is None else dim_size
+        out = src.new_zeros(n).scatter_reduce(0, index, src, reduce="amax", include_self=False)
+        arg = torch.full((n,), src.shape[0], dtype=torch.long)
+        hit = src == out[index]
+        arg = arg.scatter_reduce(0, index[hit], torch.arange(src.shape[0])[hit], reduce="amin", include_self=True)
+        return out, arg
+
+    ts.scatter_max = scatter_max
+    for name, mod in (("torch_geometric", tg), ("torch_geometric.nn", tg_nn), ("torch_geometric.nn.inits", tg_inits),
+                      ("torch_geometric.utils", tg_utils), ("torch_scatter", ts)):
+        sys.modules[name] = mod
+    import modules  # noqa: F401  (the reference's namespace package)
+    te = types.ModuleType("modules.time_enc")
+
+    class TimeEncoder(torch.nn.Module):
+        def __init__(self, out_channels):
+            super().__init__()
+            self.out_channels = out_channels
+            self.lin = torch.nn.Linear(1, out_channels)
+
+        def reset_parameters(self):
+            self.lin.reset_parameters()
+
+        def forward(self, t):
+            return self.lin(t.view(-1, 1)).cos()
+
+    te.TimeEncoder = TimeEncoder
+    sys.modules["modules.time_enc"] = te
+    from modules import memory_module, msg_agg, msg_func
+    return memory_module, msg_agg, msg_func
+
+
+def capture_tgn_memory(ref, aggr, updater, seed, N=40, d=5, D=8, B=12, n_train=5, n_eval=2):
+    """TGNMemory (modules/memory_module.py:25-215) driven as the canonical loop drives it: per train batch
+    memory(n_id) over the batch's nodes plus a few others (:116-124, _get_updated_memory), then
+    update_state (:126-138, train order); then train(False) (:209-215, the flush); then eval batches
+    (memory(n_id), update_state in eval order).  Timestamps strictly increase and are int64: the module
+    assigns scatter-max(t) into its long last_update buffer (:150), which refuses float32 t (the cast of
+    temporal_dataset.py:53) — PyG's TGN convention of integer times is what it runs with; nodes repeat
+    within batches."""
+    mm, ma, mf = _install_tgn_placeholders(ref)
+    torch.manual_seed(seed)
+    agg = ma.LastAggregator() if aggr == "last" else ma.MeanAggregator()
+    mem = mm.TGNMemory(N, d, D, D, mf.IdentityMessage(d, D, D), agg, memory_updater_cell=updater)
+    rng = np.random.default_rng(seed)
+    out = {f"p_{k.replace('.', '__')}": v.detach().numpy().copy() for k, v in mem.state_dict().items()
+           if not k.startswith("_") and k not in ("memory", "last_update")}
+    nb = n_train + n_eval
+    src = rng.integers(0, N, (nb, B)).astype(np.int64)
+    dst = rng.integers(0, N, (nb, B)).astype(np.int64)
+    src[:, 1] = src[:, 0]                              # a node twice in one batch (store ordering)
+    t = (np.arange(nb * B).reshape(nb, B) * 3 + 1).astype(np.int64)
+    msg = rng.random((nb, B, d), dtype=np.float32)
+    extra = rng.integers(0, N, (nb, 4)).astype(np.int64)
+    out.update(src=src, dst=dst, t=t, msg=msg, extra=extra, meta=np.array([N, d, D, B, n_train, n_eval]))
+    mem.train()
+    for b in range(nb):
+        if b == n_train:
+            mem.train(False)                            # the flush
+            out["flush_memory"] = mem.memory.detach().numpy().copy()
+            out["flush_last_update"] = mem.last_update.numpy().copy()
+        s, dd = torch.from_numpy(src[b]), torch.from_numpy(dst[b])
+        n_id = torch.cat([s, dd, torch.from_numpy(extra[b])]).unique()
+        with torch.no_grad():
+            z, lu = mem(n_id)
+            out[f"b{b}_nid"] = n_id.numpy()
+            out[f"b{b}_z"] = z.detach().numpy().copy()
+            out[f"b{b}_lu"] = lu.detach().numpy().copy()
+            mem.update_state(s, dd, torch.from_numpy(t[b]), torch.from_numpy(msg[b]))
+        out[f"b{b}_memory"] = mem.memory.detach().numpy().copy()
+        out[f"b{b}_last_update"] = mem.last_update.numpy().copy()
+        # the stores' event times per node (src / dst direction): their layout and order
+        out[f"b{b}_store_s_t"] = np.concatenate([mem.msg_s_store[j][2].numpy().astype(np.float64) for j in range(N)]
+                                                or [np.zeros(0)])
+        out[f"b{b}_store_s_n"] = np.array([mem.msg_s_store[j][2].numel() for j in range(N)])
+        out[f"b{b}_store_d_n"] = np.array([mem.msg_d_store[j][2].numel() for j in range(N)])
+    np.savez(os.path.join(HERE, f"tgn_memory_{aggr}_{updater}.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="", help="comma-separated capture names (tgn_memory, sampler, ...)")
     args = ap.parse_args()
     sys.dont_write_bytecode = True
     sys.path.insert(0, args.ref)
     torch.set_num_threads(1)
+    if args.only:
+        if "tgn_memory" in args.only.split(","):
+            for i, (aggr, upd) in enumerate((("last", "gru"), ("mean", "gru"), ("last", "rnn"))):
+                capture_tgn_memory(args.ref, aggr, upd, seed=20 + i)
+        print("goldens written to", HERE)
+        return
     capture_sampler(args.ref, "k4_mono", num_nodes=40, K=4, num_batches=12, batch=12, monotone=True, seed=1)
     capture_sampler(args.ref, "k4_shuffled_t", num_nodes=40, K=4, num_batches=10, batch=12, monotone=False,
                     seed=2)
@@ -249,6 +381,8 @@ def main():
     capture_model(7)
     capture_msg(8)
     capture_link_pred(9)
+    for i, (aggr, upd) in enumerate((("last", "gru"), ("mean", "gru"), ("last", "rnn"))):
+        capture_tgn_memory(args.ref, aggr, upd, seed=20 + i)
     print("goldens written to", HERE)
 
 

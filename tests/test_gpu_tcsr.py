@@ -40,7 +40,7 @@ def test_build_matches_oracle():
     assert ip[8] - ip[7] > 9000
 
 
-@pytest.mark.parametrize("K", [1, 10, 64, 100])
+@pytest.mark.parametrize("K", [1, 10, 16, 17, 32, 64, 100])   # (<= 16 / <= 32: the grouped kernel; more: a wave per root)
 def test_sample_matches_oracle_both_cutoffs(K):
     from oracle.tcsr_ref import gen_graph, sample_recent
     src, dst, t = _stream(seed=1)

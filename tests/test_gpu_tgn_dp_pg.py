@@ -140,6 +140,8 @@ def _worker(case, rank, world, port, lr, mode, out_dir):
                 assert err < 1e-5, (st, err)
                 assert torch.equal(mine["flat"], ref["flat"]) and torch.equal(mine["flat"], flat0), st  # lr = 0
             res["compared"].append(st)
+            if rank == 0:
+                print(f"[dp_pg {case} {mode} lr={lr}] step {st} compared", flush=True)
         if lr:
             assert not torch.equal(eng.model.flat, flat0)    # Adam moved the parameters on every rank alike
         dist.barrier()

@@ -104,3 +104,44 @@ def test_model_parameter_inventory(golden):
     for n, p in m.named_parameters():
         assert tuple(p.shape) == tuple(z[f"shape_{n}"].tolist())
     assert sum(p.numel() for p in m.parameters() if p.requires_grad) == int(z["n_trainable"][0])
+
+
+@pytest.mark.parametrize("aggr,updater", [("last", "gru"), ("mean", "gru"), ("last", "rnn")])
+def test_tgn_memory_oracle_matches_reference_module(golden, aggr, updater):
+    """oracle/tgn_ref.RefTGNMemory against the reference's own TGNMemory (modules/memory_module.py:25-215,
+    msg_agg.py, msg_func.py; tests/golden/make_goldens.py capture_tgn_memory): the same parameters, the same
+    train batches (memory(n_id), update_state in train order), train(False) (the flush), eval batches —
+    every returned memory / last_update row and both buffers after every call, plus the per-node store
+    sizes and the src-direction stores' event times in node order.  Pins the module's control flow (store
+    layout and order, update-vs-store order, t_rel, the flush); the placeholder scatter / time-encoder
+    arithmetic the reference module ran with is the oracle's own restatement (parity unpinned there)."""
+    from oracle.tgn_ref import RefTGNMemory
+    z = golden(f"tgn_memory_{aggr}_{updater}.npz")
+    N, d, D, B, n_train, n_eval = z["meta"].tolist()
+    mem = RefTGNMemory(N, d, D, D, aggr=aggr, updater=updater)
+    sd = {k[2:].replace("__", "."): torch.from_numpy(z[k]) for k in z.files if k.startswith("p_")}
+    missing = mem.load_state_dict(sd, strict=False)
+    assert not missing.unexpected_keys and set(missing.missing_keys) <= {"memory", "last_update", "_assoc"}
+    mem.train()
+    for b in range(n_train + n_eval):
+        if b == n_train:
+            mem.train(False)
+            np.testing.assert_allclose(mem.memory.numpy(), z["flush_memory"], rtol=0, atol=2e-6)
+            np.testing.assert_array_equal(mem.last_update.numpy(), z["flush_last_update"])
+        s, dd = torch.from_numpy(z["src"][b]), torch.from_numpy(z["dst"][b])
+        n_id = torch.cat([s, dd, torch.from_numpy(z["extra"][b])]).unique()
+        np.testing.assert_array_equal(n_id.numpy(), z[f"b{b}_nid"])
+        with torch.no_grad():
+            zz, lu = mem(n_id)
+            np.testing.assert_allclose(zz.numpy(), z[f"b{b}_z"], rtol=0, atol=2e-6, err_msg=f"batch {b}")
+            np.testing.assert_array_equal(lu.numpy(), z[f"b{b}_lu"])
+            mem.update_state(s, dd, torch.from_numpy(z["t"][b]), torch.from_numpy(z["msg"][b]))
+        np.testing.assert_allclose(mem.memory.numpy(), z[f"b{b}_memory"], rtol=0, atol=2e-6, err_msg=f"batch {b}")
+        np.testing.assert_array_equal(mem.last_update.numpy(), z[f"b{b}_last_update"])
+        empty = torch.empty(0)
+        st_n = np.array([mem.msg_s_store.get(j, (empty,) * 3)[2].numel() for j in range(N)])
+        np.testing.assert_array_equal(st_n, z[f"b{b}_store_s_n"])
+        np.testing.assert_array_equal(np.array([mem.msg_d_store.get(j, (empty,) * 3)[2].numel() for j in range(N)]),
+                                      z[f"b{b}_store_d_n"])
+        got_t = [mem.msg_s_store[j][2].numpy().astype(np.float64) for j in range(N) if j in mem.msg_s_store]
+        np.testing.assert_array_equal(np.concatenate(got_t or [np.zeros(0)]), z[f"b{b}_store_s_t"])

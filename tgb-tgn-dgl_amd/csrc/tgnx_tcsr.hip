@@ -19,6 +19,9 @@ namespace tgnx {
 namespace tcsr {
 
 constexpr int EID_BITS = 36;
+#ifndef TGNX_TCSR_GROUPS
+#define TGNX_TCSR_GROUPS 1  // K <= 32: G-lane groups per root (sample_recent_g); 0: a wave per root
+#endif
 
 __global__ void build_keys(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                            const float* __restrict__ t, int64_t E, int add_reverse, uint64_t* __restrict__ key,
@@ -99,6 +102,64 @@ __global__ void __launch_bounds__(256) sample_recent(const int64_t* __restrict__
       out_t[q * K + j] = ok ? ts[p] : -1.0f;
     }
     if (lane == 0 && out_cnt) out_cnt[q] = c;
+  }
+}
+
+// K <= 32: G-lane groups (G = 16 or 32), 64 / G roots per wave at once — the wave-per-root loop above left
+// 64 - K lanes idle in the window read and walked its roots one after another, each root a chain of dependent
+// loads (root -> indptr -> probes -> window).  A group's search is G-ary (ceil(log_G n) rounds: a wiki-shaped
+// user row of <= 16 entries takes one, a hub page's thousands three); the groups of a wave diverge only in
+// their round counts.  Consecutive groups take consecutive roots, so a wave's window stores are one
+// contiguous run of (64 / G) K entries.
+template <int G, class KEY>
+__device__ __forceinline__ int64_t group_lower_bound(const KEY* __restrict__ k, int64_t lo, int64_t hi, KEY cut, int gl,
+                                                     int gshift) {
+  constexpr uint64_t GM = (1ull << G) - 1ull;
+  while (hi - lo > G) {
+    const int64_t step = (hi - lo + G - 1) / G;
+    const int64_t pos = lo + (int64_t)gl * step;
+    const bool below = pos < hi && k[pos] < cut;
+    const int cnt = __popcll((__ballot(below) >> gshift) & GM);
+    if (cnt == 0) return lo;
+    const int64_t nlo = lo + (int64_t)(cnt - 1) * step + 1;
+    hi = min(hi, lo + (int64_t)cnt * step);
+    lo = nlo;
+  }
+  const int64_t pos = lo + gl;
+  const bool below = pos < hi && k[pos] < cut;
+  return lo + __popcll((__ballot(below) >> gshift) & GM);
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) sample_recent_g(const int64_t* __restrict__ indptr,
+                                                       const int64_t* __restrict__ indices,
+                                                       const int64_t* __restrict__ eid, const float* __restrict__ ts,
+                                                       int K, const int64_t* __restrict__ roots, int64_t Q, int mode,
+                                                       const int64_t* __restrict__ cut_eid, int64_t cut_eid_all,
+                                                       const float* __restrict__ cut_t, int64_t* __restrict__ out_nbr,
+                                                       int64_t* __restrict__ out_eid, float* __restrict__ out_t,
+                                                       int32_t* __restrict__ out_cnt) {
+  static_assert(G == 16 || G == 32, "group width");
+  constexpr int GPW = 64 / G;
+  const int lane = threadIdx.x & 63, gl = lane % G, grp = lane / G;
+  const int64_t stride = (int64_t)gridDim.x * 4 * GPW;
+  for (int64_t q = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * GPW + grp; q < Q; q += stride) {
+    const int64_t v = roots[q];
+    const int64_t ce = mode == 0 ? (cut_eid ? cut_eid[q] : cut_eid_all) : 0;
+    const float ct = mode == 1 ? cut_t[q] : 0.f;
+    const int64_t lo = indptr[v], hi = indptr[v + 1];
+    const int64_t b = mode == 0 ? group_lower_bound<G, int64_t>(eid, lo, hi, ce, gl, grp * G)
+                                : group_lower_bound<G, float>(ts, lo, hi, ct, gl, grp * G);
+    const int c = (int)min((int64_t)K, b - lo);
+    if (gl < K) {
+      const bool ok = gl < c;
+      const int64_t p = ok ? b - 1 - gl : lo;
+      const int64_t o = q * K + gl;
+      out_nbr[o] = ok ? indices[p] : -1;
+      out_eid[o] = ok ? eid[p] : -1;
+      out_t[o] = ok ? ts[p] : -1.0f;
+    }
+    if (gl == 0 && out_cnt) out_cnt[q] = c;
   }
 }
 
@@ -199,9 +260,21 @@ int tgnx_tcsr_sample(const int64_t* indptr, const int64_t* indices, const int64_
   TGNX_CHECK_ARG(mode == 0 || (mode == 1 && cut_t), "tgnx_tcsr_sample: mode 0 (eid < cut) or 1 (ts < cut_t[q])");
   if (Q == 0) return TGNX_OK;
   TGNX_CHECK_ARG(indptr && indices && eid && ts && roots && out_nbr && out_eid && out_t, "tgnx_tcsr_sample: null pointer");
-  const int grid = (int)std::min<int64_t>(8192, (Q + 3) / 4);
-  sample_recent<<<grid, 256, 0, as_stream(stream)>>>(indptr, indices, eid, ts, K, roots, Q, mode, cut_eid, cut_eid_all,
-                                                     cut_t, out_nbr, out_eid, out_t, out_cnt);
+  hipStream_t s = as_stream(stream);
+  if (K <= 32 && TGNX_TCSR_GROUPS) {
+    const int G = K <= 16 ? 16 : 32, per = 4 * (64 / G);
+    const int grid = (int)std::min<int64_t>(8192, (Q + per - 1) / per);
+    if (G == 16)
+      sample_recent_g<16><<<grid, 256, 0, s>>>(indptr, indices, eid, ts, K, roots, Q, mode, cut_eid, cut_eid_all, cut_t,
+                                               out_nbr, out_eid, out_t, out_cnt);
+    else
+      sample_recent_g<32><<<grid, 256, 0, s>>>(indptr, indices, eid, ts, K, roots, Q, mode, cut_eid, cut_eid_all, cut_t,
+                                               out_nbr, out_eid, out_t, out_cnt);
+  } else {
+    const int grid = (int)std::min<int64_t>(8192, (Q + 3) / 4);
+    sample_recent<<<grid, 256, 0, s>>>(indptr, indices, eid, ts, K, roots, Q, mode, cut_eid, cut_eid_all, cut_t,
+                                       out_nbr, out_eid, out_t, out_cnt);
+  }
   TGNX_LAUNCH_CHECK("tcsr_sample_recent");
   return TGNX_OK;
 }

@@ -3823,14 +3823,20 @@ static int ksplit(int K, int smin) { return std::max(smin, std::min(64, K / 2048
 #ifndef TGNX_S_LP
 #define TGNX_S_LP 10  // (one 64-deep chunk per split at B = 200: A/B 0.1010 vs 0.1022 ms with 5; dW_edge 16 and dW_proj 8 splits: ±0)
 #endif
+#ifndef TGNX_DWE_SMAX
+#define TGNX_DWE_SMAX 64  // (experiments: caps on the split counts of dW_edge / dW_gru)
+#endif
+#ifndef TGNX_DWG_SMAX
+#define TGNX_DWG_SMAX 64
+#endif
 // the deferred (split-K) weight-gradient GEMMs of a train step
-static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.Etr, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, ksplit(k.Etr, TGNX_S_WE)); }
+static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.Etr, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, std::min(TGNX_DWE_SMAX, ksplit(k.Etr, TGNX_S_WE))); }
 static GemmShape shp_dWp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.HC, k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, TGNX_S_WP)); }
 // 2 hops: conv2's projections (K = outer centres) and lin_edge (K = root edges)
 static GemmShape shp_dWp2(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(4 * k.HC, k.D + 1, k.Rtr, nullptr, nullptr, cnt ? cnt + CNT_R : nullptr, ksplit(k.Rtr, 4)); }
 static GemmShape shp_dWe2(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.E1tr, nullptr, nullptr, cnt ? cnt + CNT_E1 : nullptr, ksplit(k.E1tr, 8)); }
 static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, std::max(TGNX_S_LP, std::min(64, (3 * k.B + 63) / 64))); }
-static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, ksplit(k.Mtr, TGNX_S_WG)); }
+static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, std::min(TGNX_DWG_SMAX, ksplit(k.Mtr, TGNX_S_WG))); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, kj, kx, ke, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
       Ep, alpha, alk, Qo, Zc, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
