@@ -579,9 +579,16 @@ __host__ __device__ inline size_t tgn_scan_smem(int Bmax) {
 // every partition's entries (so each knows its key offset), compact their own entries in entry order and
 // sort only those: P sorts of ~2B / P keys in parallel instead of one of 2B (a data-parallel step plans
 // the whole global batch; sorting 3,200 keys took one workgroup 49 us).
-template <class AT>
+// where a partitioned plan writes (one parity set's keys, runs and per-partition counts / offsets)
+struct PlanOut {
+  uint64_t *rkeys, *skeys;
+  int *rruns, *sruns, *pc;  // pc: rpc | rpo | spc | spo, TGNX_PLAN_PMAX each
+};
+__host__ __device__ inline PlanOut plan_out(const Ctx& c) { return PlanOut{c.rkeys, c.skeys, c.rruns, c.sruns, c.rpc}; }
+// MAXE: entries per thread (2B <= MAXE x the workgroup size)
+template <int MAXE = 8, class AT>
 __device__ __forceinline__ void plan_part(const Ctx& c, int which, int part, int P, int B, int64_t start, unsigned char* smem, int* sh,
-                          AT at) {
+                          AT at, const PlanOut& po) {
   const int tid = threadIdx.x, T = blockDim.x, n2 = 2 * B;
   const int64_t* src = c.ev_src + start;
   const int64_t* dst = c.ev_dst + start;
@@ -607,7 +614,6 @@ __device__ __forceinline__ void plan_part(const Ctx& c, int which, int part, int
   uint64_t* tmp = reinterpret_cast<uint64_t*>(smem + (size_t)next_pow2(n2) * 8 + (size_t)(n2 + 2) * 4 + 8);
   // entries p = tid + j T (all loads of a thread in flight at once); a partition's keys are compacted in
   // any order (wave-aggregated LDS slots): the keys are distinct, so the sort fixes their order
-  constexpr int MAXE = 8;  // 2B <= 8192 at T = 1024
   int64_t v[MAXE];
 #pragma unroll
   for (int j = 0; j < MAXE; ++j) v[j] = node_of(min(tid + j * T, n2 - 1));  // unconditional (clamped) loads
@@ -681,14 +687,14 @@ __device__ __forceinline__ void plan_part(const Ctx& c, int which, int part, int
   for (int p = p0; p < p1; ++p)
     if (p == 0 || (key[p] >> sh_run) != (key[p - 1] >> sh_run)) runs[rid++] = p;
   __syncthreads();
-  uint64_t* gk = which == 0 ? c.rkeys : c.skeys;
-  int* gr = (which == 0 ? c.rruns : c.sruns) + off + part;
+  uint64_t* gk = which == 0 ? po.rkeys : po.skeys;
+  int* gr = (which == 0 ? po.rruns : po.sruns) + off + part;
   for (int p = tid; p < nk; p += T) gk[off + p] = key[p];
   for (int r = tid; r < U; r += T) gr[r] = off + runs[r];
   if (tid == 0) {
     gr[U] = off + nk;
-    (which == 0 ? c.rpc : c.spc)[part] = U;
-    (which == 0 ? c.rpo : c.spo)[part] = off;
+    po.pc[(which == 0 ? 0 : 2) * TGNX_PLAN_PMAX + part] = U;
+    po.pc[(which == 0 ? 1 : 3) * TGNX_PLAN_PMAX + part] = off;
   }
 }
 template <class AT>
@@ -697,7 +703,7 @@ __device__ __forceinline__ void plan_blocks(const Ctx& c, int which, int B, int6
   // world-1 batch): the single-workgroup plans (their keys come straight from the events, no compaction)
   const int P = c.pplan;
   if (P > 1) {
-    plan_part(c, which < P ? 0 : 1, which % P, P, B, start, smem, sh, at);
+    plan_part(c, which < P ? 0 : 1, which % P, P, B, start, smem, sh, at, plan_out(c));
   } else if (which == 0) {
     const int tid = threadIdx.x, T = blockDim.x;
     uint64_t* key;
@@ -2181,8 +2187,19 @@ __device__ void edge_sort_body(const Ctx& c, int* cntr, int cap) {
   }
 }
 
+// the NEXT batch's partitioned plans (data-parallel steps whose global batch's plans do not fit the dW_cell
+// launch's LDS): plan workgroup `role` (0 .. 2 pplan) into the other parity set (po), batch one past the
+// counters; up to 2 x 2048 keys at 256 threads (MAXE 16)
+constexpr int PRED_PLAN_MAXE = 16;
+__device__ __forceinline__ void pred_plan_body(const Ctx& c, int role, const PlanOut& po, unsigned char* smem) {
+  __shared__ int sh[40];
+  const ResDesc d = res_desc(c, 1);
+  if (d.B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int P = c.pplan;
+  plan_part<PRED_PLAN_MAXE>(c, role < P ? 0 : 1, role % P, P, d.B, d.start, smem, sh, NoCheckpoint{}, po);
+}
 template <bool ATT>
-__global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt) {
+__global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, PlanOut po, int npl) {
   TGNX_STAMP(5);
   extern __shared__ __attribute__((aligned(16))) float Wl[];  // [2][D][DP]: lin_src, lin_dst
   __shared__ __attribute__((aligned(16))) float z[3][TDMAX];
@@ -2196,6 +2213,10 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt) 
   }
   if ((int)blockIdx.x >= (int)gridDim.x - nmk - nsrt) {
     edge_sort_body(c, reinterpret_cast<int*>(Wl), (int)(tgn_pred_smem(c.D) / 4));
+    return;
+  }
+  if ((int)blockIdx.x >= (int)gridDim.x - nmk - nsrt - npl) {
+    pred_plan_body(c, (int)blockIdx.x - ((int)gridDim.x - nmk - nsrt - npl), po, reinterpret_cast<unsigned char*>(Wl));
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -3584,6 +3605,9 @@ struct MarkNextJob {
 #ifndef TGNX_MD_CAP
 #define TGNX_MD_CAP 512  // grid cap of the step's M x D GEMMs (dz0, dX_enc): 7 column tiles at D = 100, ~30 row tiles at B = 200 (A/B 0.0966 vs 0.0971 ms with 1024)
 #endif
+#ifndef TGNX_PLANS_IN_PRED
+#define TGNX_PLANS_IN_PRED 1  // parity-set steps with partitioned plans: the plans in the predictor launch (0: own scan launch)
+#endif
 #ifndef TGNX_SCAN_AT
 #define TGNX_SCAN_AT 7  // parity step: the launch the next batch's scan rides in (7: dW_gru; 6: dz0, 0.1005 vs 0.0965 ms)
 #endif
@@ -3647,6 +3671,8 @@ __device__ void scan_body(const Ctx& c, int role, unsigned char* smem, AT at, in
 // the next batch's scan as extra workgroups of the dW_cell / dX_enc launch (tgnx_tgn_train_step_pp): into the
 // other parity's set (c), batch one past the counters (they advance in the fixup launch), no descriptor
 // write (the fixup launch writes it)
+// (blocks: the walk (role 0) and the 2 pplan plan roles, or the walk alone when the plans ride in the
+// predictor launch: large global batches, tgn_pred_train's plan blocks)
 struct ScanJob {
   Ctx c;
   __device__ void operator()(int bid, float* smem) const {
@@ -3827,7 +3853,7 @@ static int ksplit(int K, int smin) { return std::max(smin, std::min(64, K / 2048
 #define TGNX_DWE_SMAX 64  // (experiments: caps on the split counts of dW_edge / dW_gru)
 #endif
 #ifndef TGNX_DWG_SMAX
-#define TGNX_DWG_SMAX 64
+#define TGNX_DWG_SMAX 2  // (dW_gru split-K: same-box A/B 0.0965 vs 0.0970 ms with the 3 splits of the K / 2048 rule, a third fewer partials)
 #endif
 // the deferred (split-K) weight-gradient GEMMs of a train step
 static GemmShape shp_dWe(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.Etr, nullptr, nullptr, cnt ? cnt + CNT_E : nullptr, std::min(TGNX_DWE_SMAX, ksplit(k.Etr, TGNX_S_WE))); }
@@ -4317,11 +4343,12 @@ extern "C++" {  // (inside the extern "C" block: the cell-templated step)
 #endif
 // the next batch's scan as 256-thread head workgroups of the fixup launch: its LDS within the launch's,
 // and (small graphs, walked directly) <= 2 bitmap words per thread
-static inline bool scan_rides(const Ctx& c, const Caps& k, size_t lds) {
-  return tgn_scan_smem(k.B) <= lds && (size_t)3 * k.B * 12 <= lds && (!scan_direct(c.words) || c.words <= 2 * 256);
+// (k: the global batch, whose plans the scan sorts; kr: the rank's share, whose centres the walk stages)
+static inline bool scan_rides(const Ctx& c, const Caps& k, const Caps& kr, size_t lds) {
+  return tgn_scan_smem(k.B) <= lds && (size_t)3 * kr.B * 12 <= lds && (!scan_direct(c.words) || c.words <= 2 * 256);
 }
-static inline bool scan_folds(const Ctx& c, const Caps& k) {
-  return TGNX_SCAN_FOLD && scan_rides(c, k, (size_t)GEMM_FIX_SMEM * 4);
+static inline bool scan_folds(const Ctx& c, const Caps& k, const Caps& kr) {
+  return TGNX_SCAN_FOLD && scan_rides(c, k, kr, (size_t)GEMM_FIX_SMEM * 4);
 }
 // pp >= 0 (tgnx_tgn_train_step_pp, world 1, 1 hop): the step reads scan-output set pp; the next batch is marked
 // in the predictor launch and scanned into set 1 - pp inside the k / v reduction launch (its outputs are then
@@ -4354,6 +4381,15 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     c.adv_world = adv->world;
     c.adv_seed = adv->seed;
   }
+  // data parallel: the rank's share ceil(B / world) of the global batch sets every per-rank capacity that
+  // sizes a grid or a GEMM shape (roots, sampled nodes / edges, predictor rows, update list): grids sized
+  // from the global batch launched ~W x the workgroups a rank needs (tgn_pred_train at world 8: 1,600
+  // blocks for 200 events).  The global batch keeps what replays it whole on every rank (ring insert,
+  // store update, their plans).  World 1 and the advance-driven form (world read on the device): kr == k.
+  tgnx_tgn_config cfg_r = *cfg;
+  if (adv) cfg_r.max_batch = (int)((cfg->max_batch + adv->world - 1) / adv->world);
+  const Caps kr = make_caps(&cfg_r);
+  c.Bmax = kr.B;  // (the scan walk stages the rank's centres in LDS: 3 Bmax entries)
   TGNX_CHECK_ARG(buf->neg && buf->grads && buf->out_pos && buf->out_neg, "tgnx_tgn_train_fwd_bwd: null buffer");
   // DyRep embedding messages need every embedding of src ∪ dst on this rank: world 1 only
   TGNX_CHECK_ARG(!c.emb || !buf->xrows, "tgn: DyRep embedding messages (emb_in_msg) are a world-1 step");
@@ -4389,7 +4425,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   float* G = c.grads;
   const int D = c.D, HC = c.HC, Qm = c.Qm, d = c.d;
   if (pipe != 1) {
-    const int nmark = gridn(3 * k.B * 16, 256);
+    const int nmark = gridn(3 * kr.B * 16, 256);
     tgn_mark<true><<<nmark, 256, 0, s>>>(c, nmark);
     TGNX_LAUNCH_CHECK("tgn_mark");
     probe_begin(TGNX_K_ASSEMBLE, s);
@@ -4397,10 +4433,10 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     probe_end(TGNX_K_ASSEMBLE, s);
     TGNX_LAUNCH_CHECK("tgn_scan");
   }
-  const int nedge = gridn((int64_t)k.Rtr * c.K, 4, TGNX_AGG_EDGE_CAP);
+  const int nedge = gridn((int64_t)kr.Rtr * c.K, 4, TGNX_AGG_EDGE_CAP);
   probe_begin(TGNX_K_EDGE_META, s);
-  const int nevb = gridn(3 * k.B * (c.evj ? 16 : 1), 256);
-  const int nagg = nevb + nedge + gridn(k.Mtr, 4, TGNX_AGG_NODE_CAP);
+  const int nevb = gridn(3 * kr.B * (c.evj ? 16 : 1), 256);
+  const int nagg = nevb + nedge + gridn(kr.Mtr, 4, TGNX_AGG_NODE_CAP);
   const int64_t* nol = nullptr;
   const int* noc = nullptr;
   if (c.aggr == 0 && TGNX_AGG_SPECIALIZE)
@@ -4413,31 +4449,31 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   TGNX_LAUNCH_CHECK("tgn_agg_emit");
   // GRU over every sampled node ‖ lin_edge over every sampled edge (‖ 2 hops: conv2's lin_edge over the
   // root edges)
-  const LoadRowK ea{c.encE, k.Etr, D + d, D + d};  // the edges' [cos enc | msg] rows (tgn_agg_emit, train)
+  const LoadRowK ea{c.encE, kr.Etr, D + d, D + d};  // the edges' [cos enc | msg] rows (tgn_agg_emit, train)
   const bool two = k.layers == 2;
   const LoadAttrMap ea1{c.encE, c.e1_e2, D + d};  // root edge -> its outer edge's row
-  const auto j_gru = gemm_job<G32L>(gemm_shape<G32L>(k.Mtr, Cl::G * D, Qm + D, c.cnt + CNT_M),
+  const auto j_gru = gemm_job<G32L>(gemm_shape<G32L>(kr.Mtr, Cl::G * D, Qm + D, c.cnt + CNT_M),
                                     LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0}, Cl::w(c), Cl::epi(c, c.nid, 0),
                                     (float*)nullptr);
-  const auto j_edge = gemm_job<G32>(gemm_shape<G32>(k.Etr, HC, D + d, c.cnt + CNT_E), ea,
+  const auto j_edge = gemm_job<G32>(gemm_shape<G32>(kr.Etr, HC, D + d, c.cnt + CNT_E), ea,
                                     LoadRowK{P + c.L.we, HC, D + d, D + d}, EpiStore{c.Ep, nullptr, HC, 0}, (float*)nullptr);
   const BlockJob<RingMergeJob> j_ring{RingMergeJob{c}, gridn(2 * k.B, 4)};
   probe_begin(TGNX_K_EDGE_FWD, s);
   if (two)
     gemmN_launch(s, j_ring, j_gru, j_edge,
-                 gemm_job<G32>(gemm_shape<G32>(k.E1tr, HC, D + d, c.cnt + CNT_E1), ea1,
+                 gemm_job<G32>(gemm_shape<G32>(kr.E1tr, HC, D + d, c.cnt + CNT_E1), ea1,
                                LoadRowK{P + c.L.we2, HC, D + d, D + d}, EpiStore{c.Ep2, nullptr, HC, 0}, (float*)nullptr));
   else
     gemmN_launch(s, j_ring, j_gru, j_edge);
   probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgn_gru_edge");
-  const int nmark = gridn(3 * k.B * 16, 256);
+  const int nmark = gridn(3 * kr.B * 16, 256);
   // 1 hop with the attention forward in the predictor: the attention backward computes each edge's (dk, dv)
   // where it sums them (kv_edge_body), so the k / v reduction launch is gone and the GEMMs that need only dE
   // ride in a later launch
   // (2 hops: the outer level, whose attention forward is tgn_attn_fwd; its edges keep the sampling order)
   const bool kvf = TGNX_KV_FUSE && (two ? TGNX_KVF_2HOP : TGNX_PRED_ATT);
-  const bool kvs = kvf && !two && TGNX_KVE_GSORT && (size_t)k.Mtr + 1 <= tgn_pred_smem(c.D) / 4;
+  const bool kvs = kvf && !two && TGNX_KVE_GSORT && (size_t)kr.Mtr + 1 <= tgn_pred_smem(c.D) / 4;
   c.kvf = kvf ? 1 : 0;
   c.kvs = kvs ? 1 : 0;
   // (kvf: no k / v launch; the next batch's marking of a non-parity pipelined step rides in the predictor launch
@@ -4450,7 +4486,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   };
   probe_begin(TGNX_K_PROJ, s);
   gemmN_launch(s, mk_at(3),
-               gemm_job<G32>(gemm_shape<G32>(k.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
+               gemm_job<G32>(gemm_shape<G32>(kr.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
                              LoadProjW{P + c.L.wq, c.L.pw, HC, D}, EpiProj{P + c.L.bq, c.L.pb, c.P, HC}, (float*)nullptr));
   probe_end(TGNX_K_PROJ, s);
   TGNX_LAUNCH_CHECK("tgn_proj");
@@ -4458,28 +4494,39 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const bool att_in_pred = !two && TGNX_PRED_ATT;
   if (!att_in_pred) {
     probe_begin(TGNX_K_SEG_FWD, s);
-    launch_k(tgn_attn_fwd<true>, dim3(gridn(k.Rtr, 4, 1 << 20)), dim3(256), 0, s, c);
+    launch_k(tgn_attn_fwd<true>, dim3(gridn(kr.Rtr, 4, 1 << 20)), dim3(256), 0, s, c);
     probe_end(TGNX_K_SEG_FWD, s);
     TGNX_LAUNCH_CHECK("tgn_attn_fwd");
   }
   Ctx cr = two ? root_view(c) : c;  // the level the predictor reads
   if (two) cr.kvf = cr.kvs = 0;    // (conv2 keeps its k / v reduction launch)
   if (two) {  // conv2 over the roots: projections of h1 (rows = outer centres), attention per root
-    gemm_launch<G32>(gemm_shape<G32>(k.Rtr, 4 * HC, HC, c.cnt + CNT_R), LoadRowK{c.Zc, k.Rtr, HC, HC},
+    gemm_launch<G32>(gemm_shape<G32>(kr.Rtr, 4 * HC, HC, c.cnt + CNT_R), LoadRowK{c.Zc, kr.Rtr, HC, HC},
                      LoadProjW{P + c.L.wq2, c.L.pw, HC, HC}, EpiProj{P + c.L.bq2, c.L.pb, c.P2, HC}, nullptr, s);
     TGNX_LAUNCH_CHECK("tgn_proj2");
-    tgn_attn_fwd<true><<<gridn(k.R1tr, 4, 1 << 20), 256, 0, s>>>(cr);
+    tgn_attn_fwd<true><<<gridn(kr.R1tr, 4, 1 << 20), 256, 0, s>>>(cr);
     TGNX_LAUNCH_CHECK("tgn_attn_fwd2");
   }
+  // where the next batch's scan runs (parity-set steps): all of it as the first workgroups of the dW_cell
+  // launch when its LDS holds the plans; else, for partitioned plans (data parallel: the global batch's
+  // 2 B keys) that fit the predictor launch's LDS, the plans there and the walk alone in the dW_cell launch;
+  // else its own launch after the dW_cell launch
+  const bool scan_w3 = ppm && scan_rides(c, k, kr, (size_t)3 * MARK_LDS_WORDS * 4);
+  const bool plans_pred = ppm && !scan_w3 && TGNX_PLANS_IN_PRED && c.pplan > 1 && 2 * k.B <= PRED_PLAN_MAXE * 256 &&
+                          scan_rides(c, kr, kr, (size_t)3 * MARK_LDS_WORDS * 4) &&
+                          tgn_scan_smem(k.B) <= tgn_pred_smem(TDMAX);
+  const int npl = plans_pred ? 2 * c.pplan : 0;
   probe_begin(TGNX_K_PRED, s);
   TGNX_CHECK_ARG(pred_smem_ok(c.D), "tgn_pred_train: dynamic LDS attribute refused");
   const int nmk = (ppm ? pp_mark_at == 5 : pipe && mark_at == 5) ? nmark : 0;
-  const size_t psm = std::max(tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0);
+  const size_t psm = std::max({tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0,
+                               npl ? tgn_scan_smem(k.B) : (size_t)0});
   const int nsrt = kvs ? 1 : 0;  // (kvs: the rows fit the sort's LDS counters)
+  const PlanOut po = plan_out(ppm ? cn : c);
   if (att_in_pred)
-    launch_k(tgn_pred_train<true>, dim3(k.B + nsrt + nmk), dim3(256), (uint32_t)psm, s, cr, nmk, nsrt);
+    launch_k(tgn_pred_train<true>, dim3(kr.B + npl + nsrt + nmk), dim3(256), (uint32_t)psm, s, cr, nmk, nsrt, po, npl);
   else
-    launch_k(tgn_pred_train<false>, dim3(k.B + nsrt + nmk), dim3(256), (uint32_t)psm, s, cr, nmk, nsrt);
+    launch_k(tgn_pred_train<false>, dim3(kr.B + npl + nsrt + nmk), dim3(256), (uint32_t)psm, s, cr, nmk, nsrt, po, npl);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
   if (c.emb) {
@@ -4487,35 +4534,35 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     // stored messages with the embeddings of this batch's forward in place of memory rows (:387-408) — the
     // stores are still the previous batch's (StoreJob runs later); the fixup writes these rows (Zupd)
     const Ctx ce = emb_view(c, W, reinterpret_cast<char*>(buf->ws));
-    gru_list_c<CELL>(ce, c.upd, c.cnt + CNT_U, 0, 0, k.Ucap, s, true);
+    gru_list_c<CELL>(ce, c.upd, c.cnt + CNT_U, 0, 0, kr.Ucap, s, true);
     TGNX_LAUNCH_CHECK("tgn_emb_update");
   }
   probe_begin(TGNX_K_SEG_BWD, s);
   if (two) {
     // conv2 backward (‖ predictor reductions) -> dP2, dE2; then dh1 = dP2 [Wq2; Wk2; Wv2; Wsk2] ‖ dW_proj2,
     // dW_edge2 (deferred) ‖ conv2's lin_edge -> Δt-encoding partials; then conv backward from dh1
-    const int ncb1 = gridn(k.R1tr, 4, 1 << 20);
+    const int ncb1 = gridn(kr.R1tr, 4, 1 << 20);
     tgn_attn_bwd<<<ncb1 + gridn(3 * D + 2, 4), 256, 0, s>>>(cr, ncb1, 0);
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
     // conv2's (dk, dv) sums ‖ its dE2-only GEMMs (as in the 1-hop step below), then dh1 ‖ dW_proj2
-    gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{cr}, gridn(k.E1tr, KVR_CH, 1 << 20)},
-                 gemm_job<GW>(shp_dWe2(k, c.cnt), LoadKRow{c.dE2, HC, k.E1tr, HC}, LoadAttrMapT{ea1},
+    gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{cr}, gridn(kr.E1tr, KVR_CH, 1 << 20)},
+                 gemm_job<GW>(shp_dWe2(kr, c.cnt), LoadKRow{c.dE2, HC, kr.E1tr, HC}, LoadAttrMapT{ea1},
                                EpiDeferred{}, c.pF),
-                 gemm_job<G32>(gemm_shape<G32>(k.E1tr, D, HC, c.cnt + CNT_E1), LoadRowK{c.dE2, k.E1tr, HC, HC},
+                 gemm_job<G32>(gemm_shape<G32>(kr.E1tr, D, HC, c.cnt + CNT_E1), LoadRowK{c.dE2, kr.E1tr, HC, HC},
                                LoadKRow{P + c.L.we2, D, HC, D + d},
                                EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, c.e1_e2, c.tgp_e1}, (float*)nullptr));
     TGNX_LAUNCH_CHECK("tgn_kv_reduce2");
     gemmN_launch(s,
-                 gemm_job<G32L>(gemm_shape<G32L>(k.Rtr, HC, 4 * HC, c.cnt + CNT_R), LoadRowK{c.dP2, k.Rtr, 4 * HC, 4 * HC},
+                 gemm_job<G32L>(gemm_shape<G32L>(kr.Rtr, HC, 4 * HC, c.cnt + CNT_R), LoadRowK{c.dP2, kr.Rtr, 4 * HC, 4 * HC},
                                 LoadProjWT{P + c.L.wq2, c.L.pw, HC, HC}, EpiStore{c.dZc, nullptr, HC, 0}, (float*)nullptr),
-                 gemm_job<GW>(shp_dWp2(k, c.cnt), LoadKRow{c.dP2, 4 * HC, k.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
+                 gemm_job<GW>(shp_dWp2(kr, c.cnt), LoadKRow{c.dP2, 4 * HC, kr.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
                                EpiDeferred{}, c.pE));
     TGNX_LAUNCH_CHECK("tgn_dh1");
-    const int ncb = gridn(k.Rtr, 4, 1 << 20), nkv = kvf ? gridn(k.Etr, KVE_CH, 1 << 20) : 0;
+    const int ncb = gridn(kr.Rtr, 4, 1 << 20), nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
     tgn_attn_bwd<<<ncb + nkv, 256, 0, s>>>(c, ncb, nkv);
   } else {
-    const int ncb = gridn(k.Rtr, 4, 1 << 20);
-    const int nkv = kvf ? gridn(k.Etr, KVE_CH, 1 << 20) : 0;
+    const int ncb = gridn(kr.Rtr, 4, 1 << 20);
+    const int nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
     launch_k(tgn_attn_bwd, dim3(ncb + nkv + gridn(3 * D + 2, 4)), dim3(256), 0, s, c, ncb, nkv);
   }
   probe_end(TGNX_K_SEG_BWD, s);
@@ -4526,10 +4573,10 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // idle: the dE-only GEMMs fill them here instead of lengthening the dP launch below.
   const Ctx cf = fixup_view(c);
   const EpiGradStore e_dWe{G, c.L.we, D + d, cf.adf};
-  const auto j_kvr = BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(k.Etr, KVR_CH, 1 << 20)};
-  const auto j_dwe = gemm_job<GW>(shp_dWe(k, c.cnt), LoadKRow{c.dE, HC, k.Etr, HC}, LoadKRow{c.encE, D + d, k.Etr, D + d},
+  const auto j_kvr = BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(kr.Etr, KVR_CH, 1 << 20)};
+  const auto j_dwe = gemm_job<GW>(shp_dWe(kr, c.cnt), LoadKRow{c.dE, HC, kr.Etr, HC}, LoadKRow{c.encE, D + d, kr.Etr, D + d},
                                   EpiDeferred{}, c.pA);
-  const auto j_denc = gemm_job<G32>(gemm_shape<G32>(k.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, k.Etr, HC, HC},
+  const auto j_denc = gemm_job<G32>(gemm_shape<G32>(kr.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, kr.Etr, HC, HC},
                                     LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
                                     (float*)nullptr);
   if (!kvf) {
@@ -4544,12 +4591,12 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const auto e_dWg = Cl::wgrad(cf);
   // one launch: dW_proj, dW_src/dst (deferred split-K) ‖ dz0 = dP W with the GRU backward in its
   // epilogue — all read only what attn_bwd / kv_reduce / pred_train produced
-  const int rows_edge = (k.Etr + G32::TM - 1) / G32::TM, rows_msg = (k.Mtr + G32::TM - 1) / G32::TM;
+  const int rows_edge = (kr.Etr + G32::TM - 1) / G32::TM, rows_msg = (kr.Mtr + G32::TM - 1) / G32::TM;
   probe_begin(TGNX_K_EDGE_BWD, s);
-  const auto j_dwp = gemm_job<GW>(shp_dWp(k, c.cnt), LoadKRow{c.dP, 4 * HC, k.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB);
-  const auto j_dwlp = gemm_job<GW>(shp_dWlp(k, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
+  const auto j_dwp = gemm_job<GW>(shp_dWp(kr, c.cnt), LoadKRow{c.dP, 4 * HC, kr.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB);
+  const auto j_dwlp = gemm_job<GW>(shp_dWlp(kr, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
                                    LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, EpiDeferred{}, c.pC);
-  const auto j_dz0 = gemm_job<G32L>(with_cap(gemm_shape<G32L>(k.Mtr, D, 4 * HC, c.cnt + CNT_M), TGNX_MD_CAP), LoadRowK{c.dP, k.Mtr, 4 * HC, 4 * HC},
+  const auto j_dz0 = gemm_job<G32L>(with_cap(gemm_shape<G32L>(kr.Mtr, D, 4 * HC, c.cnt + CNT_M), TGNX_MD_CAP), LoadRowK{c.dP, kr.Mtr, 4 * HC, 4 * HC},
                                     LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, Cl::bwd(c), (float*)nullptr);
   auto l7 = [&](auto... jobs) {
     gemmN_launch(s, mk_at(8), jobs...);
@@ -4559,23 +4606,23 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   };
   // ‖ the message stores ‖ the fixup's descriptor copy + the counter advance (SnapJob)
   const int nst = gridn(2 * k.B, 256);
-  const auto j_dwg = gemm_job<GW>(shp_dWg(k, c.cnt), LoadKRow{c.dG, Cl::G * D, k.Mtr, Cl::G * D},
+  const auto j_dwg = gemm_job<GW>(shp_dWg(kr, c.cnt), LoadKRow{c.dG, Cl::G * D, kr.Mtr, Cl::G * D},
                                   LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{}, c.pD);
-  const auto j_dxe = gemm_job<G32L>(with_cap(gemm_shape<G32L>(k.Mtr, D, Cl::G * D, c.cnt + CNT_M), TGNX_MD_CAP),
-                                    LoadRowK{c.dG, k.Mtr, Cl::G * D, Cl::G * D}, Cl::wenc(c),
+  const auto j_dxe = gemm_job<G32L>(with_cap(gemm_shape<G32L>(kr.Mtr, D, Cl::G * D, c.cnt + CNT_M), TGNX_MD_CAP),
+                                    LoadRowK{c.dG, kr.Mtr, Cl::G * D, Cl::G * D}, Cl::wenc(c),
                                     EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, (float*)nullptr);
   // ppm: the next batch's scan (into set 1 - pp; the counters advance in the fixup launch) as this launch's
   // first workgroups when it fits their LDS, else its own launch after it
-  const bool scan_w3 = ppm && scan_rides(c, k, (size_t)3 * MARK_LDS_WORDS * 4);
-  const auto j_scan = BlockJob<ScanJob, 3 * MARK_LDS_WORDS>{ScanJob{cn}, 1 + 2 * c.pplan};
+  const auto j_scan = BlockJob<ScanJob, 3 * MARK_LDS_WORDS>{ScanJob{cn}, plans_pred ? 1 : 1 + 2 * c.pplan};
   const auto j_snap = BlockJob<SnapJob>{SnapJob{c, ppm ? 1 : 0}, 1};
   const auto j_store = BlockJob<StoreJob>{StoreJob{c, nst}, nst};
   // (the scan may ride in the dz0 launch instead: TGNX_SCAN_AT 6)
   const bool scan6 = scan_w3 && kvf && TGNX_SCAN_AT == 6;
+  const bool walk_w3 = scan_w3 || plans_pred;  // (the walk rides in the dW_cell launch)
   auto l8 = [&](auto... jobs) {
     probe_begin(TGNX_K_WGRAD3, s);
     // the GEMM jobs before the snapshot / store blocks (0.0970 vs 0.0986 ms with those first)
-    if (scan_w3 && !scan6)
+    if (walk_w3 && !scan6)
       gemmN_launch(s, j_scan, j_dxe, j_dwg, jobs..., j_snap, j_store);
     else
       gemmN_launch(s, j_dxe, j_dwg, jobs..., j_snap, j_store);
@@ -4593,7 +4640,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   } else {
     if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) return rc;
   }
-  if (ppm && !scan_w3) {
+  if (ppm && !walk_w3) {
     tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(cn, 1, 0);
     TGNX_LAUNCH_CHECK("tgn_scan_early");
   }
@@ -4602,22 +4649,22 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // step descriptor from SnapJob's copy (cf) — so that the pipelined step's next-batch scan (counters
   // advanced by SnapJob) rides in the same launch as its first workgroups when it fits (scan_folds)
   const int nte = (2 * D + 63) / 64;
-  const int nmem = gridn(k.Ucap, 4, 1024);
+  const int nmem = gridn(kr.Ucap, 4, 1024);
   const bool scan_next = pipe && !no_tail && !ppm;
-  const bool fold = scan_next && scan_folds(c, k);
+  const bool fold = scan_next && scan_folds(c, k, kr);
   const int nscan = fold ? 1 + 2 * c.pplan : 0;
   const TrainTail tail{TeReduceTail{cf, rows_edge, rows_msg}, c, nscan, nte, nmem, ppm ? 1 : 0};
   probe_begin(TGNX_K_FINISH, s);
   if (two)
-    gemm_fixup_launch_h(nscan, nscan + nte + nmem, tail, s, gemm_fix<GW>(shp_dWe(k, cf.cnt), c.pA, e_dWe),
-                        gemm_fix<GW>(shp_dWp(k, cf.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(k, cf.cnt), c.pC, e_dWlp),
-                        gemm_fix<GW>(shp_dWg(k, cf.cnt), c.pD, e_dWg),
-                        gemm_fix<GW>(shp_dWp2(k, cf.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC, cf.adf}),
-                        gemm_fix<GW>(shp_dWe2(k, cf.cnt), c.pF, EpiGradStore{G, c.L.we2, D + d, cf.adf}));
+    gemm_fixup_launch_h(nscan, nscan + nte + nmem, tail, s, gemm_fix<GW>(shp_dWe(kr, cf.cnt), c.pA, e_dWe),
+                        gemm_fix<GW>(shp_dWp(kr, cf.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(kr, cf.cnt), c.pC, e_dWlp),
+                        gemm_fix<GW>(shp_dWg(kr, cf.cnt), c.pD, e_dWg),
+                        gemm_fix<GW>(shp_dWp2(kr, cf.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC, cf.adf}),
+                        gemm_fix<GW>(shp_dWe2(kr, cf.cnt), c.pF, EpiGradStore{G, c.L.we2, D + d, cf.adf}));
   else
-    gemm_fixup_launch_h(nscan, nscan + nte + nmem, tail, s, gemm_fix<GW>(shp_dWe(k, cf.cnt), c.pA, e_dWe),
-                        gemm_fix<GW>(shp_dWp(k, cf.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(k, cf.cnt), c.pC, e_dWlp),
-                        gemm_fix<GW>(shp_dWg(k, cf.cnt), c.pD, e_dWg));
+    gemm_fixup_launch_h(nscan, nscan + nte + nmem, tail, s, gemm_fix<GW>(shp_dWe(kr, cf.cnt), c.pA, e_dWe),
+                        gemm_fix<GW>(shp_dWp(kr, cf.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(kr, cf.cnt), c.pC, e_dWlp),
+                        gemm_fix<GW>(shp_dWg(kr, cf.cnt), c.pD, e_dWg));
   probe_end(TGNX_K_FINISH, s);
   TGNX_LAUNCH_CHECK("tgn_fixup_update");
   if (scan_next && !fold) {  // the next batch (counters advanced by SnapJob): sorted node sets, plans, descriptor
