@@ -3606,7 +3606,7 @@ struct MarkNextJob {
 #define TGNX_MD_CAP 512  // grid cap of the step's M x D GEMMs (dz0, dX_enc): 7 column tiles at D = 100, ~30 row tiles at B = 200 (A/B 0.0966 vs 0.0971 ms with 1024)
 #endif
 #ifndef TGNX_PLANS_IN_PRED
-#define TGNX_PLANS_IN_PRED 1  // parity-set steps with partitioned plans: the plans in the predictor launch (0: own scan launch)
+#define TGNX_PLANS_IN_PRED 4  // parity-set steps whose plans have 2..N partitions: the plans in the predictor launch (0: never; DP floor A/B at world 2 / 4 / 8: N = 4 0.1034 / 0.1078 / 0.1283 ms, 16 0.1040 / 0.1087 / 0.1328, 0 0.1039 / 0.1176 / 0.1285)
 #endif
 #ifndef TGNX_SCAN_AT
 #define TGNX_SCAN_AT 7  // parity step: the launch the next batch's scan rides in (7: dW_gru; 6: dz0, 0.1005 vs 0.0965 ms)
@@ -4247,6 +4247,11 @@ static Ctx root_view(const Ctx& c) {
 #ifndef TGNX_AGG_NODE_CAP
 #define TGNX_AGG_NODE_CAP 512
 #endif
+// integer knob from the environment (host, read once by the caller's static), else the build default
+static inline int env_int(const char* name, int def) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : def;
+}
 static inline int gridn(int64_t n, int per, int cap = 4096) {
   int64_t g = (n + per - 1) / per;
   if (g < 1) g = 1;
@@ -4512,7 +4517,9 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // 2 B keys) that fit the predictor launch's LDS, the plans there and the walk alone in the dW_cell launch;
   // else its own launch after the dW_cell launch
   const bool scan_w3 = ppm && scan_rides(c, k, kr, (size_t)3 * MARK_LDS_WORDS * 4);
-  const bool plans_pred = ppm && !scan_w3 && TGNX_PLANS_IN_PRED && c.pplan > 1 && 2 * k.B <= PRED_PLAN_MAXE * 256 &&
+  static const int plans_in_pred = env_int("TGNX_PLANS_IN_PRED", TGNX_PLANS_IN_PRED);  // (runtime A/B switch)
+  const bool plans_pred = ppm && !scan_w3 && plans_in_pred && c.pplan > 1 && c.pplan <= plans_in_pred &&
+                          2 * k.B <= PRED_PLAN_MAXE * 256 &&
                           scan_rides(c, kr, kr, (size_t)3 * MARK_LDS_WORDS * 4) &&
                           tgn_scan_smem(k.B) <= tgn_pred_smem(TDMAX);
   const int npl = plans_pred ? 2 * c.pplan : 0;
