@@ -321,6 +321,11 @@ typedef struct {
                                      sigmoid(pos), sigmoid(neg) of event e at [2e], [2e + 1] — so that an
                                      epoch of replayed steps leaves every batch's outputs for the AP / AUC
                                      display (pyg_epoch_utils.py:139-147) without a copy per step */
+  const void* plan_table;         /* optional (NULL: unused): the plan table tgnx_tgn_plan_table built for the
+                                     split / batch the resident parity-set steps run (tgnx_tgn_train_step_pp,
+                                     tgnx_tgn_train_fwd_bwd_pp); they then read every batch's ring-insert and
+                                     message-store plans from it and their scan is the node-set walk alone.
+                                     Other calls ignore it.  Must match the steps' split_lo / split_hi / batch. */
 } tgnx_tgn_buffers;
 /* exchanged memory row, all fields floats holding exact integers so that the row survives a SUM exchange
  * (one all-reduce over [gradients | every rank's row slots, zero but the sender's] is the all-gather):
@@ -331,6 +336,16 @@ int tgnx_tgn_param_layout(const tgnx_tgn_config* cfg,
                           int64_t* offsets /* [TGNX_TGN_NPARAM+1], layers = 2: [TGNX_TGN_NPARAM2+1] */);
 size_t tgnx_tgn_ws_bytes(const tgnx_tgn_config* cfg);
 size_t tgnx_tgn_store_words(const tgnx_tgn_config* cfg);
+/* The ring-insert plan (neighbor_loader.py:52-104: the batch's (node, event, direction) entries in node
+ * order, newest first, runs per node) and the message-store plan (memory_module.py:180-191: stable per
+ * (node, direction), runs) of every batch of a resident split [split_lo, split_hi) in batches of `batch`
+ * (the global batch under data parallelism): a function of the event table alone, so one launch per
+ * binding builds what each step's scan would otherwise sort again.  Table: tgnx_tgn_plan_table_bytes bytes
+ * (a 64-B header + one slot per batch, ~24 B per event entry); hand it to the resident parity-set steps as
+ * buf->plan_table. */
+size_t tgnx_tgn_plan_table_bytes(const tgnx_tgn_config* cfg, int64_t split_lo, int64_t split_hi, int64_t batch);
+int tgnx_tgn_plan_table(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo, int64_t split_hi,
+                        int64_t batch, void* table, size_t table_bytes, void* stream);
 /* memory = 0, last_update = 0, message stores empty (memory_module.py:106-110). */
 int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream);
 /* Train batch, part 1 (the canonical loop pyg_epoch_utils.py:106-137 carries commented out): negatives

@@ -277,10 +277,10 @@ def test_tgn_resident_folded_cursor_equals_advance_plus_step():
             m1.memory.memory.copy_(m2.memory.memory)
 
 
-@pytest.mark.parametrize("pp", [True, False])
+@pytest.mark.parametrize("pp,table", [(True, True), (True, False), (False, False)])
 @pytest.mark.parametrize("layers,updater,emb", [(1, "gru", (0, 0)), (2, "gru", (0, 0)), (1, "rnn", (0, 0)),
                                                 (1, "rnn", (1, 1))])
-def test_tgn_pipelined_equals_resident(layers, updater, emb, pp):
+def test_tgn_pipelined_equals_resident(layers, updater, emb, pp, table):
     """tgnx_tgn_train_step_pipelined (each step marks the next batch inside its predictor launch and scans it
     after its last launch; ring insert beside the GRU) — or, pp (1 hop), tgnx_tgn_train_step_pp (the next batch
     scanned into the other parity's set inside the k / v reduction launch, two graphs replayed alternately) —
@@ -288,7 +288,8 @@ def test_tgn_pipelined_equals_resident(layers, updater, emb, pp):
     prefetched = 0), device negatives, attention dropout, a partial last batch and a step past the split.
     After every step: step counters and the ring exactly, this batch's negatives exactly (the pipelined
     engine has drawn the next batch's too), outputs, parameters and memory within the fused-Adam tolerances
-    (resynchronised per step)."""
+    (resynchronised per step).  table: the parity-set step reads the split's plans from the table built at
+    binding (tgnx_tgn_plan_table) instead of its scan's, which then only walks the node sets."""
     if pp and layers == 2:
         pytest.skip("parity sets are a 1-hop step (2 hops: the pipelined step)")
     engines = []
@@ -298,6 +299,7 @@ def test_tgn_pipelined_equals_resident(layers, updater, emb, pp):
         model.cfg.dropout = 0.1
         eng.pipeline = pipe
         eng.parity_sets = pp
+        eng.use_plan_table = table and pipe
         eng.bind_resident(0, 7 * 50 + 20, 50, dropout=True)   # the last batch is partial (20 events)
         eng.begin_epoch()
         if pipe:

@@ -228,6 +228,7 @@ struct Ctx {
   int* snap_upd_loc;
   int64_t* errw;
   int Bmax, Qcap, Rcap, Mcap, Ecap, Ucap, tgp_rows;
+  int Bplan;  // the global max_batch (plan sizes)
   Lay L;
   // ---- 2-hop (layers = 2).  The arrays above then describe the OUTER sample: centres = the 1-hop node
   // set (roots ∪ their ring neighbours, sorted), nodes = the 2-hop set; gnn.conv runs over it and
@@ -255,6 +256,10 @@ struct Ctx {
   float* Zupd;
   // tgnx_tgn_train_step_pp: tgn_agg_emit checks that the scan-output set holds this step's batch (cnt[CNT_NB])
   int tagchk;
+  // resident steps over a split whose plans were built once (tgnx_tgn_plan_table): the ring-insert / store
+  // plans of batch b at ptab + 64 + b * ptab_stride (plan_view), instead of the scan's per-step set
+  const char* ptab;
+  int64_t ptab_stride;
 };
 constexpr int CNT_R1 = 7, CNT_E1 = 8;
 
@@ -739,6 +744,30 @@ __device__ __forceinline__ int plan_runs(const int* pc, int P) {
   int u = 0;
   for (int q = 0; q < P; ++q) u += pc[q];
   return u;
+}
+// per-batch plan slot of the split's plan table: rkeys [2 Bmax] u64 | skeys [2 Bmax] u64 | rruns, sruns
+// [2 Bmax + 2 + PMAX] i32 each | pc [4 PMAX] i32 (rpc | rpo | spc | spo); a 64-B header {lo, hi, batch,
+// Bmax} precedes the slots
+__host__ __device__ inline int64_t plan_slot_bytes(int Bmax) {
+  const int64_t n2 = 2 * (int64_t)Bmax;
+  return ((n2 * 16 + (n2 + 2 + TGNX_PLAN_PMAX) * 8 + 4 * TGNX_PLAN_PMAX * 4) + 255) & ~(int64_t)255;
+}
+__host__ __device__ inline PlanOut plan_slot(const char* tab, int64_t stride, int Bmax, int64_t b) {
+  char* base = const_cast<char*>(tab) + 64 + b * stride;
+  const int64_t n2 = 2 * (int64_t)Bmax;
+  PlanOut o;
+  o.rkeys = reinterpret_cast<uint64_t*>(base);
+  o.skeys = o.rkeys + n2;
+  o.rruns = reinterpret_cast<int*>(o.skeys + n2);
+  o.sruns = o.rruns + n2 + 2 + TGNX_PLAN_PMAX;
+  o.pc = o.sruns + n2 + 2 + TGNX_PLAN_PMAX;
+  return o;
+}
+// the plans a consumer reads for the batch starting at event `start`: the table's slot (resident split steps
+// with a plan table), else the scan's set
+__device__ __forceinline__ PlanOut plan_view(const Ctx& c, int64_t start) {
+  if (!c.ptab) return plan_out(c);
+  return plan_slot(c.ptab, c.ptab_stride, c.Bplan, (start - c.adv_lo) / c.adv_batch);
 }
 
 // K2 (3 workgroups): WG0 ordered bitmap walks -> centres (+ edge offsets, update list) and sampled
@@ -2198,6 +2227,23 @@ __device__ __forceinline__ void pred_plan_body(const Ctx& c, int role, const Pla
   const int P = c.pplan;
   plan_part<PRED_PLAN_MAXE>(c, role < P ? 0 : 1, role % P, P, d.B, d.start, smem, sh, NoCheckpoint{}, po);
 }
+// the split's plan table (tgnx_tgn_plan_table): workgroup (batch b, plan role) sorts batch b's ring-insert or
+// message-store plan partition into slot b — the plans are a function of the event table alone, so the whole
+// split's are built once per binding instead of by every step's scan
+__global__ void __launch_bounds__(1024) tgn_plan_table_kernel(Ctx c, char* tab, int64_t stride, int64_t lo, int64_t hi,
+                                                              int64_t batch) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char psm_[];
+  __shared__ int sh[40];
+  const int P = c.pplan, b = (int)(blockIdx.x / (2 * P)), role = (int)(blockIdx.x % (2 * P));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    int64_t* h = reinterpret_cast<int64_t*>(tab);
+    h[0] = lo; h[1] = hi; h[2] = batch; h[3] = c.Bplan; h[4] = P;
+  }
+  const int64_t start = lo + (int64_t)b * batch;
+  const int B = (int)min(batch, hi - start);
+  if (B <= 0) return;
+  plan_part<8>(c, role < P ? 0 : 1, role % P, P, B, start, psm_, sh, NoCheckpoint{}, plan_slot(tab, stride, c.Bplan, b));
+}
 template <bool ATT>
 __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, PlanOut po, int npl) {
   TGNX_STAMP(5);
@@ -3498,10 +3544,11 @@ __device__ __forceinline__ void xrow_header(float* h, int64_t v, int64_t luv) {
 // ring insert of the batch (neighbor_loader.py:52-104): wave per node run of the ring plan (4 per block)
 __device__ __forceinline__ void ring_merge_block(const Ctx& c, int blk, int B, int64_t start) {
   const int r = blk * 4 + (threadIdx.x >> 6);
+  const PlanOut pv = plan_view(c, start);
   int a, len;
-  if (plan_run(c.rruns, c.rpc, c.rpo, c.pplan, r, a, len))  // r = the node's rank among the batch's nodes
+  if (plan_run(pv.rruns, pv.pc, pv.pc + TGNX_PLAN_PMAX, c.pplan, r, a, len))  // r = the node's rank among the batch's nodes
     ring_merge_run(c.nbr, c.eid, c.rt, c.K, c.ev_src + start, c.ev_dst + start, c.ev_t + start, B,
-                   c.ctl[TGNX_CTL_CUR_EID], c.assoc, c.rkeys, a, len, r, threadIdx.x & 63);
+                   c.ctl[TGNX_CTL_CUR_EID], c.assoc, pv.rkeys, a, len, r, threadIdx.x & 63);
 }
 // update_state pieces (memory_module.py:126-150, :180-191) and the ring insert, by block range:
 // [0, nmem): memory / last_update of the update list from the GRU rows (wave per node; train rows
@@ -3549,14 +3596,16 @@ __device__ __forceinline__ void update_body(const Ctx& c, int blk, int nmem, int
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   if (blk < nmem + nst) {
     const int bid = blk - nmem;
-    const int n2 = 2 * B, U = plan_runs(c.spc, c.pplan);
+    const PlanOut pv = plan_view(c, start);
+    const int* spc = pv.pc + 2 * TGNX_PLAN_PMAX;
+    const int n2 = 2 * B, U = plan_runs(spc, c.pplan);
     const int64_t ab = 2 * start;  // arena slot of this batch
     for (int p = bid * blockDim.x + threadIdx.x; p < n2; p += nst * blockDim.x)
-      c.arena[ab + p] = start + (int64_t)(c.skeys[p] & 0xFFFFFFFFull);
+      c.arena[ab + p] = start + (int64_t)(pv.skeys[p] & 0xFFFFFFFFull);
     for (int r = bid * blockDim.x + threadIdx.x; r < U; r += nst * blockDim.x) {
       int a, len;
-      plan_run(c.sruns, c.spc, c.spo, c.pplan, r, a, len);
-      const uint64_t k = c.skeys[a];
+      plan_run(pv.sruns, spc, spc + TGNX_PLAN_PMAX, c.pplan, r, a, len);
+      const uint64_t k = pv.skeys[a];
       const int64_t v = (int64_t)(k >> 33);
       const int dir = (int)((k >> 32) & 1u);
       c.st[4 * v + 2 * dir] = ab + a;
@@ -4138,6 +4187,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.errw = b->ctl + TGNX_CTL_ERR;
   c.pplan = plan_parts(k.B);
   c.Bmax = k.B;
+  c.Bplan = k.B;
   c.Qcap = k.Qcap;
   c.Rcap = k.Rcap;
   c.Mcap = k.Mcap;
@@ -4313,6 +4363,36 @@ size_t tgnx_tgn_store_words(const tgnx_tgn_config* cfg) {
   return (size_t)(4 * cfg->num_nodes + 2 * cfg->num_events);
 }
 
+size_t tgnx_tgn_plan_table_bytes(const tgnx_tgn_config* cfg, int64_t split_lo, int64_t split_hi, int64_t batch) {
+  if (check_cfg(cfg) || batch <= 0 || batch > cfg->max_batch || split_hi < split_lo) return 0;
+  const int64_t nb = (split_hi - split_lo + batch - 1) / batch;
+  return (size_t)(64 + (nb > 0 ? nb : 1) * plan_slot_bytes(cfg->max_batch));
+}
+
+int tgnx_tgn_plan_table(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo, int64_t split_hi,
+                        int64_t batch, void* table, size_t table_bytes, void* stream) {
+  Ctx c;
+  Caps k;
+  WsLay W;
+  int rc = make_ctx(cfg, buf, 1, c, k, W);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(batch > 0 && batch <= cfg->max_batch && split_lo >= 0 && split_hi >= split_lo && split_hi <= c.nev,
+                 "tgnx_tgn_plan_table: bad split / batch");
+  const size_t need = tgnx_tgn_plan_table_bytes(cfg, split_lo, split_hi, batch);
+  TGNX_CHECK_ARG(table && table_bytes >= need && ((uintptr_t)table & 15) == 0,
+                 "tgnx_tgn_plan_table: table of tgnx_tgn_plan_table_bytes(...) bytes, 16-B aligned");
+  const int64_t nb = (split_hi - split_lo + batch - 1) / batch;
+  if (nb == 0) return TGNX_OK;
+  const size_t smem = tgn_scan_smem(k.B);
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tgn_plan_table_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  TGNX_CHECK_ARG(attr && smem <= 160 * 1024, "tgnx_tgn_plan_table: dynamic LDS");
+  tgn_plan_table_kernel<<<(unsigned)(nb * 2 * c.pplan), 1024, smem, as_stream(stream)>>>(
+      c, reinterpret_cast<char*>(table), plan_slot_bytes(k.B), split_lo, split_hi, batch);
+  TGNX_LAUNCH_CHECK("tgn_plan_table");
+  return TGNX_OK;
+}
+
 int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream) {
   int rc = check_cfg(cfg);
   if (rc) return rc;
@@ -4415,6 +4495,10 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   c.gen_neg = gen_neg ? 1 : 0;
   c.drop = dropout && cfg->dropout > 0.f;
   const bool ppm = pp >= 0;
+  if (ppm && buf->plan_table) {  // the split's plans from the table built at binding (tgnx_tgn_plan_table)
+    c.ptab = reinterpret_cast<const char*>(buf->plan_table);
+    c.ptab_stride = plan_slot_bytes(k.B);
+  }
   Ctx cn;  // ppm: the other parity's set (the next batch's scan writes it)
   if (ppm) {
     TGNX_CHECK_ARG(pp <= 1 && pipe != 0 && !no_tail && k.layers == 1 && adv && (!fuse_adam || adv->world == 1),
@@ -4516,9 +4600,11 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // launch when its LDS holds the plans; else, for partitioned plans (data parallel: the global batch's
   // 2 B keys) that fit the predictor launch's LDS, the plans there and the walk alone in the dW_cell launch;
   // else its own launch after the dW_cell launch
-  const bool scan_w3 = ppm && scan_rides(c, k, kr, (size_t)3 * MARK_LDS_WORDS * 4);
+  // (with a plan table the scan is the walk alone: it rides when the rank's centres fit the launch's LDS)
+  const bool scan_w3 = ppm && (c.ptab ? scan_rides(c, kr, kr, (size_t)3 * MARK_LDS_WORDS * 4)
+                                      : scan_rides(c, k, kr, (size_t)3 * MARK_LDS_WORDS * 4));
   static const int plans_in_pred = env_int("TGNX_PLANS_IN_PRED", TGNX_PLANS_IN_PRED);  // (runtime A/B switch)
-  const bool plans_pred = ppm && !scan_w3 && plans_in_pred && c.pplan > 1 && c.pplan <= plans_in_pred &&
+  const bool plans_pred = ppm && !c.ptab && !scan_w3 && plans_in_pred && c.pplan > 1 && c.pplan <= plans_in_pred &&
                           2 * k.B <= PRED_PLAN_MAXE * 256 &&
                           scan_rides(c, kr, kr, (size_t)3 * MARK_LDS_WORDS * 4) &&
                           tgn_scan_smem(k.B) <= tgn_pred_smem(TDMAX);
@@ -4620,7 +4706,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                                     EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, (float*)nullptr);
   // ppm: the next batch's scan (into set 1 - pp; the counters advance in the fixup launch) as this launch's
   // first workgroups when it fits their LDS, else its own launch after it
-  const auto j_scan = BlockJob<ScanJob, 3 * MARK_LDS_WORDS>{ScanJob{cn}, plans_pred ? 1 : 1 + 2 * c.pplan};
+  const auto j_scan = BlockJob<ScanJob, 3 * MARK_LDS_WORDS>{ScanJob{cn}, plans_pred || c.ptab ? 1 : 1 + 2 * c.pplan};
   const auto j_snap = BlockJob<SnapJob>{SnapJob{c, ppm ? 1 : 0}, 1};
   const auto j_store = BlockJob<StoreJob>{StoreJob{c, nst}, nst};
   // (the scan may ride in the dz0 launch instead: TGNX_SCAN_AT 6)

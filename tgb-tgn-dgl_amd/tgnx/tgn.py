@@ -57,7 +57,7 @@ class TgnBuffers(ctypes.Structure):
                 ("n_dst", ctypes.c_int64), ("nbr", P), ("eid", P), ("rt", P), ("assoc", P), ("memory", P),
                 ("last_update", P), ("store", P), ("node_gen", P), ("params", P), ("grads", P), ("adam_m", P),
                 ("adam_v", P), ("ctl", P), ("out_pos", P), ("out_neg", P), ("mrr", P), ("ws", P), ("xrows", P),
-                ("xcap", ctypes.c_int64), ("out_ev", P)]
+                ("xcap", ctypes.c_int64), ("out_ev", P), ("plan_table", P)]
 
 
 # the memory modules' updater cell: TGNMemory.memory_updater (memory_module.py:70-78, memory_updater_cell
@@ -286,7 +286,10 @@ class TgnEngine:
         self.out_pos = torch.zeros(cfg.max_batch, dtype=torch.float32, device=self.dev)
         self.out_neg = torch.zeros(cfg.max_batch * max(cfg.max_neg, 1), dtype=torch.float32, device=self.dev)
         self.mrr = torch.zeros(cfg.max_batch, dtype=torch.float64, device=self.dev)
-        self.out_ev = None    # optional per-event train-output log (log_outputs)
+        self.out_ev = None    # optional per-event train-output log (tgnx_tgn_buffers.out_ev)
+        # the bound split's plan table (tgnx_tgn_plan_table; resident parity-set steps read it), TGNX_PLAN_TABLE=0: off
+        self.plan_table = None
+        self.use_plan_table = os.environ.get("TGNX_PLAN_TABLE", "1") != "0"
         self.dst_nodes = None if dst_nodes is None else torch.as_tensor(dst_nodes).to(self.dev, torch.long).contiguous()
         self.seed, self.rank, self.world = int(seed), int(rank), int(world)
         self.fuse_adam = True
@@ -367,6 +370,7 @@ class TgnEngine:
         b.ctl, b.out_pos, b.out_neg, b.mrr, b.ws = _p(self.ctl), _p(self.out_pos), _p(self.out_neg), _p(self.mrr), _p(self.ws)
         b.xrows, b.xcap = _p(self.xrows), (0 if self.xrows is None else self.xcap)
         b.out_ev = _p(self.out_ev)
+        b.plan_table = _p(self.plan_table)
         return b
 
     def _stream(self):
@@ -462,6 +466,14 @@ class TgnEngine:
         self._res = (int(split_lo), int(split_hi), int(batch))
         self._res_drop = 1 if dropout else 0
         self._prefetched = False
+        self.plan_table = None
+        if self.use_plan_table:   # the split's ring-insert / store plans, built once for every batch
+            nbytes = int(_lib.lib().tgnx_tgn_plan_table_bytes(ctypes.byref(self.cfg), *self._res))
+            if nbytes == 0:
+                raise RuntimeError(f"tgnx_tgn_plan_table_bytes: {_lib.lib().tgnx_last_error().decode()}")
+            self.plan_table = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+            _lib.call("tgnx_tgn_plan_table", ctypes.byref(self.cfg), ctypes.byref(self._buffers(0)), *self._res,
+                      _p(self.plan_table), nbytes, self._stream())
         self._res_buf = self._buffers(_p(self.neg_train))
         L = _lib.lib()
         self._res_fused = self._fused()
