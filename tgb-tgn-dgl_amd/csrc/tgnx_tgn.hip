@@ -4384,9 +4384,9 @@ int tgnx_tgn_plan_table(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf,
   const int64_t nb = (split_hi - split_lo + batch - 1) / batch;
   if (nb == 0) return TGNX_OK;
   const size_t smem = tgn_scan_smem(k.B);
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tgn_plan_table_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-  TGNX_CHECK_ARG(attr && smem <= 160 * 1024, "tgnx_tgn_plan_table: dynamic LDS");
+  TGNX_CHECK_ARG(hipFuncSetAttribute(reinterpret_cast<const void*>(&tgn_plan_table_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) == hipSuccess,
+                 "tgnx_tgn_plan_table: dynamic LDS of %zu bytes refused", smem);
   tgn_plan_table_kernel<<<(unsigned)(nb * 2 * c.pplan), 1024, smem, as_stream(stream)>>>(
       c, reinterpret_cast<char*>(table), plan_slot_bytes(k.B), split_lo, split_hi, batch);
   TGNX_LAUNCH_CHECK("tgn_plan_table");
