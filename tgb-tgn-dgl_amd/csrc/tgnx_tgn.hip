@@ -2744,8 +2744,15 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
 // coalesced stores) and summed into dP by tgn_kv_reduce: a hub neighbour is shared by most centres (a
 // wiki-shaped hub user sits in ~40 % of the page rings), and per-edge global atomics on its row
 // serialised at the L2 (attn_bwd 36 us, 15 us without them).
-__global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv) {
+// nwalk (parity-set steps with a plan table, TGNX_WALK_AT 1): the last block walks the NEXT batch's node sets
+// into the other parity's set (cw; the plans come from the table), instead of a workgroup of the dW_cell launch
+__global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int nwalk, Ctx cw) {
   TGNX_STAMP(6);
+  if ((int)blockIdx.x >= (int)gridDim.x - nwalk) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char wsm[];
+    scan_body<true, NoCheckpoint, 512>(cw, 0, wsm, NoCheckpoint{}, 1, false);
+    return;
+  }
   if ((int)blockIdx.x >= ncb + nkv) {
     lp_vec_body(c, ((int)blockIdx.x - ncb - nkv) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
     return;
@@ -3653,6 +3660,10 @@ struct MarkNextJob {
 #endif
 #ifndef TGNX_MD_CAP
 #define TGNX_MD_CAP 512  // grid cap of the step's M x D GEMMs (dz0, dX_enc): 7 column tiles at D = 100, ~30 row tiles at B = 200 (A/B 0.0966 vs 0.0971 ms with 1024)
+#endif
+#ifndef TGNX_WALK_AT
+#define TGNX_WALK_AT 0  // parity-set steps with a plan table: the next batch's node-set walk in the dW_cell launch (0)
+                        // or the attention-backward launch (1); TGNX_WALK_AT in the environment overrides
 #endif
 #ifndef TGNX_PLANS_IN_PRED
 #define TGNX_PLANS_IN_PRED 4  // parity-set steps whose plans have 2..N partitions: the plans in the predictor launch (0: never; DP floor A/B at world 2 / 4 / 8: N = 4 0.1034 / 0.1078 / 0.1283 ms, 16 0.1040 / 0.1087 / 0.1328, 0 0.1039 / 0.1176 / 0.1285)
@@ -4600,9 +4611,14 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // launch when its LDS holds the plans; else, for partitioned plans (data parallel: the global batch's
   // 2 B keys) that fit the predictor launch's LDS, the plans there and the walk alone in the dW_cell launch;
   // else its own launch after the dW_cell launch
-  // (with a plan table the scan is the walk alone: it rides when the rank's centres fit the launch's LDS)
-  const bool scan_w3 = ppm && (c.ptab ? scan_rides(c, kr, kr, (size_t)3 * MARK_LDS_WORDS * 4)
-                                      : scan_rides(c, k, kr, (size_t)3 * MARK_LDS_WORDS * 4));
+  // (with a plan table the scan is the walk alone: it rides when the rank's centres fit the launch's LDS; with
+  // TGNX_WALK_AT 1 in the attention-backward launch instead of the dW_cell launch)
+  static const int walk_at = env_int("TGNX_WALK_AT", TGNX_WALK_AT);
+  const bool walk_bwd = ppm && c.ptab && walk_at == 1 && !two && scan_rides(c, kr, kr, (size_t)3 * MARK_LDS_WORDS * 4);
+  const int nwalk = walk_bwd ? 1 : 0;
+  const uint32_t walk_lds = walk_bwd ? (uint32_t)(3 * kr.B * 12 + 16) : 0u;
+  const bool scan_w3 = ppm && !walk_bwd && (c.ptab ? scan_rides(c, kr, kr, (size_t)3 * MARK_LDS_WORDS * 4)
+                                                   : scan_rides(c, k, kr, (size_t)3 * MARK_LDS_WORDS * 4));
   static const int plans_in_pred = env_int("TGNX_PLANS_IN_PRED", TGNX_PLANS_IN_PRED);  // (runtime A/B switch)
   const bool plans_pred = ppm && !c.ptab && !scan_w3 && plans_in_pred && c.pplan > 1 && c.pplan <= plans_in_pred &&
                           2 * k.B <= PRED_PLAN_MAXE * 256 &&
@@ -4635,7 +4651,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     // conv2 backward (‖ predictor reductions) -> dP2, dE2; then dh1 = dP2 [Wq2; Wk2; Wv2; Wsk2] ‖ dW_proj2,
     // dW_edge2 (deferred) ‖ conv2's lin_edge -> Δt-encoding partials; then conv backward from dh1
     const int ncb1 = gridn(kr.R1tr, 4, 1 << 20);
-    tgn_attn_bwd<<<ncb1 + gridn(3 * D + 2, 4), 256, 0, s>>>(cr, ncb1, 0);
+    tgn_attn_bwd<<<ncb1 + gridn(3 * D + 2, 4), 256, 0, s>>>(cr, ncb1, 0, 0, cr);
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
     // conv2's (dk, dv) sums ‖ its dE2-only GEMMs (as in the 1-hop step below), then dh1 ‖ dW_proj2
     gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{cr}, gridn(kr.E1tr, KVR_CH, 1 << 20)},
@@ -4652,11 +4668,12 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                                EpiDeferred{}, c.pE));
     TGNX_LAUNCH_CHECK("tgn_dh1");
     const int ncb = gridn(kr.Rtr, 4, 1 << 20), nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
-    tgn_attn_bwd<<<ncb + nkv, 256, 0, s>>>(c, ncb, nkv);
+    tgn_attn_bwd<<<ncb + nkv, 256, 0, s>>>(c, ncb, nkv, 0, c);
   } else {
     const int ncb = gridn(kr.Rtr, 4, 1 << 20);
     const int nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
-    launch_k(tgn_attn_bwd, dim3(ncb + nkv + gridn(3 * D + 2, 4)), dim3(256), 0, s, c, ncb, nkv);
+    launch_k(tgn_attn_bwd, dim3(ncb + nkv + gridn(3 * D + 2, 4) + nwalk), dim3(256), walk_lds, s, c, ncb, nkv, nwalk,
+             nwalk ? cn : c);
   }
   probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_attn_bwd");
@@ -4706,12 +4723,12 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                                     EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, (float*)nullptr);
   // ppm: the next batch's scan (into set 1 - pp; the counters advance in the fixup launch) as this launch's
   // first workgroups when it fits their LDS, else its own launch after it
-  const auto j_scan = BlockJob<ScanJob, 3 * MARK_LDS_WORDS>{ScanJob{cn}, plans_pred || c.ptab ? 1 : 1 + 2 * c.pplan};
+  const auto j_scan = BlockJob<ScanJob, 3 * MARK_LDS_WORDS>{ScanJob{cn}, walk_bwd ? 0 : plans_pred || c.ptab ? 1 : 1 + 2 * c.pplan};
   const auto j_snap = BlockJob<SnapJob>{SnapJob{c, ppm ? 1 : 0}, 1};
   const auto j_store = BlockJob<StoreJob>{StoreJob{c, nst}, nst};
   // (the scan may ride in the dz0 launch instead: TGNX_SCAN_AT 6)
   const bool scan6 = scan_w3 && kvf && TGNX_SCAN_AT == 6;
-  const bool walk_w3 = scan_w3 || plans_pred;  // (the walk rides in the dW_cell launch)
+  const bool walk_w3 = (scan_w3 || plans_pred) && !walk_bwd;  // (the walk rides in the dW_cell launch)
   auto l8 = [&](auto... jobs) {
     probe_begin(TGNX_K_WGRAD3, s);
     // the GEMM jobs before the snapshot / store blocks (0.0970 vs 0.0986 ms with those first)
@@ -4733,7 +4750,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   } else {
     if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) return rc;
   }
-  if (ppm && !walk_w3) {
+  if (ppm && !walk_w3 && !walk_bwd) {
     tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(cn, 1, 0);
     TGNX_LAUNCH_CHECK("tgn_scan_early");
   }
