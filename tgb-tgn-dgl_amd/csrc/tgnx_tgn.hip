@@ -3662,8 +3662,10 @@ struct MarkNextJob {
 #define TGNX_MD_CAP 512  // grid cap of the step's M x D GEMMs (dz0, dX_enc): 7 column tiles at D = 100, ~30 row tiles at B = 200 (A/B 0.0966 vs 0.0971 ms with 1024)
 #endif
 #ifndef TGNX_WALK_AT
-#define TGNX_WALK_AT 0  // parity-set steps with a plan table: the next batch's node-set walk in the dW_cell launch (0)
-                        // or the attention-backward launch (1); TGNX_WALK_AT in the environment overrides
+#define TGNX_WALK_AT 1  // parity-set steps with a plan table: the next batch's node-set walk in the dW_cell launch (0)
+                        // or the attention-backward launch (1; same-box A/B: wiki step 0.0982 vs 0.0988 ms, dW_cell
+                        // launch span 17.2 -> 14.6 us, DP floor at world 2 / 4 / 8 -1.3 / -1.0 / -0.7 %);
+                        // TGNX_WALK_AT in the environment overrides
 #endif
 #ifndef TGNX_PLANS_IN_PRED
 #define TGNX_PLANS_IN_PRED 4  // parity-set steps whose plans have 2..N partitions: the plans in the predictor launch (0: never; DP floor A/B at world 2 / 4 / 8: N = 4 0.1034 / 0.1078 / 0.1283 ms, 16 0.1040 / 0.1087 / 0.1328, 0 0.1039 / 0.1176 / 0.1285)
