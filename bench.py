@@ -506,7 +506,9 @@ def run_tgn(args, world, rank, dev):
                     and args.updater == "gru" and not args.global_batch)
     pmc = _pmc(pmc_workload)
     step_algo = tgn_step_bytes(d, D, K, args.layers) * Bw          # per GPU per step
-    pmc_step = sum(v.get("bytes_per_launch", 0) for k, v in pmc.items() if k.startswith("tgn_")) if pmc else None
+    # the launches of the benched step (probes that ran: the parity-set step has no separate mark / scan /
+    # attention-forward / k-v / Adam launch)
+    pmc_step = sum(v.get("bytes_per_launch", 0) for k, v in pmc.items() if k in probes) if pmc else None
     roofline = {
         "bound": "hbm", "kernel": dom, "achieved": round(pd["gbs"], 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(pd["gbs"] / HBM_PEAK_GBS, 5),
