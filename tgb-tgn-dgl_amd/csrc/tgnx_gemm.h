@@ -320,8 +320,11 @@ __device__ __forceinline__ GemmWork gemm_work(const GemmShape& g, int Mr, int Nr
   const int L = (bid & 7) * per + (bid >> 3);
   w.ok = (bid >> 3) < per && L < T && tiles > 0;
   const int s = w.ok ? L / tiles : 0, tl = w.ok ? L - s * tiles : 0;
-  const int gw = GEMM_GROUP * max(tnr, 1), grp = tl / gw, m_first = grp * GEMM_GROUP;
-  const int gsz = max(1, min(tmr - m_first, GEMM_GROUP)), r = tl - grp * gw;
+  // GEMM_GROUP 0: groups of half the m-tiles, so that each XCD's ~T/8 tiles form a (tmr/2) x (tnr/4) rectangle
+  // (A fetched by 4 XCDs, B by 2, instead of a 4-row strip across ~all of B)
+  const int GG = GEMM_GROUP > 0 ? GEMM_GROUP : max(1, (tmr + 1) >> 1);
+  const int gw = GG * max(tnr, 1), grp = tl / gw, m_first = grp * GG;
+  const int gsz = max(1, min(tmr - m_first, GG)), r = tl - grp * gw;
   w.s = s;
   w.tm = m_first + r % gsz;
   w.tn = r / gsz;
