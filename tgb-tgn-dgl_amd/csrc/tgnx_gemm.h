@@ -884,8 +884,16 @@ constexpr int GEMM_FIX_SMEM = 64 * 65 + 512;  // floats: the largest C tile (G64
 // Sum the partials of several deferred GEMMs (block ranges in argument order); the first `head` blocks
 // and the blocks past the GEMMs call `tail(bid, smem)` (bid: 0 .. head - 1, then head, head + 1, ...):
 // extra work that rides in the same launch, the head blocks dispatched first.
+// XCD-contiguous tiles (TGNX_FIX_XCD): the fix range is padded to a multiple of the 8 XCDs and XCD x takes
+// the run [x nfix / 8, (x + 1) nfix / 8) of tiles in order, so the n-neighbour tiles of a weight row block run
+// on one XCD.  A 32-float tile row of a weight whose row length is not a multiple of 32 floats (572 + 1, 272,
+// 101, 100) straddles two 128-B lines shared with its neighbour tile; with bid-order tiles the neighbour ran on
+// another XCD and every Adam operand line (param, m, v) left HBM twice.
+#ifndef TGNX_FIX_XCD
+#define TGNX_FIX_XCD 1
+#endif
 template <class TAIL, class... F>
-__global__ void __launch_bounds__(256) gemm_fixup_kernel(TAIL tail, int head, F... f) {
+__global__ void __launch_bounds__(256) gemm_fixup_kernel(TAIL tail, int head, int nfix, F... f) {
   TGNX_STAMP(23);
   __shared__ __attribute__((aligned(16))) float smem[GEMM_FIX_SMEM];
   int bid = blockIdx.x;
@@ -894,7 +902,17 @@ __global__ void __launch_bounds__(256) gemm_fixup_kernel(TAIL tail, int head, F.
     return;
   }
   bid -= head;
-  if (!(gemm_fix_dispatch(f, bid, smem) || ...)) tail(head + bid, smem);
+  if (bid < nfix) {
+    if constexpr (TGNX_FIX_XCD) bid = (bid & 7) * (nfix >> 3) + (bid >> 3);
+    (gemm_fix_dispatch(f, bid, smem) || ...);  // (padding blocks: past every GEMM's tiles)
+    return;
+  }
+  tail(head + bid - nfix, smem);
+}
+template <class... F>
+inline int gemm_fix_range(const F&... f) {
+  const int nt = (gemm_fix_blocks(f) + ... + 0);
+  return TGNX_FIX_XCD ? (nt + 7) & ~7 : nt;
 }
 struct NoTail {
   __device__ void operator()(int, float*) const {}
@@ -944,14 +962,14 @@ static inline void gemm2_launch(const GemmShape& g1, const AL1& a1, const BL1& b
 }
 template <class TAIL, class... F>
 static inline void gemm_fixup_launch(int tail_blocks, const TAIL& tail, hipStream_t s, const F&... f) {
-  const int nb = (gemm_fix_blocks(f) + ... + 0) + tail_blocks;
-  if (nb > 0) launch_k(gemm_fixup_kernel<TAIL, F...>, dim3(nb), dim3(256), 0, s, tail, 0, f...);
+  const int nfix = gemm_fix_range(f...), nb = nfix + tail_blocks;
+  if (nb > 0) launch_k(gemm_fixup_kernel<TAIL, F...>, dim3(nb), dim3(256), 0, s, tail, 0, nfix, f...);
 }
 // the same with `head` of the tail blocks first in the grid
 template <class TAIL, class... F>
 static inline void gemm_fixup_launch_h(int head, int tail_blocks, const TAIL& tail, hipStream_t s, const F&... f) {
-  const int nb = (gemm_fix_blocks(f) + ... + 0) + tail_blocks;
-  if (nb > 0) launch_k(gemm_fixup_kernel<TAIL, F...>, dim3(nb), dim3(256), 0, s, tail, head, f...);
+  const int nfix = gemm_fix_range(f...), nb = nfix + tail_blocks;
+  if (nb > 0) launch_k(gemm_fixup_kernel<TAIL, F...>, dim3(nb), dim3(256), 0, s, tail, head, nfix, f...);
 }
 
 }  // namespace tgnx

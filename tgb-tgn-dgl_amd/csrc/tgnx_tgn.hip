@@ -39,6 +39,9 @@ namespace tgn {
 constexpr int TH = 2;        // TransformerConv heads (emb_module.py:66)
 constexpr int TDMAX = 128;   // memory / time / embedding dim capacity (C = D / 2 <= 64 lanes)
 constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touch keys)
+#ifndef TGNX_SIN_RECOMPUTE
+#define TGNX_SIN_RECOMPUTE 1  // the backward's Δt-encoding sine recomputed from (w, lu - t, b), not an [E][D] round trip
+#endif
 #ifndef TGNX_PRED_ATT_REC
 #define TGNX_PRED_ATT_REC 1  // per-root neighbour-row records for the attention in tgn_pred_train<ATT>
 #endif
@@ -1673,10 +1676,14 @@ __global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, 
 #pragma unroll
         for (int i = 0; i < 4; ++i) mv[i] = msg[min(lane + 64 * i, max(d - 1, 0))];  // (loads before the sincos)
         for (int q = lane; q < D; q += 64) {
-          float sn, cs;
-          te_sincos(fmaf(tw[q], dt, tb[q]), sn, cs);
-          row[q] = cs;
-          c.sinE[(int64_t)o * D + q] = sn;
+          if constexpr (TGNX_SIN_RECOMPUTE) {
+            row[q] = te_cos(fmaf(tw[q], dt, tb[q]));
+          } else {
+            float sn, cs;
+            te_sincos(fmaf(tw[q], dt, tb[q]), sn, cs);
+            row[q] = cs;
+            c.sinE[(int64_t)o * D + q] = sn;
+          }
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -3143,6 +3150,7 @@ struct EpiTeEdge {
   int D;
   const int* map = nullptr;
   int row0 = 0;
+  const float *tw = nullptr, *tb = nullptr;  // TGNX_SIN_RECOMPUTE: the time encoder (sin from Δt, not sinE)
   template <class T>
   __device__ void operator()(const T& t) const {
     constexpr int groups = 256 / T::tn, per = T::tm / groups;
@@ -3160,10 +3168,22 @@ struct EpiTeEdge {
       const bool ok = e < t.M && n < t.N;
       ej[i] = ok ? e_j[e2[i]] : 0;
       et[i] = ok ? e_t[e2[i]] : 0.f;
-      sn[i] = ok ? sinE[(int64_t)e2[i] * D + n] : 0.f;
+      if constexpr (!TGNX_SIN_RECOMPUTE) sn[i] = ok ? sinE[(int64_t)e2[i] * D + n] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < per; ++i) dt[i] = lu[ej[i]] - et[i];
+    if constexpr (TGNX_SIN_RECOMPUTE) {
+      // the forward's own argument (tgn_agg_emit: fmaf(w, lu - t, b), same lu / t), so the same sin
+      const int nc = min(n, D - 1);
+      const float w = tw[nc], b = tb[nc];
+#pragma unroll
+      for (int i = 0; i < per; ++i) {
+        float cs;
+        te_sincos(fmaf(w, dt[i], b), sn[i], cs);
+        const int e = t.m0 + g + groups * i;
+        if (!(e < t.M && n < t.N)) sn[i] = 0.f;
+      }
+    }
     float sw = 0.f, sb = 0.f;
 #pragma unroll
     for (int i = 0; i < per; ++i) {
@@ -3992,7 +4012,7 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.tgp_rows = W.tgp_e1 + (k.E1tr + G32::TM - 1) / G32::TM;
   W.tgp = carve(off, (size_t)W.tgp_rows * 2 * D * 4);
   W.encE = carve(off, (size_t)k.Ecap * (D + k.d) * 4);  // train: [cos enc | msg] rows; eval: cos rows (stride D)
-  W.sinE = carve(off, (size_t)k.Etr * D * 4);
+  W.sinE = carve(off, TGNX_SIN_RECOMPUTE ? 0 : (size_t)k.Etr * D * 4);
   W.s0m = carve(off, (size_t)k.Mtr * D * 4);
   W.s1m = carve(off, (size_t)k.Mtr * D * 4);
   W.pA = carve(off, gemm_partial_floats(shp_dWe(k, nullptr)) * 4);
@@ -4661,7 +4681,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                                EpiDeferred{}, c.pF),
                  gemm_job<G32>(gemm_shape<G32>(kr.E1tr, D, HC, c.cnt + CNT_E1), LoadRowK{c.dE2, kr.E1tr, HC, HC},
                                LoadKRow{P + c.L.we2, D, HC, D + d},
-                               EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, c.e1_e2, c.tgp_e1}, (float*)nullptr));
+                               EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, c.e1_e2, c.tgp_e1, P + c.L.te_w, P + c.L.te_b}, (float*)nullptr));
     TGNX_LAUNCH_CHECK("tgn_kv_reduce2");
     gemmN_launch(s,
                  gemm_job<G32L>(gemm_shape<G32L>(kr.Rtr, HC, 4 * HC, c.cnt + CNT_R), LoadRowK{c.dP2, kr.Rtr, 4 * HC, 4 * HC},
@@ -4689,7 +4709,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const auto j_dwe = gemm_job<GW>(shp_dWe(kr, c.cnt), LoadKRow{c.dE, HC, kr.Etr, HC}, LoadKRow{c.encE, D + d, kr.Etr, D + d},
                                   EpiDeferred{}, c.pA);
   const auto j_denc = gemm_job<G32>(gemm_shape<G32>(kr.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, kr.Etr, HC, HC},
-                                    LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D},
+                                    LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, nullptr, 0, P + c.L.te_w, P + c.L.te_b},
                                     (float*)nullptr);
   if (!kvf) {
     probe_begin(TGNX_K_KV, s);

@@ -32,12 +32,42 @@ KERNELS = {
 }
 
 
-def load(path):
-    """kernel name -> list of per-dispatch counter values (KB)"""
+def load(path, counter=None):
+    """kernel name -> list of per-dispatch counter values (KB; raw counters: counts), one counter per call"""
     out = {}
     for r in csv.DictReader(open(path)):
-        out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+        if counter is None or r["Counter_Name"] == counter:
+            out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     return out
+
+
+# exact memory-side bytes from the raw request counters (tools/pmc_calib.hip on the box: every coalesced read
+# width — 4, 8, 16 B per lane — goes out as 128-B requests, counted in TCC_EA0_RDREQ_128B; FETCH_SIZE tallies
+# them at 64 B, hence its factor 2; writes are 64-B or 32-B requests and WRITE_SIZE is exact):
+#   read  = 128 RDREQ_128B + 64 RDREQ_64B + 32 RDREQ_32B      (RDREQ = their sum)
+#   write = 64 WRREQ_64B + 32 (WRREQ - WRREQ_64B)
+RAW_RD = {"TCC_EA0_RDREQ_128B_sum": 128, "TCC_EA0_RDREQ_64B_sum": 64, "TCC_EA0_RDREQ_32B_sum": 32}
+
+
+def raw_bytes(rd_csv, wr_csv, keys):
+    """per-launch (read, write, 64-B read requests) bytes of the kernels matching keys, or None"""
+    rd = 0.0
+    n64 = 0.0
+    for ctr, sz in RAW_RD.items():
+        t = load(rd_csv, ctr)
+        v = [x for n in t if match(n, keys) for x in t[n]]
+        if not v:
+            return None
+        rd += sz * sum(v) / len(v)
+        if sz == 64:
+            n64 = sum(v) / len(v)
+    tw, t64 = load(wr_csv, "TCC_EA0_WRREQ_sum"), load(wr_csv, "TCC_EA0_WRREQ_64B_sum")
+    w = [x for n in tw if match(n, keys) for x in tw[n]]
+    w64 = [x for n in t64 if match(n, keys) for x in t64[n]]
+    if not w or not w64:
+        return None
+    a, b = sum(w) / len(w), sum(w64) / len(w64)
+    return rd, 64 * b + 32 * (a - b), n64
 
 
 def match(name, keys):
@@ -51,11 +81,9 @@ def main(d):
     for model in ("tgn", "tgnn"):
         f = glob.glob(os.path.join(d, f"{model}_fetch", "**", "*counter_collection.csv"), recursive=True)
         w = glob.glob(os.path.join(d, f"{model}_write", "**", "*counter_collection.csv"), recursive=True)
-        if not f or not w:
-            continue
-        fe, wr = load(f[0]), load(w[0])
+        fe, wr = (load(f[0]), load(w[0])) if f and w else ({}, {})
         for probe, sel in KERNELS.items():
-            if not probe.startswith(model + "_"):
+            if not fe or not probe.startswith(model + "_"):
                 continue
             fkb = wkb = 0.0
             launches = None
@@ -72,6 +100,18 @@ def main(d):
             else:
                 res[probe] = {"fetch_kb": round(fkb, 2), "write_kb": round(wkb, 2), "launches": launches,
                               "bytes_per_launch": int((2 * fkb + wkb) * 1024)}
+        rf = glob.glob(os.path.join(d, f"{model}_rd", "**", "*counter_collection.csv"), recursive=True)
+        rw = glob.glob(os.path.join(d, f"{model}_wr", "**", "*counter_collection.csv"), recursive=True)
+        if rf and rw:
+            for probe, sel in KERNELS.items():
+                if not probe.startswith(model + "_"):
+                    continue
+                r = raw_bytes(rf[0], rw[0], sel)
+                if r is None:
+                    continue
+                e = res.setdefault(probe, {})
+                e["raw_read_bytes"], e["raw_write_bytes"], e["raw_rdreq_64b"] = int(r[0]), int(r[1]), int(r[2])
+                e["raw_bytes_per_launch"] = int(r[0] + r[1])
     print(json.dumps(res, indent=1))
 
 
