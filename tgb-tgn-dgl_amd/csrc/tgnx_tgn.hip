@@ -39,6 +39,10 @@ namespace tgn {
 constexpr int TH = 2;        // TransformerConv heads (emb_module.py:66)
 constexpr int TDMAX = 128;   // memory / time / embedding dim capacity (C = D / 2 <= 64 lanes)
 constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touch keys)
+#ifndef TGNX_DENSE_H
+#define TGNX_DENSE_H 1  // GRU train step: the GRU forward also stores its rows' pre-update memory densely ([M][D], Hp),
+                        // so the GRU backward and dW_gru read rows instead of gathering memory through node ids
+#endif
 #ifndef TGNX_SIN_RECOMPUTE
 #define TGNX_SIN_RECOMPUTE 1  // the backward's Δt-encoding sine recomputed from (w, lu - t, b), not an [E][D] round trip
 #endif
@@ -198,6 +202,7 @@ struct Ctx {
                // the same values)
   int64_t* xw;
   float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
+  float* Hp;  // TGNX_DENSE_H (GRU train step): row m's pre-update memory mem[nid[m]] [M][D], written by the GRU forward
   float *dZc, *dP, *dE, *dG, *tgp;
   // resident batch cursor folded into tgn_mark (tgnx_tgn_train_step_resident): mark derives the batch
   // descriptor from the step counters, the step's last launch advances them
@@ -1795,6 +1800,7 @@ struct EpiGru {
   int64_t base;
   int D;
   float *Z0, *gates;
+  float* Hp = nullptr;  // (train step, TGNX_DENSE_H) the row's pre-update memory, stored densely
   // thread x < 64 of a 16 x 16 tile: row x / 4, unit n0 / 4 + x % 4 — its biases and memory entry, loaded
   // with the tile's first operand round (gemm_tile_direct); rowidx(r) = row r's node (LoadGruA's index)
   struct Pre {
@@ -1829,6 +1835,7 @@ struct EpiGru {
     Z0[(int64_t)m * D + j] = (p.h - nn) * zz + nn;
     float4* gp = reinterpret_cast<float4*>(gates + ((int64_t)m * D + j) * 4);
     *gp = make_float4(rr, zz, nn, ghn);
+    if (Hp) Hp[(int64_t)m * D + j] = p.h;
   }
   template <class T>  // (staged tiles of any shape: the loads after the MFMAs)
   __device__ void operator()(const T& t) const {
@@ -1848,6 +1855,7 @@ struct EpiGru {
       Z0[(int64_t)m * D + j] = (h - nn) * zz + nn;
       float4* gp = reinterpret_cast<float4*>(gates + ((int64_t)m * D + j) * 4);
       *gp = make_float4(rr, zz, nn, ghn);
+      if (Hp) Hp[(int64_t)m * D + j] = h;
     }
   }
 };
@@ -2313,7 +2321,7 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
     const int st = ATT ? tid : tid - 64;  // NST staging threads
     if (blockIdx.x == 0 && st == 0) {
       c.cnt[CNT_LIST] = 3 * (hi - lo);
-      if (c.adf.p) {  // fused Adam: this step's scalars for the gradient writers (tgn_adam computes them itself)
+      {  // this step's Adam scalars for the gradient writers (fused) or tgn_adam (the separate pass after the step)
         const int64_t t = c.ctl[TGNX_CTL_ADAM_T] + (c.adv ? 1 : 0);
         float* sc = reinterpret_cast<float*>(c.ctl + TGNX_CTL_ADAM_SC);
         sc[0] = (float)(c.lr / (1.0 - pow((double)c.b1, (double)t)));
@@ -3226,22 +3234,25 @@ struct EpiGruBwd {
   const int64_t* nid;
   float* dG;
   int D;
+  const float* Hp = nullptr;  // TGNX_DENSE_H: the rows' pre-update memory (no node-id gather)
   // a 16 x 16 tile's element of this thread (GemmTile<16, 16>::row_of / col_of (0)): its node and saved gates,
   // loaded with the tile's first operand round (gemm_tile_direct)
   struct Pre {
     int64_t node;
     float4 gt;
+    float h;
   };
   template <class RI>
   __device__ Pre pre(int m0, int n0, int M, int N, RI) const {
     const int m = min(m0 + GemmTile<16, 16>::row_of(0), M - 1), j = min(n0 + GemmTile<16, 16>::col_of(0), N - 1);
-    return Pre{nid[m], *reinterpret_cast<const float4*>(gates + ((int64_t)m * D + j) * 4)};
+    if (Hp) return Pre{0, *reinterpret_cast<const float4*>(gates + ((int64_t)m * D + j) * 4), Hp[(int64_t)m * D + j]};
+    return Pre{nid[m], *reinterpret_cast<const float4*>(gates + ((int64_t)m * D + j) * 4), 0.f};
   }
   template <class T>
   __device__ void operator()(const T& t, const Pre& p) const {
     static_assert(T::per == 1, "16 x 16 tiles");
     const int r = T::row_of(0), cc = T::col_of(0), m = t.m0 + r, j = t.n0 + cc;
-    const float h = mem[p.node * D + min(j, t.N - 1)];
+    const float h = Hp ? p.h : mem[p.node * D + min(j, t.N - 1)];
     if (m >= t.M || j >= t.N) return;
     const float dhp = t(r, cc);
     const float rr = p.gt.x, zz = p.gt.y, nn = p.gt.z, ghn = p.gt.w;
@@ -3260,11 +3271,14 @@ struct EpiGruBwd {
     for (int i = 0; i < T::per; ++i) {  // gathers first (no stores in between)
       const int m = t.m0 + T::row_of(i), j = t.n0 + T::col_of(i);
       const bool ok = m < t.M && j < t.N;
-      node[i] = ok ? nid[m] : 0;
+      node[i] = ok && !Hp ? nid[m] : 0;
       gt[i] = ok ? *reinterpret_cast<const float4*>(gates + ((int64_t)m * D + j) * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int i = 0; i < T::per; ++i) h[i] = mem[node[i] * D + t.n0 + T::col_of(i)];
+    for (int i = 0; i < T::per; ++i) {
+      const int m = min(t.m0 + T::row_of(i), t.M - 1), j = min(t.n0 + T::col_of(i), t.N - 1);
+      h[i] = Hp ? Hp[(int64_t)m * D + j] : mem[node[i] * D + t.n0 + T::col_of(i)];
+    }
 #pragma unroll
     for (int i = 0; i < T::per; ++i) {
       const int r = T::row_of(i), cc = T::col_of(i), m = t.m0 + r, j = t.n0 + cc;
@@ -3292,6 +3306,17 @@ struct LoadGruAT1 {
   __device__ float load(Idx v, int n, int m) const {
     const bool x = n < Qm, one = n >= Qm + D;
     return *(x ? X + (int64_t)m * Qm + n : one ? kOne4 : mem + v * D + (n - Qm));
+  }
+};
+// the same with the rows' pre-update memory stored densely (TGNX_DENSE_H): no node-id round per K chunk
+struct LoadGruAT1H {
+  const float* X;
+  const float* Hp;
+  int Qm, D;
+  static constexpr bool k_fast = false;
+  __device__ float operator()(int n, int m) const {
+    const bool x = n < Qm, one = n >= Qm + D;
+    return *(x ? X + (int64_t)m * Qm + n : one ? kOne4 : Hp + (int64_t)m * D + (n - Qm));
   }
 };
 struct EpiGruWGrad {
@@ -3447,7 +3472,19 @@ struct CellOps<0> {
   static __host__ EpiGru epi(const Ctx& c, const int64_t* list, int64_t base) {
     return EpiGru{c.params + c.L.b_ih, c.params + c.L.b_hh, c.mem, list, base, c.D, c.Z0, c.gates};
   }
-  static __host__ EpiGruBwd bwd(const Ctx& c) { return EpiGruBwd{c.gates, c.mem, c.nid, c.dG, c.D}; }
+  static __host__ EpiGru epi_train(const Ctx& c) {
+    EpiGru e = epi(c, c.nid, 0);
+    e.Hp = TGNX_DENSE_H ? c.Hp : nullptr;
+    return e;
+  }
+  static __host__ EpiGruBwd bwd(const Ctx& c) {
+    return EpiGruBwd{c.gates, c.mem, c.nid, c.dG, c.D, TGNX_DENSE_H ? c.Hp : nullptr};
+  }
+  // B operand of dW_cell = dGᵀ [X | H | 1]
+  static __host__ auto hT(const Ctx& c) {
+    if constexpr (TGNX_DENSE_H) return LoadGruAT1H{c.X, c.Hp, c.Qm, c.D};
+    else return LoadGruAT1{c.X, c.mem, c.nid, c.Qm, c.D};
+  }
   static __host__ EpiGruWGrad wgrad(const Ctx& c) {
     return EpiGruWGrad{c.grads, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, c.Qm, c.D, c.adf};
   }
@@ -3460,7 +3497,9 @@ struct CellOps<1> {
   static __host__ EpiRnn epi(const Ctx& c, const int64_t*, int64_t) {
     return EpiRnn{c.params + c.L.b_ih, c.params + c.L.b_hh, c.D, c.Z0};
   }
+  static __host__ EpiRnn epi_train(const Ctx& c) { return epi(c, c.nid, 0); }
   static __host__ EpiRnnBwd bwd(const Ctx& c) { return EpiRnnBwd{c.Z0, c.dG, c.D}; }
+  static __host__ LoadGruAT1 hT(const Ctx& c) { return LoadGruAT1{c.X, c.mem, c.nid, c.Qm, c.D}; }
   static __host__ EpiRnnWGrad wgrad(const Ctx& c) {
     return EpiRnnWGrad{c.grads, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, c.Qm, c.D, c.adf};
   }
@@ -3528,26 +3567,23 @@ __global__ void __launch_bounds__(256) tgn_adam(Ctx c, float* rows, int64_t nrow
     apply_rows_body(c.mem, c.lu_buf, rows, nrows, c.D, c.N, (int)blockIdx.x - ((int)gridDim.x - nrb), nrb);
     return;
   }
-  __shared__ float sc[2];
-  const int64_t B = c.ctl[TGNX_CTL_STEP_B];
-  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  if (threadIdx.x == 0) {
-    const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
-    sc[0] = (float)(c.lr / (1.0 - pow((double)c.b1, (double)t)));
-    sc[1] = (float)sqrt(1.0 - pow((double)c.b2, (double)t));
-    if (blockIdx.x == 0) *reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS) += (double)c.grads[c.L.total] * (double)B;
-  }
-  __syncthreads();
-  const float step = sc[0], bc2s = sc[1];
+  // one load round: the step's B / error words and Adam scalars (tgn_pred_train wrote them for this t) with this
+  // thread's elements (the separate optimizer pass of the data-parallel step heads the next step's graph)
   const int64_t n4 = c.L.total / 4;
   const int nab = (int)gridDim.x - nrb;
   float4* P4 = reinterpret_cast<float4*>(c.params);
   float4* M4 = reinterpret_cast<float4*>(c.am);
   float4* V4 = reinterpret_cast<float4*>(c.av);
   const float4* G4 = reinterpret_cast<const float4*>(c.grads);
+  const int64_t B = c.ctl[TGNX_CTL_STEP_B], err = c.ctl[TGNX_CTL_ERR];
+  const float* sc = reinterpret_cast<const float*>(c.ctl + TGNX_CTL_ADAM_SC);
+  const float step = sc[0], bc2s = sc[1];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && B != 0 && err == 0)
+    *reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS) += (double)c.grads[c.L.total] * (double)B;
   for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < n4; x += (int64_t)nab * blockDim.x) {
     const float4 g = G4[x];
     float4 m = M4[x], v = V4[x], p = P4[x];
+    if (B == 0 || err != 0) return;
     adam1(g.x, m.x, v.x, p.x, c.b1, c.b2, c.eps, step, bc2s);
     adam1(g.y, m.y, v.y, p.y, c.b1, c.b2, c.eps, step, bc2s);
     adam1(g.z, m.z, v.z, p.z, c.b1, c.b2, c.eps, step, bc2s);
@@ -3947,7 +3983,7 @@ static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_spl
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, std::min(TGNX_DWG_SMAX, ksplit(k.Mtr, TGNX_S_WG))); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, kj, kx, ke, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
-      Ep, alpha, alk, Qo, Zc, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
+      Ep, alpha, alk, Qo, Zc, Hp, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
       snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF,
       uX, uZ, uG, ulu, uxw, utrel, total;
   int tgp_rows, tgp_e1;
@@ -3988,6 +4024,7 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.lu = carve(off, (size_t)k.Mcap * 4);
   W.xw = carve(off, (size_t)k.Mcap * 8);
   W.gates = carve(off, (size_t)k.Mcap * 4 * D * 4);
+  W.Hp = carve(off, TGNX_DENSE_H ? (size_t)k.Mcap * D * 4 : 0);
   W.Z0 = carve(off, (size_t)k.Mcap * D * 4);
   W.P = carve(off, (size_t)k.Mcap * 4 * HC * 4);
   W.Ep = carve(off, (size_t)k.Ecap * HC * 4);
@@ -4176,6 +4213,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.lu = reinterpret_cast<float*>(ws + W.lu);
   c.xw = reinterpret_cast<int64_t*>(ws + W.xw);
   c.gates = reinterpret_cast<float*>(ws + W.gates);
+  c.Hp = reinterpret_cast<float*>(ws + W.Hp);
   c.Z0 = reinterpret_cast<float*>(ws + W.Z0);
   c.P = reinterpret_cast<float*>(ws + W.P);
   c.Ep = reinterpret_cast<float*>(ws + W.Ep);
@@ -4575,7 +4613,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const bool two = k.layers == 2;
   const LoadAttrMap ea1{c.encE, c.e1_e2, D + d};  // root edge -> its outer edge's row
   const auto j_gru = gemm_job<G32L>(gemm_shape<G32L>(kr.Mtr, Cl::G * D, Qm + D, c.cnt + CNT_M),
-                                    LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0}, Cl::w(c), Cl::epi(c, c.nid, 0),
+                                    LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0}, Cl::w(c), Cl::epi_train(c),
                                     (float*)nullptr);
   const auto j_edge = gemm_job<G32>(gemm_shape<G32>(kr.Etr, HC, D + d, c.cnt + CNT_E), ea,
                                     LoadRowK{P + c.L.we, HC, D + d, D + d}, EpiStore{c.Ep, nullptr, HC, 0}, (float*)nullptr);
@@ -4739,7 +4777,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // ‖ the message stores ‖ the fixup's descriptor copy + the counter advance (SnapJob)
   const int nst = gridn(2 * k.B, 256);
   const auto j_dwg = gemm_job<GW>(shp_dWg(kr, c.cnt), LoadKRow{c.dG, Cl::G * D, kr.Mtr, Cl::G * D},
-                                  LoadGruAT1{c.X, c.mem, c.nid, Qm, D}, EpiDeferred{}, c.pD);
+                                  Cl::hT(c), EpiDeferred{}, c.pD);
   const auto j_dxe = gemm_job<G32L>(with_cap(gemm_shape<G32L>(kr.Mtr, D, Cl::G * D, c.cnt + CNT_M), TGNX_MD_CAP),
                                     LoadRowK{c.dG, kr.Mtr, Cl::G * D, Cl::G * D}, Cl::wenc(c),
                                     EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, (float*)nullptr);
