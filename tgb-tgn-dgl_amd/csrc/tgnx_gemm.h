@@ -800,6 +800,24 @@ static inline void gemmN_launch(hipStream_t s, const J&... j) {
   const int nb = (job_blocks(j) + ... + 0);
   if (nb > 0) launch_k(gemmN_kernel<J...>, dim3(nb), dim3(256), 0, s, j...);
 }
+// the same with a waves-per-SIMD floor for one launch (its register budget capped so W workgroups fit a CU)
+template <int W, class... J>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) gemmN_kernel_w(J... j) {
+  TGNX_STAMP(22);
+  constexpr int SM = std::max({J::Cfg::SMEM...});
+  __shared__ __attribute__((aligned(16))) float smem[SM];
+  int bid = blockIdx.x;
+  (void)(gemm_job_dispatch(j, bid, smem) || ...);
+}
+template <int W, class... J>
+static inline void gemmN_launch_w(hipStream_t s, const J&... j) {
+  const int nb = (job_blocks(j) + ... + 0);
+  if constexpr (W > 0) {
+    if (nb > 0) launch_k(gemmN_kernel_w<W, J...>, dim3(nb), dim3(256), 0, s, j...);
+  } else {
+    gemmN_launch(s, j...);
+  }
+}
 
 // ---------------------------------------------------------------- split-K fixup
 template <class CFG, class EPI>

@@ -39,6 +39,13 @@ namespace tgn {
 constexpr int TH = 2;        // TransformerConv heads (emb_module.py:66)
 constexpr int TDMAX = 128;   // memory / time / embedding dim capacity (C = D / 2 <= 64 lanes)
 constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touch keys)
+#ifndef TGNX_GRU_WAVES
+#define TGNX_GRU_WAVES 0  // waves-per-SIMD floor of the ring ‖ GRU ‖ lin_edge launch (1 hop)
+#endif
+#ifndef TGNX_W3_WAVES
+#define TGNX_W3_WAVES 7  // waves-per-SIMD floor of the dW_cell launch (0: the compiler's register count, 84 + 8 -> 5 waves;
+                         // same-box A/B: 0.0966 / 0.0961 ms, 6 waves 0.0961 / 0.0955, 7 (72 VGPRs, 12 B spilled) 0.0951 / 0.0951)
+#endif
 #ifndef TGNX_DENSE_H
 #define TGNX_DENSE_H 1  // GRU train step: the GRU forward also stores its rows' pre-update memory densely ([M][D], Hp),
                         // so the GRU backward and dW_gru read rows instead of gathering memory through node ids
@@ -1579,8 +1586,16 @@ __device__ __forceinline__ int root_row(const Ctx& c, int64_t v) {
 // The rest: mode 0 aggregation over the sampled nodes (train) + zeroing of the backward
 // accumulators, mode 1 last_update of the sampled nodes from the buffer (eval scoring), mode 2
 // aggregation over a node list (eval update / flush; list == nullptr: nodes base + m).
+#ifndef TGNX_AGG_WAVES
+#define TGNX_AGG_WAVES 0  // waves-per-SIMD floor of tgn_agg_emit (0: the compiler's register count)
+#endif
+#if TGNX_AGG_WAVES > 0
+#define TGNX_AGG_ATTR __attribute__((amdgpu_waves_per_eu(TGNX_AGG_WAVES)))
+#else
+#define TGNX_AGG_ATTR
+#endif
 template <int AG, bool EMB = false>
-__global__ void __launch_bounds__(256) tgn_agg_emit(Ctx c, int mode, int nedge, const int64_t* list,
+__global__ void __launch_bounds__(256) TGNX_AGG_ATTR tgn_agg_emit(Ctx c, int mode, int nedge, const int64_t* list,
                                                     const int* list_cnt, int n_host, int64_t base, int nevb = 0) {
   TGNX_STAMP(3);
   if (mode != 2) {
@@ -4624,7 +4639,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                  gemm_job<G32>(gemm_shape<G32>(kr.E1tr, HC, D + d, c.cnt + CNT_E1), ea1,
                                LoadRowK{P + c.L.we2, HC, D + d, D + d}, EpiStore{c.Ep2, nullptr, HC, 0}, (float*)nullptr));
   else
-    gemmN_launch(s, j_ring, j_gru, j_edge);
+    gemmN_launch_w<TGNX_GRU_WAVES>(s, j_ring, j_gru, j_edge);
   probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgn_gru_edge");
   const int nmark = gridn(3 * kr.B * 16, 256);
@@ -4795,7 +4810,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     if (walk_w3 && !scan6)
       gemmN_launch(s, j_scan, j_dxe, j_dwg, jobs..., j_snap, j_store);
     else
-      gemmN_launch(s, j_dxe, j_dwg, jobs..., j_snap, j_store);
+      gemmN_launch_w<TGNX_W3_WAVES>(s, j_dxe, j_dwg, jobs..., j_snap, j_store);
     probe_end(TGNX_K_WGRAD3, s);
     TGNX_LAUNCH_CHECK("tgn_wgrad3");
     return TGNX_OK;
