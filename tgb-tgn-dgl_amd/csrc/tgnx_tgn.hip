@@ -39,6 +39,12 @@ namespace tgn {
 constexpr int TH = 2;        // TransformerConv heads (emb_module.py:66)
 constexpr int TDMAX = 128;   // memory / time / embedding dim capacity (C = D / 2 <= 64 lanes)
 constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touch keys)
+#ifndef TGNX_GRU_CAP
+#define TGNX_GRU_CAP TGNX_GEMM_GRID_CAP  // grid cap of the GRU GEMM (its workgroups loop past it; 512: +0.3 %)
+#endif
+#ifndef TGNX_EDGE_CAP200
+#define TGNX_EDGE_CAP200 1024  // grid cap of the lin_edge GEMM per 200 events of the rank's batch (env TGNX_EDGE_CAP200)
+#endif
 #ifndef TGNX_GRU_WAVES
 #define TGNX_GRU_WAVES 0  // waves-per-SIMD floor of the ring ‖ GRU ‖ lin_edge launch (1 hop)
 #endif
@@ -3729,8 +3735,9 @@ struct MarkNextJob {
 #ifndef TGNX_KVF_MARK_AT
 #define TGNX_KVF_MARK_AT 5  // with TGNX_KV_FUSE: the launch of a non-parity pipelined step's next-batch marking (5 or 8)
 #endif
-#ifndef TGNX_MD_CAP
-#define TGNX_MD_CAP 512  // grid cap of the step's M x D GEMMs (dz0, dX_enc): 7 column tiles at D = 100, ~30 row tiles at B = 200 (A/B 0.0966 vs 0.0971 ms with 1024)
+#ifndef TGNX_MD_CAP200
+#define TGNX_MD_CAP200 512  // grid cap of the step's M x D GEMMs (dz0, dX_enc) per 200 events of the rank's batch (env
+                            // TGNX_MD_CAP200): 7 column tiles at D = 100, ~30 row tiles at B = 200 (A/B 0.0966 vs 0.0971 ms with 1024)
 #endif
 #ifndef TGNX_WALK_AT
 #define TGNX_WALK_AT 1  // parity-set steps with a plan table: the next batch's node-set walk in the dW_cell launch (0)
@@ -4388,6 +4395,11 @@ static inline int env_int(const char* name, int def) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : def;
 }
+// a GEMM grid cap that scales with the rank's batch (the runtime rows / edges do; the capacity shapes are worst cases)
+static inline int cap_per200(const char* env, int per200, int B) {
+  const int64_t v = (int64_t)env_int(env, per200) * std::max(B, 1) / 200;
+  return (int)std::max<int64_t>(64, std::min<int64_t>(TGNX_GEMM_GRID_CAP, v));
+}
 static inline int gridn(int64_t n, int per, int cap = 4096) {
   int64_t g = (n + per - 1) / per;
   if (g < 1) g = 1;
@@ -4627,10 +4639,12 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const LoadRowK ea{c.encE, kr.Etr, D + d, D + d};  // the edges' [cos enc | msg] rows (tgn_agg_emit, train)
   const bool two = k.layers == 2;
   const LoadAttrMap ea1{c.encE, c.e1_e2, D + d};  // root edge -> its outer edge's row
-  const auto j_gru = gemm_job<G32L>(gemm_shape<G32L>(kr.Mtr, Cl::G * D, Qm + D, c.cnt + CNT_M),
+  const int edge_cap = cap_per200("TGNX_EDGE_CAP200", TGNX_EDGE_CAP200, kr.B);
+  const int md_cap = cap_per200("TGNX_MD_CAP200", TGNX_MD_CAP200, kr.B);
+  const auto j_gru = gemm_job<G32L>(with_cap(gemm_shape<G32L>(kr.Mtr, Cl::G * D, Qm + D, c.cnt + CNT_M), TGNX_GRU_CAP),
                                     LoadGruA{c.X, c.mem, c.nid, 0, Qm, D, 0}, Cl::w(c), Cl::epi_train(c),
                                     (float*)nullptr);
-  const auto j_edge = gemm_job<G32>(gemm_shape<G32>(kr.Etr, HC, D + d, c.cnt + CNT_E), ea,
+  const auto j_edge = gemm_job<G32>(with_cap(gemm_shape<G32>(kr.Etr, HC, D + d, c.cnt + CNT_E), edge_cap), ea,
                                     LoadRowK{P + c.L.we, HC, D + d, D + d}, EpiStore{c.Ep, nullptr, HC, 0}, (float*)nullptr);
   const BlockJob<RingMergeJob> j_ring{RingMergeJob{c}, gridn(2 * k.B, 4)};
   probe_begin(TGNX_K_EDGE_FWD, s);
@@ -4781,7 +4795,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const auto j_dwp = gemm_job<GW>(shp_dWp(kr, c.cnt), LoadKRow{c.dP, 4 * HC, kr.Mtr, 4 * HC}, LoadZ1T{c.Z0, D}, EpiDeferred{}, c.pB);
   const auto j_dwlp = gemm_job<GW>(shp_dWlp(kr, c.cnt), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
                                    LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, EpiDeferred{}, c.pC);
-  const auto j_dz0 = gemm_job<G32L>(with_cap(gemm_shape<G32L>(kr.Mtr, D, 4 * HC, c.cnt + CNT_M), TGNX_MD_CAP), LoadRowK{c.dP, kr.Mtr, 4 * HC, 4 * HC},
+  const auto j_dz0 = gemm_job<G32L>(with_cap(gemm_shape<G32L>(kr.Mtr, D, 4 * HC, c.cnt + CNT_M), md_cap), LoadRowK{c.dP, kr.Mtr, 4 * HC, 4 * HC},
                                     LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, Cl::bwd(c), (float*)nullptr);
   auto l7 = [&](auto... jobs) {
     gemmN_launch(s, mk_at(8), jobs...);
@@ -4793,7 +4807,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const int nst = gridn(2 * k.B, 256);
   const auto j_dwg = gemm_job<GW>(shp_dWg(kr, c.cnt), LoadKRow{c.dG, Cl::G * D, kr.Mtr, Cl::G * D},
                                   Cl::hT(c), EpiDeferred{}, c.pD);
-  const auto j_dxe = gemm_job<G32L>(with_cap(gemm_shape<G32L>(kr.Mtr, D, Cl::G * D, c.cnt + CNT_M), TGNX_MD_CAP),
+  const auto j_dxe = gemm_job<G32L>(with_cap(gemm_shape<G32L>(kr.Mtr, D, Cl::G * D, c.cnt + CNT_M), md_cap),
                                     LoadRowK{c.dG, kr.Mtr, Cl::G * D, Cl::G * D}, Cl::wenc(c),
                                     EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, (float*)nullptr);
   // ppm: the next batch's scan (into set 1 - pp; the counters advance in the fixup launch) as this launch's
