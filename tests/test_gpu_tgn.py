@@ -282,16 +282,14 @@ def test_tgn_resident_folded_cursor_equals_advance_plus_step():
                                                 (1, "rnn", (1, 1))])
 def test_tgn_pipelined_equals_resident(layers, updater, emb, pp, table):
     """tgnx_tgn_train_step_pipelined (each step marks the next batch inside its predictor launch and scans it
-    after its last launch; ring insert beside the GRU) — or, pp (1 hop), tgnx_tgn_train_step_pp (the next batch
-    scanned into the other parity's set inside the k / v reduction launch, two graphs replayed alternately) —
+    after its last launch; ring insert beside the GRU) — or, pp (1 or 2 hops), tgnx_tgn_train_step_pp (the next
+    batch scanned into the other parity's set inside an earlier launch of the step, two graphs replayed alternately) —
     against tgnx_tgn_train_step_resident on a twin engine: graph replay (the first step eager with
     prefetched = 0), device negatives, attention dropout, a partial last batch and a step past the split.
     After every step: step counters and the ring exactly, this batch's negatives exactly (the pipelined
     engine has drawn the next batch's too), outputs, parameters and memory within the fused-Adam tolerances
     (resynchronised per step).  table: the parity-set step reads the split's plans from the table built at
     binding (tgnx_tgn_plan_table) instead of its scan's, which then only walks the node sets."""
-    if pp and layers == 2:
-        pytest.skip("parity sets are a 1-hop step (2 hops: the pipelined step)")
     engines = []
     for pipe in (True, False):
         s, ref, opt_ref, lref, model, opt, eng = _setup("last", layers=layers, updater=updater,

@@ -4012,6 +4012,7 @@ struct WsLay {
   // the scan's per-batch outputs of the second parity (tgnx_tgn_train_step_pp: a step reads its parity's
   // set while the next batch's scan writes the other)
   size_t cnt2, cent2, cent_loc2, ceoff2, crank2, upd_loc2, nid2, upd2, rkeys2, rruns2, skeys2, sruns2, pcnt2;
+  size_t x2r2, cent12, r_x22, ceoff12;  // (2 hops)
 };
 static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   WsLay W;
@@ -4127,6 +4128,10 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.skeys2 = carve(off, (size_t)n2 * 8);
   W.sruns2 = carve(off, (size_t)(n2 + 2 + TGNX_PLAN_PMAX) * 4);
   W.pcnt2 = carve(off, (size_t)4 * TGNX_PLAN_PMAX * 4);
+  W.x2r2 = carve(off, R2 * 4);
+  W.cent12 = carve(off, R1 * 8);
+  W.r_x22 = carve(off, R1 * 4);
+  W.ceoff12 = carve(off, two ? (R1 + 1) * 4 : 0);
   W.total = off;
   return W;
 }
@@ -4341,6 +4346,12 @@ static Ctx set_view(const Ctx& c, const WsLay& W, char* ws, int p) {
   v.rpo = v.rpc + TGNX_PLAN_PMAX;
   v.spc = v.rpo + TGNX_PLAN_PMAX;
   v.spo = v.spc + TGNX_PLAN_PMAX;
+  if (c.x2r) {  // 2 hops: the root level's sets
+    v.x2r = reinterpret_cast<int*>(at(W.x2r, W.x2r2));
+    v.cent1 = reinterpret_cast<int64_t*>(at(W.cent1, W.cent12));
+    v.r_x2 = reinterpret_cast<int*>(at(W.r_x2, W.r_x22));
+    v.ceoff1 = reinterpret_cast<int*>(at(W.ceoff1, W.ceoff12));
+  }
   return v;
 }
 
@@ -4599,8 +4610,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   }
   Ctx cn;  // ppm: the other parity's set (the next batch's scan writes it)
   if (ppm) {
-    TGNX_CHECK_ARG(pp <= 1 && pipe != 0 && !no_tail && k.layers == 1 && adv && (!fuse_adam || adv->world == 1),
-                   "tgnx_tgn_train_step_pp / tgnx_tgn_train_fwd_bwd_pp: a 1-hop resident step, parity 0 or 1 "
+    TGNX_CHECK_ARG(pp <= 1 && pipe != 0 && !no_tail && adv && (!fuse_adam || adv->world == 1),
+                   "tgnx_tgn_train_step_pp / tgnx_tgn_train_fwd_bwd_pp: a resident step, parity 0 or 1 "
                    "(Adam fused at world 1 only)");
     char* ws = reinterpret_cast<char*>(buf->ws);
     cn = set_view(c, W, ws, 1 - pp);
@@ -4703,10 +4714,15 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // (with a plan table the scan is the walk alone: it rides when the rank's centres fit the launch's LDS; with
   // TGNX_WALK_AT 1 in the attention-backward launch instead of the dW_cell launch)
   static const int walk_at = env_int("TGNX_WALK_AT", TGNX_WALK_AT);
-  const bool walk_bwd = ppm && c.ptab && walk_at == 1 && !two && scan_rides(c, kr, kr, (size_t)3 * MARK_LDS_WORDS * 4);
+  // (with a plan table the scan is the walk alone: its LDS is the centre staging, 3 B x 12 bytes, and the small-graph
+  // direct walk's <= 2 words per thread; 2 hops: the walk rides in conv1's attention-backward launch)
+  const auto walk_rides = [&](size_t lds) {
+    return (size_t)3 * kr.B * 12 <= lds && (!scan_direct(c.words) || c.words <= 2 * 256);
+  };
+  const bool walk_bwd = ppm && c.ptab && walk_at == 1 && pp_mark_at == 5 && walk_rides((size_t)3 * MARK_LDS_WORDS * 4);
   const int nwalk = walk_bwd ? 1 : 0;
   const uint32_t walk_lds = walk_bwd ? (uint32_t)(3 * kr.B * 12 + 16) : 0u;
-  const bool scan_w3 = ppm && !walk_bwd && (c.ptab ? scan_rides(c, kr, kr, (size_t)3 * MARK_LDS_WORDS * 4)
+  const bool scan_w3 = ppm && !walk_bwd && (c.ptab ? walk_rides((size_t)3 * MARK_LDS_WORDS * 4)
                                                    : scan_rides(c, k, kr, (size_t)3 * MARK_LDS_WORDS * 4));
   static const int plans_in_pred = env_int("TGNX_PLANS_IN_PRED", TGNX_PLANS_IN_PRED);  // (runtime A/B switch)
   const bool plans_pred = ppm && !c.ptab && !scan_w3 && plans_in_pred && c.pplan > 1 && c.pplan <= plans_in_pred &&
@@ -4757,7 +4773,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                                EpiDeferred{}, c.pE));
     TGNX_LAUNCH_CHECK("tgn_dh1");
     const int ncb = gridn(kr.Rtr, 4, 1 << 20), nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
-    tgn_attn_bwd<<<ncb + nkv, 256, 0, s>>>(c, ncb, nkv, 0, c);
+    launch_k(tgn_attn_bwd, dim3(ncb + nkv + nwalk), dim3(256), walk_lds, s, c, ncb, nkv, nwalk, nwalk ? cn : c);
   } else {
     const int ncb = gridn(kr.Rtr, 4, 1 << 20);
     const int nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
@@ -4839,8 +4855,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   } else {
     if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) return rc;
   }
-  if (ppm && !walk_w3 && !walk_bwd) {
-    tgn_scan<true><<<1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(cn, 1, 0);
+  if (ppm && !walk_w3 && !walk_bwd) {  // (with a plan table: the walk alone)
+    tgn_scan<true><<<c.ptab ? 1 : 1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(cn, 1, 0);
     TGNX_LAUNCH_CHECK("tgn_scan_early");
   }
   // split-K sums + epilogues ‖ Δt reduction ‖ update_state's memory half (train order: memory of src ∪
