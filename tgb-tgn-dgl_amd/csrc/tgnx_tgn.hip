@@ -43,7 +43,8 @@ constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touc
 #define TGNX_GRU_CAP TGNX_GEMM_GRID_CAP  // grid cap of the GRU GEMM (its workgroups loop past it; 512: +0.3 %)
 #endif
 #ifndef TGNX_EDGE_CAP200
-#define TGNX_EDGE_CAP200 1024  // grid cap of the lin_edge GEMM per 200 events of the rank's batch (env TGNX_EDGE_CAP200)
+#define TGNX_EDGE_CAP200 768  // grid cap of the lin_edge GEMM per 200 events of the rank's batch (env TGNX_EDGE_CAP200; same-box
+                              // A/Bs at wiki: 1024 0.0953 / 0.0952 / 0.0949 / 0.0948 ms, 768 0.0947 / 0.0946 / 0.0943 / 0.0942)
 #endif
 #ifndef TGNX_GRU_WAVES
 #define TGNX_GRU_WAVES 0  // waves-per-SIMD floor of the ring ‖ GRU ‖ lin_edge launch (1 hop)
