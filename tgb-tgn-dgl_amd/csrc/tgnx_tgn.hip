@@ -4792,7 +4792,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const auto j_kvr = BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(kr.Etr, KVR_CH, 1 << 20)};
   const auto j_dwe = gemm_job<GW>(shp_dWe(kr, c.cnt), LoadKRow{c.dE, HC, kr.Etr, HC}, LoadKRow{c.encE, D + d, kr.Etr, D + d},
                                   EpiDeferred{}, c.pA);
-  const auto j_denc = gemm_job<G32>(gemm_shape<G32>(kr.Etr, D, HC, c.cnt + CNT_E), LoadRowK{c.dE, kr.Etr, HC, HC},
+  const auto j_denc = gemm_job<G32>(with_cap(gemm_shape<G32>(kr.Etr, D, HC, c.cnt + CNT_E), edge_cap), LoadRowK{c.dE, kr.Etr, HC, HC},
                                     LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, nullptr, 0, P + c.L.te_w, P + c.L.te_b},
                                     (float*)nullptr);
   if (!kvf) {
