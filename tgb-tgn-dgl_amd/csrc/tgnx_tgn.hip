@@ -800,8 +800,9 @@ __device__ __forceinline__ PlanOut plan_view(const Ctx& c, int64_t start) {
 // graph's bitmap words <= 2 T when scan_direct (scan_folds), LDS at smem (tgn_scan_smem)
 // ahead: the batch `ahead` past the step counters' (1: the early scan of tgnx_tgn_train_step_pp, before this
 // step's counter advance); wdesc: write the batch descriptor into ctl (not while this step's launches still
-// read it); LW: capacity of the listed walk's LDS word list (>= 2 x the workgroup size)
-template <bool TRAIN, class AT, int LW = SCAN_LW>
+// read it); LW: capacity of the listed walk's LDS word list (>= 2 x the workgroup size); WPT: bitmap words per thread
+// of the register walk (direct / listed), 2 at 1024 threads, 8 for the 256-thread walk that rides in another launch
+template <bool TRAIN, class AT, int LW = SCAN_LW, int WPT = 2>
 __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char* smem, AT at, int ahead, bool wdesc) {
   __shared__ int sh[40];
   const int tid = threadIdx.x, T = blockDim.x;
@@ -846,7 +847,7 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
     for (int64_t i = s0 + SCAN_SWR; i < s1; ++i) nz += __popc(c.nbs[i]);
     int tw;
     int o = block_excl_scan(nz, sh, &tw);
-    listed = tw <= min(2 * T, LW);  // (block-uniform)
+    listed = tw <= min(WPT * T, LW);  // (block-uniform)
     if (listed) {
       auto emit = [&](int64_t i, uint32_t m) {
         if (!m) return;
@@ -896,14 +897,14 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
   const int cq = (ncw + T - 1) / T, c0 = min(ncw, tid * cq), c1 = min(ncw, c0 + cq);
   const int nq = (nnw + T - 1) / T, n0 = min(nnw, tid * nq), n1 = min(nnw, n0 + nq);
   int nc = 0, np = 0;
-  uint32_t dcw[2] = {0u, 0u}, dnw[2] = {0u, 0u};
-  int64_t dwi[2] = {0, 0};  // the words (direct: c0 + j; listed: from the LDS list)
+  uint32_t dcw[WPT] = {}, dnw[WPT] = {};
+  int64_t dwi[WPT] = {};  // the words (direct: c0 + j; listed: from the LDS list)
   const bool walk = direct || listed;
-  if (walk) {  // c0..c1 == n0..n1, <= 2 words
+  if (walk) {  // c0..c1 == n0..n1, <= WPT words
 #pragma unroll
-    for (int j = 0; j < 2; ++j) dwi[j] = direct ? (int64_t)(c0 + j) : (int64_t)lwl[min(c0 + j, max(ncw - 1, 0))];
+    for (int j = 0; j < WPT; ++j) dwi[j] = direct ? (int64_t)(c0 + j) : (int64_t)lwl[min(c0 + j, max(ncw - 1, 0))];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < WPT; ++j) {
       if (c0 + j < c1) {
         dcw[j] = c.cb[dwi[j]];
         dnw[j] = c.nb[dwi[j]];
@@ -923,7 +924,7 @@ __device__ __forceinline__ void scan_body(const Ctx& c, int role, unsigned char*
   int* lloc = reinterpret_cast<int*>(smem + (size_t)3 * c.Bmax * 8);       // [3 Bmax] its node rank
   if (walk) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < WPT; ++j) {
       if (c0 + j >= c1) break;
       const int64_t w = dwi[j];
       const int rw = rank;
@@ -3807,8 +3808,6 @@ static inline Ctx fixup_view(const Ctx& c) {
   if (f.adf.p) f.adf.ctl = c.snap_ctl;
   return f;
 }
-template <bool TRAIN, class AT, int LW>
-__device__ void scan_body(const Ctx& c, int role, unsigned char* smem, AT at, int ahead, bool wdesc);
 // the next batch's scan as extra workgroups of the dW_cell / dX_enc launch (tgnx_tgn_train_step_pp): into the
 // other parity's set (c), batch one past the counters (they advance in the fixup launch), no descriptor
 // write (the fixup launch writes it)
@@ -3817,7 +3816,7 @@ __device__ void scan_body(const Ctx& c, int role, unsigned char* smem, AT at, in
 struct ScanJob {
   Ctx c;
   __device__ void operator()(int bid, float* smem) const {
-    scan_body<true, NoCheckpoint, 512>(c, bid, reinterpret_cast<unsigned char*>(smem), NoCheckpoint{}, 1, false);
+    scan_body<true, NoCheckpoint, 8 * 256, 8>(c, bid, reinterpret_cast<unsigned char*>(smem), NoCheckpoint{}, 1, false);
   }
 };
 // tail blocks of the train step's fixup launch: [0, nscan) the next batch's scan (pipelined steps whose
@@ -4717,13 +4716,17 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   static const int walk_at = env_int("TGNX_WALK_AT", TGNX_WALK_AT);
   // (with a plan table the scan is the walk alone: its LDS is the centre staging, 3 B x 12 bytes, and the small-graph
   // direct walk's <= 2 words per thread; 2 hops: the walk rides in conv1's attention-backward launch)
-  const auto walk_rides = [&](size_t lds) {
-    return (size_t)3 * kr.B * 12 <= lds && (!scan_direct(c.words) || c.words <= 2 * 256);
+  // (the attention-backward walk holds 2 bitmap words per thread, the dW_cell launch's ScanJob 8: its LDS word list
+  // takes the 2-hop comment-shaped walk's ~1,100 words; 2 hops: the walk rides there — comment-shaped A/B 0.2383 /
+  // 0.2397 ms against 0.2462 / 0.2459 for the pipelined step, 0.2504 / 0.2498 in the attention backward; the wide
+  // walk in the attention backward cost the wiki step +0.9 %)
+  const auto walk_rides = [&](size_t lds, int wpt) {
+    return (size_t)3 * kr.B * 12 <= lds && (!scan_direct(c.words) || c.words <= (int64_t)wpt * 256);
   };
-  const bool walk_bwd = ppm && c.ptab && walk_at == 1 && pp_mark_at == 5 && walk_rides((size_t)3 * MARK_LDS_WORDS * 4);
+  const bool walk_bwd = ppm && c.ptab && walk_at == 1 && !two && pp_mark_at == 5 && walk_rides((size_t)3 * MARK_LDS_WORDS * 4, 2);
   const int nwalk = walk_bwd ? 1 : 0;
   const uint32_t walk_lds = walk_bwd ? (uint32_t)(3 * kr.B * 12 + 16) : 0u;
-  const bool scan_w3 = ppm && !walk_bwd && (c.ptab ? walk_rides((size_t)3 * MARK_LDS_WORDS * 4)
+  const bool scan_w3 = ppm && !walk_bwd && (c.ptab ? walk_rides((size_t)3 * MARK_LDS_WORDS * 4, 8)
                                                    : scan_rides(c, k, kr, (size_t)3 * MARK_LDS_WORDS * 4));
   static const int plans_in_pred = env_int("TGNX_PLANS_IN_PRED", TGNX_PLANS_IN_PRED);  // (runtime A/B switch)
   const bool plans_pred = ppm && !c.ptab && !scan_w3 && plans_in_pred && c.pplan > 1 && c.pplan <= plans_in_pred &&
