@@ -395,8 +395,9 @@ int tgnx_tgn_train_step_pipelined(const tgnx_tgn_config* cfg, const tgnx_tgn_buf
  * Alternate parity 0, 1, 0, ... across consecutive calls (two HIP graphs); prefetched as for
  * tgnx_tgn_train_step_pipelined (prefetched = 0 marks + scans this batch into set `parity` first).  A step
  * whose set holds another batch (wrong parity) sets ctl[ERR] bit 16 and computes nothing after its first
- * launch.  World 1, 1 hop (layers = 1); other calls use set 0 and scan for themselves.  Results equal
- * tgnx_tgn_train_step_pipelined's step for step.  Test: tests/test_gpu_tgn.py (pp vs resident). */
+ * launch.  World 1, 1 or 2 hops (2 hops: the root level's sets are doubled too, and the next batch's node-set
+ * walk rides in the dW_cell launch); other calls use set 0 and scan for themselves.  Results equal
+ * tgnx_tgn_train_step_pipelined's step for step.  Test: tests/test_gpu_tgn.py (pp vs resident, both hops). */
 int tgnx_tgn_train_step_pp(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo,
                            int64_t split_hi, int64_t batch, uint64_t base_seed, int32_t dropout, int32_t prefetched,
                            int32_t parity, void* stream);
@@ -427,7 +428,7 @@ int tgnx_tgn_train_fwd_bwd_split(const tgnx_tgn_config* cfg, const tgnx_tgn_buff
                                  int32_t dropout, int32_t prefetched, void* stream);
 int tgnx_tgn_scan_next(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo, int64_t split_hi,
                        int64_t batch, int32_t rank, int32_t world, uint64_t base_seed, void* stream);
-/* The data-parallel step on the parity-set design of tgnx_tgn_train_step_pp (world >= 1, 1 hop, Adam not
+/* The data-parallel step on the parity-set design of tgnx_tgn_train_step_pp (world >= 1, 1 or 2 hops, Adam not
  * folded in): the next batch (this rank's slice) is marked in the predictor launch and scanned into set
  * 1 - parity inside the dW_cell launch; the last launch writes the gradients, packs this rank's updated
  * memory rows into buf->xrows, advances the counters and writes the next descriptor.  One step is this
