@@ -53,6 +53,14 @@ constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touc
 #define TGNX_W3_WAVES 7  // waves-per-SIMD floor of the dW_cell launch (0: the compiler's register count, 84 + 8 -> 5 waves;
                          // same-box A/B: 0.0966 / 0.0961 ms, 6 waves 0.0961 / 0.0955, 7 (72 VGPRs, 12 B spilled) 0.0951 / 0.0951)
 #endif
+#ifndef TGNX_KVF_ROOT
+#define TGNX_KVF_ROOT 0  // 2 hops: conv2's attention backward sums its edges' (dk, dv) too (no k / v reduction launch;
+                         // comment-shaped same-box A/B: 0.2433 / 0.2406 ms sorted, 0.2442 / 0.2406 unsorted, against
+                         // 0.2398 / 0.2381 with the k / v launch, whose dE2 GEMMs otherwise lengthen the dh1 launch)
+#endif
+#ifndef TGNX_KVF_ROOT_SORT
+#define TGNX_KVF_ROOT_SORT 1  // (with TGNX_KVF_ROOT) the root edges sorted by neighbour: plain stores for whole rows
+#endif
 #ifndef TGNX_DENSE_H
 #define TGNX_DENSE_H 1  // GRU train step: the GRU forward also stores its rows' pre-update memory densely ([M][D], Hp),
                         // so the GRU backward and dW_gru read rows instead of gathering memory through node ids
@@ -266,6 +274,8 @@ struct Ctx {
   int64_t* cent1;  // roots (sorted)
   int *r_x2, *ceoff1;                // root -> its outer-centre index (row of P2 / h1); root edge offsets
   int *e1_j, *e1_e2;                 // root edge -> neighbour's outer-centre index; -> outer edge index
+  int* e1_c;                         // (TGNX_KVF_ROOT) root edge -> its root index
+  float *alk1, *Qo1;                 // (TGNX_KVF_ROOT) conv2's alpha * keep per root edge, [q | o] per root
   int64_t* e1_id;                    // root edge -> event id
   float *P2, *Ep2, *alpha1, *Zr, *dZr, *dP2, *dE2, *pE, *pF;
   int R1cap, E1cap, tgp_e1;          // tgp rows of the root edges start at tgp_e1
@@ -1690,6 +1700,7 @@ __global__ void __launch_bounds__(256) TGNX_AGG_ATTR tgn_agg_emit(Ctx c, int mod
         if (x1 >= 0) {
           const int o1 = c.ceoff1[x1] + (o - c.ceoff[x]);
           c.e1_j[o1] = c.crank[ju];
+          if (TGNX_KVF_ROOT) c.e1_c[o1] = x1;
           c.e1_e2[o1] = o;
           c.e1_id[o1] = e;
         }
@@ -4006,7 +4017,7 @@ static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_spli
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, kj, kx, ke, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
       Ep, alpha, alk, Qo, Zc, Hp, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
-      snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF,
+      snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, e1_c, alk1, Qo1, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF,
       uX, uZ, uG, ulu, uxw, utrel, total;
   int tgp_rows, tgp_e1;
   // the scan's per-batch outputs of the second parity (tgnx_tgn_train_step_pp: a step reads its parity's
@@ -4096,6 +4107,9 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.r_x2 = carve(off, R1 * 4);
   W.ceoff1 = carve(off, (R1 + 1) * 4);
   W.e1_j = carve(off, E1 * 4);
+  W.e1_c = carve(off, TGNX_KVF_ROOT ? E1 * 4 : 0);
+  W.alk1 = carve(off, TGNX_KVF_ROOT && two ? (size_t)k.E1tr * TH * 4 : 0);
+  W.Qo1 = carve(off, TGNX_KVF_ROOT && two ? (size_t)k.R1tr * 2 * HC * 4 : 0);
   W.e1_e2 = carve(off, E1 * 4);
   W.e1_id = carve(off, E1 * 8);
   W.P2 = carve(off, R2 * 4 * HC * 4);
@@ -4309,6 +4323,9 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
     c.ceoff1 = reinterpret_cast<int*>(ws + W.ceoff1);
     c.e1_j = reinterpret_cast<int*>(ws + W.e1_j);
     c.e1_e2 = reinterpret_cast<int*>(ws + W.e1_e2);
+    c.e1_c = reinterpret_cast<int*>(ws + W.e1_c);
+    c.alk1 = reinterpret_cast<float*>(ws + W.alk1);
+    c.Qo1 = reinterpret_cast<float*>(ws + W.Qo1);
     c.e1_id = reinterpret_cast<int64_t*>(ws + W.e1_id);
     c.P2 = reinterpret_cast<float*>(ws + W.P2);
     c.Ep2 = reinterpret_cast<float*>(ws + W.Ep2);
@@ -4383,6 +4400,9 @@ static Ctx root_view(const Ctx& c) {
   r.dZc = c.dZr;
   r.dP = c.dP2;
   r.dE = c.dE2;
+  r.e_c = c.e1_c;
+  r.alk = c.alk1;
+  r.Qo = c.Qo1;
   r.rsel = CNT_R1;
   r.ccap = c.R1cap;
   r.att_salt = 9;
@@ -4699,7 +4719,11 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     TGNX_LAUNCH_CHECK("tgn_attn_fwd");
   }
   Ctx cr = two ? root_view(c) : c;  // the level the predictor reads
-  if (two) cr.kvf = cr.kvs = 0;    // (conv2 keeps its k / v reduction launch)
+  if (two) {  // conv2: its attention backward sums the root edges' (dk, dv) too (TGNX_KVF_ROOT), the root edges
+              // sorted by neighbour row in the predictor launch (its sort block, as the 1-hop step's edges)
+    cr.kvf = TGNX_KVF_ROOT && kvf ? 1 : 0;
+    cr.kvs = cr.kvf && TGNX_KVE_GSORT && TGNX_KVF_ROOT_SORT && (size_t)kr.Mtr + 1 <= tgn_pred_smem(c.D) / 4 ? 1 : 0;
+  }
   if (two) {  // conv2 over the roots: projections of h1 (rows = outer centres), attention per root
     gemm_launch<G32>(gemm_shape<G32>(kr.Rtr, 4 * HC, HC, c.cnt + CNT_R), LoadRowK{c.Zc, kr.Rtr, HC, HC},
                      LoadProjW{P + c.L.wq2, c.L.pw, HC, HC}, EpiProj{P + c.L.bq2, c.L.pb, c.P2, HC}, nullptr, s);
@@ -4739,7 +4763,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const int nmk = (ppm ? pp_mark_at == 5 : pipe && mark_at == 5) ? nmark : 0;
   const size_t psm = std::max({tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0,
                                npl ? tgn_scan_smem(k.B) : (size_t)0});
-  const int nsrt = kvs ? 1 : 0;  // (kvs: the rows fit the sort's LDS counters)
+  const int nsrt = (two ? cr.kvs : kvs) ? 1 : 0;  // (kvs: the rows fit the sort's LDS counters)
   const PlanOut po = plan_out(ppm ? cn : c);
   if (att_in_pred)
     launch_k(tgn_pred_train<true>, dim3(kr.B + npl + nsrt + nmk), dim3(256), (uint32_t)psm, s, cr, nmk, nsrt, po, npl);
@@ -4759,22 +4783,30 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   if (two) {
     // conv2 backward (‖ predictor reductions) -> dP2, dE2; then dh1 = dP2 [Wq2; Wk2; Wv2; Wsk2] ‖ dW_proj2,
     // dW_edge2 (deferred) ‖ conv2's lin_edge -> Δt-encoding partials; then conv backward from dh1
-    const int ncb1 = gridn(kr.R1tr, 4, 1 << 20);
-    tgn_attn_bwd<<<ncb1 + gridn(3 * D + 2, 4), 256, 0, s>>>(cr, ncb1, 0, 0, cr);
+    const int ncb1 = gridn(kr.R1tr, 4, 1 << 20), nkv1 = cr.kvf ? gridn(kr.E1tr, KVE_CH, 1 << 20) : 0;
+    tgn_attn_bwd<<<ncb1 + nkv1 + gridn(3 * D + 2, 4), 256, 0, s>>>(cr, ncb1, nkv1, 0, cr);
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
-    // conv2's (dk, dv) sums ‖ its dE2-only GEMMs (as in the 1-hop step below), then dh1 ‖ dW_proj2
-    gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{cr}, gridn(kr.E1tr, KVR_CH, 1 << 20)},
-                 gemm_job<GW>(shp_dWe2(kr, c.cnt), LoadKRow{c.dE2, HC, kr.E1tr, HC}, LoadAttrMapT{ea1},
-                               EpiDeferred{}, c.pF),
-                 gemm_job<G32>(gemm_shape<G32>(kr.E1tr, D, HC, c.cnt + CNT_E1), LoadRowK{c.dE2, kr.E1tr, HC, HC},
-                               LoadKRow{P + c.L.we2, D, HC, D + d},
-                               EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, c.e1_e2, c.tgp_e1, P + c.L.te_w, P + c.L.te_b}, (float*)nullptr));
-    TGNX_LAUNCH_CHECK("tgn_kv_reduce2");
-    gemmN_launch(s,
-                 gemm_job<G32L>(gemm_shape<G32L>(kr.Rtr, HC, 4 * HC, c.cnt + CNT_R), LoadRowK{c.dP2, kr.Rtr, 4 * HC, 4 * HC},
-                                LoadProjWT{P + c.L.wq2, c.L.pw, HC, HC}, EpiStore{c.dZc, nullptr, HC, 0}, (float*)nullptr),
-                 gemm_job<GW>(shp_dWp2(kr, c.cnt), LoadKRow{c.dP2, 4 * HC, kr.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
-                               EpiDeferred{}, c.pE));
+    // conv2's (dk, dv) sums (unless its attention backward summed them) ‖ its dE2-only GEMMs (as in the 1-hop
+    // step below), then dh1 ‖ dW_proj2 (with the root-level fusion the dE2 GEMMs ride in that launch instead)
+    const auto j_dwe2 = gemm_job<GW>(shp_dWe2(kr, c.cnt), LoadKRow{c.dE2, HC, kr.E1tr, HC}, LoadAttrMapT{ea1},
+                                     EpiDeferred{}, c.pF);
+    const auto j_denc2 = gemm_job<G32>(gemm_shape<G32>(kr.E1tr, D, HC, c.cnt + CNT_E1), LoadRowK{c.dE2, kr.E1tr, HC, HC},
+                                       LoadKRow{P + c.L.we2, D, HC, D + d},
+                                       EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, c.e1_e2, c.tgp_e1, P + c.L.te_w,
+                                                 P + c.L.te_b},
+                                       (float*)nullptr);
+    const auto j_dh1 = gemm_job<G32L>(gemm_shape<G32L>(kr.Rtr, HC, 4 * HC, c.cnt + CNT_R),
+                                      LoadRowK{c.dP2, kr.Rtr, 4 * HC, 4 * HC}, LoadProjWT{P + c.L.wq2, c.L.pw, HC, HC},
+                                      EpiStore{c.dZc, nullptr, HC, 0}, (float*)nullptr);
+    const auto j_dwp2 = gemm_job<GW>(shp_dWp2(kr, c.cnt), LoadKRow{c.dP2, 4 * HC, kr.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
+                                     EpiDeferred{}, c.pE);
+    if (cr.kvf) {
+      gemmN_launch(s, j_dh1, j_dwp2, j_dwe2, j_denc2);
+    } else {
+      gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{cr}, gridn(kr.E1tr, KVR_CH, 1 << 20)}, j_dwe2, j_denc2);
+      TGNX_LAUNCH_CHECK("tgn_kv_reduce2");
+      gemmN_launch(s, j_dh1, j_dwp2);
+    }
     TGNX_LAUNCH_CHECK("tgn_dh1");
     const int ncb = gridn(kr.Rtr, 4, 1 << 20), nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
     launch_k(tgn_attn_bwd, dim3(ncb + nkv + nwalk), dim3(256), walk_lds, s, c, ncb, nkv, nwalk, nwalk ? cn : c);
