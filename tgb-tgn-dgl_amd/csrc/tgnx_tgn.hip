@@ -53,6 +53,10 @@ constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touc
 #define TGNX_W3_WAVES 7  // waves-per-SIMD floor of the dW_cell launch (0: the compiler's register count, 84 + 8 -> 5 waves;
                          // same-box A/B: 0.0966 / 0.0961 ms, 6 waves 0.0961 / 0.0955, 7 (72 VGPRs, 12 B spilled) 0.0951 / 0.0951)
 #endif
+#ifndef TGNX_DXE_DR
+#define TGNX_DXE_DR TGNX_G32L_DR  // direct-operand slabs per round of the dX_enc GEMM (the 7-wave dW_cell launch)
+#endif
+using GXE = GemmCfg<TGNX_G32L_T, TGNX_G32L_T, TGNX_G32L_KC, TGNX_G32L_PF, TGNX_G32L_WS, TGNX_DXE_DR>;
 #ifndef TGNX_KVF_ROOT
 #define TGNX_KVF_ROOT 0  // 2 hops: conv2's attention backward sums its edges' (dk, dv) too (no k / v reduction launch;
                          // comment-shaped same-box A/B: 0.2433 / 0.2406 ms sorted, 0.2442 / 0.2406 unsorted, against
@@ -4859,7 +4863,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const int nst = gridn(2 * k.B, 256);
   const auto j_dwg = gemm_job<GW>(shp_dWg(kr, c.cnt), LoadKRow{c.dG, Cl::G * D, kr.Mtr, Cl::G * D},
                                   Cl::hT(c), EpiDeferred{}, c.pD);
-  const auto j_dxe = gemm_job<G32L>(with_cap(gemm_shape<G32L>(kr.Mtr, D, Cl::G * D, c.cnt + CNT_M), md_cap),
+  const auto j_dxe = gemm_job<GXE>(with_cap(gemm_shape<GXE>(kr.Mtr, D, Cl::G * D, c.cnt + CNT_M), md_cap),
                                     LoadRowK{c.dG, kr.Mtr, Cl::G * D, Cl::G * D}, Cl::wenc(c),
                                     EpiTeMsg{c.s0m, c.s1m, c.tgp, D, rows_edge}, (float*)nullptr);
   // ppm: the next batch's scan (into set 1 - pp; the counters advance in the fixup launch) as this launch's
