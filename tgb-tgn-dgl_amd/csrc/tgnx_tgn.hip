@@ -57,6 +57,9 @@ constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touc
 #define TGNX_DXE_DR TGNX_G32L_DR  // direct-operand slabs per round of the dX_enc GEMM (the 7-wave dW_cell launch)
 #endif
 using GXE = GemmCfg<TGNX_G32L_T, TGNX_G32L_T, TGNX_G32L_KC, TGNX_G32L_PF, TGNX_G32L_WS, TGNX_DXE_DR>;
+#ifndef TGNX_DWE_AT7
+#define TGNX_DWE_AT7 0
+#endif
 #ifndef TGNX_KVF_ROOT
 #define TGNX_KVF_ROOT 0  // 2 hops: conv2's attention backward sums its edges' (dk, dv) too (no k / v reduction launch;
                          // comment-shaped same-box A/B: 0.2433 / 0.2406 ms sorted, 0.2442 / 0.2406 unsorted, against
@@ -4893,7 +4896,11 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   } else if (scan6) {
     if ((rc = l7(j_scan, j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) return rc;
   } else {
-    if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) return rc;
+    if (TGNX_DWE_AT7) {  // (experiment: dW_edge in the dz0 launch, which fits one dispatch round)
+      if ((rc = l7(j_dz0, j_dwp, j_dwlp, j_dwe)) || (rc = l8(j_denc))) return rc;
+    } else if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) {
+      return rc;
+    }
   }
   if (ppm && !walk_w3 && !walk_bwd) {  // (with a plan table: the walk alone)
     tgn_scan<true><<<c.ptab ? 1 : 1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(cn, 1, 0);
