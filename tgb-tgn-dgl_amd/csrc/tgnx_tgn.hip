@@ -57,6 +57,9 @@ constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touc
 #define TGNX_DXE_DR TGNX_G32L_DR  // direct-operand slabs per round of the dX_enc GEMM (the 7-wave dW_cell launch)
 #endif
 using GXE = GemmCfg<TGNX_G32L_T, TGNX_G32L_T, TGNX_G32L_KC, TGNX_G32L_PF, TGNX_G32L_WS, TGNX_DXE_DR>;
+#ifndef TGNX_PRED_GLDS
+#define TGNX_PRED_GLDS 0  // predictor weights staged with global_load_lds (LDS-DMA) instead of through registers
+#endif
 #ifndef TGNX_DWE_AT7
 #define TGNX_DWE_AT7 0
 #endif
@@ -2375,7 +2378,33 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
     const float invD = 1.0f / (float)D;
     const float4* S4 = reinterpret_cast<const float4*>(c.params + c.L.lsw);
     const float4* D4 = reinterpret_cast<const float4*>(c.params + c.L.ldw);
-    for (int b0 = 0; b0 < n4; b0 += NST * PRED_SU) {
+    bool staged = false;
+#if TGNX_PRED_GLDS
+    if (ATT && flat) {  // the LDS image is the global one: global_load_lds_dwordx4 straight into it, no registers,
+                        // every row in flight at once (then the wave drains them before the barrier)
+      for (int x0 = 0; x0 < n4; x0 += NST) {
+        const int x = x0 + st;
+        if (x < n4) {
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S4 + x),
+                                           (__attribute__((address_space(3))) void*)(reinterpret_cast<float4*>(Wsrc) + x0),
+                                           16, 0, 0);
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(D4 + x),
+                                           (__attribute__((address_space(3))) void*)(reinterpret_cast<float4*>(Wdst) + x0),
+                                           16, 0, 0);
+        }
+      }
+      for (int x = st; x < 3 * D + 1; x += NST) {
+        const float v = x < D ? c.params[c.L.lsb + x] : x < 2 * D ? c.params[c.L.ldb + x - D]
+                      : x < 3 * D ? c.params[c.L.lfw + x - 2 * D] : c.params[c.L.lfb];
+        if (x < D) vsb[x] = v;
+        else if (x < 2 * D) vdb[x - D] = v;
+        else vfw[x - 2 * D] = v;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the barrier below waits for LDS only)
+      staged = true;
+    }
+#endif
+    for (int b0 = 0; b0 < n4 && !staged; b0 += NST * PRED_SU) {
       float4 ws4[PRED_SU], wd4[PRED_SU];
 #pragma unroll
       for (int u = 0; u < PRED_SU; ++u) {
