@@ -97,6 +97,12 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _group_size(world: int) -> int:
+    """Ranks as the process group reports them (world from the environment otherwise)."""
+    import torch.distributed as dist
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else world
+
+
 def _metric(dataset: str, model: str) -> str:
     return (f"temporal edges/sec on {dataset} TGN (train step)" if model == "tgn" else
             f"temporal edges/sec on {dataset} TGNN, running DGL block-loop path (train step)")
@@ -255,7 +261,7 @@ def run_tgnn(args, world, rank, dev):
             "metric": _metric(args.dataset, "tgnn"),
             "value": round(args.steps * Bg / elapsed, 1),
             "unit": "events/s",
-            "n_gpus": world,
+            "n_gpus": _group_size(world),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -435,15 +441,26 @@ def run_tgn(args, world, rank, dev):
             eng.resident_train_step()
         counter["i"] += 1
 
+    def units():   # running sums of sampled edges / nodes (ctl[13:15]; begin_epoch does not reset them)
+        eng.finish()
+        torch.cuda.synchronize()
+        return list(eng.units())
+
     def barrier():
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
-    _log(f"tgn: {args.dataset} B={Bg} warmup {args.warmup}")
-    for _ in range(args.warmup):
+    # the timed window: K consecutive batches centred in the epoch (the rings and message stores are in their
+    # steady state there; an early window samples partly empty rings).  `prefill` untimed steps reach it first.
+    start = max(0, (nb_epoch - args.steps) // 2) if args.window == "mid" else args.warmup
+    prefill = max(0, start - args.warmup)
+    _log(f"tgn: {args.dataset} B={Bg} prefill {prefill} + warmup {args.warmup}, timed batches {start}..{start + args.steps - 1}")
+    for _ in range(prefill + args.warmup):
         step()
+    barrier()
+    u0 = units()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -451,6 +468,10 @@ def run_tgn(args, world, rank, dev):
     eng.finish()          # data-parallel parity-set steps: the last step's exchanged rows + Adam (else a no-op)
     barrier()
     elapsed = time.perf_counter() - t0
+    u1 = units()
+    # (the pipelined step prefetches: after step j the counters include batch j + 1's sampled sets, so the window
+    # counts batches start + 1 .. start + K)
+    win_edges, win_nodes = (u1[0] - u0[0]) / args.steps, (u1[1] - u0[1]) / args.steps
     if world > 1:
         tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
@@ -573,7 +594,7 @@ def run_tgn(args, world, rank, dev):
         "metric": _metric(args.dataset, "tgn"),
         "value": round(value, 1),
         "unit": "events/s",
-        "n_gpus": world,
+        "n_gpus": _group_size(world),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),
@@ -593,8 +614,15 @@ def run_tgn(args, world, rank, dev):
                    "global_batch": Bg, "parallelism": f"dp{world}",
                    "launch": "hip-graph replay per step" if use_graph else "eager",
                    "layers": args.layers,
-                   "sampled_edges_per_step": round(pd["edges"], 1),
-                   "sampled_nodes_per_step": round(pd["nodes"], 1)},
+                   "timed_batches": [start, start + args.steps - 1],
+                   "timed_window": (f"batches {start}..{start + args.steps - 1} of the {nb_epoch}-batch train epoch "
+                                    f"(0-based; {prefill} untimed prefill + {args.warmup} warmup steps before it"
+                                    + (", the window wraps into the next epoch: its begin_epoch is timed"
+                                       if start + args.steps > nb_epoch else "") + ")"),
+                   "sampled_edges_per_step": round(win_edges, 1),
+                   "sampled_nodes_per_step": round(win_nodes, 1),
+                   "probe_window_edges_per_step": round(pd["edges"], 1),
+                   "probe_window_nodes_per_step": round(pd["nodes"], 1)},
         "roofline": roofline,
         "kernels_us": {k: round(v["avg_us"], 3) for k, v in probes.items()},
         "kernels_gbs": {k: round(v["gbs"], 1) for k, v in probes.items() if v["gbs"]},
@@ -691,9 +719,50 @@ def tcsr_sampler_bench(args, K=10, reps=20):
     return out
 
 
+def _spawn_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N rank processes of this script, one per GPU (RANK =
+    LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), as `torch.distributed.run --nproc-per-node N`
+    would.  This parent never touches the GPU (no torch.cuda call before or after the spawn; the ranks are
+    children, not an exec of this process).  Rank 0 prints the JSON line; if a rank fails, the others are
+    stopped and its exit code is returned."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    _log(f"spawned {args.gpus} rank processes (MASTER_PORT {port})")
+    rc, stopped = 0, None
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                _log(f"rank process {procs.index(p)} exited with {code}: stopping the others")
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+                stopped = time.monotonic()
+        if stopped is not None and live and time.monotonic() - stopped > 30:
+            for q in live:       # (a rank blocked inside a collective may not honour SIGTERM)
+                q.kill()
+            stopped = time.monotonic()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks); without a torch.distributed launcher N > 1 spawns N rank processes")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--batch", type=int, default=200, help="events per GPU per step (weak scaling)")
@@ -713,12 +782,19 @@ def main():
     ap.add_argument("--no-train-loop", action="store_true", help="skip timing the drop-in pyg_epoch_utils.train loop")
     ap.add_argument("--no-tcsr", action="store_true", help="skip the t-CSR sampler leg")
     ap.add_argument("--probe-steps", type=int, default=100)
+    ap.add_argument("--window", choices=["mid", "start"], default="mid",
+                    help="TGN timed window: K batches centred in the train epoch (mid, after untimed prefill steps) "
+                         "or right after the warmup (start)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
     ap.add_argument("--dist-backend", default="nccl", help="rehearsal only: 'gloo' to run N>1 on one device")
     ap.add_argument("--one-device", action="store_true", help="rehearsal only: every rank on cuda:0")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        _log(f"--gpus {args.gpus} but WORLD_SIZE={world} (launcher): running {world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)

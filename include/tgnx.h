@@ -325,7 +325,10 @@ typedef struct {
                                      split / batch the resident parity-set steps run (tgnx_tgn_train_step_pp,
                                      tgnx_tgn_train_fwd_bwd_pp); they then read every batch's ring-insert and
                                      message-store plans from it and their scan is the node-set walk alone.
-                                     Other calls ignore it.  Must match the steps' split_lo / split_hi / batch. */
+                                     Other calls ignore it.  Must be the table tgnx_tgn_plan_table built for
+                                     the steps' split_lo / split_hi / batch and this config's max_batch: the
+                                     library records that when it builds the table and the steps refuse
+                                     (TGNX_EINVAL) a table it did not build or one built for another split. */
 } tgnx_tgn_buffers;
 /* exchanged memory row, all fields floats holding exact integers so that the row survives a SUM exchange
  * (one all-reduce over [gradients | every rank's row slots, zero but the sender's] is the all-gather):
@@ -341,8 +344,9 @@ size_t tgnx_tgn_store_words(const tgnx_tgn_config* cfg);
  * (node, direction), runs) of every batch of a resident split [split_lo, split_hi) in batches of `batch`
  * (the global batch under data parallelism): a function of the event table alone, so one launch per
  * binding builds what each step's scan would otherwise sort again.  Table: tgnx_tgn_plan_table_bytes bytes
- * (a 64-B header + one slot per batch, ~24 B per event entry); hand it to the resident parity-set steps as
- * buf->plan_table. */
+ * (a 64-B header + one slot per batch, sized by max_batch: 2 max_batch entries of 20 B each, i.e. about 40 B
+ * per event of the split when batch = max_batch — ~6 MB for the tgbl-wiki train split, ~1.3 GB for a
+ * tgbl-comment-sized one of 31M events); hand it to the resident parity-set steps as buf->plan_table. */
 size_t tgnx_tgn_plan_table_bytes(const tgnx_tgn_config* cfg, int64_t split_lo, int64_t split_hi, int64_t batch);
 int tgnx_tgn_plan_table(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo, int64_t split_hi,
                         int64_t batch, void* table, size_t table_bytes, void* stream);

@@ -10,7 +10,7 @@ Follows, in /root/reference:
                        first index (its CPU kernel); PyG scatter 'max'/'mean' give 0 for empty rows
   TimeEncoder          [ext] torch_geometric.nn.models.tgn.TimeEncoder: cos(Linear(1, D)(t))
                        (modules/time_enc.py is absent from the reference)
-  GraphAttentionEmbedding  modules/emb_module.py:55-73 over
+  GraphAttentionEmbedding  modules/emb_module.py:11-29 over
   TransformerConv      [ext] torch_geometric.nn.TransformerConv(in, C, heads=2, dropout=0.1, edge_dim,
                        concat=True, beta=False, root_weight=True): k_j += e, v_j += e with
                        e = lin_edge(edge_attr) (no bias), alpha = softmax_i(q_i·k_j / sqrt(C)) with
@@ -227,7 +227,7 @@ class RefTransformerConv(nn.Module):
 
 
 class RefGraphAttentionEmbedding(nn.Module):
-    """modules/emb_module.py:55-73.  layers = 2 is the build's 2-hop extension (SURVEY §8d comment
+    """modules/emb_module.py:11-29.  layers = 2 is the build's 2-hop extension (SURVEY §8d comment
     config, "no reference parity"): conv2(conv1(x)) over the same 2-hop edge set (the sampler called
     on the 1-hop node set), sharing the edge attributes; no activation between the layers."""
 

@@ -28,6 +28,12 @@ Modules exercised (file:line of the code that produced each fixture):
                  fixture pins the module's own control flow — store layout and ordering, update-vs-store
                  order in train / eval, _compute_msg's t_rel, the flush — while the placeholder arithmetic
                  (scatter, the time encoder) stays parity-unpinned
+  tgn_model_wiring.npz  pyg_model_utils.py:10-43 getModel / getOptimizer as written + emb_module.py:11-29 +
+                 decoder.py LinkPredictor + neighbor_loader.py, driven by the canonical PyG TGN batch
+                 (pyg_epoch_utils.py:106-137): outputs, loss, every parameter gradient, memory / last_update
+                 per batch over 4 batches with Adam; a torch_geometric.nn.TransformerConv placeholder (PyG's
+                 published semantics) added to the ones above — pins the wiring (rel_t sign, edge_attr order,
+                 the shared time encoder, the composition), not the placeholders' arithmetic
 """
 from __future__ import annotations
 
@@ -357,6 +363,123 @@ def capture_tgn_memory(ref, aggr, updater, seed, N=40, d=5, D=8, B=12, n_train=5
     np.savez(os.path.join(HERE, f"tgn_memory_{aggr}_{updater}.npz"), **out)
 
 
+def _install_transformer_conv():
+    """torch_geometric.nn.TransformerConv placeholder (emb_module.py:7 imports it), restating PyG's published
+    semantics for the arguments emb_module.py:21-23 passes (concat=True, beta=False, root_weight=True,
+    edge_dim set): lin_key / lin_query / lin_value / lin_skip with bias, lin_edge without; messages flow
+    source -> target (x_j = x[edge_index[0]], x_i = x[edge_index[1]]); key_j += lin_edge(e), value_j +=
+    lin_edge(e); alpha = softmax over each target's edges of q_i·k_j / sqrt(C) (PyG softmax: exp(a - max) /
+    (sum + 1e-16)), dropout on alpha in training; out_i = Σ alpha v_j, heads concatenated, + lin_skip(x_i)."""
+    import math
+    tg_nn = sys.modules["torch_geometric.nn"]
+
+    class TransformerConv(torch.nn.Module):
+        def __init__(self, in_channels, out_channels, heads=1, concat=True, beta=False, dropout=0.0, edge_dim=None,
+                     bias=True, root_weight=True, **kwargs):
+            super().__init__()
+            assert concat and not beta and root_weight and edge_dim is not None
+            self.heads, self.out_channels, self.dropout = heads, out_channels, dropout
+            HC = heads * out_channels
+            self.lin_key = torch.nn.Linear(in_channels, HC)
+            self.lin_query = torch.nn.Linear(in_channels, HC)
+            self.lin_value = torch.nn.Linear(in_channels, HC)
+            self.lin_edge = torch.nn.Linear(edge_dim, HC, bias=False)
+            self.lin_skip = torch.nn.Linear(in_channels, HC, bias=bias)
+
+        def forward(self, x, edge_index, edge_attr):
+            H, C, N = self.heads, self.out_channels, x.size(0)
+            j, i = edge_index[0], edge_index[1]
+            q = self.lin_query(x).view(-1, H, C)[i]
+            k = self.lin_key(x).view(-1, H, C)[j]
+            v = self.lin_value(x).view(-1, H, C)[j]
+            e = self.lin_edge(edge_attr).view(-1, H, C)
+            k = k + e
+            a = (q * k).sum(-1) / math.sqrt(C)
+            idx = i.view(-1, 1).expand(-1, H)
+            amax = torch.full((N, H), -math.inf).scatter_reduce(0, idx, a.detach(), "amax", include_self=True)
+            ex = (a - amax[i]).exp()
+            den = torch.zeros(N, H).scatter_add(0, idx, ex) + 1e-16
+            a = torch.nn.functional.dropout(ex / den[i], p=self.dropout, training=self.training)
+            msg = (v + e) * a.unsqueeze(-1)
+            out = torch.zeros(N, H, C).index_add(0, i, msg).view(N, H * C)
+            return out + self.lin_skip(x)
+
+    tg_nn.TransformerConv = TransformerConv
+
+
+def capture_tgn_model(ref, seed, N=60, d=5, D=8, B=10, nb=4, lr=1e-3):
+    """The reference's own model wiring (verdict r4 item 4): pyg_model_utils.py:10-36 getModel(d, D, N, 'cpu')
+    called as written — TGNMemory + IdentityMessage + LastAggregator, GraphAttentionEmbedding
+    (modules/emb_module.py:11-29) sharing memory.time_enc, LinkPredictor (modules/decoder.py) — and
+    getOptimizer (:38-43), driven by the canonical PyG TGN batch (the sequence pyg_epoch_utils.py:106-137
+    carries commented out) with the reference's LastNeighborLoader (neighbor_loader.py): n_id = unique(src, pos,
+    neg) -> loader -> memory(n_id) -> gnn(z, last_update, edge_index, t[e_id], msg[e_id]) -> link_pred on
+    (src, pos) and (src, neg) -> BCEWithLogits on the sigmoid outputs -> update_state -> insert -> backward ->
+    Adam -> memory.detach().  Pins emb_module's rel_t = last_update[edge_index[0]] - t, edge_attr =
+    [time_enc(rel_t) ‖ msg], the shared time encoder (its gradient from both uses) and the composition; the
+    TransformerConv / scatter / TimeEncoder placeholders' arithmetic stays parity-unpinned.  Attention dropout is
+    off (gnn.conv in eval mode; the memory trains).  Integer timestamps (TGNMemory's long last_update)."""
+    _install_tgn_placeholders(ref)
+    _install_transformer_conv()
+    import neighbor_loader
+    import pyg_model_utils
+    torch.manual_seed(seed)
+    model = pyg_model_utils.getModel(d, D, N, "cpu")
+    opt = pyg_model_utils.getOptimizer(model, lr)
+    model["gnn"].conv.train(False)
+    loader = neighbor_loader.LastNeighborLoader(N, 10)
+    rng = np.random.default_rng(seed)
+    out = {}
+    for part in ("memory", "gnn", "link_pred"):
+        for k, v in model[part].state_dict().items():
+            if not k.startswith("_") and k not in ("memory", "last_update"):
+                out[f"p_{part}__{k.replace('.', '__')}"] = v.detach().numpy().copy()
+    src = rng.integers(0, N, (nb, B)).astype(np.int64)
+    dst = rng.integers(0, N, (nb, B)).astype(np.int64)
+    neg = rng.integers(0, N, (nb, B)).astype(np.int64)
+    src[:, 1] = src[:, 0]
+    t = (np.arange(nb * B).reshape(nb, B) * 7 + 3).astype(np.int64)
+    msg = rng.random((nb * B, d), dtype=np.float32)
+    out.update(src=src, dst=dst, neg=neg, t=t, msg=msg, meta=np.array([N, d, D, B, nb]), lr=np.array([lr]))
+    ev_t, ev_msg = torch.from_numpy(t.reshape(-1)), torch.from_numpy(msg)
+    assoc = torch.empty(N, dtype=torch.long)
+    crit = torch.nn.BCEWithLogitsLoss()
+    named = {}
+    for part in ("memory", "gnn", "link_pred"):
+        for k, p in model[part].named_parameters():
+            named.setdefault(p, f"{part}.{k}")
+    for b in range(nb):
+        for part in ("memory", "gnn", "link_pred"):
+            model[part].train()
+        model["gnn"].conv.train(False)
+        opt.zero_grad()
+        s, pd_, ng = (torch.from_numpy(x[b]) for x in (src, dst, neg))
+        n_id = torch.cat([s, pd_, ng]).unique()
+        n_id, edge_index, e_id, _ = loader(n_id)
+        assoc[n_id] = torch.arange(n_id.size(0))
+        z, last_update = model["memory"](n_id)
+        z = model["gnn"](z, last_update, edge_index, ev_t[e_id], ev_msg[e_id])
+        pos_out = model["link_pred"](z[assoc[s]], z[assoc[pd_]])
+        neg_out = model["link_pred"](z[assoc[s]], z[assoc[ng]])
+        loss = crit(pos_out, torch.ones_like(pos_out)) + crit(neg_out, torch.zeros_like(neg_out))
+        model["memory"].update_state(s, pd_, torch.from_numpy(t[b]), torch.from_numpy(msg[b * B:(b + 1) * B]))
+        loader.insert(s, pd_, torch.from_numpy(t[b]))
+        loss.backward()
+        out[f"b{b}_nid"] = n_id.numpy()
+        out[f"b{b}_pos"] = pos_out.detach().view(-1).numpy()
+        out[f"b{b}_neg"] = neg_out.detach().view(-1).numpy()
+        out[f"b{b}_loss"] = np.array([float(loss)])
+        # the shared time encoder appears under memory.time_enc and gnn.time_enc: one tensor, one gradient
+        for p, name in named.items():
+            if p.grad is not None:
+                out[f"b{b}_g_{name.replace('.', '__')}"] = p.grad.numpy().copy()
+        opt.step()
+        model["memory"].detach()
+        out[f"b{b}_memory"] = model["memory"].memory.detach().numpy().copy()
+        out[f"b{b}_last_update"] = model["memory"].last_update.numpy().copy()
+    np.savez(os.path.join(HERE, "tgn_model_wiring.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -369,6 +492,8 @@ def main():
         if "tgn_memory" in args.only.split(","):
             for i, (aggr, upd) in enumerate((("last", "gru"), ("mean", "gru"), ("last", "rnn"))):
                 capture_tgn_memory(args.ref, aggr, upd, seed=20 + i)
+        if "tgn_model" in args.only.split(","):
+            capture_tgn_model(args.ref, seed=30)
         print("goldens written to", HERE)
         return
     capture_sampler(args.ref, "k4_mono", num_nodes=40, K=4, num_batches=12, batch=12, monotone=True, seed=1)
@@ -383,6 +508,7 @@ def main():
     capture_link_pred(9)
     for i, (aggr, upd) in enumerate((("last", "gru"), ("mean", "gru"), ("last", "rnn"))):
         capture_tgn_memory(args.ref, aggr, upd, seed=20 + i)
+    capture_tgn_model(args.ref, seed=30)
     print("goldens written to", HERE)
 
 

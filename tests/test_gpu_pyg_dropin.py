@@ -151,3 +151,71 @@ def test_reference_script_with_one_line_swap(tmp_path, monkeypatch):
         assert torch.allclose(pg.cpu(), po, atol=2e-5) and torch.allclose(ng.cpu(), no, atol=2e-5), st
         diff_last = max(diff_last, float((pg.cpu() - outs["last"][1]).abs().max()))
     assert diff_last > 1e-3   # the two aggregations differ on this stream: the match above selects 'mean'
+
+
+def test_dropin_train_twice_with_test_between_matches_oracle(tmp_path):
+    """The drop-in train() as the reference script calls it, twice, with test() between: the graphs
+    captured in epoch 1 are replayed in epoch 2 after begin_epoch / flush / eval ran on the same buffers.  Every
+    step of both epochs is checked — without resynchronisation — through the per-event output log (out_ev)
+    against oracle/tgn_ref.train_step fed the negatives the device drew (eng.neg_train after each epoch), on a
+    wiki-shaped stream whose timestamps span 2,000 s (not chaotic: DESIGN §7), dropout off.  Tolerances:
+    per-event outputs 1e-4 abs, train() loss sums 1e-4 relative, val MRR 5e-3 (test_gpu_tgn_epochs.py's)."""
+    import pyg_epoch_utils as pe
+    import pyg_model_utils as pm
+    from epoch_parity import scaled_stream
+    from oracle.sampler_ref import RefLastNeighborLoader
+    from oracle.tgn_ref import RefTGN, eval_step, mrr_per_event, train_step
+    from tgnx.data import getDataWithDependecyBlock
+    from tgnx.neg import NegLinkSamplerDest
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.synth import eval_negatives
+    s = scaled_stream(4, N=1000, E=3000, d=16, t_max=2000)
+    path = str(tmp_path / "short.npz")
+    np.savez(path, src=s.src, dst=s.dst, t=s.t, msg=s.msg, val_neg=eval_negatives(s, "val", 30),
+             test_neg=eval_negatives(s, "test", 30))
+    B = 200
+    data, tr, va, te, ns, ev, metric = getDataWithDependecyBlock(path, {"batch_size": B})
+    d, D, N = data.msg.shape[1], 100, data.num_nodes
+    torch.manual_seed(0)
+    ref = RefTGN(N, d, hidden=D, aggr="last", dropout=0.0)
+    model = pm.getModel(d, D, N, "cuda", ring=10, max_batch=B, dropout=0.0)
+    model["model"].load_reference_state(ref.state_dict())
+    opt = pm.getOptimizer(model, 1e-4)
+    nl = LastNeighborLoader(N, 10, device="cuda")
+    nds = NegLinkSamplerDest(torch.unique(data.dst), device="cuda")
+    crit = torch.nn.BCEWithLogitsLoss()
+    runs = []
+    for ep in range(2):
+        loss = pe.train(model, data.msg, tr, nl, nds, None, "cuda", opt, crit)
+        eng = model["model"]._tgnx_engine
+        runs.append(dict(loss=loss, neg=eng.neg_train[tr.lo:tr.hi].cpu().clone(),
+                         out=eng.out_ev[tr.lo:tr.hi].cpu().clone()))
+        runs[-1]["mrr"] = pe.test(model, data.msg, va, nl, ns, None, "cuda", opt, crit, ev, metric, "val")
+    assert model["model"]._tgnx_engine._graphs is not None
+    opt_ref = torch.optim.Adam(ref.parameters(), lr=1e-4)
+    ev_t, ev_msg = data.t.float(), data.msg.float()
+    vneg = va.negatives
+    for ep, run in enumerate(runs):
+        ref.memory.reset_state()
+        ref.memory.train(True)
+        lref = RefLastNeighborLoader(N, 10)
+        tot = 0.0
+        for a in range(tr.lo, tr.hi, B):
+            b = min(a + B, tr.hi)
+            sl = slice(a, b)
+            loss, po, no = train_step(ref, opt_ref, lref, ev_t, ev_msg, data.src[sl], data.dst[sl],
+                                      run["neg"][a - tr.lo:b - tr.lo], ev_t[sl], ev_msg[sl])
+            tot += loss * (b - a)
+            got = run["out"][a - tr.lo:b - tr.lo]
+            assert torch.allclose(got[:, 0], po, atol=1e-4), (ep, a, float((got[:, 0] - po).abs().max()))
+            assert torch.allclose(got[:, 1], no, atol=1e-4), (ep, a, float((got[:, 1] - no).abs().max()))
+        assert abs(run["loss"] - tot) <= 1e-4 * abs(tot), (ep, run["loss"], tot)
+        ref.memory.train(False)
+        per = []
+        for a in range(va.lo, va.hi, B):
+            b = min(a + B, va.hi)
+            sl = slice(a, b)
+            po, no = eval_step(ref, lref, ev_t, ev_msg, data.src[sl], data.dst[sl], vneg[a - va.lo:b - va.lo],
+                               ev_t[sl], ev_msg[sl])
+            per.append(float(np.mean(mrr_per_event(po, no))))
+        assert abs(run["mrr"] - float(np.mean(per))) < 5e-3, (ep, run["mrr"], float(np.mean(per)))

@@ -440,3 +440,76 @@ def test_tgn_pp_wrong_parity_sets_error():
     assert torch.equal(model.memory.memory, mem) and torch.equal(model.flat, flat)
     with pytest.raises(RuntimeError):
         eng.check()
+
+
+def test_tgn_pp_refuses_foreign_plan_table():
+    """The resident parity-set step refuses a plan table that tgnx_tgn_plan_table built for another split or
+    batch (the slot index and stride would otherwise hand it another batch's plans or read past the
+    table) and one the library did not build; nothing is launched (ctl untouched)."""
+    import ctypes
+    from tgnx import _lib
+    s, ref, opt_ref, lref, model, opt, eng = _setup("last")
+    eng.bind_resident(0, 7 * 50, 50, dropout=False)
+    eng.begin_epoch()
+    torch.cuda.synchronize()
+    L = _lib.lib()
+    ctl0 = eng.ctl.clone()
+    # the engine's table is for [0, 350) batch 50: a step over [0, 300) or batch 40 must be refused
+    for lo, hi, batch in ((0, 6 * 50, 50), (0, 7 * 50, 40), (50, 7 * 50, 50)):
+        rc = L.tgnx_tgn_train_step_pp(eng._cfg_ref, eng._buf_ref, lo, hi, batch, 0, 0, 0, 0, eng._stream())
+        assert rc != 0, (lo, hi, batch)
+        assert "plan_table" in L.tgnx_last_error().decode()
+    # a buffer of the right size the library never built a table in
+    fake = torch.zeros_like(eng.plan_table)
+    eng._res_buf.plan_table = fake.data_ptr()
+    rc = L.tgnx_tgn_train_step_pp(eng._cfg_ref, eng._buf_ref, 0, 7 * 50, 50, 0, 0, 0, 0, eng._stream())
+    assert rc != 0 and "not built" in L.tgnx_last_error().decode()
+    eng._res_buf.plan_table = eng.plan_table.data_ptr()
+    torch.cuda.synchronize()
+    assert torch.equal(eng.ctl, ctl0)
+    eng.resident_train_step()            # the matching table still works
+    torch.cuda.synchronize()
+    eng.check()
+
+
+def test_tgn_engine_matches_reference_model_wiring():
+    """The HIP step against the reference's own model wiring (tests/golden/tgn_model_wiring.npz:
+    pyg_model_utils.getModel as written, GraphAttentionEmbedding emb_module.py:11-29, LinkPredictor, the
+    reference LastNeighborLoader; make_goldens.py capture_tgn_model), 4 batches with Adam, nothing
+    resynchronised: outputs 2e-5, loss, every gradient 2e-3 relative (lin_key.bias: negligible on both sides),
+    memory 1e-5, last_update exact."""
+    import os
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "tgn_model_wiring.npz"))
+    N, d, D, B, nb = z["meta"].tolist()
+    dev = torch.device("cuda")
+    model = TGNModel(N, nb * B, d, D, dev, ring=10, max_batch=B, max_neg=1, aggr="last", dropout=0.0)
+    sd = {k[2:].replace("__", ".", 1).replace("__", "."): torch.from_numpy(z[k]) for k in z.files if k.startswith("p_")}
+    model.load_reference_state(sd)
+    opt = TgnAdam(model, float(z["lr"][0]))
+    eng = TgnEngine(model, LastNeighborLoader(N, 10, device=dev),
+                    dict(src=z["src"].reshape(-1), dst=z["dst"].reshape(-1), t=z["t"].reshape(-1).astype(np.float32),
+                         msg=z["msg"]), opt, dst_nodes=np.unique(z["dst"]))
+    eng.reset_state()
+    for b in range(nb):
+        pg, ng = eng.train_batch(b * B, B, neg=torch.from_numpy(z["neg"][b]), dropout=False)
+        torch.cuda.synchronize()
+        eng.check()
+        assert np.allclose(pg.cpu().numpy(), z[f"b{b}_pos"], atol=2e-5), b
+        assert np.allclose(ng.cpu().numpy(), z[f"b{b}_neg"], atol=2e-5), b
+        assert abs(float(model.grad_flat[-1]) - float(z[f"b{b}_loss"][0])) < 1e-5, b
+        g = model.grads_by_name()
+        for name in model.param_order:
+            want = torch.from_numpy(z[f"b{b}_g_" + name.replace(".", "__")])
+            if name in SHIFT_INVARIANT:
+                scale = float(torch.from_numpy(z[f"b{b}_g_" + SHIFT_INVARIANT[name].replace(".", "__")]).norm())
+                assert float(g[name].norm()) <= 1e-4 * scale + 1e-9, (b, name)
+                continue
+            if float(want.norm()) == 0.0:
+                assert float(g[name].norm()) < 1e-7, (b, name)
+                continue
+            r = _rel(g[name], want)
+            assert r < 2e-3, (b, name, r)
+        assert np.allclose(model.memory.memory.cpu().numpy(), z[f"b{b}_memory"], atol=1e-5), b
+        assert np.array_equal(model.memory.last_update.cpu().numpy(), z[f"b{b}_last_update"]), b

@@ -16,7 +16,16 @@ Checks (inside the rank processes; rank 0 also runs a world-1 engine over the sa
   * lr = 0 (parameters fixed, so states compare step after step): every rank bit-identical (digests of
     memory, last_update, ring, stores, all-gathered), and rank 0 against the world-1 engine — memory 1e-5
     abs, last_update / ring / stores exact, parameters unchanged;
-  * lr = 1e-3: every rank's parameters, Adam moments and memory bit-identical after every compared step.
+  * lr = 1e-3: every rank's parameters, Adam moments and memory bit-identical after every compared step, and
+    rank 0 against the world-1 engine trained on the same global batches (no resynchronisation): every
+    parameter tensor and both Adam moments within 1e-5 relative (L2), memory 1e-5 abs, last_update / ring /
+    stores exact.  That closes the data-parallel gradient chain directly: a wrong gradient sum moves the
+    replicas away from world 1 at the first step.  The lr = 1e-3 runs use the stream with its timestamps
+    rescaled to span 2,000 s, where the trajectory is not chaotic (at the TGB time scales one ulp of
+    the time-encoder weight turns the highest encoding frequencies by ~0.16 rad, so two summation orders
+    drift apart within a few steps).  `gnn.conv*.lin_key.bias` has an exactly zero gradient (q·b_k is
+    constant per centre; softmax is shift invariant): both sides step it by Adam on rounding noise, so it is
+    excluded from the parameter / moment comparison.
 In the pp form the exchange of step k is applied at the head of step k + 1's graph; states are compared after
 odd steps (finish() applies it there), so the even steps run the graph with the apply inside.  The epoch
 includes a partial last batch and a step past the split (B = 0)."""
@@ -40,10 +49,23 @@ CASES = {   # name: (shape, N, d, D, global batch, world, layers)
 }
 
 
-def _stream(case):
+SHIFT_INVARIANT = ("gnn.conv.lin_key.bias", "gnn.conv2.lin_key.bias")
+
+
+def _stream(case, short=False):
+    """The case's stream; short: timestamps rescaled to integers over [0, 2,000] s (order kept)."""
     from tgnx.synth import make_stream
     shape, N, d, D, Bg, W, layers = CASES[case]
-    return make_stream(shape, seed=41, num_events=Bg * NB, num_nodes=N, msg_dim=d)
+    s = make_stream(shape, seed=41, num_events=Bg * NB, num_nodes=N, msg_dim=d)
+    if short:
+        span = max(float(s.t[-1] - s.t[0]), 1.0)
+        s.t = np.floor((s.t - s.t[0]) * (2000.0 / span))
+    return s
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / (b.norm() + 1e-12))
 
 
 def _engine(case, s, rank, world, lr):
@@ -99,7 +121,7 @@ def _worker(case, rank, world, port, lr, mode, out_dir):
     res = {"rank": rank, "ok": False, "compared": []}
     try:
         Bg = CASES[case][4]
-        s = _stream(case)
+        s = _stream(case, short=lr != 0.0)
         eng = _engine(case, s, rank, world, lr)
         _configure(eng, mode)
         eng.bind_resident(0, _split_hi(case), Bg, dropout=True)
@@ -107,8 +129,8 @@ def _worker(case, rank, world, port, lr, mode, out_dir):
         eng.capture_resident()
         assert eng._dp_pp() == (mode == "pp"), (mode, eng._dp_pp())
         e1 = None
-        if rank == 0 and lr == 0.0:
-            e1 = _engine(case, s, 0, 1, 0.0)    # world 1 over the same GLOBAL batches
+        if rank == 0:
+            e1 = _engine(case, s, 0, 1, lr)     # world 1 over the same GLOBAL batches
             e1.bind_resident(0, _split_hi(case), Bg, dropout=True)
             e1.begin_epoch()
         flat0 = eng.model.flat.clone()
@@ -138,10 +160,22 @@ def _worker(case, rank, world, port, lr, mode, out_dir):
                 assert torch.equal(mine["nbr"][live], ref["nbr"][live]), st
                 err = float((mine["memory"] - ref["memory"]).abs().max())
                 assert err < 1e-5, (st, err)
-                assert torch.equal(mine["flat"], ref["flat"]) and torch.equal(mine["flat"], flat0), st  # lr = 0
+                if lr == 0.0:
+                    assert torch.equal(mine["flat"], ref["flat"]) and torch.equal(mine["flat"], flat0), st
+                else:   # the gradient sum over ranks, checked through Adam against the world-1 trajectory
+                    worst = 0.0
+                    for name, (o, n, _) in eng.model._views.items():
+                        if name in SHIFT_INVARIANT:
+                            continue
+                        for key in ("flat", "adam_m", "adam_v"):
+                            r = _rel(mine[key][o:o + n], ref[key][o:o + n])
+                            worst = max(worst, r)
+                            assert r < 1e-5, (st, name, key, r)
+                    res.setdefault("worst_rel", []).append(worst)
             res["compared"].append(st)
             if rank == 0:
-                print(f"[dp_pg {case} {mode} lr={lr}] step {st} compared", flush=True)
+                w = res.get("worst_rel", [None])[-1]
+                print(f"[dp_pg {case} {mode} lr={lr}] step {st} compared (worst rel vs world 1: {w})", flush=True)
         if lr:
             assert not torch.equal(eng.model.flat, flat0)    # Adam moved the parameters on every rank alike
         dist.barrier()
@@ -195,10 +229,11 @@ def test_tgn_dp_process_group_replicas_stay_identical(tmp_path, mode):
     _run_ranks("wiki-small", 1e-3, mode, tmp_path)
 
 
-@pytest.mark.parametrize("case", ["coin-w4", "comment2hop-w8", "wiki-w8"])
-def test_tgn_dp_process_group_baseline_worlds(tmp_path, case):
-    """BASELINE configs #4 / #5 and the wiki headline at their world sizes, lr = 0 against world 1 and
-    lr = 1e-3 replicas (the 2-hop comment case takes the split form; the others the parity-set step)."""
-    mode = "split" if CASES[case][6] == 2 else "pp"
+@pytest.mark.parametrize("case,mode", [("coin-w4", "pp"), ("comment2hop-w8", "pp"), ("comment2hop-w8", "split"),
+                                       ("wiki-w8", "pp")])
+def test_tgn_dp_process_group_baseline_worlds(tmp_path, case, mode):
+    """BASELINE configs #4 / #5 and the wiki headline at their world sizes, lr = 0 and lr = 1e-3 against
+    world 1, in the parity-set form bench.py runs (the engine's default at world > 1, 1 and 2 hops: _dp_pp()
+    is asserted) and, for the 2-hop comment case, also in the split pipelined form."""
     _run_ranks(case, 0.0, mode, tmp_path / "lr0")
     _run_ranks(case, 1e-3, mode, tmp_path / "lr1")

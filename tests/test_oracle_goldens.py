@@ -145,3 +145,49 @@ def test_tgn_memory_oracle_matches_reference_module(golden, aggr, updater):
                                       z[f"b{b}_store_d_n"])
         got_t = [mem.msg_s_store[j][2].numpy().astype(np.float64) for j in range(N) if j in mem.msg_s_store]
         np.testing.assert_array_equal(np.concatenate(got_t or [np.zeros(0)]), z[f"b{b}_store_s_t"])
+
+
+def test_tgn_oracle_matches_reference_model_wiring(golden):
+    """oracle/tgn_ref.RefTGN + train_step against the reference's own model wiring (make_goldens.py
+    capture_tgn_model): pyg_model_utils.py:10-43 getModel / getOptimizer called as written, so
+    GraphAttentionEmbedding (modules/emb_module.py:11-29: rel_t = last_update[edge_index[0]] - t, edge_attr =
+    [time_enc(rel_t) ‖ msg], time_enc shared with the memory) and LinkPredictor (decoder.py) run as the
+    reference composes them, with the reference's LastNeighborLoader, over 4 canonical batches with Adam:
+    every output, the loss, every parameter gradient (the shared time encoder's summed over both uses),
+    memory and last_update after each batch, nothing resynchronised.  The placeholder TransformerConv /
+    scatter / time-encoder arithmetic the reference modules ran with is restated on both sides (parity
+    unpinned there); this pins the wiring around it."""
+    from oracle.sampler_ref import RefLastNeighborLoader
+    from oracle.tgn_ref import RefTGN, train_step
+    z = golden("tgn_model_wiring.npz")
+    N, d, D, B, nb = z["meta"].tolist()
+    ref = RefTGN(N, d, hidden=D, aggr="last", dropout=0.0)
+    sd = {k[2:].replace("__", "."): torch.from_numpy(z[k]) for k in z.files if k.startswith("p_")}
+    missing = ref.load_state_dict(sd, strict=False)
+    assert not missing.unexpected_keys
+    assert set(missing.missing_keys) <= {"memory.memory", "memory.last_update", "memory._assoc"}, missing.missing_keys
+    opt = torch.optim.Adam(ref.parameters(), lr=float(z["lr"][0]))
+    loader = RefLastNeighborLoader(N, 10)
+    ev_t = torch.from_numpy(z["t"].reshape(-1).astype(np.float32))
+    ev_msg = torch.from_numpy(z["msg"])
+    named = dict(ref.named_parameters())
+    for b in range(nb):
+        sl = slice(b * B, (b + 1) * B)
+        src, pos, neg = (torch.from_numpy(z[k][b]) for k in ("src", "dst", "neg"))
+        loss, po, no = train_step(ref, opt, loader, ev_t, ev_msg, src, pos, neg, ev_t[sl], ev_msg[sl])
+        np.testing.assert_allclose(po.numpy(), z[f"b{b}_pos"], rtol=0, atol=2e-6, err_msg=f"batch {b}")
+        np.testing.assert_allclose(no.numpy(), z[f"b{b}_neg"], rtol=0, atol=2e-6, err_msg=f"batch {b}")
+        assert abs(loss - float(z[f"b{b}_loss"][0])) < 2e-6, b
+        grads = {k[len(f"b{b}_g_"):].replace("__", "."): z[k] for k in z.files if k.startswith(f"b{b}_g_")}
+        assert set(grads) == set(named), sorted(set(grads) ^ set(named))
+        for name, g in grads.items():
+            got = named[name].grad.numpy()
+            if name == "gnn.conv.lin_key.bias":   # exactly zero in exact arithmetic (softmax shift invariance)
+                wscale = float(np.abs(grads["gnn.conv.lin_key.weight"]).max())
+                assert np.abs(got).max() <= 1e-4 * wscale and np.abs(g).max() <= 1e-4 * wscale, b
+                continue
+            scale = max(float(np.abs(g).max()), 1e-6)
+            np.testing.assert_allclose(got, g, rtol=0, atol=2e-5 * scale, err_msg=f"batch {b} {name}")
+        np.testing.assert_allclose(ref.memory.memory.detach().numpy(), z[f"b{b}_memory"], rtol=0, atol=2e-6,
+                                   err_msg=f"batch {b}")
+        np.testing.assert_array_equal(ref.memory.last_update.numpy(), z[f"b{b}_last_update"])

@@ -25,6 +25,9 @@
 // (conv2) level keeps its k / v reduction launch (tgn_kv_reduce2 beside its dE2-only GEMMs).
 // Data parallel (world > 1): the same launches without fused Adam; the exchange (one all-reduce of
 // [gradients | memory-row slots]) and tgnx_tgn_apply_rows_update follow.
+#include <mutex>
+#include <unordered_map>
+
 #include "tgnx_gemm.h"
 #include "tgnx_math.h"
 #include "tgnx_ring_dev.h"
@@ -4535,6 +4538,21 @@ size_t tgnx_tgn_plan_table_bytes(const tgnx_tgn_config* cfg, int64_t split_lo, i
   return (size_t)(64 + (nb > 0 ? nb : 1) * plan_slot_bytes(cfg->max_batch));
 }
 
+// what each plan table was built for (tgnx_tgn_plan_table), keyed by its device address: the resident parity-set
+// steps index slot (batch start - split_lo) / batch with a stride sized by max_batch, so a table built for another
+// split, batch or max_batch would silently hand them another batch's plans or read past the table
+namespace {
+struct PlanTableKey {
+  int64_t lo, hi, batch, stride;
+  size_t bytes;
+};
+std::mutex g_ptab_mu;
+std::unordered_map<const void*, PlanTableKey>& ptab_registry() {
+  static std::unordered_map<const void*, PlanTableKey> m;
+  return m;
+}
+}  // namespace
+
 int tgnx_tgn_plan_table(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo, int64_t split_hi,
                         int64_t batch, void* table, size_t table_bytes, void* stream) {
   Ctx c;
@@ -4548,6 +4566,10 @@ int tgnx_tgn_plan_table(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf,
   TGNX_CHECK_ARG(table && table_bytes >= need && ((uintptr_t)table & 15) == 0,
                  "tgnx_tgn_plan_table: table of tgnx_tgn_plan_table_bytes(...) bytes, 16-B aligned");
   const int64_t nb = (split_hi - split_lo + batch - 1) / batch;
+  {
+    std::lock_guard<std::mutex> lk(g_ptab_mu);
+    ptab_registry()[table] = PlanTableKey{split_lo, split_hi, batch, plan_slot_bytes(k.B), need};
+  }
   if (nb == 0) return TGNX_OK;
   const size_t smem = tgn_scan_smem(k.B);
   TGNX_CHECK_ARG(hipFuncSetAttribute(reinterpret_cast<const void*>(&tgn_plan_table_kernel),
@@ -4662,6 +4684,23 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   c.drop = dropout && cfg->dropout > 0.f;
   const bool ppm = pp >= 0;
   if (ppm && buf->plan_table) {  // the split's plans from the table built at binding (tgnx_tgn_plan_table)
+    PlanTableKey pk{-1, -1, -1, -1, 0};
+    bool known = false;
+    {
+      std::lock_guard<std::mutex> lk(g_ptab_mu);
+      const auto it = ptab_registry().find(buf->plan_table);
+      if (it != ptab_registry().end()) {
+        pk = it->second;
+        known = true;
+      }
+    }
+    TGNX_CHECK_ARG(known, "tgn: buf->plan_table was not built by tgnx_tgn_plan_table in this process");
+    TGNX_CHECK_ARG(adv, "tgn: plan tables serve the resident parity-set steps only");
+    TGNX_CHECK_ARG(pk.lo == adv->lo && pk.hi == adv->hi && pk.batch == adv->batch && pk.stride == plan_slot_bytes(k.B),
+                   "tgn: buf->plan_table was built for split [%lld, %lld) batch %lld (slot %lld B), the step runs "
+                   "[%lld, %lld) batch %lld (slot %lld B): rebuild it with tgnx_tgn_plan_table",
+                   (long long)pk.lo, (long long)pk.hi, (long long)pk.batch, (long long)pk.stride, (long long)adv->lo,
+                   (long long)adv->hi, (long long)adv->batch, (long long)plan_slot_bytes(k.B));
     c.ptab = reinterpret_cast<const char*>(buf->plan_table);
     c.ptab_stride = plan_slot_bytes(k.B);
   }

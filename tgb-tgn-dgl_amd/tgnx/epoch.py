@@ -80,8 +80,10 @@ def train(model, feats, train_loader, neighbor_loader, neg_dest_sampler, assoc, 
         if eng.out_ev is None or eng.out_ev.shape[0] < n:
             eng.out_ev = torch.zeros(n, 2, dtype=torch.float32, device=eng.dev)
         B = train_loader.batch_size
-        key = (train_loader.lo, train_loader.hi, B, gnn.training, ev["src"].data_ptr(), neg_buf.data_ptr(),
-               eng.out_ev.data_ptr())
+        # the captured graph bakes in every pointer of the step's buffer block (events, negatives, output log,
+        # destination set, parameters, optimizer state, workspace, ring): key it on all of them
+        bufs = eng._buffers(ev["src"], ev["dst"], ev["t"], ev["blk"], ev["msg"], neg_buf)
+        key = (train_loader.lo, train_loader.hi, B, gnn.training, bytes(bufs))
         if getattr(eng, "_bound", None) != key:   # (gnn.training: dropout of the first epoch only, :170-172)
             eng.bind_resident(ev["src"], ev["dst"], ev["t"], ev["blk"], ev["msg"], neg_buf, train_loader.lo,
                               train_loader.hi, B)

@@ -218,6 +218,18 @@ class TGNModel(nn.Module):
     def grads_by_name(self) -> dict:
         return {name: self.grad_flat[o:o + n].view(s) for name, (o, n, s) in self._views.items()}
 
+    def settle(self) -> None:
+        """Apply a data-parallel engine's deferred exchange (TgnEngine.finish) so that memory, last_update,
+        the parameters and the Adam moments are current.  state_dict() calls it; direct
+        reads of model.flat / model.memory.* between data-parallel steps need it (or engine.finish())."""
+        f = self._tgnx_finish() if getattr(self, "_tgnx_finish", None) is not None else None
+        if f is not None:
+            f()
+
+    def state_dict(self, *a, **k):
+        self.settle()
+        return super().state_dict(*a, **k)
+
     def forward(self, *a, **k):
         raise RuntimeError("tgnx TGN runs through tgnx.tgn.TgnEngine / pyg_epoch_utils (the fused HIP step)")
 
@@ -259,12 +271,20 @@ def _p(t):
 
 class TgnEngine:
     """Owns the workspace of one TGN model + one neighbour ring over a resident event table
-    (src, dst, t, msg rows = e_id)."""
+    (src, dst, t, msg rows = e_id).
+
+    Data parallel (world > 1) resident steps defer the exchanged memory rows and Adam of step k to the head of
+    step k + 1 (tgnx_tgn_train_fwd_bwd_pp).  Between such steps memory, last_update, the parameters and the
+    Adam moments are one apply behind: call finish() before reading them directly.  check(), loss_sum(),
+    flush(), eval / reset / binding calls and model.state_dict() do so themselves (the gradient buffer is final
+    once the step's exchange returned: the apply does not change it)."""
 
     def __init__(self, model: TGNModel, loader, events: dict, optimizer: TgnAdam | None = None,
                  dst_nodes=None, seed: int = 0, rank: int = 0, world: int = 1):
         self.model, self.loader, self.opt = model, loader, optimizer
         self.dev = model.device
+        import weakref
+        model._tgnx_finish = weakref.WeakMethod(self.finish)   # model.settle(): the deferred apply, if any
         cfg = model.cfg
         if cfg.ring != loader.size:
             cfg.ring = loader.size
@@ -685,7 +705,12 @@ class TgnEngine:
                     "or a prefetch that no longer holds",
                 32: "edge sort beyond its LDS counters"}
 
-    def check(self):
+    def check(self, settle: bool = True):
+        """Raise on the step error flags (ctl[11]).  settle: first apply a deferred data-parallel exchange
+        (finish()), so the state is current afterwards; False leaves it pending (tests that perform the
+        exchange themselves after the step returned)."""
+        if settle:
+            self.finish()
         err = int(self.ctl[11].item())
         if err:
             why = "; ".join(m for b, m in self.ERR_BITS.items() if err & b) or "unknown"
