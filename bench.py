@@ -424,6 +424,7 @@ def run_tgn(args, world, rank, dev):
     loader = LastNeighborLoader(N, K, device=dev)
     eng = TgnEngine(model, loader, dict(src=stream.src, dst=stream.dst, t=stream.t.astype(np.float32), msg=stream.msg),
                     opt, dst_nodes=np.unique(stream.dst), seed=1234, rank=rank, world=world)
+    eng.keep_grads = False    # nothing reads the gradient buffer (world 1: TGNX_TGN_NO_GRAD_STORE)
     eng.bind_resident(0, stream.train_end, Bg, dropout=not args.no_dropout)
     nb_epoch = math.ceil(stream.train_end / Bg)
     counter = {"i": 0}

@@ -329,7 +329,12 @@ typedef struct {
                                      the steps' split_lo / split_hi / batch and this config's max_batch: the
                                      library records that when it builds the table and the steps refuse
                                      (TGNX_EINVAL) a table it did not build or one built for another split. */
+  int32_t flags;                  /* TGNX_TGN_* bits below (0: defaults) */
 } tgnx_tgn_buffers;
+/* tgnx_tgn_buffers.flags: the steps with Adam fused into the gradient writers (tgnx_tgn_train_step*, world 1)
+ * update parameters and moments without storing the gradient in buf->grads (the batch loss slot
+ * grads[P] is still written); for loops that never read the gradients (the benchmark, the drop-in train()) */
+#define TGNX_TGN_NO_GRAD_STORE 1
 /* exchanged memory row, all fields floats holding exact integers so that the row survives a SUM exchange
  * (one all-reduce over [gradients | every rank's row slots, zero but the sender's] is the all-gather):
  * node (-1 = unused slot; num_nodes < 2^24), last_update bits 0-23, 24-47, 48-63, memory[D] */

@@ -513,3 +513,52 @@ def test_tgn_engine_matches_reference_model_wiring():
             assert r < 2e-3, (b, name, r)
         assert np.allclose(model.memory.memory.cpu().numpy(), z[f"b{b}_memory"], atol=1e-5), b
         assert np.array_equal(model.memory.last_update.cpu().numpy(), z[f"b{b}_last_update"]), b
+
+
+def test_tgn_no_grad_store_same_step():
+    """TGNX_TGN_NO_GRAD_STORE (TgnEngine.keep_grads = False, what bench.py and the drop-in train() run): the
+    replayed parity-set steps with Adam fused leave the gradient buffer untouched (the loss slot aside) and
+    produce the same parameters, moments, memory, outputs and loss as the same steps storing it — within the
+    run-to-run spread of the float atomics' order (dZc / hub dP sums), as the other step-form comparisons."""
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    s, ref, opt_ref, lref, model, opt, eng = _setup("last")
+    dev = torch.device("cuda")
+    sd = ref.state_dict()
+    engs = []
+    for keep in (True, False):
+        m = TGNModel(300, s.num_events, 16, 32, dev, ring=10, max_batch=50, max_neg=1, aggr="last", dropout=0.1)
+        m.load_reference_state(sd)
+        e = TgnEngine(m, LastNeighborLoader(300, 10, device=dev), dict(src=s.src, dst=s.dst,
+                      t=s.t.astype(np.float32), msg=s.msg), TgnAdam(m, 1e-3), dst_nodes=s.dst_nodes, seed=5)
+        e.keep_grads = keep
+        e.bind_resident(0, 8 * 50, 50, dropout=True)
+        e.begin_epoch()
+        e.capture_resident()
+        m.grad_flat.fill_(7.0)
+        engs.append(e)
+    for st in range(8):
+        for e in engs:
+            e.replay_resident()
+        torch.cuda.synchronize()
+        a, b = engs
+        a.check()
+        b.check()
+        for name in a.model.param_order:
+            if name in SHIFT_INVARIANT:
+                continue
+            o, n, _ = a.model._views[name]
+            assert _rel(b.model.flat[o:o + n], a.model.flat[o:o + n]) < 1e-5, (st, name)
+            assert _rel(b.adam_m[o:o + n], a.adam_m[o:o + n]) < 1e-4, (st, name)
+        assert torch.allclose(a.model.memory.memory, b.model.memory.memory, atol=1e-5), st
+        assert torch.equal(a.model.memory.last_update, b.model.memory.last_update), st
+        assert torch.allclose(a.out_pos, b.out_pos, atol=1e-5) and torch.allclose(a.out_neg, b.out_neg, atol=1e-5), st
+        assert abs(a.loss_sum() - b.loss_sum()) <= 1e-5 * max(1.0, abs(a.loss_sum())), st
+        G = b.model.grad_flat
+        assert torch.all(G[:-1] == 7.0), st                    # never stored
+        assert not torch.all(a.model.grad_flat[:-1] == 7.0), st
+        with torch.no_grad():   # re-synchronise (the wiki time scale turns ulp differences chaotic, DESIGN §7)
+            b.model.flat.copy_(a.model.flat)
+            b.adam_m.copy_(a.adam_m)
+            b.adam_v.copy_(a.adam_v)
+            b.model.memory.memory.copy_(a.model.memory.memory)

@@ -61,6 +61,9 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // the kernel id, block and XCC into a buffer set by tgnx_stamps_set (tools/stamps.py reads it).  Without the
 // flag TGNX_STAMP(k) is empty and the buffer entry points return TGNX_EINVAL.
 #ifdef TGNX_STAMPS
+#ifndef TGNX_STAMP_TID
+#define TGNX_STAMP_TID 0  // the recording thread (its wave's view of the checkpoints)
+#endif
 struct StampRec {
   unsigned long long t0, t1;
   unsigned kid, blk, xcc, wave;
@@ -77,7 +80,7 @@ struct StampScope {  // wave 0 of each workgroup records
     mid = slot ? (mid & 0xFFFFu) | (d << 16) : (mid & 0xFFFF0000u) | d;
   }
   __device__ ~StampScope() {
-    if (threadIdx.x == 0 && g_stamp_buf) {
+    if (threadIdx.x == TGNX_STAMP_TID && g_stamp_buf) {
       const unsigned sh = blockIdx.x & 63, i = atomicAdd(&g_stamp_cnt[sh * 32], 1u);
       if (i < g_stamp_cap)
         g_stamp_buf[(size_t)sh * g_stamp_cap + i] =

@@ -156,6 +156,7 @@ struct AdamFuse {
   float *p = nullptr, *m = nullptr, *v = nullptr;
   const int64_t* ctl = nullptr;
   float b1 = 0.f, b2 = 0.f, eps = 0.f;
+  int keep_g = 1;  // fused: also store the gradient (0: TGNX_TGN_NO_GRAD_STORE, nothing reads it; 1.1 MB less per step)
   // n gradient elements (idx < 0: none) of one thread: every load issued before any store (the
   // buffers may alias as far as the compiler knows, so interleaving would serialise the elements)
   template <int N>
@@ -182,7 +183,7 @@ struct AdamFuse {
     for (int i = 0; i < N; ++i) {
       if (idx[i] < 0) continue;
       adam1(val[i], mm[i], vv[i], pp[i], b1, b2, eps, s0, s1);
-      st_wt(g + idx[i], val[i]);
+      if (keep_g) st_wt(g + idx[i], val[i]);
       st_wt(m + idx[i], mm[i]);
       st_wt(v + idx[i], vv[i]);
       st_wt(p + idx[i], pp[i]);
@@ -2072,8 +2073,33 @@ constexpr int ATT_EB = 16;  // edges whose neighbour rows are loaded in one batc
 // edge rows of every edge and its skip row as one round (each edge row loaded once for k + e and v + e);
 // longer rings walk ATT_EB-edge load batches.  Train: the softmax weights go to alpha (tgn_attn_bwd).
 // jrec >= 0 (a per-root record, lanes 0..ne-1): lane e's neighbour row of edge e, instead of e_j
+// st != nullptr (train): the alpha / alk / Qo stores are left in *st for the caller to issue later (tgn_pred_train
+// issues them after its first barrier: an LDS read after that barrier waits for vmcnt(0) — the staging wave's LDS-DMA
+// is tracked by vmcnt — and would otherwise wait for these stores to land)
+struct AttnStores {
+  float a0, a1, t0, t1, q0, q1, o0, o1;
+  int x, e0, ne;
+  __device__ void issue(const Ctx& c, int lane) const {
+    if (lane < ne) {
+      c.alpha[(int64_t)(e0 + lane) * 2] = a0;
+      c.alpha[(int64_t)(e0 + lane) * 2 + 1] = a1;
+      if (c.kvf) {
+        c.alk[(int64_t)(e0 + lane) * 2] = t0;
+        c.alk[(int64_t)(e0 + lane) * 2 + 1] = t1;
+      }
+    }
+    if (c.kvf && lane < c.C) {
+      float* qo = c.Qo + (int64_t)x * 2 * c.HC;
+      qo[lane] = q0;
+      qo[c.C + lane] = q1;
+      qo[c.HC + lane] = o0;
+      qo[c.HC + c.C + lane] = o1;
+    }
+  }
+};
 template <bool TRAIN>
-__device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0, int ne, int lane, int jrec = -1) {
+__device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0, int ne, int lane, int jrec = -1,
+                                              AttnStores* st = nullptr) {
   const int C = c.C, HC = c.HC;
   const float on = f01(lane < C);
   const int l0 = min(lane, C - 1);
@@ -2100,21 +2126,38 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
     t0 = a0;
     t1 = a1;
     if (TRAIN && lane < ne) {
-      c.alpha[(int64_t)(e0 + lane) * 2] = a0;
-      c.alpha[(int64_t)(e0 + lane) * 2 + 1] = a1;
       if (c.drop) {
         const uint32_t base = drop_base(dseed, (uint64_t)c.att_salt, dnode, deid);
         t0 *= keep32(base, 0u, c.p, c.inv_keep);
         t1 *= keep32(base, 1u, c.p, c.inv_keep);
       }
-      if (c.kvf) {
-        c.alk[(int64_t)(e0 + lane) * 2] = t0;
-        c.alk[(int64_t)(e0 + lane) * 2 + 1] = t1;
+      if (st) {
+        st->a0 = a0;
+        st->a1 = a1;
+        st->t0 = t0;
+        st->t1 = t1;
+      } else {
+        c.alpha[(int64_t)(e0 + lane) * 2] = a0;
+        c.alpha[(int64_t)(e0 + lane) * 2 + 1] = a1;
+        if (c.kvf) {
+          c.alk[(int64_t)(e0 + lane) * 2] = t0;
+          c.alk[(int64_t)(e0 + lane) * 2 + 1] = t1;
+        }
       }
     }
   };
   // kvf: the centre's q and aggregated message output (every root of the centre writes equal values)
   auto put_qo = [&]() {
+    if (TRAIN && st) {
+      st->q0 = q0;
+      st->q1 = q1;
+      st->o0 = o0;
+      st->o1 = o1;
+      st->x = x;
+      st->e0 = e0;
+      st->ne = ne;
+      return;
+    }
     if (TRAIN && c.kvf && lane < C) {
       float* qo = c.Qo + (int64_t)x * 2 * HC;
       qo[lane] = q0;
@@ -2307,6 +2350,13 @@ __global__ void __launch_bounds__(1024) tgn_plan_table_kernel(Ctx c, char* tab, 
   if (B <= 0) return;
   plan_part<8>(c, role < P ? 0 : 1, role % P, P, B, start, psm_, sh, NoCheckpoint{}, plan_slot(tab, stride, c.Bplan, b));
 }
+#ifndef TGNX_PRED_DEFER
+#define TGNX_PRED_DEFER 1  // the 1-hop attention's global stores issued after the first barrier (0: inside attn_centre)
+#endif
+#ifndef TGNX_PRED_TAIL2
+#define TGNX_PRED_TAIL2 0  // predictor tail: every wave runs the epilogue, backward by output quarters (1), or the
+                           // wave-0 epilogue + split-k backward (0)
+#endif
 template <bool ATT>
 __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, PlanOut po, int npl) {
   TGNX_STAMP(5);
@@ -2343,12 +2393,26 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
   const int i = lo + blockIdx.x;
   const bool live = !(B == 0 || i >= hi || err != 0);
   constexpr int NST = ATT ? 64 : 192;  // staging threads (ATT: wave 0; 8 waves with 5 staging ones: ±0)
+  // (out_ev: the batch's first event, loaded with the first round — a load after the evs-row stores would wait
+  // for all of them, vmcnt retiring in order)
+  const int64_t bstart = c.out_ev ? c.ctl[TGNX_CTL_BATCH_START] : 0;
+  AttnStores ast;  // ATT, waves 1-3: the attention's alpha / alk / Qo stores, issued after the first barrier
+  ast.ne = 0;
+  ast.x = -1;
   if (ATT && wv >= 1) {
     const int r = wv - 1;
     const int4 q = c.evq[3 * blockIdx.x + r];  // {centre row, P row, edge range}; grid = max_batch: in bounds
     const int jr = c.evj ? c.evj[(3 * blockIdx.x + r) * 16 + (lane & 15)] : -1;  // the edges' neighbour rows
     if (!live) return;
-    const float2 o = attn_centre<true>(c, q.x, q.y, q.z, q.w - q.z, lane, c.evj && q.w - q.z <= 16 ? max(jr, 0) : -1);
+#if TGNX_PRED_CKPT == 3  // (diagnostic, with TGNX_STAMP_TID 64: wave 1's first round landed / its attention done)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    TGNX_STAMP_AT(0);
+#endif
+    const float2 o = attn_centre<true>(c, q.x, q.y, q.z, q.w - q.z, lane, c.evj && q.w - q.z <= 16 ? max(jr, 0) : -1,
+                                       TGNX_PRED_DEFER ? &ast : nullptr);
+#if TGNX_PRED_CKPT == 3
+    TGNX_STAMP_AT(1);
+#endif
     if (lane < c.C) {
       z[r][lane] = o.x;
       z[r][c.C + lane] = o.y;
@@ -2452,16 +2516,78 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
       }
     }
   }
-#ifdef TGNX_STAMP_STAGE  // diagnostic: checkpoint 1 = wave 0 done with its part before the first barrier
-  TGNX_STAMP_AT(1);
+// diagnostic checkpoint placement (stamps build, wave 0's view): TGNX_PRED_CKPT 0 = after the forward contraction's
+// barrier / after the epilogue's barrier; 1 = wave 0 done staging / the first barrier passed; 2 = the last barrier
+// passed / the dZc atomics issued
+#ifndef TGNX_PRED_CKPT
+#define TGNX_PRED_CKPT 0
+#endif
+#if TGNX_PRED_CKPT == 1 || defined(TGNX_STAMP_STAGE)  // checkpoint = wave 0 done with its part before the first barrier
+  TGNX_STAMP_AT(TGNX_PRED_CKPT == 1 ? 0 : 1);
 #endif
   // LDS-only barriers in this kernel (the weights, embedding rows and partial sums are LDS; the attention's
   // alpha stores and the evs rows need not have landed): __syncthreads would wait for vmcnt(0)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+#if TGNX_PRED_CKPT == 1
+  TGNX_STAMP_AT(1);
+#endif
+  if (ATT && TGNX_PRED_DEFER && ast.x >= 0) ast.issue(c, lane);
   const int cr[3] = {scr[0], scr[1], scr[2]};
   const int kc = (D + 3) / 4, k0 = wv * kc, nk = min(D - k0, kc);
-  if (flat) {  // lin_src(z_s), lin_dst(z_p), lin_dst(z_n): wave wv takes float4 columns [q0, q0 + nq)
+  if (TGNX_PRED_TAIL2 >= 2 && flat) {
+    // lin_src(z_s), lin_dst(z_p), lin_dst(z_n): wave wv takes float4 columns [q0, q0 + nq) of both output halves at
+    // once; the embedding values come from this wave's slice held one per lane and broadcast through scalar
+    // registers (v_readlane), so the LDS carries only the weight rows (a broadcast ds_read_b128 of z costs the
+    // same LDS cycles as a row read: they were 3 of every 5 reads)
+    const int c4 = D / 4, kq = (c4 + 3) / 4, q0 = wv * kq, nq = max(0, min(c4 - q0, kq));
+    const int kz = min(4 * q0 + lane, D - 1);
+    const float zl0 = z[0][kz], zl1 = z[1][kz], zl2 = z[2][kz];
+    const int oA = min(lane, D - 1), oB = min(lane + 64, D - 1);
+    const float4* wsA = reinterpret_cast<const float4*>(Wsrc + oA * D) + q0;
+    const float4* wdA = reinterpret_cast<const float4*>(Wdst + oA * D) + q0;
+    const float4* wsB = reinterpret_cast<const float4*>(Wsrc + oB * D) + q0;
+    const float4* wdB = reinterpret_cast<const float4*>(Wdst + oB * D) + q0;
+    float a0 = 0.f, b0 = 0.f, c0 = 0.f, a1 = 0.f, b1 = 0.f, c1 = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // (kq <= 8 for D <= 128): two rounds of <= 4 columns, every row read in flight
+      if (4 * h >= nq) break;
+      float4 u0[4], v0[4], u1[4], v1[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = min(4 * h + t, nq - 1);
+        u0[t] = wsA[j];
+        v0[t] = wdA[j];
+        u1[t] = wsB[j];
+        v1[t] = wdB[j];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = 4 * h + t;
+        if (j >= nq) break;
+        const float x00 = lane_f(zl0, 4 * j), x01 = lane_f(zl0, 4 * j + 1), x02 = lane_f(zl0, 4 * j + 2),
+                    x03 = lane_f(zl0, 4 * j + 3);
+        const float x10 = lane_f(zl1, 4 * j), x11 = lane_f(zl1, 4 * j + 1), x12 = lane_f(zl1, 4 * j + 2),
+                    x13 = lane_f(zl1, 4 * j + 3);
+        const float x20 = lane_f(zl2, 4 * j), x21 = lane_f(zl2, 4 * j + 1), x22 = lane_f(zl2, 4 * j + 2),
+                    x23 = lane_f(zl2, 4 * j + 3);
+        a0 += (u0[t].x * x00 + u0[t].y * x01) + (u0[t].z * x02 + u0[t].w * x03);
+        b0 += (v0[t].x * x10 + v0[t].y * x11) + (v0[t].z * x12 + v0[t].w * x13);
+        c0 += (v0[t].x * x20 + v0[t].y * x21) + (v0[t].z * x22 + v0[t].w * x23);
+        a1 += (u1[t].x * x00 + u1[t].y * x01) + (u1[t].z * x02 + u1[t].w * x03);
+        b1 += (v1[t].x * x10 + v1[t].y * x11) + (v1[t].z * x12 + v1[t].w * x13);
+        c1 += (v1[t].x * x20 + v1[t].y * x21) + (v1[t].z * x22 + v1[t].w * x23);
+      }
+    }
+    part[wv][0][lane] = a0;
+    part[wv][1][lane] = b0;
+    part[wv][2][lane] = c0;
+    if (lane + 64 < D) {
+      part[wv][0][lane + 64] = a1;
+      part[wv][1][lane + 64] = b1;
+      part[wv][2][lane + 64] = c1;
+    }
+  } else if (flat) {  // lin_src(z_s), lin_dst(z_p), lin_dst(z_n): wave wv takes float4 columns [q0, q0 + nq)
     const int c4 = D / 4, kq = (c4 + 3) / 4, q0 = wv * kq, nq = max(0, min(c4 - q0, kq));
     const float4* z0 = reinterpret_cast<const float4*>(z[0]) + q0;
     const float4* z1 = reinterpret_cast<const float4*>(z[1]) + q0;
@@ -2505,8 +2631,166 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+#if TGNX_PRED_CKPT == 0
   TGNX_STAMP_AT(0);
+#endif
   float* ev = c.evs + (int64_t)i * evs_stride(D);
+#if TGNX_PRED_TAIL2
+  // every wave runs the forward epilogue (the same values in each: no dh round through a barrier); then wave wv
+  // computes the input gradients of its quarter of the outputs over the whole hidden width (lanes: 2 halves of the
+  // hidden units x the quarter's outputs, dh from this wave's own LDS copy) and issues their dZc atomics; wave 0
+  // stores the event's row, outputs and loss term last (off the chain to the atomics)
+#if TGNX_PRED_TAIL2 < 2
+  __shared__ float dhw[4][2][TDMAX];
+#endif
+  float hp[2], hn[2], dhp[2], dhn[2];
+  float ap, an, sp, sn, dap, dan;
+  const float invB = 1.0f / (float)B;
+  {
+    float zp = 0.f, zn = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int o = lane + 64 * q;
+      hp[q] = hn[q] = 0.f;
+      if (o < D) {
+        const float s = ((part[0][0][o] + part[1][0][o]) + (part[2][0][o] + part[3][0][o])) + vsb[o];
+        const float dp = ((part[0][1][o] + part[1][1][o]) + (part[2][1][o] + part[3][1][o])) + vdb[o];
+        const float dn = ((part[0][2][o] + part[1][2][o]) + (part[2][2][o] + part[3][2][o])) + vdb[o];
+        hp[q] = fmaxf(s + dp, 0.f);
+        hn[q] = fmaxf(s + dn, 0.f);
+        zp += vfw[o] * hp[q];
+        zn += vfw[o] * hn[q];
+      }
+    }
+    ap = wave_sum_f(zp) + vfw[D];
+    an = wave_sum_f(zn) + vfw[D];
+    sp = sigm(ap);
+    sn = sigm(an);
+    dap = (sigm(sp) - 1.0f) * sp * (1.0f - sp) * invB;
+    dan = sigm(sn) * sn * (1.0f - sn) * invB;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int o = lane + 64 * q;
+      const float wf = o < D ? vfw[o] : 0.f;
+      dhp[q] = hp[q] > 0.f ? dap * wf : 0.f;
+      dhn[q] = hn[q] > 0.f ? dan * wf : 0.f;
+#if TGNX_PRED_TAIL2 < 2
+      if (o < D) {
+        dhw[wv][0][o] = dhp[q];
+        dhw[wv][1][o] = dhn[q];
+      }
+#endif
+    }
+  }
+#if TGNX_PRED_CKPT == 0
+  TGNX_STAMP_AT(1);
+#endif
+#if TGNX_PRED_TAIL2 >= 2
+  {
+    // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn: wave wv takes the hidden units [kb, kb + nkb),
+    // lanes over the outputs o = lane, lane + 64 (conflict-free row reads), dh[kk] broadcast from the lane that
+    // holds it (v_readlane); the four partial sums meet in LDS behind one barrier
+    __shared__ float pb[4][3][TDMAX];  // (not part: a slower wave may still read part in its epilogue)
+    const int kcb = (D + 3) / 4, kb = wv * kcb, nkb = max(0, min(D - kb, kcb));
+    const int oA = min(lane, D - 1), oB = min(lane + 64, D - 1);
+    float a0 = 0.f, b0 = 0.f, c0 = 0.f, a1 = 0.f, b1 = 0.f, c1 = 0.f;
+#pragma unroll 5
+    for (int t = 0; t < nkb; ++t) {
+      const int kk = kb + t;
+      const float h0 = kk < 64 ? lane_f(dhp[0], kk) : lane_f(dhp[1], kk - 64);
+      const float h1 = kk < 64 ? lane_f(dhn[0], kk) : lane_f(dhn[1], kk - 64);
+      const float* rs = Wsrc + kk * DP;
+      const float* rd = Wdst + kk * DP;
+      const float sA = rs[oA], dA = rd[oA], sB = rs[oB], dB = rd[oB];
+      a0 += sA * (h0 + h1);
+      b0 += dA * h0;
+      c0 += dA * h1;
+      a1 += sB * (h0 + h1);
+      b1 += dB * h0;
+      c1 += dB * h1;
+    }
+    pb[wv][0][lane] = a0;
+    pb[wv][1][lane] = b0;
+    pb[wv][2][lane] = c0;
+    if (lane + 64 < D) {
+      pb[wv][0][lane + 64] = a1;
+      pb[wv][1][lane + 64] = b1;
+      pb[wv][2][lane + 64] = c1;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#if TGNX_PRED_CKPT == 2
+    TGNX_STAMP_AT(0);
+#endif
+    for (int x = tid; x < 3 * D; x += blockDim.x) {
+      const int r = x >= 2 * D ? 2 : x >= D ? 1 : 0, o = x - r * D;
+      const float g = (pb[0][r][o] + pb[1][r][o]) + (pb[2][r][o] + pb[3][r][o]);
+      atomicAdd(&c.dZc[(int64_t)cr[r] * D + o], g);
+    }
+#if TGNX_PRED_CKPT == 2
+    TGNX_STAMP_AT(1);
+#endif
+  }
+#else
+  {
+    // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn for outputs o of this wave's quarter
+    const int ow = (D + 3) / 4, ol = lane & 31, kh = lane >> 5, o = wv * ow + ol, hw = D / 2;  // (D even, ow <= 32)
+    const bool oko = ol < ow && o < D;
+    const int oc = oko ? o : 0, kb = kh * hw;
+    float a = 0.f, b = 0.f, d2 = 0.f;
+#pragma unroll 5
+    for (int j = 0; j < hw; ++j) {
+      const int kk = kb + j;
+      const float h0 = dhw[wv][0][kk], h1 = dhw[wv][1][kk];
+      const float w1 = Wsrc[kk * DP + oc], w2 = Wdst[kk * DP + oc];
+      a += w1 * (h0 + h1);
+      b += w2 * h0;
+      d2 += w2 * h1;
+    }
+    a = swap32_sum(a);
+    b = swap32_sum(b);
+    d2 = swap32_sum(d2);
+#if TGNX_PRED_CKPT == 2
+    TGNX_STAMP_AT(0);
+#endif
+    if (kh == 0 && oko) {
+      atomicAdd(&c.dZc[(int64_t)cr[0] * D + o], a);
+      atomicAdd(&c.dZc[(int64_t)cr[1] * D + o], b);
+      atomicAdd(&c.dZc[(int64_t)cr[2] * D + o], d2);
+    }
+#if TGNX_PRED_CKPT == 2
+    TGNX_STAMP_AT(1);
+#endif
+  }
+#endif
+  if (wv == 0) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int o = lane + 64 * q;
+      if (o < D) {
+        ev[o] = z[0][o];
+        ev[D + o] = z[1][o];
+        ev[2 * D + o] = z[2][o];
+        ev[3 * D + o] = dhp[q];
+        ev[4 * D + o] = dhn[q];
+        ev[5 * D + o] = hp[q];
+        ev[6 * D + o] = hn[q];
+      }
+    }
+    if (lane == 0) {
+      float* s = ev + 7 * D;
+      s[0] = ap; s[1] = an; s[2] = sp; s[3] = sn; s[4] = dap; s[5] = dan;
+      s[6] = (softplusf(-sp) + softplusf(sn)) * invB;
+      c.out_pos[i] = sp;
+      c.out_neg[i] = sn;
+      if (c.out_ev) {
+        const int64_t e = bstart + i;
+        c.out_ev[2 * e] = sp;
+        c.out_ev[2 * e + 1] = sn;
+      }
+    }
+  }
+#else
   if (wv == 0) {
     float hp[2], hn[2], zp = 0.f, zn = 0.f;
 #pragma unroll
@@ -2553,7 +2837,7 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
       c.out_pos[i] = sp;
       c.out_neg[i] = sn;
       if (c.out_ev) {
-        const int64_t e = c.ctl[TGNX_CTL_BATCH_START] + i;
+        const int64_t e = bstart + i;
         c.out_ev[2 * e] = sp;
         c.out_ev[2 * e + 1] = sn;
       }
@@ -2562,7 +2846,7 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
   // barrier for dh (LDS) only: the evs-row stores of wave 0 stay in flight (__syncthreads waits vmcnt(0))
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-#ifndef TGNX_STAMP_STAGE
+#if TGNX_PRED_CKPT == 0 && !defined(TGNX_STAMP_STAGE)
   TGNX_STAMP_AT(1);
 #endif
   // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn (split over k, lanes over o)
@@ -2586,12 +2870,19 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
   // LDS-only barrier again: the evs-row and alpha stores stay in flight
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+#if TGNX_PRED_CKPT == 2
+  TGNX_STAMP_AT(0);
+#endif
 #pragma unroll
   for (int r = 0; r < 3; ++r)
     for (int o = tid; o < D; o += blockDim.x) {
       const float g = (part[0][r][o] + part[1][r][o]) + (part[2][r][o] + part[3][r][o]);
       atomicAdd(&c.dZc[(int64_t)cr[r] * D + o], g);
     }
+#if TGNX_PRED_CKPT == 2
+  TGNX_STAMP_AT(1);
+#endif
+#endif
 }
 
 // predictor bias / output-layer / loss reductions over this rank's events (wave per output)
@@ -4677,6 +4968,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     c.adf.b1 = c.b1;
     c.adf.b2 = c.b2;
     c.adf.eps = c.eps;
+    c.adf.keep_g = (buf->flags & TGNX_TGN_NO_GRAD_STORE) ? 0 : 1;
   }
   TGNX_CHECK_ARG(!gen_neg || (buf->dst_nodes && buf->n_dst > 0), "tgnx_tgn_train_fwd_bwd: no destination set");
   TGNX_CHECK_ARG(pipe == 0 || adv, "tgnx_tgn_train_step_pipelined: resident steps only");

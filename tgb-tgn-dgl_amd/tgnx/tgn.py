@@ -57,7 +57,7 @@ class TgnBuffers(ctypes.Structure):
                 ("n_dst", ctypes.c_int64), ("nbr", P), ("eid", P), ("rt", P), ("assoc", P), ("memory", P),
                 ("last_update", P), ("store", P), ("node_gen", P), ("params", P), ("grads", P), ("adam_m", P),
                 ("adam_v", P), ("ctl", P), ("out_pos", P), ("out_neg", P), ("mrr", P), ("ws", P), ("xrows", P),
-                ("xcap", ctypes.c_int64), ("out_ev", P), ("plan_table", P)]
+                ("xcap", ctypes.c_int64), ("out_ev", P), ("plan_table", P), ("flags", ctypes.c_int32)]
 
 
 # the memory modules' updater cell: TGNMemory.memory_updater (memory_module.py:70-78, memory_updater_cell
@@ -313,6 +313,10 @@ class TgnEngine:
         self.dst_nodes = None if dst_nodes is None else torch.as_tensor(dst_nodes).to(self.dev, torch.long).contiguous()
         self.seed, self.rank, self.world = int(seed), int(rank), int(world)
         self.fuse_adam = True
+        # fused-Adam steps also store the gradient in model.grad_flat (grads_by_name); loops that never read it
+        # (bench.py, the drop-in train()) set False before bind_resident: TGNX_TGN_NO_GRAD_STORE, 1.1 MB of
+        # stores less per wiki-shaped step.  Data-parallel steps always write it (it is the exchange).
+        self.keep_grads = True
         # resident steps fold the batch cursor into the step's first launch: tgnx_tgn_train_step_resident
         # (world 1, Adam fused) or tgnx_tgn_train_fwd_bwd_resident (world > 1; exchange + update follow).
         # Both forms are tested against advance + step per rank (test_gpu_tgn.py, test_gpu_tgn_dp.py).
@@ -391,6 +395,7 @@ class TgnEngine:
         b.xrows, b.xcap = _p(self.xrows), (0 if self.xrows is None else self.xcap)
         b.out_ev = _p(self.out_ev)
         b.plan_table = _p(self.plan_table)
+        b.flags = 0 if self.keep_grads else 1   # TGNX_TGN_NO_GRAD_STORE
         return b
 
     def _stream(self):

@@ -50,6 +50,7 @@ def _engine(model, train_loader, neighbor_loader, optimizer, neg_dest_sampler=No
         # the per-event train-output log (tgnx_tgn_buffers.out_ev): every replayed step writes its batch's
         # outputs at their event rows, so the epoch's AP / AUC need no copy per step
         eng.out_ev = torch.zeros(eng.cfg.num_events, 2, dtype=torch.float32, device=eng.dev)
+        eng.keep_grads = False    # the loop never reads the gradients (Adam fused: TGNX_TGN_NO_GRAD_STORE)
         eng._mode_train = None
         eng._bound = None
         m._tgnx_engine = eng
