@@ -74,3 +74,39 @@ def test_exchange_all_reduce_is_all_gather():
     # header round trip
     for v, lu in ((0, 0), (16_777_215, (1 << 63) - 1), (5, -(1 << 40)), (123, 1_700_000_000)):
         assert row_decode(np.asarray(row_header(v, lu), dtype=np.float32)) == (v, lu)
+
+
+def _run_modes(rank, world, port, out_dir):
+    import sys
+    if PKG not in sys.path:
+        sys.path.insert(0, PKG)
+    from tgnx.tgn import exchange_collectives
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rw = D + 4
+    for mode in ("fused", "split"):
+        for async_op in (False, True):
+            comm = torch.zeros(G + world * XCAP * rw, dtype=torch.float32)
+            comm[:G] = torch.from_numpy(np.random.default_rng(rank).standard_normal(G).astype(np.float32))
+            xg = comm[G:].view(world * XCAP, rw)
+            xg[rank * XCAP:(rank + 1) * XCAP] = torch.from_numpy(_slot(rank))
+            for w in exchange_collectives(comm, G, rank, world, mode, async_op=async_op):
+                w.wait()
+            np.save(os.path.join(out_dir, f"{mode}_{int(async_op)}_r{rank}.npy"), comm.numpy())
+    dist.destroy_process_group()
+
+
+def test_exchange_modes_agree():
+    """The engine's exchange knob (TgnEngine.exchange_mode / TGNX_EXCHANGE; tgnx.tgn.exchange_collectives):
+    'split' = gradient all-reduce + in-place all_gather_into_tensor of the row slots gives bit for bit the buffer
+    that 'fused' (one all-reduce of [gradients | slots]) gives, on every rank, blocking and async."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_run_modes, args=(world, _free_port(), d), nprocs=world, join=True)
+        outs = {(m, a, r): np.load(os.path.join(d, f"{m}_{a}_r{r}.npy"))
+                for m in ("fused", "split") for a in (0, 1) for r in range(world)}
+    ref = outs[("fused", 0, 0)]
+    want = np.concatenate([_slot(r) for r in range(world)])
+    assert np.array_equal(ref[G:].reshape(world * XCAP, D + 4).view(np.uint32), want.view(np.uint32))
+    for k, v in outs.items():
+        assert np.array_equal(v.view(np.uint32), ref.view(np.uint32)), k

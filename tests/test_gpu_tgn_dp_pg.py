@@ -6,7 +6,8 @@ dist.all_reduce over [gradients | memory-row slots].  Step forms (tgnx/tgn.py Tg
             (1 hop; the default);
   * split — the split pipelined step: fwd_bwd graph, the collective with the next batch's scan replayed
             beside it, the apply + Adam graph (the 2-hop form);
-  * fold  — fwd_bwd with the scan folded in, the collective, the apply + Adam graph.
+  * fold  — fwd_bwd with the scan folded in, the collective, the apply + Adam graph;
+  * pp-xsplit — pp with the exchange split into a gradient all-reduce and a row all-gather (TGNX_EXCHANGE=split).
 BASELINE's configs at their world sizes: #4 tgbl-coin-shaped at world 4 (global batch 800: 1,600 plan keys,
 partitioned plans, 4 row slots), #5 tgbl-comment-shaped 2-hop at world 8 with the strong-scaling reading
 (global 600 -> 75 events per rank, N = 994,790), and the headline tgbl-wiki shape at world 8 (weak scaling,
@@ -105,8 +106,10 @@ def _state(eng):
 
 
 def _configure(eng, mode):
-    eng.parity_sets = mode == "pp"
+    eng.parity_sets = mode in ("pp", "pp-xsplit")
     eng.split_scan = mode == "split"
+    # pp-xsplit: the parity-set step with the exchange as gradient all-reduce + row all-gather (TGNX_EXCHANGE=split)
+    eng.exchange_mode = "split" if mode == "pp-xsplit" else "fused"
 
 
 def _worker(case, rank, world, port, lr, mode, out_dir):
@@ -127,7 +130,7 @@ def _worker(case, rank, world, port, lr, mode, out_dir):
         eng.bind_resident(0, _split_hi(case), Bg, dropout=True)
         eng.begin_epoch()
         eng.capture_resident()
-        assert eng._dp_pp() == (mode == "pp"), (mode, eng._dp_pp())
+        assert eng._dp_pp() == mode.startswith("pp"), (mode, eng._dp_pp())
         e1 = None
         if rank == 0:
             e1 = _engine(case, s, 0, 1, lr)     # world 1 over the same GLOBAL batches
@@ -138,7 +141,7 @@ def _worker(case, rank, world, port, lr, mode, out_dir):
             eng.replay_resident()
             if e1 is not None:
                 e1.resident_train_step()
-            compare = mode != "pp" or st % 2 == 1 or st == NB - 2
+            compare = not mode.startswith("pp") or st % 2 == 1 or st == NB - 2
             if not compare:
                 continue
             eng.finish()
@@ -224,7 +227,7 @@ def test_tgn_dp_process_group_lr0_matches_world1(tmp_path, mode):
     _run_ranks("wiki-small", 0.0, mode, tmp_path)
 
 
-@pytest.mark.parametrize("mode", ["pp", "split"])
+@pytest.mark.parametrize("mode", ["pp", "split", "pp-xsplit"])
 def test_tgn_dp_process_group_replicas_stay_identical(tmp_path, mode):
     _run_ranks("wiki-small", 1e-3, mode, tmp_path)
 

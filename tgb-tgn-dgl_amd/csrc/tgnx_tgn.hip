@@ -319,6 +319,10 @@ __device__ __forceinline__ int div_small(int e, int d, float inv) {
   return q;
 }
 __device__ __forceinline__ float softplusf(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
+// softplus of an argument in [-1, 1] (BCE-with-logits on a sigmoid output): 1 + e^-|x| lies in [1.37, 2], so the
+// hardware log / exp (1-2 ulp) carry no cancellation; log1pf + expf took ~130 instructions each on the predictor's
+// epilogue path
+__device__ __forceinline__ float softplus_unit(float x) { return fmaxf(x, 0.f) + __logf(1.0f + __expf(-fabsf(x))); }
 
 // ------------------------------------------------------------------ sampling (neighbor_loader.py:26-50)
 // Node sets are bitmaps over N with a summary level (bit per bitmap word, set by the lane whose atomicOr
@@ -426,7 +430,9 @@ __device__ void mark_body(const Ctx& c, int bid, int nmark, int ahead, uint32_t*
   const int nq = nl * (2 + Kn);
   const int sl = threadIdx.x & 15, grp = (threadIdx.x & 63) >> 4;
   const int gstride = (nmark * 256) >> 4;
-  for (int q = (bid * 256 + (int)threadIdx.x) >> 4; q < nq; q += gstride) {
+  // (the entries are dealt to 256 threads per block; a wider block's other threads only share the LDS bitmaps' clear
+  // and flush — the 8-wave predictor launch that hosts these blocks)
+  for (int q = threadIdx.x < 256 ? (bid * 256 + (int)threadIdx.x) >> 4 : nq; q < nq; q += gstride) {
     int64_t v;
     if (q < nl) {
       v = c.ev_src[start + lo + q];
@@ -2097,7 +2103,7 @@ struct AttnStores {
     }
   }
 };
-template <bool TRAIN>
+template <bool TRAIN, int EB = ATT_EB>
 __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0, int ne, int lane, int jrec = -1,
                                               AttnStores* st = nullptr) {
   const int C = c.C, HC = c.HC;
@@ -2166,10 +2172,10 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
       qo[HC + C + lane] = o1;
     }
   };
-  if (ne > 0 && ne <= ATT_EB) {  // every ring of K <= 16: one load round
-    float k0[ATT_EB], k1[ATT_EB], v0[ATT_EB], v1[ATT_EB];
+  if (ne > 0 && ne <= EB) {  // every ring of K <= 16: one load round
+    float k0[EB], k1[EB], v0[EB], v1[EB];
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       const int e = min(u, ne - 1);
       const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
@@ -2180,14 +2186,17 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
       v1[u] = Pj[2 * HC + C + l0] + eb;
     }
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       if (u >= ne) break;
-      const float p0 = wave_sum_f(q0 * k0[u] * on) / sqc, p1 = wave_sum_f(q1 * k1[u] * on) / sqc;
+      const float p0 = wave_sum_f(q0 * k0[u] * on), p1 = wave_sum_f(q1 * k1[u] * on);
       if (lane == u) { my0 = p0; my1 = p1; }
     }
+    // the scale once per lane (lane e holds edge e's scores): the same quotients as per edge, one division
+    // instead of one (a ~10-instruction dependent sequence) per edge and head
+    if (lane < ne) { my0 /= sqc; my1 /= sqc; }
     softmax();
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       if (u >= ne) break;
       o0 += v0[u] * lane_f(t0, u);
       o1 += v1[u] * lane_f(t1, u);
@@ -2195,10 +2204,10 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
     put_qo();
     return make_float2(o0 + sk0, o1 + sk1);
   }
-  for (int b = 0; b < ne; b += ATT_EB) {
-    float k0[ATT_EB], k1[ATT_EB];
+  for (int b = 0; b < ne; b += EB) {
+    float k0[EB], k1[EB];
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {  // all loads of the batch in flight
+    for (int u = 0; u < EB; ++u) {  // all loads of the batch in flight
       const int e = min(b + u, ne - 1);
       const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
@@ -2206,17 +2215,18 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
       k1[u] = Pj[HC + C + l0] + Ee[C + l0];
     }
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       if (b + u >= ne) break;
-      const float p0 = wave_sum_f(q0 * k0[u] * on) / sqc, p1 = wave_sum_f(q1 * k1[u] * on) / sqc;
+      const float p0 = wave_sum_f(q0 * k0[u] * on), p1 = wave_sum_f(q1 * k1[u] * on);
       if (lane == b + u) { my0 = p0; my1 = p1; }
     }
   }
+  if (lane < ne) { my0 /= sqc; my1 /= sqc; }
   softmax();
-  for (int b = 0; b < ne; b += ATT_EB) {
-    float v0[ATT_EB], v1[ATT_EB];
+  for (int b = 0; b < ne; b += EB) {
+    float v0[EB], v1[EB];
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       const int e = min(b + u, ne - 1);
       const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
@@ -2224,7 +2234,7 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
       v1[u] = Pj[2 * HC + C + l0] + Ee[C + l0];
     }
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       if (b + u >= ne) break;
       o0 += v0[u] * lane_f(t0, b + u);
       o1 += v1[u] * lane_f(t1, b + u);
@@ -2353,29 +2363,41 @@ __global__ void __launch_bounds__(1024) tgn_plan_table_kernel(Ctx c, char* tab, 
 #ifndef TGNX_PRED_DEFER
 #define TGNX_PRED_DEFER 1  // the 1-hop attention's global stores issued after the first barrier (0: inside attn_centre)
 #endif
-#ifndef TGNX_PRED_TAIL2
-#define TGNX_PRED_TAIL2 0  // predictor tail: every wave runs the epilogue, backward by output quarters (1), or the
-                           // wave-0 epilogue + split-k backward (0)
+// diagnostic checkpoint placement (stamps build, wave 0's view): TGNX_PRED_CKPT 0 = after the forward contraction's
+// barrier / after the epilogue; 1 = wave 0 done staging / the first barrier passed; 2 = the backward done / the dZc
+// atomics issued; 3 (with TGNX_STAMP_TID 64) = wave 1's first round landed / its attention done
+#ifndef TGNX_PRED_CKPT
+#define TGNX_PRED_CKPT 0
+#endif
+// waves per workgroup: 1 hop (ATT) 8 — waves 1-3 the roots' attention, waves 0 and 4-7 the weight staging, then
+// all 8 share the contractions (the workgroup is alone on its CU: one wave per SIMD left each dependent step's
+// latency exposed, measured 38 % of the waves' cycles issuing); 2 hops 4
+#ifndef TGNX_PRED_WAVES
+#define TGNX_PRED_WAVES 8  // 1-hop predictor workgroup waves (4: the round-4 layout, one staging wave)
 #endif
 template <bool ATT>
-__global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, PlanOut po, int npl) {
+constexpr int pred_waves() { return ATT ? TGNX_PRED_WAVES : 4; }
+// EB: edges per attention load batch (attn_centre): 10 for rings of K <= 10 (the reference's sampling size), else 16
+template <bool ATT, int EB = ATT_EB>
+__global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, int nmk, int nsrt, PlanOut po, int npl) {
+  constexpr int NW = pred_waves<ATT>();
   TGNX_STAMP(5);
   extern __shared__ __attribute__((aligned(16))) float Wl[];  // [2][D][DP]: lin_src, lin_dst
   __shared__ __attribute__((aligned(16))) float z[3][TDMAX];
-  __shared__ float part[4][3][TDMAX];
-  __shared__ float dh[2][TDMAX];
+  __shared__ float part[NW][3][TDMAX];
+  __shared__ float dhw[NW][2][TDMAX];  // each wave's own copy of dh (no barrier between the epilogue and the backward)
   __shared__ float vsb[TDMAX], vdb[TDMAX], vfw[TDMAX + 1];  // lin_src.bias, lin_dst.bias, lin_final (w | b)
   __shared__ int scr[3];
-  if ((int)blockIdx.x >= (int)gridDim.x - nmk) {  // (the dynamic LDS holds >= 3 x MARK_LDS_WORDS words)
-    mark_body<true>(c, (int)blockIdx.x - ((int)gridDim.x - nmk), nmk, 1, reinterpret_cast<uint32_t*>(Wl));
-    return;
-  }
-  if ((int)blockIdx.x >= (int)gridDim.x - nmk - nsrt) {
-    edge_sort_body(c, reinterpret_cast<int*>(Wl), (int)(tgn_pred_smem(c.D) / 4));
-    return;
-  }
-  if ((int)blockIdx.x >= (int)gridDim.x - nmk - nsrt - npl) {
-    pred_plan_body(c, (int)blockIdx.x - ((int)gridDim.x - nmk - nsrt - npl), po, reinterpret_cast<unsigned char*>(Wl));
+  if ((int)blockIdx.x >= (int)gridDim.x - nmk - nsrt - npl) {  // riding jobs (mark: entries dealt to 256 threads;
+                                                                // sort: 256 threads; plans: any block width)
+    if ((int)blockIdx.x >= (int)gridDim.x - nmk) {  // (the dynamic LDS holds >= 3 x MARK_LDS_WORDS words)
+      mark_body<true>(c, (int)blockIdx.x - ((int)gridDim.x - nmk), nmk, 1, reinterpret_cast<uint32_t*>(Wl));
+    } else if ((int)blockIdx.x >= (int)gridDim.x - nmk - nsrt) {
+      if (threadIdx.x >= 256) return;
+      edge_sort_body(c, reinterpret_cast<int*>(Wl), (int)(tgn_pred_smem(c.D) / 4));
+    } else {
+      pred_plan_body(c, (int)blockIdx.x - ((int)gridDim.x - nmk - nsrt - npl), po, reinterpret_cast<unsigned char*>(Wl));
+    }
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2392,24 +2414,24 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
   const int64_t err = c.ctl[TGNX_CTL_ERR];
   const int i = lo + blockIdx.x;
   const bool live = !(B == 0 || i >= hi || err != 0);
-  constexpr int NST = ATT ? 64 : 192;  // staging threads (ATT: wave 0; 8 waves with 5 staging ones: ±0)
+  constexpr int NST = ATT ? (NW - 3) * 64 : 3 * 64;  // staging threads: ATT waves 0, 4 .. NW-1; else waves 1-3
   // (out_ev: the batch's first event, loaded with the first round — a load after the evs-row stores would wait
   // for all of them, vmcnt retiring in order)
   const int64_t bstart = c.out_ev ? c.ctl[TGNX_CTL_BATCH_START] : 0;
   AttnStores ast;  // ATT, waves 1-3: the attention's alpha / alk / Qo stores, issued after the first barrier
   ast.ne = 0;
   ast.x = -1;
-  if (ATT && wv >= 1) {
+  if (ATT && wv >= 1 && wv <= 3) {
     const int r = wv - 1;
     const int4 q = c.evq[3 * blockIdx.x + r];  // {centre row, P row, edge range}; grid = max_batch: in bounds
     const int jr = c.evj ? c.evj[(3 * blockIdx.x + r) * 16 + (lane & 15)] : -1;  // the edges' neighbour rows
     if (!live) return;
-#if TGNX_PRED_CKPT == 3  // (diagnostic, with TGNX_STAMP_TID 64: wave 1's first round landed / its attention done)
+#if TGNX_PRED_CKPT == 3
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     TGNX_STAMP_AT(0);
 #endif
-    const float2 o = attn_centre<true>(c, q.x, q.y, q.z, q.w - q.z, lane, c.evj && q.w - q.z <= 16 ? max(jr, 0) : -1,
-                                       TGNX_PRED_DEFER ? &ast : nullptr);
+    const float2 o = attn_centre<true, EB>(c, q.x, q.y, q.z, q.w - q.z, lane, c.evj && q.w - q.z <= 16 ? max(jr, 0) : -1,
+                                           TGNX_PRED_DEFER ? &ast : nullptr);
 #if TGNX_PRED_CKPT == 3
     TGNX_STAMP_AT(1);
 #endif
@@ -2430,7 +2452,8 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
     for (int x = lane; x < 3 * D; x += 64) z[x / D][x % D] = c.Zc[(int64_t)cr[x / D] * D + x % D];
     if (lane < 3) scr[lane] = cr[lane];
   } else {
-    const int st = ATT ? tid : tid - 64;  // NST staging threads
+    const int sw = ATT ? (wv == 0 ? 0 : wv - 3) : wv - 1;  // staging wave index
+    const int st = sw * 64 + lane;                        // staging thread index in [0, NST)
     if (blockIdx.x == 0 && st == 0) {
       c.cnt[CNT_LIST] = 3 * (hi - lo);
       {  // this step's Adam scalars for the gradient writers (fused) or tgn_adam (the separate pass after the step)
@@ -2447,17 +2470,20 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
     const float4* S4 = reinterpret_cast<const float4*>(c.params + c.L.lsw);
     const float4* D4 = reinterpret_cast<const float4*>(c.params + c.L.ldw);
     bool staged = false;
+#ifdef TGNX_PRED_DIAG_NOSTAGE  // diagnostic only (wrong results): no weight staging at all
+    staged = true;
+#endif
 #if TGNX_PRED_GLDS
-    if (ATT && flat) {  // the LDS image is the global one: global_load_lds_dwordx4 straight into it, no registers,
-                        // every row in flight at once (then the wave drains them before the barrier)
+    if (ATT && flat && !staged) {  // the LDS image is the global one: global_load_lds_dwordx4 straight into it, no
+                                   // registers, every row in flight at once (the waves drain them before the barrier)
       for (int x0 = 0; x0 < n4; x0 += NST) {
         const int x = x0 + st;
-        if (x < n4) {
+        if (x < n4) {  // (a wave's 64 lanes land at consecutive 16-B slots from its base x0 + 64 sw)
           __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(S4 + x),
-                                           (__attribute__((address_space(3))) void*)(reinterpret_cast<float4*>(Wsrc) + x0),
+                                           (__attribute__((address_space(3))) void*)(reinterpret_cast<float4*>(Wsrc) + x0 + 64 * sw),
                                            16, 0, 0);
           __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(D4 + x),
-                                           (__attribute__((address_space(3))) void*)(reinterpret_cast<float4*>(Wdst) + x0),
+                                           (__attribute__((address_space(3))) void*)(reinterpret_cast<float4*>(Wdst) + x0 + 64 * sw),
                                            16, 0, 0);
         }
       }
@@ -2516,14 +2542,8 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
       }
     }
   }
-// diagnostic checkpoint placement (stamps build, wave 0's view): TGNX_PRED_CKPT 0 = after the forward contraction's
-// barrier / after the epilogue's barrier; 1 = wave 0 done staging / the first barrier passed; 2 = the last barrier
-// passed / the dZc atomics issued
-#ifndef TGNX_PRED_CKPT
-#define TGNX_PRED_CKPT 0
-#endif
-#if TGNX_PRED_CKPT == 1 || defined(TGNX_STAMP_STAGE)  // checkpoint = wave 0 done with its part before the first barrier
-  TGNX_STAMP_AT(TGNX_PRED_CKPT == 1 ? 0 : 1);
+#if TGNX_PRED_CKPT == 1
+  TGNX_STAMP_AT(0);
 #endif
   // LDS-only barriers in this kernel (the weights, embedding rows and partial sums are LDS; the attention's
   // alpha stores and the evs rows need not have landed): __syncthreads would wait for vmcnt(0)
@@ -2534,61 +2554,9 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
 #endif
   if (ATT && TGNX_PRED_DEFER && ast.x >= 0) ast.issue(c, lane);
   const int cr[3] = {scr[0], scr[1], scr[2]};
-  const int kc = (D + 3) / 4, k0 = wv * kc, nk = min(D - k0, kc);
-  if (TGNX_PRED_TAIL2 >= 2 && flat) {
-    // lin_src(z_s), lin_dst(z_p), lin_dst(z_n): wave wv takes float4 columns [q0, q0 + nq) of both output halves at
-    // once; the embedding values come from this wave's slice held one per lane and broadcast through scalar
-    // registers (v_readlane), so the LDS carries only the weight rows (a broadcast ds_read_b128 of z costs the
-    // same LDS cycles as a row read: they were 3 of every 5 reads)
-    const int c4 = D / 4, kq = (c4 + 3) / 4, q0 = wv * kq, nq = max(0, min(c4 - q0, kq));
-    const int kz = min(4 * q0 + lane, D - 1);
-    const float zl0 = z[0][kz], zl1 = z[1][kz], zl2 = z[2][kz];
-    const int oA = min(lane, D - 1), oB = min(lane + 64, D - 1);
-    const float4* wsA = reinterpret_cast<const float4*>(Wsrc + oA * D) + q0;
-    const float4* wdA = reinterpret_cast<const float4*>(Wdst + oA * D) + q0;
-    const float4* wsB = reinterpret_cast<const float4*>(Wsrc + oB * D) + q0;
-    const float4* wdB = reinterpret_cast<const float4*>(Wdst + oB * D) + q0;
-    float a0 = 0.f, b0 = 0.f, c0 = 0.f, a1 = 0.f, b1 = 0.f, c1 = 0.f;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {  // (kq <= 8 for D <= 128): two rounds of <= 4 columns, every row read in flight
-      if (4 * h >= nq) break;
-      float4 u0[4], v0[4], u1[4], v1[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int j = min(4 * h + t, nq - 1);
-        u0[t] = wsA[j];
-        v0[t] = wdA[j];
-        u1[t] = wsB[j];
-        v1[t] = wdB[j];
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int j = 4 * h + t;
-        if (j >= nq) break;
-        const float x00 = lane_f(zl0, 4 * j), x01 = lane_f(zl0, 4 * j + 1), x02 = lane_f(zl0, 4 * j + 2),
-                    x03 = lane_f(zl0, 4 * j + 3);
-        const float x10 = lane_f(zl1, 4 * j), x11 = lane_f(zl1, 4 * j + 1), x12 = lane_f(zl1, 4 * j + 2),
-                    x13 = lane_f(zl1, 4 * j + 3);
-        const float x20 = lane_f(zl2, 4 * j), x21 = lane_f(zl2, 4 * j + 1), x22 = lane_f(zl2, 4 * j + 2),
-                    x23 = lane_f(zl2, 4 * j + 3);
-        a0 += (u0[t].x * x00 + u0[t].y * x01) + (u0[t].z * x02 + u0[t].w * x03);
-        b0 += (v0[t].x * x10 + v0[t].y * x11) + (v0[t].z * x12 + v0[t].w * x13);
-        c0 += (v0[t].x * x20 + v0[t].y * x21) + (v0[t].z * x22 + v0[t].w * x23);
-        a1 += (u1[t].x * x00 + u1[t].y * x01) + (u1[t].z * x02 + u1[t].w * x03);
-        b1 += (v1[t].x * x10 + v1[t].y * x11) + (v1[t].z * x12 + v1[t].w * x13);
-        c1 += (v1[t].x * x20 + v1[t].y * x21) + (v1[t].z * x22 + v1[t].w * x23);
-      }
-    }
-    part[wv][0][lane] = a0;
-    part[wv][1][lane] = b0;
-    part[wv][2][lane] = c0;
-    if (lane + 64 < D) {
-      part[wv][0][lane + 64] = a1;
-      part[wv][1][lane + 64] = b1;
-      part[wv][2][lane + 64] = c1;
-    }
-  } else if (flat) {  // lin_src(z_s), lin_dst(z_p), lin_dst(z_n): wave wv takes float4 columns [q0, q0 + nq)
-    const int c4 = D / 4, kq = (c4 + 3) / 4, q0 = wv * kq, nq = max(0, min(c4 - q0, kq));
+  // lin_src(z_s), lin_dst(z_p), lin_dst(z_n), split over the hidden units' inputs k: NW partial sums per output
+  if (flat) {  // wave wv takes float4 columns [q0, q0 + nq)
+    const int c4 = D / 4, kq = (c4 + NW - 1) / NW, q0 = wv * kq, nq = max(0, min(c4 - q0, kq));
     const float4* z0 = reinterpret_cast<const float4*>(z[0]) + q0;
     const float4* z1 = reinterpret_cast<const float4*>(z[1]) + q0;
     const float4* z2 = reinterpret_cast<const float4*>(z[2]) + q0;
@@ -2612,8 +2580,9 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
       }
     }
   } else {
+    const int kc = (D + NW - 1) / NW, k0 = wv * kc, nk = max(0, min(D - k0, kc));
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {  // lin_src(z_s), lin_dst(z_p), lin_dst(z_n): split contraction
+    for (int q = 0; q < 2; ++q) {
       const int o = lane + 64 * q;
       if (o < D) {
         float a = 0.f, b = 0.f, d2 = 0.f;
@@ -2635,27 +2604,30 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
   TGNX_STAMP_AT(0);
 #endif
   float* ev = c.evs + (int64_t)i * evs_stride(D);
-#if TGNX_PRED_TAIL2
-  // every wave runs the forward epilogue (the same values in each: no dh round through a barrier); then wave wv
-  // computes the input gradients of its quarter of the outputs over the whole hidden width (lanes: 2 halves of the
-  // hidden units x the quarter's outputs, dh from this wave's own LDS copy) and issues their dZc atomics; wave 0
-  // stores the event's row, outputs and loss term last (off the chain to the atomics)
-#if TGNX_PRED_TAIL2 < 2
-  __shared__ float dhw[4][2][TDMAX];
-#endif
+  // every wave runs the forward epilogue (the same values in each: no dh round through a barrier) and keeps its own
+  // copy of dh; wave 0 stores the event's row, outputs and loss term (they drain during the backward)
   float hp[2], hn[2], dhp[2], dhn[2];
   float ap, an, sp, sn, dap, dan;
   const float invB = 1.0f / (float)B;
   {
+    auto psum = [&](int r, int o) {
+      float s = 0.f;
+      if (NW == 8)
+        s = ((part[0][r][o] + part[1][r][o]) + (part[2][r][o] + part[3][r][o])) +
+            ((part[4][r][o] + part[5][r][o]) + (part[6][r][o] + part[7][r][o]));
+      else
+        s = (part[0][r][o] + part[1][r][o]) + (part[2][r][o] + part[3][r][o]);
+      return s;
+    };
     float zp = 0.f, zn = 0.f;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int o = lane + 64 * q;
       hp[q] = hn[q] = 0.f;
       if (o < D) {
-        const float s = ((part[0][0][o] + part[1][0][o]) + (part[2][0][o] + part[3][0][o])) + vsb[o];
-        const float dp = ((part[0][1][o] + part[1][1][o]) + (part[2][1][o] + part[3][1][o])) + vdb[o];
-        const float dn = ((part[0][2][o] + part[1][2][o]) + (part[2][2][o] + part[3][2][o])) + vdb[o];
+        const float s = psum(0, o) + vsb[o];
+        const float dp = psum(1, o) + vdb[o];
+        const float dn = psum(2, o) + vdb[o];
         hp[q] = fmaxf(s + dp, 0.f);
         hn[q] = fmaxf(s + dn, 0.f);
         zp += vfw[o] * hp[q];
@@ -2674,95 +2646,12 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
       const float wf = o < D ? vfw[o] : 0.f;
       dhp[q] = hp[q] > 0.f ? dap * wf : 0.f;
       dhn[q] = hn[q] > 0.f ? dan * wf : 0.f;
-#if TGNX_PRED_TAIL2 < 2
       if (o < D) {
         dhw[wv][0][o] = dhp[q];
         dhw[wv][1][o] = dhn[q];
       }
-#endif
     }
   }
-#if TGNX_PRED_CKPT == 0
-  TGNX_STAMP_AT(1);
-#endif
-#if TGNX_PRED_TAIL2 >= 2
-  {
-    // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn: wave wv takes the hidden units [kb, kb + nkb),
-    // lanes over the outputs o = lane, lane + 64 (conflict-free row reads), dh[kk] broadcast from the lane that
-    // holds it (v_readlane); the four partial sums meet in LDS behind one barrier
-    __shared__ float pb[4][3][TDMAX];  // (not part: a slower wave may still read part in its epilogue)
-    const int kcb = (D + 3) / 4, kb = wv * kcb, nkb = max(0, min(D - kb, kcb));
-    const int oA = min(lane, D - 1), oB = min(lane + 64, D - 1);
-    float a0 = 0.f, b0 = 0.f, c0 = 0.f, a1 = 0.f, b1 = 0.f, c1 = 0.f;
-#pragma unroll 5
-    for (int t = 0; t < nkb; ++t) {
-      const int kk = kb + t;
-      const float h0 = kk < 64 ? lane_f(dhp[0], kk) : lane_f(dhp[1], kk - 64);
-      const float h1 = kk < 64 ? lane_f(dhn[0], kk) : lane_f(dhn[1], kk - 64);
-      const float* rs = Wsrc + kk * DP;
-      const float* rd = Wdst + kk * DP;
-      const float sA = rs[oA], dA = rd[oA], sB = rs[oB], dB = rd[oB];
-      a0 += sA * (h0 + h1);
-      b0 += dA * h0;
-      c0 += dA * h1;
-      a1 += sB * (h0 + h1);
-      b1 += dB * h0;
-      c1 += dB * h1;
-    }
-    pb[wv][0][lane] = a0;
-    pb[wv][1][lane] = b0;
-    pb[wv][2][lane] = c0;
-    if (lane + 64 < D) {
-      pb[wv][0][lane + 64] = a1;
-      pb[wv][1][lane + 64] = b1;
-      pb[wv][2][lane + 64] = c1;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#if TGNX_PRED_CKPT == 2
-    TGNX_STAMP_AT(0);
-#endif
-    for (int x = tid; x < 3 * D; x += blockDim.x) {
-      const int r = x >= 2 * D ? 2 : x >= D ? 1 : 0, o = x - r * D;
-      const float g = (pb[0][r][o] + pb[1][r][o]) + (pb[2][r][o] + pb[3][r][o]);
-      atomicAdd(&c.dZc[(int64_t)cr[r] * D + o], g);
-    }
-#if TGNX_PRED_CKPT == 2
-    TGNX_STAMP_AT(1);
-#endif
-  }
-#else
-  {
-    // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn for outputs o of this wave's quarter
-    const int ow = (D + 3) / 4, ol = lane & 31, kh = lane >> 5, o = wv * ow + ol, hw = D / 2;  // (D even, ow <= 32)
-    const bool oko = ol < ow && o < D;
-    const int oc = oko ? o : 0, kb = kh * hw;
-    float a = 0.f, b = 0.f, d2 = 0.f;
-#pragma unroll 5
-    for (int j = 0; j < hw; ++j) {
-      const int kk = kb + j;
-      const float h0 = dhw[wv][0][kk], h1 = dhw[wv][1][kk];
-      const float w1 = Wsrc[kk * DP + oc], w2 = Wdst[kk * DP + oc];
-      a += w1 * (h0 + h1);
-      b += w2 * h0;
-      d2 += w2 * h1;
-    }
-    a = swap32_sum(a);
-    b = swap32_sum(b);
-    d2 = swap32_sum(d2);
-#if TGNX_PRED_CKPT == 2
-    TGNX_STAMP_AT(0);
-#endif
-    if (kh == 0 && oko) {
-      atomicAdd(&c.dZc[(int64_t)cr[0] * D + o], a);
-      atomicAdd(&c.dZc[(int64_t)cr[1] * D + o], b);
-      atomicAdd(&c.dZc[(int64_t)cr[2] * D + o], d2);
-    }
-#if TGNX_PRED_CKPT == 2
-    TGNX_STAMP_AT(1);
-#endif
-  }
-#endif
   if (wv == 0) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -2780,7 +2669,7 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
     if (lane == 0) {
       float* s = ev + 7 * D;
       s[0] = ap; s[1] = an; s[2] = sp; s[3] = sn; s[4] = dap; s[5] = dan;
-      s[6] = (softplusf(-sp) + softplusf(sn)) * invB;
+      s[6] = (softplus_unit(-sp) + softplus_unit(sn)) * invB;
       c.out_pos[i] = sp;
       c.out_neg[i] = sn;
       if (c.out_ev) {
@@ -2790,99 +2679,48 @@ __global__ void __launch_bounds__(256) tgn_pred_train(Ctx c, int nmk, int nsrt, 
       }
     }
   }
-#else
-  if (wv == 0) {
-    float hp[2], hn[2], zp = 0.f, zn = 0.f;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int o = lane + 64 * q;
-      hp[q] = hn[q] = 0.f;
-      if (o < D) {
-        const float s = ((part[0][0][o] + part[1][0][o]) + (part[2][0][o] + part[3][0][o])) + vsb[o];
-        const float dp = ((part[0][1][o] + part[1][1][o]) + (part[2][1][o] + part[3][1][o])) + vdb[o];
-        const float dn = ((part[0][2][o] + part[1][2][o]) + (part[2][2][o] + part[3][2][o])) + vdb[o];
-        hp[q] = fmaxf(s + dp, 0.f);
-        hn[q] = fmaxf(s + dn, 0.f);
-        zp += vfw[o] * hp[q];
-        zn += vfw[o] * hn[q];
-      }
-    }
-    const float ap = wave_sum_f(zp) + vfw[D], an = wave_sum_f(zn) + vfw[D];
-    const float sp = sigm(ap), sn = sigm(an);
-    const float invB = 1.0f / (float)B;
-    const float dap = (sigm(sp) - 1.0f) * sp * (1.0f - sp) * invB;
-    const float dan = sigm(sn) * sn * (1.0f - sn) * invB;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int o = lane + 64 * q;
-      if (o < D) {
-        const float wf = vfw[o];
-        const float dhp = hp[q] > 0.f ? dap * wf : 0.f;
-        const float dhn = hn[q] > 0.f ? dan * wf : 0.f;
-        dh[0][o] = dhp;
-        dh[1][o] = dhn;
-        ev[o] = z[0][o];
-        ev[D + o] = z[1][o];
-        ev[2 * D + o] = z[2][o];
-        ev[3 * D + o] = dhp;
-        ev[4 * D + o] = dhn;
-        ev[5 * D + o] = hp[q];
-        ev[6 * D + o] = hn[q];
-      }
-    }
-    if (lane == 0) {
-      float* s = ev + 7 * D;
-      s[0] = ap; s[1] = an; s[2] = sp; s[3] = sn; s[4] = dap; s[5] = dan;
-      s[6] = (softplusf(-sp) + softplusf(sn)) * invB;
-      c.out_pos[i] = sp;
-      c.out_neg[i] = sn;
-      if (c.out_ev) {
-        const int64_t e = bstart + i;
-        c.out_ev[2 * e] = sp;
-        c.out_ev[2 * e + 1] = sn;
-      }
-    }
-  }
-  // barrier for dh (LDS) only: the evs-row stores of wave 0 stay in flight (__syncthreads waits vmcnt(0))
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-#if TGNX_PRED_CKPT == 0 && !defined(TGNX_STAMP_STAGE)
+#if TGNX_PRED_CKPT == 0
   TGNX_STAMP_AT(1);
 #endif
-  // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn (split over k, lanes over o)
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int o = lane + 64 * q;
-    if (o < D) {
-      float a = 0.f, b = 0.f, d2 = 0.f;
+  {
+    // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn for the outputs [wv ow, wv ow + ow) of this
+    // wave: lanes = KG groups of the hidden units x OL outputs, dh from this wave's own LDS copy, the groups summed
+    // across lanes, then the wave's dZc atomics
+    constexpr int OL = NW == 8 ? 16 : 32, KG = 64 / OL;
+    const int ow = (D + NW - 1) / NW, ol = lane % OL, kg = lane / OL, o = wv * ow + ol, hw = (D + KG - 1) / KG;
+    const bool oko = ol < ow && o < D;  // (ow <= OL: D <= 128)
+    const int oc = oko ? o : 0, kb = kg * hw;
+    float a = 0.f, b = 0.f, d2 = 0.f;
 #pragma unroll 5
-      for (int k = 0; k < nk; ++k) {
-        const int kk = k0 + k;
-        a += Wsrc[kk * DP + o] * (dh[0][kk] + dh[1][kk]);
-        b += Wdst[kk * DP + o] * dh[0][kk];
-        d2 += Wdst[kk * DP + o] * dh[1][kk];
-      }
-      part[wv][0][o] = a;
-      part[wv][1][o] = b;
-      part[wv][2][o] = d2;
+    for (int j = 0; j < hw; ++j) {
+      const int kk = min(kb + j, D - 1);
+      const float live_k = f01(kb + j < D);
+      const float h0 = dhw[wv][0][kk] * live_k, h1 = dhw[wv][1][kk] * live_k;
+      const float w1 = Wsrc[kk * DP + oc], w2 = Wdst[kk * DP + oc];
+      a += w1 * (h0 + h1);
+      b += w2 * h0;
+      d2 += w2 * h1;
     }
+    if (KG == 4) {
+      a = swap16_sum(a);
+      b = swap16_sum(b);
+      d2 = swap16_sum(d2);
+    }
+    a = swap32_sum(a);
+    b = swap32_sum(b);
+    d2 = swap32_sum(d2);
+#if TGNX_PRED_CKPT == 2
+    TGNX_STAMP_AT(0);
+#endif
+    if (kg == 0 && oko) {
+      atomicAdd(&c.dZc[(int64_t)cr[0] * D + o], a);
+      atomicAdd(&c.dZc[(int64_t)cr[1] * D + o], b);
+      atomicAdd(&c.dZc[(int64_t)cr[2] * D + o], d2);
+    }
+#if TGNX_PRED_CKPT == 2
+    TGNX_STAMP_AT(1);
+#endif
   }
-  // LDS-only barrier again: the evs-row and alpha stores stay in flight
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-#if TGNX_PRED_CKPT == 2
-  TGNX_STAMP_AT(0);
-#endif
-#pragma unroll
-  for (int r = 0; r < 3; ++r)
-    for (int o = tid; o < D; o += blockDim.x) {
-      const float g = (part[0][r][o] + part[1][r][o]) + (part[2][r][o] + part[3][r][o]);
-      atomicAdd(&c.dZc[(int64_t)cr[r] * D + o], g);
-    }
-#if TGNX_PRED_CKPT == 2
-  TGNX_STAMP_AT(1);
-#endif
-#endif
 }
 
 // predictor bias / output-layer / loss reductions over this rank's events (wave per output)
@@ -3126,6 +2964,7 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
 // serialised at the L2 (attn_bwd 36 us, 15 us without them).
 // nwalk (parity-set steps with a plan table, TGNX_WALK_AT 1): the last block walks the NEXT batch's node sets
 // into the other parity's set (cw; the plans come from the table), instead of a workgroup of the dW_cell launch
+template <int EB>
 __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int nwalk, Ctx cw) {
   TGNX_STAMP(6);
   if ((int)blockIdx.x >= (int)gridDim.x - nwalk) {
@@ -3183,10 +3022,10 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
     k0v = att_keep(c, seed, x, e0 + lane, 0);
     k1v = att_keep(c, seed, x, e0 + lane, 1);
   }
-  if (ne > 0 && ne <= ATT_EB) {  // every ring of K <= 16: v, k and edge rows of all edges in one round
-    float kk0[ATT_EB], kk1[ATT_EB], v0[ATT_EB], v1[ATT_EB];
+  if (ne > 0 && ne <= EB) {  // every ring of K <= 16: v, k and edge rows of all edges in one round
+    float kk0[EB], kk1[EB], v0[EB], v1[EB];
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       const int e = min(u, ne - 1);
       const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
@@ -3198,7 +3037,7 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
     }
     float da0 = 0.f, da1 = 0.f;
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       if (u >= ne) break;
       const float p0 = wave_sum_f(g0 * v0[u]), p1 = wave_sum_f(g1 * v1[u]);
       if (lane == u) { da0 = p0 * k0v; da1 = p1 * k1v; }
@@ -3206,11 +3045,12 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
     const float s0 = wave_sum_f(a0 * da0), s1 = wave_sum_f(a1 * da1);
     const float ds0 = a0 * (da0 - s0), ds1 = a1 * (da1 - s1);
     const float t0 = a0 * k0v, t1 = a1 * k1v;
+    const float dq0s = ds0 / sqc, dq1s = ds1 / sqc;  // (per lane = per edge: one division, not one per edge)
     float dq0 = 0.f, dq1 = 0.f;
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       if (u >= ne) break;
-      const float d0 = lane_f(ds0, u) / sqc, d1 = lane_f(ds1, u) / sqc;
+      const float d0 = lane_f(dq0s, u), d1 = lane_f(dq1s, u);
       const float b0 = lane_f(t0, u), b1 = lane_f(t1, u);
       float* dEe = c.dE + (int64_t)(e0 + u) * HC;
       float* dKe = c.dKV + (int64_t)(e0 + u) * 2 * HC;  // [dk (HC) | dv (HC)]
@@ -3237,10 +3077,10 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
   }
   // d alpha~_eh = Σ_{ch in h} dout (v_j + e); d alpha = d alpha~ * keep
   float da0 = 0.f, da1 = 0.f;
-  for (int b = 0; b < ne; b += ATT_EB) {
-    float v0[ATT_EB], v1[ATT_EB];
+  for (int b = 0; b < ne; b += EB) {
+    float v0[EB], v1[EB];
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       const int e = min(b + u, ne - 1);
       const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
@@ -3248,7 +3088,7 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
       v1[u] = Pj[2 * HC + C + l0] + Ee[C + l0];
     }
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       if (b + u >= ne) break;
       const float p0 = wave_sum_f(g0 * v0[u]), p1 = wave_sum_f(g1 * v1[u]);
       if (lane == b + u) { da0 = p0 * k0v; da1 = p1 * k1v; }
@@ -3258,11 +3098,12 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
   const float s0 = wave_sum_f(a0 * da0), s1 = wave_sum_f(a1 * da1);
   const float ds0 = a0 * (da0 - s0), ds1 = a1 * (da1 - s1);
   const float t0 = a0 * k0v, t1 = a1 * k1v;
+  const float dq0s = ds0 / sqc, dq1s = ds1 / sqc;
   float dq0 = 0.f, dq1 = 0.f;
-  for (int b = 0; b < ne; b += ATT_EB) {
-    float kk0[ATT_EB], kk1[ATT_EB];
+  for (int b = 0; b < ne; b += EB) {
+    float kk0[EB], kk1[EB];
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       const int e = min(b + u, ne - 1);
       const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
       const float* Ee = c.Ep + (int64_t)(e0 + e) * HC;
@@ -3270,10 +3111,10 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
       kk1[u] = Pj[HC + C + l0] + Ee[C + l0];
     }
 #pragma unroll
-    for (int u = 0; u < ATT_EB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       const int e = b + u;
       if (e >= ne) break;
-      const float d0 = lane_f(ds0, e) / sqc, d1 = lane_f(ds1, e) / sqc;
+      const float d0 = lane_f(dq0s, e), d1 = lane_f(dq1s, e);
       const float b0 = lane_f(t0, e), b1 = lane_f(t1, e);
       float* dEe = c.dE + (int64_t)(e0 + e) * HC;
       float* dKe = c.dKV + (int64_t)(e0 + e) * 2 * HC;  // [dk (HC) | dv (HC)]
@@ -4832,6 +4673,7 @@ size_t tgnx_tgn_plan_table_bytes(const tgnx_tgn_config* cfg, int64_t split_lo, i
 // what each plan table was built for (tgnx_tgn_plan_table), keyed by its device address: the resident parity-set
 // steps index slot (batch start - split_lo) / batch with a stride sized by max_batch, so a table built for another
 // split, batch or max_batch would silently hand them another batch's plans or read past the table
+extern "C++" {  // (inside the C-ABI block)
 namespace {
 struct PlanTableKey {
   int64_t lo, hi, batch, stride;
@@ -4843,6 +4685,7 @@ std::unordered_map<const void*, PlanTableKey>& ptab_registry() {
   return m;
 }
 }  // namespace
+}  // extern "C++"
 
 int tgnx_tgn_plan_table(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo, int64_t split_hi,
                         int64_t batch, void* table, size_t table_bytes, void* stream) {
@@ -4889,7 +4732,8 @@ static bool pred_smem_ok(int D) {
     return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tgn_pred_smem(TDMAX)) == hipSuccess;
   };
   static const bool ok = set(reinterpret_cast<const void*>(&tgn_pred_train<false>)) &&
-                         set(reinterpret_cast<const void*>(&tgn_pred_train<true>));
+                         set(reinterpret_cast<const void*>(&tgn_pred_train<true, 10>)) &&
+                         set(reinterpret_cast<const void*>(&tgn_pred_train<true, ATT_EB>));
   return ok && tgn_pred_smem(D) <= tgn_pred_smem(TDMAX);
 }
 
@@ -5134,9 +4978,11 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const int nsrt = (two ? cr.kvs : kvs) ? 1 : 0;  // (kvs: the rows fit the sort's LDS counters)
   const PlanOut po = plan_out(ppm ? cn : c);
   if (att_in_pred)
-    launch_k(tgn_pred_train<true>, dim3(kr.B + npl + nsrt + nmk), dim3(256), (uint32_t)psm, s, cr, nmk, nsrt, po, npl);
+    launch_k(c.K <= 10 ? tgn_pred_train<true, 10> : tgn_pred_train<true, ATT_EB>, dim3(kr.B + npl + nsrt + nmk),
+             dim3(64 * pred_waves<true>()), (uint32_t)psm, s, cr, nmk, nsrt, po, npl);
   else
-    launch_k(tgn_pred_train<false>, dim3(kr.B + npl + nsrt + nmk), dim3(256), (uint32_t)psm, s, cr, nmk, nsrt, po, npl);
+    launch_k(tgn_pred_train<false>, dim3(kr.B + npl + nsrt + nmk), dim3(64 * pred_waves<false>()), (uint32_t)psm, s, cr,
+             nmk, nsrt, po, npl);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
   if (c.emb) {
@@ -5152,7 +4998,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     // conv2 backward (‖ predictor reductions) -> dP2, dE2; then dh1 = dP2 [Wq2; Wk2; Wv2; Wsk2] ‖ dW_proj2,
     // dW_edge2 (deferred) ‖ conv2's lin_edge -> Δt-encoding partials; then conv backward from dh1
     const int ncb1 = gridn(kr.R1tr, 4, 1 << 20), nkv1 = cr.kvf ? gridn(kr.E1tr, KVE_CH, 1 << 20) : 0;
-    tgn_attn_bwd<<<ncb1 + nkv1 + gridn(3 * D + 2, 4), 256, 0, s>>>(cr, ncb1, nkv1, 0, cr);
+    launch_k(c.K <= 10 ? tgn_attn_bwd<10> : tgn_attn_bwd<ATT_EB>, dim3(ncb1 + nkv1 + gridn(3 * D + 2, 4)), dim3(256), 0u,
+             s, cr, ncb1, nkv1, 0, cr);
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
     // conv2's (dk, dv) sums (unless its attention backward summed them) ‖ its dE2-only GEMMs (as in the 1-hop
     // step below), then dh1 ‖ dW_proj2 (with the root-level fusion the dE2 GEMMs ride in that launch instead)
@@ -5177,12 +5024,13 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     }
     TGNX_LAUNCH_CHECK("tgn_dh1");
     const int ncb = gridn(kr.Rtr, 4, 1 << 20), nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
-    launch_k(tgn_attn_bwd, dim3(ncb + nkv + nwalk), dim3(256), walk_lds, s, c, ncb, nkv, nwalk, nwalk ? cn : c);
+    launch_k(c.K <= 10 ? tgn_attn_bwd<10> : tgn_attn_bwd<ATT_EB>, dim3(ncb + nkv + nwalk), dim3(256), walk_lds, s, c,
+             ncb, nkv, nwalk, nwalk ? cn : c);
   } else {
     const int ncb = gridn(kr.Rtr, 4, 1 << 20);
     const int nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
-    launch_k(tgn_attn_bwd, dim3(ncb + nkv + gridn(3 * D + 2, 4) + nwalk), dim3(256), walk_lds, s, c, ncb, nkv, nwalk,
-             nwalk ? cn : c);
+    launch_k(c.K <= 10 ? tgn_attn_bwd<10> : tgn_attn_bwd<ATT_EB>, dim3(ncb + nkv + gridn(3 * D + 2, 4) + nwalk),
+             dim3(256), walk_lds, s, c, ncb, nkv, nwalk, nwalk ? cn : c);
   }
   probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgn_attn_bwd");

@@ -269,6 +269,30 @@ def _p(t):
     return 0 if t is None else t.data_ptr()
 
 
+EXCHANGE_MODES = ("fused", "split")
+
+
+def exchange_collectives(comm, G: int, rank: int, world: int, mode: str = "fused", async_op: bool = False):
+    """The data-parallel step's exchange over comm = [G gradient floats | world row slots] (each rank's kernels
+    wrote its own slot):
+      fused — ONE all-reduce of the whole buffer: the gradient sum, and (the other slots holding zeros) the
+              all-gather of the rows, bit-exact (TgnEngine.__init__);
+      split — an all-reduce of the G gradient floats and an in-place all_gather_into_tensor of the row slots:
+              two collectives, but the rows travel once instead of as W-times-padded zeros in a sum.
+    Returns the work handles (async_op) or []."""
+    import torch.distributed as dist
+    if mode == "split":
+        rows = comm[G:]
+        n = rows.numel() // world
+        w1 = dist.all_reduce(comm[:G], async_op=async_op)
+        w2 = dist.all_gather_into_tensor(rows, rows[rank * n:(rank + 1) * n], async_op=async_op)
+        return [w for w in (w1, w2) if w is not None]
+    if mode != "fused":
+        raise ValueError(f"exchange mode must be one of {EXCHANGE_MODES}, got {mode!r}")
+    w = dist.all_reduce(comm, async_op=async_op)
+    return [] if w is None else [w]
+
+
 class TgnEngine:
     """Owns the workspace of one TGN model + one neighbour ring over a resident event table
     (src, dst, t, msg rows = e_id).
@@ -353,6 +377,11 @@ class TgnEngine:
         # the exchange collective: torch.distributed.all_reduce over the default group, unless a callable
         # (comm, async_op) -> work | None is set here (tools/dp_compute.py: a stand-in without a collective)
         self.exchange = None
+        # fused: one all-reduce of [gradients | row slots]; split: gradient all-reduce + row all-gather
+        # (exchange_collectives; TGNX_EXCHANGE, for the first 8-GPU A/B of the two)
+        self.exchange_mode = os.environ.get("TGNX_EXCHANGE", "fused")
+        if self.exchange_mode not in EXCHANGE_MODES:
+            raise ValueError(f"TGNX_EXCHANGE must be one of {EXCHANGE_MODES}, got {self.exchange_mode!r}")
         if self.world > 1:
             self.xcap = min(cfg.num_nodes, 2 * (-(-cfg.max_batch // self.world)))
             rw = cfg.mem_dim + 4
@@ -464,8 +493,7 @@ class TgnEngine:
         if self.exchange is not None:
             self.exchange(self.comm, False)
             return
-        import torch.distributed as dist
-        dist.all_reduce(self.comm)
+        exchange_collectives(self.comm, self.model.grad_flat.numel(), self.rank, self.world, self.exchange_mode)
 
     def _apply_rows(self, b):
         _lib.call("tgnx_tgn_apply_rows", ctypes.byref(self.cfg), ctypes.byref(b), _p(self.xgather),
@@ -587,13 +615,14 @@ class TgnEngine:
         if self.world > 1:
             if self.exchange is not None:
                 work = self.exchange(self.comm, True)
+                works = [] if work is None else [work]
             else:
-                import torch.distributed as dist
-                work = dist.all_reduce(self.comm, async_op=True)
+                works = exchange_collectives(self.comm, self.model.grad_flat.numel(), self.rank, self.world,
+                                             self.exchange_mode, async_op=True)
             if between is not None:
                 between()
-            if work is not None:
-                work.wait()
+            for w in works:
+                w.wait()
         elif between is not None:
             between()
 

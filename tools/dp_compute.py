@@ -18,14 +18,14 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
-def run(W, B, steps, warmup, dataset, layers):
+def run(W, B, steps, warmup, dataset, layers, global_batch=0):
     from tgnx.sampler import LastNeighborLoader
     from tgnx.synth import SHAPES, make_stream
     from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
     shape = SHAPES[dataset]
     s = make_stream(shape, seed=0)
     dev = torch.device("cuda")
-    Bg = B * W
+    Bg = global_batch if global_batch else B * W
     model = TGNModel(shape.num_nodes, s.num_events, shape.msg_dim, 100, dev, ring=10, max_batch=Bg, max_neg=1,
                      dropout=0.1, layers=layers, generator=torch.Generator().manual_seed(0))
     eng = TgnEngine(model, LastNeighborLoader(shape.num_nodes, 10, device=dev),
@@ -54,8 +54,18 @@ def run(W, B, steps, warmup, dataset, layers):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / steps * 1e3
     eng.check()
-    return {"world": W, "global_batch": Bg, "ms_per_step": round(ms, 4),
-            "comm_floats": 0 if eng.comm is None else int(eng.comm.numel())}
+    out = {"world": W, "global_batch": Bg, "events_per_rank": -(-Bg // W), "ms_per_step": round(ms, 4),
+           "comm_floats": 0 if eng.comm is None else int(eng.comm.numel())}
+    if eng.comm is not None:   # the exchange payload: gradients (+ loss slot) and W row slots of xcap rows
+        G = model.grad_flat.numel()
+        rows = eng.comm.numel() - G
+        out.update(grad_floats=G, row_slot_floats=rows, row_slots_per_rank=eng.xcap, row_floats=model.D + 4,
+                   fused_allreduce_bytes=4 * eng.comm.numel(),
+                   split_bytes={"grad_allreduce": 4 * G, "row_allgather_out": 4 * rows,
+                                "row_allgather_in_per_rank": 4 * rows // W},
+                   ring_send_bytes_per_rank={"fused": round(2 * (W - 1) / W * 4 * eng.comm.numel()),
+                                             "split": round(2 * (W - 1) / W * 4 * G + (W - 1) / W * 4 * rows)})
+    return out
 
 
 def main():
@@ -66,9 +76,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--dataset", default="tgbl-wiki")
     ap.add_argument("--layers", type=int, default=1)
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="events per step over all ranks (strong scaling: BASELINE #4 coin 800 at W 4, #5 comment 600 at W 8)")
     a = ap.parse_args()
-    out = [run(W, a.batch, a.steps, a.warmup, a.dataset, a.layers) for W in a.worlds]
-    print(json.dumps({"dp_compute_only": out, "note": "rank 0 of a W-rank step on one device, exchange skipped"}))
+    out = [run(W, a.batch, a.steps, a.warmup, a.dataset, a.layers, a.global_batch) for W in a.worlds]
+    print(json.dumps({"dp_compute_only": out, "dataset": a.dataset, "layers": a.layers,
+                      "note": "rank 0 of a W-rank step on one device, exchange skipped; ring_send_bytes_per_rank = "
+                              "the bytes a ring collective sends per rank for the fused all-reduce vs the split "
+                              "gradient all-reduce + row all-gather"}))
 
 
 if __name__ == "__main__":
