@@ -139,6 +139,11 @@ __device__ __forceinline__ float swap32_sum(float v) {  // v + v[lane ^ 32]
 }
 #ifdef TGNX_NO_DPP  // A/B: the ds_bpermute forms
 __device__ __forceinline__ float wave_sum_f(float v) { return wave_sum(v); }
+__device__ __forceinline__ float half_sum_f(float v) {  // sum over each 32-lane half
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
 __device__ __forceinline__ float wave_max_f(float v) { return wave_max(v); }
 __device__ __forceinline__ float lane_f(float v, int l) { return __shfl(v, l, WAVE); }
 __device__ __forceinline__ int lane_i(int v, int l) { return __shfl(v, l, WAVE); }
@@ -156,6 +161,14 @@ __device__ __forceinline__ float wave_sum_f(float v) {
   v += dpp_f<0x141>(v);  // row_half_mirror: the other quad of the 8-lane half-row (quads are uniform)
   v += dpp_f<0x140>(v);  // row_mirror: the other half of the 16-lane row
   return swap32_sum(swap16_sum(v));
+}
+// sum over each 32-lane half (lanes 0-31 and 32-63 get their own half's sum)
+__device__ __forceinline__ float half_sum_f(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  return swap16_sum(v);
 }
 __device__ __forceinline__ float wave_max_f(float v) {
   v = fmaxf(v, dpp_f<0xB1>(v));

@@ -241,6 +241,12 @@ struct Ctx {
   float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
   float* Hp;  // TGNX_DENSE_H (GRU train step): row m's pre-update memory mem[nid[m]] [M][D], written by the GRU forward
   float *dZc, *dP, *dE, *dG, *tgp;
+  // 1-hop train: the predictor accumulates the centres' output gradient into dzrep copies of dZc (dzstride floats
+  // apart; workgroup b adds into copy b % dzrep), which the attention backward sums: a hub centre's row takes the
+  // float atomics of ~40 % of the batch's workgroups (one row: ~14x slower, MI355X_MICROARCH.md 'Global float
+  // atomics'); 2 hops: 1
+  int dzrep;
+  int64_t dzstride;
   // resident batch cursor folded into tgn_mark (tgnx_tgn_train_step_resident): mark derives the batch
   // descriptor from the step counters, the step's last launch advances them
   int adv = 0;
@@ -1323,7 +1329,7 @@ __device__ void agg_node(const Ctx& c, int64_t n, int m, int lane, bool grad) {
           }
 #pragma unroll
           for (int u = 0; u < AGG_MB; ++u) {
-            if (qb + u >= nq) break;
+            if (qb + u >= nq) continue;  // (not break: it kept the loop rolled)
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
               const int k = k0 + lane + 64 * i;
@@ -1423,7 +1429,7 @@ __device__ void agg_node_mean_wg(const Ctx& c, int64_t n, int m, bool grad) {
         }
 #pragma unroll
         for (int u = 0; u < AGG_MB; ++u) {
-          if (qb + u >= nq) break;
+          if (qb + u >= nq) continue;  // (not break: it kept the loop rolled)
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const int k = k0 + lane + 64 * i;
@@ -1544,7 +1550,7 @@ __device__ void agg_node_mean_cols(const Ctx& c, int64_t n, int m, bool grad) {
       }
 #pragma unroll
       for (int u = 0; u < MC; ++u) {
-        if (qb + u >= nq) break;
+        if (qb + u >= nq) continue;  // (not break: it kept the loop rolled)
         const float dt = lane_f(t_l, qb + u) - lun;
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
@@ -1773,8 +1779,9 @@ __global__ void __launch_bounds__(256) TGNX_AGG_ATTR tgn_agg_emit(Ctx c, int mod
       for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R1 * c.HC; x += (int64_t)nb * blockDim.x)
         c.dZr[x] = 0.f;
     } else {
-      for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R * c.HC; x += (int64_t)nb * blockDim.x)
-        c.dZc[x] = 0.f;
+      for (int rp = 0; rp < c.dzrep; ++rp)
+        for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R * c.HC; x += (int64_t)nb * blockDim.x)
+          c.dZc[rp * c.dzstride + x] = 0.f;
     }
   }
   const int n = mode == 0 ? c.cnt[CNT_M] : (list_cnt ? *list_cnt : n_host);
@@ -2103,9 +2110,9 @@ struct AttnStores {
     }
   }
 };
-template <bool TRAIN, int EB = ATT_EB>
+template <bool TRAIN, int EB = ATT_EB, class CK = NoCheckpoint>
 __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0, int ne, int lane, int jrec = -1,
-                                              AttnStores* st = nullptr) {
+                                              AttnStores* st = nullptr, CK ck = CK{}) {
   const int C = c.C, HC = c.HC;
   const float on = f01(lane < C);
   const int l0 = min(lane, C - 1);
@@ -2185,19 +2192,26 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
       v0[u] = Pj[2 * HC + l0] + ea;
       v1[u] = Pj[2 * HC + C + l0] + eb;
     }
+#ifdef TGNX_ATT_CK  // diagnostic: the edge rows landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ck(0);
+#endif
+    // (no early exit: a runtime `break` kept these loops rolled — indexed register reads, one edge's reduction
+    // after another; the clamped rows of edges >= ne are reduced and discarded)
 #pragma unroll
     for (int u = 0; u < EB; ++u) {
-      if (u >= ne) break;
       const float p0 = wave_sum_f(q0 * k0[u] * on), p1 = wave_sum_f(q1 * k1[u] * on);
-      if (lane == u) { my0 = p0; my1 = p1; }
+      if (lane == u && u < ne) { my0 = p0; my1 = p1; }
     }
+#ifdef TGNX_ATT_CK  // diagnostic: the scores computed
+    ck(1);
+#endif
     // the scale once per lane (lane e holds edge e's scores): the same quotients as per edge, one division
     // instead of one (a ~10-instruction dependent sequence) per edge and head
     if (lane < ne) { my0 /= sqc; my1 /= sqc; }
     softmax();
 #pragma unroll
-    for (int u = 0; u < EB; ++u) {
-      if (u >= ne) break;
+    for (int u = 0; u < EB; ++u) {  // (t of lanes >= ne is 0: the clamped rows add exact zeros)
       o0 += v0[u] * lane_f(t0, u);
       o1 += v1[u] * lane_f(t1, u);
     }
@@ -2216,9 +2230,8 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
     }
 #pragma unroll
     for (int u = 0; u < EB; ++u) {
-      if (b + u >= ne) break;
       const float p0 = wave_sum_f(q0 * k0[u] * on), p1 = wave_sum_f(q1 * k1[u] * on);
-      if (lane == b + u) { my0 = p0; my1 = p1; }
+      if (lane == b + u && b + u < ne) { my0 = p0; my1 = p1; }
     }
   }
   if (lane < ne) { my0 /= sqc; my1 /= sqc; }
@@ -2234,14 +2247,101 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
       v1[u] = Pj[2 * HC + C + l0] + Ee[C + l0];
     }
 #pragma unroll
-    for (int u = 0; u < EB; ++u) {
-      if (b + u >= ne) break;
+    for (int u = 0; u < EB; ++u) {  // (t of lanes >= ne is 0)
       o0 += v0[u] * lane_f(t0, b + u);
       o1 += v1[u] * lane_f(t1, b + u);
     }
   }
   put_qo();
   return make_float2(o0 + sk0, o1 + sk1);
+}
+// One root's 1-hop train attention in the paired-channel lane layout (tgn_pred_train<ATT>): lanes 0-31 carry head 0,
+// lanes 32-63 head 1, lane (h, j) channels 2j and 2j + 1 of head h (j < C / 2): one float2 load per row part instead
+// of two scalar ones, and one 32-lane reduction per edge scores both heads (two full-wave reductions per edge in
+// attn_centre).  Edges [e0, e0 + ne), ne <= EB, neighbour rows from the per-root record (jrec, lane e).  Needs C even
+// and C <= 64.  Returns this lane's two output channels (z[chan], z[chan + 1]; chan = -1 on an idle lane); the alpha /
+// alk / Qo stores are left in *st (issued after the predictor's first barrier, as attn_centre's).
+struct AttnStoresPair {
+  float a0, a1, t0, t1;
+  float2 q, o;
+  int x, e0, ne, chan;
+  __device__ void issue(const Ctx& c, int lane) const {
+    if (lane < ne) {
+      c.alpha[(int64_t)(e0 + lane) * 2] = a0;
+      c.alpha[(int64_t)(e0 + lane) * 2 + 1] = a1;
+      if (c.kvf) {
+        c.alk[(int64_t)(e0 + lane) * 2] = t0;
+        c.alk[(int64_t)(e0 + lane) * 2 + 1] = t1;
+      }
+    }
+    if (c.kvf && chan >= 0) {
+      float* qo = c.Qo + (int64_t)x * 2 * c.HC;
+      *reinterpret_cast<float2*>(qo + chan) = q;
+      *reinterpret_cast<float2*>(qo + c.HC + chan) = o;
+    }
+  }
+};
+template <int EB>
+__device__ __forceinline__ float2 attn_root_pair(const Ctx& c, int x, int i, int e0, int ne, int lane, int jrec,
+                                                 AttnStoresPair* st) {
+  const int C = c.C, HC = c.HC, hc = C >> 1;
+  const int h = lane >> 5, j = lane & 31;
+  const bool act = j < hc;
+  const int ch = h * C + 2 * (act ? j : hc - 1);  // (rows are 8-B aligned: HC even, ch even)
+  const float on = f01(act);
+  const float* Pi = c.P + (int64_t)i * 4 * HC;
+  const float2 q = *reinterpret_cast<const float2*>(Pi + ch);
+  const float2 sk = *reinterpret_cast<const float2*>(Pi + 3 * HC + ch);
+  const float sqc = sqrtf((float)C);
+  const uint64_t dseed = (uint64_t)c.ctl[TGNX_CTL_SEED];
+  const uint64_t dnode = (uint64_t)c.cent[x];
+  const uint64_t deid = (uint64_t)c.e_id[e0 + min(lane, max(ne - 1, 0))];
+  float2 k[EB], v[EB];
+#pragma unroll
+  for (int u = 0; u < EB; ++u) {
+    const int e = min(u, ne - 1);
+    const float* Pj = c.P + (int64_t)lane_i(jrec, e) * 4 * HC;
+    const float2 ee = *reinterpret_cast<const float2*>(c.Ep + (int64_t)(e0 + e) * HC + ch);
+    const float2 kk = *reinterpret_cast<const float2*>(Pj + HC + ch);
+    const float2 vv = *reinterpret_cast<const float2*>(Pj + 2 * HC + ch);
+    k[u] = make_float2(kk.x + ee.x, kk.y + ee.y);
+    v[u] = make_float2(vv.x + ee.x, vv.y + ee.y);
+  }
+  float my0 = -INFINITY, my1 = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < EB; ++u) {
+    const float pr = half_sum_f((q.x * k[u].x + q.y * k[u].y) * on);
+    const float p0 = lane_f(pr, 0), p1 = lane_f(pr, 32);
+    if (lane == u && u < ne) { my0 = p0; my1 = p1; }
+  }
+  if (lane < ne) { my0 /= sqc; my1 /= sqc; }
+  const float mx0 = wave_max_f(my0), mx1 = wave_max_f(my1);
+  const float ex0 = lane < ne ? expf(my0 - mx0) : 0.f, ex1 = lane < ne ? expf(my1 - mx1) : 0.f;
+  const float a0 = ex0 / (wave_sum_f(ex0) + 1e-16f), a1 = ex1 / (wave_sum_f(ex1) + 1e-16f);
+  float t0 = a0, t1 = a1;
+  if (lane < ne && c.drop) {
+    const uint32_t base = drop_base(dseed, (uint64_t)c.att_salt, dnode, deid);
+    t0 *= keep32(base, 0u, c.p, c.inv_keep);
+    t1 *= keep32(base, 1u, c.p, c.inv_keep);
+  }
+  float2 o = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int u = 0; u < EB; ++u) {  // (t of lanes >= ne is 0: the clamped rows add exact zeros)
+    const float tu = h ? lane_f(t1, u) : lane_f(t0, u);
+    o.x += v[u].x * tu;
+    o.y += v[u].y * tu;
+  }
+  st->a0 = a0;
+  st->a1 = a1;
+  st->t0 = t0;
+  st->t1 = t1;
+  st->q = q;
+  st->o = o;
+  st->x = x;
+  st->e0 = e0;
+  st->ne = ne;
+  st->chan = act ? ch : -1;
+  return make_float2(o.x + sk.x, o.y + sk.y);
 }
 template <bool TRAIN>
 __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
@@ -2372,6 +2472,15 @@ __global__ void __launch_bounds__(1024) tgn_plan_table_kernel(Ctx c, char* tab, 
 // waves per workgroup: 1 hop (ATT) 8 — waves 1-3 the roots' attention, waves 0 and 4-7 the weight staging, then
 // all 8 share the contractions (the workgroup is alone on its CU: one wave per SIMD left each dependent step's
 // latency exposed, measured 38 % of the waves' cycles issuing); 2 hops 4
+#ifndef TGNX_PRED_WIDE_ATOM
+#define TGNX_PRED_WIDE_ATOM 0  // the predictor's dZc adds as whole-row wave instructions through LDS (one more barrier)
+#endif
+#ifndef TGNX_DZC_REP
+#define TGNX_DZC_REP 1  // 1-hop train: copies of dZc the predictor's workgroups spread their atomics over
+#endif
+#ifndef TGNX_ATT_PAIR
+#define TGNX_ATT_PAIR 1  // the predictor's attention in the paired-channel lane layout (attn_root_pair)
+#endif
 #ifndef TGNX_PRED_WAVES
 #define TGNX_PRED_WAVES 8  // 1-hop predictor workgroup waves (4: the round-4 layout, one staging wave)
 #endif
@@ -2421,29 +2530,54 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
   AttnStores ast;  // ATT, waves 1-3: the attention's alpha / alk / Qo stores, issued after the first barrier
   ast.ne = 0;
   ast.x = -1;
+  AttnStoresPair asp;  // (the paired-channel form's)
+  asp.x = -1;
   if (ATT && wv >= 1 && wv <= 3) {
     const int r = wv - 1;
     const int4 q = c.evq[3 * blockIdx.x + r];  // {centre row, P row, edge range}; grid = max_batch: in bounds
     const int jr = c.evj ? c.evj[(3 * blockIdx.x + r) * 16 + (lane & 15)] : -1;  // the edges' neighbour rows
     if (!live) return;
-#if TGNX_PRED_CKPT == 3
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    TGNX_STAMP_AT(0);
-#endif
-    const float2 o = attn_centre<true, EB>(c, q.x, q.y, q.z, q.w - q.z, lane, c.evj && q.w - q.z <= 16 ? max(jr, 0) : -1,
-                                           TGNX_PRED_DEFER ? &ast : nullptr);
-#if TGNX_PRED_CKPT == 3
-    TGNX_STAMP_AT(1);
-#endif
-    if (lane < c.C) {
-      z[r][lane] = o.x;
-      z[r][c.C + lane] = o.y;
-      if (c.emb) {  // DyRep embedding messages read the centre's embedding (every root of it writes equal values)
-        c.Zc[(int64_t)q.x * c.HC + lane] = o.x;
-        c.Zc[(int64_t)q.x * c.HC + c.C + lane] = o.y;
+    bool paired = false;
+#if TGNX_ATT_PAIR
+    if (c.evj && q.w - q.z <= EB && (c.C & 1) == 0 && c.C <= 64) {
+      paired = true;
+      const float2 o = attn_root_pair<EB>(c, q.x, q.y, q.z, q.w - q.z, lane, max(jr, 0), &asp);
+      if (asp.chan >= 0) {
+        z[r][asp.chan] = o.x;
+        z[r][asp.chan + 1] = o.y;
+        if (c.emb) {  // DyRep embedding messages read the centre's embedding (every root of it writes equal values)
+          c.Zc[(int64_t)q.x * c.HC + asp.chan] = o.x;
+          c.Zc[(int64_t)q.x * c.HC + asp.chan + 1] = o.y;
+        }
       }
+      if (lane == 0) scr[r] = q.x;
     }
-    if (lane == 0) scr[r] = q.x;
+#endif
+    if (!paired) {
+#if TGNX_PRED_CKPT == 3
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      TGNX_STAMP_AT(0);
+#endif
+#if TGNX_PRED_CKPT == 4  // (diagnostic, with TGNX_STAMP_TID 64 and TGNX_ATT_CK: wave 1's edge rows landed / scores done)
+      const float2 o = attn_centre<true, EB>(c, q.x, q.y, q.z, q.w - q.z, lane, c.evj && q.w - q.z <= 16 ? max(jr, 0) : -1,
+                                             TGNX_PRED_DEFER ? &ast : nullptr, [&](int slot) { TGNX_STAMP_AT(slot); });
+#else
+      const float2 o = attn_centre<true, EB>(c, q.x, q.y, q.z, q.w - q.z, lane, c.evj && q.w - q.z <= 16 ? max(jr, 0) : -1,
+                                             TGNX_PRED_DEFER ? &ast : nullptr);
+#endif
+#if TGNX_PRED_CKPT == 3
+      TGNX_STAMP_AT(1);
+#endif
+      if (lane < c.C) {
+        z[r][lane] = o.x;
+        z[r][c.C + lane] = o.y;
+        if (c.emb) {  // DyRep embedding messages read the centre's embedding (every root of it writes equal values)
+          c.Zc[(int64_t)q.x * c.HC + lane] = o.x;
+          c.Zc[(int64_t)q.x * c.HC + c.C + lane] = o.y;
+        }
+      }
+      if (lane == 0) scr[r] = q.x;
+    }
   } else if (!ATT && wv == 0) {
     int cr[3];  // the roots' centre rows (tgn_agg_emit) by rank-local event: issued with the ctl loads
 #pragma unroll
@@ -2553,6 +2687,7 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
   TGNX_STAMP_AT(1);
 #endif
   if (ATT && TGNX_PRED_DEFER && ast.x >= 0) ast.issue(c, lane);
+  if (ATT && asp.x >= 0) asp.issue(c, lane);
   const int cr[3] = {scr[0], scr[1], scr[2]};
   // lin_src(z_s), lin_dst(z_p), lin_dst(z_n), split over the hidden units' inputs k: NW partial sums per output
   if (flat) {  // wave wv takes float4 columns [q0, q0 + nq)
@@ -2712,11 +2847,35 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
 #if TGNX_PRED_CKPT == 2
     TGNX_STAMP_AT(0);
 #endif
+    float* dz = c.dZc + (int64_t)(blockIdx.x % c.dzrep) * c.dzstride;
+#if TGNX_PRED_WIDE_ATOM
+    // the three rows gathered in LDS first, then added with whole-row wave instructions (contiguous lanes: 6 per
+    // workgroup instead of 3 per wave on 13-lane segments — every one of them queues on a hub centre's row)
+    __shared__ float dzl[3][TDMAX];
     if (kg == 0 && oko) {
-      atomicAdd(&c.dZc[(int64_t)cr[0] * D + o], a);
-      atomicAdd(&c.dZc[(int64_t)cr[1] * D + o], b);
-      atomicAdd(&c.dZc[(int64_t)cr[2] * D + o], d2);
+      dzl[0][o] = a;
+      dzl[1][o] = b;
+      dzl[2][o] = d2;
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int x = tid; x < 3 * D; x += 64 * NW) {
+      const int r = x >= 2 * D ? 2 : x >= D ? 1 : 0, oo = x - r * D;
+      atomicAdd(&dz[(int64_t)cr[r] * D + oo], dzl[r][oo]);
+    }
+#else
+    if (kg == 0 && oko) {
+#ifdef TGNX_PRED_DIAG_NOATOM  // diagnostic only (wrong sums): plain stores instead of the dZc atomics
+      dz[(int64_t)cr[0] * D + o] = a;
+      dz[(int64_t)cr[1] * D + o] = b;
+      dz[(int64_t)cr[2] * D + o] = d2;
+#else
+      atomicAdd(&dz[(int64_t)cr[0] * D + o], a);
+      atomicAdd(&dz[(int64_t)cr[1] * D + o], b);
+      atomicAdd(&dz[(int64_t)cr[2] * D + o], d2);
+#endif
+    }
+#endif
 #if TGNX_PRED_CKPT == 2
     TGNX_STAMP_AT(1);
 #endif
@@ -2877,6 +3036,10 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
       const float* Ee = c.Ep + (int64_t)er[u] * HC;
       g0[u] = G[l0];
       g1[u] = G[C + l0];
+      for (int rp = 1; rp < c.dzrep; ++rp) {  // (the predictor's dZc copies, in copy order)
+        g0[u] += G[rp * c.dzstride + l0];
+        g1[u] += G[rp * c.dzstride + C + l0];
+      }
       q0[u] = Q[l0];
       q1[u] = Q[C + l0];
       o0[u] = Q[HC + l0];
@@ -2884,9 +3047,19 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
       v0[u] = Pj[l0] + Ee[l0];
       v1[u] = Pj[C + l0] + Ee[C + l0];
     }
+    // the batch's reductions first, all independent (a runtime `break` in one loop kept it rolled: indexed register
+    // reads and one edge's four reductions after another's), then the run bookkeeping
+    float gv0[KVE_B], gv1[KVE_B], go0[KVE_B], go1[KVE_B];
 #pragma unroll
     for (int u = 0; u < KVE_B; ++u) {
-      if (u >= nb) break;
+      gv0[u] = wave_sum_f(g0[u] * v0[u] * on);
+      gv1[u] = wave_sum_f(g1[u] * v1[u] * on);
+      go0[u] = wave_sum_f(g0[u] * o0[u] * on);
+      go1[u] = wave_sum_f(g1[u] * o1[u] * on);
+    }
+#pragma unroll
+    for (int u = 0; u < KVE_B; ++u) {
+      if (u >= nb) continue;
       if (jj[u] != jc) {  // wave-uniform run boundary
 #if TGNX_KVE_MERGE
         if (first) {
@@ -2903,9 +3076,7 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
         s[0] = s[1] = s[2] = s[3] = 0.f;
         jc = jj[u];
       }
-      const float gv0 = wave_sum_f(g0[u] * v0[u] * on), gv1 = wave_sum_f(g1[u] * v1[u] * on);
-      const float go0 = wave_sum_f(g0[u] * o0[u] * on), go1 = wave_sum_f(g1[u] * o1[u] * on);
-      const float ds0 = (t0[u] * gv0 - a0[u] * go0) * isq, ds1 = (t1[u] * gv1 - a1[u] * go1) * isq;
+      const float ds0 = (t0[u] * gv0[u] - a0[u] * go0[u]) * isq, ds1 = (t1[u] * gv1[u] - a1[u] * go1[u]) * isq;
       const float dk0 = ds0 * q0[u], dk1 = ds1 * q1[u];
       const float dv0 = t0[u] * g0[u], dv1 = t1[u] * g1[u];
       if (okl) {
@@ -3009,7 +3180,13 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
   const float* Pi = c.P + (int64_t)i * 4 * HC;
   float* dPi = c.dP + (int64_t)i * 4 * HC;
   const float q0 = Pi[l0], q1 = Pi[C + l0];
-  const float g0 = c.dZc[(int64_t)x * HC + l0] * on, g1 = c.dZc[(int64_t)x * HC + C + l0] * on;
+  float g0 = c.dZc[(int64_t)x * HC + l0], g1 = c.dZc[(int64_t)x * HC + C + l0];
+  for (int rp = 1; rp < c.dzrep; ++rp) {  // (the predictor's dZc copies, in copy order)
+    g0 += c.dZc[rp * c.dzstride + (int64_t)x * HC + l0];
+    g1 += c.dZc[rp * c.dzstride + (int64_t)x * HC + C + l0];
+  }
+  g0 *= on;
+  g1 *= on;
   const float sqc = sqrtf((float)C);
   const int ne = e1 - e0;
   const int le = e0 + min(lane, max(ne - 1, 0));
@@ -3037,10 +3214,9 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
     }
     float da0 = 0.f, da1 = 0.f;
 #pragma unroll
-    for (int u = 0; u < EB; ++u) {
-      if (u >= ne) break;
+    for (int u = 0; u < EB; ++u) {  // (no early exit: it kept the loop rolled; see attn_centre)
       const float p0 = wave_sum_f(g0 * v0[u]), p1 = wave_sum_f(g1 * v1[u]);
-      if (lane == u) { da0 = p0 * k0v; da1 = p1 * k1v; }
+      if (lane == u && u < ne) { da0 = p0 * k0v; da1 = p1 * k1v; }
     }
     const float s0 = wave_sum_f(a0 * da0), s1 = wave_sum_f(a1 * da1);
     const float ds0 = a0 * (da0 - s0), ds1 = a1 * (da1 - s1);
@@ -3048,15 +3224,14 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
     const float dq0s = ds0 / sqc, dq1s = ds1 / sqc;  // (per lane = per edge: one division, not one per edge)
     float dq0 = 0.f, dq1 = 0.f;
 #pragma unroll
-    for (int u = 0; u < EB; ++u) {
-      if (u >= ne) break;
+    for (int u = 0; u < EB; ++u) {  // (lanes >= ne hold ds = 0: the clamped rows add exact zeros to dq)
       const float d0 = lane_f(dq0s, u), d1 = lane_f(dq1s, u);
       const float b0 = lane_f(t0, u), b1 = lane_f(t1, u);
       float* dEe = c.dE + (int64_t)(e0 + u) * HC;
       float* dKe = c.dKV + (int64_t)(e0 + u) * 2 * HC;  // [dk (HC) | dv (HC)]
       dq0 += d0 * kk0[u];
       dq1 += d1 * kk1[u];
-      if (okl && wkv) {
+      if (okl && wkv && u < ne) {
         const float dk0 = d0 * q0, dk1 = d1 * q1;
         const float dv0 = b0 * g0, dv1 = b1 * g1;
         dEe[lane] = dk0 + dv0;
@@ -3089,9 +3264,8 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
     }
 #pragma unroll
     for (int u = 0; u < EB; ++u) {
-      if (b + u >= ne) break;
       const float p0 = wave_sum_f(g0 * v0[u]), p1 = wave_sum_f(g1 * v1[u]);
-      if (lane == b + u) { da0 = p0 * k0v; da1 = p1 * k1v; }
+      if (lane == b + u && b + u < ne) { da0 = p0 * k0v; da1 = p1 * k1v; }
     }
   }
   // softmax backward: d score = alpha (d alpha - Σ alpha d alpha)
@@ -3112,15 +3286,14 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
     }
 #pragma unroll
     for (int u = 0; u < EB; ++u) {
-      const int e = b + u;
-      if (e >= ne) break;
+      const int e = b + u;  // (e >= ne: ds = 0 there, and no stores)
       const float d0 = lane_f(dq0s, e), d1 = lane_f(dq1s, e);
       const float b0 = lane_f(t0, e), b1 = lane_f(t1, e);
       float* dEe = c.dE + (int64_t)(e0 + e) * HC;
       float* dKe = c.dKV + (int64_t)(e0 + e) * 2 * HC;  // [dk (HC) | dv (HC)]
       dq0 += d0 * kk0[u];
       dq1 += d1 * kk1[u];
-      if (okl && wkv) {
+      if (okl && wkv && e < ne) {
         const float dk0 = d0 * q0, dk1 = d1 * q1;
         const float dv0 = b0 * g0, dv1 = b1 * g1;
         dEe[lane] = dk0 + dv0;
@@ -4246,7 +4419,7 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.cevj = carve(off, (size_t)k.Rcap * 16 * 4);
   W.Hs = carve(off, (size_t)k.Rcap * D * 4);
   W.Hd = carve(off, (size_t)k.Rcap * D * 4);
-  W.dZc = carve(off, (size_t)k.Rtr * HC * 4);
+  W.dZc = carve(off, (size_t)k.Rtr * HC * 4 * (k.layers == 2 ? 1 : TGNX_DZC_REP));
   W.dP = carve(off, (size_t)k.Mtr * 4 * HC * 4);
   W.dE = carve(off, (size_t)k.Etr * HC * 4);
   W.dKV = carve(off, (size_t)(k.Etr > k.E1tr ? k.Etr : k.E1tr) * 2 * HC * 4);  // both levels (used in turn)
@@ -4443,6 +4616,8 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.Hs = reinterpret_cast<float*>(ws + W.Hs);
   c.Hd = reinterpret_cast<float*>(ws + W.Hd);
   c.dZc = reinterpret_cast<float*>(ws + W.dZc);
+  c.dzrep = k.layers == 2 ? 1 : TGNX_DZC_REP;
+  c.dzstride = (int64_t)k.Rtr * k.HC;
   c.dP = reinterpret_cast<float*>(ws + W.dP);
   c.dE = reinterpret_cast<float*>(ws + W.dE);
   c.dKV = reinterpret_cast<float*>(ws + W.dKV);

@@ -18,12 +18,19 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
+_STREAMS = {}
+
+
 def run(W, B, steps, warmup, dataset, layers, global_batch=0):
     from tgnx.sampler import LastNeighborLoader
     from tgnx.synth import SHAPES, make_stream
     from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
     shape = SHAPES[dataset]
-    s = make_stream(shape, seed=0)
+    if dataset not in _STREAMS:   # (the full tgbl-comment stream takes a while to draw: once per dataset)
+        print(f"[dp_compute] drawing the {dataset} stream", file=sys.stderr, flush=True)
+        _STREAMS[dataset] = make_stream(shape, seed=0)
+    print(f"[dp_compute] {dataset} W={W}", file=sys.stderr, flush=True)
+    s = _STREAMS[dataset]
     dev = torch.device("cuda")
     Bg = global_batch if global_batch else B * W
     model = TGNModel(shape.num_nodes, s.num_events, shape.msg_dim, 100, dev, ring=10, max_batch=Bg, max_neg=1,
@@ -65,6 +72,8 @@ def run(W, B, steps, warmup, dataset, layers, global_batch=0):
                                 "row_allgather_in_per_rank": 4 * rows // W},
                    ring_send_bytes_per_rank={"fused": round(2 * (W - 1) / W * 4 * eng.comm.numel()),
                                              "split": round(2 * (W - 1) / W * 4 * G + (W - 1) / W * 4 * rows)})
+    del eng, model
+    torch.cuda.empty_cache()
     return out
 
 
