@@ -2473,13 +2473,18 @@ __global__ void __launch_bounds__(1024) tgn_plan_table_kernel(Ctx c, char* tab, 
 // all 8 share the contractions (the workgroup is alone on its CU: one wave per SIMD left each dependent step's
 // latency exposed, measured 38 % of the waves' cycles issuing); 2 hops 4
 #ifndef TGNX_PRED_WIDE_ATOM
-#define TGNX_PRED_WIDE_ATOM 0  // the predictor's dZc adds as whole-row wave instructions through LDS (one more barrier)
+#define TGNX_PRED_WIDE_ATOM 1  // the predictor's dZc adds as whole-row wave instructions through LDS (one more barrier;
+                               // same-box A/B: predictor 14.1 -> 12.6-13.1 us, step -1 %)
 #endif
 #ifndef TGNX_DZC_REP
-#define TGNX_DZC_REP 1  // 1-hop train: copies of dZc the predictor's workgroups spread their atomics over
+#define TGNX_DZC_REP 1  // 1-hop train: copies of dZc the predictor's workgroups spread their atomics over (4: predictor
+                        // -1 us, but the attention backward +6 us reading the copies per edge; profiles/r5/r5_pred_p7_ab.txt)
 #endif
 #ifndef TGNX_ATT_PAIR
 #define TGNX_ATT_PAIR 1  // the predictor's attention in the paired-channel lane layout (attn_root_pair)
+#endif
+#ifndef TGNX_BWD_PAIR
+#define TGNX_BWD_PAIR 0  // the attention backward (centre and edge blocks) in that layout: measured slower (12.0 -> 12.2-12.5 us)
 #endif
 #ifndef TGNX_PRED_WAVES
 #define TGNX_PRED_WAVES 8  // 1-hop predictor workgroup waves (4: the round-4 layout, one staging wave)
@@ -2937,6 +2942,9 @@ constexpr int KVE_CH = TGNX_KVE_CH, KVE_PW = KVE_CH / 4;
 #define TGNX_KVE_B 8
 #endif
 constexpr int KVE_B = TGNX_KVE_B < KVE_PW ? TGNX_KVE_B : KVE_PW;  // edges per load batch of a wave
+// PAIR: the paired-channel lane layout (attn_root_pair): lane (h, j) carries channels 2j, 2j + 1 of head h, so one
+// 32-lane reduction per edge serves both heads and the rows move as float2 (C even, C <= 64)
+template <bool PAIR>
 __device__ void kv_edge_body(const Ctx& c, int bid) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
@@ -2986,9 +2994,13 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
   const int n = min(KVE_PW, ne - i0);
 #endif
   const int C = c.C, HC = c.HC;
-  const bool okl = lane < C;
+  // this lane's two channels (oA, oB within HC; clamped for loads) and head of each
+  const int hc = C >> 1, ph = lane >> 5, pj = lane & 31;
+  const bool okl = PAIR ? pj < hc : lane < C;
   const float on = f01(okl);
-  const int l0 = min(lane, C - 1);
+  const int l0 = min(lane, C - 1), pc = ph * C + 2 * (pj < hc ? pj : hc - 1);
+  const int oA = PAIR ? pc : l0, oB = PAIR ? pc + 1 : C + l0;
+  const int hA = PAIR ? ph : 0, hB = PAIR ? ph : 1;
   const float isq = 1.0f / sqrtf((float)C);
   float s[4] = {0.f, 0.f, 0.f, 0.f};  // run sums: dk (head 0, 1), dv (head 0, 1)
   int jc = n > 0 ? sj[sorder[i0]] : -1;
@@ -2996,19 +3008,19 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
   auto flush = [&]() {
     if (okl) {
       float* dst = c.dP + (int64_t)jc * 4 * HC + HC;
-      atomicAdd(dst + lane, s[0]);
-      atomicAdd(dst + C + lane, s[1]);
-      atomicAdd(dst + HC + lane, s[2]);
-      atomicAdd(dst + HC + C + lane, s[3]);
+      atomicAdd(dst + oA, s[0]);
+      atomicAdd(dst + oB, s[1]);
+      atomicAdd(dst + HC + oA, s[2]);
+      atomicAdd(dst + HC + oB, s[3]);
     }
   };
   auto store = [&]() {  // the row's complete (dk, dv) sums (globally sorted edges)
     if (okl) {
       float* dst = c.dP + (int64_t)jc * 4 * HC + HC;
-      dst[lane] = s[0];
-      dst[C + lane] = s[1];
-      dst[HC + lane] = s[2];
-      dst[HC + C + lane] = s[3];
+      dst[oA] = s[0];
+      dst[oB] = s[1];
+      dst[HC + oA] = s[2];
+      dst[HC + oB] = s[3];
     }
   };
   // the wave's sorted edges in batches of KVE_B (all of a batch's loads in flight), runs continuing across
@@ -3026,36 +3038,41 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
     float g0[KVE_B], g1[KVE_B], q0[KVE_B], q1[KVE_B], o0[KVE_B], o1[KVE_B], v0[KVE_B], v1[KVE_B];
 #pragma unroll
     for (int u = 0; u < KVE_B; ++u) {  // softmax weights, centre rows (g, q, o), the neighbour's v row + edge row
-      a0[u] = c.alpha[(int64_t)er[u] * 2];
-      a1[u] = c.alpha[(int64_t)er[u] * 2 + 1];
-      t0[u] = c.alk[(int64_t)er[u] * 2];
-      t1[u] = c.alk[(int64_t)er[u] * 2 + 1];
+      a0[u] = c.alpha[(int64_t)er[u] * 2 + hA];   // (PAIR: the lane's head for both channels)
+      a1[u] = c.alpha[(int64_t)er[u] * 2 + hB];
+      t0[u] = c.alk[(int64_t)er[u] * 2 + hA];
+      t1[u] = c.alk[(int64_t)er[u] * 2 + hB];
       const float* G = c.dZc + (int64_t)xx[u] * HC;
       const float* Q = c.Qo + (int64_t)xx[u] * 2 * HC;
       const float* Pj = c.P + (int64_t)jj[u] * 4 * HC + 2 * HC;
       const float* Ee = c.Ep + (int64_t)er[u] * HC;
-      g0[u] = G[l0];
-      g1[u] = G[C + l0];
+      g0[u] = G[oA];
+      g1[u] = G[oB];
       for (int rp = 1; rp < c.dzrep; ++rp) {  // (the predictor's dZc copies, in copy order)
-        g0[u] += G[rp * c.dzstride + l0];
-        g1[u] += G[rp * c.dzstride + C + l0];
+        g0[u] += G[rp * c.dzstride + oA];
+        g1[u] += G[rp * c.dzstride + oB];
       }
-      q0[u] = Q[l0];
-      q1[u] = Q[C + l0];
-      o0[u] = Q[HC + l0];
-      o1[u] = Q[HC + C + l0];
-      v0[u] = Pj[l0] + Ee[l0];
-      v1[u] = Pj[C + l0] + Ee[C + l0];
+      q0[u] = Q[oA];
+      q1[u] = Q[oB];
+      o0[u] = Q[HC + oA];
+      o1[u] = Q[HC + oB];
+      v0[u] = Pj[oA] + Ee[oA];
+      v1[u] = Pj[oB] + Ee[oB];
     }
     // the batch's reductions first, all independent (a runtime `break` in one loop kept it rolled: indexed register
     // reads and one edge's four reductions after another's), then the run bookkeeping
     float gv0[KVE_B], gv1[KVE_B], go0[KVE_B], go1[KVE_B];
 #pragma unroll
     for (int u = 0; u < KVE_B; ++u) {
-      gv0[u] = wave_sum_f(g0[u] * v0[u] * on);
-      gv1[u] = wave_sum_f(g1[u] * v1[u] * on);
-      go0[u] = wave_sum_f(g0[u] * o0[u] * on);
-      go1[u] = wave_sum_f(g1[u] * o1[u] * on);
+      if (PAIR) {  // each 32-lane half sums its own head: both channels of a lane share it
+        gv0[u] = gv1[u] = half_sum_f((g0[u] * v0[u] + g1[u] * v1[u]) * on);
+        go0[u] = go1[u] = half_sum_f((g0[u] * o0[u] + g1[u] * o1[u]) * on);
+      } else {
+        gv0[u] = wave_sum_f(g0[u] * v0[u] * on);
+        gv1[u] = wave_sum_f(g1[u] * v1[u] * on);
+        go0[u] = wave_sum_f(g0[u] * o0[u] * on);
+        go1[u] = wave_sum_f(g1[u] * o1[u] * on);
+      }
     }
 #pragma unroll
     for (int u = 0; u < KVE_B; ++u) {
@@ -3081,8 +3098,8 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
       const float dv0 = t0[u] * g0[u], dv1 = t1[u] * g1[u];
       if (okl) {
         float* dEe = c.dE + (int64_t)er[u] * HC;
-        dEe[lane] = dk0 + dv0;
-        dEe[C + lane] = dk1 + dv1;
+        dEe[oA] = dk0 + dv0;
+        dEe[oB] = dk1 + dv1;
       }
       s[0] += dk0;
       s[1] += dk1;
@@ -3148,7 +3165,8 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
     return;
   }
   if ((int)blockIdx.x >= ncb) {
-    kv_edge_body(c, (int)blockIdx.x - ncb);
+    if (TGNX_BWD_PAIR && (c.C & 1) == 0 && c.C <= 64) kv_edge_body<true>(c, (int)blockIdx.x - ncb);
+    else kv_edge_body<false>(c, (int)blockIdx.x - ncb);
     return;
   }
   const bool wkv = nkv == 0;  // per-edge dk / dv / dE written here (else by the edge blocks)
@@ -3198,6 +3216,65 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
   if (lane < ne && c.drop) {
     k0v = att_keep(c, seed, x, e0 + lane, 0);
     k1v = att_keep(c, seed, x, e0 + lane, 1);
+  }
+  if (TGNX_BWD_PAIR && ne > 0 && ne <= EB && (C & 1) == 0 && C <= 64) {
+    // the paired-channel lane layout of attn_root_pair: lanes 0-31 head 0, 32-63 head 1, two channels per lane;
+    // one 32-lane reduction per edge for both heads' d alpha, float2 rows
+    const int hh = lane >> 5, jj = lane & 31, hc = C >> 1;
+    const bool act = jj < hc;
+    const int ch = hh * C + 2 * (act ? jj : hc - 1);
+    const float onp = f01(act);
+    float2 g = *reinterpret_cast<const float2*>(c.dZc + (int64_t)x * HC + ch);
+    for (int rp = 1; rp < c.dzrep; ++rp) {  // (the predictor's dZc copies, in copy order)
+      const float2 gr = *reinterpret_cast<const float2*>(c.dZc + rp * c.dzstride + (int64_t)x * HC + ch);
+      g.x += gr.x;
+      g.y += gr.y;
+    }
+    g.x *= onp;
+    g.y *= onp;
+    const float2 qp = *reinterpret_cast<const float2*>(Pi + ch);
+    float2 kk[EB], vv[EB];
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      const int e = min(u, ne - 1);
+      const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
+      const float2 ee = *reinterpret_cast<const float2*>(c.Ep + (int64_t)(e0 + e) * HC + ch);
+      const float2 k2 = *reinterpret_cast<const float2*>(Pj + HC + ch);
+      const float2 v2 = *reinterpret_cast<const float2*>(Pj + 2 * HC + ch);
+      kk[u] = make_float2(k2.x + ee.x, k2.y + ee.y);
+      vv[u] = make_float2(v2.x + ee.x, v2.y + ee.y);
+    }
+    float da0 = 0.f, da1 = 0.f;
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      const float pr = half_sum_f(g.x * vv[u].x + g.y * vv[u].y);
+      const float p0 = lane_f(pr, 0), p1 = lane_f(pr, 32);
+      if (lane == u && u < ne) { da0 = p0 * k0v; da1 = p1 * k1v; }
+    }
+    const float s0 = wave_sum_f(a0 * da0), s1 = wave_sum_f(a1 * da1);
+    const float ds0 = a0 * (da0 - s0), ds1 = a1 * (da1 - s1);
+    const float t0 = a0 * k0v, t1 = a1 * k1v;
+    const float dq0s = ds0 / sqc, dq1s = ds1 / sqc;
+    float2 dq = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {  // (lanes >= ne hold ds = 0: the clamped rows add exact zeros to dq)
+      const float d = hh ? lane_f(dq1s, u) : lane_f(dq0s, u);
+      dq.x += d * kk[u].x;
+      dq.y += d * kk[u].y;
+      if (act && wkv && u < ne) {
+        const float b = hh ? lane_f(t1, u) : lane_f(t0, u);
+        const float2 dk = make_float2(d * qp.x, d * qp.y), dv = make_float2(b * g.x, b * g.y);
+        *reinterpret_cast<float2*>(c.dE + (int64_t)(e0 + u) * HC + ch) = make_float2(dk.x + dv.x, dk.y + dv.y);
+        float* dKe = c.dKV + (int64_t)(e0 + u) * 2 * HC;  // [dk (HC) | dv (HC)]
+        *reinterpret_cast<float2*>(dKe + ch) = dk;
+        *reinterpret_cast<float2*>(dKe + HC + ch) = dv;
+      }
+    }
+    if (act) {
+      *reinterpret_cast<float2*>(dPi + ch) = dq;
+      *reinterpret_cast<float2*>(dPi + 3 * HC + ch) = g;
+    }
+    return;
   }
   if (ne > 0 && ne <= EB) {  // every ring of K <= 16: v, k and edge rows of all edges in one round
     float kk0[EB], kk1[EB], v0[EB], v1[EB];
