@@ -10,7 +10,7 @@ for model in tgn tgnn; do
   for ctr in FETCH_SIZE WRITE_SIZE; do
     sub=$(echo $ctr | cut -d_ -f1 | tr A-Z a-z)
     timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d $R/gpurun_out/${tag}_pmc/${model}_${sub} -o run -- \
-      python3 $R/bench.py --model $model --only --no-graph --steps 30 --warmup 5 --probe-steps 1 --no-cpu-baseline --no-train-loop --no-tcsr \
+      python3 $R/bench.py --model $model --only --no-graph --steps 30 --warmup 5 --probe-steps 1 --window start --no-cpu-baseline --no-train-loop --no-tcsr \
       > $R/gpurun_out/${tag}_pmc_${model}_${sub}.log 2>&1 || exit $?
   done
 done
