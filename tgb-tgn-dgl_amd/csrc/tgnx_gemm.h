@@ -830,7 +830,16 @@ template <class CFG, class EPI>
 inline GemmFix<CFG, EPI> gemm_fix(const GemmShape& g, const float* part, const EPI& epi) {
   return GemmFix<CFG, EPI>{g, part, epi};
 }
-// one output tile of a deferred GEMM: Σ partials over the runtime splits in order, then the epilogue
+// one output tile of a deferred GEMM: Σ partials over the runtime splits in order, then the epilogue.
+// An epilogue with `fix_pre(tile)` (the fused-Adam weight-gradient writers) gets its loads issued before the
+// partials' (they need only the tile's coordinates): one dependent round per tile instead of three
+template <class E, class = void>
+struct HasFixPre : std::false_type {};
+template <class E>
+struct HasFixPre<E, std::void_t<decltype(E::fix_pre_tag)>> : std::true_type {};
+#ifndef TGNX_FIX_PRE
+#define TGNX_FIX_PRE 0  // (same-box A/Bs: fixup 11.6-12.0 -> 12.1-12.6 us with the prefetch, step +0.3 %; kept as a knob)
+#endif
 template <class CFG, class EPI>
 __device__ void gemm_fix_tile(const GemmFix<CFG, EPI>& f, int tile, float* smem) {
   constexpr int TM = CFG::TM, TN = CFG::TN, FM = CFG::FM, FN = CFG::FN, PB = CFG::PB;
@@ -841,48 +850,57 @@ __device__ void gemm_fix_tile(const GemmFix<CFG, EPI>& f, int tile, float* smem)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wr = (wv >> 1) * (TM / 2), wc = (wv & 1) * (TN / 2), li = lane & 15, lk = lane >> 4;
   float* Ct = smem;
-  if constexpr (CFG::WS) {  // row-major partials
-    constexpr int PER = TM * TN / 256, SU = 8;
+  const GemmTile<TM, TN> tl{Ct, m0, n0, rt.Mr, rt.Nr, smem + TM * PB};
+  auto sum_tile = [&]() {
+    if constexpr (CFG::WS) {  // row-major partials
+      constexpr int PER = TM * TN / 256, SU = 8;
 #pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      const int x = threadIdx.x + 256 * e;
-      float sum = 0.f;
-      for (int q0 = 0; q0 < rt.Sr; q0 += SU) {
-        float pv[SU];
+      for (int e = 0; e < PER; ++e) {
+        const int x = threadIdx.x + 256 * e;
+        float sum = 0.f;
+        for (int q0 = 0; q0 < rt.Sr; q0 += SU) {
+          float pv[SU];
 #pragma unroll
-        for (int u = 0; u < SU; ++u) pv[u] = f.part[((size_t)tile * f.g.S + min(q0 + u, rt.Sr - 1)) * TM * TN + x];
+          for (int u = 0; u < SU; ++u) pv[u] = f.part[((size_t)tile * f.g.S + min(q0 + u, rt.Sr - 1)) * TM * TN + x];
 #pragma unroll
-        for (int u = 0; u < SU; ++u) sum += pv[u] * f01(q0 + u < rt.Sr);
-      }
-      Ct[(x / TN) * PB + x % TN] = sum;
-    }
-    __syncthreads();
-    f.epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, smem + TM * PB});
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      // every split's partial in flight at once (clamped loads, masked sum; split order fixed)
-      constexpr int SU = 8;
-      f32x4_t sum = {0.f, 0.f, 0.f, 0.f};
-      for (int q0 = 0; q0 < rt.Sr; q0 += SU) {
-        f32x4_t pv[SU];
-#pragma unroll
-        for (int u = 0; u < SU; ++u) {
-          const int q = min(q0 + u, rt.Sr - 1);
-          pv[u] = reinterpret_cast<const f32x4_t*>(f.part + ((size_t)tile * f.g.S + q) * TM * TN)
-              [((wv * FM + i) * FN + j) * 64 + lane];
+          for (int u = 0; u < SU; ++u) sum += pv[u] * f01(q0 + u < rt.Sr);
         }
-#pragma unroll
-        for (int u = 0; u < SU; ++u) sum += pv[u] * f01(q0 + u < rt.Sr);
+        Ct[(x / TN) * PB + x % TN] = sum;
       }
+    } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Ct[(wr + 16 * i + lk * 4 + r) * PB + wc + 16 * j + li] = sum[r];
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          // every split's partial in flight at once (clamped loads, masked sum; split order fixed)
+          constexpr int SU = 8;
+          f32x4_t sum = {0.f, 0.f, 0.f, 0.f};
+          for (int q0 = 0; q0 < rt.Sr; q0 += SU) {
+            f32x4_t pv[SU];
+#pragma unroll
+            for (int u = 0; u < SU; ++u) {
+              const int q = min(q0 + u, rt.Sr - 1);
+              pv[u] = reinterpret_cast<const f32x4_t*>(f.part + ((size_t)tile * f.g.S + q) * TM * TN)
+                  [((wv * FM + i) * FN + j) * 64 + lane];
+            }
+#pragma unroll
+            for (int u = 0; u < SU; ++u) sum += pv[u] * f01(q0 + u < rt.Sr);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Ct[(wr + 16 * i + lk * 4 + r) * PB + wc + 16 * j + li] = sum[r];
+        }
     }
-  __syncthreads();
-  f.epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, smem + TM * PB});
+  };
+  if constexpr (TGNX_FIX_PRE && HasFixPre<EPI>::value) {
+    const auto pr = f.epi.fix_pre(tl);
+    sum_tile();
+    __syncthreads();
+    f.epi(tl, pr);
+  } else {
+    sum_tile();
+    __syncthreads();
+    f.epi(tl);
+  }
 }
 template <class CFG, class EPI>
 __device__ __forceinline__ bool gemm_fix_dispatch(const GemmFix<CFG, EPI>& f, int& bid, float* smem) {

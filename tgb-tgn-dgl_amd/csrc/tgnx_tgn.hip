@@ -82,6 +82,9 @@ using GXE = GemmCfg<TGNX_G32L_T, TGNX_G32L_T, TGNX_G32L_KC, TGNX_G32L_PF, TGNX_G
 #ifndef TGNX_SIN_RECOMPUTE
 #define TGNX_SIN_RECOMPUTE 1  // the backward's Δt-encoding sine recomputed from (w, lu - t, b), not an [E][D] round trip
 #endif
+#ifndef TGNX_EDGES_1ROUND
+#define TGNX_EDGES_1ROUND 1  // edge blocks read the level's edge count from the scan's counters (level_edges)
+#endif
 #ifndef TGNX_PRED_ATT_REC
 #define TGNX_PRED_ATT_REC 1  // per-root neighbour-row records for the attention in tgn_pred_train<ATT>
 #endif
@@ -159,6 +162,52 @@ struct AdamFuse {
   int keep_g = 1;  // fused: also store the gradient (0: TGNX_TGN_NO_GRAD_STORE, nothing reads it; 1.1 MB less per step)
   // n gradient elements (idx < 0: none) of one thread: every load issued before any store (the
   // buffers may alias as far as the compiler knows, so interleaving would serialise the elements)
+  // Two-phase form for the split-K fixup (gemm_fix_tile): pre_n issues the update's loads (the step flags, the step
+  // scalars and the elements' m, v, p) before the tile's partial sums, so they ride in the partials' load round
+  // instead of two dependent rounds after them; apply_n then needs no load.  Same arithmetic as put_n.
+  template <int N>
+  struct Pre {
+    float mm[N], vv[N], pp[N];
+    float s0, s1;
+    bool live;
+  };
+  template <int N>
+  __device__ __forceinline__ Pre<N> pre_n(const int64_t (&idx)[N]) const {
+    Pre<N> r;
+    r.live = false;
+    if (!p) return r;  // (a kernel argument: no load)
+    const int64_t nb = ctl[TGNX_CTL_B], er = ctl[TGNX_CTL_ERR];  // (both loads unconditional: no branch between)
+    r.live = (nb != 0) & (er == 0);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int64_t j = idx[i] >= 0 ? idx[i] : 0;
+      r.mm[i] = m[j];
+      r.vv[i] = v[j];
+      r.pp[i] = p[j];
+    }
+    const float* sc = reinterpret_cast<const float*>(ctl + TGNX_CTL_ADAM_SC);
+    r.s0 = sc[0];
+    r.s1 = sc[1];
+    return r;
+  }
+  template <int N>
+  __device__ __forceinline__ void apply_n(float* g, const int64_t (&idx)[N], const float (&val)[N], Pre<N> r) const {
+    if (!r.live) {  // plain gradient store (no optimizer, or an empty batch)
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if (idx[i] >= 0) g[idx[i]] = val[i];
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      if (idx[i] < 0) continue;
+      adam1(val[i], r.mm[i], r.vv[i], r.pp[i], b1, b2, eps, r.s0, r.s1);
+      if (keep_g) st_wt(g + idx[i], val[i]);
+      st_wt(m + idx[i], r.mm[i]);
+      st_wt(v + idx[i], r.vv[i]);
+      st_wt(p + idx[i], r.pp[i]);
+    }
+  }
   template <int N>
   __device__ __forceinline__ void put_n(float* g, const int64_t (&idx)[N], const float (&val)[N]) const {
     // no update for an empty batch (a resident cursor past the split): the split-K fixup still finishes
@@ -195,6 +244,25 @@ struct AdamFuse {
     put_n<1>(g, ix, vx);
   }
 };
+// the fused-Adam weight-gradient epilogues' two-phase form for the split-K fixup (gemm_fix_tile, TGNX_FIX_PRE):
+// fix_pre(tile) issues the update's loads from the tile coordinates alone; operator()(tile, pre) then computes
+// the values and writes (an epilogue defining nx<T>() and items(t, ix, vx))
+#define TGNX_FIX_PRE_METHODS                                                  \
+  static constexpr int fix_pre_tag = 1;                                       \
+  template <class T>                                                          \
+  __device__ auto fix_pre(const T& t) const {                                 \
+    int64_t ix[nx<T>()];                                                      \
+    float vx[nx<T>()];                                                        \
+    items(t, ix, vx);                                                         \
+    return af.pre_n(ix);                                                      \
+  }                                                                           \
+  template <class T, class PR>                                                \
+  __device__ void operator()(const T& t, const PR& pr) const {                \
+    int64_t ix[nx<T>()];                                                      \
+    float vx[nx<T>()];                                                        \
+    items(t, ix, vx);                                                         \
+    af.apply_n(g, ix, vx, pr);                                                \
+  }
 struct Ctx {
   int64_t N, nev, words;
   int K, D, d, Qm, HC, C, aggr, Kn, drop, gen_neg;
@@ -315,6 +383,15 @@ struct Ctx {
   int64_t ptab_stride;
 };
 constexpr int CNT_R1 = 7, CNT_E1 = 8;
+// the level's sampled-edge count (= ceoff[cnt[rsel]], written beside it by the scan): one load instead of two
+// dependent ones at the head of the edge blocks
+__device__ __forceinline__ int level_edges(const Ctx& c) {
+#if TGNX_EDGES_1ROUND
+  return c.cnt[c.rsel == CNT_R1 ? CNT_E1 : CNT_E];
+#else
+  return c.ceoff[c.cnt[c.rsel]];
+#endif
+}
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 // e / d for 0 <= e < 2^22, 0 < d (inv = 1.0f / d): float estimate, corrected to the exact quotient
@@ -2395,7 +2472,7 @@ __device__ void edge_sort_body(const Ctx& c, int* cntr, int cap) {
   __shared__ int wsum[256];
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int E = c.ceoff[c.cnt[c.rsel]], M = c.cnt[CNT_M];
+  const int E = level_edges(c), M = c.cnt[CNT_M];
   const int t = threadIdx.x;
   if (M + 1 > cap) {  // (the host enables the sort for Mtr + 1 <= cap only)
     if (t == 0) c.ctl[TGNX_CTL_ERR] |= ERR_SORT_CAP;
@@ -2460,6 +2537,13 @@ __global__ void __launch_bounds__(1024) tgn_plan_table_kernel(Ctx c, char* tab, 
   if (B <= 0) return;
   plan_part<8>(c, role < P ? 0 : 1, role % P, P, B, start, psm_, sh, NoCheckpoint{}, plan_slot(tab, stride, c.Bplan, b));
 }
+#ifndef TGNX_PRED_ZHOIST
+#define TGNX_PRED_ZHOIST 1  // the forward contraction's embedding slices held in registers across both output rounds
+#endif
+constexpr int ZH_MAX = 4;  // float4 columns per wave it holds (D <= 128 at 8 waves)
+#ifndef TGNX_PRED_DMA_WAIT_BUILTIN
+#define TGNX_PRED_DMA_WAIT_BUILTIN 1
+#endif
 #ifndef TGNX_PRED_DEFER
 #define TGNX_PRED_DEFER 1  // the 1-hop attention's global stores issued after the first barrier (0: inside attn_centre)
 #endif
@@ -2546,7 +2630,14 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
 #if TGNX_ATT_PAIR
     if (c.evj && q.w - q.z <= EB && (c.C & 1) == 0 && c.C <= 64) {
       paired = true;
+#if TGNX_PRED_CKPT == 3
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      TGNX_STAMP_AT(0);
+#endif
       const float2 o = attn_root_pair<EB>(c, q.x, q.y, q.z, q.w - q.z, lane, max(jr, 0), &asp);
+#if TGNX_PRED_CKPT == 3
+      TGNX_STAMP_AT(1);
+#endif
       if (asp.chan >= 0) {
         z[r][asp.chan] = o.x;
         z[r][asp.chan + 1] = o.y;
@@ -2633,7 +2724,14 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
         else if (x < 2 * D) vdb[x - D] = v;
         else vfw[x - 2 * D] = v;
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the barrier below waits for LDS only)
+      // (the barrier below waits for LDS only).  The builtin, not inline asm: the compiler then knows the LDS-DMA
+      // has landed, else it keeps it pending past the join with the attention waves and puts a vmcnt(0) before the
+      // next LDS read — which waits on the attention's deferred global stores too
+#if TGNX_PRED_DMA_WAIT_BUILTIN
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait)
+#else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
       staged = true;
     }
 #endif
@@ -2686,6 +2784,11 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
 #endif
   // LDS-only barriers in this kernel (the weights, embedding rows and partial sums are LDS; the attention's
   // alpha stores and the evs rows need not have landed): __syncthreads would wait for vmcnt(0)
+#if TGNX_PRED_DMA_WAIT_BUILTIN
+  // (every wave's loads are consumed here and no store is in flight yet: a free wait that leaves the compiler's
+  // scoreboard empty at the join, so the deferred stores below are not waited for at the next barrier)
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 #if TGNX_PRED_CKPT == 1
@@ -2700,6 +2803,41 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     const float4* z0 = reinterpret_cast<const float4*>(z[0]) + q0;
     const float4* z1 = reinterpret_cast<const float4*>(z[1]) + q0;
     const float4* z2 = reinterpret_cast<const float4*>(z[2]) + q0;
+#if TGNX_PRED_ZHOIST
+    // the three embedding slices (wave-uniform) read once into registers for both output rounds: the LDS
+    // reads were 3 broadcast b128 per 2 weight b128, twice
+    if (NW == 8 && kq <= ZH_MAX) {
+      float4 x0[ZH_MAX], x1[ZH_MAX], x2[ZH_MAX];
+#pragma unroll
+      for (int j = 0; j < ZH_MAX; ++j) {
+        const bool in = j < nq;
+        x0[j] = in ? z0[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        x1[j] = in ? z1[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        x2[j] = in ? z2[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int o = lane + 64 * q;
+        if (o < D) {
+          const float4* ws = reinterpret_cast<const float4*>(Wsrc + o * D) + q0;
+          const float4* wd = reinterpret_cast<const float4*>(Wdst + o * D) + q0;
+          float a = 0.f, b = 0.f, d2 = 0.f;
+#pragma unroll
+          for (int j = 0; j < ZH_MAX; ++j) {
+            if (j < nq) {
+              const float4 u = ws[j], v = wd[j];
+              a += (u.x * x0[j].x + u.y * x0[j].y) + (u.z * x0[j].z + u.w * x0[j].w);
+              b += (v.x * x1[j].x + v.y * x1[j].y) + (v.z * x1[j].z + v.w * x1[j].w);
+              d2 += (v.x * x2[j].x + v.y * x2[j].y) + (v.z * x2[j].z + v.w * x2[j].w);
+            }
+          }
+          part[wv][0][o] = a;
+          part[wv][1][o] = b;
+          part[wv][2][o] = d2;
+        }
+      }
+    } else
+#endif
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int o = lane + 64 * q;
@@ -2948,7 +3086,7 @@ template <bool PAIR>
 __device__ void kv_edge_body(const Ctx& c, int bid) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int E = c.ceoff[c.cnt[c.rsel]];
+  const int E = level_edges(c);
   const int eb = bid * KVE_CH;
   if (eb >= E) return;  // whole workgroup
   const int ne = min(KVE_CH, E - eb);
@@ -3404,7 +3542,7 @@ constexpr int KVR_PW = KVR_CH / 4;    // sorted edges per wave
 __device__ void kv_reduce_body(const Ctx& c, int bid) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int E = c.ceoff[c.cnt[c.rsel]];
+  const int E = level_edges(c);
   const int eb = bid * KVR_CH;
   if (eb >= E) return;  // whole workgroup
   const int ne = min(KVR_CH, E - eb);
@@ -3488,10 +3626,9 @@ struct EpiProjGrad {
   int HC, D;
   AdamFuse af;
   template <class T>
-  __device__ void operator()(const T& t) const {
-    constexpr int NI = (T::tm * T::tn + 255) / 256;
-    int64_t ix[NI];
-    float vx[NI];
+  static constexpr int nx() { return (T::tm * T::tn + 255) / 256; }
+  template <class T, int NI>
+  __device__ void items(const T& t, int64_t (&ix)[NI], float (&vx)[NI]) const {
 #pragma unroll
     for (int it = 0; it < NI; ++it) {
       const int x = threadIdx.x + 256 * it;
@@ -3501,8 +3638,15 @@ struct EpiProjGrad {
       vx[it] = ok ? t(r, cc) : 0.f;
       ix[it] = !ok ? -1 : n < D ? wq + gi * pw + (int64_t)q * D + n : bq + gi * pb + q;
     }
+  }
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    int64_t ix[nx<T>()];
+    float vx[nx<T>()];
+    items(t, ix, vx);
     af.put_n(g, ix, vx);
   }
+  TGNX_FIX_PRE_METHODS
 };
 // plain row-major weight gradient (lin_edge): g[off + m ldc + n]
 struct EpiGradStore {
@@ -3511,18 +3655,25 @@ struct EpiGradStore {
   int ldc;
   AdamFuse af;
   template <class T>
-  __device__ void operator()(const T& t) const {
-    int64_t ix[T::per];
-    float vx[T::per];
+  static constexpr int nx() { return T::per; }
+  template <class T, int NI>
+  __device__ void items(const T& t, int64_t (&ix)[NI], float (&vx)[NI]) const {
 #pragma unroll
-    for (int i = 0; i < T::per; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int r = T::row_of(i), cc = T::col_of(i), m = t.m0 + r, n = t.n0 + cc;
       const bool ok = m < t.M && n < t.N;
       vx[i] = ok ? t(r, cc) : 0.f;
       ix[i] = ok ? off + (int64_t)m * ldc + n : -1;
     }
+  }
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    int64_t ix[nx<T>()];
+    float vx[nx<T>()];
+    items(t, ix, vx);
     af.put_n(g, ix, vx);
   }
+  TGNX_FIX_PRE_METHODS
 };
 // link predictor weight grads as one GEMM over 3 * nloc rows (block-diagonal K):
 // rows r < D: dW_src = Σ (dhp + dhn) zsᵀ ; rows r >= D: dW_dst = Σ dhp zpᵀ + dhn znᵀ
@@ -3558,10 +3709,9 @@ struct EpiLpGrad {
   int D;
   AdamFuse af;
   template <class T>
-  __device__ void operator()(const T& t) const {
-    constexpr int NI = (T::tm * T::tn + 255) / 256;
-    int64_t ix[NI];
-    float vx[NI];
+  static constexpr int nx() { return (T::tm * T::tn + 255) / 256; }
+  template <class T, int NI>
+  __device__ void items(const T& t, int64_t (&ix)[NI], float (&vx)[NI]) const {
 #pragma unroll
     for (int it = 0; it < NI; ++it) {
       const int x = threadIdx.x + 256 * it;
@@ -3570,8 +3720,15 @@ struct EpiLpGrad {
       vx[it] = ok ? t(r, cc) : 0.f;
       ix[it] = ok ? (row < D ? lsw + (int64_t)row * D : ldw + (int64_t)(row - D) * D) + n : -1;
     }
+  }
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    int64_t ix[nx<T>()];
+    float vx[nx<T>()];
+    items(t, ix, vx);
     af.put_n(g, ix, vx);
   }
+  TGNX_FIX_PRE_METHODS
 };
 // Δt-encoding parameter grads from a tile of d(encoding) (dA): per row-tile partials
 //   tgp[row][n] = Σ_r -dA[r][n] S1[r][n],  tgp[row][D + n] = Σ_r -dA[r][n] S0[r][n]
@@ -3781,12 +3938,11 @@ struct EpiGruWGrad {
   int Qm, D;
   AdamFuse af;
   template <class T>
-  __device__ void operator()(const T& t) const {
-    constexpr int NI = (T::tm * T::tn + 255) / 256;
-    int64_t ix[2 * NI];  // the (r, z) bias columns feed both b_ih and b_hh
-    float vx[2 * NI];
+  static constexpr int nx() { return 2 * ((T::tm * T::tn + 255) / 256); }  // the (r, z) bias columns feed both b_ih and b_hh
+  template <class T, int N2>
+  __device__ void items(const T& t, int64_t (&ix)[N2], float (&vx)[N2]) const {
 #pragma unroll
-    for (int it = 0; it < NI; ++it) {
+    for (int it = 0; it < N2 / 2; ++it) {
       const int x = threadIdx.x + 256 * it;
       const int r = x / T::tn, cc = x % T::tn, row = t.m0 + r, n = t.n0 + cc;
       const bool ok = x < T::tm * T::tn && row < t.M && n < t.N;
@@ -3809,8 +3965,15 @@ struct EpiGruWGrad {
       ix[2 * it + 1] = b;
       vx[2 * it] = vx[2 * it + 1] = v;
     }
+  }
+  template <class T>
+  __device__ void operator()(const T& t) const {
+    int64_t ix[nx<T>()];
+    float vx[nx<T>()];
+    items(t, ix, vx);
     af.put_n(g, ix, vx);
   }
+  TGNX_FIX_PRE_METHODS
 };
 // encoding columns of W_ih as the B operand of dX_enc = dG W_cat[:, enc]: element (n, r = 4j+g)
 struct LoadGruWencT {

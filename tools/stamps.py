@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--layers", type=int, default=1)
     ap.add_argument("--raw", default="", help="save the raw records (.npy)")
     ap.add_argument("--bins", action="store_true", help="per block-range start / duration table")
+    ap.add_argument("--top", type=int, default=0, help="per launch, the N workgroups ending last")
     args = ap.parse_args()
     args.bins_at = {}
     from tgnx import _lib
@@ -172,6 +173,19 @@ def main():
                     st_, du = np.array(ws, dtype=np.float64).T * 0.01
                     parts.append(f"[{a}-{b - 1}] {st_.mean():.1f}/{du.mean():.1f}/{du.max():.1f}")
             print(f"  {i:2d} {NAMES.get(ls[0][0][2], ls[0][0][2]):14s} " + "  ".join(parts))
+    if args.top:
+        print(f"per launch: the {args.top} workgroups ending last (block: mean start / mean duration / mean end, us)")
+        for i in range(nl):
+            ls = [s[i] for s in steps]
+            acc = defaultdict(list)
+            for l in ls:
+                t0 = min(x[0] for x in l)
+                for w in l:
+                    acc[w[3]].append(((w[0] - t0) * 0.01, (w[1] - w[0]) * 0.01))
+            m = sorted(((b, np.mean([a for a, _ in v]), np.mean([d for _, d in v])) for b, v in acc.items()),
+                       key=lambda r: -(r[1] + r[2]))[:args.top]
+            print(f"  {i:2d} {NAMES.get(ls[0][0][2], ls[0][0][2]):14s} " +
+                  "  ".join(f"{b}: {s_:.1f}/{d:.1f}/{s_ + d:.1f}" for b, s_, d in m))
     for i in range(nl):  # intra-kernel checkpoints (TGNX_STAMP_AT), busy workgroups
         ls = [s[i] for s in steps]
         mids = [(w[5] & 0xFFFF, w[5] >> 16, w[1] - w[0]) for l in ls for w in l if w[5]]
