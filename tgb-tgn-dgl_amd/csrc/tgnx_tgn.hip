@@ -2537,6 +2537,9 @@ __global__ void __launch_bounds__(1024) tgn_plan_table_kernel(Ctx c, char* tab, 
   if (B <= 0) return;
   plan_part<8>(c, role < P ? 0 : 1, role % P, P, B, start, psm_, sh, NoCheckpoint{}, plan_slot(tab, stride, c.Bplan, b));
 }
+#ifndef TGNX_PRED_PSUM1
+#define TGNX_PRED_PSUM1 0  // the forward's 8 partial sums reduced once per workgroup, not by every wave
+#endif
 #ifndef TGNX_PRED_ZHOIST
 #define TGNX_PRED_ZHOIST 1  // the forward contraction's embedding slices held in registers across both output rounds
 #endif
@@ -2561,8 +2564,12 @@ constexpr int ZH_MAX = 4;  // float4 columns per wave it holds (D <= 128 at 8 wa
                                // same-box A/B: predictor 14.1 -> 12.6-13.1 us, step -1 %)
 #endif
 #ifndef TGNX_DZC_REP
-#define TGNX_DZC_REP 1  // 1-hop train: copies of dZc the predictor's workgroups spread their atomics over (4: predictor
-                        // -1 us, but the attention backward +6 us reading the copies per edge; profiles/r5/r5_pred_p7_ab.txt)
+#define TGNX_DZC_REP 4  // 1-hop train: copies of dZc the predictor's workgroups spread their atomics over (a wiki batch's hub
+                        // centre is the root of ~90 of its 600 root slots: its row's adds serialise at the memory side;
+                        // the no-atomics diagnostic bounds that at 1.3 us).  The attention backward sums the copies with
+                        // compile-time unrolled loads in the same round (tgn_attn_bwd<EB, REP>).  Same-box A/B
+                        // (profiles/r5/r5_dzc_rep_ab.txt): predictor 12.7-12.9 -> 11.6 us, attention backward +0.5,
+                        // step 0.0926 / 0.0928 -> 0.0922 / 0.0922 ms; 8 copies: attention backward +1.3, step 0.0932
 #endif
 #ifndef TGNX_ATT_PAIR
 #define TGNX_ATT_PAIR 1  // the predictor's attention in the paired-channel lane layout (attn_root_pair)
@@ -2898,14 +2905,32 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
       return s;
     };
     float zp = 0.f, zn = 0.f;
+#if TGNX_PRED_PSUM1
+    // the 8 waves' partials summed once (thread per (root, output), into part[0]) instead of by every wave
+    if (NW == 8) {
+      for (int x = tid; x < 3 * D; x += 64 * NW) {
+        const int r = x >= 2 * D ? 2 : x >= D ? 1 : 0, o = x - r * D;
+        part[0][r][o] = psum(r, o) + (r == 0 ? vsb[o] : vdb[o]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+#endif
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int o = lane + 64 * q;
       hp[q] = hn[q] = 0.f;
       if (o < D) {
+#if TGNX_PRED_PSUM1
+        const bool one = NW == 8;
+        const float s = one ? part[0][0][o] : psum(0, o) + vsb[o];
+        const float dp = one ? part[0][1][o] : psum(1, o) + vdb[o];
+        const float dn = one ? part[0][2][o] : psum(2, o) + vdb[o];
+#else
         const float s = psum(0, o) + vsb[o];
         const float dp = psum(1, o) + vdb[o];
         const float dn = psum(2, o) + vdb[o];
+#endif
         hp[q] = fmaxf(s + dp, 0.f);
         hn[q] = fmaxf(s + dn, 0.f);
         zp += vfw[o] * hp[q];
@@ -3004,7 +3029,11 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     __builtin_amdgcn_s_barrier();
     for (int x = tid; x < 3 * D; x += 64 * NW) {
       const int r = x >= 2 * D ? 2 : x >= D ? 1 : 0, oo = x - r * D;
+#ifdef TGNX_PRED_DIAG_NOATOM  // diagnostic only (wrong sums): plain stores instead of the dZc atomics
+      dz[(int64_t)cr[r] * D + oo] = dzl[r][oo];
+#else
       atomicAdd(&dz[(int64_t)cr[r] * D + oo], dzl[r][oo]);
+#endif
     }
 #else
     if (kg == 0 && oko) {
@@ -3082,7 +3111,7 @@ constexpr int KVE_CH = TGNX_KVE_CH, KVE_PW = KVE_CH / 4;
 constexpr int KVE_B = TGNX_KVE_B < KVE_PW ? TGNX_KVE_B : KVE_PW;  // edges per load batch of a wave
 // PAIR: the paired-channel lane layout (attn_root_pair): lane (h, j) carries channels 2j, 2j + 1 of head h, so one
 // 32-lane reduction per edge serves both heads and the rows move as float2 (C even, C <= 64)
-template <bool PAIR>
+template <bool PAIR, int REP = 1>
 __device__ void kv_edge_body(const Ctx& c, int bid) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
@@ -3186,7 +3215,9 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
       const float* Ee = c.Ep + (int64_t)er[u] * HC;
       g0[u] = G[oA];
       g1[u] = G[oB];
-      for (int rp = 1; rp < c.dzrep; ++rp) {  // (the predictor's dZc copies, in copy order)
+#pragma unroll
+      for (int rp = 1; rp < REP; ++rp) {  // (the predictor's dZc copies, in copy order; REP = c.dzrep, compile-time
+                                          // so that every copy's load is in the batch's one round)
         g0[u] += G[rp * c.dzstride + oA];
         g1[u] += G[rp * c.dzstride + oB];
       }
@@ -3290,7 +3321,7 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
 // serialised at the L2 (attn_bwd 36 us, 15 us without them).
 // nwalk (parity-set steps with a plan table, TGNX_WALK_AT 1): the last block walks the NEXT batch's node sets
 // into the other parity's set (cw; the plans come from the table), instead of a workgroup of the dW_cell launch
-template <int EB>
+template <int EB, int REP = 1>
 __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int nwalk, Ctx cw) {
   TGNX_STAMP(6);
   if ((int)blockIdx.x >= (int)gridDim.x - nwalk) {
@@ -3303,8 +3334,8 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
     return;
   }
   if ((int)blockIdx.x >= ncb) {
-    if (TGNX_BWD_PAIR && (c.C & 1) == 0 && c.C <= 64) kv_edge_body<true>(c, (int)blockIdx.x - ncb);
-    else kv_edge_body<false>(c, (int)blockIdx.x - ncb);
+    if (TGNX_BWD_PAIR && (c.C & 1) == 0 && c.C <= 64) kv_edge_body<true, REP>(c, (int)blockIdx.x - ncb);
+    else kv_edge_body<false, REP>(c, (int)blockIdx.x - ncb);
     return;
   }
   const bool wkv = nkv == 0;  // per-edge dk / dv / dE written here (else by the edge blocks)
@@ -3337,7 +3368,8 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
   float* dPi = c.dP + (int64_t)i * 4 * HC;
   const float q0 = Pi[l0], q1 = Pi[C + l0];
   float g0 = c.dZc[(int64_t)x * HC + l0], g1 = c.dZc[(int64_t)x * HC + C + l0];
-  for (int rp = 1; rp < c.dzrep; ++rp) {  // (the predictor's dZc copies, in copy order)
+#pragma unroll
+  for (int rp = 1; rp < REP; ++rp) {  // (the predictor's dZc copies, in copy order)
     g0 += c.dZc[rp * c.dzstride + (int64_t)x * HC + l0];
     g1 += c.dZc[rp * c.dzstride + (int64_t)x * HC + C + l0];
   }
@@ -3363,7 +3395,8 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
     const int ch = hh * C + 2 * (act ? jj : hc - 1);
     const float onp = f01(act);
     float2 g = *reinterpret_cast<const float2*>(c.dZc + (int64_t)x * HC + ch);
-    for (int rp = 1; rp < c.dzrep; ++rp) {  // (the predictor's dZc copies, in copy order)
+#pragma unroll
+    for (int rp = 1; rp < REP; ++rp) {  // (the predictor's dZc copies, in copy order)
       const float2 gr = *reinterpret_cast<const float2*>(c.dZc + rp * c.dzstride + (int64_t)x * HC + ch);
       g.x += gr.x;
       g.y += gr.y;
@@ -5008,6 +5041,12 @@ static Ctx root_view(const Ctx& c) {
 #ifndef TGNX_AGG_NODE_CAP
 #define TGNX_AGG_NODE_CAP 512
 #endif
+// the attention backward for a ring of K and the predictor's dZc copy count (compile-time: the copies' loads batched)
+using AttnBwdFn = void (*)(Ctx, int, int, int, Ctx);
+static AttnBwdFn attn_bwd_fn(int K, int rep) {
+  if (rep == TGNX_DZC_REP && TGNX_DZC_REP > 1) return K <= 10 ? tgn_attn_bwd<10, TGNX_DZC_REP> : tgn_attn_bwd<ATT_EB, TGNX_DZC_REP>;
+  return K <= 10 ? tgn_attn_bwd<10, 1> : tgn_attn_bwd<ATT_EB, 1>;
+}
 // integer knob from the environment (host, read once by the caller's static), else the build default
 static inline int env_int(const char* name, int def) {
   const char* v = getenv(name);
@@ -5413,7 +5452,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     // conv2 backward (‖ predictor reductions) -> dP2, dE2; then dh1 = dP2 [Wq2; Wk2; Wv2; Wsk2] ‖ dW_proj2,
     // dW_edge2 (deferred) ‖ conv2's lin_edge -> Δt-encoding partials; then conv backward from dh1
     const int ncb1 = gridn(kr.R1tr, 4, 1 << 20), nkv1 = cr.kvf ? gridn(kr.E1tr, KVE_CH, 1 << 20) : 0;
-    launch_k(c.K <= 10 ? tgn_attn_bwd<10> : tgn_attn_bwd<ATT_EB>, dim3(ncb1 + nkv1 + gridn(3 * D + 2, 4)), dim3(256), 0u,
+    launch_k(attn_bwd_fn(c.K, cr.dzrep), dim3(ncb1 + nkv1 + gridn(3 * D + 2, 4)), dim3(256), 0u,
              s, cr, ncb1, nkv1, 0, cr);
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
     // conv2's (dk, dv) sums (unless its attention backward summed them) ‖ its dE2-only GEMMs (as in the 1-hop
@@ -5439,12 +5478,12 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     }
     TGNX_LAUNCH_CHECK("tgn_dh1");
     const int ncb = gridn(kr.Rtr, 4, 1 << 20), nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
-    launch_k(c.K <= 10 ? tgn_attn_bwd<10> : tgn_attn_bwd<ATT_EB>, dim3(ncb + nkv + nwalk), dim3(256), walk_lds, s, c,
+    launch_k(attn_bwd_fn(c.K, c.dzrep), dim3(ncb + nkv + nwalk), dim3(256), walk_lds, s, c,
              ncb, nkv, nwalk, nwalk ? cn : c);
   } else {
     const int ncb = gridn(kr.Rtr, 4, 1 << 20);
     const int nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
-    launch_k(c.K <= 10 ? tgn_attn_bwd<10> : tgn_attn_bwd<ATT_EB>, dim3(ncb + nkv + gridn(3 * D + 2, 4) + nwalk),
+    launch_k(attn_bwd_fn(c.K, c.dzrep), dim3(ncb + nkv + gridn(3 * D + 2, 4) + nwalk),
              dim3(256), walk_lds, s, c, ncb, nkv, nwalk, nwalk ? cn : c);
   }
   probe_end(TGNX_K_SEG_BWD, s);
