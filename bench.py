@@ -545,7 +545,7 @@ def run_tgn(args, world, rank, dev):
                        "§8(d) B_ev(train) x events per GPU (bench.tgn_step_bytes)",
         "timing": "avg_launch_us: the kernel's own begin / end timestamps (hipExtLaunchKernelGGL start / stop "
                   "events bound to the dispatch, on its launch stream: what rocprofv3 --kernel-trace reports), "
-                  "eager launches of the same step; rocprofv3 summary of the same command: profiles/r4/ (r4_kernel_stats.csv)",
+                  "eager launches of the same step; rocprofv3 summary of the same command: profiles/r5/ (r5_kernel_stats.csv)",
         "units_window": "probe windows count batches k+1..k+n (pipelined prefetch), stationary stream",
     }
     if flops_gru_edge:
