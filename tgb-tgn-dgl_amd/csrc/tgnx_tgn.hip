@@ -82,6 +82,9 @@ using GXE = GemmCfg<TGNX_G32L_T, TGNX_G32L_T, TGNX_G32L_KC, TGNX_G32L_PF, TGNX_G
 #ifndef TGNX_SIN_RECOMPUTE
 #define TGNX_SIN_RECOMPUTE 1  // the backward's Δt-encoding sine recomputed from (w, lu - t, b), not an [E][D] round trip
 #endif
+#ifndef TGNX_KVE_EARLY
+#define TGNX_KVE_EARLY 1  // the attention backward's edge blocks load their sorted records in the edge count's round
+#endif
 #ifndef TGNX_EDGES_1ROUND
 #define TGNX_EDGES_1ROUND 1  // edge blocks read the level's edge count from the scan's counters (level_edges)
 #endif
@@ -315,6 +318,8 @@ struct Ctx {
   // atomics'); 2 hops: 1
   int dzrep;
   int64_t dzstride;
+  int dzrep1;           // 2 hops: the same for the root level's dZr (the predictor's rows there; root_view)
+  int64_t dzstride1;
   // resident batch cursor folded into tgn_mark (tgnx_tgn_train_step_resident): mark derives the batch
   // descriptor from the step counters, the step's last launch advances them
   int adv = 0;
@@ -329,6 +334,7 @@ struct Ctx {
   int kvf = 0;
   int *kj, *kx, *ke;  // kvf: the sampled edges sorted by neighbour row (tgn_pred_train's sort block): row, centre, edge
   int kvs = 0;        // kvf: those arrays are this step's (else the edge blocks read the edges in sampling order)
+  int ktr = 1;        // rows of kj / kx / ke (the train edge capacity)
   float *encE, *sinE;  // per sampled edge: cos / sin of the Δt encoding argument [E][D]
   float *s0m, *s1m;    // per GRU row: (mean over its messages of) sin(arg), sin(arg) Δt  [M][D]
   float *pA, *pB, *pC, *pD;  // split-K partials of the deferred weight-gradient GEMMs
@@ -1853,8 +1859,9 @@ __global__ void __launch_bounds__(256) TGNX_AGG_ATTR tgn_agg_emit(Ctx c, int mod
       const int R1 = c.cnt[CNT_R1];
       for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R * 4 * c.HC; x += (int64_t)nb * blockDim.x)
         c.dP2[x] = 0.f;
-      for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R1 * c.HC; x += (int64_t)nb * blockDim.x)
-        c.dZr[x] = 0.f;
+      for (int rp = 0; rp < c.dzrep1; ++rp)
+        for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R1 * c.HC; x += (int64_t)nb * blockDim.x)
+          c.dZr[rp * c.dzstride1 + x] = 0.f;
     } else {
       for (int rp = 0; rp < c.dzrep; ++rp)
         for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R * c.HC; x += (int64_t)nb * blockDim.x)
@@ -2571,6 +2578,10 @@ constexpr int ZH_MAX = 4;  // float4 columns per wave it holds (D <= 128 at 8 wa
                         // (profiles/r5/r5_dzc_rep_ab.txt): predictor 12.7-12.9 -> 11.6 us, attention backward +0.5,
                         // step 0.0926 / 0.0928 -> 0.0922 / 0.0922 ms; 8 copies: attention backward +1.3, step 0.0932
 #endif
+#ifndef TGNX_DZR_REP
+#define TGNX_DZR_REP 1  // 2 hops: copies of the root level's dZr for the predictor's adds (1 or TGNX_DZC_REP; 4: comment-shaped
+                        // 2-hop step 0.2770 / 0.2762 -> 0.2942 / 0.2899 ms, profiles/r5/r5_dzr_rep_ab.txt)
+#endif
 #ifndef TGNX_ATT_PAIR
 #define TGNX_ATT_PAIR 1  // the predictor's attention in the paired-channel lane layout (attn_root_pair)
 #endif
@@ -2617,9 +2628,15 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
   const int B = (int)c.ctl[TGNX_CTL_B];
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
   const int64_t err = c.ctl[TGNX_CTL_ERR];
-  const int i = lo + blockIdx.x;
-  const bool live = !(B == 0 || i >= hi || err != 0);
   constexpr int NST = ATT ? (NW - 3) * 64 : 3 * 64;  // staging threads: ATT waves 0, 4 .. NW-1; else waves 1-3
+  // a workgroup takes events slot, slot + G, ... (G = the event workgroups, at most one per CU: the weights are
+  // staged once per workgroup, and its LDS leaves room for one workgroup per CU, so a batch of more events than
+  // CUs ran in dispatch rounds of a whole workgroup each; pred_groups)
+  const int G = (int)gridDim.x - nmk - nsrt - npl;
+  for (int slot = blockIdx.x;; slot += G) {
+  const bool first = slot == (int)blockIdx.x;
+  const int i = lo + slot;
+  const bool live = !(B == 0 || i >= hi || err != 0);
   // (out_ev: the batch's first event, loaded with the first round — a load after the evs-row stores would wait
   // for all of them, vmcnt retiring in order)
   const int64_t bstart = c.out_ev ? c.ctl[TGNX_CTL_BATCH_START] : 0;
@@ -2630,8 +2647,8 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
   asp.x = -1;
   if (ATT && wv >= 1 && wv <= 3) {
     const int r = wv - 1;
-    const int4 q = c.evq[3 * blockIdx.x + r];  // {centre row, P row, edge range}; grid = max_batch: in bounds
-    const int jr = c.evj ? c.evj[(3 * blockIdx.x + r) * 16 + (lane & 15)] : -1;  // the edges' neighbour rows
+    const int4 q = c.evq[3 * slot + r];  // {centre row, P row, edge range}; slot < max_batch: in bounds
+    const int jr = c.evj ? c.evj[(3 * slot + r) * 16 + (lane & 15)] : -1;  // the edges' neighbour rows
     if (!live) return;
     bool paired = false;
 #if TGNX_ATT_PAIR
@@ -2684,14 +2701,14 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
   } else if (!ATT && wv == 0) {
     int cr[3];  // the roots' centre rows (tgn_agg_emit) by rank-local event: issued with the ctl loads
 #pragma unroll
-    for (int r = 0; r < 3; ++r) cr[r] = c.evr[3 * blockIdx.x + r];  // grid = max_batch: in bounds
+    for (int r = 0; r < 3; ++r) cr[r] = c.evr[3 * slot + r];  // slot < max_batch: in bounds
     if (!live) return;
     for (int x = lane; x < 3 * D; x += 64) z[x / D][x % D] = c.Zc[(int64_t)cr[x / D] * D + x % D];
     if (lane < 3) scr[lane] = cr[lane];
   } else {
     const int sw = ATT ? (wv == 0 ? 0 : wv - 3) : wv - 1;  // staging wave index
     const int st = sw * 64 + lane;                        // staging thread index in [0, NST)
-    if (blockIdx.x == 0 && st == 0) {
+    if (blockIdx.x == 0 && st == 0 && first) {
       c.cnt[CNT_LIST] = 3 * (hi - lo);
       {  // this step's Adam scalars for the gradient writers (fused) or tgn_adam (the separate pass after the step)
         const int64_t t = c.ctl[TGNX_CTL_ADAM_T] + (c.adv ? 1 : 0);
@@ -2702,6 +2719,7 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     }
     if (!live) return;
     // D is even, so D * D % 4 == 0; the flat buffer's blocks are 16-B aligned (tgnx_tgn_param_layout)
+    if (first) {  // (later events of the workgroup: the weights are in LDS already)
     const int n4 = D * D / 4;
     const float invD = 1.0f / (float)D;
     const float4* S4 = reinterpret_cast<const float4*>(c.params + c.L.lsw);
@@ -2785,6 +2803,7 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
         }
       }
     }
+    }  // first
   }
 #if TGNX_PRED_CKPT == 1
   TGNX_STAMP_AT(0);
@@ -3015,7 +3034,7 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
 #if TGNX_PRED_CKPT == 2
     TGNX_STAMP_AT(0);
 #endif
-    float* dz = c.dZc + (int64_t)(blockIdx.x % c.dzrep) * c.dzstride;
+    float* dz = c.dZc + (int64_t)(slot % c.dzrep) * c.dzstride;
 #if TGNX_PRED_WIDE_ATOM
     // the three rows gathered in LDS first, then added with whole-row wave instructions (contiguous lanes: 6 per
     // workgroup instead of 3 per wave on 13-lane segments — every one of them queues on a hub centre's row)
@@ -3052,6 +3071,12 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     TGNX_STAMP_AT(1);
 #endif
   }
+  if (ATT || lo + slot + G >= hi) break;  // (ATT: one event per workgroup — the loop's live ranges spilled the
+                                           // 8-wave kernel: 168 -> 256 VGPRs + 47 spilled, predictor 12 -> 20 us)
+  // (the next event's rows overwrite z, scr and the partial sums: every wave past this event's last LDS read)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  }  // slot
 }
 
 // predictor bias / output-layer / loss reductions over this rank's events (wave per output)
@@ -3117,13 +3142,46 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
   const int E = level_edges(c);
   const int eb = bid * KVE_CH;
+  const int t = threadIdx.x;
+  const bool gs = c.kvs;  // workgroup-uniform
+#if TGNX_KVE_EARLY
+  // globally sorted edges: the chunk's records (and the keys just outside it) loaded in the edge count's round,
+  // clamped to the sorted arrays' rows (ktr) and masked by the count after
+  int kj0 = 0, kx0 = 0, ke0 = 0, kb = -1;
+  if (gs) {
+    if (t < KVE_CH) {
+      const int ec = min(eb + t, c.ktr - 1);
+      kj0 = c.kj[ec];
+      kx0 = c.kx[ec];
+      ke0 = c.ke[ec];
+    } else if (t == KVE_CH) {
+      kb = eb > 0 ? c.kj[min(eb - 1, c.ktr - 1)] : -1;
+    } else if (t == KVE_CH + 1) {
+      kb = c.kj[min(eb + KVE_CH, c.ktr - 1)];
+    }
+  }
+#endif
   if (eb >= E) return;  // whole workgroup
   const int ne = min(KVE_CH, E - eb);
   __shared__ int sj[KVE_CH], sx[KVE_CH], se[KVE_CH], sorder[KVE_CH], sb[2];
-  const int t = threadIdx.x;
-  const bool gs = c.kvs;  // workgroup-uniform
   // globally sorted: a run whose row has no edge in the neighbouring chunks is the row's whole sum (a plain
   // store); the chunk's first / last runs may continue there (the keys just outside the chunk tell)
+#if TGNX_KVE_EARLY
+  if (gs) {
+    if (t == KVE_CH) sb[0] = kb;
+    if (t == KVE_CH + 1) sb[1] = eb + ne < E ? kb : -1;  // (ne < KVE_CH: eb + ne = E)
+    if (t < KVE_CH) {
+      sj[t] = t < ne ? kj0 : INT_MAX;
+      sx[t] = kx0;
+      se[t] = ke0;
+    }
+  } else if (t < KVE_CH) {
+    const int ec = min(eb + t, E - 1);
+    sj[t] = t < ne ? c.e_j[ec] : INT_MAX;
+    sx[t] = c.e_c[ec];
+    se[t] = ec;
+  }
+#else
   if (gs && t == KVE_CH) sb[0] = eb > 0 ? c.kj[eb - 1] : -1;
   if (gs && t == KVE_CH + 1) sb[1] = eb + ne < E ? c.kj[eb + ne] : -1;
   if (t < KVE_CH) {  // the edge's neighbour (sort key), centre and id, one round
@@ -3133,6 +3191,7 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
     sx[t] = x;
     se[t] = eo;
   }
+#endif
   __syncthreads();
   if (t < ne) {  // stable rank of (neighbour, edge)
     const int key = sj[t];
@@ -4734,7 +4793,7 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.Ep2 = carve(off, E1 * HC * 4);
   W.alpha1 = carve(off, (size_t)k.E1tr * TH * 4);
   W.Zr = carve(off, R1 * HC * 4);
-  W.dZr = carve(off, (two ? (size_t)k.R1tr : 0) * HC * 4);
+  W.dZr = carve(off, (two ? (size_t)k.R1tr : 0) * HC * 4 * TGNX_DZR_REP);
   W.dP2 = carve(off, (two ? (size_t)k.Rtr : 0) * 4 * HC * 4);
   W.dE2 = carve(off, (size_t)k.E1tr * HC * 4);
   W.pE = carve(off, two ? gemm_partial_floats(shp_dWp2(k, nullptr)) * 4 : 0);
@@ -4891,6 +4950,8 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.dZc = reinterpret_cast<float*>(ws + W.dZc);
   c.dzrep = k.layers == 2 ? 1 : TGNX_DZC_REP;
   c.dzstride = (int64_t)k.Rtr * k.HC;
+  c.dzrep1 = k.layers == 2 ? TGNX_DZR_REP : 1;
+  c.dzstride1 = (int64_t)k.R1tr * k.HC;
   c.dP = reinterpret_cast<float*>(ws + W.dP);
   c.dE = reinterpret_cast<float*>(ws + W.dE);
   c.dKV = reinterpret_cast<float*>(ws + W.dKV);
@@ -4924,6 +4985,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.Rcap = k.Rcap;
   c.Mcap = k.Mcap;
   c.Ecap = k.Ecap;
+  c.ktr = std::max<int64_t>(1, k.Etr);
   c.Ucap = k.Ucap;
   c.tgp_rows = W.tgp_rows;
   c.L = make_lay(c.D, c.d, k.layers, k.cell);
@@ -5018,6 +5080,8 @@ static Ctx root_view(const Ctx& c) {
   r.alpha = c.alpha1;
   r.Zc = c.Zr;
   r.dZc = c.dZr;
+  r.dzrep = c.dzrep1;
+  r.dzstride = c.dzstride1;
   r.dP = c.dP2;
   r.dE = c.dE2;
   r.e_c = c.e1_c;
@@ -5044,6 +5108,7 @@ static Ctx root_view(const Ctx& c) {
 // the attention backward for a ring of K and the predictor's dZc copy count (compile-time: the copies' loads batched)
 using AttnBwdFn = void (*)(Ctx, int, int, int, Ctx);
 static AttnBwdFn attn_bwd_fn(int K, int rep) {
+  static_assert(TGNX_DZR_REP == 1 || TGNX_DZR_REP == TGNX_DZC_REP, "dZr copies: 1 or the dZc copy count (instantiated)");
   if (rep == TGNX_DZC_REP && TGNX_DZC_REP > 1) return K <= 10 ? tgn_attn_bwd<10, TGNX_DZC_REP> : tgn_attn_bwd<ATT_EB, TGNX_DZC_REP>;
   return K <= 10 ? tgn_attn_bwd<10, 1> : tgn_attn_bwd<ATT_EB, 1>;
 }
@@ -5063,6 +5128,19 @@ static inline int gridn(int64_t n, int per, int cap = 4096) {
   return (int)(g < cap ? g : cap);
 }
 
+// event workgroups of the predictor launch: one per event up to the CU count, else the batch dealt evenly to at most
+// that many (tgn_pred_train loops; its LDS holds one workgroup per CU)
+static int pred_groups(int B) {
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return std::max(1, env_int("TGNX_PRED_GROUPS", n));
+  }();
+  if (B <= ncu) return std::max(B, 1);
+  const int per = (B + ncu - 1) / ncu;
+  return (B + per - 1) / per;
+}
 // the GRU of a node list (eval update / flush): messages -> GRUCell (X, Z0 rows 0..n)
 template <int CELL>
 static void gru_list_c(const Ctx& c, const int64_t* list, const int* list_cnt, int n_host, int64_t base, int mcap,
@@ -5435,7 +5513,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     launch_k(c.K <= 10 ? tgn_pred_train<true, 10> : tgn_pred_train<true, ATT_EB>, dim3(kr.B + npl + nsrt + nmk),
              dim3(64 * pred_waves<true>()), (uint32_t)psm, s, cr, nmk, nsrt, po, npl);
   else
-    launch_k(tgn_pred_train<false>, dim3(kr.B + npl + nsrt + nmk), dim3(64 * pred_waves<false>()), (uint32_t)psm, s, cr,
+    launch_k(tgn_pred_train<false>, dim3(pred_groups(kr.B) + npl + nsrt + nmk), dim3(64 * pred_waves<false>()), (uint32_t)psm, s, cr,
              nmk, nsrt, po, npl);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
