@@ -28,6 +28,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "tgb-tgn-dgl_amd"))
 
+# the step is replayed from HIP graphs; CLR's graph packet capture (its default) left ~0.5 us more between the
+# replayed launches: 0.0917 vs 0.0878 ms per step (profiles/r5/r5_graph_packet_ab.txt). Read when the HIP runtime
+# initialises, so set before torch; an explicit setting wins (tgnx/__init__.py does the same for the drop-in).
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

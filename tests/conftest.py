@@ -3,6 +3,9 @@ import sys
 
 import pytest
 
+# the product's runtime configuration (tgnx/__init__.py, bench.py), set before the first HIP call
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "tgb-tgn-dgl_amd")
 for p in (ROOT, PKG):

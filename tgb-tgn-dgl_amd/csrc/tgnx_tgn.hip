@@ -66,6 +66,9 @@ using GXE = GemmCfg<TGNX_G32L_T, TGNX_G32L_T, TGNX_G32L_KC, TGNX_G32L_PF, TGNX_G
 #define TGNX_PRED_GLDS 1  // predictor weights staged with global_load_lds (LDS-DMA) instead of through registers
                           // (same-box A/B 0.0951 / 0.0951 -> 0.0945 / 0.0946 ms)
 #endif
+#ifndef TGNX_W3_JOBS_FIRST
+#define TGNX_W3_JOBS_FIRST 0  // dW_cell launch job order (0: dX_enc, dW_gru, dW_edge, dEnc; 1: dW_edge, dEnc first; 2: dEnc, dW_edge first)
+#endif
 #ifndef TGNX_DWE_AT7
 #define TGNX_DWE_AT7 0
 #endif
@@ -5625,6 +5628,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     // the GEMM jobs before the snapshot / store blocks (0.0970 vs 0.0986 ms with those first)
     if (walk_w3 && !scan6)
       gemmN_launch(s, j_scan, j_dxe, j_dwg, jobs..., j_snap, j_store);
+    else if constexpr (TGNX_W3_JOBS_FIRST)  // (experiment: the edge jobs — dEnc, the launch's tail — dispatched first)
+      gemmN_launch_w<TGNX_W3_WAVES>(s, jobs..., j_dxe, j_dwg, j_snap, j_store);
     else
       gemmN_launch_w<TGNX_W3_WAVES>(s, j_dxe, j_dwg, jobs..., j_snap, j_store);
     probe_end(TGNX_K_WGRAD3, s);
@@ -5641,6 +5646,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   } else {
     if (TGNX_DWE_AT7) {  // (experiment: dW_edge in the dz0 launch, which fits one dispatch round)
       if ((rc = l7(j_dz0, j_dwp, j_dwlp, j_dwe)) || (rc = l8(j_denc))) return rc;
+    } else if (TGNX_W3_JOBS_FIRST == 2) {  // (dEnc before dW_edge)
+      if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_denc, j_dwe))) return rc;
     } else if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) {
       return rc;
     }
