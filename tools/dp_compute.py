@@ -14,6 +14,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tgb-tgn-dgl_amd")]
 
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")  # as bench.py (before the first HIP call)
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
