@@ -1719,6 +1719,38 @@ __device__ __forceinline__ int root_row(const Ctx& c, int64_t v) {
 // The rest: mode 0 aggregation over the sampled nodes (train) + zeroing of the backward
 // accumulators, mode 1 last_update of the sampled nodes from the buffer (eval scoring), mode 2
 // aggregation over a node list (eval update / flush; list == nullptr: nodes base + m).
+#ifndef TGNX_AGG_ZERO_EDGE
+#define TGNX_AGG_ZERO_EDGE 0  // 1: the backward accumulators zeroed by the sampled-edge blocks after their edges (0: by
+                              // the node blocks before their aggregation; same-box A/B 0.0885 / 0.0884 vs 0.0873 /
+                              // 0.0871 ms, agg_emit 10.9 vs 10.1 us: the edge blocks are not idle, profiles/r5/r5_agg_zero_ab.txt)
+#endif
+#ifndef TGNX_AGG_ZERO_VEC
+#define TGNX_AGG_ZERO_VEC 0  // 16-B stores for that zeroing (0: 4-B)
+#endif
+// zero n floats at p as threads [t, t + nt) of the launch: 16-B stores over the aligned part
+__device__ __forceinline__ void zero_span(float* p, int64_t n, int64_t t, int64_t nt) {
+  int64_t head = 0;
+  if (TGNX_AGG_ZERO_VEC && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    const int64_t n4 = n >> 2;
+    float4* q = reinterpret_cast<float4*>(p);
+    for (int64_t x = t; x < n4; x += nt) q[x] = make_float4(0.f, 0.f, 0.f, 0.f);
+    head = n4 << 2;
+  }
+  for (int64_t x = head + t; x < n; x += nt) p[x] = 0.f;
+}
+// the atomically accumulated backward rows of a train step: dP; 1 hop the dZc copies; 2 hops dP2 (conv2 projections
+// of the outer centres) and the root level's dZr copies (dZc = dh1 is written whole by a GEMM)
+__device__ void zero_bwd_acc(const Ctx& c, int64_t t, int64_t nt) {
+  const int M = c.cnt[CNT_M], R = c.cnt[CNT_R];
+  zero_span(c.dP, (int64_t)M * 4 * c.HC, t, nt);
+  if (c.layers == 2) {
+    const int R1 = c.cnt[CNT_R1];
+    zero_span(c.dP2, (int64_t)R * 4 * c.HC, t, nt);
+    for (int rp = 0; rp < c.dzrep1; ++rp) zero_span(c.dZr + rp * c.dzstride1, (int64_t)R1 * c.HC, t, nt);
+  } else {
+    for (int rp = 0; rp < c.dzrep; ++rp) zero_span(c.dZc + rp * c.dzstride, (int64_t)R * c.HC, t, nt);
+  }
+}
 #ifndef TGNX_AGG_WAVES
 #define TGNX_AGG_WAVES 0  // waves-per-SIMD floor of tgn_agg_emit (0: the compiler's register count)
 #endif
@@ -1847,6 +1879,8 @@ __global__ void __launch_bounds__(256) TGNX_AGG_ATTR tgn_agg_emit(Ctx c, int mod
         for (int q = lane; q < D; q += 64) c.encE[(int64_t)o * D + q] = te_cos(fmaf(tw[q], dt, tb[q]));
       }
     }
+    if (TGNX_AGG_ZERO_EDGE && mode == 0)  // (the node blocks, the launch's tail, keep only their aggregation)
+      zero_bwd_acc(c, ((int64_t)blockIdx.x - nevb - nnode) * blockDim.x + threadIdx.x, (int64_t)nedge * blockDim.x);
     return;
   }
   const int bid = blockIdx.x - nevb, nb = nnode;
@@ -1855,24 +1889,8 @@ __global__ void __launch_bounds__(256) TGNX_AGG_ATTR tgn_agg_emit(Ctx c, int mod
     for (int x = bid * blockDim.x + threadIdx.x; x < M; x += nb * blockDim.x) c.lu[x] = (float)c.lu_buf[c.nid[x]];
     return;
   }
-  if (mode == 0) {  // zero the atomically accumulated backward rows
-    const int M = c.cnt[CNT_M], R = c.cnt[CNT_R];
-    for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)M * 4 * c.HC; x += (int64_t)nb * blockDim.x)
-      c.dP[x] = 0.f;
-    if (c.layers == 2) {  // root level: dZr (predictor rows), dP2 (conv2 projections of the outer centres);
-                          // dZc = dh1 is written whole by a GEMM
-      const int R1 = c.cnt[CNT_R1];
-      for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R * 4 * c.HC; x += (int64_t)nb * blockDim.x)
-        c.dP2[x] = 0.f;
-      for (int rp = 0; rp < c.dzrep1; ++rp)
-        for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R1 * c.HC; x += (int64_t)nb * blockDim.x)
-          c.dZr[rp * c.dzstride1 + x] = 0.f;
-    } else {
-      for (int rp = 0; rp < c.dzrep; ++rp)
-        for (int64_t x = bid * (int64_t)blockDim.x + threadIdx.x; x < (int64_t)R * c.HC; x += (int64_t)nb * blockDim.x)
-          c.dZc[rp * c.dzstride + x] = 0.f;
-    }
-  }
+  if (mode == 0 && (!TGNX_AGG_ZERO_EDGE || nedge == 0))  // zero the atomically accumulated backward rows
+    zero_bwd_acc(c, bid * (int64_t)blockDim.x + threadIdx.x, (int64_t)nb * blockDim.x);
   const int n = mode == 0 ? c.cnt[CNT_M] : (list_cnt ? *list_cnt : n_host);
   if (AG != 0 && c.aggr == 1 && (mode == 0 || list)) {  // MeanAggregator, train / eval update: a workgroup per node (hub
                                              // nodes store many messages); the all-node flush stays wave-per-node
