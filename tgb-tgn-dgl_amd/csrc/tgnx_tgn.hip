@@ -1725,7 +1725,8 @@ __device__ __forceinline__ int root_row(const Ctx& c, int64_t v) {
                               // 0.0871 ms, agg_emit 10.9 vs 10.1 us: the edge blocks are not idle, profiles/r5/r5_agg_zero_ab.txt)
 #endif
 #ifndef TGNX_AGG_ZERO_VEC
-#define TGNX_AGG_ZERO_VEC 0  // 16-B stores for that zeroing (0: 4-B)
+#define TGNX_AGG_ZERO_VEC 0  // 16-B stores for that zeroing (0: 4-B; 1 measured 0.0878 / 0.0876 vs 0.0871 / 0.0872 ms,
+                             // profiles/r5/r5_agg_caps_ab.txt)
 #endif
 // zero n floats at p as threads [t, t + nt) of the launch: 16-B stores over the aligned part
 __device__ __forceinline__ void zero_span(float* p, int64_t n, int64_t t, int64_t nt) {
@@ -5123,7 +5124,7 @@ static Ctx root_view(const Ctx& c) {
 #define TGNX_AGG_SPECIALIZE 1  // last-aggregation steps launch tgn_agg_emit<0> (97 VGPRs instead of 233)
 #endif
 #ifndef TGNX_AGG_EDGE_CAP
-#define TGNX_AGG_EDGE_CAP 1024
+#define TGNX_AGG_EDGE_CAP 1024  // (512: 0.0887 / 0.0886 vs 0.0871 / 0.0872 ms; node cap 128: +-0 — r5_agg_caps_ab.txt)
 #endif
 #ifndef TGNX_AGG_NODE_CAP
 #define TGNX_AGG_NODE_CAP 512
