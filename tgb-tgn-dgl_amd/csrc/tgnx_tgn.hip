@@ -50,7 +50,9 @@ constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touc
                               // A/Bs at wiki: 1024 0.0953 / 0.0952 / 0.0949 / 0.0948 ms, 768 0.0947 / 0.0946 / 0.0943 / 0.0942)
 #endif
 #ifndef TGNX_GRU_WAVES
-#define TGNX_GRU_WAVES 0  // waves-per-SIMD floor of the ring ‖ GRU ‖ lin_edge launch (1 hop)
+#define TGNX_GRU_WAVES 6  // waves-per-SIMD floor of the ring ‖ GRU ‖ lin_edge launch (1 hop; round 5 with the graphs
+                          // replayed without packet capture: 6 0.0867 / 0.0867 vs 0 0.0874 / 0.0872 ms, the launch 13.1-13.4 vs
+                          // 13.8-13.9 us; tgn_agg_emit floors 6 / 8: 0.0879 / 0.0901 — profiles/r5/r5_agg_gru_waves_ab.txt)
 #endif
 #ifndef TGNX_W3_WAVES
 #define TGNX_W3_WAVES 7  // waves-per-SIMD floor of the dW_cell launch (0: the compiler's register count, 84 + 8 -> 5 waves;
