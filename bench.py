@@ -113,6 +113,23 @@ def _metric(dataset: str, model: str) -> str:
             f"temporal edges/sec on {dataset} TGNN, running DGL block-loop path (train step)")
 
 
+def timed_window(nb_epoch, steps, warmup, mode):
+    """The timed window: `steps` consecutive batches from batch `start` of the train epoch (0-based).  mid: centred
+    in the epoch (rings and message stores in their steady state; an early window samples partly empty rings),
+    start: right after the warmup.  Never before the warmup's end: the loop runs `prefill` untimed steps, then
+    `warmup` steps, then times batches start .. start + steps - 1 (wrapping through the epoch boundaries when
+    steps > nb_epoch - start; each boundary's begin_epoch is then inside the timed region)."""
+    start = max(0, (nb_epoch - steps) // 2) if mode == "mid" else 0
+    start = max(start, warmup)
+    prefill = start - warmup
+    boundaries = sum(1 for i in range(start, start + steps) if i > 0 and i % nb_epoch == 0)
+    note = (f"batches {start}..{start + steps - 1} of the {nb_epoch}-batch train epoch sequence (0-based; {prefill} "
+            f"untimed prefill + {warmup} warmup steps before it"
+            + (f"; the window crosses {boundaries} epoch boundar{'y' if boundaries == 1 else 'ies'}, whose "
+               f"begin_epoch (ring / state reset) is timed" if boundaries else "") + ")")
+    return start, prefill, boundaries, note
+
+
 def cpu_baseline(stream, B, budget_s=15.0, max_batches=40):
     """Oracle (faithful per-block CPU restatement, the 'port') on the same stream, bounded sample; the
     train epoch's time is extrapolated from it (stated in the sample)."""
@@ -154,8 +171,9 @@ def cpu_baseline(stream, B, budget_s=15.0, max_batches=40):
                       f"threads={cores}; the train epoch ({stream.train_end} events) extrapolated at this rate"}
 
 
-def run_tgnn(args, world, rank, dev):
-    """The running reference path (model_utils.TGNN, DGL EdgeGATConv block loop)."""
+def run_tgnn(args, world, rank, dev, probe=True):
+    """The running reference path (model_utils.TGNN, DGL EdgeGATConv block loop).  probe=False: the timed
+    window only (the B = 2,000 config-#1 line)."""
     _log(f"tgnn: {args.dataset} B={args.batch * world}")
 
     from tgnx import _lib
@@ -202,7 +220,9 @@ def run_tgnn(args, world, rank, dev):
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    start, prefill, boundaries, window_note = timed_window(nb_epoch, args.steps, args.warmup, args.window)
+    _log(f"tgnn: B={Bg}: timed window {window_note}")
+    for _ in range(prefill + args.warmup):
         step()
     barrier()
     e0, s0 = eng.units()
@@ -220,15 +240,22 @@ def run_tgnn(args, world, rank, dev):
     loss = eng.loss_sum()
     assert math.isfinite(loss), "non-finite loss"
 
-    # live kernel timing (HIP events on the launch stream) for the roofline, same workload
+    # live kernel timing (HIP events on the launch stream) for the roofline, over the TIMED window: before each
+    # kernel's probe the epoch is rewound (begin_epoch) and replayed to batch `start`, then the probe's eager steps
+    # run the same batches start .. start + steps - 1 as the timed region
     bytes_edge = 20 + 4 * d + 4 * D + 4
     bytes_root = 4 * D + 4
     probes = {}
-    for name, kid in (("tgnn_edge_fwd", 1), ("tgnn_edge_bwd", 2), ("tgnn_seg_fwd", 6), ("tgnn_seg_bwd", 8),
-                      ("tgnn_pred_train", 4), ("tgnn_assemble", 3), ("tgnn_meta_collapse", 9), ("tgnn_adam", 7)):
+    kernels = (("tgnn_edge_fwd", 1), ("tgnn_edge_bwd", 2), ("tgnn_seg_fwd", 6), ("tgnn_seg_bwd", 8),
+               ("tgnn_pred_train", 4), ("tgnn_assemble", 3), ("tgnn_meta_collapse", 9), ("tgnn_adam", 7))
+    for name, kid in (kernels if probe else ()):
+        counter["i"] = 0
+        for _ in range(start):
+            step()
+        barrier()
         _lib.call("tgnx_probe_enable", kid)
         pe0, ps0 = eng.units()
-        for _ in range(args.probe_steps):
+        for _ in range(args.steps):
             step(eager=True)          # probes record events around eager launches
         barrier()
         ms, n = ctypes.c_double(), ctypes.c_int64()
@@ -245,6 +272,13 @@ def run_tgnn(args, world, rank, dev):
         algo = edges * bytes_edge if name.startswith("tgnn_edge") else roots * bytes_root
         probes[name] = dict(avg_us=avg_ms * 1e3, launches=launches, edges=edges, roots=roots, bytes=algo,
                             gbs=algo / (avg_ms * 1e-3) / 1e9)
+    blocks_mean = float(np.mean([blk[i:i + Bg].max() + 1 for i in range(0, stream.train_end, Bg)]))
+    if not probes:
+        return {"value": round(args.steps * Bg / elapsed, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                "steps": args.steps, "timed_window": window_note, "loss_sum": round(loss, 4),
+                "edges_per_step": round((e1 - e0) / args.steps / world, 1),
+                "segments_per_step": round((s1 - s0) / args.steps / world, 1),
+                "blocks_per_batch_mean": round(blocks_mean, 1)}
     # roofline kernel: the slowest of the per-edge / per-segment kernels (the gather path of §8(d))
     dom = max((k for k in probes if k.startswith(("tgnn_edge", "tgnn_seg"))), key=lambda k: probes[k]["avg_us"])
     pd = probes[dom]
@@ -281,8 +315,9 @@ def run_tgnn(args, world, rank, dev):
                        "global_batch": Bg, "parallelism": f"dp{world}",
                        "launch": "hip-graph replay per step" if use_graph else "eager",
                        "edges_per_step": round((e1 - e0) / args.steps / world, 1),
-                       "blocks_per_batch_mean": float(np.mean([blk[i:i + Bg].max() + 1
-                                                               for i in range(0, stream.train_end, Bg)]))},
+                       "timed_batches": [start, start + args.steps - 1], "timed_window": window_note,
+                       "probe_window": "the timed batches (each probe rewinds the epoch and replays to its start)",
+                       "blocks_per_batch_mean": round(blocks_mean, 1)},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(pd["gbs"], 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(pd["gbs"] / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "avg_launch_us": round(pd["avg_us"], 3),
@@ -458,11 +493,8 @@ def run_tgn(args, world, rank, dev):
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
-    # the timed window: K consecutive batches centred in the epoch (the rings and message stores are in their
-    # steady state there; an early window samples partly empty rings).  `prefill` untimed steps reach it first.
-    start = max(0, (nb_epoch - args.steps) // 2) if args.window == "mid" else args.warmup
-    prefill = max(0, start - args.warmup)
-    _log(f"tgn: {args.dataset} B={Bg} prefill {prefill} + warmup {args.warmup}, timed batches {start}..{start + args.steps - 1}")
+    start, prefill, boundaries, window_note = timed_window(nb_epoch, args.steps, args.warmup, args.window)
+    _log(f"tgn: {args.dataset} B={Bg}: timed window {window_note}")
     for _ in range(prefill + args.warmup):
         step()
     barrier()
@@ -490,30 +522,40 @@ def run_tgn(args, world, rank, dev):
     value = args.steps * Bg / elapsed
 
     # live per-launch timing: HIP events around eager launches on the launch stream, units from the device
-    # counters.  The pipelined step prefetches: after step j the counters include batch j + 1, so a window
-    # of n probe steps counts batches k + 1 .. k + n (stationary stream: the per-launch averages hold).
+    # counters, over the TIMED window: before each launch's probe the epoch is rewound (begin_epoch) and replayed
+    # from the graphs to batch `start`, and the probe's eager steps then run the timed batches start .. start + K - 1
+    # again (the pipelined step prefetches: its counters count batches start + 1 .. start + K, as the timed ones)
     Bw = Bg / world
     P = model.trainable_count()
     probes = {}
     spec = (("tgn_agg_emit", 9), ("tgn_gru_edge", 1), ("tgn_proj", 11), ("tgn_attn_fwd", 6), ("tgn_pred_train", 4),
             ("tgn_attn_bwd", 8), ("tgn_kv_dE", 10), ("tgn_wgrad_dz0", 2), ("tgn_wgrad3", 12), ("tgn_fixup_update", 5),
             ("tgn_scan", 3), ("tgn_adam", 7))
+
+    def rewind():
+        eng.begin_epoch()
+        counter["i"] = 0
+        for _ in range(start):
+            step()
+        barrier()
+
     for name, kid in spec:
+        rewind()
         _lib.call("tgnx_probe_enable", kid)
-        pe0, pm0 = eng.units()
-        for _ in range(args.probe_steps):
+        pe0, pm0 = units()
+        for _ in range(args.steps):
             step(eager=True)
         eng.finish()
         barrier()
         ms, n = ctypes.c_double(), ctypes.c_int64()
         _lib.call("tgnx_probe_read", ctypes.byref(ms), ctypes.byref(n))
         _lib.call("tgnx_probe_enable", 0)
-        pe1, pm1 = eng.units()
+        pe1, pm1 = units()
         if int(n.value) == 0:   # no such launch in this step (1 hop: attention forward inside tgn_pred_train; scan folded)
             continue
         launches = int(n.value)
         avg_ms = ms.value / launches
-        steps_n = max(args.probe_steps, 1)
+        steps_n = args.steps
         E = (pe1 - pe0) / steps_n
         M = (pm1 - pm0) / steps_n
         probes[name] = dict(avg_us=avg_ms * 1e3, launches=launches, edges=E, nodes=M, steps_n=steps_n)
@@ -551,7 +593,8 @@ def run_tgn(args, world, rank, dev):
         "timing": "avg_launch_us: the kernel's own begin / end timestamps (hipExtLaunchKernelGGL start / stop "
                   "events bound to the dispatch, on its launch stream: what rocprofv3 --kernel-trace reports), "
                   "eager launches of the same step; rocprofv3 summary of the same command: profiles/r5/ (r5_kernel_stats.csv)",
-        "units_window": "probe windows count batches k+1..k+n (pipelined prefetch), stationary stream",
+        "units_window": "each probe replays the timed batches (epoch rewound and replayed to the window's start); "
+                        "units are the probe's own device counters over those batches",
     }
     if flops_gru_edge:
         roofline["tgn_gru_edge_tflops"] = round(flops_gru_edge / (probes["tgn_gru_edge"]["avg_us"] * 1e-6) / 1e12, 3)
@@ -577,9 +620,11 @@ def run_tgn(args, world, rank, dev):
     val = {"mrr": round(float(torch.stack(rrs).mean()), 5), "batches": nval, "negatives": int(shape.num_neg_eval),
            "events_per_s": round(nval * Be / tv, 1), "note": "synthetic stream, mid-epoch state; "
            "eval-path smoke at full size (MRR parity vs the oracle: tests/test_gpu_tgn*.py)"}
-    cpu = cpu1 = cpu_tgn2000 = loop = tcsr = None
+    cpu = cpu1 = cpu_tgn2000 = loop = tcsr = gpu1 = None
     _log("tgn: eval pass done")
     headline = args.dataset == "tgbl-wiki" and args.layers == 1 and args.aggr == "last" and args.updater == "gru"
+    if rank == 0 and world == 1 and headline and not args.no_config1:
+        gpu1 = tgnn_config1_gpu(args, dev)
     if rank == 0 and world == 1 and headline and not args.no_train_loop:
         loop = train_loop_rate(args, dev, value)
     if rank == 0 and world == 1 and not args.no_tcsr:
@@ -592,6 +637,8 @@ def run_tgn(args, world, rank, dev):
             cpu1 = cpu_baseline(stream, 2000, budget_s=25.0, max_batches=12)
             cpu1["config"] = ("BASELINE #1: tgbl-wiki, config/TGN.yml batch_size 2000, the path pyg-mem-tgn.py runs "
                               "(TGNN block loop, epoch_utils.train), CPU; sampled batches, epoch extrapolated")
+            if gpu1 is not None:
+                gpu1["vs_cpu_baseline_config1"] = round(gpu1["value"] / max(cpu1["value"], 1e-9), 1)
             # the TGN memory-path oracle at TGN.yml's batch (the headline model on the CPU; NOT config #1's model)
             cpu_tgn2000 = cpu_baseline_tgn(stream, 2000)
             cpu_tgn2000["config"] = ("TGN memory-path oracle (the headline model) at config/TGN.yml's batch_size "
@@ -621,10 +668,8 @@ def run_tgn(args, world, rank, dev):
                    "launch": "hip-graph replay per step" if use_graph else "eager",
                    "layers": args.layers,
                    "timed_batches": [start, start + args.steps - 1],
-                   "timed_window": (f"batches {start}..{start + args.steps - 1} of the {nb_epoch}-batch train epoch "
-                                    f"(0-based; {prefill} untimed prefill + {args.warmup} warmup steps before it"
-                                    + (", the window wraps into the next epoch: its begin_epoch is timed"
-                                       if start + args.steps > nb_epoch else "") + ")"),
+                   "timed_window": window_note,
+                   "epoch_boundaries_in_window": boundaries,
                    "sampled_edges_per_step": round(win_edges, 1),
                    "sampled_nodes_per_step": round(win_nodes, 1),
                    "probe_window_edges_per_step": round(pd["edges"], 1),
@@ -634,12 +679,32 @@ def run_tgn(args, world, rank, dev):
         "kernels_gbs": {k: round(v["gbs"], 1) for k, v in probes.items() if v["gbs"]},
         "cpu_baseline": cpu,
         "cpu_baseline_config1": cpu1,
+        "gpu_tgnn_config1": gpu1,
         "cpu_baseline_tgn_b2000": cpu_tgn2000,
         "train_loop": loop,
         "tcsr_sampler": tcsr,
         "val_eval_gpu": val,
         "loss_sum": round(loss, 4),
     }
+
+
+def tgnn_config1_gpu(args, dev):
+    """BASELINE #1's workload on the HIP path: config/TGN.yml's batch_size 2000 (TGN.yml:27) through the TGNN
+    dependency-block loop pyg-mem-tgn.py runs (epoch_utils.py:168-318, model_utils.py:61-159), one GPU, on the
+    same wiki-shaped stream as cpu_baseline_config1 (~930 blocks per batch), so the two are one configuration.
+    Timed window: min(K, 40) batches centred in the 56-batch epoch, graph replay; parity at this batch size:
+    tests/test_gpu_tgnn_b2000.py."""
+    import copy
+    a = copy.copy(args)
+    a.batch, a.steps, a.warmup = 2000, min(args.steps, 40), min(args.warmup, 5)
+    a.dataset = "tgbl-wiki"
+    r = run_tgnn(a, 1, 0, dev, probe=False)
+    r.update(unit="events/s", batch=2000, dtype="f32",
+             workload="tgbl-wiki TGNN (running reference path: DGL EdgeGATConv block loop), config/TGN.yml "
+                      "batch_size 2000, 10 temporal neighbours, H=8, D=100, d=172, "
+                      f"dropout {'off' if args.no_dropout else '0.6 (epoch-1)'}; 1x MI355X, hip-graph replay")
+    _log(f"tgnn config #1 (B=2000): {r['value']:.0f} events/s, {r['ms_per_step']:.3f} ms/step")
+    return r
 
 
 def train_loop_rate(args, dev, engine_value, epochs=3):
@@ -787,7 +852,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-loop", action="store_true", help="skip timing the drop-in pyg_epoch_utils.train loop")
     ap.add_argument("--no-tcsr", action="store_true", help="skip the t-CSR sampler leg")
-    ap.add_argument("--probe-steps", type=int, default=100)
+    ap.add_argument("--no-config1", action="store_true",
+                    help="skip the GPU TGNN line at config/TGN.yml's batch_size 2000 (BASELINE #1's workload)")
     ap.add_argument("--window", choices=["mid", "start"], default="mid",
                     help="TGN timed window: K batches centred in the train epoch (mid, after untimed prefill steps) "
                          "or right after the warmup (start)")

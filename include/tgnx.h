@@ -355,6 +355,10 @@ size_t tgnx_tgn_store_words(const tgnx_tgn_config* cfg);
 size_t tgnx_tgn_plan_table_bytes(const tgnx_tgn_config* cfg, int64_t split_lo, int64_t split_hi, int64_t batch);
 int tgnx_tgn_plan_table(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, int64_t split_lo, int64_t split_hi,
                         int64_t batch, void* table, size_t table_bytes, void* stream);
+/* Forget what `table` was built for (the library keeps, per table address, the split / batch it serves, and the
+ * steps refuse a table built for another): call before freeing a plan table, so a later allocation at the same
+ * address is not taken for it.  A (re)build forgets first and records only after its launch was issued. */
+int tgnx_tgn_plan_table_release(const void* table);
 /* memory = 0, last_update = 0, message stores empty (memory_module.py:106-110). */
 int tgnx_tgn_reset_state(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* stream);
 /* Train batch, part 1 (the canonical loop pyg_epoch_utils.py:106-137 carries commented out): negatives

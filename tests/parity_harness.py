@@ -18,16 +18,20 @@ from oracle.tgnn_ref import RefTGNN
 
 
 class Pair:
-    def __init__(self, N=400, E=1400, d=172, D=100, K=10, B=200, Kn_eval=20, seed=0, t_max=None):
+    def __init__(self, N=400, E=1400, d=172, D=100, K=10, B=200, Kn_eval=20, seed=0, t_max=None, shape=None):
         from tgnx.engine import TgnnEngine
         from tgnx.model import TGNN, getOptimizer
         from tgnx.sampler import LastNeighborLoader
         from tgnx.synth import SHAPES, StreamShape, make_stream
 
-        base = SHAPES["tgbl-wiki"]
-        shape = StreamShape("parity", N, E, d, True, num_src=int(N * 0.85),
-                            t_max=base.t_max if t_max is None else t_max)
-        self.s = make_stream(shape, seed=seed)
+        if shape is None:
+            base = SHAPES["tgbl-wiki"]
+            shape = StreamShape("parity", N, E, d, True, num_src=int(N * 0.85),
+                                t_max=base.t_max if t_max is None else t_max)
+            self.s = make_stream(shape, seed=seed)
+        else:       # a named TGB shape (full node count), first E events of its stream
+            self.s = make_stream(shape, seed=seed, num_events=E)
+            N, d = self.s.num_nodes, self.s.shape.msg_dim
         self.B, self.K, self.D, self.d, self.N, self.Kn_eval = B, K, D, d, N, Kn_eval
         self.blk = blocks_ref.block_ids(self.s.src, self.s.dst, B)
         self.feats = torch.from_numpy(self.s.msg)
@@ -51,6 +55,21 @@ class Pair:
         t32 = s.t[sl].astype(np.float32)
         return (torch.from_numpy(s.src[sl]), torch.from_numpy(s.dst[sl]), torch.from_numpy(t32),
                 torch.from_numpy(s.msg[sl]), torch.from_numpy(self.blk[sl]))
+
+    def prefill(self, n_events, chunk=None):
+        """Advance both rings (and the e_id counter) over the next `n_events` events, batch by batch,
+        without training: a later step then samples full rings, as mid-epoch (`neighbor_loader.insert`,
+        epoch_utils.py:300)."""
+        chunk = chunk or self.B
+        end = self.pos + n_events
+        while self.pos < end:
+            n = min(chunk, end - self.pos)
+            sl = slice(self.pos, self.pos + n)
+            self.pos += n
+            t32 = self.s.t[sl].astype(np.float32)
+            self.ref_loader.insert(self.s.src[sl], self.s.dst[sl], t32)
+            self.loader.insert(torch.from_numpy(self.s.src[sl]), torch.from_numpy(self.s.dst[sl]),
+                               torch.from_numpy(t32))
 
     def train_step(self):
         src, dst, t, msg, blk = self._batch(self.B)

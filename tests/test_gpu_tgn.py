@@ -557,6 +557,9 @@ def test_tgn_no_grad_store_same_step():
         G = b.model.grad_flat
         assert torch.all(G[:-1] == 7.0), st                    # never stored
         assert not torch.all(a.model.grad_flat[:-1] == 7.0), st
+        with pytest.raises(RuntimeError, match="keep_grads"):  # stale gradients are not handed out
+            b.model.grads_by_name()
+        assert a.model.grads_by_name()
         with torch.no_grad():   # re-synchronise (the wiki time scale turns ulp differences chaotic)
             b.model.flat.copy_(a.model.flat)
             b.adam_m.copy_(a.adam_m)

@@ -5258,18 +5258,25 @@ int tgnx_tgn_plan_table(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf,
   TGNX_CHECK_ARG(table && table_bytes >= need && ((uintptr_t)table & 15) == 0,
                  "tgnx_tgn_plan_table: table of tgnx_tgn_plan_table_bytes(...) bytes, 16-B aligned");
   const int64_t nb = (split_hi - split_lo + batch - 1) / batch;
-  {
-    std::lock_guard<std::mutex> lk(g_ptab_mu);
-    ptab_registry()[table] = PlanTableKey{split_lo, split_hi, batch, plan_slot_bytes(k.B), need};
+  // a (re)build first forgets what the table held: a failed build leaves it unknown, not valid for its old split
+  tgnx_tgn_plan_table_release(table);
+  if (nb > 0) {
+    const size_t smem = tgn_scan_smem(k.B);
+    TGNX_CHECK_ARG(hipFuncSetAttribute(reinterpret_cast<const void*>(&tgn_plan_table_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) == hipSuccess,
+                   "tgnx_tgn_plan_table: dynamic LDS of %zu bytes refused", smem);
+    tgn_plan_table_kernel<<<(unsigned)(nb * 2 * c.pplan), 1024, smem, as_stream(stream)>>>(
+        c, reinterpret_cast<char*>(table), plan_slot_bytes(k.B), split_lo, split_hi, batch);
+    TGNX_LAUNCH_CHECK("tgn_plan_table");
   }
-  if (nb == 0) return TGNX_OK;
-  const size_t smem = tgn_scan_smem(k.B);
-  TGNX_CHECK_ARG(hipFuncSetAttribute(reinterpret_cast<const void*>(&tgn_plan_table_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) == hipSuccess,
-                 "tgnx_tgn_plan_table: dynamic LDS of %zu bytes refused", smem);
-  tgn_plan_table_kernel<<<(unsigned)(nb * 2 * c.pplan), 1024, smem, as_stream(stream)>>>(
-      c, reinterpret_cast<char*>(table), plan_slot_bytes(k.B), split_lo, split_hi, batch);
-  TGNX_LAUNCH_CHECK("tgn_plan_table");
+  std::lock_guard<std::mutex> lk(g_ptab_mu);
+  ptab_registry()[table] = PlanTableKey{split_lo, split_hi, batch, plan_slot_bytes(k.B), need};
+  return TGNX_OK;
+}
+
+int tgnx_tgn_plan_table_release(const void* table) {
+  std::lock_guard<std::mutex> lk(g_ptab_mu);
+  ptab_registry().erase(table);
   return TGNX_OK;
 }
 

@@ -41,6 +41,7 @@ SIGNATURES = {
     "tgnx_tgn_reset_state": (ctypes.c_int, [P, P, c_vp]),
     "tgnx_tgn_plan_table_bytes": (c_sz, [P, c_i64, c_i64, c_i64]),
     "tgnx_tgn_plan_table": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, P, c_sz, c_vp]),
+    "tgnx_tgn_plan_table_release": (ctypes.c_int, [P]),
     "tgnx_tgn_train_fwd_bwd": (ctypes.c_int, [P, P, c_i32, c_i32, c_vp]),
     "tgnx_tgn_train_update": (ctypes.c_int, [P, P, c_vp]),
     "tgnx_tgn_train_step": (ctypes.c_int, [P, P, c_i32, c_i32, c_vp]),

@@ -216,6 +216,12 @@ class TGNModel(nn.Module):
                 self.flat[o:o + n].copy_(sd[name].reshape(-1).to(self.flat.device))
 
     def grads_by_name(self) -> dict:
+        """The last step's gradient of every parameter tensor (views into grad_flat).  Raises while an engine runs
+        this model's steps with keep_grads=False (bench.py, the drop-in train()): those fused steps do not store the
+        gradient (TGNX_TGN_NO_GRAD_STORE), so grad_flat would hold a stale step's values."""
+        if getattr(self, "_grads_stale", False):
+            raise RuntimeError("grads_by_name: the bound TgnEngine runs with keep_grads=False (fused Adam without the "
+                               "gradient store): set engine.keep_grads = True before binding to read gradients")
         return {name: self.grad_flat[o:o + n].view(s) for name, (o, n, s) in self._views.items()}
 
     def settle(self) -> None:
@@ -304,7 +310,7 @@ class TgnEngine:
     once the step's exchange returned: the apply does not change it)."""
 
     def __init__(self, model: TGNModel, loader, events: dict, optimizer: TgnAdam | None = None,
-                 dst_nodes=None, seed: int = 0, rank: int = 0, world: int = 1):
+                 dst_nodes=None, seed: int = 0, rank: int = 0, world: int = 1, data_parallel: bool | None = None):
         self.model, self.loader, self.opt = model, loader, optimizer
         self.dev = model.device
         import weakref
@@ -336,6 +342,12 @@ class TgnEngine:
         self.use_plan_table = os.environ.get("TGNX_PLAN_TABLE", "1") != "0"
         self.dst_nodes = None if dst_nodes is None else torch.as_tensor(dst_nodes).to(self.dev, torch.long).contiguous()
         self.seed, self.rank, self.world = int(seed), int(rank), int(world)
+        # the data-parallel step forms (exchange collective, then the apply + Adam launch): world > 1, or forced at
+        # world 1 (data_parallel=True), where the exchange over a 1-rank group is an identity and the step must
+        # equal the world-1 one (tests/test_gpu_tgn_rccl.py runs it through RCCL)
+        self.dp = self.world > 1 if data_parallel is None else bool(data_parallel)
+        if self.world > 1 and not self.dp:
+            raise ValueError("TgnEngine: world > 1 needs the data-parallel step forms")
         self.fuse_adam = True
         # fused-Adam steps also store the gradient in model.grad_flat (grads_by_name); loops that never read it
         # (bench.py, the drop-in train()) set False before bind_resident: TGNX_TGN_NO_GRAD_STORE, 1.1 MB of
@@ -382,7 +394,7 @@ class TgnEngine:
         self.exchange_mode = os.environ.get("TGNX_EXCHANGE", "fused")
         if self.exchange_mode not in EXCHANGE_MODES:
             raise ValueError(f"TGNX_EXCHANGE must be one of {EXCHANGE_MODES}, got {self.exchange_mode!r}")
-        if self.world > 1:
+        if self.dp:
             self.xcap = min(cfg.num_nodes, 2 * (-(-cfg.max_batch // self.world)))
             rw = cfg.mem_dim + 4
             G = model.grad_flat.numel()
@@ -425,6 +437,9 @@ class TgnEngine:
         b.out_ev = _p(self.out_ev)
         b.plan_table = _p(self.plan_table)
         b.flags = 0 if self.keep_grads else 1   # TGNX_TGN_NO_GRAD_STORE
+        # steps on these buffers leave grad_flat stale (fused Adam without the store; data-parallel steps always
+        # write it: it heads the exchange buffer)
+        m._grads_stale = not self.keep_grads and not self.dp
         return b
 
     def _stream(self):
@@ -476,12 +491,12 @@ class TgnEngine:
     def _fused(self) -> bool:
         """Adam folded into the step's gradient writers (tgnx_tgn_train_step): world 1 only, since data
         parallel steps all-reduce the gradients before the update."""
-        return self.fuse_adam and self.world == 1
+        return self.fuse_adam and not self.dp
 
     def apply_update(self, allreduce: bool = True):
-        if allreduce and self.world > 1:
+        if allreduce and self.dp:
             self._exchange()
-        if self.world > 1:   # the exchanged rows and Adam in one launch
+        if self.dp:   # the exchanged rows and Adam in one launch
             _lib.call("tgnx_tgn_apply_rows_update", ctypes.byref(self.cfg), ctypes.byref(self._pending),
                       _p(self.xgather), self.xgather.shape[0], self._stream())
         else:
@@ -519,7 +534,7 @@ class TgnEngine:
         self._res = (int(split_lo), int(split_hi), int(batch))
         self._res_drop = 1 if dropout else 0
         self._prefetched = False
-        self.plan_table = None
+        self._release_plan_table()
         if self.use_plan_table:   # the split's ring-insert / store plans, built once for every batch
             nbytes = int(_lib.lib().tgnx_tgn_plan_table_bytes(ctypes.byref(self.cfg), *self._res))
             if nbytes == 0:
@@ -535,6 +550,21 @@ class TgnEngine:
         self._cfg_ref, self._buf_ref = ctypes.byref(self.cfg), ctypes.byref(self._res_buf)
         self._ctl_p = ctypes.c_void_p(self.ctl.data_ptr())
 
+    def _release_plan_table(self):
+        """Drop the bound split's plan table, and the library's record of it (tgnx_tgn_plan_table_release): the
+        caching allocator may hand its address to another tensor."""
+        if self.plan_table is not None:
+            torch.cuda.synchronize(self.dev)      # (no step still reading it)
+            _lib.lib().tgnx_tgn_plan_table_release(ctypes.c_void_p(self.plan_table.data_ptr()))
+        self.plan_table = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "plan_table", None) is not None:
+                _lib.lib().tgnx_tgn_plan_table_release(ctypes.c_void_p(self.plan_table.data_ptr()))
+        except Exception:
+            pass
+
     def begin_epoch(self):
         """pyg_epoch_utils.py:11-16: memory reset_state + neighbor_loader reset_state; cursor to 0."""
         self.reset_state()
@@ -542,7 +572,7 @@ class TgnEngine:
         self._prefetched = False
 
     def _pipelined(self) -> bool:
-        return self.pipeline and self.fold_cursor and (self._res_fused or self.world > 1)
+        return self.pipeline and self.fold_cursor and (self._res_fused or self.dp)
 
     def _pp(self) -> bool:
         """Parity-set steps: world 1 with Adam fused (tgnx_tgn_train_step_pp), or data parallel
@@ -552,10 +582,10 @@ class TgnEngine:
             return False
         if self.model.layers == 2 and os.environ.get("TGNX_PP_2HOP", "1") == "0":
             return False
-        return self._res_fused if self.world == 1 else True
+        return self._res_fused if not self.dp else True
 
     def _dp_pp(self) -> bool:
-        return self.world > 1 and self._pp()
+        return self.dp and self._pp()
 
     def _pre(self, prefetched: bool = False, parity=None, apply=None):
         adv, fb = self._f[:2]
@@ -590,7 +620,7 @@ class TgnEngine:
     def _post(self):
         st = self._stream()
         rc = 0
-        if self.world > 1:   # the exchanged rows and Adam, one launch
+        if self.dp:   # the exchanged rows and Adam, one launch
             rc |= self._f[3](self._cfg_ref, self._buf_ref, ctypes.c_void_p(self.xgather.data_ptr()),
                              ctypes.c_int64(self.xgather.shape[0]), st)
         elif not self._res_fused:   # fused step: Adam already applied
@@ -599,7 +629,7 @@ class TgnEngine:
             raise RuntimeError(f"tgnx TGN resident update failed: {_lib.lib().tgnx_last_error().decode()}")
 
     def _split(self) -> bool:
-        return self.split_scan and self.world > 1 and self._pipelined() and not self._res_fused and not self._pp()
+        return self.split_scan and self.dp and self._pipelined() and not self._res_fused and not self._pp()
 
     def _scan_next(self):
         """The next batch's scan (split pipelined steps): rides beside the exchange."""
@@ -612,7 +642,7 @@ class TgnEngine:
 
     def _allreduce(self, between=None):
         """The exchange; `between` (the next batch's scan) runs on the compute stream while it is in flight."""
-        if self.world > 1:
+        if self.dp:
             if self.exchange is not None:
                 work = self.exchange(self.comm, True)
                 works = [] if work is None else [work]
@@ -674,13 +704,13 @@ class TgnEngine:
                     with torch.cuda.graph(gd[par, ap]):
                         self._pre(True, par, bool(ap))
             self._graphs = (gd, None, None)
-        elif self.world == 1 and self._pp():   # one graph per parity, replayed alternately
+        elif not self.dp and self._pp():   # one graph per parity, replayed alternately
             gp = (torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph())
             for par in (0, 1):
                 with torch.cuda.graph(gp[par]):
                     self._pre(True, par)
             self._graphs = (gp, None, None)
-        elif self.world == 1:
+        elif not self.dp:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):   # pipelined: the steady-state step (the previous step prefetched)
                 self._pre(True)
