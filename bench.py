@@ -248,7 +248,7 @@ def run_tgnn(args, world, rank, dev, probe=True):
     probes = {}
     kernels = (("tgnn_edge_fwd", 1), ("tgnn_edge_bwd", 2), ("tgnn_seg_fwd", 6), ("tgnn_seg_bwd", 8),
                ("tgnn_pred_train", 4), ("tgnn_assemble", 3), ("tgnn_meta_collapse", 9), ("tgnn_adam", 7))
-    for name, kid in (kernels if probe else ()):
+    for name, kid in (kernels if probe and not args.no_probe else ()):
         counter["i"] = 0
         for _ in range(start):
             step()
@@ -274,8 +274,10 @@ def run_tgnn(args, world, rank, dev, probe=True):
                             gbs=algo / (avg_ms * 1e-3) / 1e9)
     blocks_mean = float(np.mean([blk[i:i + Bg].max() + 1 for i in range(0, stream.train_end, Bg)]))
     if not probes:
-        return {"value": round(args.steps * Bg / elapsed, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        return {"metric": _metric(args.dataset, "tgnn"), "value": round(args.steps * Bg / elapsed, 1),
+                "ms_per_step": round(elapsed / args.steps * 1e3, 4),
                 "steps": args.steps, "timed_window": window_note, "loss_sum": round(loss, 4),
+                "config": {"timed_steps": [prefill + args.warmup, prefill + args.warmup + args.steps]},
                 "edges_per_step": round((e1 - e0) / args.steps / world, 1),
                 "segments_per_step": round((s1 - s0) / args.steps / world, 1),
                 "blocks_per_batch_mean": round(blocks_mean, 1)}
@@ -316,6 +318,7 @@ def run_tgnn(args, world, rank, dev, probe=True):
                        "launch": "hip-graph replay per step" if use_graph else "eager",
                        "edges_per_step": round((e1 - e0) / args.steps / world, 1),
                        "timed_batches": [start, start + args.steps - 1], "timed_window": window_note,
+                       "timed_steps": [prefill + args.warmup, prefill + args.warmup + args.steps],
                        "probe_window": "the timed batches (each probe rewinds the epoch and replays to its start)",
                        "blocks_per_batch_mean": round(blocks_mean, 1)},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(pd["gbs"], 2), "peak": HBM_PEAK_GBS,
@@ -539,7 +542,7 @@ def run_tgn(args, world, rank, dev):
             step()
         barrier()
 
-    for name, kid in spec:
+    for name, kid in (() if args.no_probe else spec):
         rewind()
         _lib.call("tgnx_probe_enable", kid)
         pe0, pm0 = units()
@@ -559,6 +562,17 @@ def run_tgn(args, world, rank, dev):
         E = (pe1 - pe0) / steps_n
         M = (pm1 - pm0) / steps_n
         probes[name] = dict(avg_us=avg_ms * 1e3, launches=launches, edges=E, nodes=M, steps_n=steps_n)
+    if not probes:      # --no-probe (A/B timing runs): the timed window only
+        return {"metric": _metric(args.dataset, "tgn"), "value": round(value, 1), "unit": "events/s",
+                "n_gpus": _group_size(world), "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+                "scaling": "strong" if args.global_batch else "weak", "vs_baseline": None, "dtype": "f32",
+                "data": f"synthetic {args.dataset}-shaped stream (SURVEY.md §8d), events resident in HBM",
+                "config": {"workload": f"{args.dataset} TGN memory path, batch {Bg}", "global_batch": Bg,
+                           "parallelism": f"dp{world}", "layers": args.layers, "timed_window": window_note,
+                           "timed_steps": [prefill + args.warmup, prefill + args.warmup + args.steps],
+                           "sampled_edges_per_step": round(win_edges, 1)},
+                "roofline": None, "note": "--no-probe: no per-launch probes", "loss_sum": round(loss, 4)}
     kvf = args.layers == 1 and "tgn_kv_dE" not in probes
     for name, q in probes.items():
         algo = tgn_launch_bytes(name, q["edges"], q["nodes"], Bw, Bg, D, d, K, P, N, kvf) * (
@@ -623,7 +637,7 @@ def run_tgn(args, world, rank, dev):
     cpu = cpu1 = cpu_tgn2000 = loop = tcsr = gpu1 = None
     _log("tgn: eval pass done")
     headline = args.dataset == "tgbl-wiki" and args.layers == 1 and args.aggr == "last" and args.updater == "gru"
-    if rank == 0 and world == 1 and headline and not args.no_config1:
+    if rank == 0 and world == 1 and headline and not args.no_config1 and not args.no_probe:
         gpu1 = tgnn_config1_gpu(args, dev)
     if rank == 0 and world == 1 and headline and not args.no_train_loop:
         loop = train_loop_rate(args, dev, value)
@@ -670,6 +684,10 @@ def run_tgn(args, world, rank, dev):
                    "timed_batches": [start, start + args.steps - 1],
                    "timed_window": window_note,
                    "epoch_boundaries_in_window": boundaries,
+                   # ordinals of the timed steps among this run's steps (0 = the first step): a kernel launched once
+                   # per step has these dispatch indices in a rocprofv3 trace of the command
+                   # (tools/rocprof_window.py, tools/pmc_summary.py PMC_WINDOW)
+                   "timed_steps": [prefill + args.warmup, prefill + args.warmup + args.steps],
                    "sampled_edges_per_step": round(win_edges, 1),
                    "sampled_nodes_per_step": round(win_nodes, 1),
                    "probe_window_edges_per_step": round(pd["edges"], 1),
@@ -852,6 +870,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-train-loop", action="store_true", help="skip timing the drop-in pyg_epoch_utils.train loop")
     ap.add_argument("--no-tcsr", action="store_true", help="skip the t-CSR sampler leg")
+    ap.add_argument("--no-probe", action="store_true",
+                    help="A/B timing runs: skip the per-launch probes (no roofline) and the secondary legs")
     ap.add_argument("--no-config1", action="store_true",
                     help="skip the GPU TGNN line at config/TGN.yml's batch_size 2000 (BASELINE #1's workload)")
     ap.add_argument("--window", choices=["mid", "start"], default="mid",
@@ -882,10 +902,10 @@ def main():
     if not args.only:
         other = "tgnn" if args.model == "tgn" else "tgn"
         sec = run[other](args, world, rank, dev)
-        out["secondary_path"] = {"model": other, "workload": sec["config"]["workload"], "value": sec["value"],
-                                 "unit": sec["unit"], "ms_per_step": sec["ms_per_step"],
-                                 "roofline": sec["roofline"], "kernels_us": sec["kernels_us"],
-                                 "cpu_baseline": sec["cpu_baseline"]}
+        out["secondary_path"] = {"model": other, "workload": sec.get("config", {}).get("workload"),
+                                 "value": sec["value"], "unit": sec.get("unit", "events/s"),
+                                 "ms_per_step": sec["ms_per_step"], "roofline": sec.get("roofline"),
+                                 "kernels_us": sec.get("kernels_us"), "cpu_baseline": sec.get("cpu_baseline")}
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

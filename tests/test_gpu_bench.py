@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.timeout(400)
 def test_bench_gpus2_spawns_two_ranks():
     cmd = [sys.executable, "-u", "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--one-device", "--steps", "5",
-           "--warmup", "2", "--probe-steps", "2", "--no-cpu-baseline", "--no-train-loop", "--no-tcsr", "--only"]
+           "--warmup", "2", "--no-cpu-baseline", "--no-train-loop", "--no-tcsr", "--only"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=360)
     assert r.returncode == 0, r.stderr[-4000:]

@@ -137,24 +137,6 @@ __device__ __forceinline__ float swap32_sum(float v) {  // v + v[lane ^ 32]
   const auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
   return __int_as_float(p[0]) + __int_as_float(p[1]);
 }
-#ifdef TGNX_NO_DPP  // A/B: the ds_bpermute forms
-__device__ __forceinline__ float wave_sum_f(float v) { return wave_sum(v); }
-__device__ __forceinline__ float half_sum_f(float v) {  // sum over each 32-lane half
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-  return v;
-}
-__device__ __forceinline__ float wave_max_f(float v) { return wave_max(v); }
-__device__ __forceinline__ float lane_f(float v, int l) { return __shfl(v, l, WAVE); }
-__device__ __forceinline__ int lane_i(int v, int l) { return __shfl(v, l, WAVE); }
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, WAVE));
-  return v;
-}
-__device__ __forceinline__ float xor32_f(float v) { return __shfl_xor(v, 32, WAVE); }
-__device__ __forceinline__ float xor16_f(float v) { return __shfl_xor(v, 16, WAVE); }
-#else
 __device__ __forceinline__ float wave_sum_f(float v) {
   v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
   v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
@@ -204,7 +186,6 @@ __device__ __forceinline__ float lane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 __device__ __forceinline__ int lane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-#endif
 __device__ __forceinline__ int wave_incl_scan(int v) {
   const int l = lane_id();
 #pragma unroll
@@ -295,13 +276,12 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
 
 // lane i <- lane i ^ J, picking the cheapest cross-lane path for each distance: DPP quad_perm
 // (1, 2), DPP row_ror:8 (8), ds_swizzle xor mode within 32 lanes (4), v_permlane16_swap (16) and
-// v_permlane32_swap (32) (full waves; -DTGNX_NO_DPP: swizzle / bpermute).
+// v_permlane32_swap (32) (full waves; the round-2 shuffles, ds_bpermute LDS round trips, measured 3.7 % slower).
 template <int J>
 __device__ __forceinline__ unsigned xlane_xor(unsigned v) {
   if constexpr (J == 1) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
   else if constexpr (J == 2) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
   else if constexpr (J == 8) return (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
-#ifndef TGNX_NO_DPP
   else if constexpr (J == 16) {  // v_permlane16_swap: rows 0 <-> 1, 2 <-> 3
     const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
     return (threadIdx.x & 16) ? (unsigned)p[0] : (unsigned)p[1];
@@ -309,7 +289,6 @@ __device__ __forceinline__ unsigned xlane_xor(unsigned v) {
     const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
     return (threadIdx.x & 32) ? (unsigned)p[0] : (unsigned)p[1];
   }
-#endif
   else if constexpr (J < 32) return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (J << 10));
   else return __shfl_xor(v, J, WAVE);
 }
@@ -455,9 +434,6 @@ __device__ __forceinline__ void sort_u64_chunks(uint64_t* key, uint64_t* tmp, in
 #ifndef TGNX_SORT_CHUNKS_MIN
 #define TGNX_SORT_CHUNKS_MIN 64  // distinct keys: chunked sort above this many (rank sort below)
 #endif
-#ifndef TGNX_SORT_REG4
-#define TGNX_SORT_REG4 1
-#endif
 __device__ __forceinline__ void cmpx_u64(uint64_t& a, uint64_t& b, bool up) {
   const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
   a = up ? lo : hi;
@@ -520,9 +496,6 @@ __device__ __forceinline__ void sort_u64_reg4(uint64_t* key, uint64_t* tmp, int 
 // tmp_full: tmp holds n_pow2 keys (enables the four-keys-per-thread sort for T < n_pow2 <= 4 T)
 __device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, int n_pow2, bool distinct = false,
                                          bool tmp_full = false) {
-#ifdef TGNX_DIAG_NOSORT  // timing experiment only: results wrong
-  if (distinct) return;
-#endif
   if (distinct && (n <= (int)blockDim.x || n <= 1024)) {
     if (n > TGNX_SORT_CHUNKS_MIN && n <= 1024) sort_u64_chunks(key, tmp, n);
     else sort_u64_rank(key, tmp, n);
@@ -533,7 +506,7 @@ __device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, in
   for (int i = n + threadIdx.x; i < n_pow2; i += blockDim.x) key[i] = ~0ull;
   __syncthreads();
   if (n_pow2 <= (int)blockDim.x) sort_u64_reg(key, tmp, n_pow2);
-  else if (tmp_full && n_pow2 <= 4 * (int)blockDim.x && TGNX_SORT_REG4) sort_u64_reg4(key, tmp, n_pow2);
+  else if (tmp_full && n_pow2 <= 4 * (int)blockDim.x) sort_u64_reg4(key, tmp, n_pow2);
   else bitonic_sort_u64(key, n_pow2);
 }
 

@@ -26,24 +26,12 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // Write-through (sc1) stores for what a launch hands to the next one: a kernel boundary writes back the dirty
 // L2 lines its predecessor left (MI355X_MICROARCH.md price list: + B / 6 TB/s), write-through stores leave none.
 // (Vector stores: a relaxed agent-scope atomic store is global_store_dword sc1; 16 B: a buffer store, aux 16.)
-#ifndef TGNX_WT
-#define TGNX_WT 0  // (split-K partials + fused-Adam stores write-through: 0.0969 vs 0.0967 ms plain, same box)
-#endif
 __device__ __forceinline__ void st_wt(float* p, float v) {
-#if TGNX_WT
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
   *p = v;
-#endif
 }
 // 16 B at byte offset off (per lane) of the wave-uniform base, whose extent is bytes
 __device__ __forceinline__ void st_wt4(float* base, int off, int bytes, f32x4_t v) {
-#if TGNX_WT
-  const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r, off, 0, 16);
-#else
   *reinterpret_cast<f32x4_t*>(reinterpret_cast<char*>(base) + off) = v;
-#endif
 }
 
 template <int TM_, int TN_, int KC_, int PF_ = 1, bool WS_ = false, int DR_ = 0>
@@ -233,9 +221,6 @@ struct LoaderTraits<L, std::void_t<typename L::Idx>> {  // two-phase gather
 // of row r, k % 4 == 0, one global_load_dwordx4).  When vec4() holds for both operands and K % 4 == 0,
 // the body fetches such operands 4 k per lane (a quarter of the load instructions; ~1 us per launch on
 // the TGN GEMMs, tools/gemm_lab.hip) and stashes them with one ds_write_b128.
-#ifndef TGNX_GEMM_VEC4
-#define TGNX_GEMM_VEC4 1
-#endif
 template <class L, class = void>
 struct HasVec4 : std::false_type {};
 template <class L>
@@ -692,7 +677,7 @@ __device__ __forceinline__ void gemm_body(const GemmShape& g, const AL& al, cons
   const GemmRt rt = gemm_runtime<CFG>(g);
   const int tmr = (rt.Mr + CFG::TM - 1) / CFG::TM, tnr = (rt.Nr + CFG::TN - 1) / CFG::TN;
   const int per = (tmr * tnr * rt.Sr + 7) >> 3, grid = gemm_blocks(g);
-  if constexpr (TGNX_GEMM_VEC4 && (HasVec4<AL>::value || HasVec4<BL>::value)) {
+  if constexpr (HasVec4<AL>::value || HasVec4<BL>::value) {
     if ((rt.Kr & 3) == 0 && rt.Kr >= 4 && vec_ok(al) && vec_ok(bl)) {
       for (int vb = bid; vb < 8 * per; vb += grid) {
         gemm_tile<CFG, true>(g, rt, al, bl, epi, part, vb, smem);
@@ -752,12 +737,8 @@ __device__ __forceinline__ bool gemm_job_dispatch(const J& j, int& bid, float* s
   return false;
 }
 // a non-GEMM piece of work riding in a gemmN launch: nb 256-thread workgroups running f(bid, smem), smem
-// at least SM floats of LDS.  Its block range is padded to a multiple of the 8 XCDs (the pad blocks exit), so
-// the GEMM ranges after it keep their XCD grouping (TGNX_BLOCKJOB_PAD 0: unpadded)
-#ifndef TGNX_BLOCKJOB_PAD
-#define TGNX_BLOCKJOB_PAD 0  // (A/B: 0.0965 vs 0.0962 ms unpadded; the step's launches are not fabric-bound)
-#endif
-__host__ __device__ constexpr int blockjob_span(int nb) { return TGNX_BLOCKJOB_PAD ? (nb + 7) & ~7 : nb; }
+// at least SM floats of LDS (its block range unpadded: padding it to a multiple of the 8 XCDs measured ±0)
+__host__ __device__ constexpr int blockjob_span(int nb) { return nb; }
 template <class F, int SM = 4>
 struct BlockJob {
   struct Cfg {
@@ -830,16 +811,7 @@ template <class CFG, class EPI>
 inline GemmFix<CFG, EPI> gemm_fix(const GemmShape& g, const float* part, const EPI& epi) {
   return GemmFix<CFG, EPI>{g, part, epi};
 }
-// one output tile of a deferred GEMM: Σ partials over the runtime splits in order, then the epilogue.
-// An epilogue with `fix_pre(tile)` (the fused-Adam weight-gradient writers) gets its loads issued before the
-// partials' (they need only the tile's coordinates): one dependent round per tile instead of three
-template <class E, class = void>
-struct HasFixPre : std::false_type {};
-template <class E>
-struct HasFixPre<E, std::void_t<decltype(E::fix_pre_tag)>> : std::true_type {};
-#ifndef TGNX_FIX_PRE
-#define TGNX_FIX_PRE 0  // (same-box A/Bs: fixup 11.6-12.0 -> 12.1-12.6 us with the prefetch, step +0.3 %; kept as a knob)
-#endif
+// one output tile of a deferred GEMM: Σ partials over the runtime splits in order, then the epilogue
 template <class CFG, class EPI>
 __device__ void gemm_fix_tile(const GemmFix<CFG, EPI>& f, int tile, float* smem) {
   constexpr int TM = CFG::TM, TN = CFG::TN, FM = CFG::FM, FN = CFG::FN, PB = CFG::PB;
@@ -891,16 +863,9 @@ __device__ void gemm_fix_tile(const GemmFix<CFG, EPI>& f, int tile, float* smem)
         }
     }
   };
-  if constexpr (TGNX_FIX_PRE && HasFixPre<EPI>::value) {
-    const auto pr = f.epi.fix_pre(tl);
-    sum_tile();
-    __syncthreads();
-    f.epi(tl, pr);
-  } else {
-    sum_tile();
-    __syncthreads();
-    f.epi(tl);
-  }
+  sum_tile();
+  __syncthreads();
+  f.epi(tl);
 }
 template <class CFG, class EPI>
 __device__ __forceinline__ bool gemm_fix_dispatch(const GemmFix<CFG, EPI>& f, int& bid, float* smem) {
@@ -920,14 +885,11 @@ constexpr int GEMM_FIX_SMEM = 64 * 65 + 512;  // floats: the largest C tile (G64
 // Sum the partials of several deferred GEMMs (block ranges in argument order); the first `head` blocks
 // and the blocks past the GEMMs call `tail(bid, smem)` (bid: 0 .. head - 1, then head, head + 1, ...):
 // extra work that rides in the same launch, the head blocks dispatched first.
-// XCD-contiguous tiles (TGNX_FIX_XCD): the fix range is padded to a multiple of the 8 XCDs and XCD x takes
+// XCD-contiguous tiles: the fix range is padded to a multiple of the 8 XCDs and XCD x takes
 // the run [x nfix / 8, (x + 1) nfix / 8) of tiles in order, so the n-neighbour tiles of a weight row block run
 // on one XCD.  A 32-float tile row of a weight whose row length is not a multiple of 32 floats (572 + 1, 272,
 // 101, 100) straddles two 128-B lines shared with its neighbour tile; with bid-order tiles the neighbour ran on
 // another XCD and every Adam operand line (param, m, v) left HBM twice.
-#ifndef TGNX_FIX_XCD
-#define TGNX_FIX_XCD 1
-#endif
 template <class TAIL, class... F>
 __global__ void __launch_bounds__(256) gemm_fixup_kernel(TAIL tail, int head, int nfix, F... f) {
   TGNX_STAMP(23);
@@ -939,7 +901,7 @@ __global__ void __launch_bounds__(256) gemm_fixup_kernel(TAIL tail, int head, in
   }
   bid -= head;
   if (bid < nfix) {
-    if constexpr (TGNX_FIX_XCD) bid = (bid & 7) * (nfix >> 3) + (bid >> 3);
+    bid = (bid & 7) * (nfix >> 3) + (bid >> 3);
     (gemm_fix_dispatch(f, bid, smem) || ...);  // (padding blocks: past every GEMM's tiles)
     return;
   }
@@ -948,7 +910,7 @@ __global__ void __launch_bounds__(256) gemm_fixup_kernel(TAIL tail, int head, in
 template <class... F>
 inline int gemm_fix_range(const F&... f) {
   const int nt = (gemm_fix_blocks(f) + ... + 0);
-  return TGNX_FIX_XCD ? (nt + 7) & ~7 : nt;
+  return (nt + 7) & ~7;
 }
 struct NoTail {
   __device__ void operator()(int, float*) const {}

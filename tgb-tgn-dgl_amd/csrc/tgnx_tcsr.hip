@@ -19,11 +19,6 @@ namespace tgnx {
 namespace tcsr {
 
 constexpr int EID_BITS = 36;
-#ifndef TGNX_TCSR_GROUPS
-#define TGNX_TCSR_GROUPS 1  // K <= 32: G-lane groups per root (sample_recent_g); 0: a wave per root.  TGNX_TCSR_GROUPS
-                            // in the environment overrides (A/B; two roots per group in lockstep measured no faster:
-                            // wiki-shaped pass 43.6 vs 41.7 us, comment-shaped 3.49 vs 3.44 ms)
-#endif
 
 __global__ void build_keys(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                            const float* __restrict__ t, int64_t E, int add_reverse, uint64_t* __restrict__ key,
@@ -263,11 +258,7 @@ int tgnx_tcsr_sample(const int64_t* indptr, const int64_t* indices, const int64_
   if (Q == 0) return TGNX_OK;
   TGNX_CHECK_ARG(indptr && indices && eid && ts && roots && out_nbr && out_eid && out_t, "tgnx_tcsr_sample: null pointer");
   hipStream_t s = as_stream(stream);
-  static const int groups = [] {
-    const char* e = getenv("TGNX_TCSR_GROUPS");
-    return e && *e ? atoi(e) : TGNX_TCSR_GROUPS;
-  }();
-  if (K <= 32 && groups) {
+  if (K <= 32) {
     const int G = K <= 16 ? 16 : 32, per = 4 * (64 / G);
     const int grid = (int)std::min<int64_t>(8192, (Q + per - 1) / per);
     if (G == 16)

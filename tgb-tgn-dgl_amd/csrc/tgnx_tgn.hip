@@ -64,40 +64,6 @@ constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touc
 #define TGNX_DXE_DR TGNX_G32L_DR  // direct-operand slabs per round of the dX_enc GEMM (the 7-wave dW_cell launch)
 #endif
 using GXE = GemmCfg<TGNX_G32L_T, TGNX_G32L_T, TGNX_G32L_KC, TGNX_G32L_PF, TGNX_G32L_WS, TGNX_DXE_DR>;
-#ifndef TGNX_PRED_GLDS
-#define TGNX_PRED_GLDS 1  // predictor weights staged with global_load_lds (LDS-DMA) instead of through registers
-                          // (same-box A/B 0.0951 / 0.0951 -> 0.0945 / 0.0946 ms)
-#endif
-#ifndef TGNX_W3_JOBS_FIRST
-#define TGNX_W3_JOBS_FIRST 0  // dW_cell launch job order (0: dX_enc, dW_gru, dW_edge, dEnc; 1: dW_edge, dEnc first; 2: dEnc, dW_edge first)
-#endif
-#ifndef TGNX_DWE_AT7
-#define TGNX_DWE_AT7 0
-#endif
-#ifndef TGNX_KVF_ROOT
-#define TGNX_KVF_ROOT 0  // 2 hops: conv2's attention backward sums its edges' (dk, dv) too (no k / v reduction launch;
-                         // comment-shaped same-box A/B: 0.2433 / 0.2406 ms sorted, 0.2442 / 0.2406 unsorted, against
-                         // 0.2398 / 0.2381 with the k / v launch, whose dE2 GEMMs otherwise lengthen the dh1 launch)
-#endif
-#ifndef TGNX_KVF_ROOT_SORT
-#define TGNX_KVF_ROOT_SORT 1  // (with TGNX_KVF_ROOT) the root edges sorted by neighbour: plain stores for whole rows
-#endif
-#ifndef TGNX_DENSE_H
-#define TGNX_DENSE_H 1  // GRU train step: the GRU forward also stores its rows' pre-update memory densely ([M][D], Hp),
-                        // so the GRU backward and dW_gru read rows instead of gathering memory through node ids
-#endif
-#ifndef TGNX_SIN_RECOMPUTE
-#define TGNX_SIN_RECOMPUTE 1  // the backward's Δt-encoding sine recomputed from (w, lu - t, b), not an [E][D] round trip
-#endif
-#ifndef TGNX_KVE_EARLY
-#define TGNX_KVE_EARLY 1  // the attention backward's edge blocks load their sorted records in the edge count's round
-#endif
-#ifndef TGNX_EDGES_1ROUND
-#define TGNX_EDGES_1ROUND 1  // edge blocks read the level's edge count from the scan's counters (level_edges)
-#endif
-#ifndef TGNX_PRED_ATT_REC
-#define TGNX_PRED_ATT_REC 1  // per-root neighbour-row records for the attention in tgn_pred_train<ATT>
-#endif
 enum { CNT_R = 0, CNT_M = 1, CNT_E = 2, CNT_U = 3, CNT_LIST = 6, CNT_NB = 9, CNT_WORDS = 16 };  // (4, 5: unused)
 // ctl[ERR] bit of a step that found its scan-output set holding another batch (tgnx_tgn_train_step_pp)
 constexpr int64_t ERR_STALE_SET = 16;
@@ -172,52 +138,6 @@ struct AdamFuse {
   int keep_g = 1;  // fused: also store the gradient (0: TGNX_TGN_NO_GRAD_STORE, nothing reads it; 1.1 MB less per step)
   // n gradient elements (idx < 0: none) of one thread: every load issued before any store (the
   // buffers may alias as far as the compiler knows, so interleaving would serialise the elements)
-  // Two-phase form for the split-K fixup (gemm_fix_tile): pre_n issues the update's loads (the step flags, the step
-  // scalars and the elements' m, v, p) before the tile's partial sums, so they ride in the partials' load round
-  // instead of two dependent rounds after them; apply_n then needs no load.  Same arithmetic as put_n.
-  template <int N>
-  struct Pre {
-    float mm[N], vv[N], pp[N];
-    float s0, s1;
-    bool live;
-  };
-  template <int N>
-  __device__ __forceinline__ Pre<N> pre_n(const int64_t (&idx)[N]) const {
-    Pre<N> r;
-    r.live = false;
-    if (!p) return r;  // (a kernel argument: no load)
-    const int64_t nb = ctl[TGNX_CTL_B], er = ctl[TGNX_CTL_ERR];  // (both loads unconditional: no branch between)
-    r.live = (nb != 0) & (er == 0);
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int64_t j = idx[i] >= 0 ? idx[i] : 0;
-      r.mm[i] = m[j];
-      r.vv[i] = v[j];
-      r.pp[i] = p[j];
-    }
-    const float* sc = reinterpret_cast<const float*>(ctl + TGNX_CTL_ADAM_SC);
-    r.s0 = sc[0];
-    r.s1 = sc[1];
-    return r;
-  }
-  template <int N>
-  __device__ __forceinline__ void apply_n(float* g, const int64_t (&idx)[N], const float (&val)[N], Pre<N> r) const {
-    if (!r.live) {  // plain gradient store (no optimizer, or an empty batch)
-#pragma unroll
-      for (int i = 0; i < N; ++i)
-        if (idx[i] >= 0) g[idx[i]] = val[i];
-      return;
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      if (idx[i] < 0) continue;
-      adam1(val[i], r.mm[i], r.vv[i], r.pp[i], b1, b2, eps, r.s0, r.s1);
-      if (keep_g) st_wt(g + idx[i], val[i]);
-      st_wt(m + idx[i], r.mm[i]);
-      st_wt(v + idx[i], r.vv[i]);
-      st_wt(p + idx[i], r.pp[i]);
-    }
-  }
   template <int N>
   __device__ __forceinline__ void put_n(float* g, const int64_t (&idx)[N], const float (&val)[N]) const {
     // no update for an empty batch (a resident cursor past the split): the split-K fixup still finishes
@@ -254,25 +174,6 @@ struct AdamFuse {
     put_n<1>(g, ix, vx);
   }
 };
-// the fused-Adam weight-gradient epilogues' two-phase form for the split-K fixup (gemm_fix_tile, TGNX_FIX_PRE):
-// fix_pre(tile) issues the update's loads from the tile coordinates alone; operator()(tile, pre) then computes
-// the values and writes (an epilogue defining nx<T>() and items(t, ix, vx))
-#define TGNX_FIX_PRE_METHODS                                                  \
-  static constexpr int fix_pre_tag = 1;                                       \
-  template <class T>                                                          \
-  __device__ auto fix_pre(const T& t) const {                                 \
-    int64_t ix[nx<T>()];                                                      \
-    float vx[nx<T>()];                                                        \
-    items(t, ix, vx);                                                         \
-    return af.pre_n(ix);                                                      \
-  }                                                                           \
-  template <class T, class PR>                                                \
-  __device__ void operator()(const T& t, const PR& pr) const {                \
-    int64_t ix[nx<T>()];                                                      \
-    float vx[nx<T>()];                                                        \
-    items(t, ix, vx);                                                         \
-    af.apply_n(g, ix, vx, pr);                                                \
-  }
 struct Ctx {
   int64_t N, nev, words;
   int K, D, d, Qm, HC, C, aggr, Kn, drop, gen_neg;
@@ -317,7 +218,7 @@ struct Ctx {
                // the same values)
   int64_t* xw;
   float *gates, *Z0, *P, *Ep, *alpha, *Zc, *evs, *Hs, *Hd;
-  float* Hp;  // TGNX_DENSE_H (GRU train step): row m's pre-update memory mem[nid[m]] [M][D], written by the GRU forward
+  float* Hp;  // (GRU train step) row m's pre-update memory mem[nid[m]] [M][D], written by the GRU forward
   float *dZc, *dP, *dE, *dG, *tgp;
   // 1-hop train: the predictor accumulates the centres' output gradient into dzrep copies of dZc (dzstride floats
   // apart; workgroup b adds into copy b % dzrep), which the attention backward sums: a hub centre's row takes the
@@ -342,7 +243,7 @@ struct Ctx {
   int *kj, *kx, *ke;  // kvf: the sampled edges sorted by neighbour row (tgn_pred_train's sort block): row, centre, edge
   int kvs = 0;        // kvf: those arrays are this step's (else the edge blocks read the edges in sampling order)
   int ktr = 1;        // rows of kj / kx / ke (the train edge capacity)
-  float *encE, *sinE;  // per sampled edge: cos / sin of the Δt encoding argument [E][D]
+  float* encE;  // per sampled edge: the dense train edge row [cos of the Δt encoding argument | msg] [E][D + d]
   float *s0m, *s1m;    // per GRU row: (mean over its messages of) sin(arg), sin(arg) Δt  [M][D]
   float *pA, *pB, *pC, *pD;  // split-K partials of the deferred weight-gradient GEMMs
   uint64_t *rkeys, *skeys;
@@ -376,8 +277,6 @@ struct Ctx {
   int64_t* cent1;  // roots (sorted)
   int *r_x2, *ceoff1;                // root -> its outer-centre index (row of P2 / h1); root edge offsets
   int *e1_j, *e1_e2;                 // root edge -> neighbour's outer-centre index; -> outer edge index
-  int* e1_c;                         // (TGNX_KVF_ROOT) root edge -> its root index
-  float *alk1, *Qo1;                 // (TGNX_KVF_ROOT) conv2's alpha * keep per root edge, [q | o] per root
   int64_t* e1_id;                    // root edge -> event id
   float *P2, *Ep2, *alpha1, *Zr, *dZr, *dP2, *dE2, *pE, *pF;
   int R1cap, E1cap, tgp_e1;          // tgp rows of the root edges start at tgp_e1
@@ -399,11 +298,7 @@ constexpr int CNT_R1 = 7, CNT_E1 = 8;
 // the level's sampled-edge count (= ceoff[cnt[rsel]], written beside it by the scan): one load instead of two
 // dependent ones at the head of the edge blocks
 __device__ __forceinline__ int level_edges(const Ctx& c) {
-#if TGNX_EDGES_1ROUND
   return c.cnt[c.rsel == CNT_R1 ? CNT_E1 : CNT_E];
-#else
-  return c.ceoff[c.cnt[c.rsel]];
-#endif
 }
 
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
@@ -1721,25 +1616,10 @@ __device__ __forceinline__ int root_row(const Ctx& c, int64_t v) {
 // The rest: mode 0 aggregation over the sampled nodes (train) + zeroing of the backward
 // accumulators, mode 1 last_update of the sampled nodes from the buffer (eval scoring), mode 2
 // aggregation over a node list (eval update / flush; list == nullptr: nodes base + m).
-#ifndef TGNX_AGG_ZERO_EDGE
-#define TGNX_AGG_ZERO_EDGE 0  // 1: the backward accumulators zeroed by the sampled-edge blocks after their edges (0: by
-                              // the node blocks before their aggregation; same-box A/B 0.0885 / 0.0884 vs 0.0873 /
-                              // 0.0871 ms, agg_emit 10.9 vs 10.1 us: the edge blocks are not idle, profiles/r5/r5_agg_zero_ab.txt)
-#endif
-#ifndef TGNX_AGG_ZERO_VEC
-#define TGNX_AGG_ZERO_VEC 0  // 16-B stores for that zeroing (0: 4-B; 1 measured 0.0878 / 0.0876 vs 0.0871 / 0.0872 ms,
-                             // profiles/r5/r5_agg_caps_ab.txt)
-#endif
-// zero n floats at p as threads [t, t + nt) of the launch: 16-B stores over the aligned part
+// zero n floats at p as threads [t, t + nt) of the launch (4-B stores: 16-B ones, and the zeroing moved to the
+// edge blocks, measured slower, r5_agg_zero_ab.txt)
 __device__ __forceinline__ void zero_span(float* p, int64_t n, int64_t t, int64_t nt) {
-  int64_t head = 0;
-  if (TGNX_AGG_ZERO_VEC && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
-    const int64_t n4 = n >> 2;
-    float4* q = reinterpret_cast<float4*>(p);
-    for (int64_t x = t; x < n4; x += nt) q[x] = make_float4(0.f, 0.f, 0.f, 0.f);
-    head = n4 << 2;
-  }
-  for (int64_t x = head + t; x < n; x += nt) p[x] = 0.f;
+  for (int64_t x = t; x < n; x += nt) p[x] = 0.f;
 }
 // the atomically accumulated backward rows of a train step: dP; 1 hop the dZc copies; 2 hops dP2 (conv2 projections
 // of the outer centres) and the root level's dZr copies (dZc = dh1 is written whole by a GEMM)
@@ -1850,7 +1730,6 @@ __global__ void __launch_bounds__(256) TGNX_AGG_ATTR tgn_agg_emit(Ctx c, int mod
         if (x1 >= 0) {
           const int o1 = c.ceoff1[x1] + (o - c.ceoff[x]);
           c.e1_j[o1] = c.crank[ju];
-          if (TGNX_KVF_ROOT) c.e1_c[o1] = x1;
           c.e1_e2[o1] = o;
           c.e1_id[o1] = e;
         }
@@ -1864,16 +1743,8 @@ __global__ void __launch_bounds__(256) TGNX_AGG_ATTR tgn_agg_emit(Ctx c, int mod
         float mv[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) mv[i] = msg[min(lane + 64 * i, max(d - 1, 0))];  // (loads before the sincos)
-        for (int q = lane; q < D; q += 64) {
-          if constexpr (TGNX_SIN_RECOMPUTE) {
-            row[q] = te_cos(fmaf(tw[q], dt, tb[q]));
-          } else {
-            float sn, cs;
-            te_sincos(fmaf(tw[q], dt, tb[q]), sn, cs);
-            row[q] = cs;
-            c.sinE[(int64_t)o * D + q] = sn;
-          }
-        }
+        // (the backward recomputes the sine from the same argument, EpiTeEdge: no [E][D] sine round trip)
+        for (int q = lane; q < D; q += 64) row[q] = te_cos(fmaf(tw[q], dt, tb[q]));
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (lane + 64 * i < d) row[D + lane + 64 * i] = mv[i];
@@ -1882,8 +1753,6 @@ __global__ void __launch_bounds__(256) TGNX_AGG_ATTR tgn_agg_emit(Ctx c, int mod
         for (int q = lane; q < D; q += 64) c.encE[(int64_t)o * D + q] = te_cos(fmaf(tw[q], dt, tb[q]));
       }
     }
-    if (TGNX_AGG_ZERO_EDGE && mode == 0)  // (the node blocks, the launch's tail, keep only their aggregation)
-      zero_bwd_acc(c, ((int64_t)blockIdx.x - nevb - nnode) * blockDim.x + threadIdx.x, (int64_t)nedge * blockDim.x);
     return;
   }
   const int bid = blockIdx.x - nevb, nb = nnode;
@@ -1892,7 +1761,7 @@ __global__ void __launch_bounds__(256) TGNX_AGG_ATTR tgn_agg_emit(Ctx c, int mod
     for (int x = bid * blockDim.x + threadIdx.x; x < M; x += nb * blockDim.x) c.lu[x] = (float)c.lu_buf[c.nid[x]];
     return;
   }
-  if (mode == 0 && (!TGNX_AGG_ZERO_EDGE || nedge == 0))  // zero the atomically accumulated backward rows
+  if (mode == 0)  // zero the atomically accumulated backward rows
     zero_bwd_acc(c, bid * (int64_t)blockDim.x + threadIdx.x, (int64_t)nb * blockDim.x);
   const int n = mode == 0 ? c.cnt[CNT_M] : (list_cnt ? *list_cnt : n_host);
   if (AG != 0 && c.aggr == 1 && (mode == 0 || list)) {  // MeanAggregator, train / eval update: a workgroup per node (hub
@@ -1972,7 +1841,7 @@ struct EpiGru {
   int64_t base;
   int D;
   float *Z0, *gates;
-  float* Hp = nullptr;  // (train step, TGNX_DENSE_H) the row's pre-update memory, stored densely
+  float* Hp = nullptr;  // (train step) the row's pre-update memory, stored densely
   // thread x < 64 of a 16 x 16 tile: row x / 4, unit n0 / 4 + x % 4 — its biases and memory entry, loaded
   // with the tile's first operand round (gemm_tile_direct); rowidx(r) = row r's node (LoadGruA's index)
   struct Pre {
@@ -2302,10 +2171,6 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
       v0[u] = Pj[2 * HC + l0] + ea;
       v1[u] = Pj[2 * HC + C + l0] + eb;
     }
-#ifdef TGNX_ATT_CK  // diagnostic: the edge rows landed
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ck(0);
-#endif
     // (no early exit: a runtime `break` kept these loops rolled — indexed register reads, one edge's reduction
     // after another; the clamped rows of edges >= ne are reduced and discarded)
 #pragma unroll
@@ -2313,9 +2178,6 @@ __device__ __forceinline__ float2 attn_centre(const Ctx& c, int x, int i, int e0
       const float p0 = wave_sum_f(q0 * k0[u] * on), p1 = wave_sum_f(q1 * k1[u] * on);
       if (lane == u && u < ne) { my0 = p0; my1 = p1; }
     }
-#ifdef TGNX_ATT_CK  // diagnostic: the scores computed
-    ck(1);
-#endif
     // the scale once per lane (lane e holds edge e's scores): the same quotients as per edge, one division
     // instead of one (a ~10-instruction dependent sequence) per edge and head
     if (lane < ne) { my0 /= sqc; my1 /= sqc; }
@@ -2570,32 +2432,10 @@ __global__ void __launch_bounds__(1024) tgn_plan_table_kernel(Ctx c, char* tab, 
   if (B <= 0) return;
   plan_part<8>(c, role < P ? 0 : 1, role % P, P, B, start, psm_, sh, NoCheckpoint{}, plan_slot(tab, stride, c.Bplan, b));
 }
-#ifndef TGNX_PRED_PSUM1
-#define TGNX_PRED_PSUM1 0  // the forward's 8 partial sums reduced once per workgroup, not by every wave
-#endif
-#ifndef TGNX_PRED_ZHOIST
-#define TGNX_PRED_ZHOIST 1  // the forward contraction's embedding slices held in registers across both output rounds
-#endif
 constexpr int ZH_MAX = 4;  // float4 columns per wave it holds (D <= 128 at 8 waves)
-#ifndef TGNX_PRED_DMA_WAIT_BUILTIN
-#define TGNX_PRED_DMA_WAIT_BUILTIN 1
-#endif
-#ifndef TGNX_PRED_DEFER
-#define TGNX_PRED_DEFER 1  // the 1-hop attention's global stores issued after the first barrier (0: inside attn_centre)
-#endif
-// diagnostic checkpoint placement (stamps build, wave 0's view): TGNX_PRED_CKPT 0 = after the forward contraction's
-// barrier / after the epilogue; 1 = wave 0 done staging / the first barrier passed; 2 = the backward done / the dZc
-// atomics issued; 3 (with TGNX_STAMP_TID 64) = wave 1's first round landed / its attention done
-#ifndef TGNX_PRED_CKPT
-#define TGNX_PRED_CKPT 0
-#endif
 // waves per workgroup: 1 hop (ATT) 8 — waves 1-3 the roots' attention, waves 0 and 4-7 the weight staging, then
 // all 8 share the contractions (the workgroup is alone on its CU: one wave per SIMD left each dependent step's
 // latency exposed, measured 38 % of the waves' cycles issuing); 2 hops 4
-#ifndef TGNX_PRED_WIDE_ATOM
-#define TGNX_PRED_WIDE_ATOM 1  // the predictor's dZc adds as whole-row wave instructions through LDS (one more barrier;
-                               // same-box A/B: predictor 14.1 -> 12.6-13.1 us, step -1 %)
-#endif
 #ifndef TGNX_DZC_REP
 #define TGNX_DZC_REP 4  // 1-hop train: copies of dZc the predictor's workgroups spread their atomics over (a wiki batch's hub
                         // centre is the root of ~90 of its 600 root slots: its row's adds serialise at the memory side;
@@ -2603,16 +2443,6 @@ constexpr int ZH_MAX = 4;  // float4 columns per wave it holds (D <= 128 at 8 wa
                         // compile-time unrolled loads in the same round (tgn_attn_bwd<EB, REP>).  Same-box A/B
                         // (profiles/r5/r5_dzc_rep_ab.txt): predictor 12.7-12.9 -> 11.6 us, attention backward +0.5,
                         // step 0.0926 / 0.0928 -> 0.0922 / 0.0922 ms; 8 copies: attention backward +1.3, step 0.0932
-#endif
-#ifndef TGNX_DZR_REP
-#define TGNX_DZR_REP 1  // 2 hops: copies of the root level's dZr for the predictor's adds (1 or TGNX_DZC_REP; 4: comment-shaped
-                        // 2-hop step 0.2770 / 0.2762 -> 0.2942 / 0.2899 ms, profiles/r5/r5_dzr_rep_ab.txt)
-#endif
-#ifndef TGNX_ATT_PAIR
-#define TGNX_ATT_PAIR 1  // the predictor's attention in the paired-channel lane layout (attn_root_pair)
-#endif
-#ifndef TGNX_BWD_PAIR
-#define TGNX_BWD_PAIR 0  // the attention backward (centre and edge blocks) in that layout: measured slower (12.0 -> 12.2-12.5 us)
 #endif
 #ifndef TGNX_PRED_WAVES
 #define TGNX_PRED_WAVES 8  // 1-hop predictor workgroup waves (4: the round-4 layout, one staging wave)
@@ -2677,17 +2507,9 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     const int jr = c.evj ? c.evj[(3 * slot + r) * 16 + (lane & 15)] : -1;  // the edges' neighbour rows
     if (!live) return;
     bool paired = false;
-#if TGNX_ATT_PAIR
     if (c.evj && q.w - q.z <= EB && (c.C & 1) == 0 && c.C <= 64) {
       paired = true;
-#if TGNX_PRED_CKPT == 3
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      TGNX_STAMP_AT(0);
-#endif
       const float2 o = attn_root_pair<EB>(c, q.x, q.y, q.z, q.w - q.z, lane, max(jr, 0), &asp);
-#if TGNX_PRED_CKPT == 3
-      TGNX_STAMP_AT(1);
-#endif
       if (asp.chan >= 0) {
         z[r][asp.chan] = o.x;
         z[r][asp.chan + 1] = o.y;
@@ -2698,22 +2520,9 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
       }
       if (lane == 0) scr[r] = q.x;
     }
-#endif
     if (!paired) {
-#if TGNX_PRED_CKPT == 3
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      TGNX_STAMP_AT(0);
-#endif
-#if TGNX_PRED_CKPT == 4  // (diagnostic, with TGNX_STAMP_TID 64 and TGNX_ATT_CK: wave 1's edge rows landed / scores done)
       const float2 o = attn_centre<true, EB>(c, q.x, q.y, q.z, q.w - q.z, lane, c.evj && q.w - q.z <= 16 ? max(jr, 0) : -1,
-                                             TGNX_PRED_DEFER ? &ast : nullptr, [&](int slot) { TGNX_STAMP_AT(slot); });
-#else
-      const float2 o = attn_centre<true, EB>(c, q.x, q.y, q.z, q.w - q.z, lane, c.evj && q.w - q.z <= 16 ? max(jr, 0) : -1,
-                                             TGNX_PRED_DEFER ? &ast : nullptr);
-#endif
-#if TGNX_PRED_CKPT == 3
-      TGNX_STAMP_AT(1);
-#endif
+                                             &ast);
       if (lane < c.C) {
         z[r][lane] = o.x;
         z[r][c.C + lane] = o.y;
@@ -2751,10 +2560,6 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     const float4* S4 = reinterpret_cast<const float4*>(c.params + c.L.lsw);
     const float4* D4 = reinterpret_cast<const float4*>(c.params + c.L.ldw);
     bool staged = false;
-#ifdef TGNX_PRED_DIAG_NOSTAGE  // diagnostic only (wrong results): no weight staging at all
-    staged = true;
-#endif
-#if TGNX_PRED_GLDS
     if (ATT && flat && !staged) {  // the LDS image is the global one: global_load_lds_dwordx4 straight into it, no
                                    // registers, every row in flight at once (the waves drain them before the barrier)
       for (int x0 = 0; x0 < n4; x0 += NST) {
@@ -2778,14 +2583,9 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
       // (the barrier below waits for LDS only).  The builtin, not inline asm: the compiler then knows the LDS-DMA
       // has landed, else it keeps it pending past the join with the attention waves and puts a vmcnt(0) before the
       // next LDS read — which waits on the attention's deferred global stores too
-#if TGNX_PRED_DMA_WAIT_BUILTIN
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15 = no wait)
-#else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
       staged = true;
     }
-#endif
     for (int b0 = 0; b0 < n4 && !staged; b0 += NST * PRED_SU) {
       float4 ws4[PRED_SU], wd4[PRED_SU];
 #pragma unroll
@@ -2831,22 +2631,14 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     }
     }  // first
   }
-#if TGNX_PRED_CKPT == 1
-  TGNX_STAMP_AT(0);
-#endif
   // LDS-only barriers in this kernel (the weights, embedding rows and partial sums are LDS; the attention's
   // alpha stores and the evs rows need not have landed): __syncthreads would wait for vmcnt(0)
-#if TGNX_PRED_DMA_WAIT_BUILTIN
   // (every wave's loads are consumed here and no store is in flight yet: a free wait that leaves the compiler's
   // scoreboard empty at the join, so the deferred stores below are not waited for at the next barrier)
   __builtin_amdgcn_s_waitcnt(0x0F70);
-#endif
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-#if TGNX_PRED_CKPT == 1
-  TGNX_STAMP_AT(1);
-#endif
-  if (ATT && TGNX_PRED_DEFER && ast.x >= 0) ast.issue(c, lane);
+  if (ATT && ast.x >= 0) ast.issue(c, lane);
   if (ATT && asp.x >= 0) asp.issue(c, lane);
   const int cr[3] = {scr[0], scr[1], scr[2]};
   // lin_src(z_s), lin_dst(z_p), lin_dst(z_n), split over the hidden units' inputs k: NW partial sums per output
@@ -2855,7 +2647,6 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     const float4* z0 = reinterpret_cast<const float4*>(z[0]) + q0;
     const float4* z1 = reinterpret_cast<const float4*>(z[1]) + q0;
     const float4* z2 = reinterpret_cast<const float4*>(z[2]) + q0;
-#if TGNX_PRED_ZHOIST
     // the three embedding slices (wave-uniform) read once into registers for both output rounds: the LDS
     // reads were 3 broadcast b128 per 2 weight b128, twice
     if (NW == 8 && kq <= ZH_MAX) {
@@ -2889,7 +2680,6 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
         }
       }
     } else
-#endif
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int o = lane + 64 * q;
@@ -2930,9 +2720,7 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-#if TGNX_PRED_CKPT == 0
   TGNX_STAMP_AT(0);
-#endif
   float* ev = c.evs + (int64_t)i * evs_stride(D);
   // every wave runs the forward epilogue (the same values in each: no dh round through a barrier) and keeps its own
   // copy of dh; wave 0 stores the event's row, outputs and loss term (they drain during the backward)
@@ -2950,32 +2738,14 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
       return s;
     };
     float zp = 0.f, zn = 0.f;
-#if TGNX_PRED_PSUM1
-    // the 8 waves' partials summed once (thread per (root, output), into part[0]) instead of by every wave
-    if (NW == 8) {
-      for (int x = tid; x < 3 * D; x += 64 * NW) {
-        const int r = x >= 2 * D ? 2 : x >= D ? 1 : 0, o = x - r * D;
-        part[0][r][o] = psum(r, o) + (r == 0 ? vsb[o] : vdb[o]);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-#endif
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int o = lane + 64 * q;
       hp[q] = hn[q] = 0.f;
       if (o < D) {
-#if TGNX_PRED_PSUM1
-        const bool one = NW == 8;
-        const float s = one ? part[0][0][o] : psum(0, o) + vsb[o];
-        const float dp = one ? part[0][1][o] : psum(1, o) + vdb[o];
-        const float dn = one ? part[0][2][o] : psum(2, o) + vdb[o];
-#else
         const float s = psum(0, o) + vsb[o];
         const float dp = psum(1, o) + vdb[o];
         const float dn = psum(2, o) + vdb[o];
-#endif
         hp[q] = fmaxf(s + dp, 0.f);
         hn[q] = fmaxf(s + dn, 0.f);
         zp += vfw[o] * hp[q];
@@ -3027,9 +2797,7 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
       }
     }
   }
-#if TGNX_PRED_CKPT == 0
   TGNX_STAMP_AT(1);
-#endif
   {
     // dz_s = Wsrcᵀ (dhp + dhn), dz_p = Wdstᵀ dhp, dz_n = Wdstᵀ dhn for the outputs [wv ow, wv ow + ow) of this
     // wave: lanes = KG groups of the hidden units x OL outputs, dh from this wave's own LDS copy, the groups summed
@@ -3057,11 +2825,7 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     a = swap32_sum(a);
     b = swap32_sum(b);
     d2 = swap32_sum(d2);
-#if TGNX_PRED_CKPT == 2
-    TGNX_STAMP_AT(0);
-#endif
     float* dz = c.dZc + (int64_t)(slot % c.dzrep) * c.dzstride;
-#if TGNX_PRED_WIDE_ATOM
     // the three rows gathered in LDS first, then added with whole-row wave instructions (contiguous lanes: 6 per
     // workgroup instead of 3 per wave on 13-lane segments — every one of them queues on a hub centre's row)
     __shared__ float dzl[3][TDMAX];
@@ -3074,28 +2838,8 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     __builtin_amdgcn_s_barrier();
     for (int x = tid; x < 3 * D; x += 64 * NW) {
       const int r = x >= 2 * D ? 2 : x >= D ? 1 : 0, oo = x - r * D;
-#ifdef TGNX_PRED_DIAG_NOATOM  // diagnostic only (wrong sums): plain stores instead of the dZc atomics
-      dz[(int64_t)cr[r] * D + oo] = dzl[r][oo];
-#else
       atomicAdd(&dz[(int64_t)cr[r] * D + oo], dzl[r][oo]);
-#endif
     }
-#else
-    if (kg == 0 && oko) {
-#ifdef TGNX_PRED_DIAG_NOATOM  // diagnostic only (wrong sums): plain stores instead of the dZc atomics
-      dz[(int64_t)cr[0] * D + o] = a;
-      dz[(int64_t)cr[1] * D + o] = b;
-      dz[(int64_t)cr[2] * D + o] = d2;
-#else
-      atomicAdd(&dz[(int64_t)cr[0] * D + o], a);
-      atomicAdd(&dz[(int64_t)cr[1] * D + o], b);
-      atomicAdd(&dz[(int64_t)cr[2] * D + o], d2);
-#endif
-    }
-#endif
-#if TGNX_PRED_CKPT == 2
-    TGNX_STAMP_AT(1);
-#endif
   }
   if (ATT || lo + slot + G >= hi) break;  // (ATT: one event per workgroup — the loop's live ranges spilled the
                                            // 8-wave kernel: 168 -> 256 VGPRs + 47 spilled, predictor 12 -> 20 us)
@@ -3147,22 +2891,13 @@ __device__ void lp_vec_body(const Ctx& c, int y, int lane) {
 #define TGNX_KVE_CH 32
 #endif
 constexpr int KVE_CH = TGNX_KVE_CH, KVE_PW = KVE_CH / 4;
-#ifndef TGNX_KVF_2HOP
-#define TGNX_KVF_2HOP 1  // 2 hops: the outer level's attention backward sums its edges' (dk, dv) too
-#endif
-#ifndef TGNX_KVE_GSORT
-#define TGNX_KVE_GSORT 1  // edges globally sorted by neighbour (edge_sort_body in the predictor launch)
-#endif
-#ifndef TGNX_KVE_MERGE
-#define TGNX_KVE_MERGE 1  // runs crossing the workgroup's waves merged in LDS before their atomics
-#endif
 #ifndef TGNX_KVE_B
 #define TGNX_KVE_B 8
 #endif
 constexpr int KVE_B = TGNX_KVE_B < KVE_PW ? TGNX_KVE_B : KVE_PW;  // edges per load batch of a wave
-// PAIR: the paired-channel lane layout (attn_root_pair): lane (h, j) carries channels 2j, 2j + 1 of head h, so one
-// 32-lane reduction per edge serves both heads and the rows move as float2 (C even, C <= 64)
-template <bool PAIR, int REP = 1>
+// (lane l carries channel l of both heads; the paired-channel layout of attn_root_pair measured slower here:
+// attention backward 12.0 -> 12.2-12.5 us)
+template <int REP = 1>
 __device__ void kv_edge_body(const Ctx& c, int bid) {
   const int B = (int)c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
@@ -3170,7 +2905,6 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
   const int eb = bid * KVE_CH;
   const int t = threadIdx.x;
   const bool gs = c.kvs;  // workgroup-uniform
-#if TGNX_KVE_EARLY
   // globally sorted edges: the chunk's records (and the keys just outside it) loaded in the edge count's round,
   // clamped to the sorted arrays' rows (ktr) and masked by the count after
   int kj0 = 0, kx0 = 0, ke0 = 0, kb = -1;
@@ -3186,13 +2920,11 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
       kb = c.kj[min(eb + KVE_CH, c.ktr - 1)];
     }
   }
-#endif
   if (eb >= E) return;  // whole workgroup
   const int ne = min(KVE_CH, E - eb);
   __shared__ int sj[KVE_CH], sx[KVE_CH], se[KVE_CH], sorder[KVE_CH], sb[2];
   // globally sorted: a run whose row has no edge in the neighbouring chunks is the row's whole sum (a plain
   // store); the chunk's first / last runs may continue there (the keys just outside the chunk tell)
-#if TGNX_KVE_EARLY
   if (gs) {
     if (t == KVE_CH) sb[0] = kb;
     if (t == KVE_CH + 1) sb[1] = eb + ne < E ? kb : -1;  // (ne < KVE_CH: eb + ne = E)
@@ -3207,17 +2939,6 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
     sx[t] = c.e_c[ec];
     se[t] = ec;
   }
-#else
-  if (gs && t == KVE_CH) sb[0] = eb > 0 ? c.kj[eb - 1] : -1;
-  if (gs && t == KVE_CH + 1) sb[1] = eb + ne < E ? c.kj[eb + ne] : -1;
-  if (t < KVE_CH) {  // the edge's neighbour (sort key), centre and id, one round
-    const int ec = min(eb + t, E - 1);
-    const int j = gs ? c.kj[ec] : c.e_j[ec], x = gs ? c.kx[ec] : c.e_c[ec], eo = gs ? c.ke[ec] : ec;
-    sj[t] = t < ne ? j : INT_MAX;
-    sx[t] = x;
-    se[t] = eo;
-  }
-#endif
   __syncthreads();
   if (t < ne) {  // stable rank of (neighbour, edge)
     const int key = sj[t];
@@ -3232,7 +2953,6 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
   __syncthreads();
   const int w = t >> 6, lane = t & 63;
   const int i0 = w * KVE_PW;
-#if TGNX_KVE_MERGE
   // a wave's first and last runs may continue in the neighbouring waves: they go to LDS pieces (slots 2w, 2w + 1,
   // key -1 = none), merged in wave order by wave 0 before their atomics
   __shared__ float ps[8][4][64];
@@ -3241,18 +2961,13 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
     if (lane == 0) pk[2 * w] = pk[2 * w + 1] = -1;
   }
   const int n = max(0, min(KVE_PW, ne - i0));
-#else
-  if (i0 >= ne) return;
-  const int n = min(KVE_PW, ne - i0);
-#endif
   const int C = c.C, HC = c.HC;
   // this lane's two channels (oA, oB within HC; clamped for loads) and head of each
-  const int hc = C >> 1, ph = lane >> 5, pj = lane & 31;
-  const bool okl = PAIR ? pj < hc : lane < C;
+  const bool okl = lane < C;
   const float on = f01(okl);
-  const int l0 = min(lane, C - 1), pc = ph * C + 2 * (pj < hc ? pj : hc - 1);
-  const int oA = PAIR ? pc : l0, oB = PAIR ? pc + 1 : C + l0;
-  const int hA = PAIR ? ph : 0, hB = PAIR ? ph : 1;
+  const int l0 = min(lane, C - 1);
+  const int oA = l0, oB = C + l0;
+  constexpr int hA = 0, hB = 1;
   const float isq = 1.0f / sqrtf((float)C);
   float s[4] = {0.f, 0.f, 0.f, 0.f};  // run sums: dk (head 0, 1), dv (head 0, 1)
   int jc = n > 0 ? sj[sorder[i0]] : -1;
@@ -3290,7 +3005,7 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
     float g0[KVE_B], g1[KVE_B], q0[KVE_B], q1[KVE_B], o0[KVE_B], o1[KVE_B], v0[KVE_B], v1[KVE_B];
 #pragma unroll
     for (int u = 0; u < KVE_B; ++u) {  // softmax weights, centre rows (g, q, o), the neighbour's v row + edge row
-      a0[u] = c.alpha[(int64_t)er[u] * 2 + hA];   // (PAIR: the lane's head for both channels)
+      a0[u] = c.alpha[(int64_t)er[u] * 2 + hA];
       a1[u] = c.alpha[(int64_t)er[u] * 2 + hB];
       t0[u] = c.alk[(int64_t)er[u] * 2 + hA];
       t1[u] = c.alk[(int64_t)er[u] * 2 + hB];
@@ -3318,21 +3033,15 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
     float gv0[KVE_B], gv1[KVE_B], go0[KVE_B], go1[KVE_B];
 #pragma unroll
     for (int u = 0; u < KVE_B; ++u) {
-      if (PAIR) {  // each 32-lane half sums its own head: both channels of a lane share it
-        gv0[u] = gv1[u] = half_sum_f((g0[u] * v0[u] + g1[u] * v1[u]) * on);
-        go0[u] = go1[u] = half_sum_f((g0[u] * o0[u] + g1[u] * o1[u]) * on);
-      } else {
-        gv0[u] = wave_sum_f(g0[u] * v0[u] * on);
-        gv1[u] = wave_sum_f(g1[u] * v1[u] * on);
-        go0[u] = wave_sum_f(g0[u] * o0[u] * on);
-        go1[u] = wave_sum_f(g1[u] * o1[u] * on);
-      }
+      gv0[u] = wave_sum_f(g0[u] * v0[u] * on);
+      gv1[u] = wave_sum_f(g1[u] * v1[u] * on);
+      go0[u] = wave_sum_f(g0[u] * o0[u] * on);
+      go1[u] = wave_sum_f(g1[u] * o1[u] * on);
     }
 #pragma unroll
     for (int u = 0; u < KVE_B; ++u) {
       if (u >= nb) continue;
       if (jj[u] != jc) {  // wave-uniform run boundary
-#if TGNX_KVE_MERGE
         if (first) {
           for (int q = 0; q < 4; ++q) ps[2 * w][q][lane] = s[q];
           if (lane == 0) pk[2 * w] = jc;
@@ -3341,9 +3050,6 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
           if (gs) store();
           else flush();
         }
-#else
-        flush();
-#endif
         s[0] = s[1] = s[2] = s[3] = 0.f;
         jc = jj[u];
       }
@@ -3361,7 +3067,6 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
       s[3] += dv1;
     }
   }
-#if TGNX_KVE_MERGE
   if (n > 0) {  // the open run: the wave's only (slot 2w) or its last (slot 2w + 1)
     const int sl = first ? 2 * w : 2 * w + 1;
     for (int q = 0; q < 4; ++q) ps[sl][q][lane] = s[q];
@@ -3393,9 +3098,6 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
     if (gs && !(firstg && jc == kprev) && jc != knext) store();
     else flush();
   }
-#else
-  flush();
-#endif
 }
 
 // Backward of tgn_attn_fwd (wave per centre) ‖ [nkv > 0: kv_edge_body blocks; the centre waves then write
@@ -3404,7 +3106,7 @@ __device__ void kv_edge_body(const Ctx& c, int bid) {
 // coalesced stores) and summed into dP by tgn_kv_reduce: a hub neighbour is shared by most centres (a
 // wiki-shaped hub user sits in ~40 % of the page rings), and per-edge global atomics on its row
 // serialised at the L2 (attn_bwd 36 us, 15 us without them).
-// nwalk (parity-set steps with a plan table, TGNX_WALK_AT 1): the last block walks the NEXT batch's node sets
+// nwalk (1-hop parity-set steps with a plan table): the last block walks the NEXT batch's node sets
 // into the other parity's set (cw; the plans come from the table), instead of a workgroup of the dW_cell launch
 template <int EB, int REP = 1>
 __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int nwalk, Ctx cw) {
@@ -3419,8 +3121,7 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
     return;
   }
   if ((int)blockIdx.x >= ncb) {
-    if (TGNX_BWD_PAIR && (c.C & 1) == 0 && c.C <= 64) kv_edge_body<true, REP>(c, (int)blockIdx.x - ncb);
-    else kv_edge_body<false, REP>(c, (int)blockIdx.x - ncb);
+    kv_edge_body<REP>(c, (int)blockIdx.x - ncb);
     return;
   }
   const bool wkv = nkv == 0;  // per-edge dk / dv / dE written here (else by the edge blocks)
@@ -3471,66 +3172,6 @@ __global__ void __launch_bounds__(256) tgn_attn_bwd(Ctx c, int ncb, int nkv, int
   if (lane < ne && c.drop) {
     k0v = att_keep(c, seed, x, e0 + lane, 0);
     k1v = att_keep(c, seed, x, e0 + lane, 1);
-  }
-  if (TGNX_BWD_PAIR && ne > 0 && ne <= EB && (C & 1) == 0 && C <= 64) {
-    // the paired-channel lane layout of attn_root_pair: lanes 0-31 head 0, 32-63 head 1, two channels per lane;
-    // one 32-lane reduction per edge for both heads' d alpha, float2 rows
-    const int hh = lane >> 5, jj = lane & 31, hc = C >> 1;
-    const bool act = jj < hc;
-    const int ch = hh * C + 2 * (act ? jj : hc - 1);
-    const float onp = f01(act);
-    float2 g = *reinterpret_cast<const float2*>(c.dZc + (int64_t)x * HC + ch);
-#pragma unroll
-    for (int rp = 1; rp < REP; ++rp) {  // (the predictor's dZc copies, in copy order)
-      const float2 gr = *reinterpret_cast<const float2*>(c.dZc + rp * c.dzstride + (int64_t)x * HC + ch);
-      g.x += gr.x;
-      g.y += gr.y;
-    }
-    g.x *= onp;
-    g.y *= onp;
-    const float2 qp = *reinterpret_cast<const float2*>(Pi + ch);
-    float2 kk[EB], vv[EB];
-#pragma unroll
-    for (int u = 0; u < EB; ++u) {
-      const int e = min(u, ne - 1);
-      const float* Pj = c.P + (int64_t)lane_i(jl, e) * 4 * HC;
-      const float2 ee = *reinterpret_cast<const float2*>(c.Ep + (int64_t)(e0 + e) * HC + ch);
-      const float2 k2 = *reinterpret_cast<const float2*>(Pj + HC + ch);
-      const float2 v2 = *reinterpret_cast<const float2*>(Pj + 2 * HC + ch);
-      kk[u] = make_float2(k2.x + ee.x, k2.y + ee.y);
-      vv[u] = make_float2(v2.x + ee.x, v2.y + ee.y);
-    }
-    float da0 = 0.f, da1 = 0.f;
-#pragma unroll
-    for (int u = 0; u < EB; ++u) {
-      const float pr = half_sum_f(g.x * vv[u].x + g.y * vv[u].y);
-      const float p0 = lane_f(pr, 0), p1 = lane_f(pr, 32);
-      if (lane == u && u < ne) { da0 = p0 * k0v; da1 = p1 * k1v; }
-    }
-    const float s0 = wave_sum_f(a0 * da0), s1 = wave_sum_f(a1 * da1);
-    const float ds0 = a0 * (da0 - s0), ds1 = a1 * (da1 - s1);
-    const float t0 = a0 * k0v, t1 = a1 * k1v;
-    const float dq0s = ds0 / sqc, dq1s = ds1 / sqc;
-    float2 dq = make_float2(0.f, 0.f);
-#pragma unroll
-    for (int u = 0; u < EB; ++u) {  // (lanes >= ne hold ds = 0: the clamped rows add exact zeros to dq)
-      const float d = hh ? lane_f(dq1s, u) : lane_f(dq0s, u);
-      dq.x += d * kk[u].x;
-      dq.y += d * kk[u].y;
-      if (act && wkv && u < ne) {
-        const float b = hh ? lane_f(t1, u) : lane_f(t0, u);
-        const float2 dk = make_float2(d * qp.x, d * qp.y), dv = make_float2(b * g.x, b * g.y);
-        *reinterpret_cast<float2*>(c.dE + (int64_t)(e0 + u) * HC + ch) = make_float2(dk.x + dv.x, dk.y + dv.y);
-        float* dKe = c.dKV + (int64_t)(e0 + u) * 2 * HC;  // [dk (HC) | dv (HC)]
-        *reinterpret_cast<float2*>(dKe + ch) = dk;
-        *reinterpret_cast<float2*>(dKe + HC + ch) = dv;
-      }
-    }
-    if (act) {
-      *reinterpret_cast<float2*>(dPi + ch) = dq;
-      *reinterpret_cast<float2*>(dPi + 3 * HC + ch) = g;
-    }
-    return;
   }
   if (ne > 0 && ne <= EB) {  // every ring of K <= 16: v, k and edge rows of all edges in one round
     float kk0[EB], kk1[EB], v0[EB], v1[EB];
@@ -3764,7 +3405,6 @@ struct EpiProjGrad {
     items(t, ix, vx);
     af.put_n(g, ix, vx);
   }
-  TGNX_FIX_PRE_METHODS
 };
 // plain row-major weight gradient (lin_edge): g[off + m ldc + n]
 struct EpiGradStore {
@@ -3791,7 +3431,6 @@ struct EpiGradStore {
     items(t, ix, vx);
     af.put_n(g, ix, vx);
   }
-  TGNX_FIX_PRE_METHODS
 };
 // link predictor weight grads as one GEMM over 3 * nloc rows (block-diagonal K):
 // rows r < D: dW_src = Σ (dhp + dhn) zsᵀ ; rows r >= D: dW_dst = Σ dhp zpᵀ + dhn znᵀ
@@ -3846,7 +3485,6 @@ struct EpiLpGrad {
     items(t, ix, vx);
     af.put_n(g, ix, vx);
   }
-  TGNX_FIX_PRE_METHODS
 };
 // Δt-encoding parameter grads from a tile of d(encoding) (dA): per row-tile partials
 //   tgp[row][n] = Σ_r -dA[r][n] S1[r][n],  tgp[row][D + n] = Σ_r -dA[r][n] S0[r][n]
@@ -3884,12 +3522,12 @@ __device__ __forceinline__ void te_tile_grad(const T& t, const float* S0, const 
 // (map != nullptr: rows are root edges, their Δt data that of the outer edge map[e]; partial rows from row0)
 struct EpiTeEdge {
   const int* e_j;
-  const float *e_t, *lu, *sinE;
+  const float *e_t, *lu;
   float* tgp;
   int D;
   const int* map = nullptr;
   int row0 = 0;
-  const float *tw = nullptr, *tb = nullptr;  // TGNX_SIN_RECOMPUTE: the time encoder (sin from Δt, not sinE)
+  const float *tw = nullptr, *tb = nullptr;  // the time encoder: the sine recomputed from Δt
   template <class T>
   __device__ void operator()(const T& t) const {
     constexpr int groups = 256 / T::tn, per = T::tm / groups;
@@ -3907,12 +3545,10 @@ struct EpiTeEdge {
       const bool ok = e < t.M && n < t.N;
       ej[i] = ok ? e_j[e2[i]] : 0;
       et[i] = ok ? e_t[e2[i]] : 0.f;
-      if constexpr (!TGNX_SIN_RECOMPUTE) sn[i] = ok ? sinE[(int64_t)e2[i] * D + n] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < per; ++i) dt[i] = lu[ej[i]] - et[i];
-    if constexpr (TGNX_SIN_RECOMPUTE) {
-      // the forward's own argument (tgn_agg_emit: fmaf(w, lu - t, b), same lu / t), so the same sin
+    {  // the forward's own argument (tgn_agg_emit: fmaf(w, lu - t, b), same lu / t), so the same sin
       const int nc = min(n, D - 1);
       const float w = tw[nc], b = tb[nc];
 #pragma unroll
@@ -3965,7 +3601,7 @@ struct EpiGruBwd {
   const int64_t* nid;
   float* dG;
   int D;
-  const float* Hp = nullptr;  // TGNX_DENSE_H: the rows' pre-update memory (no node-id gather)
+  const float* Hp = nullptr;  // the rows' pre-update memory, stored densely by the GRU forward (no node-id gather)
   // a 16 x 16 tile's element of this thread (GemmTile<16, 16>::row_of / col_of (0)): its node and saved gates,
   // loaded with the tile's first operand round (gemm_tile_direct)
   struct Pre {
@@ -4039,7 +3675,7 @@ struct LoadGruAT1 {
     return *(x ? X + (int64_t)m * Qm + n : one ? kOne4 : mem + v * D + (n - Qm));
   }
 };
-// the same with the rows' pre-update memory stored densely (TGNX_DENSE_H): no node-id round per K chunk
+// the same with the rows' pre-update memory stored densely: no node-id round per K chunk
 struct LoadGruAT1H {
   const float* X;
   const float* Hp;
@@ -4091,7 +3727,6 @@ struct EpiGruWGrad {
     items(t, ix, vx);
     af.put_n(g, ix, vx);
   }
-  TGNX_FIX_PRE_METHODS
 };
 // encoding columns of W_ih as the B operand of dX_enc = dG W_cat[:, enc]: element (n, r = 4j+g)
 struct LoadGruWencT {
@@ -4211,16 +3846,15 @@ struct CellOps<0> {
   }
   static __host__ EpiGru epi_train(const Ctx& c) {
     EpiGru e = epi(c, c.nid, 0);
-    e.Hp = TGNX_DENSE_H ? c.Hp : nullptr;
+    e.Hp = c.Hp;
     return e;
   }
   static __host__ EpiGruBwd bwd(const Ctx& c) {
-    return EpiGruBwd{c.gates, c.mem, c.nid, c.dG, c.D, TGNX_DENSE_H ? c.Hp : nullptr};
+    return EpiGruBwd{c.gates, c.mem, c.nid, c.dG, c.D, c.Hp};
   }
   // B operand of dW_cell = dGᵀ [X | H | 1]
   static __host__ auto hT(const Ctx& c) {
-    if constexpr (TGNX_DENSE_H) return LoadGruAT1H{c.X, c.Hp, c.Qm, c.D};
-    else return LoadGruAT1{c.X, c.mem, c.nid, c.Qm, c.D};
+    return LoadGruAT1H{c.X, c.Hp, c.Qm, c.D};
   }
   static __host__ EpiGruWGrad wgrad(const Ctx& c) {
     return EpiGruWGrad{c.grads, c.L.w_ih, c.L.w_hh, c.L.b_ih, c.L.b_hh, c.Qm, c.D, c.adf};
@@ -4434,41 +4068,18 @@ struct MarkNextJob {
     mark_body<true>(c, bid, nb, 1, reinterpret_cast<uint32_t*>(smem));
   }
 };
-// launch of the pipelined step that carries the next batch's marking: 3 = q|k|v|skip GEMM, 5 =
-// tgn_pred_train, 7 = kv_reduce ‖ dE GEMMs, 8 = weight gradients ‖ dz0, 9 = dW_gru ‖ dX_enc
 #ifndef TGNX_SCAN_T
 #define TGNX_SCAN_T TGN_SCAN_THREADS  // train-step scan workgroup size (experiments)
-#endif
-#ifndef TGNX_PRED_ATT
-#define TGNX_PRED_ATT 1  // 1 hop: attention forward inside tgn_pred_train (0: its own launch)
-#endif
-#ifndef TGNX_KV_FUSE
-#define TGNX_KV_FUSE 1  // 1-hop train: (dk, dv) per edge computed and summed in tgn_attn_bwd (no k / v reduction launch)
-#endif
-#ifndef TGNX_PP_MARK_AT_LARGE
-#define TGNX_PP_MARK_AT_LARGE 5  // (8: review-shaped 0.1040 vs 0.1037 ms, not kept)
-#endif
-#ifndef TGNX_KVF_MARK_AT
-#define TGNX_KVF_MARK_AT 5  // with TGNX_KV_FUSE: the launch of a non-parity pipelined step's next-batch marking (5 or 8)
 #endif
 #ifndef TGNX_MD_CAP200
 #define TGNX_MD_CAP200 512  // grid cap of the step's M x D GEMMs (dz0, dX_enc) per 200 events of the rank's batch (env
                             // TGNX_MD_CAP200): 7 column tiles at D = 100, ~30 row tiles at B = 200 (A/B 0.0966 vs 0.0971 ms with 1024)
-#endif
-#ifndef TGNX_WALK_AT
-#define TGNX_WALK_AT 1  // parity-set steps with a plan table: the next batch's node-set walk in the dW_cell launch (0)
-                        // or the attention-backward launch (1; same-box A/B: wiki step 0.0982 vs 0.0988 ms, dW_cell
-                        // launch span 17.2 -> 14.6 us, DP floor at world 2 / 4 / 8 -1.3 / -1.0 / -0.7 %);
-                        // TGNX_WALK_AT in the environment overrides
 #endif
 #ifndef TGNX_PLANS_IN_PRED
 #define TGNX_PLANS_IN_PRED 4  // parity-set steps whose plans have 2..N partitions: the plans in the predictor launch (0: never; DP floor A/B at world 2 / 4 / 8: N = 4 0.1034 / 0.1078 / 0.1283 ms, 16 0.1040 / 0.1087 / 0.1328, 0 0.1039 / 0.1176 / 0.1285)
 #endif
 #ifndef TGNX_SCAN_AT
 #define TGNX_SCAN_AT 7  // parity step: the launch the next batch's scan rides in (7: dW_gru; 6: dz0, 0.1005 vs 0.0965 ms)
-#endif
-#ifndef TGNX_PIPE_MARK_AT
-#define TGNX_PIPE_MARK_AT 7
 #endif
 
 __global__ void __launch_bounds__(256) tgn_update(Ctx c, int nmem, int nst, int mem_mode, const int64_t* list,
@@ -4511,7 +4122,6 @@ struct SnapJob {
     if (tid == 0) advance_counters(c.ctl);
   }
 };
-static_assert(TGNX_PIPE_MARK_AT != 9, "the next batch's marking reads the step counters SnapJob advances");
 // the fixup launch's Ctx: SnapJob's copies in place of the live descriptor
 static inline Ctx fixup_view(const Ctx& c) {
   Ctx f = c;
@@ -4719,8 +4329,8 @@ static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_spl
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, std::min(TGNX_DWG_SMAX, ksplit(k.Mtr, TGNX_S_WG))); }
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, kj, kx, ke, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
-      Ep, alpha, alk, Qo, Zc, Hp, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, sinE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
-      snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, e1_c, alk1, Qo1, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF,
+      Ep, alpha, alk, Qo, Zc, Hp, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
+      snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF,
       uX, uZ, uG, ulu, uxw, utrel, total;
   int tgp_rows, tgp_e1;
   // the scan's per-batch outputs of the second parity (tgnx_tgn_train_step_pp: a step reads its parity's
@@ -4761,7 +4371,7 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.lu = carve(off, (size_t)k.Mcap * 4);
   W.xw = carve(off, (size_t)k.Mcap * 8);
   W.gates = carve(off, (size_t)k.Mcap * 4 * D * 4);
-  W.Hp = carve(off, TGNX_DENSE_H ? (size_t)k.Mcap * D * 4 : 0);
+  W.Hp = carve(off, (size_t)k.Mcap * D * 4);
   W.Z0 = carve(off, (size_t)k.Mcap * D * 4);
   W.P = carve(off, (size_t)k.Mcap * 4 * HC * 4);
   W.Ep = carve(off, (size_t)k.Ecap * HC * 4);
@@ -4786,7 +4396,6 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.tgp_rows = W.tgp_e1 + (k.E1tr + G32::TM - 1) / G32::TM;
   W.tgp = carve(off, (size_t)W.tgp_rows * 2 * D * 4);
   W.encE = carve(off, (size_t)k.Ecap * (D + k.d) * 4);  // train: [cos enc | msg] rows; eval: cos rows (stride D)
-  W.sinE = carve(off, TGNX_SIN_RECOMPUTE ? 0 : (size_t)k.Etr * D * 4);
   W.s0m = carve(off, (size_t)k.Mtr * D * 4);
   W.s1m = carve(off, (size_t)k.Mtr * D * 4);
   W.pA = carve(off, gemm_partial_floats(shp_dWe(k, nullptr)) * 4);
@@ -4810,16 +4419,13 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.r_x2 = carve(off, R1 * 4);
   W.ceoff1 = carve(off, (R1 + 1) * 4);
   W.e1_j = carve(off, E1 * 4);
-  W.e1_c = carve(off, TGNX_KVF_ROOT ? E1 * 4 : 0);
-  W.alk1 = carve(off, TGNX_KVF_ROOT && two ? (size_t)k.E1tr * TH * 4 : 0);
-  W.Qo1 = carve(off, TGNX_KVF_ROOT && two ? (size_t)k.R1tr * 2 * HC * 4 : 0);
   W.e1_e2 = carve(off, E1 * 4);
   W.e1_id = carve(off, E1 * 8);
   W.P2 = carve(off, R2 * 4 * HC * 4);
   W.Ep2 = carve(off, E1 * HC * 4);
   W.alpha1 = carve(off, (size_t)k.E1tr * TH * 4);
   W.Zr = carve(off, R1 * HC * 4);
-  W.dZr = carve(off, (two ? (size_t)k.R1tr : 0) * HC * 4 * TGNX_DZR_REP);
+  W.dZr = carve(off, (two ? (size_t)k.R1tr : 0) * HC * 4);  // (one copy: 4 copies measured slower, 0.2770 -> 0.2942 ms)
   W.dP2 = carve(off, (two ? (size_t)k.Rtr : 0) * 4 * HC * 4);
   W.dE2 = carve(off, (size_t)k.E1tr * HC * 4);
   W.pE = carve(off, two ? gemm_partial_floats(shp_dWp2(k, nullptr)) * 4 : 0);
@@ -4968,7 +4574,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.evs = reinterpret_cast<float*>(ws + W.evs);
   c.evr = reinterpret_cast<int*>(ws + W.evr);
   c.evq = k.layers == 2 ? nullptr : reinterpret_cast<int4*>(ws + W.evq);
-  c.evj = k.layers == 2 || cfg->ring > 16 || !TGNX_PRED_ATT_REC ? nullptr : reinterpret_cast<int*>(ws + W.evj);
+  c.evj = k.layers == 2 || cfg->ring > 16 ? nullptr : reinterpret_cast<int*>(ws + W.evj);
   c.cevq = c.evj ? reinterpret_cast<int4*>(ws + W.cevq) : nullptr;
   c.cevj = c.evj ? reinterpret_cast<int*>(ws + W.cevj) : nullptr;
   c.Hs = reinterpret_cast<float*>(ws + W.Hs);
@@ -4976,7 +4582,7 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.dZc = reinterpret_cast<float*>(ws + W.dZc);
   c.dzrep = k.layers == 2 ? 1 : TGNX_DZC_REP;
   c.dzstride = (int64_t)k.Rtr * k.HC;
-  c.dzrep1 = k.layers == 2 ? TGNX_DZR_REP : 1;
+  c.dzrep1 = 1;
   c.dzstride1 = (int64_t)k.R1tr * k.HC;
   c.dP = reinterpret_cast<float*>(ws + W.dP);
   c.dE = reinterpret_cast<float*>(ws + W.dE);
@@ -4984,7 +4590,6 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.dG = reinterpret_cast<float*>(ws + W.dG);
   c.tgp = reinterpret_cast<float*>(ws + W.tgp);
   c.encE = reinterpret_cast<float*>(ws + W.encE);
-  c.sinE = reinterpret_cast<float*>(ws + W.sinE);
   c.s0m = reinterpret_cast<float*>(ws + W.s0m);
   c.s1m = reinterpret_cast<float*>(ws + W.s1m);
   c.pA = reinterpret_cast<float*>(ws + W.pA);
@@ -5031,9 +4636,6 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
     c.ceoff1 = reinterpret_cast<int*>(ws + W.ceoff1);
     c.e1_j = reinterpret_cast<int*>(ws + W.e1_j);
     c.e1_e2 = reinterpret_cast<int*>(ws + W.e1_e2);
-    c.e1_c = reinterpret_cast<int*>(ws + W.e1_c);
-    c.alk1 = reinterpret_cast<float*>(ws + W.alk1);
-    c.Qo1 = reinterpret_cast<float*>(ws + W.Qo1);
     c.e1_id = reinterpret_cast<int64_t*>(ws + W.e1_id);
     c.P2 = reinterpret_cast<float*>(ws + W.P2);
     c.Ep2 = reinterpret_cast<float*>(ws + W.Ep2);
@@ -5110,9 +4712,9 @@ static Ctx root_view(const Ctx& c) {
   r.dzstride = c.dzstride1;
   r.dP = c.dP2;
   r.dE = c.dE2;
-  r.e_c = c.e1_c;
-  r.alk = c.alk1;
-  r.Qo = c.Qo1;
+  r.e_c = nullptr;  // (the root level's attention backward leaves its (dk, dv) sums to the k / v reduction job:
+  r.alk = nullptr;  //  summing them in the attention backward measured slower, r4_kvf_root_ab.txt)
+  r.Qo = nullptr;
   r.rsel = CNT_R1;
   r.ccap = c.R1cap;
   r.att_salt = 9;
@@ -5122,9 +4724,6 @@ static Ctx root_view(const Ctx& c) {
 // tgn_agg_emit's two grid-stride parts (sampled edges, wave per (centre, ring slot); sampled nodes):
 // grids sized from capacities launch mostly idle workgroups, which hold dispatch slots
 // (stamps timeline, wiki shape: caps 4096 / 2048 -> 1024 / 512 took agg_emit 16.5 -> 13.9 us)
-#ifndef TGNX_AGG_SPECIALIZE
-#define TGNX_AGG_SPECIALIZE 1  // last-aggregation steps launch tgn_agg_emit<0> (97 VGPRs instead of 233)
-#endif
 #ifndef TGNX_AGG_EDGE_CAP
 #define TGNX_AGG_EDGE_CAP 1024  // (512: 0.0887 / 0.0886 vs 0.0871 / 0.0872 ms; node cap 128: +-0 — r5_agg_caps_ab.txt)
 #endif
@@ -5134,7 +4733,6 @@ static Ctx root_view(const Ctx& c) {
 // the attention backward for a ring of K and the predictor's dZc copy count (compile-time: the copies' loads batched)
 using AttnBwdFn = void (*)(Ctx, int, int, int, Ctx);
 static AttnBwdFn attn_bwd_fn(int K, int rep) {
-  static_assert(TGNX_DZR_REP == 1 || TGNX_DZR_REP == TGNX_DZC_REP, "dZr copies: 1 or the dZc copy count (instantiated)");
   if (rep == TGNX_DZC_REP && TGNX_DZC_REP > 1) return K <= 10 ? tgn_attn_bwd<10, TGNX_DZC_REP> : tgn_attn_bwd<ATT_EB, TGNX_DZC_REP>;
   return K <= 10 ? tgn_attn_bwd<10, 1> : tgn_attn_bwd<ATT_EB, 1>;
 }
@@ -5311,9 +4909,6 @@ struct AdvArgs {
 // scanned by the previous pipelined step; 2 = pipelined, mark + scan this batch first.  A pipelined step
 // marks the next batch inside tgn_pred_train and scans it after its own last launch.
 extern "C++" {  // (inside the extern "C" block: the cell-templated step)
-#ifndef TGNX_SCAN_FOLD
-#define TGNX_SCAN_FOLD 1  // pipelined step: the next batch's scan inside the fixup launch when it fits (0: own launch)
-#endif
 // the next batch's scan as 256-thread head workgroups of the fixup launch: its LDS within the launch's,
 // and (small graphs, walked directly) <= 2 bitmap words per thread
 // (k: the global batch, whose plans the scan sorts; kr: the rank's share, whose centres the walk stages)
@@ -5321,7 +4916,7 @@ static inline bool scan_rides(const Ctx& c, const Caps& k, const Caps& kr, size_
   return tgn_scan_smem(k.B) <= lds && (size_t)3 * kr.B * 12 <= lds && (!scan_direct(c.words) || c.words <= 2 * 256);
 }
 static inline bool scan_folds(const Ctx& c, const Caps& k, const Caps& kr) {
-  return TGNX_SCAN_FOLD && scan_rides(c, k, kr, (size_t)GEMM_FIX_SMEM * 4);
+  return scan_rides(c, k, kr, (size_t)GEMM_FIX_SMEM * 4);
 }
 // pp >= 0 (tgnx_tgn_train_step_pp, world 1, 1 hop): the step reads scan-output set pp; the next batch is marked
 // in the predictor launch and scanned into set 1 - pp inside the k / v reduction launch (its outputs are then
@@ -5434,9 +5029,9 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const int nagg = nevb + nedge + gridn(kr.Mtr, 4, TGNX_AGG_NODE_CAP);
   const int64_t* nol = nullptr;
   const int* noc = nullptr;
-  if (c.aggr == 0 && TGNX_AGG_SPECIALIZE)
+  if (c.aggr == 0)
     launch_k(tgn_agg_emit<0>, dim3(nagg), dim3(256), 0, s, c, 0, nedge, nol, noc, 0, (int64_t)0, nevb);
-  else if (c.aggr == 1 && c.d <= 192 && TGNX_AGG_SPECIALIZE)
+  else if (c.aggr == 1 && c.d <= 192)
     launch_k(tgn_agg_emit<1>, dim3(nagg), dim3(256), 0, s, c, 0, nedge, nol, noc, 0, (int64_t)0, nevb);
   else
     launch_k(tgn_agg_emit<-1>, dim3(nagg), dim3(256), 0, s, c, 0, nedge, nol, noc, 0, (int64_t)0, nevb);
@@ -5469,26 +5064,19 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // where it sums them (kv_edge_body), so the k / v reduction launch is gone and the GEMMs that need only dE
   // ride in a later launch
   // (2 hops: the outer level, whose attention forward is tgn_attn_fwd; its edges keep the sampling order)
-  const bool kvf = TGNX_KV_FUSE && (two ? TGNX_KVF_2HOP : TGNX_PRED_ATT);
-  const bool kvs = kvf && !two && TGNX_KVE_GSORT && (size_t)kr.Mtr + 1 <= tgn_pred_smem(c.D) / 4;
-  c.kvf = kvf ? 1 : 0;
+  const bool kvf = true;  // (the separate k / v reduction launch: slower)
+  const bool kvs = !two && (size_t)kr.Mtr + 1 <= tgn_pred_smem(c.D) / 4;
+  c.kvf = 1;
   c.kvs = kvs ? 1 : 0;
-  // (kvf: no k / v launch; the next batch's marking of a non-parity pipelined step rides in the predictor launch
-  // beside its sort block, as the parity step's does)
-  const int mark_at = kvf ? TGNX_KVF_MARK_AT : TGNX_PIPE_MARK_AT;
-  // parity step: the predictor launch (5) or, for graphs marked through summary bitmaps, the dz0 launch (8)
-  const int pp_mark_at = TGNX_PP_MARK_AT_LARGE == 8 && kvf && !scan_direct(c.words) ? 8 : 5;
-  auto mk_at = [&](int at) {
-    return BlockJob<MarkNextJob, 3 * MARK_LDS_WORDS>{MarkNextJob{c, nmark}, pipe && at == (ppm ? pp_mark_at : mark_at) ? nmark : 0};
-  };
+  // a pipelined step marks the next batch in the predictor launch, beside its sort block (in the dz0 launch for
+  // graphs marked through summary bitmaps: review-shaped 0.1040 vs 0.1037 ms, not kept)
   probe_begin(TGNX_K_PROJ, s);
-  gemmN_launch(s, mk_at(3),
-               gemm_job<G32>(gemm_shape<G32>(kr.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
+  gemmN_launch(s, gemm_job<G32>(gemm_shape<G32>(kr.Mtr, 4 * HC, D, c.cnt + CNT_M), LoadZ{c.Z0, c.mem, c.nid, D, 0},
                              LoadProjW{P + c.L.wq, c.L.pw, HC, D}, EpiProj{P + c.L.bq, c.L.pb, c.P, HC}, (float*)nullptr));
   probe_end(TGNX_K_PROJ, s);
   TGNX_LAUNCH_CHECK("tgn_proj");
   // 1 hop: the attention forward runs inside tgn_pred_train (per root, beside its weight staging)
-  const bool att_in_pred = !two && TGNX_PRED_ATT;
+  const bool att_in_pred = !two;
   if (!att_in_pred) {
     probe_begin(TGNX_K_SEG_FWD, s);
     launch_k(tgn_attn_fwd<true>, dim3(gridn(kr.Rtr, 4, 1 << 20)), dim3(256), 0, s, c);
@@ -5496,11 +5084,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     TGNX_LAUNCH_CHECK("tgn_attn_fwd");
   }
   Ctx cr = two ? root_view(c) : c;  // the level the predictor reads
-  if (two) {  // conv2: its attention backward sums the root edges' (dk, dv) too (TGNX_KVF_ROOT), the root edges
-              // sorted by neighbour row in the predictor launch (its sort block, as the 1-hop step's edges)
-    cr.kvf = TGNX_KVF_ROOT && kvf ? 1 : 0;
-    cr.kvs = cr.kvf && TGNX_KVE_GSORT && TGNX_KVF_ROOT_SORT && (size_t)kr.Mtr + 1 <= tgn_pred_smem(c.D) / 4 ? 1 : 0;
-  }
+  if (two) cr.kvf = cr.kvs = 0;  // conv2's attention backward leaves its (dk, dv) sums to the k / v reduction job
   if (two) {  // conv2 over the roots: projections of h1 (rows = outer centres), attention per root
     gemm_launch<G32>(gemm_shape<G32>(kr.Rtr, 4 * HC, HC, c.cnt + CNT_R), LoadRowK{c.Zc, kr.Rtr, HC, HC},
                      LoadProjW{P + c.L.wq2, c.L.pw, HC, HC}, EpiProj{P + c.L.bq2, c.L.pb, c.P2, HC}, nullptr, s);
@@ -5512,9 +5096,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // launch when its LDS holds the plans; else, for partitioned plans (data parallel: the global batch's
   // 2 B keys) that fit the predictor launch's LDS, the plans there and the walk alone in the dW_cell launch;
   // else its own launch after the dW_cell launch
-  // (with a plan table the scan is the walk alone: it rides when the rank's centres fit the launch's LDS; with
-  // TGNX_WALK_AT 1 in the attention-backward launch instead of the dW_cell launch)
-  static const int walk_at = env_int("TGNX_WALK_AT", TGNX_WALK_AT);
+  // (with a plan table the scan is the walk alone: it rides when the rank's centres fit the launch's LDS, 1 hop in
+  // the attention-backward launch instead of the dW_cell launch)
   // (with a plan table the scan is the walk alone: its LDS is the centre staging, 3 B x 12 bytes, and the small-graph
   // direct walk's <= 2 words per thread; 2 hops: the walk rides in conv1's attention-backward launch)
   // (the attention-backward walk holds 2 bitmap words per thread, the dW_cell launch's ScanJob 8: its LDS word list
@@ -5524,7 +5107,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const auto walk_rides = [&](size_t lds, int wpt) {
     return (size_t)3 * kr.B * 12 <= lds && (!scan_direct(c.words) || c.words <= (int64_t)wpt * 256);
   };
-  const bool walk_bwd = ppm && c.ptab && walk_at == 1 && !two && pp_mark_at == 5 && walk_rides((size_t)3 * MARK_LDS_WORDS * 4, 2);
+  const bool walk_bwd = ppm && c.ptab && !two && walk_rides((size_t)3 * MARK_LDS_WORDS * 4, 2);
   const int nwalk = walk_bwd ? 1 : 0;
   const uint32_t walk_lds = walk_bwd ? (uint32_t)(3 * kr.B * 12 + 16) : 0u;
   const bool scan_w3 = ppm && !walk_bwd && (c.ptab ? walk_rides((size_t)3 * MARK_LDS_WORDS * 4, 8)
@@ -5537,7 +5120,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const int npl = plans_pred ? 2 * c.pplan : 0;
   probe_begin(TGNX_K_PRED, s);
   TGNX_CHECK_ARG(pred_smem_ok(c.D), "tgn_pred_train: dynamic LDS attribute refused");
-  const int nmk = (ppm ? pp_mark_at == 5 : pipe && mark_at == 5) ? nmark : 0;
+  const int nmk = ppm || pipe ? nmark : 0;
   const size_t psm = std::max({tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0,
                                npl ? tgn_scan_smem(k.B) : (size_t)0});
   const int nsrt = (two ? cr.kvs : kvs) ? 1 : 0;  // (kvs: the rows fit the sort's LDS counters)
@@ -5562,17 +5145,15 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   if (two) {
     // conv2 backward (‖ predictor reductions) -> dP2, dE2; then dh1 = dP2 [Wq2; Wk2; Wv2; Wsk2] ‖ dW_proj2,
     // dW_edge2 (deferred) ‖ conv2's lin_edge -> Δt-encoding partials; then conv backward from dh1
-    const int ncb1 = gridn(kr.R1tr, 4, 1 << 20), nkv1 = cr.kvf ? gridn(kr.E1tr, KVE_CH, 1 << 20) : 0;
-    launch_k(attn_bwd_fn(c.K, cr.dzrep), dim3(ncb1 + nkv1 + gridn(3 * D + 2, 4)), dim3(256), 0u,
-             s, cr, ncb1, nkv1, 0, cr);
+    const int ncb1 = gridn(kr.R1tr, 4, 1 << 20);
+    launch_k(attn_bwd_fn(c.K, cr.dzrep), dim3(ncb1 + gridn(3 * D + 2, 4)), dim3(256), 0u, s, cr, ncb1, 0, 0, cr);
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
-    // conv2's (dk, dv) sums (unless its attention backward summed them) ‖ its dE2-only GEMMs (as in the 1-hop
-    // step below), then dh1 ‖ dW_proj2 (with the root-level fusion the dE2 GEMMs ride in that launch instead)
+    // conv2's (dk, dv) sums ‖ its dE2-only GEMMs (as in the 1-hop step below), then dh1 ‖ dW_proj2
     const auto j_dwe2 = gemm_job<GW>(shp_dWe2(kr, c.cnt), LoadKRow{c.dE2, HC, kr.E1tr, HC}, LoadAttrMapT{ea1},
                                      EpiDeferred{}, c.pF);
     const auto j_denc2 = gemm_job<G32>(gemm_shape<G32>(kr.E1tr, D, HC, c.cnt + CNT_E1), LoadRowK{c.dE2, kr.E1tr, HC, HC},
                                        LoadKRow{P + c.L.we2, D, HC, D + d},
-                                       EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, c.e1_e2, c.tgp_e1, P + c.L.te_w,
+                                       EpiTeEdge{c.e_j, c.e_t, c.lu, c.tgp, D, c.e1_e2, c.tgp_e1, P + c.L.te_w,
                                                  P + c.L.te_b},
                                        (float*)nullptr);
     const auto j_dh1 = gemm_job<G32L>(gemm_shape<G32L>(kr.Rtr, HC, 4 * HC, c.cnt + CNT_R),
@@ -5580,13 +5161,9 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                                       EpiStore{c.dZc, nullptr, HC, 0}, (float*)nullptr);
     const auto j_dwp2 = gemm_job<GW>(shp_dWp2(kr, c.cnt), LoadKRow{c.dP2, 4 * HC, kr.Rtr, 4 * HC}, LoadZ1T{c.Zc, HC},
                                      EpiDeferred{}, c.pE);
-    if (cr.kvf) {
-      gemmN_launch(s, j_dh1, j_dwp2, j_dwe2, j_denc2);
-    } else {
-      gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{cr}, gridn(kr.E1tr, KVR_CH, 1 << 20)}, j_dwe2, j_denc2);
-      TGNX_LAUNCH_CHECK("tgn_kv_reduce2");
-      gemmN_launch(s, j_dh1, j_dwp2);
-    }
+    gemmN_launch(s, BlockJob<KvReduceJob>{KvReduceJob{cr}, gridn(kr.E1tr, KVR_CH, 1 << 20)}, j_dwe2, j_denc2);
+    TGNX_LAUNCH_CHECK("tgn_kv_reduce2");
+    gemmN_launch(s, j_dh1, j_dwp2);
     TGNX_LAUNCH_CHECK("tgn_dh1");
     const int ncb = gridn(kr.Rtr, 4, 1 << 20), nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
     launch_k(attn_bwd_fn(c.K, c.dzrep), dim3(ncb + nkv + nwalk), dim3(256), walk_lds, s, c,
@@ -5605,18 +5182,11 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // idle: the dE-only GEMMs fill them here instead of lengthening the dP launch below.
   const Ctx cf = fixup_view(c);
   const EpiGradStore e_dWe{G, c.L.we, D + d, cf.adf};
-  const auto j_kvr = BlockJob<KvReduceJob>{KvReduceJob{c}, gridn(kr.Etr, KVR_CH, 1 << 20)};
   const auto j_dwe = gemm_job<GW>(shp_dWe(kr, c.cnt), LoadKRow{c.dE, HC, kr.Etr, HC}, LoadKRow{c.encE, D + d, kr.Etr, D + d},
                                   EpiDeferred{}, c.pA);
   const auto j_denc = gemm_job<G32>(with_cap(gemm_shape<G32>(kr.Etr, D, HC, c.cnt + CNT_E), edge_cap), LoadRowK{c.dE, kr.Etr, HC, HC},
-                                    LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.sinE, c.tgp, D, nullptr, 0, P + c.L.te_w, P + c.L.te_b},
+                                    LoadKRow{P + c.L.we, D, HC, D + d}, EpiTeEdge{c.e_j, c.e_t, c.lu, c.tgp, D, nullptr, 0, P + c.L.te_w, P + c.L.te_b},
                                     (float*)nullptr);
-  if (!kvf) {
-    probe_begin(TGNX_K_KV, s);
-    gemmN_launch(s, mk_at(7), j_kvr, j_dwe, j_denc);
-    probe_end(TGNX_K_KV, s);
-    TGNX_LAUNCH_CHECK("tgn_kv_reduce_dE");
-  }
   // weight gradients (deferred split-K) ‖ ...
   const EpiProjGrad e_dWp{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D, cf.adf};
   const EpiLpGrad e_dWlp{G, c.L.lsw, c.L.ldw, D, cf.adf};
@@ -5631,7 +5201,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const auto j_dz0 = gemm_job<G32L>(with_cap(gemm_shape<G32L>(kr.Mtr, D, 4 * HC, c.cnt + CNT_M), md_cap), LoadRowK{c.dP, kr.Mtr, 4 * HC, 4 * HC},
                                     LoadProjWT{P + c.L.wq, c.L.pw, HC, D}, Cl::bwd(c), (float*)nullptr);
   auto l7 = [&](auto... jobs) {
-    gemmN_launch(s, mk_at(8), jobs...);
+    gemmN_launch(s, jobs...);
     probe_end(TGNX_K_EDGE_BWD, s);
     TGNX_LAUNCH_CHECK("tgn_wgrad_dz0");
     return TGNX_OK;
@@ -5649,15 +5219,14 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   const auto j_snap = BlockJob<SnapJob>{SnapJob{c, ppm ? 1 : 0}, 1};
   const auto j_store = BlockJob<StoreJob>{StoreJob{c, nst}, nst};
   // (the scan may ride in the dz0 launch instead: TGNX_SCAN_AT 6)
-  const bool scan6 = scan_w3 && kvf && TGNX_SCAN_AT == 6;
+  const bool scan6 = scan_w3 && TGNX_SCAN_AT == 6;
   const bool walk_w3 = (scan_w3 || plans_pred) && !walk_bwd;  // (the walk rides in the dW_cell launch)
   auto l8 = [&](auto... jobs) {
     probe_begin(TGNX_K_WGRAD3, s);
     // the GEMM jobs before the snapshot / store blocks (0.0970 vs 0.0986 ms with those first)
+    // (the edge jobs dEnc / dW_edge first instead: that launch 12.8 -> 14.7 us, r5_w3_jobs_first_ab.txt)
     if (walk_w3 && !scan6)
       gemmN_launch(s, j_scan, j_dxe, j_dwg, jobs..., j_snap, j_store);
-    else if constexpr (TGNX_W3_JOBS_FIRST)  // (experiment: the edge jobs — dEnc, the launch's tail — dispatched first)
-      gemmN_launch_w<TGNX_W3_WAVES>(s, jobs..., j_dxe, j_dwg, j_snap, j_store);
     else
       gemmN_launch_w<TGNX_W3_WAVES>(s, j_dxe, j_dwg, jobs..., j_snap, j_store);
     probe_end(TGNX_K_WGRAD3, s);
@@ -5667,18 +5236,10 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // kvf: the dE-only GEMMs ride in the dW_gru launch (in the dz0 launch: 0.1013 vs 0.0987 ms; dW_proj / dW_lp
   // moved to the dW_gru launch too: 0.1013 - 0.1035), dz0 first in its launch (0.0985 vs 0.0991)
   // (the lambdas return the launch checks' status)
-  if (!kvf) {
-    if ((rc = l7(j_dwp, j_dwlp, j_dz0)) || (rc = l8())) return rc;
-  } else if (scan6) {
+  if (scan6) {
     if ((rc = l7(j_scan, j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) return rc;
-  } else {
-    if (TGNX_DWE_AT7) {  // (experiment: dW_edge in the dz0 launch, which fits one dispatch round)
-      if ((rc = l7(j_dz0, j_dwp, j_dwlp, j_dwe)) || (rc = l8(j_denc))) return rc;
-    } else if (TGNX_W3_JOBS_FIRST == 2) {  // (dEnc before dW_edge)
-      if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_denc, j_dwe))) return rc;
-    } else if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) {
-      return rc;
-    }
+  } else if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) {  // (dW_edge in the dz0 launch: slower,
+    return rc;                                                                 //  r4_dwe_in_dz0_ab.txt)
   }
   if (ppm && !walk_w3 && !walk_bwd) {  // (with a plan table: the walk alone)
     tgn_scan<true><<<c.ptab ? 1 : 1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(cn, 1, 0);

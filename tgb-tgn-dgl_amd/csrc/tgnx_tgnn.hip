@@ -42,10 +42,10 @@ constexpr int MRR_SLOTS = 65536;  // per-batch MRR ring in buffers.mrr
 constexpr int BATCH_MAX = 2048;   // max events per batch (touch sort capacity 3 * BATCH_MAX in LDS)
 enum { MISC_RUNS = 0, MISC_KMAX = 1, MISC_STAMPS = 16, MISC_WORDS = TGNX_MISC_WORDS };
 #ifdef TGNX_TIMING  // phase timestamps of the single-workgroup kernels (measurement builds only)
-#define TGNX_STAMP(c, i) \
+#define TGNN_PHASE_STAMP(c, i) \
   do { if (threadIdx.x == 0) reinterpret_cast<int64_t*>((c).misc + MISC_STAMPS)[i] = (int64_t)wall_clock64(); } while (0)
 #else
-#define TGNX_STAMP(c, i) do {} while (0)
+#define TGNN_PHASE_STAMP(c, i) do {} while (0)
 #endif
 
 // ------------------------------------------------------------------ layouts
@@ -398,18 +398,18 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   if (blockIdx.x == 1) {  // ring insert plan
     if (B == 0 || B > c.Bmax) return;
-    TGNX_STAMP(c, 8);
+    TGNN_PHASE_STAMP(c, 8);
     uint64_t* key;
     int* runs;
     const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs);
-    TGNX_STAMP(c, 9);
+    TGNN_PHASE_STAMP(c, 9);
     for (int p = tid; p < 2 * B; p += T) c.rkeys[p] = key[p];
     for (int r = tid; r < U; r += T) c.rruns[r] = runs[r];
     if (tid == 0) {
       c.rruns[U] = 2 * B;
       c.misc[MISC_RUNS] = U;
     }
-    TGNX_STAMP(c, 10);
+    TGNN_PHASE_STAMP(c, 10);
     return;
   }
   if (blockIdx.x == 2) {  // per-block max t (eval's time_assoc[:] = max, model_utils.py:78), block order
@@ -454,7 +454,7 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   int* run_start = reinterpret_cast<int*>(smem + (size_t)next_pow2(NTc) * 8);
   int* run_of = run_start + NTc;
   uint64_t* tmp = reinterpret_cast<uint64_t*>(run_of + NTc);
-  TGNX_STAMP(c, 0);
+  TGNN_PHASE_STAMP(c, 0);
   if (TRAIN && c.gen_neg) {  // NegLinkSamplerDest.sample (neg_sampler.py:8-23), counter-based stream
     const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
     const uint64_t off = (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
@@ -480,9 +480,9 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     key[p] = k;
   }
   __syncthreads();
-  TGNX_STAMP(c, 1);
+  TGNN_PHASE_STAMP(c, 1);
   sort_u64(key, tmp, NT, n);
-  TGNX_STAMP(c, 2);
+  TGNN_PHASE_STAMP(c, 2);
   const int pc = (NT + T - 1) / T;
   const int p0 = tid * pc, p1 = min(NT, p0 + pc);
   // compacted s/p list (kind != 0), exclusive prefix over the sorted touches
@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     }
     if (tid == 0) c.sp_pref[NT] = tot;
   }
-  TGNX_STAMP(c, 3);
+  TGNN_PHASE_STAMP(c, 3);
   // node runs -> node map; run id of every touch
   {
     int cnt = 0;
@@ -516,7 +516,7 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
       c.nodemap[knode(key[a])] = make_int4(gen, a, e - a, c.sp_pref[a]);
     }
   }
-  TGNX_STAMP(c, 4);
+  TGNN_PHASE_STAMP(c, 4);
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
   const int nloc = hi - lo;
   const int S = nloc * (2 + c.Kn);
@@ -539,8 +539,8 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     }
   }
   __syncthreads();
-  TGNX_STAMP(c, 5);
-  TGNX_STAMP(c, 6);
+  TGNN_PHASE_STAMP(c, 5);
+  TGNN_PHASE_STAMP(c, 6);
   if (TRAIN) {  // segment edge offsets (seg_cnt written above by this workgroup)
     const int chunk = (S + T - 1) / T;
     const int r0 = tid * chunk, r1 = min(S, r0 + chunk);
@@ -568,7 +568,7 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     c.ctl[TGNX_CTL_S] = S;
     c.ctl[TGNX_CTL_E] = -1;   // counted by tgnn_seg_count / tgnn_seg_scan
   }
-  TGNX_STAMP(c, 7);
+  TGNN_PHASE_STAMP(c, 7);
 }
 
 // exclusive scan of the edge counts (one workgroup) -> edge offsets
@@ -720,17 +720,10 @@ __device__ __forceinline__ float wave_sum8(const float (&v)[H], int lane) {
     const float keep = b4 ? k4[2 + i] : k4[i], send = b4 ? k4[i] : k4[2 + i];
     k2[i] = keep + xor16_f(send);
   }
-#ifdef TGNX_NO_DPP
-  float s = (b3 ? k2[1] : k2[0]) + __shfl_xor(b3 ? k2[0] : k2[1], 8, 64);
-  s += __shfl_xor(s, 4, 64);
-  s += __shfl_xor(s, 2, 64);
-  s += __shfl_xor(s, 1, 64);
-#else
   float s = (b3 ? k2[1] : k2[0]) + dpp_f<0x128>(b3 ? k2[0] : k2[1]);  // row_ror:8 = lane ^ 8 in the row
   s += dpp_f<0xB1>(s);   // lane ^ 1
   s += dpp_f<0x4E>(s);   // lane ^ 2
   s += dpp_f<0x141>(s);  // half-row mirror: the other quad (quads uniform by now)
-#endif
   return s;
 }
 
@@ -1259,9 +1252,7 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
     for (int x = tid; x < 3 * D; x += blockDim.x) {
       const int r = x / D, dd = x % D;
       float v = c.mem[roots[r] * D + dd];
-#ifndef TGNX_EXP_NOHASH
       if (c.drop) v *= node_keep(c, seed, blk, roots[r], dd);
-#endif
       se[r][dd] = v + sv[r];
     }
   }
@@ -1302,9 +1293,6 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
     }
   }
   __syncthreads();
-#ifdef TGNX_EXP_NOEPI
-  return;
-#endif
   if (wv != 0) return;
   float hs[2], hp[2], hn[2];
 #pragma unroll

@@ -7,7 +7,7 @@ out=/root/repo/gpurun_out/${tag}_ab.txt
 for round in 1 2; do
   for lib in "$@"; do
     if [ "$lib" = default ]; then unset TGNX_LIB; else export TGNX_LIB=$lib; fi
-    r=$(timeout -k 10 300 python /root/repo/bench.py --model ${MODEL:-tgn} --only --steps 500 --warmup 50 --no-cpu-baseline --no-train-loop --no-tcsr --probe-steps 5 ${BENCH_ARGS:-} 2>/dev/null | grep metric) || exit 1
+    r=$(timeout -k 10 300 python /root/repo/bench.py --model ${MODEL:-tgn} --only --steps 500 --warmup 50 --no-cpu-baseline --no-train-loop --no-tcsr --no-probe ${BENCH_ARGS:-} 2>/dev/null | grep metric) || exit 1
     echo "$lib $(echo "$r" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"])')" >> $out
   done
 done

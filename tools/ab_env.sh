@@ -9,7 +9,7 @@ out=gpurun_out/${tag}_ab.txt
 for round in $(seq ${ROUNDS:-3}); do
   for e in "$A" "$B"; do
     [ "$e" = "-" ] && envs="" || envs="$e"
-    r=$(env $envs timeout -k 10 300 python bench.py --model tgn --only --no-cpu-baseline --no-train-loop --no-tcsr --probe-steps 1 "$@" 2>/dev/null | grep metric) || exit 1
+    r=$(env $envs timeout -k 10 300 python bench.py --model tgn --only --no-cpu-baseline --no-train-loop --no-tcsr --no-probe "$@" 2>/dev/null | grep metric) || exit 1
     echo "$e $(echo "$r" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"])')" >> $out
   done
 done

@@ -8,7 +8,7 @@ out=/root/repo/gpurun_out/${tag}_ab.txt
 for round in 1 2; do
   for e in "$@"; do
     [ "$e" = "-" ] && envs="" || envs="$e"
-    r=$(env $envs timeout -k 10 300 python /root/repo/bench.py --model tgn --only --steps 500 --warmup 50 --no-cpu-baseline --no-train-loop --no-tcsr --probe-steps 5 ${BENCH_ARGS:-} 2>/dev/null | grep metric) || exit 1
+    r=$(env $envs timeout -k 10 300 python /root/repo/bench.py --model tgn --only --steps 500 --warmup 50 --no-cpu-baseline --no-train-loop --no-tcsr --no-probe ${BENCH_ARGS:-} 2>/dev/null | grep metric) || exit 1
     echo "$e $(echo "$r" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"])')" >> $out
   done
 done

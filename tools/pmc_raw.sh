@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp
 run() {  # sub counters
   local sub=$1; shift
   TGNX_LIB=$lib timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d $R/gpurun_out/${tag}_pmc/tgn_${sub} -o run -- \
-    python3 $R/bench.py --model tgn --only --no-graph --steps 30 --warmup 5 --probe-steps 1 --window start --no-cpu-baseline --no-train-loop --no-tcsr \
+    python3 $R/bench.py --model tgn --only --no-graph --steps 30 --warmup 5 --window mid --no-probe --no-cpu-baseline --no-train-loop --no-tcsr \
     > $R/gpurun_out/${tag}_pmc_tgn_${sub}.log 2>&1
 }
 run rd TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum || exit $?

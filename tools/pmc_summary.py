@@ -32,12 +32,20 @@ KERNELS = {
 }
 
 
-def load(path, counter=None):
-    """kernel name -> list of per-dispatch counter values (KB; raw counters: counts), one counter per call"""
+def load(path, counter=None, win=None):
+    """kernel name -> list of per-dispatch counter values (KB; raw counters: counts), one counter per call, in
+    dispatch order; win = "a:b": only dispatches [a, b) of each kernel (a kernel launched once per step: the bench
+    line's config.timed_steps, i.e. the timed window's steps; PMC_WINDOW_TGN / PMC_WINDOW_TGNN)"""
     out = {}
-    for r in csv.DictReader(open(path)):
+    rows = list(csv.DictReader(open(path)))
+    if rows and "Dispatch_Id" in rows[0]:
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    for r in rows:
         if counter is None or r["Counter_Name"] == counter:
             out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    if win:
+        a, b = (int(x) for x in win.split(":"))
+        out = {k: v[a:b] for k, v in out.items() if v[a:b]}
     return out
 
 
@@ -49,19 +57,19 @@ def load(path, counter=None):
 RAW_RD = {"TCC_EA0_RDREQ_128B_sum": 128, "TCC_EA0_RDREQ_64B_sum": 64, "TCC_EA0_RDREQ_32B_sum": 32}
 
 
-def raw_bytes(rd_csv, wr_csv, keys):
+def raw_bytes(rd_csv, wr_csv, keys, win=None):
     """per-launch (read, write, 64-B read requests) bytes of the kernels matching keys, or None"""
     rd = 0.0
     n64 = 0.0
     for ctr, sz in RAW_RD.items():
-        t = load(rd_csv, ctr)
+        t = load(rd_csv, ctr, win)
         v = [x for n in t if match(n, keys) for x in t[n]]
         if not v:
             return None
         rd += sz * sum(v) / len(v)
         if sz == 64:
             n64 = sum(v) / len(v)
-    tw, t64 = load(wr_csv, "TCC_EA0_WRREQ_sum"), load(wr_csv, "TCC_EA0_WRREQ_64B_sum")
+    tw, t64 = load(wr_csv, "TCC_EA0_WRREQ_sum", win), load(wr_csv, "TCC_EA0_WRREQ_64B_sum", win)
     w = [x for n in tw if match(n, keys) for x in tw[n]]
     w64 = [x for n in t64 if match(n, keys) for x in t64[n]]
     if not w or not w64:
@@ -81,7 +89,10 @@ def main(d):
     for model in ("tgn", "tgnn"):
         f = glob.glob(os.path.join(d, f"{model}_fetch", "**", "*counter_collection.csv"), recursive=True)
         w = glob.glob(os.path.join(d, f"{model}_write", "**", "*counter_collection.csv"), recursive=True)
-        fe, wr = (load(f[0]), load(w[0])) if f and w else ({}, {})
+        win = os.environ.get(f"PMC_WINDOW_{model.upper()}")
+        if win:
+            res[f"_window_{model}"] = f"dispatches [{win.replace(':', ', ')}) of each kernel: the timed steps"
+        fe, wr = (load(f[0], win=win), load(w[0], win=win)) if f and w else ({}, {})
         for probe, sel in KERNELS.items():
             if not fe or not probe.startswith(model + "_"):
                 continue
@@ -106,7 +117,7 @@ def main(d):
             for probe, sel in KERNELS.items():
                 if not probe.startswith(model + "_"):
                     continue
-                r = raw_bytes(rf[0], rw[0], sel)
+                r = raw_bytes(rf[0], rw[0], sel, win)
                 if r is None:
                     continue
                 e = res.setdefault(probe, {})

@@ -12,7 +12,7 @@ for round in 1 2; do
     if [ "$v" != default ]; then
       if [ -f $R/$v/bench.py ]; then b=$R/$v/bench.py; else export TGNX_LIB=$R/$v/libtgnx.so; fi
     fi
-    r=$(timeout -k 10 300 python $b --model ${MODEL:-tgn} --only --steps 300 --warmup 30 --probe-steps 30 \
+    r=$(timeout -k 10 300 python $b --model ${MODEL:-tgn} --only --steps 300 --warmup 30 \
         --no-cpu-baseline ${EXTRA} 2>/dev/null | grep metric) || exit 1
     echo "$v $(echo "$r" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["value"], {k: round(x, 1) for k, x in d["kernels_us"].items()})')" >> $out
   done

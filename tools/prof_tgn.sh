@@ -5,7 +5,7 @@ tag=${1:-pt}
 R=/root/repo
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${tag}_prof -o run -- \
-  python3 $R/bench.py --model tgn --only --steps 200 --warmup 20 --probe-steps 1 --no-cpu-baseline ${EXTRA} \
+  python3 $R/bench.py --model tgn --only --steps 200 --warmup 20 --no-cpu-baseline ${EXTRA} \
   > $R/gpurun_out/${tag}_prof.json 2> $R/gpurun_out/${tag}_prof.err || exit $?
 python3 - $R/gpurun_out/${tag}_prof <<'PY'
 import csv, glob, sys
