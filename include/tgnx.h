@@ -223,6 +223,13 @@ int tgnx_tgnn_advance(int64_t* ctl, int32_t mode, int64_t batch_start, int64_t B
  * once the forward has read them (nothing later in the step does). */
 int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t gen_neg,
                             int32_t dropout, void* stream);
+/* The same for a resident split with the batch cursor folded in (one launch fewer per step):
+ * tgnx_tgnn_advance(ctl, mode 1, ..., split_lo, split_hi, batch, rank, world, base_seed, train 1) followed by
+ * tgnx_tgnn_train_fwd_bwd(gen_neg 1), as one call.  The step's first launch derives the batch descriptor from the
+ * step counter and publishes it; the counter advances in its second launch.  Same results (ctl words included). */
+int tgnx_tgnn_train_fwd_bwd_resident(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int64_t split_lo,
+                                     int64_t split_hi, int64_t batch, int32_t rank, int32_t world,
+                                     uint64_t base_seed, int32_t dropout, void* stream);
 /* Train step, part 2 (optimizer.step): Adam on the (possibly all-reduced) grads, loss sum. */
 int tgnx_tgnn_train_update(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, void* stream);
 /* Eval step (epoch_utils.py:28-157): Kn negatives per event, logits in block order,

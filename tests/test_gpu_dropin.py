@@ -99,3 +99,39 @@ def test_entry_script_runs_one_epoch():
                         "--epochs", "2", "--batch", "200"], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "Validation mrr" in r.stdout and "ap and auc" in r.stdout, r.stdout[-2000:]
+
+
+def test_folded_cursor_equals_advance_plus_step():
+    """tgnx_tgnn_train_fwd_bwd_resident (the batch cursor folded into tgnn_assemble, the counter advanced in the next
+    launch) against tgnx_tgnn_advance + tgnx_tgnn_train_fwd_bwd: the same parameters, ring, time_assoc, outputs and
+    every ctl word after each replayed step of a split whose last batch is partial, then a step past the split, with
+    device-drawn negatives and dropout."""
+    from tgnx.data import block_ids
+    s = _stream(E=1300)
+    B = 200
+    blk = torch.from_numpy(block_ids(s.src, s.dst, B)).cuda()
+    dev = torch.device("cuda")
+    ev = [torch.from_numpy(x).to(dev) for x in (s.src, s.dst, s.t.astype(np.float32))]
+    msg = torch.from_numpy(s.msg).to(dev)
+    engs = []
+    for fold in (True, False):
+        m, e = _make(s)
+        m.cfg.feat_drop = m.cfg.attn_drop = 0.6
+        e.fold_cursor = fold
+        neg_buf = torch.zeros(s.num_events, dtype=torch.long, device=dev)
+        e.bind_resident(ev[0], ev[1], ev[2], blk, msg, neg_buf, 0, 1100, B, dropout=True)
+        assert e._fold == fold
+        e.begin_epoch()
+        e.capture_resident(1)
+        engs.append((m, e, neg_buf))
+    for st in range(7):      # 5 full batches, a partial one (100 events), one past the split
+        for m, e, _ in engs:
+            e.replay_resident()
+        torch.cuda.synchronize()
+        (ma, ea, na), (mb, eb, nb) = engs
+        ea.check()
+        eb.check()
+        assert torch.equal(ea.ctl, eb.ctl), (st, ea.ctl.tolist(), eb.ctl.tolist())
+        assert torch.equal(ma.flat, mb.flat) and torch.equal(ma.time_assoc, mb.time_assoc), st
+        assert torch.equal(ea.loader.e_id, eb.loader.e_id) and torch.equal(na, nb), st
+        assert torch.equal(ea.out_pos, eb.out_pos) and torch.equal(ea.out_neg, eb.out_neg), st

@@ -2447,8 +2447,11 @@ constexpr int ZH_MAX = 4;  // float4 columns per wave it holds (D <= 128 at 8 wa
 #ifndef TGNX_PRED_WAVES
 #define TGNX_PRED_WAVES 8  // 1-hop predictor workgroup waves (4: the round-4 layout, one staging wave)
 #endif
+#ifndef TGNX_PRED_WAVES2
+#define TGNX_PRED_WAVES2 8  // 2-hop predictor workgroup waves: wave 0 loads the roots' embedding rows, the others stage
+#endif                      // the weights (LDS-DMA), all share the contractions (4: the round-5 layout)
 template <bool ATT>
-constexpr int pred_waves() { return ATT ? TGNX_PRED_WAVES : 4; }
+constexpr int pred_waves() { return ATT ? TGNX_PRED_WAVES : TGNX_PRED_WAVES2; }
 // EB: edges per attention load batch (attn_centre): 10 for rings of K <= 10 (the reference's sampling size), else 16
 template <bool ATT, int EB = ATT_EB>
 __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, int nmk, int nsrt, PlanOut po, int npl) {
@@ -2484,7 +2487,7 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
   const int B = (int)c.ctl[TGNX_CTL_B];
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
   const int64_t err = c.ctl[TGNX_CTL_ERR];
-  constexpr int NST = ATT ? (NW - 3) * 64 : 3 * 64;  // staging threads: ATT waves 0, 4 .. NW-1; else waves 1-3
+  constexpr int NST = ATT ? (NW - 3) * 64 : (NW - 1) * 64;  // staging threads: ATT waves 0, 4 .. NW-1; else 1 .. NW-1
   // a workgroup takes events slot, slot + G, ... (G = the event workgroups, at most one per CU: the weights are
   // staged once per workgroup, and its LDS leaves room for one workgroup per CU, so a batch of more events than
   // CUs ran in dispatch rounds of a whole workgroup each; pred_groups)
@@ -2560,7 +2563,7 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     const float4* S4 = reinterpret_cast<const float4*>(c.params + c.L.lsw);
     const float4* D4 = reinterpret_cast<const float4*>(c.params + c.L.ldw);
     bool staged = false;
-    if (ATT && flat && !staged) {  // the LDS image is the global one: global_load_lds_dwordx4 straight into it, no
+    if (flat && !staged) {  // the LDS image is the global one: global_load_lds_dwordx4 straight into it, no
                                    // registers, every row in flight at once (the waves drain them before the barrier)
       for (int x0 = 0; x0 < n4; x0 += NST) {
         const int x = x0 + st;

@@ -130,6 +130,12 @@ struct __attribute__((aligned(16))) EdgeMeta {
 struct Ctx {
   int64_t N;
   int K, D, d, F, Kn, drop, quirk, gen_neg;
+  // resident train step with the batch cursor folded into its first launch (tgnx_tgnn_train_fwd_bwd_resident):
+  // tgnn_assemble derives the step descriptor from the step counter (what tgnn_advance mode 1 computes) and writes
+  // it; the counter itself advances in the next launch (tgnn_meta_collapse), after all three workgroups read it
+  int adv, adv_rank, adv_world, adv_train;
+  int64_t adv_lo, adv_hi, adv_batch;
+  uint64_t adv_seed;
   float pf, pa, inv_kf, inv_ka;
   float lr, b1, b2, eps;
   const int64_t *ev_src, *ev_dst;
@@ -228,14 +234,28 @@ __device__ __forceinline__ float ta_at(const Ctx& c, int64_t u, int blk, int gen
 }
 
 // ------------------------------------------------------------------ small kernels
+// the resident step descriptor of batch nb (0-based within the split) of rank / world (tgnn_advance mode 1)
+struct StepDesc {
+  int64_t start, B, lo, hi, seed;
+};
+__device__ __forceinline__ StepDesc step_desc(int64_t nb, int64_t split_lo, int64_t split_hi, int64_t batch, int rank,
+                                              int world, uint64_t base_seed) {
+  StepDesc d;
+  d.start = split_lo + nb * batch;
+  d.B = d.start >= split_hi ? 0 : (split_hi - d.start < batch ? split_hi - d.start : batch);
+  d.lo = d.B * rank / world;
+  d.hi = d.B * (rank + 1) / world;
+  d.seed = (int64_t)(mix64(base_seed ^ mix64((uint64_t)(nb + 1))) >> 1);   // (the counter after the advance)
+  return d;
+}
 __global__ void tgnn_advance(int64_t* ctl, int mode, int64_t batch_start, int64_t B, int64_t cur, int64_t split_lo,
                              int64_t split_hi, int64_t batch, int rank, int world, uint64_t base_seed, int train) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   int64_t bs = batch_start, Bv = B, ce = cur;
   if (mode == 1) {
-    int64_t nb = ctl[TGNX_CTL_NB];
-    bs = split_lo + nb * batch;
-    Bv = bs >= split_hi ? 0 : (split_hi - bs < batch ? split_hi - bs : batch);
+    const StepDesc sd = step_desc(ctl[TGNX_CTL_NB], split_lo, split_hi, batch, rank, world, base_seed);
+    bs = sd.start;
+    Bv = sd.B;
     ce = bs;
   }
   ctl[TGNX_CTL_BATCH_START] = bs;
@@ -393,9 +413,18 @@ template <bool TRAIN>
 __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int sh[20];
-  const int B = (int)c.ctl[TGNX_CTL_B];
   const int tid = threadIdx.x, T = blockDim.x;
-  const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
+  int B;
+  int64_t start;
+  StepDesc sd{};
+  if (c.adv) {  // folded cursor: every workgroup derives the descriptor from the (not yet advanced) step counter
+    sd = step_desc(c.ctl[TGNX_CTL_NB], c.adv_lo, c.adv_hi, c.adv_batch, c.adv_rank, c.adv_world, c.adv_seed);
+    B = (int)sd.B;
+    start = sd.start;
+  } else {
+    B = (int)c.ctl[TGNX_CTL_B];
+    start = c.ctl[TGNX_CTL_BATCH_START];
+  }
   if (blockIdx.x == 1) {  // ring insert plan
     if (B == 0 || B > c.Bmax) return;
     TGNN_PHASE_STAMP(c, 8);
@@ -433,11 +462,25 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     if (tid == 0) c.misc[MISC_KMAX] = (int)(key[B - 1] >> 12);
     return;
   }
+  // workgroup 0 publishes the descriptor (later launches read it; tgnn_meta_collapse advances the step counter)
+  const int gen = (int)c.ctl[TGNX_CTL_GEN] + (c.adv ? 1 : 0);
+  if (c.adv) __syncthreads();  // (every thread has read the counter before thread 0 rewrites it)
+  if (c.adv && tid == 0) {
+    int64_t* ctl = c.ctl;
+    ctl[TGNX_CTL_BATCH_START] = sd.start;
+    ctl[TGNX_CTL_B] = sd.B;
+    ctl[TGNX_CTL_STEP_B] = sd.B;
+    ctl[TGNX_CTL_CUR_EID] = sd.start;
+    ctl[TGNX_CTL_GEN] = gen;
+    if (c.adv_train && sd.B > 0) ctl[TGNX_CTL_ADAM_T] += 1;
+    ctl[TGNX_CTL_LO] = sd.lo;
+    ctl[TGNX_CTL_HI] = sd.hi;
+    ctl[TGNX_CTL_SEED] = sd.seed;
+  }
   if (B == 0) {
     if (tid == 0) c.ctl[TGNX_CTL_S] = c.ctl[TGNX_CTL_E] = 0;
     return;
   }
-  const int gen = (int)c.ctl[TGNX_CTL_GEN];
   const int64_t* src = c.ev_src + start;
   const int64_t* dst = c.ev_dst + start;
   const float* evt = c.ev_t + start;
@@ -456,8 +499,8 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   uint64_t* tmp = reinterpret_cast<uint64_t*>(run_of + NTc);
   TGNN_PHASE_STAMP(c, 0);
   if (TRAIN && c.gen_neg) {  // NegLinkSamplerDest.sample (neg_sampler.py:8-23), counter-based stream
-    const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
-    const uint64_t off = (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
+    const uint64_t seed = c.adv ? (uint64_t)sd.seed : (uint64_t)c.ctl[TGNX_CTL_SEED];
+    const uint64_t off = c.adv ? (uint64_t)sd.start : (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
     for (int i = tid; i < B; i += T) {
       const int64_t pd = dst[i];
       int64_t v = c.dst_nodes[0];
@@ -517,7 +560,7 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     }
   }
   TGNN_PHASE_STAMP(c, 4);
-  const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
+  const int lo = c.adv ? (int)sd.lo : (int)c.ctl[TGNX_CTL_LO], hi = c.adv ? (int)sd.hi : (int)c.ctl[TGNX_CTL_HI];
   const int nloc = hi - lo;
   const int S = nloc * (2 + c.Kn);
   if (TRAIN) {  // in-edge count of each segment (= touch p of this rank's rows, Kn == 1):
@@ -661,6 +704,9 @@ __device__ void edge_meta_body(const Ctx& c, const int bid, const int nblk) {
 // collapse blocks
 template <bool TRAIN>
 __global__ void __launch_bounds__(256) tgnn_meta_collapse(Ctx c, int nmeta) {
+  // folded cursor: the step counter advances here, after tgnn_assemble's workgroups all read it (nothing in this
+  // launch or later reads it within the step)
+  if (c.adv && blockIdx.x == 0 && threadIdx.x == 0) c.ctl[TGNX_CTL_NB] += 1;
   if ((int)blockIdx.x < nmeta) edge_meta_body<TRAIN>(c, blockIdx.x, nmeta);
   else collapse_body(c, blockIdx.x - nmeta, gridDim.x - nmeta);
 }
@@ -1954,11 +2000,48 @@ int tgnx_tgnn_advance(int64_t* ctl, int32_t mode, int64_t batch_start, int64_t B
   return TGNX_OK;
 }
 
+static int train_fwd_bwd_impl(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t gen_neg,
+                              int32_t dropout, void* stream, const Ctx* adv);
+
 int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t gen_neg,
                             int32_t dropout, void* stream) {
+  return train_fwd_bwd_impl(cfg, buf, gen_neg, dropout, stream, nullptr);
+}
+
+int tgnx_tgnn_train_fwd_bwd_resident(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int64_t split_lo,
+                                     int64_t split_hi, int64_t batch, int32_t rank, int32_t world, uint64_t base_seed,
+                                     int32_t dropout, void* stream) {
+  TGNX_CHECK_ARG(batch > 0 && batch < 4096 && world >= 1 && rank >= 0 && rank < world && split_lo >= 0 &&
+                     split_hi >= split_lo,
+                 "tgnx_tgnn_train_fwd_bwd_resident: bad cursor arguments");
+  Ctx a;
+  memset(&a, 0, sizeof(a));
+  a.adv = 1;
+  a.adv_lo = split_lo;
+  a.adv_hi = split_hi;
+  a.adv_batch = batch;
+  a.adv_rank = rank;
+  a.adv_world = world;
+  a.adv_seed = base_seed;
+  a.adv_train = 1;
+  return train_fwd_bwd_impl(cfg, buf, 1, dropout, stream, &a);
+}
+
+static int train_fwd_bwd_impl(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t gen_neg,
+                              int32_t dropout, void* stream, const Ctx* adv) {
   Ctx c;
   int rc = make_ctx(cfg, buf, 1, c);
   if (rc) return rc;
+  if (adv) {
+    c.adv = 1;
+    c.adv_lo = adv->adv_lo;
+    c.adv_hi = adv->adv_hi;
+    c.adv_batch = adv->adv_batch;
+    c.adv_rank = adv->adv_rank;
+    c.adv_world = adv->adv_world;
+    c.adv_seed = adv->adv_seed;
+    c.adv_train = adv->adv_train;
+  }
   TGNX_CHECK_ARG(buf->neg && buf->grads && buf->out_pos && buf->out_neg && buf->feat && buf->ev_msg && buf->memory &&
                      buf->time_assoc && buf->nbr && buf->eid && buf->rt,
                  "tgnx_tgnn_train_fwd_bwd: null buffer");

@@ -69,6 +69,7 @@ SIGNATURES = {
     "tgnx_tgnn_advance": (ctypes.c_int, [P, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64,
                                          c_i32, c_vp]),
     "tgnx_tgnn_train_fwd_bwd": (ctypes.c_int, [P, P, c_i32, c_i32, c_vp]),
+    "tgnx_tgnn_train_fwd_bwd_resident": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64, c_i32, c_vp]),
     "tgnx_tgnn_train_update": (ctypes.c_int, [P, P, c_vp]),
     "tgnx_tgnn_eval_step": (ctypes.c_int, [P, P, c_i32, c_i32, c_vp]),
 }
@@ -84,6 +85,8 @@ def lib():
                                "(or __graft_entry__.build()); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("TGNX_LIB") and not hasattr(L, name):
+                continue    # (an older library selected for a same-box A/B: entry points it predates stay unbound)
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

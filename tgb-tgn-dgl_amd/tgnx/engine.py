@@ -70,6 +70,7 @@ class TgnnEngine:
             self.adam_m, self.adam_v = optimizer.exp_avg, optimizer.exp_avg_sq
         self._neg_scratch = None
         self.out_ev = None    # optional per-event train-logit log (tgnx_tgnn_buffers.out_ev)
+        self.fold_cursor = True
 
     # ------------------------------------------------------------------ plumbing
     def _buffers(self, src, dst, t, blk, msg, neg) -> TgnnBuffers:
@@ -163,6 +164,9 @@ class TgnnEngine:
         self._res_drop = 1 if (dropout and self.model.training) else 0
         L = _lib.lib()
         self._f = (L.tgnx_tgnn_advance, L.tgnx_tgnn_train_fwd_bwd, L.tgnx_tgnn_train_update)
+        # the batch cursor folded into the step's first launch (tgnx_tgnn_train_fwd_bwd_resident: one launch fewer);
+        # fold_cursor = False keeps tgnx_tgnn_advance + tgnx_tgnn_train_fwd_bwd (same results)
+        self._fold = self.fold_cursor and hasattr(L, "tgnx_tgnn_train_fwd_bwd_resident")
         self._cfg_ref = ctypes.byref(self.cfg)
         self._buf_ref = ctypes.byref(self._res_buf)
         self._ctl_p = ctypes.c_void_p(self.ctl.data_ptr())
@@ -172,12 +176,19 @@ class TgnnEngine:
         self.loader.reset_state()
         self.ctl[CTL["NB"]] = 0
 
-    def resident_train_step(self):
-        adv, fb, up = self._f
-        st = self._stream()
+    def _resident_fwd_bwd(self, st):
+        adv, fb, _ = self._f
         lo, hi, batch = self._res
+        if self._fold:
+            return _lib.lib().tgnx_tgnn_train_fwd_bwd_resident(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank,
+                                                              self.world, self.seed, self._res_drop, st)
         rc = adv(self._ctl_p, 1, 0, 0, 0, lo, hi, batch, self.rank, self.world, self.seed, 1, st)
-        rc |= fb(self._cfg_ref, self._buf_ref, 1, self._res_drop, st)
+        return rc | fb(self._cfg_ref, self._buf_ref, 1, self._res_drop, st)
+
+    def resident_train_step(self):
+        up = self._f[2]
+        st = self._stream()
+        rc = self._resident_fwd_bwd(st)
         if rc:
             raise RuntimeError(f"tgnx resident step failed: {_lib.lib().tgnx_last_error().decode()}")
         self._allreduce_grads()
@@ -189,14 +200,11 @@ class TgnnEngine:
         Every kernel reads its batch from the device control block, so replaying a graph advances
         through consecutive batches.  world > 1: the gradient all-reduce stays eager between a
         captured forward/backward graph and a captured update graph."""
-        adv, fb, up = self._f
-        lo, hi, batch = self._res
-        cfg, buf, ctl = self._cfg_ref, self._buf_ref, self._ctl_p
+        up = self._f[2]
+        cfg, buf = self._cfg_ref, self._buf_ref
 
         def pre():
-            st = self._stream()
-            rc = adv(ctl, 1, 0, 0, 0, lo, hi, batch, self.rank, self.world, self.seed, 1, st)
-            rc |= fb(cfg, buf, 1, self._res_drop, st)
+            rc = self._resident_fwd_bwd(self._stream())
             if rc:
                 raise RuntimeError(_lib.lib().tgnx_last_error().decode())
 

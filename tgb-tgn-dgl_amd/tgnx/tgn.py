@@ -553,7 +553,7 @@ class TgnEngine:
     def _release_plan_table(self):
         """Drop the bound split's plan table, and the library's record of it (tgnx_tgn_plan_table_release): the
         caching allocator may hand its address to another tensor."""
-        if self.plan_table is not None:
+        if self.plan_table is not None and hasattr(_lib.lib(), "tgnx_tgn_plan_table_release"):
             torch.cuda.synchronize(self.dev)      # (no step still reading it)
             _lib.lib().tgnx_tgn_plan_table_release(ctypes.c_void_p(self.plan_table.data_ptr()))
         self.plan_table = None
