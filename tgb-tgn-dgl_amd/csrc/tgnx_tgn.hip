@@ -2448,10 +2448,19 @@ constexpr int ZH_MAX = 4;  // float4 columns per wave it holds (D <= 128 at 8 wa
 #define TGNX_PRED_WAVES 8  // 1-hop predictor workgroup waves (4: the round-4 layout, one staging wave)
 #endif
 #ifndef TGNX_PRED_WAVES2
-#define TGNX_PRED_WAVES2 8  // 2-hop predictor workgroup waves: wave 0 loads the roots' embedding rows, the others stage
-#endif                      // the weights (LDS-DMA), all share the contractions (4: the round-5 layout)
+#define TGNX_PRED_WAVES2 4  // 2-hop predictor workgroup waves: wave 0 loads the roots' embedding rows, the others stage
+#endif                      // the weights, all share the contractions (8: 44.5 vs 42.5 us, r6e rocprof)
 template <bool ATT>
 constexpr int pred_waves() { return ATT ? TGNX_PRED_WAVES : TGNX_PRED_WAVES2; }
+#ifndef TGNX_PRED2_STAGE
+#define TGNX_PRED2_STAGE 1  // 2 hops: 1 stages lin_src / lin_dst in LDS once per workgroup and loops over events; 0 reads
+#endif                      // them from L2, one event per workgroup (uncoalesced rows: comment step 0.2444 vs 0.2395 ms)
+#ifndef TGNX_PRED2_WIDE_ATOM
+#define TGNX_PRED2_WIDE_ATOM 0  // 2 hops: the dZc adds as whole rows through LDS (the 1-hop form, one more barrier); 0: each
+#endif                          // wave adds its own outputs (the round-4 form; ±0, r6i_2hop_ab.txt)
+// whether the predictor stages its weights in LDS (1 hop: the attention waves overlap the staging)
+template <bool ATT>
+constexpr bool pred_stages() { return ATT || TGNX_PRED2_STAGE; }
 // EB: edges per attention load batch (attn_centre): 10 for rings of K <= 10 (the reference's sampling size), else 16
 template <bool ATT, int EB = ATT_EB>
 __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, int nmk, int nsrt, PlanOut po, int npl) {
@@ -2480,10 +2489,12 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
   // (start banks 4 D o mod 64 distinct over 16 lanes) and for b32 column reads, and the LDS image is the
   // global one (b128 stores); other D: pitch D + 1, element stores
   const int D = c.D;
-  const bool flat = D % 8 == 4;
+  constexpr bool STW = pred_stages<ATT>();
+  const bool flat = !STW || D % 8 == 4;
   const int DP = flat ? D : D + 1;
-  float* Wsrc = Wl;
-  float* Wdst = Wl + D * DP;
+  // the weights: the LDS image (STW), else the parameter rows in global memory (L2-resident, read by every workgroup)
+  float* Wsrc = STW ? Wl : c.params + c.L.lsw;
+  float* Wdst = STW ? Wl + D * DP : c.params + c.L.ldw;
   const int B = (int)c.ctl[TGNX_CTL_B];
   const int lo = (int)c.ctl[TGNX_CTL_LO], hi = (int)c.ctl[TGNX_CTL_HI];
   const int64_t err = c.ctl[TGNX_CTL_ERR];
@@ -2556,8 +2567,17 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
       }
     }
     if (!live) return;
+    if (!STW) {  // the biases and the output layer only
+      for (int x = st; x < 3 * D + 1; x += NST) {
+        const float v = x < D ? c.params[c.L.lsb + x] : x < 2 * D ? c.params[c.L.ldb + x - D]
+                      : x < 3 * D ? c.params[c.L.lfw + x - 2 * D] : c.params[c.L.lfb];
+        if (x < D) vsb[x] = v;
+        else if (x < 2 * D) vdb[x - D] = v;
+        else vfw[x - 2 * D] = v;
+      }
+    }
     // D is even, so D * D % 4 == 0; the flat buffer's blocks are 16-B aligned (tgnx_tgn_param_layout)
-    if (first) {  // (later events of the workgroup: the weights are in LDS already)
+    if (STW && first) {  // (later events of the workgroup: the weights are in LDS already)
     const int n4 = D * D / 4;
     const float invD = 1.0f / (float)D;
     const float4* S4 = reinterpret_cast<const float4*>(c.params + c.L.lsw);
@@ -2829,6 +2849,13 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     b = swap32_sum(b);
     d2 = swap32_sum(d2);
     float* dz = c.dZc + (int64_t)(slot % c.dzrep) * c.dzstride;
+    if (!ATT && !TGNX_PRED2_WIDE_ATOM) {
+      if (kg == 0 && oko) {
+        atomicAdd(&dz[(int64_t)cr[0] * D + o], a);
+        atomicAdd(&dz[(int64_t)cr[1] * D + o], b);
+        atomicAdd(&dz[(int64_t)cr[2] * D + o], d2);
+      }
+    } else {
     // the three rows gathered in LDS first, then added with whole-row wave instructions (contiguous lanes: 6 per
     // workgroup instead of 3 per wave on 13-lane segments — every one of them queues on a hub centre's row)
     __shared__ float dzl[3][TDMAX];
@@ -2842,6 +2869,7 @@ __global__ void __launch_bounds__(64 * pred_waves<ATT>()) tgn_pred_train(Ctx c, 
     for (int x = tid; x < 3 * D; x += 64 * NW) {
       const int r = x >= 2 * D ? 2 : x >= D ? 1 : 0, oo = x - r * D;
       atomicAdd(&dz[(int64_t)cr[r] * D + oo], dzl[r][oo]);
+    }
     }
   }
   if (ATT || lo + slot + G >= hi) break;  // (ATT: one event per workgroup — the loop's live ranges spilled the
@@ -4735,9 +4763,12 @@ static Ctx root_view(const Ctx& c) {
 #endif
 // the attention backward for a ring of K and the predictor's dZc copy count (compile-time: the copies' loads batched)
 using AttnBwdFn = void (*)(Ctx, int, int, int, Ctx);
-static AttnBwdFn attn_bwd_fn(int K, int rep) {
+#ifndef TGNX_ATTB_EB10_2HOP
+#define TGNX_ATTB_EB10_2HOP 1  // 2 hops: the attention backward in 10-edge load batches for K <= 10 (0: 16-edge batches)
+#endif
+static AttnBwdFn attn_bwd_fn(int K, int rep, bool two = false) {
   if (rep == TGNX_DZC_REP && TGNX_DZC_REP > 1) return K <= 10 ? tgn_attn_bwd<10, TGNX_DZC_REP> : tgn_attn_bwd<ATT_EB, TGNX_DZC_REP>;
-  return K <= 10 ? tgn_attn_bwd<10, 1> : tgn_attn_bwd<ATT_EB, 1>;
+  return K <= 10 && (!two || TGNX_ATTB_EB10_2HOP) ? tgn_attn_bwd<10, 1> : tgn_attn_bwd<ATT_EB, 1>;
 }
 // integer knob from the environment (host, read once by the caller's static), else the build default
 static inline int env_int(const char* name, int def) {
@@ -4755,15 +4786,12 @@ static inline int gridn(int64_t n, int per, int cap = 4096) {
   return (int)(g < cap ? g : cap);
 }
 
-// event workgroups of the predictor launch: one per event up to the CU count, else the batch dealt evenly to at most
-// that many (tgn_pred_train loops; its LDS holds one workgroup per CU)
+// event workgroups of the 2-hop predictor launch: one per event (its LDS holds one workgroup per CU, so a batch of more
+// events than CUs runs in dispatch rounds), or with TGNX_PRED_GROUPS = G at most G workgroups looping over the batch
+// with the weights staged once (G = the CU count: comment-shaped B = 600 step 0.2380 / 0.2384 ms against 0.2359 /
+// 0.2347 one per event, profiles/r6/r6i_2hop_groups_ab.txt)
 static int pred_groups(int B) {
-  static const int ncu = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      n = 256;
-    return std::max(1, env_int("TGNX_PRED_GROUPS", n));
-  }();
+  static const int ncu = std::max(1, env_int("TGNX_PRED_GROUPS", 1 << 30));
   if (B <= ncu) return std::max(B, 1);
   const int per = (B + ncu - 1) / ncu;
   return (B + per - 1) / per;
@@ -5124,7 +5152,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   probe_begin(TGNX_K_PRED, s);
   TGNX_CHECK_ARG(pred_smem_ok(c.D), "tgn_pred_train: dynamic LDS attribute refused");
   const int nmk = ppm || pipe ? nmark : 0;
-  const size_t psm = std::max({tgn_pred_smem(c.D), nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0,
+  const size_t psm = std::max({att_in_pred || pred_stages<false>() ? tgn_pred_smem(c.D) : (size_t)16,
+                               nmk ? (size_t)3 * MARK_LDS_WORDS * 4 : (size_t)0,
                                npl ? tgn_scan_smem(k.B) : (size_t)0});
   const int nsrt = (two ? cr.kvs : kvs) ? 1 : 0;  // (kvs: the rows fit the sort's LDS counters)
   const PlanOut po = plan_out(ppm ? cn : c);
@@ -5132,7 +5161,8 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     launch_k(c.K <= 10 ? tgn_pred_train<true, 10> : tgn_pred_train<true, ATT_EB>, dim3(kr.B + npl + nsrt + nmk),
              dim3(64 * pred_waves<true>()), (uint32_t)psm, s, cr, nmk, nsrt, po, npl);
   else
-    launch_k(tgn_pred_train<false>, dim3(pred_groups(kr.B) + npl + nsrt + nmk), dim3(64 * pred_waves<false>()), (uint32_t)psm, s, cr,
+    launch_k(tgn_pred_train<false>, dim3((pred_stages<false>() ? pred_groups(kr.B) : kr.B) + npl + nsrt + nmk),
+             dim3(64 * pred_waves<false>()), (uint32_t)psm, s, cr,
              nmk, nsrt, po, npl);
   probe_end(TGNX_K_PRED, s);
   TGNX_LAUNCH_CHECK("tgn_pred_train");
@@ -5149,7 +5179,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     // conv2 backward (‖ predictor reductions) -> dP2, dE2; then dh1 = dP2 [Wq2; Wk2; Wv2; Wsk2] ‖ dW_proj2,
     // dW_edge2 (deferred) ‖ conv2's lin_edge -> Δt-encoding partials; then conv backward from dh1
     const int ncb1 = gridn(kr.R1tr, 4, 1 << 20);
-    launch_k(attn_bwd_fn(c.K, cr.dzrep), dim3(ncb1 + gridn(3 * D + 2, 4)), dim3(256), 0u, s, cr, ncb1, 0, 0, cr);
+    launch_k(attn_bwd_fn(c.K, cr.dzrep, true), dim3(ncb1 + gridn(3 * D + 2, 4)), dim3(256), 0u, s, cr, ncb1, 0, 0, cr);
     TGNX_LAUNCH_CHECK("tgn_attn_bwd2");
     // conv2's (dk, dv) sums ‖ its dE2-only GEMMs (as in the 1-hop step below), then dh1 ‖ dW_proj2
     const auto j_dwe2 = gemm_job<GW>(shp_dWe2(kr, c.cnt), LoadKRow{c.dE2, HC, kr.E1tr, HC}, LoadAttrMapT{ea1},
@@ -5169,7 +5199,7 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
     gemmN_launch(s, j_dh1, j_dwp2);
     TGNX_LAUNCH_CHECK("tgn_dh1");
     const int ncb = gridn(kr.Rtr, 4, 1 << 20), nkv = kvf ? gridn(kr.Etr, KVE_CH, 1 << 20) : 0;
-    launch_k(attn_bwd_fn(c.K, c.dzrep), dim3(ncb + nkv + nwalk), dim3(256), walk_lds, s, c,
+    launch_k(attn_bwd_fn(c.K, c.dzrep, true), dim3(ncb + nkv + nwalk), dim3(256), walk_lds, s, c,
              ncb, nkv, nwalk, nwalk ? cn : c);
   } else {
     const int ncb = gridn(kr.Rtr, 4, 1 << 20);
