@@ -33,19 +33,6 @@ __device__ __forceinline__ void st_wt(float* p, float v) {
 __device__ __forceinline__ void st_wt4(float* base, int off, int bytes, f32x4_t v) {
   *reinterpret_cast<f32x4_t*>(reinterpret_cast<char*>(base) + off) = v;
 }
-// The split-K last-arriver hand-off (MI355X_MICROARCH.md, hand-off table row 1): every split stores its partial tile
-// with 16-B sc1 (write-through) buffer stores, every storing wave waits for them (vmcnt(0)), the workgroup joins a
-// barrier, then one lane adds 1 to the tile's agent-scope counter; the workgroup whose add returns S - 1 reads every
-// partial with sc1 buffer loads and finishes the tile.  No L2 write-back / invalidate (buffer_wbl2 / buffer_inv).
-__device__ __forceinline__ void st_sc1x4(float* base, int off, int bytes, f32x4_t v) {
-  const auto r = __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r, off, 0,
-                                         16);
-}
-__device__ __forceinline__ f32x4_t ld_sc1x4(const float* base, int off, int bytes) {
-  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, bytes, 0x00020000);
-  return __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
-}
 
 template <int TM_, int TN_, int KC_, int PF_ = 1, bool WS_ = false, int DR_ = 0>
 struct GemmCfg {
@@ -129,8 +116,6 @@ struct GemmShape {
   int deferred;                      // 1: write partials for gemm_fixup_kernel
   const int *Mdev, *Ndev, *Kdev;     // optional runtime sizes on the device (<= capacities)
   int cap;                           // grid cap (a multiple of 8; gemm_blocks)
-  int* arrive = nullptr;             // deferred: per-tile arrival counters (zero between steps) — the last split to
-                                     // arrive sums the partials and runs the epilogue in-launch (no fixup tile)
 };
 // direct GEMM: S = 1, the workgroup loops over all of K
 template <class CFG>
@@ -666,47 +651,13 @@ __device__ __forceinline__ void gemm_tile(const GemmShape& g, const GemmRt& rt, 
     epi(GemmTile<TM, TN>{Ct, m0, n0, rt.Mr, rt.Nr, Ct + TM * PB});
     return;
   }
-  if (g.deferred) {  // partial tile in register layout, summed by gemm_fixup_kernel (or by the last arriver)
+  if (g.deferred) {  // partial tile in register layout, summed by gemm_fixup_kernel
     float* mine = part + ((size_t)tile * g.S + s) * TM * TN;
-    if (!g.arrive) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) st_wt4(mine, (((wv * FM + i) * FN + j) * 64 + lane) * 16, TM * TN * 4, acc[i][j]);
-      return;
-    }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) st_sc1x4(mine, (((wv * FM + i) * FN + j) * 64 + lane) * 16, TM * TN * 4, acc[i][j]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its partial stores done
-    __syncthreads();
-    int* last = reinterpret_cast<int*>(smem);
-    if (tid == 0)
-      last[0] = __hip_atomic_fetch_add(g.arrive + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == rt.Sr - 1;
-    __syncthreads();
-    const bool am_last = last[0] != 0;
-    __syncthreads();  // (the flag's LDS word is the C tile's below)
-    if (!am_last) return;
-    if (tid == 0) __hip_atomic_store(g.arrive + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // Σ partials in split order (as gemm_fix_tile: bit-identical sums), every split's loads in flight at once
-    const float* tp = part + (size_t)tile * g.S * TM * TN;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        constexpr int SU = 8;
-        const int off = (((wv * FM + i) * FN + j) * 64 + lane) * 16;
-        f32x4_t sum = {0.f, 0.f, 0.f, 0.f};
-        for (int q0 = 0; q0 < rt.Sr; q0 += SU) {
-          f32x4_t pv[SU];
-#pragma unroll
-          for (int u = 0; u < SU; ++u) pv[u] = ld_sc1x4(tp + (size_t)min(q0 + u, rt.Sr - 1) * TM * TN, off, TM * TN * 4);
-#pragma unroll
-          for (int u = 0; u < SU; ++u) sum += pv[u] * f01(q0 + u < rt.Sr);
-        }
-        acc[i][j] = sum;
-      }
+      for (int j = 0; j < FN; ++j) st_wt4(mine, (((wv * FM + i) * FN + j) * 64 + lane) * 16, TM * TN * 4, acc[i][j]);
+    return;
   }
   float* Ct = smem;  // [TM][PB]
 #pragma unroll
@@ -951,7 +902,7 @@ __global__ void __launch_bounds__(256) gemm_fixup_kernel(TAIL tail, int head, in
   bid -= head;
   if (bid < nfix) {
     bid = (bid & 7) * (nfix >> 3) + (bid >> 3);
-    (void)(gemm_fix_dispatch(f, bid, smem) || ...);  // (padding blocks: past every GEMM's tiles)
+    (gemm_fix_dispatch(f, bid, smem) || ...);  // (padding blocks: past every GEMM's tiles)
     return;
   }
   tail(head + bid - nfix, smem);

@@ -246,7 +246,6 @@ struct Ctx {
   float* encE;  // per sampled edge: the dense train edge row [cos of the Δt encoding argument | msg] [E][D + d]
   float *s0m, *s1m;    // per GRU row: (mean over its messages of) sin(arg), sin(arg) Δt  [M][D]
   float *pA, *pB, *pC, *pD;  // split-K partials of the deferred weight-gradient GEMMs
-  int *aA, *aB, *aC, *aD;    // their per-tile arrival counters (the last-arriver form, TGNX_SPLITK_LA)
   uint64_t *rkeys, *skeys;
   int *rruns, *sruns;
   // plans split by node range over pplan workgroups each (tgn_scan): partition q's keys at [poff[q], +n_q) of
@@ -4100,9 +4099,6 @@ struct MarkNextJob {
     mark_body<true>(c, bid, nb, 1, reinterpret_cast<uint32_t*>(smem));
   }
 };
-#ifndef TGNX_SPLITK_LA
-#define TGNX_SPLITK_LA 1  // the 1-hop world-1 parity-set step: split-K weight gradients finished by the last arriver
-#endif
 #ifndef TGNX_SCAN_T
 #define TGNX_SCAN_T TGN_SCAN_THREADS  // train-step scan workgroup size (experiments)
 #endif
@@ -4362,16 +4358,9 @@ static GemmShape shp_dWp2(const Caps& k, const int* cnt) { return gemm_shape_spl
 static GemmShape shp_dWe2(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.HC, k.D + k.d, k.E1tr, nullptr, nullptr, cnt ? cnt + CNT_E1 : nullptr, ksplit(k.E1tr, 8)); }
 static GemmShape shp_dWlp(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(2 * k.D, k.D, 3 * k.B, nullptr, nullptr, cnt ? cnt + CNT_LIST : nullptr, std::max(TGNX_S_LP, std::min(64, (3 * k.B + 63) / 64))); }
 static GemmShape shp_dWg(const Caps& k, const int* cnt) { return gemm_shape_split<GW>(k.G * k.D, k.Qm + k.D + 1, k.Mtr, nullptr, nullptr, cnt ? cnt + CNT_M : nullptr, std::min(TGNX_DWG_SMAX, ksplit(k.Mtr, TGNX_S_WG))); }
-// arrival counters per deferred GEMM: room for the largest one's tiles
-static size_t arrive_stride(const Caps& k) {
-  const GemmShape g[4] = {shp_dWe(k, nullptr), shp_dWp(k, nullptr), shp_dWlp(k, nullptr), shp_dWg(k, nullptr)};
-  size_t m = 0;
-  for (const GemmShape& x : g) m = std::max(m, (size_t)x.tiles_m * x.tiles_n);
-  return (m + 63) & ~(size_t)63;
-}
 struct WsLay {
   size_t cb, nb, cbs, nbs, cl, nl, rbs, rl, kval, cnt, cent, cent_loc, ceoff, crank, upd_loc, nid, upd, e_j, e_c, kj, kx, ke, e_id, e_t, X, trel, lu, xw, gates, Z0, P,
-      Ep, alpha, alk, Qo, Zc, Hp, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, s0m, s1m, pA, pB, pC, pD, arv, rkeys, rruns, skeys, sruns, pcnt,
+      Ep, alpha, alk, Qo, Zc, Hp, evs, evr, evq, evj, cevq, cevj, Hs, Hd, dZc, dP, dE, dKV, dG, tgp, encE, s0m, s1m, pA, pB, pC, pD, rkeys, rruns, skeys, sruns, pcnt,
       snap, rb, x2r, cent1, r_x2, ceoff1, e1_j, e1_e2, e1_id, P2, Ep2, alpha1, Zr, dZr, dP2, dE2, pE, pF,
       uX, uZ, uG, ulu, uxw, utrel, total;
   int tgp_rows, tgp_e1;
@@ -4444,7 +4433,6 @@ static WsLay make_ws(const tgnx_tgn_config* cfg, const Caps& k) {
   W.pB = carve(off, gemm_partial_floats(shp_dWp(k, nullptr)) * 4);
   W.pC = carve(off, gemm_partial_floats(shp_dWlp(k, nullptr)) * 4);
   W.pD = carve(off, gemm_partial_floats(shp_dWg(k, nullptr)) * 4);
-  W.arv = carve(off, (size_t)4 * arrive_stride(k) * 4);  // (zeroed with the workspace; every use leaves them zero)
   const int n2 = 2 * k.B;
   W.rkeys = carve(off, (size_t)n2 * 8);
   W.rruns = carve(off, (size_t)(n2 + 2 + TGNX_PLAN_PMAX) * 4);
@@ -4639,10 +4627,6 @@ static int make_ctx(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* b, int K
   c.pB = reinterpret_cast<float*>(ws + W.pB);
   c.pC = reinterpret_cast<float*>(ws + W.pC);
   c.pD = reinterpret_cast<float*>(ws + W.pD);
-  c.aA = reinterpret_cast<int*>(ws + W.arv);
-  c.aB = c.aA + arrive_stride(k);
-  c.aC = c.aB + arrive_stride(k);
-  c.aD = c.aC + arrive_stride(k);
   c.rkeys = reinterpret_cast<uint64_t*>(ws + W.rkeys);
   c.rruns = reinterpret_cast<int*>(ws + W.rruns);
   c.skeys = reinterpret_cast<uint64_t*>(ws + W.skeys);
@@ -5230,14 +5214,6 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // the five backward jobs in one launch took 28 us, dz0 alone 16), while kv_reduce leaves most CUs
   // idle: the dE-only GEMMs fill them here instead of lengthening the dP launch below.
   const Ctx cf = fixup_view(c);
-  // the 1-hop parity-set step at world 1 (the bench's): the four deferred weight-gradient GEMMs finish in-launch —
-  // the last split of each tile to arrive sums the partials and runs the fused-Adam epilogue (the split-K hand-off of
-  // tgnx_gemm.h, st_sc1x4) — so the fixup launch keeps only the Δt reduction and the memory update
-  const bool la = TGNX_SPLITK_LA && ppm && !two && fuse_adam && adv && adv->world == 1;
-  auto la_shape = [&](GemmShape g, int* a) {
-    g.arrive = a;
-    return g;
-  };
   const EpiGradStore e_dWe{G, c.L.we, D + d, cf.adf};
   const auto j_dwe = gemm_job<GW>(shp_dWe(kr, c.cnt), LoadKRow{c.dE, HC, kr.Etr, HC}, LoadKRow{c.encE, D + d, kr.Etr, D + d},
                                   EpiDeferred{}, c.pA);
@@ -5278,14 +5254,14 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // (the scan may ride in the dz0 launch instead: TGNX_SCAN_AT 6)
   const bool scan6 = scan_w3 && TGNX_SCAN_AT == 6;
   const bool walk_w3 = (scan_w3 || plans_pred) && !walk_bwd;  // (the walk rides in the dW_cell launch)
-  auto l8 = [&](auto dwg, auto... jobs) {
+  auto l8 = [&](auto... jobs) {
     probe_begin(TGNX_K_WGRAD3, s);
     // the GEMM jobs before the snapshot / store blocks (0.0970 vs 0.0986 ms with those first)
     // (the edge jobs dEnc / dW_edge first instead: that launch 12.8 -> 14.7 us, r5_w3_jobs_first_ab.txt)
     if (walk_w3 && !scan6)
-      gemmN_launch(s, j_scan, j_dxe, dwg, jobs..., j_snap, j_store);
+      gemmN_launch(s, j_scan, j_dxe, j_dwg, jobs..., j_snap, j_store);
     else
-      gemmN_launch_w<TGNX_W3_WAVES>(s, j_dxe, dwg, jobs..., j_snap, j_store);
+      gemmN_launch_w<TGNX_W3_WAVES>(s, j_dxe, j_dwg, jobs..., j_snap, j_store);
     probe_end(TGNX_K_WGRAD3, s);
     TGNX_LAUNCH_CHECK("tgn_wgrad3");
     return TGNX_OK;
@@ -5293,25 +5269,10 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
   // kvf: the dE-only GEMMs ride in the dW_gru launch (in the dz0 launch: 0.1013 vs 0.0987 ms; dW_proj / dW_lp
   // moved to the dW_gru launch too: 0.1013 - 0.1035), dz0 first in its launch (0.0985 vs 0.0991)
   // (the lambdas return the launch checks' status)
-  if (la) {
-    const auto j_dwe_la = gemm_job<GW>(la_shape(shp_dWe(kr, c.cnt), c.aA), LoadKRow{c.dE, HC, kr.Etr, HC},
-                                       LoadKRow{c.encE, D + d, kr.Etr, D + d}, EpiGradStore{G, c.L.we, D + d, c.adf}, c.pA);
-    const auto j_dwp_la = gemm_job<GW>(la_shape(shp_dWp(kr, c.cnt), c.aB), LoadKRow{c.dP, 4 * HC, kr.Mtr, 4 * HC},
-                                       LoadZ1T{c.Z0, D}, EpiProjGrad{G, c.L.wq, c.L.bq, c.L.pw, c.L.pb, HC, D, c.adf}, c.pB);
-    const auto j_dwlp_la = gemm_job<GW>(la_shape(shp_dWlp(kr, c.cnt), c.aC), LoadLpA{c.evs, c.ctl, D, evs_stride(D)},
-                                        LoadLpB{c.evs, c.ctl, D, evs_stride(D)}, EpiLpGrad{G, c.L.lsw, c.L.ldw, D, c.adf},
-                                        c.pC);
-    const auto j_dwg_la = gemm_job<GW>(la_shape(shp_dWg(kr, c.cnt), c.aD), LoadKRow{c.dG, Cl::G * D, kr.Mtr, Cl::G * D},
-                                       Cl::hT(c), Cl::wgrad(c), c.pD);
-    if (scan6) {
-      if ((rc = l7(j_scan, j_dz0, j_dwp_la, j_dwlp_la)) || (rc = l8(j_dwg_la, j_dwe_la, j_denc))) return rc;
-    } else if ((rc = l7(j_dz0, j_dwp_la, j_dwlp_la)) || (rc = l8(j_dwg_la, j_dwe_la, j_denc))) {
-      return rc;
-    }
-  } else if (scan6) {
-    if ((rc = l7(j_scan, j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwg, j_dwe, j_denc))) return rc;
-  } else if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwg, j_dwe, j_denc))) {  // (dW_edge in the dz0 launch:
-    return rc;                                                                       //  slower, r4_dwe_in_dz0_ab.txt)
+  if (scan6) {
+    if ((rc = l7(j_scan, j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) return rc;
+  } else if ((rc = l7(j_dz0, j_dwp, j_dwlp)) || (rc = l8(j_dwe, j_denc))) {  // (dW_edge in the dz0 launch: slower,
+    return rc;                                                                 //  r4_dwe_in_dz0_ab.txt)
   }
   if (ppm && !walk_w3 && !walk_bwd) {  // (with a plan table: the walk alone)
     tgn_scan<true><<<c.ptab ? 1 : 1 + 2 * c.pplan, TGNX_SCAN_T, tgn_scan_smem(k.B), s>>>(cn, 1, 0);
@@ -5334,8 +5295,6 @@ static int train_step_impl_c(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers*
                         gemm_fix<GW>(shp_dWg(kr, cf.cnt), c.pD, e_dWg),
                         gemm_fix<GW>(shp_dWp2(kr, cf.cnt), c.pE, EpiProjGrad{G, c.L.wq2, c.L.bq2, c.L.pw, c.L.pb, HC, HC, cf.adf}),
                         gemm_fix<GW>(shp_dWe2(kr, cf.cnt), c.pF, EpiGradStore{G, c.L.we2, D + d, cf.adf}));
-  else if (la)
-    gemm_fixup_launch_h(nscan, nscan + nte + nmem, tail, s);
   else
     gemm_fixup_launch_h(nscan, nscan + nte + nmem, tail, s, gemm_fix<GW>(shp_dWe(kr, cf.cnt), c.pA, e_dWe),
                         gemm_fix<GW>(shp_dWp(kr, cf.cnt), c.pB, e_dWp), gemm_fix<GW>(shp_dWlp(kr, cf.cnt), c.pC, e_dWlp),
