@@ -230,6 +230,11 @@ int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers
 int tgnx_tgnn_train_fwd_bwd_resident(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int64_t split_lo,
                                      int64_t split_hi, int64_t batch, int32_t rank, int32_t world,
                                      uint64_t base_seed, int32_t dropout, void* stream);
+/* World 1: the resident step whole — tgnx_tgnn_train_fwd_bwd_resident (rank 0 of 1) with Adam and the loss sum
+ * folded into its gradient expansion (one launch fewer again: no tgnx_tgnn_train_update).  The gradient buffer is
+ * still written. */
+int tgnx_tgnn_train_step_resident(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int64_t split_lo,
+                                  int64_t split_hi, int64_t batch, uint64_t base_seed, int32_t dropout, void* stream);
 /* Train step, part 2 (optimizer.step): Adam on the (possibly all-reduced) grads, loss sum. */
 int tgnx_tgnn_train_update(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, void* stream);
 /* Eval step (epoch_utils.py:28-157): Kn negatives per event, logits in block order,
@@ -278,7 +283,7 @@ int tgnx_tcsr_sample(const int64_t* indptr, const int64_t* indices, const int64_
  * TGNMemory (modules/memory_module.py:25-215) with IdentityMessage (msg_func.py:12-18) and
  * Last/Mean aggregation (msg_agg.py:15-26), GRUCell memory update, GraphAttentionEmbedding over
  * TransformerConv (emb_module.py:55-73, heads = 2, dropout on the attention), LinkPredictor
- * (decoder.py:108-123, sigmoid output fed to BCE-with-logits as the reference's loop does).
+ * (decoder.py:12-27, sigmoid output fed to BCE-with-logits as the reference's loop does).
  * The sampler state is the LastNeighborLoader ring above; ctl is the tgnx_tgnn_advance block. */
 #define TGNX_TGN_NPARAM 21
 /* layers = 2 (SURVEY §8d comment config, "2-hop temporal attention"; the build's extension, no
@@ -485,6 +490,56 @@ int tgnx_tgn_eval_step(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, 
 size_t tgnx_tgn_flush_scratch_bytes(const tgnx_tgn_config* cfg);
 int tgnx_tgn_flush(const tgnx_tgn_config* cfg, const tgnx_tgn_buffers* buf, void* scratch, size_t scratch_bytes,
                    void* stream);
+
+/* ---------------------------------------------------------------- per-operator entry points
+ * The TGN modules' operators one call each (torch.ops.tgnx.msg_agg_last / msg_agg_mean / gru_update /
+ * predictor / edge_attn_fwd / edge_attn_bwd).  The fused steps above do not call these; a caller composing
+ * the modules itself does.  Row-major fp32 tensors, int64 indices. */
+
+/* LastAggregator / MeanAggregator (modules/msg_agg.py:15-26).  mode 0 (last): out[r] = msg[argmax_r] with
+ * argmax_r the FIRST message (in message order) attaining the largest t among index == r (torch_scatter
+ * scatter_max), zeros and argmax_r = n_msg for a row without messages; t is int64 (t_dtype 0, the TGN
+ * stores' Long t) or fp32 (t_dtype 1).  mode 1 (mean): out[r] = the messages' sum (sequential, in message
+ * order) / their count, zeros for an empty row; t unused (may be NULL).  Deterministic.  An index outside
+ * [0, dim_size) is dropped and counted into *n_invalid (a device int64 the caller zeroes; may be NULL).
+ * argmax (device int64[dim_size]) may be NULL.  ws: tgnx_msg_agg_ws_bytes(n_msg, dim_size) bytes. */
+size_t tgnx_msg_agg_ws_bytes(int64_t n_msg, int64_t dim_size);
+int tgnx_msg_agg(int32_t mode, const float* msg, int64_t n_msg, int64_t dim, const int64_t* index, const void* t,
+                 int32_t t_dtype, int64_t dim_size, float* out, int64_t* argmax, int64_t* n_invalid, void* ws,
+                 size_t ws_bytes, void* stream);
+
+/* TGNMemory.memory_updater (modules/memory_module.py:57,70-78,172): h_out[M,D] = GRUCell (cell 0; weights
+ * w_ih [3D,d_in], w_hh [3D,D], torch's r,z,n chunk order) or RNNCell with tanh (cell 1; w_ih [D,d_in],
+ * w_hh [D,D]) of x [M,d_in] and h [M,D].  Biases may be NULL.  ws: tgnx_memory_cell_ws_bytes bytes. */
+size_t tgnx_memory_cell_ws_bytes(int64_t M, int64_t d_in, int64_t D);
+int tgnx_memory_cell(int32_t cell, int64_t M, int64_t d_in, int64_t D, const float* x, const float* h,
+                     const float* w_ih, const float* w_hh, const float* b_ih, const float* b_hh, float* h_out,
+                     void* ws, size_t ws_bytes, void* stream);
+
+/* LinkPredictor (modules/decoder.py:12-27, sigmoid = 1) and EdgePredictor (model_utils.py:165-195,
+ * sigmoid = 0: logits): out[i] = w_out · relu(W_src z_src[i mod n_src] + b_src + W_dst z_dst[i] + b_dst) +
+ * b_out for i < M (M = n_src: the positive pairs; M = n_src * k: EdgePredictor's `tile` pairing of negative
+ * row i with source i mod B, model_utils.py:190).  W_src, W_dst [D,d_in]; w_out [D]; b_out [1]; b_src /
+ * b_dst may be NULL.  ws: tgnx_link_predictor_ws_bytes bytes. */
+size_t tgnx_link_predictor_ws_bytes(int64_t n_src, int64_t M, int64_t d_in, int64_t D);
+int tgnx_link_predictor(int64_t n_src, int64_t M, int64_t d_in, int64_t D, const float* z_src, const float* z_dst,
+                        const float* w_src, const float* b_src, const float* w_dst, const float* b_dst,
+                        const float* w_out, const float* b_out, int32_t sigmoid, float* out, void* ws,
+                        size_t ws_bytes, void* stream);
+
+/* TransformerConv's attention (modules/emb_module.py:21-29; PyG TransformerConv, concat, no beta): for
+ * destination i with incoming edges p in [indptr[i], indptr[i+1]) (rows of the per-edge k, v, e [E, H*C];
+ * q [n_dst, H*C]), per head h: a_p = q_i·(k_p + e_p) / sqrt(C), α = softmax over i's edges (max subtracted,
+ * + 1e-16 in the denominator), out_i = Σ_p α_p (v_p + e_p) (the root weight / skip is the caller's Linear).
+ * e may be NULL (no edge features).  alpha [E, H] is written.  1 <= heads <= 8, heads * C <= 256.  indptr is
+ * clamped to [0, n_edges].  No attention dropout (eval, or dropout 0).
+ * Backward: dq [n_dst, H*C], dk / dv / de [E, H*C] (de = dk + dv, needed only with e) from dout and alpha. */
+int tgnx_edge_attn_fwd(int64_t n_dst, int64_t n_edges, int32_t heads, int32_t channels, const float* q,
+                       const float* k, const float* v, const float* e, const int64_t* indptr, float* out,
+                       float* alpha, void* stream);
+int tgnx_edge_attn_bwd(int64_t n_dst, int64_t n_edges, int32_t heads, int32_t channels, const float* dout,
+                       const float* q, const float* k, const float* v, const float* e, const int64_t* indptr,
+                       const float* alpha, float* dq, float* dk, float* dv, float* de, void* stream);
 
 #ifdef __cplusplus
 }

@@ -15,10 +15,10 @@ Follows, in /root/reference:
                        concat=True, beta=False, root_weight=True): k_j += e, v_j += e with
                        e = lin_edge(edge_attr) (no bias), alpha = softmax_i(q_i·k_j / sqrt(C)) with
                        PyG's +1e-16 denominator, out_i = Σ alpha v_j + lin_skip(x_i)
-  LinkPredictor        modules/decoder.py:108-123       pinned: tests/golden/link_pred.npz
+  LinkPredictor        modules/decoder.py:12-27       pinned: tests/golden/link_pred.npz
   train / eval step    the canonical PyG TGN loop that pyg_epoch_utils.py:9-147 carries commented out
                        (:106-137): memory(n_id) -> gnn -> link_pred -> BCEWithLogits on the
-                       sigmoid outputs (decoder.py:123 + pyg-mem-tgn.py criterion) -> update_state
+                       sigmoid outputs (decoder.py:27 + pyg-mem-tgn.py criterion) -> update_state
                        -> insert -> backward -> Adam -> detach; eval per TGB's tgbl-wiki TGN example
                        (all candidates of an event scored with the batch-start state, per-event MRR).
 PARITY UNPINNED for the [ext] parts: torch_geometric / torch_scatter are not installed here.
@@ -212,18 +212,26 @@ class RefTransformerConv(nn.Module):
         k = self.lin_key(x)[j].view(-1, H, C)
         v = self.lin_value(x)[j].view(-1, H, C)
         e = self.lin_edge(edge_attr).view(-1, H, C)
-        k = k + e
-        a = (q * k).sum(-1) / math.sqrt(C)                  # [E, H]
-        N = x.size(0)
-        amax = torch.full((N, H), -math.inf).scatter_reduce(0, i.view(-1, 1).expand(-1, H), a, "amax",
-                                                             include_self=True)
-        ex = (a - amax[i]).exp()
-        den = torch.zeros(N, H).index_add(0, i, ex) + 1e-16
-        a = ex / den[i]
-        a = nn.functional.dropout(a, p=self.dropout, training=self.training)
-        out = (v + e) * a.unsqueeze(-1)
-        out = torch.zeros(N, H, C).index_add(0, i, out).view(N, H * C)
+        out, _ = transformer_attention(q, k, v, e, i, x.size(0), self.dropout if self.training else 0.0)
         return out + self.lin_skip(x)
+
+
+def transformer_attention(q, k, v, e, i, N, dropout=0.0):
+    """[ext] TransformerConv.message + aggregate (concat, beta False): q [E,H,C] (the destination's query per
+    edge), k, v, e [E,H,C], destination index i [E].  a = q·(k+e)/sqrt(C); α = softmax per destination (max
+    subtracted, + 1e-16, torch_geometric.utils.softmax); out_i = Σ α (v+e).  Returns (out [N, H*C], α [E, H])."""
+    H, C = q.shape[1], q.shape[2]
+    k = k + e
+    a = (q * k).sum(-1) / math.sqrt(C)                  # [E, H]
+    amax = torch.full((N, H), -math.inf, dtype=q.dtype).scatter_reduce(0, i.view(-1, 1).expand(-1, H), a, "amax",
+                                                                         include_self=True)
+    ex = (a - amax[i]).exp()
+    den = torch.zeros(N, H, dtype=q.dtype).index_add(0, i, ex) + 1e-16
+    alpha = ex / den[i]
+    a = nn.functional.dropout(alpha, p=dropout, training=dropout > 0)
+    out = (v + e) * a.unsqueeze(-1)
+    out = torch.zeros(N, H, C, dtype=q.dtype).index_add(0, i, out).view(N, H * C)
+    return out, alpha
 
 
 class RefGraphAttentionEmbedding(nn.Module):
@@ -251,7 +259,7 @@ class RefGraphAttentionEmbedding(nn.Module):
 
 
 class RefLinkPredictor(nn.Module):
-    """modules/decoder.py:108-123 (returns the sigmoid)."""
+    """modules/decoder.py:12-27 (returns the sigmoid)."""
 
     def __init__(self, in_channels):
         super().__init__()

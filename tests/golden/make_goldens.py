@@ -17,7 +17,7 @@ Modules exercised (file:line of the code that produced each fixture):
                  provides the imported names is put in sys.modules so the pure-torch classes
                  can be instantiated — no DGL op is ever called)
   msg.npz        modules/msg_func.py:12-18   IdentityMessage
-  link_pred.npz  modules/decoder.py:108-123  LinkPredictor (sigmoid output)
+  link_pred.npz  modules/decoder.py:12-27  LinkPredictor (sigmoid output)
   tgn_memory_*.npz  modules/memory_module.py:25-215 + msg_agg.py:15-26 + msg_func.py:12-18
                  TGNMemory itself (IdentityMessage, Last / MeanAggregator, GRUCell / RNNCell): train-mode
                  memory(n_id) and update_state over several batches, train(False) (the flush), eval-mode
@@ -235,7 +235,7 @@ def capture_msg(seed):
 
 
 def capture_link_pred(seed):
-    """modules/decoder.py:108-123 LinkPredictor (sigmoid output): weights + inputs + outputs."""
+    """modules/decoder.py:12-27 LinkPredictor (sigmoid output): weights + inputs + outputs."""
     from modules.decoder import LinkPredictor
     torch.manual_seed(seed)
     lp = LinkPredictor(6)

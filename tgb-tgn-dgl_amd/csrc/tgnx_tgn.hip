@@ -2337,7 +2337,7 @@ __global__ void __launch_bounds__(256) tgn_attn_fwd(Ctx c) {
 }
 
 
-// ------------------------------------------------------------------ link prediction (decoder.py:108-123)
+// ------------------------------------------------------------------ link prediction (decoder.py:12-27)
 // Workgroup per event of this rank's slice: h = relu(lin_src(z_s) + lin_dst(z_d)), s = sigmoid(lin_final(h)),
 // loss = BCEWithLogits(s_pos, 1) + BCEWithLogits(s_neg, 0) (the reference feeds the sigmoid output to
 // BCEWithLogitsLoss), backward rows, dz rows accumulated into the centres' dZc.

@@ -1506,6 +1506,8 @@ __device__ void pred_reduce_vec_body(const Ctx& c, int y, int lane) {
 }
 
 // re-expand the collapsed gradients into the reference's parameters
+// a*x + b*y with one fixed rounding order, so the folded-Adam expansion (tgnn_expand_adam) is bit-identical to it
+__device__ __forceinline__ float dot2(float a, float x, float b, float y) { return __fmaf_rn(b, y, __fmul_rn(a, x)); }
 __device__ void grad_attn_body(const Ctx& c, int y, int lane);
 
 // blocks [0, nexp): elementwise dU -> dW / db re-expansion; trailing blocks: d attn (wave per output)
@@ -1530,10 +1532,10 @@ __global__ void __launch_bounds__(256) tgnn_grad_expand(Ctx c, int nexp) {
     } else if (x >= L.Wn && x < L.Wn + (int64_t)H * D * D) {
       const int64_t y = x - L.Wn;
       const int j = (int)(y / D), k = (int)(y % D), h = j / D;
-      g = P[L.attn_l + j] * r[PL.Ul + h * D + k] + P[L.attn_r + j] * r[PL.Ur + h * D + k];
+      g = dot2(P[L.attn_l + j], r[PL.Ul + h * D + k], P[L.attn_r + j], r[PL.Ur + h * D + k]);
     } else if (x >= L.bn && x < L.bn + H * D) {
       const int j = (int)(x - L.bn), h = j / D;
-      g = P[L.attn_l + j] * r[PL.cl + h] + P[L.attn_r + j] * r[PL.cr + h];
+      g = dot2(P[L.attn_l + j], r[PL.cl + h], P[L.attn_r + j], r[PL.cr + h]);
     } else if (x >= L.We && x < L.We + (int64_t)H * D * F) {
       const int64_t y = x - L.We;
       const int j = (int)(y / F), f = (int)(y % F), h = j / D;
@@ -1560,17 +1562,17 @@ __device__ void grad_attn_body(const Ctx& c, int y, int lane) {
   if (which < 2) {
     const float* dU = r + (which == 0 ? PL.Ul : PL.Ur) + h * D;
     const float* w = P + L.Wn + (int64_t)j * D;
-    for (int k = lane; k < D; k += 64) g += w[k] * dU[k];
+    for (int k = lane; k < D; k += 64) g = __fmaf_rn(w[k], dU[k], g);
   } else {
     const float* dU = r + PL.Ue + h * F;
     const float* w = P + L.We + (int64_t)j * F;
-    for (int f = lane; f < F; f += 64) g += w[f] * dU[f];
+    for (int f = lane; f < F; f += 64) g = __fmaf_rn(w[f], dU[f], g);
   }
   g = wave_sum(g);
   if (lane == 0) {
-    if (which == 0) c.grads[L.attn_l + j] = g + P[L.bn + j] * r[PL.cl + h];
-    else if (which == 1) c.grads[L.attn_r + j] = g + P[L.bn + j] * r[PL.cr + h];
-    else c.grads[L.attn_e + j] = g + P[L.be + j] * r[PL.ce + h];
+    if (which == 0) c.grads[L.attn_l + j] = __fmaf_rn(P[L.bn + j], r[PL.cl + h], g);
+    else if (which == 1) c.grads[L.attn_r + j] = __fmaf_rn(P[L.bn + j], r[PL.cr + h], g);
+    else c.grads[L.attn_e + j] = __fmaf_rn(P[L.be + j], r[PL.ce + h], g);
   }
 }
 
@@ -1578,10 +1580,14 @@ __device__ void grad_attn_body(const Ctx& c, int y, int lane) {
 // the device step count, computed once per workgroup; 4 parameters per thread.
 __device__ __forceinline__ void adam1(float g, float& m, float& v, float& p, float b1, float b2, float eps, float step,
                                       float bc2s) {
+  // every operation rounded on its own (no contraction: the build's -ffp-contract=fast would otherwise fuse
+  // differently per call site), in torch's order: lerp, mul + addcmul, sqrt / bc2 + eps, addcdiv — so the
+  // separate Adam launch and the one folded into the expansion compute the same bits
+#pragma clang fp contract(off)
   m = m + (1.0f - b1) * (g - m);
-  v = v * b2 + (1.0f - b2) * g * g;
-  const float den = sqrtf(v) / bc2s + eps;
-  p -= step * (m / den);
+  v = v * b2 + ((1.0f - b2) * g) * g;
+  const float den = __fsqrt_rn(v) / bc2s + eps;
+  p = p - step * (m / den);
 }
 __global__ void __launch_bounds__(256) tgnn_adam(Ctx c) {
   __shared__ float sc[2];
@@ -1615,6 +1621,102 @@ __global__ void __launch_bounds__(256) tgnn_adam(Ctx c) {
     M4[x] = m;
     V4[x] = v;
     P4[x] = p;
+  }
+}
+
+// World 1: the gradient expansion with Adam folded in (tgnn_grad_expand + tgnn_attn grads + tgnn_adam in one launch).
+// A wave owns W_n row j = (h, d) together with b_n[j], attn_l[j], attn_r[j] — the only elements whose old values its
+// gradients read (d W_n[j, k] = attn_l[j] dU_l[h, k] + attn_r[j] dU_r[h, k]; d attn_l[j] = W_n[j, :]·dU_l[h, :] + b_n[j]
+// dc_l[h]; d b_n[j] = attn_l[j] dc_l[h] + attn_r[j] dc_r[h]) — or W_e row j with b_e[j], attn_e[j]; so every old value
+// is loaded before the same wave updates it and no other wave reads it.  The rest (te_w, te_b from the reduced
+// partials; the predictor's gradients, final since tgnn_seg_bwd_pred) elementwise.  Same per-element gradient and
+// Adam arithmetic as the three kernels (the gradient buffer is written as well).
+__device__ __forceinline__ void adam_at(const Ctx& c, int64_t x, float g, float step, float bc2s) {
+  float m = c.am[x], v = c.av[x], p = c.params[x];
+  adam1(g, m, v, p, c.b1, c.b2, c.eps, step, bc2s);
+  c.grads[x] = g;
+  c.am[x] = m;
+  c.av[x] = v;
+  c.params[x] = p;
+}
+template <int NR>
+__device__ __forceinline__ void expand_row_adam(const Ctx& c, int j, int lane, bool edge, float step, float bc2s) {
+  const Lay L = c.L;
+  const PLay PL = c.PL;
+  const int D = c.D, F = c.F, h = j / D;
+  const int W = edge ? F : D;
+  float* P = c.params;
+  const float* r = c.red;
+  const int64_t row = (edge ? L.We : L.Wn) + (int64_t)j * W;
+  // every old value first: the row, its bias, its attention element(s), the row's reduced dU
+  float w[NR], ua[NR], ub[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int k = min(lane + 64 * i, W - 1);
+    w[i] = P[row + k];
+    ua[i] = edge ? r[PL.Ue + h * F + k] : r[PL.Ul + h * D + k];
+    ub[i] = edge ? 0.f : r[PL.Ur + h * D + k];
+  }
+  const float a0 = P[(edge ? L.attn_e : L.attn_l) + j], a1 = edge ? 0.f : P[L.attn_r + j];
+  const float bj = P[(edge ? L.be : L.bn) + j];
+  const float c0 = r[(edge ? PL.ce : PL.cl) + h], c1 = edge ? 0.f : r[PL.cr + h];
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NR; ++i)
+    if (lane + 64 * i < W) {
+      s0 = __fmaf_rn(w[i], ua[i], s0);
+      s1 = __fmaf_rn(w[i], ub[i], s1);
+    }
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int k = lane + 64 * i;
+    if (k < W) adam_at(c, row + k, edge ? a0 * ua[i] : dot2(a0, ua[i], a1, ub[i]), step, bc2s);
+  }
+  if (lane == 0) {
+    adam_at(c, (edge ? L.attn_e : L.attn_l) + j, __fmaf_rn(bj, c0, s0), step, bc2s);
+    if (!edge) adam_at(c, L.attn_r + j, __fmaf_rn(bj, c1, s1), step, bc2s);
+    adam_at(c, (edge ? L.be : L.bn) + j, edge ? a0 * c0 : dot2(a0, c0, a1, c1), step, bc2s);
+  }
+}
+__global__ void __launch_bounds__(256) tgnn_expand_adam(Ctx c, int nelem_blocks) {
+  __shared__ float sc[2];
+  const int64_t B = c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;   // (as tgnn_adam: no update for an empty batch)
+  if (threadIdx.x == 0) {
+    const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
+    const double bc1 = 1.0 - pow((double)c.b1, (double)t);
+    const double bc2 = 1.0 - pow((double)c.b2, (double)t);
+    sc[0] = (float)(c.lr / bc1);
+    sc[1] = (float)sqrt(bc2);
+    if (blockIdx.x == 0) {  // loss sum (the slot after the parameters)
+      double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
+      *loss += (double)c.grads[c.L.total] * (double)B;
+    }
+  }
+  __syncthreads();
+  const float step = sc[0], bc2s = sc[1];
+  const Lay L = c.L;
+  const PLay PL = c.PL;
+  const int D = c.D, lane = threadIdx.x & 63;
+  if ((int)blockIdx.x < nelem_blocks) {  // te_w, te_b, the predictor block [Ws, total)
+    const int64_t n = 2 * D + (L.total - L.Ws);
+    for (int64_t y = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; y < n; y += (int64_t)nelem_blocks * blockDim.x) {
+      if (y < D) adam_at(c, L.te_w + y, c.red[PL.w + y], step, bc2s);
+      else if (y < 2 * D) adam_at(c, L.te_b + y - D, c.red[PL.b + y - D], step, bc2s);
+      else {
+        const int64_t x = L.Ws + y - 2 * D;
+        adam_at(c, x, c.grads[x], step, bc2s);
+      }
+    }
+    return;
+  }
+  const int wv = ((int)blockIdx.x - nelem_blocks) * 4 + (threadIdx.x >> 6);
+  if (wv < H * D) {
+    expand_row_adam<(DMAX + 63) / 64>(c, wv, lane, false, step, bc2s);
+  } else if (wv < 2 * H * D) {
+    expand_row_adam<(FMAX + 63) / 64>(c, wv - H * D, lane, true, step, bc2s);
   }
 }
 
@@ -2001,7 +2103,7 @@ int tgnx_tgnn_advance(int64_t* ctl, int32_t mode, int64_t batch_start, int64_t B
 }
 
 static int train_fwd_bwd_impl(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t gen_neg,
-                              int32_t dropout, void* stream, const Ctx* adv);
+                              int32_t dropout, void* stream, const Ctx* adv, bool fuse_adam = false);
 
 int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t gen_neg,
                             int32_t dropout, void* stream) {
@@ -2027,8 +2129,26 @@ int tgnx_tgnn_train_fwd_bwd_resident(const tgnx_tgnn_config* cfg, const tgnx_tgn
   return train_fwd_bwd_impl(cfg, buf, 1, dropout, stream, &a);
 }
 
+int tgnx_tgnn_train_step_resident(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int64_t split_lo,
+                                  int64_t split_hi, int64_t batch, uint64_t base_seed, int32_t dropout, void* stream) {
+  TGNX_CHECK_ARG(batch > 0 && batch < 4096 && split_lo >= 0 && split_hi >= split_lo,
+                 "tgnx_tgnn_train_step_resident: bad cursor arguments");
+  TGNX_CHECK_ARG(buf && buf->adam_m && buf->adam_v, "tgnx_tgnn_train_step_resident: null optimizer buffer");
+  Ctx a;
+  memset(&a, 0, sizeof(a));
+  a.adv = 1;
+  a.adv_lo = split_lo;
+  a.adv_hi = split_hi;
+  a.adv_batch = batch;
+  a.adv_rank = 0;
+  a.adv_world = 1;
+  a.adv_seed = base_seed;
+  a.adv_train = 1;
+  return train_fwd_bwd_impl(cfg, buf, 1, dropout, stream, &a, true);
+}
+
 static int train_fwd_bwd_impl(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t gen_neg,
-                              int32_t dropout, void* stream, const Ctx* adv) {
+                              int32_t dropout, void* stream, const Ctx* adv, bool fuse_adam) {
   Ctx c;
   int rc = make_ctx(cfg, buf, 1, c);
   if (rc) return rc;
@@ -2058,7 +2178,13 @@ static int train_fwd_bwd_impl(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffe
   TGNX_LAUNCH_CHECK("tgnn_pred_train");
   rc = launch_backward(c, s);
   if (rc) return rc;
-  {
+  if (fuse_adam) {  // world 1: the expansion with Adam folded in (no tgnx_tgnn_train_update launch)
+    const int nel = grid_for(2 * c.D + (c.L.total - c.L.Ws), 256);
+    probe_begin(TGNX_K_ADAM, s);
+    tgnn_expand_adam<<<nel + grid_for(2 * H * c.D, 4), 256, 0, s>>>(c, nel);
+    probe_end(TGNX_K_ADAM, s);
+    TGNX_LAUNCH_CHECK("tgnn_expand_adam");
+  } else {
     const int nexp = grid_for(c.L.Ws, 256) < 1024 ? grid_for(c.L.Ws, 256) : 1024;
     tgnn_grad_expand<<<nexp + grid_for(3 * H * c.D, 4), 256, 0, s>>>(c, nexp);
     TGNX_LAUNCH_CHECK("tgnn_grad_expand");

@@ -11,6 +11,10 @@
 //   block_ids                                get_block / dependecyAwareBatch (dependencyGraph.py:8-49), CPU
 //   tcsr_build / tcsr_sample                 TGL's ext_full.npz + recent sampler (utils.py:73, README.md:2-5)
 //   gemm_f32                                 the modules' Linear contractions on the MFMA GEMM
+//   msg_agg_last / msg_agg_mean              LastAggregator / MeanAggregator (modules/msg_agg.py:15-26)
+//   gru_update                               TGNMemory.memory_updater GRUCell / RNNCell (memory_module.py:70-78)
+//   predictor                                LinkPredictor (decoder.py:12-27) / EdgePredictor (model_utils.py:165-195)
+//   edge_attn_fwd / edge_attn_bwd            TransformerConv's attention (emb_module.py:21-29, PyG semantics)
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -212,6 +216,164 @@ at::Tensor gemm_f32(const at::Tensor& A, const at::Tensor& B, const c10::optiona
   return C;
 }
 
+const float* opt_ptr(const c10::optional<at::Tensor>& x, const at::Tensor& ref, int64_t numel, const char* name) {
+  if (!x.has_value()) return nullptr;
+  dev_tensor(*x, at::kFloat, name);
+  TORCH_CHECK(x->numel() == numel, name, " must have ", numel, " entries");
+  same_device(ref, {&*x});
+  return x->data_ptr<float>();
+}
+
+// out-of-range index -> RuntimeError, as the reference's scatter (one device -> host read of the drop count)
+std::tuple<at::Tensor, at::Tensor> msg_agg(int32_t mode, const at::Tensor& msg, const at::Tensor& index,
+                                           const at::Tensor* t, int64_t dim_size) {
+  dev_tensor(msg, at::kFloat, "msg");
+  dev_tensor(index, at::kLong, "index");
+  TORCH_CHECK(msg.dim() == 2, "msg must be [n_msg, dim]");
+  TORCH_CHECK(index.dim() == 1 && index.numel() == msg.size(0), "index must be [n_msg]");
+  TORCH_CHECK(dim_size >= 0, "dim_size must be non-negative");
+  int32_t t_dtype = 0;
+  if (t) {
+    TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->numel() == msg.size(0), "t must be a contiguous [n_msg] device tensor");
+    TORCH_CHECK(t->scalar_type() == at::kLong || t->scalar_type() == at::kFloat, "t must be int64 or float32");
+    t_dtype = t->scalar_type() == at::kLong ? 0 : 1;
+    same_device(msg, {t});
+  }
+  same_device(msg, {&index});
+  const c10::OptionalDeviceGuard guard(msg.device());
+  const int64_t n = msg.size(0), dim = msg.size(1);
+  at::Tensor out = at::empty({dim_size, dim}, msg.options());
+  at::Tensor arg = at::empty({dim_size}, index.options());
+  at::Tensor bad = at::zeros({1}, index.options());
+  const size_t nb = tgnx_msg_agg_ws_bytes(n, dim_size);
+  at::Tensor ws = at::empty({(int64_t)std::max<size_t>(nb, 1)}, index.options().dtype(at::kByte));
+  check_rc(tgnx_msg_agg(mode, msg.data_ptr<float>(), n, dim, index.data_ptr<int64_t>(), t ? t->data_ptr() : nullptr,
+                        t_dtype, dim_size, out.data_ptr<float>(), arg.data_ptr<int64_t>(), bad.data_ptr<int64_t>(),
+                        ws.data_ptr(), nb, cur_stream()),
+           "tgnx_msg_agg");
+  const int64_t nbad = bad.cpu().data_ptr<int64_t>()[0];
+  TORCH_CHECK(nbad == 0, "msg_agg: ", nbad, " index entries outside [0, ", dim_size, ")");
+  return {out, arg};
+}
+
+std::tuple<at::Tensor, at::Tensor> msg_agg_last(const at::Tensor& msg, const at::Tensor& index, const at::Tensor& t,
+                                                int64_t dim_size) {
+  return msg_agg(0, msg, index, &t, dim_size);
+}
+
+at::Tensor msg_agg_mean(const at::Tensor& msg, const at::Tensor& index, int64_t dim_size) {
+  return std::get<0>(msg_agg(1, msg, index, nullptr, dim_size));
+}
+
+at::Tensor gru_update(const at::Tensor& x, const at::Tensor& h, const at::Tensor& w_ih, const at::Tensor& w_hh,
+                      const c10::optional<at::Tensor>& b_ih, const c10::optional<at::Tensor>& b_hh, int64_t cell) {
+  dev_tensor(x, at::kFloat, "x");
+  dev_tensor(h, at::kFloat, "h");
+  dev_tensor(w_ih, at::kFloat, "w_ih");
+  dev_tensor(w_hh, at::kFloat, "w_hh");
+  TORCH_CHECK(cell == 0 || cell == 1, "cell 0 (GRUCell) or 1 (RNNCell, tanh)");
+  TORCH_CHECK(x.dim() == 2 && h.dim() == 2 && x.size(0) == h.size(0), "x [M, d_in] and h [M, D]");
+  const int64_t M = x.size(0), d_in = x.size(1), D = h.size(1), G = (cell == 0 ? 3 : 1) * D;
+  TORCH_CHECK(w_ih.dim() == 2 && w_ih.size(0) == G && w_ih.size(1) == d_in, "w_ih must be [", G, ", ", d_in, "]");
+  TORCH_CHECK(w_hh.dim() == 2 && w_hh.size(0) == G && w_hh.size(1) == D, "w_hh must be [", G, ", ", D, "]");
+  same_device(x, {&h, &w_ih, &w_hh});
+  const float* bi = opt_ptr(b_ih, x, G, "b_ih");
+  const float* bh = opt_ptr(b_hh, x, G, "b_hh");
+  const c10::OptionalDeviceGuard guard(x.device());
+  at::Tensor out = at::empty_like(h);
+  const size_t nb = tgnx_memory_cell_ws_bytes(M, d_in, D);
+  at::Tensor ws = at::empty({(int64_t)nb}, x.options().dtype(at::kByte));
+  check_rc(tgnx_memory_cell((int32_t)cell, M, d_in, D, x.data_ptr<float>(), h.data_ptr<float>(), w_ih.data_ptr<float>(),
+                            w_hh.data_ptr<float>(), bi, bh, out.data_ptr<float>(), ws.data_ptr(), nb, cur_stream()),
+           "tgnx_memory_cell");
+  return out;
+}
+
+at::Tensor predictor(const at::Tensor& z_src, const at::Tensor& z_dst, const at::Tensor& w_src,
+                     const c10::optional<at::Tensor>& b_src, const at::Tensor& w_dst,
+                     const c10::optional<at::Tensor>& b_dst, const at::Tensor& w_out, const at::Tensor& b_out,
+                     bool sigmoid) {
+  dev_tensor(z_src, at::kFloat, "z_src");
+  dev_tensor(z_dst, at::kFloat, "z_dst");
+  dev_tensor(w_src, at::kFloat, "w_src");
+  dev_tensor(w_dst, at::kFloat, "w_dst");
+  dev_tensor(w_out, at::kFloat, "w_out");
+  dev_tensor(b_out, at::kFloat, "b_out");
+  TORCH_CHECK(z_src.dim() == 2 && z_dst.dim() == 2 && z_src.size(1) == z_dst.size(1), "z_src [B, d] and z_dst [M, d]");
+  const int64_t B = z_src.size(0), M = z_dst.size(0), d_in = z_src.size(1), D = w_src.size(0);
+  TORCH_CHECK(M == 0 || (B > 0 && M % B == 0), "z_dst rows must be a multiple of z_src rows (tile pairing)");
+  TORCH_CHECK(w_src.dim() == 2 && w_src.size(1) == d_in && w_dst.dim() == 2 && w_dst.size(0) == D &&
+                  w_dst.size(1) == d_in,
+              "w_src / w_dst must be [D, d]");
+  TORCH_CHECK(w_out.numel() == D && b_out.numel() == 1, "w_out must have D entries and b_out one");
+  same_device(z_src, {&z_dst, &w_src, &w_dst, &w_out, &b_out});
+  const float* bs = opt_ptr(b_src, z_src, D, "b_src");
+  const float* bd = opt_ptr(b_dst, z_src, D, "b_dst");
+  const c10::OptionalDeviceGuard guard(z_src.device());
+  at::Tensor out = at::empty({M, 1}, z_src.options());
+  const size_t nb = tgnx_link_predictor_ws_bytes(B, M, d_in, D);
+  at::Tensor ws = at::empty({(int64_t)nb}, z_src.options().dtype(at::kByte));
+  check_rc(tgnx_link_predictor(B, M, d_in, D, z_src.data_ptr<float>(), z_dst.data_ptr<float>(), w_src.data_ptr<float>(),
+                               bs, w_dst.data_ptr<float>(), bd, w_out.data_ptr<float>(), b_out.data_ptr<float>(),
+                               sigmoid ? 1 : 0, out.data_ptr<float>(), ws.data_ptr(), nb, cur_stream()),
+           "tgnx_link_predictor");
+  return out;
+}
+
+void attn_args(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const c10::optional<at::Tensor>& e,
+               const at::Tensor& indptr, int64_t heads) {
+  dev_tensor(q, at::kFloat, "q");
+  dev_tensor(k, at::kFloat, "k");
+  dev_tensor(v, at::kFloat, "v");
+  dev_tensor(indptr, at::kLong, "indptr");
+  TORCH_CHECK(q.dim() == 2 && k.dim() == 2 && v.sizes() == k.sizes() && k.size(1) == q.size(1),
+              "q [n_dst, H*C], k / v [E, H*C]");
+  TORCH_CHECK(heads >= 1 && q.size(1) % heads == 0, "H*C must be a multiple of heads");
+  TORCH_CHECK(indptr.numel() == q.size(0) + 1, "indptr must have n_dst + 1 entries");
+  same_device(q, {&k, &v, &indptr});
+  if (e.has_value()) {
+    dev_tensor(*e, at::kFloat, "e");
+    TORCH_CHECK(e->sizes() == k.sizes(), "e must be [E, H*C]");
+    same_device(q, {&*e});
+  }
+}
+
+std::tuple<at::Tensor, at::Tensor> edge_attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                                                 const c10::optional<at::Tensor>& e, const at::Tensor& indptr,
+                                                 int64_t heads) {
+  attn_args(q, k, v, e, indptr, heads);
+  const c10::OptionalDeviceGuard guard(q.device());
+  const int64_t n = q.size(0), E = k.size(0), C = q.size(1) / heads;
+  at::Tensor out = at::empty_like(q), alpha = at::empty({E, heads}, q.options());
+  check_rc(tgnx_edge_attn_fwd(n, E, (int32_t)heads, (int32_t)C, q.data_ptr<float>(), k.data_ptr<float>(),
+                              v.data_ptr<float>(), e.has_value() ? e->data_ptr<float>() : nullptr,
+                              indptr.data_ptr<int64_t>(), out.data_ptr<float>(), alpha.data_ptr<float>(), cur_stream()),
+           "tgnx_edge_attn_fwd");
+  return {out, alpha};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> edge_attn_bwd(
+    const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+    const c10::optional<at::Tensor>& e, const at::Tensor& indptr, const at::Tensor& alpha, int64_t heads) {
+  attn_args(q, k, v, e, indptr, heads);
+  dev_tensor(dout, at::kFloat, "dout");
+  dev_tensor(alpha, at::kFloat, "alpha");
+  TORCH_CHECK(dout.sizes() == q.sizes(), "dout must be [n_dst, H*C]");
+  TORCH_CHECK(alpha.dim() == 2 && alpha.size(0) == k.size(0) && alpha.size(1) == heads, "alpha must be [E, heads]");
+  same_device(q, {&dout, &alpha});
+  const c10::OptionalDeviceGuard guard(q.device());
+  const int64_t n = q.size(0), E = k.size(0), C = q.size(1) / heads;
+  at::Tensor dq = at::empty_like(q), dk = at::empty_like(k), dv = at::empty_like(v);
+  at::Tensor de = e.has_value() ? at::empty_like(k) : at::empty({0}, k.options());
+  check_rc(tgnx_edge_attn_bwd(n, E, (int32_t)heads, (int32_t)C, dout.data_ptr<float>(), q.data_ptr<float>(),
+                              k.data_ptr<float>(), v.data_ptr<float>(), e.has_value() ? e->data_ptr<float>() : nullptr,
+                              indptr.data_ptr<int64_t>(), alpha.data_ptr<float>(), dq.data_ptr<float>(),
+                              dk.data_ptr<float>(), dv.data_ptr<float>(), e.has_value() ? de.data_ptr<float>() : nullptr,
+                              cur_stream()),
+           "tgnx_edge_attn_bwd");
+  return {dq, dk, dv, de};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tgnx, m) {
@@ -230,4 +392,17 @@ TORCH_LIBRARY(tgnx, m) {
         "-> (Tensor, Tensor, Tensor, Tensor)",
         &tcsr_sample);
   m.def("gemm_f32(Tensor A, Tensor B, Tensor? bias=None, bool trans_a=False, bool trans_b=False) -> Tensor", &gemm_f32);
+  m.def("msg_agg_last(Tensor msg, Tensor index, Tensor t, int dim_size) -> (Tensor, Tensor)", &msg_agg_last);
+  m.def("msg_agg_mean(Tensor msg, Tensor index, int dim_size) -> Tensor", &msg_agg_mean);
+  m.def("gru_update(Tensor x, Tensor h, Tensor w_ih, Tensor w_hh, Tensor? b_ih=None, Tensor? b_hh=None, int cell=0) "
+        "-> Tensor",
+        &gru_update);
+  m.def("predictor(Tensor z_src, Tensor z_dst, Tensor w_src, Tensor? b_src, Tensor w_dst, Tensor? b_dst, Tensor w_out, "
+        "Tensor b_out, bool sigmoid=True) -> Tensor",
+        &predictor);
+  m.def("edge_attn_fwd(Tensor q, Tensor k, Tensor v, Tensor? e, Tensor indptr, int heads) -> (Tensor, Tensor)",
+        &edge_attn_fwd);
+  m.def("edge_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor? e, Tensor indptr, Tensor alpha, int heads) "
+        "-> (Tensor, Tensor, Tensor, Tensor)",
+        &edge_attn_bwd);
 }

@@ -66,10 +66,21 @@ SIGNATURES = {
     "tgnx_gemm_f32_ws_bytes": (c_sz, [c_i64, c_i64, c_i64]),
     "tgnx_gemm_f32": (ctypes.c_int, [c_i64, c_i64, c_i64, P, c_i64, c_i32, P, c_i64, c_i32, P, c_i64, P, c_i32, P, c_sz,
                                      c_vp]),
+    # per-operator entry points (tgnx_ops.hip)
+    "tgnx_msg_agg_ws_bytes": (c_sz, [c_i64, c_i64]),
+    "tgnx_msg_agg": (ctypes.c_int, [c_i32, P, c_i64, c_i64, P, P, c_i32, c_i64, P, P, P, P, c_sz, c_vp]),
+    "tgnx_memory_cell_ws_bytes": (c_sz, [c_i64, c_i64, c_i64]),
+    "tgnx_memory_cell": (ctypes.c_int, [c_i32, c_i64, c_i64, c_i64, P, P, P, P, P, P, P, P, c_sz, c_vp]),
+    "tgnx_link_predictor_ws_bytes": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
+    "tgnx_link_predictor": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64, P, P, P, P, P, P, P, P, c_i32, P, P, c_sz,
+                                           c_vp]),
+    "tgnx_edge_attn_fwd": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32, P, P, P, P, P, P, P, c_vp]),
+    "tgnx_edge_attn_bwd": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32, P, P, P, P, P, P, P, P, P, P, P, c_vp]),
     "tgnx_tgnn_advance": (ctypes.c_int, [P, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64,
                                          c_i32, c_vp]),
     "tgnx_tgnn_train_fwd_bwd": (ctypes.c_int, [P, P, c_i32, c_i32, c_vp]),
     "tgnx_tgnn_train_fwd_bwd_resident": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64, c_i32, c_vp]),
+    "tgnx_tgnn_train_step_resident": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_u64, c_i32, c_vp]),
     "tgnx_tgnn_train_update": (ctypes.c_int, [P, P, c_vp]),
     "tgnx_tgnn_eval_step": (ctypes.c_int, [P, P, c_i32, c_i32, c_vp]),
 }

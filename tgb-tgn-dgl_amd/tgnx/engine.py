@@ -71,6 +71,7 @@ class TgnnEngine:
         self._neg_scratch = None
         self.out_ev = None    # optional per-event train-logit log (tgnx_tgnn_buffers.out_ev)
         self.fold_cursor = True
+        self.fuse_adam = True
 
     # ------------------------------------------------------------------ plumbing
     def _buffers(self, src, dst, t, blk, msg, neg) -> TgnnBuffers:
@@ -167,6 +168,9 @@ class TgnnEngine:
         # the batch cursor folded into the step's first launch (tgnx_tgnn_train_fwd_bwd_resident: one launch fewer);
         # fold_cursor = False keeps tgnx_tgnn_advance + tgnx_tgnn_train_fwd_bwd (same results)
         self._fold = self.fold_cursor and hasattr(L, "tgnx_tgnn_train_fwd_bwd_resident")
+        # world 1: Adam and the loss sum folded into the step's gradient expansion (tgnx_tgnn_train_step_resident: no
+        # tgnx_tgnn_train_update launch); fuse_adam = False keeps the separate update
+        self._fused = self._fold and self.fuse_adam and self.world == 1 and hasattr(L, "tgnx_tgnn_train_step_resident")
         self._cfg_ref = ctypes.byref(self.cfg)
         self._buf_ref = ctypes.byref(self._res_buf)
         self._ctl_p = ctypes.c_void_p(self.ctl.data_ptr())
@@ -179,6 +183,9 @@ class TgnnEngine:
     def _resident_fwd_bwd(self, st):
         adv, fb, _ = self._f
         lo, hi, batch = self._res
+        if self._fused:
+            return _lib.lib().tgnx_tgnn_train_step_resident(self._cfg_ref, self._buf_ref, lo, hi, batch, self.seed,
+                                                           self._res_drop, st)
         if self._fold:
             return _lib.lib().tgnx_tgnn_train_fwd_bwd_resident(self._cfg_ref, self._buf_ref, lo, hi, batch, self.rank,
                                                               self.world, self.seed, self._res_drop, st)
@@ -191,6 +198,8 @@ class TgnnEngine:
         rc = self._resident_fwd_bwd(st)
         if rc:
             raise RuntimeError(f"tgnx resident step failed: {_lib.lib().tgnx_last_error().decode()}")
+        if self._fused:
+            return
         self._allreduce_grads()
         if up(self._cfg_ref, self._buf_ref, st):
             raise RuntimeError(f"tgnx resident update failed: {_lib.lib().tgnx_last_error().decode()}")
@@ -209,6 +218,8 @@ class TgnnEngine:
                 raise RuntimeError(_lib.lib().tgnx_last_error().decode())
 
         def post():
+            if self._fused:
+                return
             if up(cfg, buf, self._stream()):
                 raise RuntimeError(_lib.lib().tgnx_last_error().decode())
 
