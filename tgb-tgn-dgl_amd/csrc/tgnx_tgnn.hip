@@ -524,7 +524,9 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   }
   __syncthreads();
   TGNN_PHASE_STAMP(c, 1);
-  sort_u64(key, tmp, NT, n);
+  // the touch keys are pairwise distinct ((kind, event) is unique): up to 1,024 touches sort in 64-key register
+  // chunks + binary-search ranks (sort_u64_chunks) instead of the 55-stage bitonic network (8.7 -> ~3 us at B = 200)
+  sort_u64(key, tmp, NT, n, /*distinct=*/true);
   TGNN_PHASE_STAMP(c, 2);
   const int pc = (NT + T - 1) / T;
   const int p0 = tid * pc, p1 = min(NT, p0 + pc);
