@@ -404,10 +404,10 @@ __global__ void tgnn_seg_count(Ctx c) {
 // tgnn_finish applies with a wave per node.
 // Workgroup 2 computes the per-block max t and the stable block order.
 // LDS of workgroup 0: sorted keys [next_pow2(NT)] u64 | run starts [NT] | run id per touch [NT] |
-// register-sort ping-pong buffer [1024] u64.
+// register-sort ping-pong buffer [1024] u64 | ring fill per unsorted touch [NT].
 __host__ __device__ inline size_t assemble_smem_bytes(int Bmax) {
   const int NT = 3 * Bmax;
-  return (size_t)next_pow2(NT) * 8 + (size_t)NT * 8 + 1024 * 8;
+  return (size_t)next_pow2(NT) * 8 + (size_t)NT * 8 + 1024 * 8 + (size_t)NT * 4;
 }
 template <bool TRAIN>
 __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
@@ -497,28 +497,39 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   int* run_start = reinterpret_cast<int*>(smem + (size_t)next_pow2(NTc) * 8);
   int* run_of = run_start + NTc;
   uint64_t* tmp = reinterpret_cast<uint64_t*>(run_of + NTc);
+  int* fill = reinterpret_cast<int*>(tmp + 1024);  // ring fill of touch p's node (one touch per thread)
   TGNN_PHASE_STAMP(c, 0);
-  if (TRAIN && c.gen_neg) {  // NegLinkSamplerDest.sample (neg_sampler.py:8-23), counter-based stream
-    const uint64_t seed = c.adv ? (uint64_t)sd.seed : (uint64_t)c.ctl[TGNX_CTL_SEED];
-    const uint64_t off = c.adv ? (uint64_t)sd.start : (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
-    for (int i = tid; i < B; i += T) {
-      const int64_t pd = dst[i];
-      int64_t v = c.dst_nodes[0];
-      for (uint64_t attempt = 0; attempt < 64; ++attempt) {
-        const uint64_t h = hash4(seed, 0x6E656773ull, off + (uint64_t)i, attempt);
-        v = c.dst_nodes[(uint64_t)(((__uint128_t)(h >> 11) * (uint64_t)c.n_dst) >> 53)];
-        if (v != pd) break;
-      }
-      c.neg[start + i] = v;
-    }
-    __syncthreads();
-  }
+  const bool draw = TRAIN && c.gen_neg;
+  const uint64_t nseed = !draw ? 0 : c.adv ? (uint64_t)sd.seed : (uint64_t)c.ctl[TGNX_CTL_SEED];
+  const uint64_t noff = !draw ? 0 : c.adv ? (uint64_t)sd.start : (uint64_t)c.ctl[TGNX_CTL_CUR_EID];
+  // one touch per thread (B <= 341): its node's ring fill is loaded here, beside the key, and parked in LDS after
+  // the sort (the segment counts read it there instead of ten dependent-on-the-sort global loads)
+  const bool one = TRAIN && NT <= T && c.K <= 16;
+  int64_t ring_eid[16];  // consumed after the sort: the loads overlap it
+#pragma unroll
+  for (int j = 0; j < 16; ++j) ring_eid[j] = -1;
   for (int p = tid; p < n; p += T) {
     uint64_t k = ~0ull;
     if (p < NT) {
       int e = p % B, which = p / B;  // 0 = s, 1 = p, 2 = n
-      int64_t node = which == 0 ? src[e] : which == 1 ? dst[e] : neg[e];
+      int64_t node;
+      if (which == 2 && draw) {  // NegLinkSamplerDest.sample (neg_sampler.py:8-23), counter-based stream
+        const int64_t pd = dst[e];
+        node = c.dst_nodes[0];
+        for (uint64_t attempt = 0; attempt < 64; ++attempt) {
+          const uint64_t h = hash4(nseed, 0x6E656773ull, noff + (uint64_t)e, attempt);
+          node = c.dst_nodes[(uint64_t)(((__uint128_t)(h >> 11) * (uint64_t)c.n_dst) >> 53)];
+          if (node != pd) break;
+        }
+        c.neg[start + e] = node;
+      } else {
+        node = which == 0 ? src[e] : which == 1 ? dst[e] : neg[e];
+      }
       k = mkkey(node, (int)blk[e], 2 - which, e);
+      if (one)
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (j < c.K) ring_eid[j] = c.eid[node * c.K + j];
     }
     key[p] = k;
   }
@@ -527,6 +538,12 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   // the touch keys are pairwise distinct ((kind, event) is unique): up to 1,024 touches sort in 64-key register
   // chunks + binary-search ranks (sort_u64_chunks) instead of the 55-stage bitonic network (8.7 -> ~3 us at B = 200)
   sort_u64(key, tmp, NT, n, /*distinct=*/true);
+  if (one && tid < NT) {  // (read after the barriers of the scans below)
+    int f = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) f += ring_eid[j] >= 0;
+    fill[tid] = f;
+  }
   TGNN_PHASE_STAMP(c, 2);
   const int pc = (NT + T - 1) / T;
   const int p0 = tid * pc, p1 = min(NT, p0 + pc);
@@ -578,7 +595,9 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
       while (g > 0 && (key[g - 1] >> 14) == (k >> 14)) --g;
       const int64_t v = knode(k);
       int nring = 0;
-      for (int j = 0; j < c.K; ++j) nring += c.eid[v * c.K + j] >= 0;
+      if (one) nring = fill[(2 - kind) * B + ev];
+      else
+        for (int j = 0; j < c.K; ++j) nring += c.eid[v * c.K + j] >= 0;
       const int nintra = c.sp_pref[g] - c.sp_pref[run_start[run_of[p]]];
       c.seg_cnt[w] = nring | (nintra << 8);
     }

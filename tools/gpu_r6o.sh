@@ -9,5 +9,5 @@ TGNX_LIB=/root/repo/var/timing/libtgnx.so timeout -k 10 200 python -u tools/phas
 cat gpurun_out/${T}_phase.txt
 timeout -k 10 600 python -u -m pytest tests/test_gpu_dropin.py tests/test_gpu_tgnn.py tests/test_gpu_tgnn_b2000.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/${T}_tests.log 2>&1 || { tail -60 gpurun_out/${T}_tests.log; exit 1; }
 tail -2 gpurun_out/${T}_tests.log
-MODEL=tgnn bash tools/ab_bench.sh ${T}_b200 default /root/repo/var/r6fused/libtgnx.so || exit 1
+MODEL=tgnn bash tools/ab_bench.sh ${T}_b200 default /root/repo/var/r6sort/libtgnx.so || exit 1
 cat gpurun_out/${T}_b200_ab.txt
