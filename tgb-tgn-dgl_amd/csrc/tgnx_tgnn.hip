@@ -14,6 +14,7 @@
 //    x_eh = U_e[h]·efeat_e + U_l[h]·nfeat_src + c, U = attn·W (a 372-wide dot per edge
 //    per head instead of an 800-wide GEMM row); backward re-expands dU into dW / dattn.
 //  * One wave (64 lanes) per segment, lanes over feature dims; online softmax per head.
+#include <rocprim/block/block_radix_sort.hpp>
 #include "tgnx_math.h"
 #include "tgnx_ring_dev.h"
 
@@ -404,11 +405,41 @@ __global__ void tgnn_seg_count(Ctx c) {
 // tgnn_finish applies with a wave per node.
 // Workgroup 2 computes the per-block max t and the stable block order.
 // LDS of workgroup 0: sorted keys [next_pow2(NT)] u64 | run starts [NT] | run id per touch [NT] |
-// register-sort ping-pong buffer [1024] u64 | ring fill per unsorted touch [NT].
+// register-sort ping-pong buffer [1024] u64 | ring fill per unsorted touch [NT]; a touch sort above 1,024 keys
+// uses everything past the keys as its ping-pong buffer (next_pow2(NT) keys).
 __host__ __device__ inline size_t assemble_smem_bytes(int Bmax) {
   const int NT = 3 * Bmax;
-  return (size_t)next_pow2(NT) * 8 + (size_t)NT * 8 + 1024 * 8 + (size_t)NT * 4;
+  const size_t tail = (size_t)NT * 8 + 1024 * 8 + (size_t)NT * 4;
+  const size_t big = (size_t)next_pow2(NT) * 8;
+  return (size_t)next_pow2(NT) * 8 + (tail > big ? tail : big);
 }
+// Touch sort above 1,024 keys (B > 341; TGN.yml's B = 2,000: 6,000 keys): an LSD radix sort of the block in
+// registers (rocprim::block_radix_sort, 8 keys per thread, 8-bit digits over the key's used bits: 26 + log2 N),
+// stable, ~5 passes.  The 8-key bitonic network measured ~100 us for 8,192 keys on the one CU (VALU-bound: 63
+// lane stages x 8 keys), the LDS bitonic network 104 us.  The rocprim storage aliases the LDS from `smem`.
+using TouchRadix = rocprim::block_radix_sort<uint64_t, 1024, 8>;
+__device__ __forceinline__ bool touch_radix_fits(int Bmax) {
+  return sizeof(TouchRadix::storage_type) <= assemble_smem_bytes(Bmax);
+}
+__device__ __forceinline__ void sort_touches_radix(uint64_t* key, int n_keys, int64_t N, unsigned char* smem) {
+  const int t = threadIdx.x;
+  uint64_t v[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int p = t * 8 + m;
+    v[m] = p < n_keys ? key[p] : ~0ull;
+  }
+  int nb = 1;
+  while (nb < 38 && (int64_t(1) << nb) < N) ++nb;
+  __syncthreads();  // (the storage overwrites the keys)
+  TouchRadix().sort(v, *reinterpret_cast<TouchRadix::storage_type*>(smem), 0, 26 + nb);
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+    if (t * 8 + m < n_keys) key[t * 8 + m] = v[m];  // (past n_keys: padding, sorted last)
+  __syncthreads();
+}
+
 template <bool TRAIN>
 __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -430,7 +461,8 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
     TGNN_PHASE_STAMP(c, 8);
     uint64_t* key;
     int* runs;
-    const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs);
+    // (the LDS holds a full ping-pong buffer past the run starts: register sorts up to 2B = 4,096)
+    const int U = ring_plan_block(c.ev_src + start, c.ev_dst + start, B, smem, sh, &key, &runs, NoCheckpoint{}, true);
     TGNN_PHASE_STAMP(c, 9);
     for (int p = tid; p < 2 * B; p += T) c.rkeys[p] = key[p];
     for (int r = tid; r < U; r += T) c.rruns[r] = runs[r];
@@ -537,7 +569,9 @@ __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   TGNN_PHASE_STAMP(c, 1);
   // the touch keys are pairwise distinct ((kind, event) is unique): up to 1,024 touches sort in 64-key register
   // chunks + binary-search ranks (sort_u64_chunks) instead of the 55-stage bitonic network (8.7 -> ~3 us at B = 200)
-  sort_u64(key, tmp, NT, n, /*distinct=*/true);
+  if (NT <= 1024) sort_u64(key, tmp, NT, n, /*distinct=*/true);
+  else if (NT <= 8192 && blockDim.x == 1024 && touch_radix_fits(c.Bmax)) sort_touches_radix(key, n, c.N, smem);
+  else sort_u64(key, reinterpret_cast<uint64_t*>(run_start), NT, n, true, /*tmp_full=*/true);
   if (one && tid < NT) {  // (read after the barriers of the scans below)
     int f = 0;
 #pragma unroll

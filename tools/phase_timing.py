@@ -59,4 +59,4 @@ def main(steps=200, B=200):
 
 
 if __name__ == "__main__":
-    main()
+    main(B=int(sys.argv[1]) if len(sys.argv) > 1 else 200)
