@@ -493,61 +493,7 @@ __device__ __forceinline__ void sort_u64_reg4(uint64_t* key, uint64_t* tmp, int 
     if (m < nm) key[t + m * T] = v[m];
   __syncthreads();
 }
-// The same network with eight keys per thread (4 T < n <= 8 T; n = 8192 at T = 1024: the touch sort of a B = 2,000
-// TGNN batch, 6,000 keys): distances >= T pair registers m and m ^ (j / T) inside the thread, 64 <= j < T one LDS
-// round each (22 barriers instead of bitonic_sort_u64's 91).  tmp: n keys.
-__device__ __forceinline__ void sort_u64_reg8(uint64_t* key, uint64_t* tmp, int n) {
-  const int T = blockDim.x, t = threadIdx.x;
-  constexpr int NM = 8;
-  uint64_t v[NM];
-#pragma unroll
-  for (int m = 0; m < NM; ++m) v[m] = key[t + m * T];
-  int flip = 0;
-  for (int k = 2; k <= n; k <<= 1) {
-    for (int j = k >> 1; j >= WAVE; j >>= 1) {
-      if (j >= T) {
-        const int jj = j / T;  // 1, 2 or 4
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-          if (m & jj) continue;
-#pragma unroll
-          for (int q = 1; q < NM; q <<= 1)
-            if (q == jj) cmpx_u64(v[m], v[m | q], ((t + m * T) & k) == 0);
-        }
-        continue;
-      }
-      uint64_t* buf = flip ? tmp : key;
-      flip ^= 1;
-#pragma unroll
-      for (int m = 0; m < NM; ++m) buf[t + m * T] = v[m];
-      __syncthreads();
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        const int p = t + m * T;
-        const uint64_t o = buf[p ^ j];
-        const bool take_min = ((p & j) == 0) == ((p & k) == 0);
-        v[m] = take_min ? (o < v[m] ? o : v[m]) : (o > v[m] ? o : v[m]);
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < NM; ++m) {
-      const int p = t + m * T;
-      switch (k >= 64 ? 32 : k >> 1) {
-        case 32: v[m] = bitonic_lane_stage<32>(v[m], p, k); [[fallthrough]];
-        case 16: v[m] = bitonic_lane_stage<16>(v[m], p, k); [[fallthrough]];
-        case 8: v[m] = bitonic_lane_stage<8>(v[m], p, k); [[fallthrough]];
-        case 4: v[m] = bitonic_lane_stage<4>(v[m], p, k); [[fallthrough]];
-        case 2: v[m] = bitonic_lane_stage<2>(v[m], p, k); [[fallthrough]];
-        default: v[m] = bitonic_lane_stage<1>(v[m], p, k);
-      }
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int m = 0; m < NM; ++m) key[t + m * T] = v[m];
-  __syncthreads();
-}
-// tmp_full: tmp holds n_pow2 keys (enables the four- / eight-keys-per-thread sorts for T < n_pow2 <= 8 T)
+// tmp_full: tmp holds n_pow2 keys (enables the four-keys-per-thread sort for T < n_pow2 <= 4 T)
 __device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, int n_pow2, bool distinct = false,
                                          bool tmp_full = false) {
   if (distinct && (n <= (int)blockDim.x || n <= 1024)) {
@@ -561,7 +507,6 @@ __device__ __forceinline__ void sort_u64(uint64_t* key, uint64_t* tmp, int n, in
   __syncthreads();
   if (n_pow2 <= (int)blockDim.x) sort_u64_reg(key, tmp, n_pow2);
   else if (tmp_full && n_pow2 <= 4 * (int)blockDim.x) sort_u64_reg4(key, tmp, n_pow2);
-  else if (tmp_full && n_pow2 == 8 * (int)blockDim.x) sort_u64_reg8(key, tmp, n_pow2);
   else bitonic_sort_u64(key, n_pow2);
 }
 
