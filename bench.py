@@ -606,7 +606,7 @@ def run_tgn(args, world, rank, dev):
                        "§8(d) B_ev(train) x events per GPU (bench.tgn_step_bytes)",
         "timing": "avg_launch_us: the kernel's own begin / end timestamps (hipExtLaunchKernelGGL start / stop "
                   "events bound to the dispatch, on its launch stream: what rocprofv3 --kernel-trace reports), "
-                  "eager launches of the same step; rocprofv3 summary of the same command: profiles/r5/ (r5_kernel_stats.csv)",
+                  "eager launches of the same step; rocprofv3 summary of the same command: profiles/r6/ (r6_kernel_stats.csv; the timed window: r6_window_kernel_stats.csv)",
         "units_window": "each probe replays the timed batches (epoch rewound and replayed to the window's start); "
                         "units are the probe's own device counters over those batches",
     }
