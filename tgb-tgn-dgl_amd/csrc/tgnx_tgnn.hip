@@ -881,7 +881,10 @@ template <bool TRAIN>
 __device__ void finish_body(const Ctx& c, const int bid, const int nblk);
 
 #ifndef TGNX_GFWD
-#define TGNX_GFWD 512
+// edge workgroups: 150 VGPRs leave room for 3 waves per SIMD, i.e. 768 four-wave workgroups on 256 CUs (512: 2 per
+// SIMD; TGN.yml's B = 2,000 step 1.174 -> 1.128 ms, B = 200 +-0, profiles/r6/r6v_*).  1,024 workgroups with the
+// registers capped for 4 waves per SIMD measured 1.22 ms (r6w_*)
+#define TGNX_GFWD 768
 #endif
 constexpr int GFWD = TGNX_GFWD;
 template <int CF, int CT, bool DROP>
