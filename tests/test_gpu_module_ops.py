@@ -149,3 +149,27 @@ def test_edge_attention_fwd_bwd_matches_torch(H, C, with_e):
     assert float(out.detach()[5].abs().max()) == 0.0                  # no edges: PyG's empty aggregation
     for got_leaf, want_leaf in zip(dl, leaves):
         _close(got_leaf.grad, want_leaf.grad, 1e-4)
+
+
+def test_survey_named_sampler_ops_are_the_ring_ops():
+    """SURVEY §8b's names (sample_recent / insert_recent / reset) run the LastNeighborLoader ring ops."""
+    ns = _ops()
+    N, K = 500, 10
+    state = []
+    for _ in range(2):
+        nbr = torch.full((N, K), -1, dtype=torch.long, device=DEV)
+        eid = torch.empty((N, K), dtype=torch.long, device=DEV)
+        t = torch.empty((N, K), device=DEV)
+        state.append((nbr, eid, t, torch.zeros(N, dtype=torch.long, device=DEV)))
+    ns.ring_reset(state[0][1], state[0][2])
+    ns.reset(state[1][1], state[1][2])
+    g = torch.Generator().manual_seed(3)
+    src, dst = torch.randint(0, N, (300,), generator=g).to(DEV), torch.randint(0, N, (300,), generator=g).to(DEV)
+    tt = torch.sort(torch.rand(300, generator=g) * 1000).values.to(DEV)
+    ns.ring_insert(*state[0][:3], src, dst, tt, 0, state[0][3])
+    ns.insert_recent(*state[1][:3], src, dst, tt, 0, state[1][3])
+    for a, b in zip(state[0], state[1]):
+        assert torch.equal(a, b)
+    q = torch.unique(torch.cat([src, dst]))
+    for a, b in zip(ns.ring_sample(*state[0][:3], state[0][3], q), ns.sample_recent(*state[1][:3], state[1][3], q)):
+        assert torch.equal(a, b)

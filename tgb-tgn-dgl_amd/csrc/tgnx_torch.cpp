@@ -6,7 +6,8 @@
 // torch caller composes directly:
 //
 //   ring_reset / ring_sample / ring_insert   LastNeighborLoader reset_state / __call__ / insert
-//                                            (neighbor_loader.py:106-109, :26-50, :52-104)
+//                                            (neighbor_loader.py:106-109, :26-50, :52-104); also registered under
+//                                            SURVEY §8b's names reset / sample_recent / insert_recent
 //   neg_sample                               NegLinkSamplerDest.sample (neg_sampler.py:8-23)
 //   block_ids                                get_block / dependecyAwareBatch (dependencyGraph.py:8-49), CPU
 //   tcsr_build / tcsr_sample                 TGL's ext_full.npz + recent sampler (utils.py:73, README.md:2-5)
@@ -392,6 +393,14 @@ TORCH_LIBRARY(tgnx, m) {
         "-> (Tensor, Tensor, Tensor, Tensor)",
         &tcsr_sample);
   m.def("gemm_f32(Tensor A, Tensor B, Tensor? bias=None, bool trans_a=False, bool trans_b=False) -> Tensor", &gemm_f32);
+  // SURVEY §8b's names for the sampler ops (the same functions as ring_sample / ring_insert / ring_reset)
+  m.def("sample_recent(Tensor nbr, Tensor e_id, Tensor t, Tensor(a!) assoc, Tensor n_id) -> "
+        "(Tensor, Tensor, Tensor, Tensor)",
+        &ring_sample);
+  m.def("insert_recent(Tensor(a!) nbr, Tensor(b!) e_id, Tensor(c!) t, Tensor src, Tensor dst, Tensor ev_t, "
+        "int cur_e_id, Tensor(d!) assoc) -> ()",
+        &ring_insert);
+  m.def("reset(Tensor(a!) e_id, Tensor(b!) t) -> ()", &ring_reset);
   m.def("msg_agg_last(Tensor msg, Tensor index, Tensor t, int dim_size) -> (Tensor, Tensor)", &msg_agg_last);
   m.def("msg_agg_mean(Tensor msg, Tensor index, int dim_size) -> Tensor", &msg_agg_mean);
   m.def("gru_update(Tensor x, Tensor h, Tensor w_ih, Tensor w_hh, Tensor? b_ih=None, Tensor? b_hh=None, int cell=0) "

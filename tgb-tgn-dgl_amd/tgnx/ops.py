@@ -20,7 +20,8 @@ import torch
 
 OPS_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtgnx_torch.so")
 OPS = ("ring_reset", "ring_sample", "ring_insert", "neg_sample", "block_ids", "tcsr_build", "tcsr_sample", "gemm_f32",
-       "msg_agg_last", "msg_agg_mean", "gru_update", "predictor", "edge_attn_fwd", "edge_attn_bwd")
+       "msg_agg_last", "msg_agg_mean", "gru_update", "predictor", "edge_attn_fwd", "edge_attn_bwd",
+       "sample_recent", "insert_recent", "reset")
 _loaded = False
 
 
