@@ -1689,16 +1689,28 @@ __global__ void __launch_bounds__(256) tgnn_adam(Ctx c) {
 // is loaded before the same wave updates it and no other wave reads it.  The rest (te_w, te_b from the reduced
 // partials; the predictor's gradients, final since tgnn_seg_bwd_pred) elementwise.  Same per-element gradient and
 // Adam arithmetic as the three kernels (the gradient buffer is written as well).
-__device__ __forceinline__ void adam_at(const Ctx& c, int64_t x, float g, float step, float bc2s) {
-  float m = c.am[x], v = c.av[x], p = c.params[x];
+__device__ __forceinline__ void adam_store(const Ctx& c, int64_t x, float g, float m, float v, float p, float step,
+                                           float bc2s) {
   adam1(g, m, v, p, c.b1, c.b2, c.eps, step, bc2s);
   c.grads[x] = g;
   c.am[x] = m;
   c.av[x] = v;
   c.params[x] = p;
 }
+__device__ __forceinline__ void adam_at(const Ctx& c, int64_t x, float g, float step, float bc2s) {
+  adam_store(c, x, g, c.am[x], c.av[x], c.params[x], step, bc2s);
+}
+// Adam's step scalars from the device step count (every wave computes them itself: no barrier, and the double-
+// precision pow runs while the wave's loads are in flight)
+__device__ __forceinline__ void adam_scalars(const Ctx& c, float& step, float& bc2s) {
+  const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
+  const double bc1 = 1.0 - pow((double)c.b1, (double)t);
+  const double bc2 = 1.0 - pow((double)c.b2, (double)t);
+  step = (float)(c.lr / bc1);
+  bc2s = (float)sqrt(bc2);
+}
 template <int NR>
-__device__ __forceinline__ void expand_row_adam(const Ctx& c, int j, int lane, bool edge, float step, float bc2s) {
+__device__ __forceinline__ void expand_row_adam(const Ctx& c, int j, int lane, bool edge) {
   const Lay L = c.L;
   const PLay PL = c.PL;
   const int D = c.D, F = c.F, h = j / D;
@@ -1706,18 +1718,26 @@ __device__ __forceinline__ void expand_row_adam(const Ctx& c, int j, int lane, b
   float* P = c.params;
   const float* r = c.red;
   const int64_t row = (edge ? L.We : L.Wn) + (int64_t)j * W;
-  // every old value first: the row, its bias, its attention element(s), the row's reduced dU
-  float w[NR], ua[NR], ub[NR];
+  // every old value first — the row, its bias, its attention element(s), the row's reduced dU, and the Adam moments
+  // of all of them — in one load round
+  float w[NR], ua[NR], ub[NR], mm[NR], vv[NR];
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
     const int k = min(lane + 64 * i, W - 1);
     w[i] = P[row + k];
+    mm[i] = c.am[row + k];
+    vv[i] = c.av[row + k];
     ua[i] = edge ? r[PL.Ue + h * F + k] : r[PL.Ul + h * D + k];
     ub[i] = edge ? 0.f : r[PL.Ur + h * D + k];
   }
-  const float a0 = P[(edge ? L.attn_e : L.attn_l) + j], a1 = edge ? 0.f : P[L.attn_r + j];
-  const float bj = P[(edge ? L.be : L.bn) + j];
+  const int64_t xa = (edge ? L.attn_e : L.attn_l) + j, xr = L.attn_r + j, xb = (edge ? L.be : L.bn) + j;
+  const float a0 = P[xa], a1 = edge ? 0.f : P[xr];
+  const float bj = P[xb];
   const float c0 = r[(edge ? PL.ce : PL.cl) + h], c1 = edge ? 0.f : r[PL.cr + h];
+  const float ma = c.am[xa], va = c.av[xa], mb = c.am[xb], vb = c.av[xb];
+  const float mr = edge ? 0.f : c.am[xr], vr = edge ? 0.f : c.av[xr];
+  float step, bc2s;
+  adam_scalars(c, step, bc2s);
   float s0 = 0.f, s1 = 0.f;
 #pragma unroll
   for (int i = 0; i < NR; ++i)
@@ -1730,35 +1750,28 @@ __device__ __forceinline__ void expand_row_adam(const Ctx& c, int j, int lane, b
 #pragma unroll
   for (int i = 0; i < NR; ++i) {
     const int k = lane + 64 * i;
-    if (k < W) adam_at(c, row + k, edge ? a0 * ua[i] : dot2(a0, ua[i], a1, ub[i]), step, bc2s);
+    if (k < W)
+      adam_store(c, row + k, edge ? a0 * ua[i] : dot2(a0, ua[i], a1, ub[i]), mm[i], vv[i], w[i], step, bc2s);
   }
   if (lane == 0) {
-    adam_at(c, (edge ? L.attn_e : L.attn_l) + j, __fmaf_rn(bj, c0, s0), step, bc2s);
-    if (!edge) adam_at(c, L.attn_r + j, __fmaf_rn(bj, c1, s1), step, bc2s);
-    adam_at(c, (edge ? L.be : L.bn) + j, edge ? a0 * c0 : dot2(a0, c0, a1, c1), step, bc2s);
+    adam_store(c, xa, __fmaf_rn(bj, c0, s0), ma, va, a0, step, bc2s);
+    if (!edge) adam_store(c, xr, __fmaf_rn(bj, c1, s1), mr, vr, a1, step, bc2s);
+    adam_store(c, xb, edge ? a0 * c0 : dot2(a0, c0, a1, c1), mb, vb, bj, step, bc2s);
   }
 }
 __global__ void __launch_bounds__(256) tgnn_expand_adam(Ctx c, int nelem_blocks) {
-  __shared__ float sc[2];
   const int64_t B = c.ctl[TGNX_CTL_B];
   if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;   // (as tgnn_adam: no update for an empty batch)
-  if (threadIdx.x == 0) {
-    const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
-    const double bc1 = 1.0 - pow((double)c.b1, (double)t);
-    const double bc2 = 1.0 - pow((double)c.b2, (double)t);
-    sc[0] = (float)(c.lr / bc1);
-    sc[1] = (float)sqrt(bc2);
-    if (blockIdx.x == 0) {  // loss sum (the slot after the parameters)
-      double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
-      *loss += (double)c.grads[c.L.total] * (double)B;
-    }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // loss sum (the slot after the parameters)
+    double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
+    *loss += (double)c.grads[c.L.total] * (double)B;
   }
-  __syncthreads();
-  const float step = sc[0], bc2s = sc[1];
   const Lay L = c.L;
   const PLay PL = c.PL;
   const int D = c.D, lane = threadIdx.x & 63;
   if ((int)blockIdx.x < nelem_blocks) {  // te_w, te_b, the predictor block [Ws, total)
+    float step, bc2s;
+    adam_scalars(c, step, bc2s);
     const int64_t n = 2 * D + (L.total - L.Ws);
     for (int64_t y = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; y < n; y += (int64_t)nelem_blocks * blockDim.x) {
       if (y < D) adam_at(c, L.te_w + y, c.red[PL.w + y], step, bc2s);
@@ -1772,9 +1785,9 @@ __global__ void __launch_bounds__(256) tgnn_expand_adam(Ctx c, int nelem_blocks)
   }
   const int wv = ((int)blockIdx.x - nelem_blocks) * 4 + (threadIdx.x >> 6);
   if (wv < H * D) {
-    expand_row_adam<(DMAX + 63) / 64>(c, wv, lane, false, step, bc2s);
+    expand_row_adam<(DMAX + 63) / 64>(c, wv, lane, false);
   } else if (wv < 2 * H * D) {
-    expand_row_adam<(FMAX + 63) / 64>(c, wv - H * D, lane, true, step, bc2s);
+    expand_row_adam<(FMAX + 63) / 64>(c, wv - H * D, lane, true);
   }
 }
 
