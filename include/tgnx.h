@@ -152,6 +152,8 @@ int64_t tgnx_stamps_count(void);
 #define TGNX_CTL_STEP_B 16      /* B of the last trained step (tgnx_tgnn_advance / the resident step's last
                                    launch): what tgnx_tgn_train_update checks, since a pipelined step's
                                    descriptor already holds the NEXT batch when its update runs */
+#define TGNX_CTL_APPLY 17       /* TGNN resident world-1 step: Adam step count of the update still to apply
+                                   (tgnx_tgnn_train_step_resident defers it to the next step's first launch), 0: none */
 #define TGNX_CTL_WORDS 24
 
 #define TGNX_TGNN_NPARAM 15     /* te_w te_b attn_l attn_r attn_e Wn bn We be Ws bs Wd bd Wo bo */
@@ -230,11 +232,16 @@ int tgnx_tgnn_train_fwd_bwd(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers
 int tgnx_tgnn_train_fwd_bwd_resident(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int64_t split_lo,
                                      int64_t split_hi, int64_t batch, int32_t rank, int32_t world,
                                      uint64_t base_seed, int32_t dropout, void* stream);
-/* World 1: the resident step whole — tgnx_tgnn_train_fwd_bwd_resident (rank 0 of 1) with Adam and the loss sum
- * folded into its gradient expansion (one launch fewer again: no tgnx_tgnn_train_update).  The gradient buffer is
- * still written. */
+/* World 1: the resident step whole — tgnx_tgnn_train_fwd_bwd_resident (rank 0 of 1) with the update deferred: the
+ * step sums its loss and records its update as pending (ctl[TGNX_CTL_APPLY]); the gradient expansion + Adam run in
+ * the NEXT call's first launch, beside its batch assembly (8 launches per step, no tgnx_tgnn_train_update).  The
+ * parameters therefore lag one step until tgnx_tgnn_apply_pending (call it before reading them; tgnx_tgnn_eval_step
+ * applies a pending update itself).  Same results as the separate update, bit for bit. */
 int tgnx_tgnn_train_step_resident(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int64_t split_lo,
                                   int64_t split_hi, int64_t batch, uint64_t base_seed, int32_t dropout, void* stream);
+/* Apply the update tgnx_tgnn_train_step_resident left pending, if any (two launches; a no-op on the device when
+ * nothing is pending). */
+int tgnx_tgnn_apply_pending(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, void* stream);
 /* Train step, part 2 (optimizer.step): Adam on the (possibly all-reduced) grads, loss sum. */
 int tgnx_tgnn_train_update(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, void* stream);
 /* Eval step (epoch_utils.py:28-157): Kn negatives per event, logits in block order,

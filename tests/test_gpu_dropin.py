@@ -103,7 +103,7 @@ def test_entry_script_runs_one_epoch():
 
 def test_folded_cursor_equals_advance_plus_step():
     """tgnx_tgnn_train_step_resident (the batch cursor folded into tgnn_assemble, the counter advanced in the next
-    launch; Adam and the loss sum folded into the gradient expansion) and tgnx_tgnn_train_fwd_bwd_resident + the
+    launch; the gradient expansion + Adam deferred into the next step's first launch, applied here by finish()) and tgnx_tgnn_train_fwd_bwd_resident + the
     separate update, against tgnx_tgnn_advance + tgnx_tgnn_train_fwd_bwd + tgnx_tgnn_train_update: the same
     parameters, Adam moments, gradients, ring, time_assoc, outputs and every ctl word after each replayed step of a
     split whose last batch is partial, then a step past the split, with device-drawn negatives and dropout."""
@@ -128,6 +128,7 @@ def test_folded_cursor_equals_advance_plus_step():
     for st in range(7):      # 5 full batches, a partial one (100 events), one past the split
         for m, e, _ in engs:
             e.replay_resident()
+            e.finish()           # (the deferred-update engine: apply the step's update before comparing)
         torch.cuda.synchronize()
         ma, ea, na = engs[-1]
         ea.check()
@@ -140,3 +141,41 @@ def test_folded_cursor_equals_advance_plus_step():
                 assert torch.equal(ma.grad_flat[:-1], mb.grad_flat[:-1]), st
             assert torch.equal(ea.loader.e_id, eb.loader.e_id) and torch.equal(na, nb), st
             assert torch.equal(ea.out_pos, eb.out_pos) and torch.equal(ea.out_neg, eb.out_neg), st
+
+
+def test_deferred_update_is_applied_before_eval():
+    """The world-1 resident step leaves its update pending (applied by the next step's first launch); an eval step
+    run right after — no finish() — applies it first: the same logits and parameters as the separate update."""
+    from tgnx.data import block_ids
+    s = _stream(E=1300)
+    B = 200
+    blk = torch.from_numpy(block_ids(s.src, s.dst, B)).cuda()
+    dev = torch.device("cuda")
+    ev = [torch.from_numpy(x).to(dev) for x in (s.src, s.dst, s.t.astype(np.float32))]
+    msg = torch.from_numpy(s.msg).to(dev)
+    engs = []
+    for fuse in (True, False):
+        m, e = _make(s)
+        e.fuse_adam = fuse
+        neg_buf = torch.zeros(s.num_events, dtype=torch.long, device=dev)
+        e.bind_resident(ev[0], ev[1], ev[2], blk, msg, neg_buf, 0, 1000, B, dropout=False)
+        assert e._defer == fuse
+        e.begin_epoch()
+        e.capture_resident(1)
+        for _ in range(3):
+            e.replay_resident()
+        engs.append((m, e))
+    (ma, ea), (mb, eb) = engs
+    torch.cuda.synchronize()
+    assert int(ea.ctl[17]) == 3 and not torch.equal(ma.flat, mb.flat)   # step 3's update pending in the first
+    sl = slice(1000, 1000 + B)
+    neg2d = np.random.default_rng(5).choice(s.dst_nodes, size=(B, 1))   # (the engines' max_neg)
+    outs = []
+    for m, e in engs:
+        e.loader.cur_e_id = 1000
+        pos, neg, _ = e.eval_batch(s.src[sl], s.dst[sl], s.t[sl].astype(np.float32), s.msg[sl], block_ids(s.src[sl], s.dst[sl], B), neg2d)
+        outs.append((pos.clone(), neg.clone()))
+    torch.cuda.synchronize()
+    assert int(ea.ctl[17]) == 0
+    assert torch.equal(ma.flat, mb.flat) and torch.equal(ea.adam_m, eb.adam_m) and torch.equal(ea.adam_v, eb.adam_v)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

@@ -135,6 +135,10 @@ struct Ctx {
   // tgnn_assemble derives the step descriptor from the step counter (what tgnn_advance mode 1 computes) and writes
   // it; the counter itself advances in the next launch (tgnn_meta_collapse), after all three workgroups read it
   int adv, adv_rank, adv_world, adv_train;
+  // world-1 resident step with a deferred update: tgnn_grad_reduce records the step's update as pending
+  // (ctl[TGNX_CTL_APPLY] = its Adam step count) and the next step's tgnn_assemble launch applies it in its extra
+  // workgroups (apply_nel of them elementwise), beside the batch assembly
+  int defer, apply_nel;
   int64_t adv_lo, adv_hi, adv_batch;
   uint64_t adv_seed;
   float pf, pa, inv_kf, inv_ka;
@@ -440,11 +444,17 @@ __device__ __forceinline__ void sort_touches_radix(uint64_t* key, int n_keys, in
   __syncthreads();
 }
 
+__device__ void expand_adam_body(const Ctx& c, int64_t t, int bid, int nblk, int nel);
 template <bool TRAIN>
 __global__ void __launch_bounds__(1024) tgnn_assemble(Ctx c) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int sh[20];
   const int tid = threadIdx.x, T = blockDim.x;
+  if (TRAIN && c.defer && blockIdx.x >= 3) {  // the previous step's pending update, beside this step's assembly
+    const int64_t t = c.ctl[TGNX_CTL_APPLY];
+    if (t > 0) expand_adam_body(c, t, blockIdx.x - 3, gridDim.x - 3, c.apply_nel);
+    return;
+  }
   int B;
   int64_t start;
   StepDesc sd{};
@@ -1323,6 +1333,17 @@ __global__ void __launch_bounds__(64 * RED_WAVES) tgnn_grad_reduce(Ctx c, int Ge
       for (int g = wv; g < Gs; g += RED_WAVES) s += c.slabs_s[(int64_t)g * ns + q];
   }
   acc[wv][lane] = s;
+  if (c.defer && blockIdx.x == 0 && threadIdx.x == 64 * RED_WAVES - 1) {
+    // deferred update: the loss sum, and the step's update recorded as pending for the next tgnn_assemble launch
+    // (or tgnx_tgnn_apply_pending); an empty or failed step records none
+    const int64_t B = c.ctl[TGNX_CTL_B];
+    const bool ok = B > 0 && c.ctl[TGNX_CTL_ERR] == 0;
+    if (ok) {
+      double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
+      *loss += (double)c.grads[c.L.total] * (double)B;
+    }
+    c.ctl[TGNX_CTL_APPLY] = ok ? c.ctl[TGNX_CTL_ADAM_T] : 0;
+  }
   __syncthreads();
   if (wv == 0 && p < P) {
     float t = 0.f;
@@ -1702,15 +1723,14 @@ __device__ __forceinline__ void adam_at(const Ctx& c, int64_t x, float g, float 
 }
 // Adam's step scalars from the device step count (every wave computes them itself: no barrier, and the double-
 // precision pow runs while the wave's loads are in flight)
-__device__ __forceinline__ void adam_scalars(const Ctx& c, float& step, float& bc2s) {
-  const int64_t t = c.ctl[TGNX_CTL_ADAM_T];
+__device__ __forceinline__ void adam_scalars(const Ctx& c, int64_t t, float& step, float& bc2s) {
   const double bc1 = 1.0 - pow((double)c.b1, (double)t);
   const double bc2 = 1.0 - pow((double)c.b2, (double)t);
   step = (float)(c.lr / bc1);
   bc2s = (float)sqrt(bc2);
 }
 template <int NR>
-__device__ __forceinline__ void expand_row_adam(const Ctx& c, int j, int lane, bool edge) {
+__device__ __forceinline__ void expand_row_adam(const Ctx& c, int j, int lane, bool edge, int64_t t) {
   const Lay L = c.L;
   const PLay PL = c.PL;
   const int D = c.D, F = c.F, h = j / D;
@@ -1737,7 +1757,7 @@ __device__ __forceinline__ void expand_row_adam(const Ctx& c, int j, int lane, b
   const float ma = c.am[xa], va = c.av[xa], mb = c.am[xb], vb = c.av[xb];
   const float mr = edge ? 0.f : c.am[xr], vr = edge ? 0.f : c.av[xr];
   float step, bc2s;
-  adam_scalars(c, step, bc2s);
+  adam_scalars(c, t, step, bc2s);
   float s0 = 0.f, s1 = 0.f;
 #pragma unroll
   for (int i = 0; i < NR; ++i)
@@ -1759,21 +1779,17 @@ __device__ __forceinline__ void expand_row_adam(const Ctx& c, int j, int lane, b
     adam_store(c, xb, edge ? a0 * c0 : dot2(a0, c0, a1, c1), mb, vb, bj, step, bc2s);
   }
 }
-__global__ void __launch_bounds__(256) tgnn_expand_adam(Ctx c, int nelem_blocks) {
-  const int64_t B = c.ctl[TGNX_CTL_B];
-  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;   // (as tgnn_adam: no update for an empty batch)
-  if (blockIdx.x == 0 && threadIdx.x == 0) {  // loss sum (the slot after the parameters)
-    double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
-    *loss += (double)c.grads[c.L.total] * (double)B;
-  }
+// The expansion + Adam of update step t over `nblk` workgroups of any size: the first `nel` elementwise (te_w, te_b,
+// the predictor block [Ws, total)), the rest a wave per W_n / W_e row.
+__device__ void expand_adam_body(const Ctx& c, int64_t t, int bid, int nblk, int nel) {
   const Lay L = c.L;
   const PLay PL = c.PL;
-  const int D = c.D, lane = threadIdx.x & 63;
-  if ((int)blockIdx.x < nelem_blocks) {  // te_w, te_b, the predictor block [Ws, total)
+  const int D = c.D, lane = threadIdx.x & 63, T = blockDim.x;
+  if (bid < nel) {
     float step, bc2s;
-    adam_scalars(c, step, bc2s);
+    adam_scalars(c, t, step, bc2s);
     const int64_t n = 2 * D + (L.total - L.Ws);
-    for (int64_t y = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; y < n; y += (int64_t)nelem_blocks * blockDim.x) {
+    for (int64_t y = bid * (int64_t)T + threadIdx.x; y < n; y += (int64_t)nel * T) {
       if (y < D) adam_at(c, L.te_w + y, c.red[PL.w + y], step, bc2s);
       else if (y < 2 * D) adam_at(c, L.te_b + y - D, c.red[PL.b + y - D], step, bc2s);
       else {
@@ -1783,12 +1799,31 @@ __global__ void __launch_bounds__(256) tgnn_expand_adam(Ctx c, int nelem_blocks)
     }
     return;
   }
-  const int wv = ((int)blockIdx.x - nelem_blocks) * 4 + (threadIdx.x >> 6);
-  if (wv < H * D) {
-    expand_row_adam<(DMAX + 63) / 64>(c, wv, lane, false);
-  } else if (wv < 2 * H * D) {
-    expand_row_adam<(FMAX + 63) / 64>(c, wv - H * D, lane, true);
+  const int wpb = T >> 6, nw = (nblk - nel) * wpb;
+  for (int wv = (bid - nel) * wpb + (threadIdx.x >> 6); wv < 2 * H * D; wv += nw) {  // (wave-uniform)
+    if (wv < H * D) expand_row_adam<(DMAX + 63) / 64>(c, wv, lane, false, t);
+    else expand_row_adam<(FMAX + 63) / 64>(c, wv - H * D, lane, true, t);
   }
+}
+__host__ __device__ inline int expand_rows_blocks(int D, int threads) { return (2 * H * D + threads / 64 - 1) / (threads / 64); }
+
+__global__ void __launch_bounds__(256) tgnn_expand_adam(Ctx c, int nelem_blocks) {
+  const int64_t B = c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;   // (as tgnn_adam: no update for an empty batch)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // loss sum (the slot after the parameters)
+    double* loss = reinterpret_cast<double*>(c.ctl + TGNX_CTL_LOSS);
+    *loss += (double)c.grads[c.L.total] * (double)B;
+  }
+  expand_adam_body(c, c.ctl[TGNX_CTL_ADAM_T], blockIdx.x, gridDim.x, nelem_blocks);
+}
+// the pending (deferred) update, if any: tgnx_tgnn_apply_pending and tgnx_tgnn_eval_step's first launch
+__global__ void __launch_bounds__(256) tgnn_apply_pending(Ctx c, int nelem_blocks) {
+  const int64_t t = c.ctl[TGNX_CTL_APPLY];
+  if (t <= 0) return;
+  expand_adam_body(c, t, blockIdx.x, gridDim.x, nelem_blocks);
+}
+__global__ void tgnn_clear_pending(int64_t* ctl) {
+  if (threadIdx.x == 0) ctl[TGNX_CTL_APPLY] = 0;
 }
 
 // Ring/time state update of a batch (many workgroups): time_assoc of the touched nodes
@@ -2092,7 +2127,8 @@ static int edge_grid(int64_t Ecap) {
 template <bool TRAIN>
 static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
   probe_begin(TGNX_K_ASSEMBLE, s);
-  tgnn_assemble<TRAIN><<<3, 1024, assemble_smem_bytes(c.Bmax), s>>>(c);
+  const int napply = TRAIN && c.defer ? c.apply_nel + expand_rows_blocks(c.D, 1024) : 0;
+  tgnn_assemble<TRAIN><<<3 + napply, 1024, assemble_smem_bytes(c.Bmax), s>>>(c);
   probe_end(TGNX_K_ASSEMBLE, s);
   TGNX_LAUNCH_CHECK("tgnn_assemble");
   if (!TRAIN) {
@@ -2215,7 +2251,22 @@ int tgnx_tgnn_train_step_resident(const tgnx_tgnn_config* cfg, const tgnx_tgnn_b
   a.adv_world = 1;
   a.adv_seed = base_seed;
   a.adv_train = 1;
+  a.defer = 1;
   return train_fwd_bwd_impl(cfg, buf, 1, dropout, stream, &a, true);
+}
+
+int tgnx_tgnn_apply_pending(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, void* stream) {
+  Ctx c;
+  int rc = make_ctx(cfg, buf, 1, c);
+  if (rc) return rc;
+  TGNX_CHECK_ARG(buf->grads && buf->adam_m && buf->adam_v, "tgnx_tgnn_apply_pending: null optimizer buffer");
+  hipStream_t s = as_stream(stream);
+  const int nel = grid_for(2 * c.D + (c.L.total - c.L.Ws), 256);
+  tgnn_apply_pending<<<nel + expand_rows_blocks(c.D, 256), 256, 0, s>>>(c, nel);
+  TGNX_LAUNCH_CHECK("tgnn_apply_pending");
+  tgnn_clear_pending<<<1, 64, 0, s>>>(c.ctl);
+  TGNX_LAUNCH_CHECK("tgnn_clear_pending");
+  return TGNX_OK;
 }
 
 static int train_fwd_bwd_impl(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* buf, int32_t gen_neg,
@@ -2232,6 +2283,8 @@ static int train_fwd_bwd_impl(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffe
     c.adv_world = adv->adv_world;
     c.adv_seed = adv->adv_seed;
     c.adv_train = adv->adv_train;
+    c.defer = adv->defer;
+    c.apply_nel = grid_for(2 * c.D + (c.L.total - c.L.Ws), 1024);
   }
   TGNX_CHECK_ARG(buf->neg && buf->grads && buf->out_pos && buf->out_neg && buf->feat && buf->ev_msg && buf->memory &&
                      buf->time_assoc && buf->nbr && buf->eid && buf->rt,
@@ -2249,7 +2302,9 @@ static int train_fwd_bwd_impl(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffe
   TGNX_LAUNCH_CHECK("tgnn_pred_train");
   rc = launch_backward(c, s);
   if (rc) return rc;
-  if (fuse_adam) {  // world 1: the expansion with Adam folded in (no tgnx_tgnn_train_update launch)
+  if (fuse_adam && c.defer) {
+    // (the expansion + Adam runs in the next step's first launch, or tgnx_tgnn_apply_pending)
+  } else if (fuse_adam) {  // world 1: the expansion with Adam folded in (no tgnx_tgnn_train_update launch)
     const int nel = grid_for(2 * c.D + (c.L.total - c.L.Ws), 256);
     probe_begin(TGNX_K_ADAM, s);
     tgnn_expand_adam<<<nel + grid_for(2 * H * c.D, 4), 256, 0, s>>>(c, nel);
@@ -2288,6 +2343,10 @@ int tgnx_tgnn_eval_step(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* bu
   c.drop = 0;
   hipStream_t s = as_stream(stream);
   const int Bmax = cfg->max_batch;
+  if (buf->grads && buf->adam_m && buf->adam_v) {  // a deferred train update still pending is applied first
+    rc = tgnx_tgnn_apply_pending(cfg, buf, stream);
+    if (rc) return rc;
+  }
   rc = launch_forward<false>(c, (int64_t)Bmax * (2 + Kn), s);
   if (rc) return rc;
   tgnn_pred_eval_src<<<grid_for(Bmax, 4), 256, 0, s>>>(c);

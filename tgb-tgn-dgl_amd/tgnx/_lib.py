@@ -81,6 +81,7 @@ SIGNATURES = {
     "tgnx_tgnn_train_fwd_bwd": (ctypes.c_int, [P, P, c_i32, c_i32, c_vp]),
     "tgnx_tgnn_train_fwd_bwd_resident": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_i32, c_i32, c_u64, c_i32, c_vp]),
     "tgnx_tgnn_train_step_resident": (ctypes.c_int, [P, P, c_i64, c_i64, c_i64, c_u64, c_i32, c_vp]),
+    "tgnx_tgnn_apply_pending": (ctypes.c_int, [P, P, c_vp]),
     "tgnx_tgnn_train_update": (ctypes.c_int, [P, P, c_vp]),
     "tgnx_tgnn_eval_step": (ctypes.c_int, [P, P, c_i32, c_i32, c_vp]),
 }

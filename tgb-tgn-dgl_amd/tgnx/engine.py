@@ -171,6 +171,8 @@ class TgnnEngine:
         # world 1: Adam and the loss sum folded into the step's gradient expansion (tgnx_tgnn_train_step_resident: no
         # tgnx_tgnn_train_update launch); fuse_adam = False keeps the separate update
         self._fused = self._fold and self.fuse_adam and self.world == 1 and hasattr(L, "tgnx_tgnn_train_step_resident")
+        # ... and deferred: each step's update runs in the next step's first launch (finish() applies the last one)
+        self._defer = self._fused and hasattr(L, "tgnx_tgnn_apply_pending")
         self._cfg_ref = ctypes.byref(self.cfg)
         self._buf_ref = ctypes.byref(self._res_buf)
         self._ctl_p = ctypes.c_void_p(self.ctl.data_ptr())
@@ -203,6 +205,14 @@ class TgnnEngine:
         self._allreduce_grads()
         if up(self._cfg_ref, self._buf_ref, st):
             raise RuntimeError(f"tgnx resident update failed: {_lib.lib().tgnx_last_error().decode()}")
+
+    def finish(self):
+        """Apply the update the last resident step left pending (world 1: tgnx_tgnn_train_step_resident defers each
+        step's gradient expansion + Adam into the next step's first launch).  Call before reading the parameters
+        or the Adam moments; the drop-in train() does, and an eval step applies a pending update itself."""
+        if getattr(self, "_defer", False):
+            if _lib.lib().tgnx_tgnn_apply_pending(self._cfg_ref, self._buf_ref, self._stream()):
+                raise RuntimeError(f"tgnx apply_pending failed: {_lib.lib().tgnx_last_error().decode()}")
 
     def capture_resident(self, steps_per_graph: int = 1):
         """Capture `steps_per_graph` resident train steps into HIP graphs (torch.cuda.CUDAGraph).

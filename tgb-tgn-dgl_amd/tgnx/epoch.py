@@ -92,6 +92,7 @@ def train(model, feats, train_loader, neighbor_loader, neg_dest_sampler, assoc, 
         eng.ctl[10] = 0
         for _ in range(len(train_loader)):
             eng.replay_resident()
+        eng.finish()                                     # the last step's update (deferred by the resident step)
         neighbor_loader.cur_e_id = train_loader.hi       # e_ids are global event rows (val continues)
         torch.cuda.synchronize(eng.dev)
         eng.check()
