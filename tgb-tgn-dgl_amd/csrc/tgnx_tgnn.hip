@@ -31,13 +31,21 @@ constexpr int TOUCH_MAX = 8192;
 #define TGNX_GBWD 256
 #endif
 #ifndef TGNX_BWD_WAVES
-#define TGNX_BWD_WAVES 8
+#define TGNX_BWD_WAVES 8  // waves per edge-backward workgroup below TGNX_BWD_BIG_BATCH events (12 at and above)
 #endif
 #ifndef TGNX_BWD_NE
 #define TGNX_BWD_NE 2
 #endif
 constexpr int GBWD = TGNX_GBWD;            // workgroups of the edge backward kernel (= partial slabs)
-constexpr int BWD_WAVES = TGNX_BWD_WAVES;  // waves per edge backward workgroup
+constexpr int BWD_WAVES = TGNX_BWD_WAVES;  // waves per edge backward workgroup (small batches)
+#ifndef TGNX_BWD_BIG_BATCH
+#define TGNX_BWD_BIG_BATCH 1000
+#endif
+// LDS partial rows of the edge backward (16 KB each at the wiki shape): waves past the 8th add theirs into row
+// wv - 8 after the first 8 stored (fixed order), so 12 waves (3 per SIMD at 144 VGPRs) fit one CU's LDS.  12 waves:
+// TGN.yml's B = 2,000 step 1.117 -> 1.061 ms, B = 200 0.0918 -> 0.0927 (profiles/r6/r6ab_*): 12 from
+// TGNX_BWD_BIG_BATCH events of capacity up
+__host__ __device__ constexpr int bwd_bufs(int nw) { return nw < 8 ? nw : 8; }
 constexpr int GSEG = 160;     // workgroups of the segment backward kernel
 constexpr int MRR_SLOTS = 65536;  // per-batch MRR ring in buffers.mrr
 constexpr int BATCH_MAX = 2048;   // max events per batch (touch sort capacity 3 * BATCH_MAX in LDS)
@@ -1152,10 +1160,12 @@ __device__ void seg_bwd_body(const Ctx& c, const int bid, const int nblk) {
 // out), the self-loop row points at a row of ones: the loop body has no divergent control flow.
 // Two register sets ping-pong so one edge's gathers are in flight during the other's math.  Each
 // wave leaves its partial in LDS and the workgroup sums them in a fixed order into its slab.
-template <int CF, int CT, bool DROP>
-__global__ void __launch_bounds__(64 * BWD_WAVES) tgnn_edge_bwd(Ctx c) {
+template <int CF, int CT, bool DROP, int NW>
+__global__ void __launch_bounds__(64 * NW) tgnn_edge_bwd(Ctx c) {
+  constexpr int BWD_BUFS = bwd_bufs(NW);
+  static_assert(NW <= 2 * BWD_BUFS, "edge backward: at most two waves per LDS partial row");
   constexpr int NJ = CF + 2 * CT;
-  extern __shared__ __attribute__((aligned(16))) float part[];   // [BWD_WAVES][PL.total]
+  extern __shared__ __attribute__((aligned(16))) float part[];   // [BWD_BUFS][PL.total]
   __shared__ __attribute__((aligned(16))) float Uenc[DMAX * H];   // U_e[h][d + i] as [i][h], zero for i >= D
   const PLay PL = c.PL;
   const int F = c.F, D = c.D, d = c.d;
@@ -1230,8 +1240,8 @@ __global__ void __launch_bounds__(64 * BWD_WAVES) tgnn_edge_bwd(Ctx c) {
     for (int h = 0; h < H; ++h) ac[h] += S.dx[h];
   };
 
-  const int stride = gridDim.x * BWD_WAVES;
-  int e = blockIdx.x * BWD_WAVES + wv;
+  const int stride = gridDim.x * NW;
+  int e = blockIdx.x * NW + wv;
   Slot A, Bs;
   if (e < E) load(e, A);
   while (e < E) {
@@ -1244,34 +1254,41 @@ __global__ void __launch_bounds__(64 * BWD_WAVES) tgnn_edge_bwd(Ctx c) {
     math(Bs);
     e = e2;
   }
-  // this wave's partial -> LDS row wv (entries owned by nobody are zeroed in the sum below)
-  float* pw = part + wv * PL.total;
+  // this wave's partial -> LDS row wv (entries owned by nobody are zeroed in the sum below); waves past BWD_BUFS
+  // add theirs into row wv - BWD_BUFS once the first BWD_BUFS have stored (each lane owns the same entries)
+  auto put = [&](float* pw, auto st) {
 #pragma unroll
-  for (int j = 0; j < CF; ++j) {
-    const int f = lane + 64 * j;
-    if (f < d)
+    for (int j = 0; j < CF; ++j) {
+      const int f = lane + 64 * j;
+      if (f < d)
 #pragma unroll
-      for (int h = 0; h < H; ++h) pw[PL.Ue + h * F + f] = aU[j][h];
-  }
+        for (int h = 0; h < H; ++h) st(pw + PL.Ue + h * F + f, aU[j][h]);
+    }
 #pragma unroll
-  for (int j = 0; j < CT; ++j) {
-    const int i = lane + 64 * j;
-    if (i < D) {
+    for (int j = 0; j < CT; ++j) {
+      const int i = lane + 64 * j;
+      if (i < D) {
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          st(pw + PL.Ue + h * F + d + i, aU[CF + j][h]);
+          st(pw + PL.Ul + h * D + i, aU[CF + CT + j][h]);
+        }
+        st(pw + PL.w + i, aw[j]);
+        st(pw + PL.b + i, ab[j]);
+      }
+    }
+    if (lane == 0)
 #pragma unroll
       for (int h = 0; h < H; ++h) {
-        pw[PL.Ue + h * F + d + i] = aU[CF + j][h];
-        pw[PL.Ul + h * D + i] = aU[CF + CT + j][h];
+        st(pw + PL.ce + h, ac[h]);
+        st(pw + PL.cl + h, ac[h]);
       }
-      pw[PL.w + i] = aw[j];
-      pw[PL.b + i] = ab[j];
-    }
+  };
+  if (wv < BWD_BUFS) put(part + wv * PL.total, [](float* q, float v) { *q = v; });
+  if constexpr (NW > BWD_BUFS) {
+    __syncthreads();
+    if (wv >= BWD_BUFS) put(part + (wv - BWD_BUFS) * PL.total, [](float* q, float v) { *q += v; });
   }
-  if (lane == 0)
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      pw[PL.ce + h] = ac[h];
-      pw[PL.cl + h] = ac[h];
-    }
   __syncthreads();
   float* slab = c.slabs + (int64_t)blockIdx.x * PL.total;
   for (int p = threadIdx.x; p < PL.total; p += blockDim.x) {
@@ -1279,20 +1296,26 @@ __global__ void __launch_bounds__(64 * BWD_WAVES) tgnn_edge_bwd(Ctx c) {
     const bool owned = (p < PL.Ur) || (p >= PL.ce && p < PL.cr) || p >= PL.w;
     if (owned)
 #pragma unroll
-      for (int w = 0; w < BWD_WAVES; ++w) s += part[w * PL.total + p];
+      for (int w = 0; w < BWD_BUFS; ++w) s += part[w * PL.total + p];
     slab[p] = s;
   }
 }
 
-template <int CF, int CT, bool DROP>
-static void launch_edge_bwd_t(const Ctx& c, size_t shp, hipStream_t s) {
+template <int CF, int CT, bool DROP, int NW>
+static void launch_edge_bwd_nw(const Ctx& c, hipStream_t s) {
   static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)tgnn_edge_bwd<CF, CT, DROP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)tgnn_edge_bwd<CF, CT, DROP, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               150 * 1024);
     return true;
   }();
   (void)attr;
-  tgnn_edge_bwd<CF, CT, DROP><<<GBWD, 64 * BWD_WAVES, shp, s>>>(c);
+  const size_t shp = (size_t)bwd_bufs(NW) * c.PL.total * 4;
+  tgnn_edge_bwd<CF, CT, DROP, NW><<<GBWD, 64 * NW, shp, s>>>(c);
+}
+template <int CF, int CT, bool DROP>
+static void launch_edge_bwd_t(const Ctx& c, size_t, hipStream_t s) {
+  if (c.Bmax >= TGNX_BWD_BIG_BATCH) launch_edge_bwd_nw<CF, CT, DROP, 12>(c, s);
+  else launch_edge_bwd_nw<CF, CT, DROP, BWD_WAVES>(c, s);
 }
 template <int CF>
 static void launch_edge_bwd_cf(const Ctx& c, size_t shp, hipStream_t s) {
@@ -1301,7 +1324,7 @@ static void launch_edge_bwd_cf(const Ctx& c, size_t shp, hipStream_t s) {
   else two ? launch_edge_bwd_t<CF, 2, false>(c, shp, s) : launch_edge_bwd_t<CF, 1, false>(c, shp, s);
 }
 static void launch_edge_bwd(const Ctx& c, hipStream_t s) {
-  const size_t shp = (size_t)BWD_WAVES * c.PL.total * 4;
+  const size_t shp = 0;  // (per wave count: launch_edge_bwd_nw)
   switch ((c.d + 63) / 64) {
     case 0: launch_edge_bwd_cf<0>(c, shp, s); break;
     case 1: launch_edge_bwd_cf<1>(c, shp, s); break;
