@@ -112,6 +112,7 @@ class TgnnEngine:
         """One train iteration on an explicit batch (epoch_utils.py:194-304).  update=False stops
         after the gradients (no all-reduce, no Adam; the ring insert / time_assoc update of the batch
         already happened once the forward had read them): see apply_update()."""
+        self.finish()   # (a resident step's deferred update first: this step overwrites the reduced gradients)
         dev = self.dev
         src, dst, t, msg, blk = self._dev_batch(dev, src, dst, t, msg, blk)
         B = int(src.numel())
