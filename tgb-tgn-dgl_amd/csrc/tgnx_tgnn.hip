@@ -33,9 +33,6 @@ constexpr int TOUCH_MAX = 8192;
 #ifndef TGNX_BWD_WAVES
 #define TGNX_BWD_WAVES 8  // waves per edge-backward workgroup below TGNX_BWD_BIG_BATCH events (12 at and above)
 #endif
-#ifndef TGNX_BWD_NE
-#define TGNX_BWD_NE 2
-#endif
 constexpr int GBWD = TGNX_GBWD;            // workgroups of the edge backward kernel (= partial slabs)
 constexpr int BWD_WAVES = TGNX_BWD_WAVES;  // waves per edge backward workgroup (small batches)
 #ifndef TGNX_BWD_BIG_BATCH
