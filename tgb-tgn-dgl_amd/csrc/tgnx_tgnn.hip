@@ -31,17 +31,17 @@ constexpr int TOUCH_MAX = 8192;
 #define TGNX_GBWD 256
 #endif
 #ifndef TGNX_BWD_WAVES
-#define TGNX_BWD_WAVES 8  // waves per edge-backward workgroup below TGNX_BWD_BIG_BATCH events (12 at and above)
+#define TGNX_BWD_WAVES 8  // waves per edge-backward workgroup below TGNX_BIG_BATCH events (12 at and above)
 #endif
 constexpr int GBWD = TGNX_GBWD;            // workgroups of the edge backward kernel (= partial slabs)
 constexpr int BWD_WAVES = TGNX_BWD_WAVES;  // waves per edge backward workgroup (small batches)
-#ifndef TGNX_BWD_BIG_BATCH
-#define TGNX_BWD_BIG_BATCH 1000
+#ifndef TGNX_BIG_BATCH
+#define TGNX_BIG_BATCH 1000  // batch capacity from which the TGNN step takes its large-batch forms (below)
 #endif
 // LDS partial rows of the edge backward (16 KB each at the wiki shape): waves past the 8th add theirs into row
 // wv - 8 after the first 8 stored (fixed order), so 12 waves (3 per SIMD at 144 VGPRs) fit one CU's LDS.  12 waves:
 // TGN.yml's B = 2,000 step 1.117 -> 1.061 ms, B = 200 0.0918 -> 0.0927 (profiles/r6/r6ab_*): 12 from
-// TGNX_BWD_BIG_BATCH events of capacity up
+// TGNX_BIG_BATCH events of capacity up
 __host__ __device__ constexpr int bwd_bufs(int nw) { return nw < 8 ? nw : 8; }
 constexpr int GSEG = 160;     // workgroups of the segment backward kernel
 constexpr int MRR_SLOTS = 65536;  // per-batch MRR ring in buffers.mrr
@@ -144,6 +144,7 @@ struct Ctx {
   // (ctl[TGNX_CTL_APPLY] = its Adam step count) and the next step's tgnn_assemble launch applies it in its extra
   // workgroups (apply_nel of them elementwise), beside the batch assembly
   int defer, apply_nel;
+  int seg_in_pred;  // train: the segment forward rides in tgnn_pred_train (batches below TGNX_BIG_BATCH)
   int64_t adv_lo, adv_hi, adv_batch;
   uint64_t adv_seed;
   float pf, pa, inv_kf, inv_ka;
@@ -1004,17 +1005,12 @@ __device__ __forceinline__ void load_x8(const float* p, float (&x)[H]) {
 }
 
 
-// per segment: LeakyReLU, edge softmax per head (model_utils.py:595-597), ft = Σ a·x, head mean
+// per segment: LeakyReLU, edge softmax per head (model_utils.py:595-597), ft = Σ a·x, head mean;
+// segment w by one wave (lane = 8 edge slots x 8 heads): edge softmax with attention dropout and the head mean
+// (model_utils.py:589-605 collapsed), online over chunks of 8 edges; returns the segment's output (every lane)
 template <bool TRAIN>
-__global__ void __launch_bounds__(256) tgnn_seg_fwd(Ctx c) {
-  // a wave per segment (lane = 8 edge slots x 8 heads): edge softmax with attention dropout and the
-  // head mean (model_utils.py:589-605 collapsed), online over chunks of 8 edges
-  const int B = (int)c.ctl[TGNX_CTL_B];
-  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
-  const int S = (int)c.ctl[TGNX_CTL_S];
-  const int lane = threadIdx.x & 63, j = lane >> 3, h = lane & 7;
-  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (w >= S) return;
+__device__ float seg_fwd_one(const Ctx& c, const int w, const int lane) {
+  const int j = lane >> 3, h = lane & 7;
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   Seg s;
   seg_of(c, w, (int)c.ctl[TGNX_CTL_LO], (int)c.ctl[TGNX_CTL_HI], start, s);
@@ -1065,8 +1061,8 @@ __global__ void __launch_bounds__(256) tgnn_seg_fwd(Ctx c) {
     m = mn;
   }
   const float ft = acc / l;
-  const float out = red_h_sum(ft);
-  if (lane == 0) c.seg_out[w] = out * (1.0f / H);
+  const float out = red_h_sum(ft) * (1.0f / H);
+  if (lane == 0) c.seg_out[w] = out;
   if (TRAIN && j == 0) {
     float* sp = c.seg_stats + (int64_t)w * 4 * H;
     sp[h] = m;
@@ -1074,6 +1070,17 @@ __global__ void __launch_bounds__(256) tgnn_seg_fwd(Ctx c) {
     sp[2 * H + h] = ft;
     sp[3 * H + h] = er;
   }
+  return out;
+}
+// eval: a wave per segment (train: the segments ride in tgnn_pred_train, three per event)
+template <bool TRAIN>
+__global__ void __launch_bounds__(256) tgnn_seg_fwd(Ctx c) {
+  const int B = (int)c.ctl[TGNX_CTL_B];
+  if (B == 0 || c.ctl[TGNX_CTL_ERR] != 0) return;
+  const int S = (int)c.ctl[TGNX_CTL_S];
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= S) return;
+  seg_fwd_one<TRAIN>(c, w, threadIdx.x & 63);
 }
 
 // ------------------------------------------------------------------ backward
@@ -1311,7 +1318,7 @@ static void launch_edge_bwd_nw(const Ctx& c, hipStream_t s) {
 }
 template <int CF, int CT, bool DROP>
 static void launch_edge_bwd_t(const Ctx& c, size_t, hipStream_t s) {
-  if (c.Bmax >= TGNX_BWD_BIG_BATCH) launch_edge_bwd_nw<CF, CT, DROP, 12>(c, s);
+  if (c.Bmax >= TGNX_BIG_BATCH) launch_edge_bwd_nw<CF, CT, DROP, 12>(c, s);
   else launch_edge_bwd_nw<CF, CT, DROP, BWD_WAVES>(c, s);
 }
 template <int CF>
@@ -1391,9 +1398,22 @@ __global__ void __launch_bounds__(256) tgnn_pred_train(Ctx c) {
   const int64_t start = c.ctl[TGNX_CTL_BATCH_START];
   const uint64_t seed = (uint64_t)c.ctl[TGNX_CTL_SEED];
   const int blk = (int)c.ev_blk[start + i];
+  // batches below TGNX_BIG_BATCH: the event's three segments (src, pos, neg: segments i, nloc + i, 2 nloc + i of
+  // the rank's slice) by waves 0-2 — tgnn_seg_fwd's work, one launch fewer (B = 200 step 0.0918 -> 0.0884 ms; at
+  // B = 2,000 the separate launch is faster, 1.061 vs 1.087: profiles/r6/r6ae_*)
+  __shared__ float sv_l[3];
+  if (c.seg_in_pred) {
+    if (wv < 3) {
+      const float o = seg_fwd_one<true>(c, wv * nloc + (i - lo), lane);
+      if (lane == 0) sv_l[wv] = o;
+    }
+  } else if (tid < 3) {
+    sv_l[tid] = c.seg_out[tid * nloc + (i - lo)];
+  }
+  __syncthreads();
   {
     const int64_t roots[3] = {c.ev_src[start + i], c.ev_dst[start + i], c.neg[start + i]};
-    const float sv[3] = {c.seg_out[i - lo], c.seg_out[nloc + i - lo], c.seg_out[2 * nloc + i - lo]};
+    const float sv[3] = {sv_l[0], sv_l[1], sv_l[2]};
     for (int x = tid; x < 3 * D; x += blockDim.x) {
       const int r = x / D, dd = x % D;
       float v = c.mem[roots[r] * D + dd];
@@ -2168,10 +2188,12 @@ static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
   launch_edge_fwd(c, TRAIN ? finish_blocks(c.Bmax) : 0, s);
   probe_end(TGNX_K_EDGE_FWD, s);
   TGNX_LAUNCH_CHECK("tgnn_edge_fwd");
-  probe_begin(TGNX_K_SEG_FWD, s);
-  tgnn_seg_fwd<TRAIN><<<grid_for(Scap, 4), 256, 0, s>>>(c);
-  probe_end(TGNX_K_SEG_FWD, s);
-  TGNX_LAUNCH_CHECK("tgnn_seg_fwd");
+  if (!TRAIN || !c.seg_in_pred) {  // (train below TGNX_BIG_BATCH: the segments ride in tgnn_pred_train)
+    probe_begin(TGNX_K_SEG_FWD, s);
+    tgnn_seg_fwd<TRAIN><<<grid_for(Scap, 4), 256, 0, s>>>(c);
+    probe_end(TGNX_K_SEG_FWD, s);
+    TGNX_LAUNCH_CHECK("tgnn_seg_fwd");
+  }
   return TGNX_OK;
 }
 
@@ -2314,6 +2336,7 @@ static int train_fwd_bwd_impl(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffe
   hipStream_t s = as_stream(stream);
   const int Bmax = cfg->max_batch;
   c.gen_neg = gen_neg ? 1 : 0;
+  c.seg_in_pred = Bmax < TGNX_BIG_BATCH ? 1 : 0;
   rc = launch_forward<true>(c, 3 * (int64_t)Bmax, s);
   if (rc) return rc;
   probe_begin(TGNX_K_PRED, s);
