@@ -43,7 +43,10 @@ constexpr int BWD_WAVES = TGNX_BWD_WAVES;  // waves per edge backward workgroup 
 // TGN.yml's B = 2,000 step 1.117 -> 1.061 ms, B = 200 0.0918 -> 0.0927 (profiles/r6/r6ab_*): 12 from
 // TGNX_BIG_BATCH events of capacity up
 __host__ __device__ constexpr int bwd_bufs(int nw) { return nw < 8 ? nw : 8; }
-constexpr int GSEG = 160;     // workgroups of the segment backward kernel
+constexpr int GSEG = 160;     // workgroups of the segment backward kernel (= segment slabs)
+constexpr int GSEG_BIG = 1024;  // ... from TGNX_BIG_BATCH events of capacity (6,000 segments at B = 2,000: 160 took
+                                // 132 us, 640 waves each walking ~9 segments)
+__host__ __device__ inline int gseg_for(int Bmax) { return Bmax >= TGNX_BIG_BATCH ? GSEG_BIG : GSEG; }
 constexpr int MRR_SLOTS = 65536;  // per-batch MRR ring in buffers.mrr
 constexpr int BATCH_MAX = 2048;   // max events per batch (touch sort capacity 3 * BATCH_MAX in LDS)
 enum { MISC_RUNS = 0, MISC_KMAX = 1, MISC_STAMPS = 16, MISC_WORDS = TGNX_MISC_WORDS };
@@ -1589,9 +1592,9 @@ __device__ void pred_reduce_body(const Ctx& c, const int bid) {
 
 // segment backward (blocks [0, GSEG)) and the predictor weight reductions (the rest) in one launch:
 // both only need tgnn_pred_train's per-event rows
-__global__ void __launch_bounds__(256) tgnn_seg_bwd_pred(Ctx c) {
-  if ((int)blockIdx.x < GSEG) seg_bwd_body(c, blockIdx.x, GSEG);
-  else pred_reduce_body(c, blockIdx.x - GSEG);
+__global__ void __launch_bounds__(256) tgnn_seg_bwd_pred(Ctx c, int nseg) {
+  if ((int)blockIdx.x < nseg) seg_bwd_body(c, blockIdx.x, nseg);
+  else pred_reduce_body(c, blockIdx.x - nseg);
 }
 __host__ __device__ inline int pred_reduce_blocks(int D) {
   const int nt = (D + 15) / 16;
@@ -2049,7 +2052,7 @@ static WsLay make_ws(const tgnx_tgnn_config* cfg) {
   W.U = carve(off, (size_t)make_ulay(D, d).total * 4);
   W.evs = carve(off, (size_t)B * (8 * D + 4) * 4);
   W.slabs = carve(off, (size_t)GBWD * P * 4);
-  W.slabs_s = carve(off, (size_t)GSEG * (H * D + H) * 4);
+  W.slabs_s = carve(off, (size_t)gseg_for(cfg->max_batch) * (H * D + H) * 4);
   W.red = carve(off, (size_t)P * 4);
   W.blkmax = carve(off, (size_t)B * 4);
   W.blk_rank = carve(off, (size_t)B * 4);
@@ -2148,7 +2151,7 @@ static int make_ctx(const tgnx_tgnn_config* cfg, const tgnx_tgnn_buffers* b, int
   c.Ecap = W.Ecap;
   c.Bmax = cfg->max_batch;
   c.Ge = GBWD;
-  c.Gs = GSEG;
+  c.Gs = gseg_for(cfg->max_batch);
   c.L = make_lay(c.D, c.d);
   c.UL = make_ulay(c.D, c.d);
   c.PL = make_play(c.D, c.d);
@@ -2199,14 +2202,14 @@ static int launch_forward(const Ctx& c, int64_t Scap, hipStream_t s) {
 
 static int launch_backward(const Ctx& c, hipStream_t s) {
   probe_begin(TGNX_K_SEG_BWD, s);
-  tgnn_seg_bwd_pred<<<GSEG + pred_reduce_blocks(c.D), 256, 0, s>>>(c);
+  tgnn_seg_bwd_pred<<<c.Gs + pred_reduce_blocks(c.D), 256, 0, s>>>(c, c.Gs);
   probe_end(TGNX_K_SEG_BWD, s);
   TGNX_LAUNCH_CHECK("tgnn_seg_bwd_pred");
   probe_begin(TGNX_K_EDGE_BWD, s);
   launch_edge_bwd(c, s);
   probe_end(TGNX_K_EDGE_BWD, s);
   TGNX_LAUNCH_CHECK("tgnn_edge_bwd");
-  tgnn_grad_reduce<<<(c.PL.total + 63) / 64, 64 * RED_WAVES, 0, s>>>(c, GBWD, GSEG);
+  tgnn_grad_reduce<<<(c.PL.total + 63) / 64, 64 * RED_WAVES, 0, s>>>(c, GBWD, c.Gs);
   TGNX_LAUNCH_CHECK("tgnn_grad_reduce");
   return TGNX_OK;
 }
