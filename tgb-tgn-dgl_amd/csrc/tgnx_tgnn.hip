@@ -1008,6 +1008,21 @@ __device__ __forceinline__ void load_x8(const float* p, float (&x)[H]) {
 }
 
 
+// Segments longer than SEG_WIDE edges (a hub node's: up to ~900 at B = 2,000) run with lane = edge slot (64 slots,
+// all 8 heads per lane) instead of 8 slots x 8 heads, so their serial chain is 8x shorter (B = 2,000 step 0.997 ->
+// 0.967 ms; from 64 edges the B = 200 step lost 2.6 %, from 128 it is unchanged: profiles/r6/r6ak_*, r6al_*)
+constexpr int SEG_WIDE = 128;
+__device__ __forceinline__ float pick8(const float (&v)[H], int h) {
+  float r = v[0];
+#pragma unroll
+  for (int k = 1; k < H; ++k) r = h == k ? v[k] : r;
+  return r;
+}
+__device__ __forceinline__ void load_row8(const float* p, float (&x)[H]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+}
+
 // per segment: LeakyReLU, edge softmax per head (model_utils.py:595-597), ft = Σ a·x, head mean;
 // segment w by one wave (lane = 8 edge slots x 8 heads): edge softmax with attention dropout and the head mean
 // (model_utils.py:589-605 collapsed), online over chunks of 8 edges; returns the segment's output (every lane)
@@ -1023,8 +1038,52 @@ __device__ float seg_fwd_one(const Ctx& c, const int w, const int lane) {
   const int e0 = c.seg_eoff[w], ne = c.seg_eoff[w + 1] - e0;
   const uint64_t sk = seg_key(s.blk, s.root);
   const float* __restrict__ X = c.X + (int64_t)e0 * H + h;
-  // each lane: online softmax over its edges o = j, j + 8, ... (no cross-lane traffic in the loop)
   float m = -INFINITY, l = 0.f, acc = 0.f;
+  if (ne > SEG_WIDE) {  // (wave-uniform) lane = edge slot, all heads per lane; lanes merged in a fixed order
+    float erh[H], mw[H], lw[H], aw[H];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      erh[k] = __shfl(er, k, WAVE);  // (lane k: slot 0, head k)
+      mw[k] = -INFINITY;
+      lw[k] = aw[k] = 0.f;
+    }
+    const float* __restrict__ Xr = c.X + (int64_t)e0 * H;
+    for (int o = lane; o < ne; o += WAVE) {
+      float xv[H];
+      load_row8(Xr + (int64_t)o * H, xv);
+      const uint32_t ab = drop ? attn_base(seed, sk, o) : 0u;
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        float sc = xv[k] + erh[k];
+        sc = sc > 0.f ? sc : 0.2f * sc;
+        const float mn = fmaxf(mw[k], sc);
+        const float r = mw[k] == -INFINITY ? 0.f : expf(mw[k] - mn);
+        const float ex = expf(sc - mn);
+        float wgt = ex;
+        if (drop) wgt *= keep32(ab, (uint32_t)k, c.pa, c.inv_ka);
+        lw[k] = lw[k] * r + ex;
+        aw[k] = aw[k] * r + wgt * xv[k];
+        mw[k] = mn;
+      }
+    }
+#pragma unroll
+    for (int st = 1; st < WAVE; st <<= 1)
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        const float mo = __shfl_xor(mw[k], st, WAVE), lo = __shfl_xor(lw[k], st, WAVE),
+                    ao = __shfl_xor(aw[k], st, WAVE);
+        const float mn = fmaxf(mw[k], mo);
+        const float r1 = mw[k] == -INFINITY ? 0.f : expf(mw[k] - mn);
+        const float r2 = mo == -INFINITY ? 0.f : expf(mo - mn);
+        lw[k] = lw[k] * r1 + lo * r2;
+        aw[k] = aw[k] * r1 + ao * r2;
+        mw[k] = mn;
+      }
+    m = pick8(mw, h);
+    l = pick8(lw, h);
+    acc = pick8(aw, h);
+  } else {
+  // each lane: online softmax over its edges o = j, j + 8, ... (no cross-lane traffic in the loop)
 #pragma unroll 4
   for (int o = j; o < ne; o += 8) {
     const float x = X[(int64_t)o * H];
@@ -1062,6 +1121,7 @@ __device__ float seg_fwd_one(const Ctx& c, const int w, const int lane) {
     l = l * r1 + lo * r2;  // fp addition commutes: both partners hold the same bits
     acc = acc * r1 + ao * r2;
     m = mn;
+  }
   }
   const float ft = acc / l;
   const float out = red_h_sum(ft) * (1.0f / H);
@@ -1118,11 +1178,47 @@ __device__ void seg_bwd_body(const Ctx& c, const int bid, const int nblk) {
     const int e0 = c.seg_eoff[w], ne = c.seg_eoff[w + 1] - e0;
     const uint64_t sk = seg_key(s.blk, s.root);
     float der = 0.f;
-    const float* __restrict__ X = c.X + (int64_t)e0 * H + h;
-    float* __restrict__ DXp = c.DX + (int64_t)e0 * H + h;
+    if (ne > SEG_WIDE) {  // (wave-uniform) lane = edge slot, all heads per lane (as tgnn_seg_fwd's long segments)
+      float mh[H], lh[H], fh[H], eh[H], dh[H];
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        mh[k] = sp[k];
+        lh[k] = sp[H + k];
+        fh[k] = sp[2 * H + k];
+        eh[k] = sp[3 * H + k];
+        dh[k] = 0.f;
+      }
+      const float* __restrict__ Xr = c.X + (int64_t)e0 * H;
+      float* __restrict__ DXr = c.DX + (int64_t)e0 * H;
+      for (int o = lane; o < ne; o += WAVE) {
+        float xv[H], dx[H];
+        load_row8(Xr + (int64_t)o * H, xv);
+        const uint32_t ab = drop ? attn_base(seed, sk, o) : 0u;
+#pragma unroll
+        for (int k = 0; k < H; ++k) {
+          float sc = xv[k] + eh[k];
+          const float lk = sc > 0.f ? 1.f : 0.2f;
+          sc = sc > 0.f ? sc : 0.2f * sc;
+          const float a = expf(sc - mh[k]) / lh[k];
+          const float mk = drop ? keep32(ab, (uint32_t)k, c.pa, c.inv_ka) : 1.f;
+          const float ds = a * gh * (xv[k] * mk - fh[k]) * lk;
+          dx[k] = gh * a * mk + ds;
+          dh[k] += ds;
+        }
+        float4* dp = reinterpret_cast<float4*>(DXr + (int64_t)o * H);
+        dp[0] = make_float4(dx[0], dx[1], dx[2], dx[3]);
+        dp[1] = make_float4(dx[4], dx[5], dx[6], dx[7]);
+      }
+#pragma unroll
+      for (int st = 1; st < WAVE; st <<= 1)
+#pragma unroll
+        for (int k = 0; k < H; ++k) dh[k] += __shfl_xor(dh[k], st, WAVE);
+      der = pick8(dh, h);
+    } else {
+      const float* __restrict__ X = c.X + (int64_t)e0 * H + h;
+      float* __restrict__ DXp = c.DX + (int64_t)e0 * H + h;
 #pragma unroll 4
-    for (int o = j; o < ne; o += 8) {
-      {
+      for (int o = j; o < ne; o += 8) {
         const float x = X[(int64_t)o * H];
         float sc = x + er;
         const float lk = sc > 0.f ? 1.f : 0.2f;
@@ -1133,8 +1229,8 @@ __device__ void seg_bwd_body(const Ctx& c, const int bid, const int nblk) {
         DXp[(int64_t)o * H] = gh * a * mk + ds;
         der += ds;
       }
+      der = red_j_sum(der);
     }
-    der = red_j_sum(der);
     const uint32_t nb = drop ? node_base(seed, s.blk, s.root) : 0u;
     float mv[KD];
 #pragma unroll
