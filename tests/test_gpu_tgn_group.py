@@ -1,0 +1,53 @@
+"""The world-1 parity-set TGN step replayed as 8-step graph groups (TgnEngine.capture_group / replay_resident_n, what
+bench.py's timed window runs) against one graph per step (replay_resident), from the same state over 24 steps of a
+wiki-shaped stream: last_update / ring / stores exact, memory 1e-4 absolute, parameters and Adam moments 2e-5 / 1e-3
+relative — the float-atomic run-to-run drift of the step (tests/test_gpu_tgn_rccl.py), timestamps rescaled to 2,000 s
+where the trajectory is not chaotic."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+N, D_MSG, D, B, NB = 9_227, 172, 100, 200, 30
+
+
+def _engine(s):
+    from tgnx.sampler import LastNeighborLoader
+    from tgnx.tgn import TgnAdam, TgnEngine, TGNModel
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    model = TGNModel(N, s.num_events, D_MSG, D, dev, ring=10, max_batch=B, max_neg=1, aggr="last", dropout=0.1)
+    eng = TgnEngine(model, LastNeighborLoader(N, 10, device=dev),
+                    dict(src=s.src, dst=s.dst, t=s.t.astype(np.float32), msg=s.msg), TgnAdam(model, 1e-3),
+                    dst_nodes=s.dst_nodes, seed=7)
+    eng.bind_resident(0, NB * B, B, dropout=True)
+    eng.begin_epoch()
+    eng.capture_resident()
+    return eng
+
+
+def test_grouped_replay_equals_per_step_replay():
+    from tgnx.synth import make_stream
+    s = make_stream("tgbl-wiki", seed=3, num_events=B * NB)
+    span = max(float(s.t[-1] - s.t[0]), 1.0)
+    s.t = np.floor((s.t - s.t[0]) * (2000.0 / span))
+    a, b = _engine(s), _engine(s)
+    assert b.capture_group(8)
+    for e in (a, b):       # the same 2 steps first (the first primes the scan sets eagerly)
+        e.replay_resident()
+        e.replay_resident()
+    for _ in range(24):
+        a.replay_resident()
+    b.replay_resident_n(24)          # 3 groups of 8
+    for e in (a, b):
+        e.finish()
+        e.check()
+    torch.cuda.synchronize()
+    ma, mb = a.model, b.model
+    assert torch.equal(ma.memory.last_update, mb.memory.last_update)
+    assert torch.equal(a.loader.e_id, b.loader.e_id) and torch.equal(ma.store, mb.store)
+    assert float((ma.memory.memory - mb.memory.memory).abs().max()) < 1e-4
+    for x, y, tol in ((ma.flat, mb.flat, 2e-5), (a.adam_m, b.adam_m, 1e-3), (a.adam_v, b.adam_v, 1e-3)):
+        rel = float((x.double() - y.double()).norm() / (y.double().norm() + 1e-12))
+        assert rel < tol, rel
+    assert abs(a.loss_sum() - b.loss_sum()) < 1e-4 * abs(a.loss_sum())

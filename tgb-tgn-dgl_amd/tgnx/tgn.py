@@ -731,6 +731,37 @@ class TgnEngine:
         torch.cuda.synchronize(self.dev)
         self.ctl.copy_(saved)
 
+    def capture_group(self, k: int = 8):
+        """World 1, parity-set steps: also capture k consecutive steps (parities 0, 1, 0, ...) as ONE HIP graph, so a
+        run of steps pays one graph launch per k (replay_resident_n).  k even: the group starts and ends at parity 0."""
+        if self.dp or not self._pp() or k < 2 or k % 2:
+            self._group = None
+            return False
+        torch.cuda.synchronize(self.dev)
+        saved = self.ctl.clone()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for q in range(k):
+                self._pre(True, q & 1)
+        torch.cuda.synchronize(self.dev)
+        self.ctl.copy_(saved)
+        self._group = (k, g)
+        return True
+
+    def replay_resident_n(self, n: int):
+        """n resident steps: whole captured k-step groups wherever the set parity and the prefetch allow, single
+        replays (or the priming eager step) otherwise.  The same steps as n calls of replay_resident()."""
+        grp = getattr(self, "_group", None)
+        done = 0
+        while done < n:
+            if grp and n - done >= grp[0] and self._parity == 0 and self._prefetch_valid():
+                grp[1].replay()
+                self._mark_prefetched()
+                done += grp[0]
+            else:
+                self.replay_resident()
+                done += 1
+
     def replay_resident(self):
         g1, g2, gs = self._graphs
         if self._pipelined() and not self._prefetch_valid():
