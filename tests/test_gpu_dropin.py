@@ -179,3 +179,41 @@ def test_deferred_update_is_applied_before_eval():
     assert int(ea.ctl[17]) == 0
     assert torch.equal(ma.flat, mb.flat) and torch.equal(ea.adam_m, eb.adam_m) and torch.equal(ea.adam_v, eb.adam_v)
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_grouped_replay_equals_per_step_replay():
+    """World 1: k resident steps captured as one graph (TgnnEngine.capture_group / replay_resident_n, what bench.py's
+    timed window replays) against one graph per step — bit-identical state (the TGNN step is deterministic)."""
+    from tgnx.data import block_ids
+    s = _stream(E=4000)
+    B = 200
+    blk = torch.from_numpy(block_ids(s.src, s.dst, B)).cuda()
+    dev = torch.device("cuda")
+    ev = [torch.from_numpy(x).to(dev) for x in (s.src, s.dst, s.t.astype(np.float32))]
+    msg = torch.from_numpy(s.msg).to(dev)
+    engs = []
+    for grouped in (False, True):
+        m, e = _make(s)
+        m.cfg.feat_drop = m.cfg.attn_drop = 0.6
+        neg_buf = torch.zeros(s.num_events, dtype=torch.long, device=dev)
+        e.bind_resident(ev[0], ev[1], ev[2], blk, msg, neg_buf, 0, 3800, B, dropout=True)
+        e.begin_epoch()
+        e.capture_resident(1)
+        if grouped:
+            assert e.capture_group(8)
+        engs.append((m, e, neg_buf))
+    (ma, ea, na), (mb, eb, nb) = engs
+    for _ in range(3):
+        ea.replay_resident()
+        eb.replay_resident()
+    for _ in range(16):
+        ea.replay_resident()
+    eb.replay_resident_n(16)
+    for _, e, _ in engs:
+        e.finish()
+        e.check()
+    torch.cuda.synchronize()
+    assert torch.equal(ea.ctl, eb.ctl)
+    assert torch.equal(ma.flat, mb.flat) and torch.equal(ea.adam_m, eb.adam_m) and torch.equal(ea.adam_v, eb.adam_v)
+    assert torch.equal(ma.time_assoc, mb.time_assoc) and torch.equal(ea.loader.e_id, eb.loader.e_id)
+    assert torch.equal(na, nb)

@@ -260,6 +260,36 @@ class TgnnEngine:
         torch.cuda.synchronize(self.dev)
         self.ctl.copy_(saved)
 
+    def capture_group(self, k: int = 8):
+        """World 1 with the folded update: also capture k consecutive resident steps as ONE HIP graph, so a run of
+        steps pays one graph launch per k (replay_resident_n)."""
+        if self.world != 1 or not getattr(self, "_fused", False) or k < 2:
+            self._group = None
+            return False
+        torch.cuda.synchronize(self.dev)
+        saved = self.ctl.clone()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(k):
+                if self._resident_fwd_bwd(self._stream()):
+                    raise RuntimeError(_lib.lib().tgnx_last_error().decode())
+        torch.cuda.synchronize(self.dev)
+        self.ctl.copy_(saved)
+        self._group = (k, g)
+        return True
+
+    def replay_resident_n(self, n: int):
+        """n resident steps: whole k-step groups, then single replays (the same steps as n replay_resident calls)."""
+        grp = getattr(self, "_group", None)
+        done = 0
+        while done < n:
+            if grp and n - done >= grp[0]:
+                grp[1].replay()
+                done += grp[0]
+            else:
+                self.replay_resident()
+                done += 1
+
     def replay_resident(self):
         """Run `steps_per_graph` resident steps from the captured graph(s)."""
         g1, g2 = self._graphs
