@@ -160,6 +160,8 @@ class TgnnEngine:
     def bind_resident(self, src, dst, t, blk, msg, neg_buf, split_lo, split_hi, batch, dropout=True):
         """Point the step at device-resident event arrays (global event index = row): the batch
         cursor lives in the control block, so a step is three launches of C calls and no host sync."""
+        self.finish()        # (a pending update of the previous binding's last step)
+        self._group = None   # (a step group captured for a previous binding)
         self._res_keep = (src, dst, t, blk, msg, neg_buf)
         self._res_buf = self._buffers(src, dst, t, blk, msg, neg_buf)
         self._res = (int(split_lo), int(split_hi), int(batch))

@@ -88,10 +88,10 @@ def train(model, feats, train_loader, neighbor_loader, neg_dest_sampler, assoc, 
             eng.bind_resident(ev["src"], ev["dst"], ev["t"], ev["blk"], ev["msg"], neg_buf, train_loader.lo,
                               train_loader.hi, B)
             eng.capture_resident(1)
+            eng.capture_group(8)                         # (world 1: 8 steps per graph launch)
             eng._bound = key
         eng.ctl[10] = 0
-        for _ in range(len(train_loader)):
-            eng.replay_resident()
+        eng.replay_resident_n(len(train_loader))
         eng.finish()                                     # the last step's update (deferred by the resident step)
         neighbor_loader.cur_e_id = train_loader.hi       # e_ids are global event rows (val continues)
         torch.cuda.synchronize(eng.dev)

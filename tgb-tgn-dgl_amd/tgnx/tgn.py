@@ -531,6 +531,7 @@ class TgnEngine:
         """Consecutive batches of `batch` events over [split_lo, split_hi), negatives drawn on the
         device; the batch cursor lives in the control block (no host arguments change per step)."""
         self.finish()
+        self._group = None   # (a step group captured for a previous binding)
         self._res = (int(split_lo), int(split_hi), int(batch))
         self._res_drop = 1 if dropout else 0
         self._prefetched = False

@@ -116,8 +116,8 @@ def train(model, feats, train_loader, neighbor_loader, neg_dest_sampler, assoc, 
     loss0 = eng.loss_sum()
     if getattr(eng, "_graphs", None) is None:
         eng.capture_resident()
-    for _ in range(len(train_loader)):
-        eng.replay_resident()
+        eng.capture_group(8)                              # (world 1: 8 steps per graph launch)
+    eng.replay_resident_n(len(train_loader))
     eng.finish()
     neighbor_loader.cur_e_id = train_loader.hi
     loss = eng.loss_sum() - loss0                         # (synchronises)
