@@ -52,7 +52,10 @@ __device__ __forceinline__ uint32_t drop_base(uint64_t seed, uint64_t stream, ui
 }
 __device__ __forceinline__ float keep32(uint32_t base, uint32_t idx, float p, float inv) {
   const uint32_t h = fmix32(base ^ (idx * 0x9E3779B9u));
-  return (float)(h >> 8) * (1.0f / 16777216.0f) >= p ? inv : 0.0f;
+  // u = (h >> 8) 2^-24 >= p  <=>  (h >> 8) >= ceil(p 2^24) (both sides exact): an integer compare, its threshold
+  // loop-invariant (p is a kernel argument)
+  const uint32_t thr = (uint32_t)ceilf(p * 16777216.0f);
+  return (h >> 8) >= thr ? inv : 0.0f;
 }
 
 }  // namespace tgnx
