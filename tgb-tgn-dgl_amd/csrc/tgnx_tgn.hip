@@ -58,7 +58,9 @@ constexpr int TB_MAX = 4095; // events per batch (12-bit event index in the touc
 #define TGNX_W3_WAVES 7  // waves-per-SIMD floor of the dW_cell launch (0: the compiler's register count, 84 + 8 -> 5 waves;
                          // same-box A/B: 0.0966 / 0.0961 ms, 6 waves 0.0961 / 0.0955, 7 (72 VGPRs, 12 B spilled) 0.0951 / 0.0951;
                          // round 5, 7 vs 0: wiki B = 200 0.0917 / 0.0914 vs 0.0927 / 0.0928 ms, B = 2,000 launch 32.6 vs
-                         // 34.2 us with the step +-0, comment 2-hop B = 600 +-0 — profiles/r5/r5_w3waves_ab.txt)
+                         // 34.2 us with the step +-0, comment 2-hop B = 600 +-0 — profiles/r5/r5_w3waves_ab.txt; round 6,
+                         // 8 waves: 0.0856 / 0.0854 vs 0.0847 / 0.0848 ms, and a 6 / 8-wave floor on the dz0 launch 0.0851 /
+                         // 0.0858 — profiles/r6/r6as_tgn_waves_ab.txt)
 #endif
 #ifndef TGNX_DXE_DR
 #define TGNX_DXE_DR TGNX_G32L_DR  // direct-operand slabs per round of the dX_enc GEMM (the 7-wave dW_cell launch)
