@@ -2921,7 +2921,8 @@ __device__ void lp_vec_body(const Ctx& c, int y, int lane) {
 // Workgroup per chunk of KVE_CH consecutive edges sorted by neighbour in LDS (as kv_reduce_body); a wave takes
 // KVE_PW sorted edges, lanes over the channels of both heads, and sums runs of equal neighbours in registers.
 #ifndef TGNX_KVE_CH
-#define TGNX_KVE_CH 32
+#define TGNX_KVE_CH 16  // 32 -> 16 (round 6, same box): wiki 0.0846 -> 0.0832 ms, coin-shaped 0.0899 / 0.0906 -> 0.0878 /
+                        // 0.0888, review-shaped 0.0996 / 0.1002 -> 0.0990 / 0.0995; 8: 0.0836, 64: 0.0902 (profiles/r6/r6av_*, r6aw_*)
 #endif
 constexpr int KVE_CH = TGNX_KVE_CH, KVE_PW = KVE_CH / 4;
 #ifndef TGNX_KVE_B
